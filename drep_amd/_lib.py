@@ -1,0 +1,262 @@
+"""ctypes binding of libdrephip.so (include/drephip.h).
+
+There is no fallback: if the HIP library is missing or cannot be loaded, every
+entry point raises :class:`DrepHipError`.  Build it with
+``python -c "import __graft_entry__ as g; g.build()"`` or ``make -C drep_amd/csrc``.
+
+The library is linked against the HIP runtime (libamdhip64.so.7).  PyTorch-ROCm
+ships its own copy; to keep exactly one HIP runtime in a process that may also
+import torch (bench.py, the multi-GPU path), the torch copy is preloaded with
+RTLD_GLOBAL before libdrephip.so when torch is installed, so both bind to it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import importlib.util
+import os
+import sys
+import threading
+from typing import Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DREPHIP_LIB", os.path.join(_HERE, "lib", "libdrephip.so"))
+
+ERR = {0: "OK", -1: "invalid argument", -2: "HIP error", -3: "I/O error", -4: "out of memory",
+       -5: "unsupported", -6: "internal error"}
+
+
+class DrepHipError(RuntimeError):
+    pass
+
+
+_lib = None
+_lock = threading.Lock()
+
+u64p = np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")
+u32p = np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS")
+u16p = np.ctypeslib.ndpointer(dtype=np.uint16, flags="C_CONTIGUOUS")
+u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
+f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+vp = C.c_void_p
+
+# name -> (restype, argtypes); every symbol declared in include/drephip.h
+SIGNATURES = {
+    "drephip_version": (C.c_int, []),
+    "drephip_last_error": (C.c_char_p, []),
+    "drephip_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "drephip_create": (C.c_int, [C.c_int, C.c_int, C.c_uint32, C.c_uint32, C.POINTER(vp)]),
+    "drephip_destroy": (C.c_int, [vp]),
+    "drephip_max_sketch": (C.c_uint32, []),
+    "drephip_tile_bases": (C.c_uint64, []),
+    "drephip_padded_bases": (C.c_uint64, [u64p, C.c_uint32]),
+    "drephip_fasta_info": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                     C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
+    "drephip_fasta_pack": (C.c_int, [C.c_char_p, C.c_int, u32p, u32p, C.c_uint64, C.c_uint64,
+                                     C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "drephip_sketch": (C.c_int, [vp, u8p, u64p, C.c_uint32, u64p, C.c_uint32, u64p, u32p, u64p]),
+    "drephip_sketch_files": (C.c_int, [vp, C.POINTER(C.c_char_p), C.c_uint32, C.c_int, u64p, u32p, u64p]),
+    "drephip_sketch_device": (C.c_int, [vp, vp, vp, u64p, u64p, u64p, C.c_uint32, vp, vp, vp]),
+    "drephip_synth_device": (C.c_int, [vp, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64,
+                                       vp, vp, vp]),
+    "drephip_allpairs": (C.c_int, [vp, u64p, u32p, C.c_uint32, u16p, vp]),
+    "drephip_allpairs_device": (C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp]),
+    "drephip_allpairs_merge_device": (C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp]),
+    "drephip_distance_lut": (C.c_int, [C.c_int, C.c_uint32, f64p]),
+    "drephip_set_timing": (C.c_int, [vp, C.c_int]),
+    "drephip_last_kernel_ms": (C.c_int, [vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
+}
+
+
+def _preload_torch_hip_runtime() -> None:
+    if "torch" in sys.modules:
+        return  # torch already put its runtime in the process
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        spec = None
+    if spec is None or not spec.submodule_search_locations:
+        return
+    for root in spec.submodule_search_locations:
+        cand = os.path.join(root, "lib", "libamdhip64.so")
+        if os.path.exists(cand):
+            try:
+                C.CDLL(cand, mode=C.RTLD_GLOBAL)
+            except OSError:
+                pass
+            return
+
+
+def lib():
+    """Load libdrephip.so (once).  Raises DrepHipError if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise DrepHipError(
+                "libdrephip.so not found at %s -- build it (make -C drep_amd/csrc); "
+                "drep_amd has no CPU fallback" % LIB_PATH)
+        _preload_torch_hip_runtime()
+        try:
+            L = C.CDLL(LIB_PATH)
+        except OSError as e:
+            raise DrepHipError("cannot load %s: %s" % (LIB_PATH, e)) from e
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+        return L
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().drephip_last_error().decode("utf-8", "replace")
+        raise DrepHipError("%s failed (%s): %s" % (what, ERR.get(rc, rc), msg))
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    rc = lib().drephip_device_count(C.byref(n))
+    return n.value if rc == 0 else 0
+
+
+def tile_bases() -> int:
+    return int(lib().drephip_tile_bases())
+
+
+def padded_bases(rec_len: Sequence[int]) -> int:
+    a = np.ascontiguousarray(rec_len, dtype=np.uint64)
+    return int(lib().drephip_padded_bases(a if len(a) else np.zeros(1, np.uint64), len(a)))
+
+
+def distance_lut(denom: int, k: int = 21) -> np.ndarray:
+    out = np.zeros(denom + 1, dtype=np.float64)
+    check(lib().drephip_distance_lut(k, denom, out), "drephip_distance_lut")
+    return out
+
+
+def fasta_info(path: str, k: int = 21):
+    length = C.c_uint64(0)
+    padded = C.c_uint64(0)
+    nrec = C.c_uint32(0)
+    nk = C.c_uint64(0)
+    check(lib().drephip_fasta_info(path.encode(), k, C.byref(length), C.byref(padded), C.byref(nrec),
+                                   C.byref(nk)), "drephip_fasta_info(%s)" % path)
+    return {"length": length.value, "padded": padded.value, "n_records": nrec.value, "n_kmers": nk.value}
+
+
+class Context:
+    """One libdrephip context: a HIP device plus (k, s, seed)."""
+
+    def __init__(self, device: int = 0, k: int = 21, s: int = 1000, seed: int = 42):
+        L = lib()
+        self.k, self.s, self.seed, self.device = int(k), int(s), int(seed), int(device)
+        h = vp()
+        check(L.drephip_create(self.device, self.k, self.s, self.seed, C.byref(h)), "drephip_create")
+        self._h = h
+
+    # -- lifecycle
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().drephip_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_timing(self, on: bool = True) -> None:
+        check(lib().drephip_set_timing(self._h, 1 if on else 0), "drephip_set_timing")
+
+    def kernel_ms(self, which: int):
+        ms = C.c_double(0)
+        n = C.c_int(0)
+        check(lib().drephip_last_kernel_ms(self._h, which, C.byref(ms), C.byref(n)), "drephip_last_kernel_ms")
+        return ms.value, n.value
+
+    # -- sketch
+    def sketch_files(self, paths: Sequence[str], threads: int = 0):
+        n = len(paths)
+        hashes = np.zeros((n, self.s), dtype=np.uint64)
+        nhash = np.zeros(n, dtype=np.uint32)
+        length = np.zeros(n, dtype=np.uint64)
+        if n == 0:
+            return hashes, nhash, length
+        arr = (C.c_char_p * n)(*[os.fsencode(p) for p in paths])
+        check(lib().drephip_sketch_files(self._h, arr, n, int(threads), hashes.reshape(-1), nhash, length),
+              "drephip_sketch_files")
+        return hashes, nhash, length
+
+    def sketch_records(self, seq: np.ndarray, rec_off: np.ndarray, genome_rec_off: np.ndarray):
+        seq = np.ascontiguousarray(seq, dtype=np.uint8)
+        rec_off = np.ascontiguousarray(rec_off, dtype=np.uint64)
+        genome_rec_off = np.ascontiguousarray(genome_rec_off, dtype=np.uint64)
+        n = len(genome_rec_off) - 1
+        hashes = np.zeros((max(n, 0), self.s), dtype=np.uint64)
+        nhash = np.zeros(max(n, 0), dtype=np.uint32)
+        length = np.zeros(max(n, 0), dtype=np.uint64)
+        if n <= 0:
+            return hashes, nhash, length
+        check(lib().drephip_sketch(self._h, seq if len(seq) else np.zeros(1, np.uint8), rec_off,
+                                   len(rec_off) - 1, genome_rec_off, n, hashes.reshape(-1), nhash, length),
+              "drephip_sketch")
+        return hashes, nhash, length
+
+    def sketch_device(self, d_codes: int, d_valid: int, base_off, padded, nkmers, n: int,
+                      d_hashes: int, d_nhash: int, stream: Optional[int] = None) -> None:
+        check(lib().drephip_sketch_device(self._h, d_codes, d_valid,
+                                          np.ascontiguousarray(base_off, dtype=np.uint64),
+                                          np.ascontiguousarray(padded, dtype=np.uint64),
+                                          np.ascontiguousarray(nkmers, dtype=np.uint64), n,
+                                          d_hashes, d_nhash, stream), "drephip_sketch_device")
+
+    def synth_device(self, seed: int, g0: int, n: int, family_size: int, L: int, d_codes: int,
+                     d_valid: int, stream: Optional[int] = None) -> None:
+        check(lib().drephip_synth_device(self._h, seed, g0, n, family_size, L, d_codes, d_valid, stream),
+              "drephip_synth_device")
+
+    # -- all-pairs
+    def allpairs(self, hashes: np.ndarray, nhash: np.ndarray, want_denom: Optional[bool] = None):
+        hashes = np.ascontiguousarray(hashes, dtype=np.uint64)
+        nhash = np.ascontiguousarray(nhash, dtype=np.uint32)
+        N = len(nhash)
+        if hashes.shape != (N, self.s):
+            raise ValueError("hashes must be [N, s] = [%d, %d], got %s" % (N, self.s, hashes.shape))
+        npairs = N * (N - 1) // 2
+        if want_denom is None:
+            want_denom = bool((nhash < self.s).any())
+        common = np.zeros(max(npairs, 1), dtype=np.uint16)
+        denom = np.zeros(max(npairs, 1), dtype=np.uint16) if want_denom else None
+        if N >= 2:
+            check(lib().drephip_allpairs(self._h, hashes.reshape(-1), nhash, N, common,
+                                         denom.ctypes.data if denom is not None else None),
+                  "drephip_allpairs")
+        common = common[:npairs]
+        if denom is None:
+            denom = np.full(npairs, self.s, dtype=np.uint16)
+        else:
+            denom = denom[:npairs]
+        return common, denom
+
+    def allpairs_device(self, d_hashes: int, d_nhash: int, N: int, row0: int, row1: int, d_common: int,
+                        d_denom: Optional[int] = None, stream: Optional[int] = None, merge: bool = False):
+        fn = lib().drephip_allpairs_merge_device if merge else lib().drephip_allpairs_device
+        check(fn(self._h, d_hashes, d_nhash, N, row0, row1, d_common, d_denom, stream),
+              "drephip_allpairs_device")

@@ -1,0 +1,424 @@
+// api.cpp -- the extern "C" surface of libdrephip.so (include/drephip.h).
+// Host glue only: argument checks, device scratch, host<->device staging,
+// threads for FASTA ingest.  All sketch/dist arithmetic runs in the HIP
+// kernels of sketch.hip and allpairs.hip.
+#include "ctx.h"
+#include "../../include/drephip.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <thread>
+
+#define DREPHIP_EXPORT extern "C" __attribute__((visibility("default")))
+
+namespace drephip {
+
+static thread_local std::string g_err;
+void set_error(const std::string &msg) { g_err = msg; }
+
+int scratch(drephip_ctx *ctx, const char *name, size_t bytes, void **out) {
+    DevBuf &b = ctx->bufs[name];
+    if (bytes == 0) bytes = 8;
+    if (b.bytes < bytes) {
+        if (b.ptr) {
+            HIPC(hipStreamSynchronize(ctx->stream));
+            HIPC(hipDeviceSynchronize());
+            HIPC(hipFree(b.ptr));
+            b.ptr = nullptr; b.bytes = 0;
+        }
+        const size_t want = std::max(bytes, b.bytes + b.bytes / 4);
+        hipError_t e = hipMalloc(&b.ptr, want);
+        if (e != hipSuccess) {
+            set_error(std::string("hipMalloc(") + std::to_string(want) + ") for " + name + ": " +
+                      hipGetErrorString(e));
+            b.ptr = nullptr;
+            return DREPHIP_ERR_NOMEM;
+        }
+        b.bytes = want;
+    }
+    *out = b.ptr;
+    return DREPHIP_OK;
+}
+
+void timing_begin(drephip_ctx *ctx) {
+    for (int i = 0; i < 4; i++) { ctx->kms[i] = 0; ctx->kn[i] = 0; }
+    ctx->spans.clear();
+    ctx->ev_used = 0;
+}
+
+static hipEvent_t next_event(drephip_ctx *ctx) {
+    if (ctx->ev_used == ctx->ev_pool.size()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        ctx->ev_pool.push_back(e);
+    }
+    return ctx->ev_pool[ctx->ev_used++];
+}
+
+void timing_mark(drephip_ctx *ctx, int which, hipStream_t st, bool start) {
+    if (!ctx->timing) return;
+    hipEvent_t e = next_event(ctx);
+    if (!e) return;
+    (void)hipEventRecord(e, st);
+    if (start) ctx->spans.push_back({which, e, nullptr});
+    else if (!ctx->spans.empty()) ctx->spans.back().b = e;
+}
+
+void timing_collect(drephip_ctx *ctx) {
+    if (!ctx->timing) return;
+    for (auto &sp : ctx->spans) {
+        if (!sp.a || !sp.b) continue;
+        float ms = 0;
+        if (hipEventSynchronize(sp.b) == hipSuccess && hipEventElapsedTime(&ms, sp.a, sp.b) == hipSuccess) {
+            ctx->kms[sp.which] += ms;
+            ctx->kn[sp.which] += 1;
+        }
+    }
+    ctx->spans.clear();
+    ctx->ev_used = 0;
+}
+
+}  // namespace drephip
+
+using namespace drephip;
+
+#define GUARD_CTX(ctx)                                              \
+    do {                                                            \
+        if (!(ctx)) { set_error("null context"); return DREPHIP_ERR_ARG; } \
+        HIPC(hipSetDevice((ctx)->device));                          \
+    } while (0)
+
+static hipStream_t pick_stream(drephip_ctx *ctx, void *stream) {
+    return stream ? (hipStream_t)stream : ctx->stream;
+}
+
+DREPHIP_EXPORT int drephip_version(void) { return 100; }
+
+DREPHIP_EXPORT const char *drephip_last_error(void) { return g_err.c_str(); }
+
+DREPHIP_EXPORT int drephip_device_count(int *n) {
+    if (!n) { set_error("null pointer"); return DREPHIP_ERR_ARG; }
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) { *n = 0; set_error(hipGetErrorString(e)); return DREPHIP_ERR_HIP; }
+    *n = c;
+    return DREPHIP_OK;
+}
+
+DREPHIP_EXPORT uint32_t drephip_max_sketch(void) { return kMaxSketch; }
+DREPHIP_EXPORT uint64_t drephip_tile_bases(void) { return kTile; }
+
+DREPHIP_EXPORT uint64_t drephip_padded_bases(const uint64_t *rec_len, uint32_t n_rec) {
+    return padded_span(genome_span(rec_len, n_rec));
+}
+
+DREPHIP_EXPORT int drephip_create(int device, int k, uint32_t s, uint32_t seed, drephip_ctx **out) {
+    if (!out) { set_error("null out"); return DREPHIP_ERR_ARG; }
+    *out = nullptr;
+    if (k < 1 || k > 32) { set_error("k must be in 1..32"); return DREPHIP_ERR_ARG; }
+    if (s < 1 || s > kMaxSketch) {
+        set_error("sketch size must be in 1.." + std::to_string(kMaxSketch));
+        return DREPHIP_ERR_UNSUPPORTED;
+    }
+    int n = 0;
+    HIPC(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) { set_error("no such HIP device"); return DREPHIP_ERR_ARG; }
+    HIPC(hipSetDevice(device));
+    drephip_ctx *c = new (std::nothrow) drephip_ctx();
+    if (!c) { set_error("out of host memory"); return DREPHIP_ERR_NOMEM; }
+    c->device = device; c->k = k; c->s = s; c->seed = seed;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) { delete c; set_error(hipGetErrorString(e)); return DREPHIP_ERR_HIP; }
+    *out = c;
+    return DREPHIP_OK;
+}
+
+DREPHIP_EXPORT int drephip_destroy(drephip_ctx *ctx) {
+    if (!ctx) return DREPHIP_OK;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto &kv : ctx->bufs) if (kv.second.ptr) (void)hipFree(kv.second.ptr);
+    for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return DREPHIP_OK;
+}
+
+DREPHIP_EXPORT int drephip_set_timing(drephip_ctx *ctx, int enable) {
+    if (!ctx) { set_error("null context"); return DREPHIP_ERR_ARG; }
+    ctx->timing = enable != 0;
+    return DREPHIP_OK;
+}
+
+DREPHIP_EXPORT int drephip_last_kernel_ms(drephip_ctx *ctx, int which, double *ms, int *launches) {
+    if (!ctx || which < 0 || which > 3 || !ms) { set_error("bad argument"); return DREPHIP_ERR_ARG; }
+    *ms = ctx->kms[which];
+    if (launches) *launches = ctx->kn[which];
+    return DREPHIP_OK;
+}
+
+DREPHIP_EXPORT int drephip_fasta_info(const char *path, int k, uint64_t *length, uint64_t *padded,
+                                      uint32_t *n_records, uint64_t *n_kmers) {
+    if (!path) { set_error("null path"); return DREPHIP_ERR_ARG; }
+    Genome g;
+    if (read_fasta(path, g)) return DREPHIP_ERR_IO;
+    const uint32_t nr = (uint32_t)g.rec_len.size();
+    if (length) *length = g.length;
+    if (padded) *padded = padded_span(genome_span(g.rec_len.data(), nr));
+    if (n_records) *n_records = nr;
+    if (n_kmers) {
+        uint64_t nk = 0, off = 0;
+        for (uint32_t r = 0; r < nr; r++) {
+            uint64_t run = 0;
+            for (uint64_t i = 0; i < g.rec_len[r]; i++) {
+                const uint8_t c = g.seq[off + i] & 0xDF;
+                const bool ok = c == 'A' || c == 'C' || c == 'G' || c == 'T';
+                run = ok ? run + 1 : 0;
+                nk += run >= (uint64_t)k;
+            }
+            off += g.rec_len[r];
+        }
+        *n_kmers = nk;
+    }
+    return DREPHIP_OK;
+}
+
+DREPHIP_EXPORT int drephip_fasta_pack(const char *path, int k, uint32_t *codes, uint32_t *valid,
+                                      uint64_t base_off, uint64_t cap_bases, uint64_t *length,
+                                      uint64_t *n_kmers) {
+    if (!path || !codes || !valid) { set_error("null argument"); return DREPHIP_ERR_ARG; }
+    if (base_off % kTile) { set_error("base_off must be a tile multiple"); return DREPHIP_ERR_ARG; }
+    Genome g;
+    if (read_fasta(path, g)) return DREPHIP_ERR_IO;
+    const uint32_t nr = (uint32_t)g.rec_len.size();
+    const uint64_t P = padded_span(genome_span(g.rec_len.data(), nr));
+    if (base_off + P > cap_bases) { set_error("packed buffer too small"); return DREPHIP_ERR_ARG; }
+    const uint64_t nk = pack_records(g.seq.data(), g.rec_len.data(), nr, k, codes, valid, base_off);
+    if (length) *length = g.length;
+    if (n_kmers) *n_kmers = nk;
+    return DREPHIP_OK;
+}
+
+// Stage a packed genome set (already laid out on the host) and sketch it.
+static int sketch_packed_host(drephip_ctx *ctx, const std::vector<uint32_t> &codes,
+                              const std::vector<uint32_t> &valid, const std::vector<uint64_t> &off,
+                              const std::vector<uint64_t> &pad, const std::vector<uint64_t> &nk,
+                              uint64_t *hashes_out, uint32_t *nhash_out) {
+    const uint32_t n = (uint32_t)off.size();
+    hipStream_t st = ctx->stream;
+    uint32_t *d_codes, *d_valid, *d_nhash;
+    uint64_t *d_hashes;
+    int rc;
+    if ((rc = scratch(ctx, "in_codes", codes.size() * 4, (void **)&d_codes))) return rc;
+    if ((rc = scratch(ctx, "in_valid", valid.size() * 4, (void **)&d_valid))) return rc;
+    if ((rc = scratch(ctx, "out_hashes", (uint64_t)n * ctx->s * 8, (void **)&d_hashes))) return rc;
+    if ((rc = scratch(ctx, "out_nhash", n * 4ull, (void **)&d_nhash))) return rc;
+    HIPC(hipMemcpyAsync(d_codes, codes.data(), codes.size() * 4, hipMemcpyHostToDevice, st));
+    HIPC(hipMemcpyAsync(d_valid, valid.data(), valid.size() * 4, hipMemcpyHostToDevice, st));
+    timing_begin(ctx);
+    rc = sketch_device_impl(ctx, d_codes, d_valid, off.data(), pad.data(), nk.data(), n, d_hashes, d_nhash, st);
+    if (rc) return rc;
+    timing_collect(ctx);
+    HIPC(hipMemcpyAsync(hashes_out, d_hashes, (uint64_t)n * ctx->s * 8, hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(nhash_out, d_nhash, n * 4ull, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    return DREPHIP_OK;
+}
+
+template <class F>
+static void parallel_for(uint32_t n, int threads, F fn) {
+    int nt = threads > 0 ? threads : (int)std::thread::hardware_concurrency();
+    nt = std::max(1, std::min<int>(nt, (int)n));
+    std::atomic<uint32_t> next(0);
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nt; t++)
+        pool.emplace_back([&] {
+            for (uint32_t i = next++; i < n; i = next++) fn(i);
+        });
+    for (auto &th : pool) th.join();
+}
+
+DREPHIP_EXPORT int drephip_sketch(drephip_ctx *ctx, const uint8_t *seq, const uint64_t *rec_off,
+                                  uint32_t n_rec, const uint64_t *genome_rec_off, uint32_t n_genomes,
+                                  uint64_t *hashes_out, uint32_t *nhash_out, uint64_t *length_out) {
+    GUARD_CTX(ctx);
+    if (n_genomes == 0) return DREPHIP_OK;
+    if (!rec_off || !genome_rec_off || !hashes_out || !nhash_out || (!seq && n_rec && rec_off[n_rec] > 0)) {
+        set_error("null argument"); return DREPHIP_ERR_ARG;
+    }
+    if (genome_rec_off[0] != 0 || genome_rec_off[n_genomes] != n_rec) {
+        set_error("genome_rec_off must start at 0 and end at n_rec"); return DREPHIP_ERR_ARG;
+    }
+    std::vector<uint64_t> off(n_genomes), pad(n_genomes), nk(n_genomes), reclen(n_rec);
+    for (uint32_t r = 0; r < n_rec; r++) {
+        if (rec_off[r + 1] < rec_off[r]) { set_error("rec_off must be non-decreasing"); return DREPHIP_ERR_ARG; }
+        reclen[r] = rec_off[r + 1] - rec_off[r];
+    }
+    uint64_t cur = kTile;
+    for (uint32_t g = 0; g < n_genomes; g++) {
+        const uint64_t r0 = genome_rec_off[g], r1 = genome_rec_off[g + 1];
+        if (r1 < r0) { set_error("genome_rec_off must be non-decreasing"); return DREPHIP_ERR_ARG; }
+        off[g] = cur;
+        pad[g] = padded_span(genome_span(reclen.data() + r0, (uint32_t)(r1 - r0)));
+        cur += pad[g];
+        uint64_t L = 0;
+        for (uint64_t r = r0; r < r1; r++) L += reclen[r];
+        if (length_out) length_out[g] = L;
+    }
+    std::vector<uint32_t> codes(cur / 16, 0), valid(cur / 32, 0);
+    parallel_for(n_genomes, 0, [&](uint32_t g) {
+        const uint64_t r0 = genome_rec_off[g], r1 = genome_rec_off[g + 1];
+        nk[g] = pack_records(seq + (r1 > r0 ? rec_off[r0] : 0), reclen.data() + r0, (uint32_t)(r1 - r0),
+                             ctx->k, codes.data(), valid.data(), off[g]);
+    });
+    return sketch_packed_host(ctx, codes, valid, off, pad, nk, hashes_out, nhash_out);
+}
+
+DREPHIP_EXPORT int drephip_sketch_files(drephip_ctx *ctx, const char *const *paths, uint32_t n_genomes,
+                                        int threads, uint64_t *hashes_out, uint32_t *nhash_out,
+                                        uint64_t *length_out) {
+    GUARD_CTX(ctx);
+    if (n_genomes == 0) return DREPHIP_OK;
+    if (!paths || !hashes_out || !nhash_out) { set_error("null argument"); return DREPHIP_ERR_ARG; }
+    const uint64_t kBatchBases = 1ull << 31;   // ~2 Gbase of ASCII per batch
+    uint32_t g0 = 0;
+    while (g0 < n_genomes) {
+        // read a batch of files in parallel (bounded by bases read so far)
+        std::vector<Genome> gs;
+        uint64_t bases = 0;
+        uint32_t g1 = g0;
+        while (g1 < n_genomes && bases < kBatchBases) {
+            const uint32_t chunk = std::min<uint32_t>(n_genomes - g1, 64);
+            std::vector<Genome> part(chunk);
+            std::vector<int> err(chunk, 0);
+            std::vector<std::string> msg(chunk);
+            parallel_for(chunk, threads, [&](uint32_t i) {
+                err[i] = read_fasta(paths[g1 + i], part[i]);
+                if (err[i]) msg[i] = drephip_last_error();
+            });
+            for (uint32_t i = 0; i < chunk; i++)
+                if (err[i]) { set_error(msg[i]); return DREPHIP_ERR_IO; }
+            for (auto &g : part) { bases += g.length; gs.push_back(std::move(g)); }
+            g1 += chunk;
+        }
+        const uint32_t n = g1 - g0;
+        std::vector<uint64_t> off(n), pad(n), nk(n);
+        uint64_t cur = kTile;
+        for (uint32_t i = 0; i < n; i++) {
+            off[i] = cur;
+            pad[i] = padded_span(genome_span(gs[i].rec_len.data(), (uint32_t)gs[i].rec_len.size()));
+            cur += pad[i];
+            if (length_out) length_out[g0 + i] = gs[i].length;
+        }
+        std::vector<uint32_t> codes(cur / 16, 0), valid(cur / 32, 0);
+        parallel_for(n, threads, [&](uint32_t i) {
+            nk[i] = pack_records(gs[i].seq.data(), gs[i].rec_len.data(), (uint32_t)gs[i].rec_len.size(),
+                                 ctx->k, codes.data(), valid.data(), off[i]);
+        });
+        gs.clear();
+        const int rc = sketch_packed_host(ctx, codes, valid, off, pad, nk,
+                                          hashes_out + (uint64_t)g0 * ctx->s, nhash_out + g0);
+        if (rc) return rc;
+        g0 = g1;
+    }
+    return DREPHIP_OK;
+}
+
+DREPHIP_EXPORT int drephip_sketch_device(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t *d_valid,
+                                         const uint64_t *h_base_off, const uint64_t *h_padded,
+                                         const uint64_t *h_nkmers, uint32_t n_genomes, uint64_t *d_hashes,
+                                         uint32_t *d_nhash, void *stream) {
+    GUARD_CTX(ctx);
+    if (n_genomes == 0) return DREPHIP_OK;
+    if (!d_codes || !d_valid || !h_base_off || !h_padded || !h_nkmers || !d_hashes || !d_nhash) {
+        set_error("null argument"); return DREPHIP_ERR_ARG;
+    }
+    hipStream_t st = pick_stream(ctx, stream);
+    timing_begin(ctx);
+    int rc = sketch_device_impl(ctx, d_codes, d_valid, h_base_off, h_padded, h_nkmers, n_genomes, d_hashes,
+                                d_nhash, st);
+    if (rc) return rc;
+    timing_collect(ctx);
+    return DREPHIP_OK;
+}
+
+DREPHIP_EXPORT int drephip_synth_device(drephip_ctx *ctx, uint64_t seed, uint32_t g0, uint32_t n,
+                                        uint32_t family_size, uint64_t L, uint32_t *d_codes, uint32_t *d_valid,
+                                        void *stream) {
+    GUARD_CTX(ctx);
+    if (!d_codes || !d_valid) { set_error("null argument"); return DREPHIP_ERR_ARG; }
+    return synth_device_impl(ctx, seed, g0, n, family_size, L, d_codes, d_valid, pick_stream(ctx, stream));
+}
+
+DREPHIP_EXPORT int drephip_allpairs_device(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash,
+                                           uint32_t N, uint32_t row0, uint32_t row1, uint16_t *d_common,
+                                           uint16_t *d_denom, void *stream) {
+    GUARD_CTX(ctx);
+    if (!d_hashes || !d_nhash || !d_common) { set_error("null argument"); return DREPHIP_ERR_ARG; }
+    timing_begin(ctx);
+    int rc = allpairs_device_impl(ctx, d_hashes, d_nhash, N, row0, row1, d_common, d_denom,
+                                  pick_stream(ctx, stream), false);
+    if (rc) return rc;
+    timing_collect(ctx);
+    return DREPHIP_OK;
+}
+
+DREPHIP_EXPORT int drephip_allpairs_merge_device(drephip_ctx *ctx, const uint64_t *d_hashes,
+                                                 const uint32_t *d_nhash, uint32_t N, uint32_t row0,
+                                                 uint32_t row1, uint16_t *d_common, uint16_t *d_denom,
+                                                 void *stream) {
+    GUARD_CTX(ctx);
+    if (!d_hashes || !d_nhash || !d_common) { set_error("null argument"); return DREPHIP_ERR_ARG; }
+    timing_begin(ctx);
+    int rc = allpairs_device_impl(ctx, d_hashes, d_nhash, N, row0, row1, d_common, d_denom,
+                                  pick_stream(ctx, stream), true);
+    if (rc) return rc;
+    timing_collect(ctx);
+    return DREPHIP_OK;
+}
+
+DREPHIP_EXPORT int drephip_allpairs(drephip_ctx *ctx, const uint64_t *hashes, const uint32_t *nhash, uint32_t N,
+                                    uint16_t *common_out, uint16_t *denom_out) {
+    GUARD_CTX(ctx);
+    if (N < 2) return DREPHIP_OK;
+    if (!hashes || !nhash || !common_out) { set_error("null argument"); return DREPHIP_ERR_ARG; }
+    const uint64_t npairs = (uint64_t)N * (N - 1) / 2;
+    hipStream_t st = ctx->stream;
+    uint64_t *d_h;
+    uint32_t *d_n;
+    uint16_t *d_c, *d_d = nullptr;
+    int rc;
+    if ((rc = scratch(ctx, "ap_in_h", (uint64_t)N * ctx->s * 8, (void **)&d_h))) return rc;
+    if ((rc = scratch(ctx, "ap_in_n", N * 4ull, (void **)&d_n))) return rc;
+    if ((rc = scratch(ctx, "ap_out_c", npairs * 2, (void **)&d_c))) return rc;
+    if (denom_out && (rc = scratch(ctx, "ap_out_d", npairs * 2, (void **)&d_d))) return rc;
+    HIPC(hipMemcpyAsync(d_h, hashes, (uint64_t)N * ctx->s * 8, hipMemcpyHostToDevice, st));
+    HIPC(hipMemcpyAsync(d_n, nhash, N * 4ull, hipMemcpyHostToDevice, st));
+    timing_begin(ctx);
+    rc = allpairs_device_impl(ctx, d_h, d_n, N, 0, N, d_c, d_d, st, false);
+    if (rc) return rc;
+    timing_collect(ctx);
+    HIPC(hipMemcpyAsync(common_out, d_c, npairs * 2, hipMemcpyDeviceToHost, st));
+    if (denom_out) HIPC(hipMemcpyAsync(denom_out, d_d, npairs * 2, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    return DREPHIP_OK;
+}
+
+DREPHIP_EXPORT int drephip_distance_lut(int k, uint32_t denom, double *lut) {
+    if (!lut || k < 1 || denom == 0) { set_error("bad argument"); return DREPHIP_ERR_ARG; }
+    for (uint32_t c = 0; c <= denom; c++) {
+        double d;
+        if (c == denom) d = 0.0;
+        else if (c == 0) d = 1.0;
+        else {
+            const double j = (double)c / (double)denom;
+            d = -std::log(2.0 * j / (1.0 + j)) / (double)k;
+            if (d > 1.0) d = 1.0;
+        }
+        lut[c] = d;
+    }
+    return DREPHIP_OK;
+}

@@ -1,0 +1,77 @@
+// ctx.h -- the drephip_ctx object behind the C ABI (host side).
+#pragma once
+
+#include "common.h"
+
+#include <hip/hip_runtime.h>
+#include <map>
+#include <string>
+#include <vector>
+
+struct DevBuf {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+};
+
+struct drephip_ctx {
+    int device = 0;
+    int k = 21;
+    uint32_t s = 1000;
+    uint32_t seed = 42;
+    hipStream_t stream = nullptr;
+    bool timing = false;
+    // named grow-only device scratch buffers
+    std::map<std::string, DevBuf> bufs;
+    // per-kernel timing of the last call: {sum ms, launches}
+    double kms[4] = {0, 0, 0, 0};
+    int kn[4] = {0, 0, 0, 0};
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
+    struct Span { int which; hipEvent_t a, b; };
+    std::vector<Span> spans;
+};
+
+namespace drephip {
+
+// hip error -> set_error + return code
+#define HIPC(expr)                                                                     \
+    do {                                                                               \
+        hipError_t _e = (expr);                                                        \
+        if (_e != hipSuccess) {                                                        \
+            ::drephip::set_error(std::string(#expr) + ": " + hipGetErrorString(_e)); \
+            return DREPHIP_ERR_HIP;                                                    \
+        }                                                                              \
+    } while (0)
+
+// Grow-only named scratch buffer on the context's device.
+int scratch(drephip_ctx *ctx, const char *name, size_t bytes, void **out);
+
+// Bracket kernel launches with events when ctx->timing is on; resolved by
+// timing_collect() after the stream is synchronised.
+void timing_begin(drephip_ctx *ctx);
+void timing_mark(drephip_ctx *ctx, int which, hipStream_t st, bool start);
+void timing_collect(drephip_ctx *ctx);
+
+// Kernel drivers (sketch.hip / allpairs.hip).
+int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t *d_valid,
+                       const uint64_t *base_off, const uint64_t *padded, const uint64_t *nkmers,
+                       uint32_t n, uint64_t *d_hashes, uint32_t *d_nhash, hipStream_t st);
+int synth_device_impl(drephip_ctx *ctx, uint64_t seed, uint32_t g0, uint32_t n, uint32_t family_size,
+                      uint64_t L, uint32_t *d_codes, uint32_t *d_valid, hipStream_t st);
+int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash,
+                         uint32_t N, uint32_t row0, uint32_t row1, uint16_t *d_common,
+                         uint16_t *d_denom, hipStream_t st, bool force_merge);
+
+// Host ingest (ingest.cpp).
+struct Genome {
+    std::vector<uint8_t> seq;        // concatenated record bytes (raw case)
+    std::vector<uint64_t> rec_len;   // record lengths
+    uint64_t length = 0;             // sum of record lengths
+};
+int read_fasta(const char *path, Genome &g);
+uint64_t genome_span(const uint64_t *rec_len, uint32_t n_rec);
+// pack records into codes/valid at base offset; returns valid k-mer count
+uint64_t pack_records(const uint8_t *seq, const uint64_t *rec_len, uint32_t n_rec, int k,
+                      uint32_t *codes, uint32_t *valid, uint64_t base_off);
+
+}  // namespace drephip

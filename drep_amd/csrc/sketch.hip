@@ -1,0 +1,392 @@
+// sketch.hip -- MI355X sketch path: replaces `mash sketch <fa> -s S` per
+// genome (drep/d_cluster.py:531-549) and `mash paste` (551-567).
+//
+// Three kernels, one pass over the packed genome set per round:
+//   k_sketch_hash     one workgroup per 32768-base tile; each lane rolls a
+//                     k-mer window over 128 window ends (2-bit codes +
+//                     validity from HBM, one 64-bit load pair per 16 bases),
+//                     keeps forward/reverse-complement ASCII windows in
+//                     registers, hashes the canonical k-mer with
+//                     MurmurHash3_x64_128 and admits it only if h <= T[g]
+//                     (per-genome candidate threshold).  Candidates go into a
+//                     per-genome open-addressing set in HBM (64-bit CAS), so
+//                     duplicates are dropped at insert time.
+//   k_sketch_finalize one workgroup per genome: compacts the set into LDS,
+//                     bitonic-sorts it and writes the s smallest.
+//   k_synth           bench input generator (not on the product path).
+// The threshold is seeded from the k-mer count so ~F*s distinct candidates
+// survive; a genome whose set ends with fewer than s distinct hashes (T too
+// low) or more than the LDS sort holds (T too high) is re-run with a bisected
+// T -- exact for every input, normally a single round.
+//
+// Roofline: integer VALU (≈40 quarter-rate 32-bit multiplies per k-mer for the
+// two 64-bit Murmur mixes); HBM traffic is 3 bits/base (0.375 B/base) plus the
+// candidate sets.
+
+#include "ctx.h"
+#include "../../include/drephip.h"
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+namespace drephip {
+
+// ------------------------------------------------------------ k-mer window
+template <int K>
+struct Window {
+    static constexpr int NW = (K + 7) / 8;
+    static constexpr int LASTB = (K - 1) % 8;
+    static constexpr uint64_t LASTMASK = (K % 8 == 0) ? ~0ull : ((1ull << (8 * (K % 8))) - 1);
+    static constexpr uint64_t CMASK = (K == 32) ? ~0ull : ((1ull << (2 * K)) - 1);
+    uint64_t f[NW];     // forward k-mer, ASCII, byte j = base (end-K+1+j)
+    uint64_t r[NW];     // reverse complement, ASCII, byte j = comp(base end-j)
+    uint64_t fc, rc;    // 2-bit codes, first character most significant
+    uint32_t run;       // consecutive valid bases ending here
+
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int i = 0; i < NW; i++) { f[i] = 0; r[i] = 0; }
+        fc = rc = 0; run = 0;
+    }
+    __device__ __forceinline__ void push(uint32_t c, uint32_t v) {
+        run = v ? run + 1 : 0;
+        fc = ((fc << 2) | c) & CMASK;
+        rc = (rc >> 2) | ((uint64_t)(3u - c) << (2 * (K - 1)));
+        const uint64_t a = (0x54474341u >> (8 * c)) & 0xffu;          // A C G T
+        const uint64_t ca = (0x41434754u >> (8 * c)) & 0xffu;         // T G C A
+#pragma unroll
+        for (int i = 0; i < NW - 1; i++) f[i] = (f[i] >> 8) | (f[i + 1] << 56);
+        f[NW - 1] = (f[NW - 1] >> 8) | (a << (8 * LASTB));
+#pragma unroll
+        for (int i = NW - 1; i > 0; i--) r[i] = (r[i] << 8) | (r[i - 1] >> 56);
+        r[0] = (r[0] << 8) | ca;
+        r[NW - 1] &= LASTMASK;
+    }
+    __device__ __forceinline__ uint64_t hash(uint32_t seed) const {
+        uint64_t w[NW];
+        const bool fwd = fc <= rc;   // memcmp(fwd, rev, K) <= 0
+#pragma unroll
+        for (int i = 0; i < NW; i++) w[i] = fwd ? f[i] : r[i];
+        return murmur3_h1_words<K>(w, seed);
+    }
+};
+
+__device__ __forceinline__ void set_insert(unsigned long long *S, uint32_t mask, uint32_t *cnt,
+                                           uint32_t limit, uint64_t h) {
+    if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= limit) return;
+    uint32_t slot = (uint32_t)h & mask;
+    for (uint32_t probe = 0; probe <= mask; probe++) {
+        unsigned long long old = atomicCAS(&S[slot], (unsigned long long)kEmpty, (unsigned long long)h);
+        if (old == kEmpty) { atomicAdd(cnt, 1u); return; }
+        if (old == h) return;
+        slot = (slot + 1) & mask;
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(kSketchWG) void k_sketch_hash(
+    const uint32_t *__restrict__ codes, const uint32_t *__restrict__ valid,
+    const uint64_t *__restrict__ tile_base, const uint32_t *__restrict__ tile_genome,
+    const uint64_t *__restrict__ thr, unsigned long long *__restrict__ sets,
+    uint32_t *__restrict__ cnt, uint32_t set_log2, uint32_t limit, uint32_t seed) {
+    const uint32_t t = blockIdx.x;
+    const uint32_t g = tile_genome[t];
+    const uint64_t T = thr[g];
+    const uint64_t start = tile_base[t] + (uint64_t)threadIdx.x * kLaneBases;
+    const uint32_t mask = (1u << set_log2) - 1;
+    unsigned long long *S = sets + ((uint64_t)g << set_log2);
+    uint32_t *C = cnt + g;
+
+    // window ends [start - 32, start) warm the window; [start, start+128) emit
+    const uint32_t *cw = codes + (start - kWarm) / 16;
+    const uint32_t *vw = valid + (start - kWarm) / 32;
+    Window<K> w;
+    w.init();
+    {
+        const uint32_t v0 = vw[0];
+        const uint32_t c0 = cw[0], c1 = cw[1];
+#pragma unroll
+        for (int b = 0; b < 16; b++) w.push((c0 >> (2 * b)) & 3u, (v0 >> b) & 1u);
+#pragma unroll
+        for (int b = 0; b < 16; b++) w.push((c1 >> (2 * b)) & 3u, (v0 >> (16 + b)) & 1u);
+    }
+    uint32_t cnext = cw[2];
+    uint32_t vcur = vw[1];
+    for (int wi = 0; wi < (int)(kLaneBases / 16); wi++) {
+        const uint32_t c = cnext;
+        const uint32_t vbits = vcur >> ((wi & 1) * 16);
+        if (wi + 1 < (int)(kLaneBases / 16)) {
+            cnext = cw[3 + wi];
+            if (wi & 1) vcur = vw[2 + (wi >> 1)];
+        }
+#pragma unroll
+        for (int b = 0; b < 16; b++) {
+            w.push((c >> (2 * b)) & 3u, (vbits >> b) & 1u);
+            if (w.run >= (uint32_t)K) {
+                const uint64_t h = w.hash(seed);
+                if (__builtin_expect(h <= T, 0)) set_insert(S, mask, C, limit, h);
+            }
+        }
+    }
+}
+
+// ----------------------------------------------------------------- finalize
+enum : uint8_t { ST_OK = 0, ST_UP = 1, ST_DOWN = 2 };
+
+template <int MAXC>
+__global__ __launch_bounds__(1024) void k_sketch_finalize(
+    const unsigned long long *__restrict__ sets, const uint32_t *__restrict__ cnt,
+    const uint64_t *__restrict__ thr, const uint32_t *__restrict__ glist, uint32_t set_log2,
+    uint32_t maxc, uint32_t s, uint64_t *__restrict__ out, uint32_t *__restrict__ nhash,
+    uint8_t *__restrict__ status) {
+    __shared__ uint64_t buf[MAXC];
+    __shared__ uint32_t pos;
+    const uint32_t g = glist[blockIdx.x];
+    const uint32_t n = cnt[g];
+    const uint32_t tid = threadIdx.x;
+    if (n > maxc) { if (tid == 0) status[g] = ST_DOWN; return; }
+    if (n < s && thr[g] < kMaxThr) { if (tid == 0) status[g] = ST_UP; return; }
+    if (tid == 0) pos = 0;
+    __syncthreads();
+    const unsigned long long *S = sets + ((uint64_t)g << set_log2);
+    const uint32_t slots = 1u << set_log2;
+    for (uint32_t i = tid; i < slots; i += blockDim.x) {
+        const uint64_t v = S[i];
+        if (v != kEmpty) buf[atomicAdd(&pos, 1u)] = v;
+    }
+    __syncthreads();
+    uint32_t P = 1;
+    while (P < n) P <<= 1;
+    for (uint32_t i = n + tid; i < P; i += blockDim.x) buf[i] = kEmpty;
+    __syncthreads();
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = tid; i < P; i += blockDim.x) {
+                const uint32_t ixj = i ^ j;
+                if (ixj > i) {
+                    const uint64_t a = buf[i], b = buf[ixj];
+                    const bool up = (i & k) == 0;
+                    if ((a > b) == up) { buf[i] = b; buf[ixj] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    const uint32_t m = n < s ? n : s;
+    uint64_t *o = out + (uint64_t)g * s;
+    for (uint32_t i = tid; i < s; i += blockDim.x) o[i] = i < m ? buf[i] : kEmpty;
+    if (tid == 0) { nhash[g] = m; status[g] = ST_OK; }
+}
+
+__global__ void k_reset_sets(unsigned long long *__restrict__ sets, uint32_t *__restrict__ cnt,
+                             const uint32_t *__restrict__ glist, uint32_t set_log2) {
+    const uint32_t g = glist[blockIdx.x];
+    unsigned long long *S = sets + ((uint64_t)g << set_log2);
+    const uint32_t slots = 1u << set_log2;
+    for (uint32_t i = threadIdx.x; i < slots; i += blockDim.x) S[i] = kEmpty;
+    if (threadIdx.x == 0) cnt[g] = 0;
+}
+
+// ----------------------------------------------------------------- synth
+// One thread per 32-base word pair (two code words + one validity word).
+__global__ void k_synth(uint64_t seed, uint32_t g0, uint32_t n, uint32_t fam, uint64_t L,
+                        uint64_t P, uint32_t *__restrict__ codes, uint32_t *__restrict__ valid,
+                        uint64_t nwords32) {
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nwords32) return;
+    const uint64_t p0 = w * 32;
+    uint32_t c_lo = 0, c_hi = 0, v = 0;
+    if (p0 >= kTile) {
+        const uint64_t rel = p0 - kTile;
+        const uint32_t i = (uint32_t)(rel / P);
+        const uint64_t q0 = rel - (uint64_t)i * P;   // 32-aligned (P is a tile multiple)
+        if (i < n && q0 < L) {
+            const uint32_t g = g0 + i;
+            const uint32_t f = g / fam;
+            const uint64_t anc = splitmix64((kSynA ^ seed) ^ ((uint64_t)f << 32) ^ (q0 >> 5));
+            const uint32_t thr = synth_rate_thr((uint32_t)(splitmix64((kSynR ^ seed) ^ g) % 7));
+            for (int b = 0; b < 32; b++) {
+                const uint64_t q = q0 + b;
+                if (q >= L) break;
+                uint32_t c = (uint32_t)(anc >> (2 * b)) & 3u;
+                const uint64_t u = splitmix64((kSynM ^ seed) ^ ((uint64_t)g << 32) ^ q);
+                if ((uint32_t)(u >> 32) < thr) c = (c + 1 + (uint32_t)(u & 0xffffffffu) % 3u) & 3u;
+                if (b < 16) c_lo |= c << (2 * b); else c_hi |= c << (2 * (b - 16));
+                v |= 1u << b;
+            }
+        }
+    }
+    codes[2 * w] = c_lo;
+    codes[2 * w + 1] = c_hi;
+    valid[w] = v;
+}
+
+// ------------------------------------------------------------- host driver
+static uint64_t initial_threshold(uint64_t nk, uint32_t s, double F) {
+    const double E = F * (double)s;
+    if ((double)nk <= E) return kMaxThr;
+    const long double t = (long double)18446744073709551616.0L * (long double)E / (long double)nk;
+    if (t >= (long double)kMaxThr) return kMaxThr;
+    return (uint64_t)t < 1 ? 1 : (uint64_t)t;
+}
+
+struct SketchPlan {
+    uint32_t maxc, set_log2;
+    double F;
+};
+static SketchPlan plan_for(uint32_t s) {
+    SketchPlan p;
+    p.F = s <= 4096 ? 2.0 : 1.3;
+    const double E = p.F * s;
+    uint32_t mc = 1024;
+    while (mc < 2 * E && mc < 16384) mc <<= 1;
+    p.maxc = mc;
+    p.set_log2 = 1;
+    while ((1u << p.set_log2) < 2 * mc) p.set_log2++;
+    return p;
+}
+
+template <int K>
+static void launch_hash(uint32_t ntiles, hipStream_t st, const uint32_t *codes, const uint32_t *valid,
+                        const uint64_t *tb, const uint32_t *tg, const uint64_t *thr,
+                        unsigned long long *sets, uint32_t *cnt, uint32_t sl, uint32_t limit, uint32_t seed) {
+    hipLaunchKernelGGL(k_sketch_hash<K>, dim3(ntiles), dim3(kSketchWG), 0, st, codes, valid, tb, tg,
+                       thr, sets, cnt, sl, limit, seed);
+}
+
+int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t *d_valid,
+                       const uint64_t *base_off, const uint64_t *padded, const uint64_t *nkmers,
+                       uint32_t n, uint64_t *d_hashes, uint32_t *d_nhash, hipStream_t st) {
+    if (n == 0) return DREPHIP_OK;
+    if (ctx->k != 21) { set_error("sketch kernel is instantiated for k=21 (Mash/dRep default) only"); return DREPHIP_ERR_UNSUPPORTED; }
+    const uint32_t s = ctx->s;
+    const SketchPlan plan = plan_for(s);
+    const uint64_t slots = 1ull << plan.set_log2;
+    const uint32_t limit = (uint32_t)(slots * 3 / 4);
+
+    // tile table + initial thresholds (host)
+    std::vector<uint64_t> tbase;
+    std::vector<uint32_t> tgen;
+    std::vector<std::vector<uint32_t>> tiles_of(n);
+    for (uint32_t g = 0; g < n; g++) {
+        if (base_off[g] % kTile || padded[g] % kTile || base_off[g] < kTile) {
+            set_error("genome base_off/padded must be tile multiples and base_off >= tile");
+            return DREPHIP_ERR_ARG;
+        }
+        for (uint64_t t = 0; t < padded[g] / kTile; t++) {
+            tiles_of[g].push_back((uint32_t)tbase.size());
+            tbase.push_back(base_off[g] + t * kTile);
+            tgen.push_back(g);
+        }
+    }
+    std::vector<uint64_t> T(n), lo(n, 0), hi(n, 0);   // hi == 0: unknown
+    for (uint32_t g = 0; g < n; g++) T[g] = initial_threshold(nkmers[g], s, plan.F);
+
+    uint64_t *d_tb, *d_thr, *d_tbsub;
+    uint32_t *d_tg, *d_cnt, *d_gl, *d_tgsub;
+    unsigned long long *d_sets;
+    uint8_t *d_st;
+    int rc;
+    const uint32_t ntiles = (uint32_t)tbase.size();
+    if ((rc = scratch(ctx, "sk_tb", ntiles * 8ull, (void **)&d_tb))) return rc;
+    if ((rc = scratch(ctx, "sk_tg", ntiles * 4ull, (void **)&d_tg))) return rc;
+    if ((rc = scratch(ctx, "sk_tbsub", ntiles * 8ull, (void **)&d_tbsub))) return rc;
+    if ((rc = scratch(ctx, "sk_tgsub", ntiles * 4ull, (void **)&d_tgsub))) return rc;
+    if ((rc = scratch(ctx, "sk_thr", n * 8ull, (void **)&d_thr))) return rc;
+    if ((rc = scratch(ctx, "sk_cnt", n * 4ull, (void **)&d_cnt))) return rc;
+    if ((rc = scratch(ctx, "sk_gl", n * 4ull, (void **)&d_gl))) return rc;
+    if ((rc = scratch(ctx, "sk_st", n * 1ull, (void **)&d_st))) return rc;
+    if ((rc = scratch(ctx, "sk_sets", (uint64_t)n * slots * 8ull, (void **)&d_sets))) return rc;
+
+    HIPC(hipMemcpyAsync(d_tb, tbase.data(), ntiles * 8ull, hipMemcpyHostToDevice, st));
+    HIPC(hipMemcpyAsync(d_tg, tgen.data(), ntiles * 4ull, hipMemcpyHostToDevice, st));
+    HIPC(hipMemcpyAsync(d_thr, T.data(), n * 8ull, hipMemcpyHostToDevice, st));
+    HIPC(hipMemsetAsync(d_sets, 0xFF, (uint64_t)n * slots * 8ull, st));
+    HIPC(hipMemsetAsync(d_cnt, 0, n * 4ull, st));
+    std::vector<uint32_t> glist(n);
+    for (uint32_t g = 0; g < n; g++) glist[g] = g;
+    HIPC(hipMemcpyAsync(d_gl, glist.data(), n * 4ull, hipMemcpyHostToDevice, st));
+
+    std::vector<uint8_t> status(n);
+    std::vector<uint32_t> todo = glist;
+    bool first = true;
+    for (int round = 0; round < 130 && !todo.empty(); round++) {
+        const uint32_t *tb_tiles_g = d_tg;
+        const uint64_t *tb_tiles_b = d_tb;
+        uint32_t nt = ntiles;
+        if (!first) {
+            // subset: reset sets of the retried genomes, gather their tiles
+            std::vector<uint64_t> sb;
+            std::vector<uint32_t> sg;
+            for (uint32_t g : todo)
+                for (uint32_t t : tiles_of[g]) { sb.push_back(tbase[t]); sg.push_back(g); }
+            nt = (uint32_t)sb.size();
+            HIPC(hipMemcpyAsync(d_tbsub, sb.data(), nt * 8ull, hipMemcpyHostToDevice, st));
+            HIPC(hipMemcpyAsync(d_tgsub, sg.data(), nt * 4ull, hipMemcpyHostToDevice, st));
+            HIPC(hipMemcpyAsync(d_gl, todo.data(), todo.size() * 4ull, hipMemcpyHostToDevice, st));
+            HIPC(hipMemcpyAsync(d_thr, T.data(), n * 8ull, hipMemcpyHostToDevice, st));
+            hipLaunchKernelGGL(k_reset_sets, dim3((uint32_t)todo.size()), dim3(256), 0, st, d_sets,
+                               d_cnt, d_gl, plan.set_log2);
+            tb_tiles_g = d_tgsub;
+            tb_tiles_b = d_tbsub;
+        }
+        if (nt > 0) {
+            timing_mark(ctx, 0, st, true);
+            launch_hash<21>(nt, st, d_codes, d_valid, tb_tiles_b, tb_tiles_g, d_thr, d_sets, d_cnt,
+                            plan.set_log2, limit, ctx->seed);
+            timing_mark(ctx, 0, st, false);
+        }
+        timing_mark(ctx, 1, st, true);
+        if (plan.maxc <= 4096)
+            hipLaunchKernelGGL(k_sketch_finalize<4096>, dim3((uint32_t)todo.size()), dim3(1024), 0, st,
+                               d_sets, d_cnt, d_thr, d_gl, plan.set_log2, plan.maxc, s, d_hashes, d_nhash, d_st);
+        else
+            hipLaunchKernelGGL(k_sketch_finalize<16384>, dim3((uint32_t)todo.size()), dim3(1024), 0, st,
+                               d_sets, d_cnt, d_thr, d_gl, plan.set_log2, plan.maxc, s, d_hashes, d_nhash, d_st);
+        timing_mark(ctx, 1, st, false);
+        HIPC(hipGetLastError());
+        HIPC(hipMemcpyAsync(status.data(), d_st, n, hipMemcpyDeviceToHost, st));
+        HIPC(hipStreamSynchronize(st));
+        first = false;
+        std::vector<uint32_t> next;
+        for (uint32_t g : todo) {
+            if (status[g] == ST_OK) continue;
+            if (status[g] == ST_UP) {
+                lo[g] = T[g];
+                if (hi[g]) T[g] = (uint64_t)(((unsigned __int128)lo[g] + hi[g]) / 2);
+                else T[g] = T[g] > kMaxThr / 8 ? kMaxThr : T[g] * 8;
+            } else if (status[g] == ST_DOWN) {
+                hi[g] = T[g];
+                T[g] = (uint64_t)(((unsigned __int128)lo[g] + hi[g]) / 2);
+            } else {
+                set_error("sketch finalize left an unknown status");
+                return DREPHIP_ERR_INTERNAL;
+            }
+            if (T[g] <= lo[g] || (hi[g] && T[g] >= hi[g])) {
+                set_error("sketch threshold bisection did not converge");
+                return DREPHIP_ERR_INTERNAL;
+            }
+            next.push_back(g);
+        }
+        todo.swap(next);
+    }
+    if (!todo.empty()) { set_error("sketch did not converge"); return DREPHIP_ERR_INTERNAL; }
+    return DREPHIP_OK;
+}
+
+int synth_device_impl(drephip_ctx *ctx, uint64_t seed, uint32_t g0, uint32_t n, uint32_t family_size,
+                      uint64_t L, uint32_t *d_codes, uint32_t *d_valid, hipStream_t st) {
+    if (family_size == 0) { set_error("family_size must be > 0"); return DREPHIP_ERR_ARG; }
+    const uint64_t P = padded_span(L);
+    const uint64_t total = kTile + (uint64_t)n * P;
+    const uint64_t nw32 = total / 32;
+    const uint32_t blocks = (uint32_t)((nw32 + 255) / 256);
+    hipLaunchKernelGGL(k_synth, dim3(blocks), dim3(256), 0, st, seed, g0, n, family_size, L, P, d_codes,
+                       d_valid, nw32);
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(st));
+    return DREPHIP_OK;
+}
+
+}  // namespace drephip

@@ -1,0 +1,436 @@
+"""Drop-in for the Mash half of dRep's primary clustering, on MI355X.
+
+Mirrors the reference functions of ``drep/d_cluster.py`` that sit on the hot
+path -- same names, arguments, return values and side effects on the work
+directory -- with the external ``mash sketch`` / ``mash paste`` /
+``mash dist`` processes replaced by libdrephip.so (HIP kernels, gfx950):
+
+===============================  ==========================================
+reference (drep/d_cluster.py)    here
+===============================  ==========================================
+all_vs_all_MASH       481-596    :func:`all_vs_all_MASH`
+cluster_mash_database 598-630    :func:`cluster_mash_database`
+cluster_hierarchical  429-461    :func:`cluster_hierarchical`
+_gen_cdb_from_fclust  463-479    :func:`_gen_cdb_from_fclust`
+_get_genome_name_from_fasta 632  :func:`_get_genome_name_from_fasta`
+load_genomes         1483-1518   :func:`load_genomes`
+===============================  ==========================================
+
+Beyond the reference (needed at 10^4-10^5 genomes, where an N^2-row Mdb does
+not fit): :func:`all_vs_all_MASH_condensed` returns the condensed
+``common``/``denom`` vectors and :func:`mdb_from_condensed` /
+:func:`cluster_mash_condensed` build the Mdb / primary clusters from them with
+the same float32 arithmetic the reference applies.
+"""
+from __future__ import annotations
+
+import io
+import logging
+import os
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import pandas as pd
+import scipy.cluster.hierarchy
+import scipy.spatial.distance as ssd
+
+from . import _lib
+from .mash_io import MashReference, read_msh, write_msh
+
+MASH_K = 21          # Mash default, never overridden by dRep (d_cluster.py:543)
+MASH_SEED = 42       # Mash default hash seed
+
+
+# --------------------------------------------------------------- genomes
+def _get_genome_name_from_fasta(fasta):
+    """os.path.basename (reference drep/d_cluster.py:632-642)."""
+    return str(os.path.basename(fasta))
+
+
+def load_genomes(genome_list):
+    """List of genome paths (or one text file listing them) -> Bdb
+    [genome, location] (reference drep/d_cluster.py:1483-1518)."""
+    assert type(genome_list) == type(list())
+    if len(genome_list) == 1:
+        logging.info('Loading genomes from a list')
+        try:
+            Table = {'genome': [], 'location': []}
+            with open(genome_list[0], 'r') as o:
+                for line in o.readlines():
+                    genome = line.strip()
+                    assert os.path.isfile(genome), "{0} is not a file".format(genome)
+                    Table['genome'].append(os.path.basename(genome))
+                    Table['location'].append(os.path.abspath(genome))
+            return pd.DataFrame(Table)
+        except Exception:
+            logging.info('Nevermind! Ill try loading as a genome now')
+    Table = {'genome': [], 'location': []}
+    for genome in genome_list:
+        assert os.path.isfile(genome), "{0} is not a file".format(genome)
+        Table['genome'].append(os.path.basename(genome))
+        Table['location'].append(os.path.abspath(genome))
+    return pd.DataFrame(Table)
+
+
+# ----------------------------------------------------------- distances
+def mash_distance_float32(common: np.ndarray, denom: np.ndarray, k: int = MASH_K) -> np.ndarray:
+    """float32 "dist" values exactly as the reference obtains them.
+
+    The reference parses Mash's text output: ``mash dist`` prints the double
+    distance with C++ ostream defaults (= ``%g``, 6 significant digits) and
+    ``pd.read_csv(..., dtype={'dist': np.float32})`` parses it
+    (d_cluster.py:570-581).  Distance is a pure function of (common, denom), so
+    the at most (s+1) x (#denominators) distinct values are formatted and
+    pushed through the same ``read_csv`` call, then gathered.
+    """
+    common = np.asarray(common)
+    denom = np.asarray(denom)
+    out = np.empty(common.shape, dtype=np.float32)
+    if common.size == 0:
+        return out
+    for d in np.unique(denom):
+        d = int(d)
+        sel = denom == d
+        if d == 0:
+            lut = np.zeros(1, dtype=np.float64)   # common == denom == 0 -> 0 (Mash)
+        else:
+            lut = _lib.distance_lut(d, k)
+        txt = "\n".join("%g" % v for v in lut) + "\n"
+        lut32 = pd.read_csv(io.StringIO(txt), header=None, names=['dist'],
+                            dtype={'dist': np.float32}, sep='\t')['dist'].to_numpy()
+        out[sel] = lut32[common[sel]]
+    return out
+
+
+def _square(vec: np.ndarray, N: int, diag: np.ndarray) -> np.ndarray:
+    M = np.zeros((N, N), dtype=vec.dtype)
+    iu = np.triu_indices(N, 1)
+    M[iu] = vec
+    M = M + M.T
+    M[np.arange(N), np.arange(N)] = diag
+    return M
+
+
+def mdb_from_condensed(names: Sequence[str], common: np.ndarray, denom: np.ndarray,
+                       nhash: np.ndarray, s: int, k: int = MASH_K) -> pd.DataFrame:
+    """Long-form Mdb (genome1, genome2, dist, similarity) from the condensed
+    all-pairs result, with the reference's row order (outer loop = query =
+    genome2, inner = reference = genome1, as `mash dist` prints), dtypes
+    (ordered categoricals sorted by name; float32) and values
+    (d_cluster.py:575-596)."""
+    N = len(names)
+    nh = np.minimum(np.asarray(nhash, dtype=np.int64), s)
+    Cm = _square(np.asarray(common, dtype=np.uint16), N, nh.astype(np.uint16))
+    Dm = _square(np.asarray(denom, dtype=np.uint16), N, nh.astype(np.uint16))
+    dist = mash_distance_float32(Cm.reshape(-1), Dm.reshape(-1), k)   # row q, col r: symmetric
+    cats = sorted(set(names))
+    pos = {n: i for i, n in enumerate(cats)}
+    codes = np.array([pos[n] for n in names], dtype=np.int32)
+    g1 = pd.Categorical.from_codes(np.tile(codes, N), categories=cats, ordered=True)
+    g2 = pd.Categorical.from_codes(np.repeat(codes, N), categories=cats, ordered=True)
+    Mdb = pd.DataFrame({'genome1': g1, 'genome2': g2, 'dist': dist})
+    Mdb['similarity'] = 1 - Mdb['dist']
+    return Mdb
+
+
+# ---------------------------------------------------------- sketch cache
+def _load_cached(path: str, s: int) -> Optional[MashReference]:
+    try:
+        m = read_msh(path)
+    except Exception:
+        return None
+    if m.kmer != MASH_K or m.sketch_size != s or m.seed != MASH_SEED or len(m.references) != 1:
+        return None
+    return m.references[0]
+
+
+@dataclass
+class SketchSet:
+    names: List[str]          # genome (basename), Bdb order
+    locations: List[str]
+    hashes: np.ndarray        # uint64 [N, s], rows padded with UINT64_MAX
+    nhash: np.ndarray         # uint32 [N]
+    length: np.ndarray        # uint64 [N]
+    s: int
+
+
+def sketch_genomes(Bdb: pd.DataFrame, data_folder: str, **kwargs) -> SketchSet:
+    """The sketch + paste half of all_vs_all_MASH (d_cluster.py:499-567):
+    same folders and files (MASH_files/sketches/chunk_<i>/<genome>.msh,
+    chunk_all.msh, ALL.msh), sketches cached across runs by file existence
+    (d_cluster.py:541-542), new ones computed on the GPU in one batch."""
+    MASH_s = int(kwargs.get('MASH_sketch', 1000))
+    p = int(kwargs.get('processors', 6))
+    groupSize = int(kwargs.get('groupSize', 1000))
+    device = int(kwargs.get('gpu', os.environ.get('DREPHIP_DEVICE', 0)))
+    write_sketches = kwargs.get('write_sketches', True)
+
+    MASH_folder = os.path.join(data_folder, 'MASH_files/')
+    sketch_folder = os.path.join(MASH_folder, 'sketches/')
+    os.makedirs(sketch_folder, exist_ok=True)
+
+    l2g = Bdb.set_index('location')['genome'].to_dict()
+    locations = list(Bdb['location'].unique())
+    chunks = [locations[x:x + groupSize] for x in range(0, len(locations), groupSize)]
+    N = len(locations)
+    names = [l2g[loc] for loc in locations]
+    hashes = np.full((N, MASH_s), np.iinfo(np.uint64).max, dtype=np.uint64)
+    nhash = np.zeros(N, dtype=np.uint32)
+    length = np.zeros(N, dtype=np.uint64)
+    msh_path: Dict[int, str] = {}
+    todo: List[int] = []
+    idx = 0
+    chunk_members: List[List[int]] = []
+    for i, chunk in enumerate(chunks):
+        chunk_folder = os.path.join(sketch_folder, "chunk_{0}".format(i))
+        os.makedirs(chunk_folder, exist_ok=True)
+        members = []
+        for _ in chunk:
+            f = os.path.join(chunk_folder, names[idx]) + '.msh'
+            msh_path[idx] = f
+            ref = _load_cached(f, MASH_s) if os.path.isfile(f) else None
+            if ref is not None:
+                n = min(len(ref.hashes), MASH_s)
+                hashes[idx, :n] = ref.hashes[:n]
+                nhash[idx] = n
+                length[idx] = ref.length
+            else:
+                todo.append(idx)
+            members.append(idx)
+            idx += 1
+        chunk_members.append(members)
+
+    if todo:
+        with _lib.Context(device=device, k=MASH_K, s=MASH_s, seed=MASH_SEED) as ctx:
+            h, nh, ln = ctx.sketch_files([locations[i] for i in todo], threads=p)
+        hashes[todo] = h
+        nhash[todo] = nh
+        length[todo] = ln
+        logging.debug("sketched %d genomes on HIP device %d", len(todo), device)
+
+    if write_sketches:
+        def ref_of(i):
+            return MashReference(locations[i], '', int(length[i]), hashes[i, :nhash[i]])
+        for i in todo:
+            write_msh(msh_path[i], [ref_of(i)], MASH_K, MASH_s, MASH_SEED)
+        alls = []
+        for ci, members in enumerate(chunk_members):
+            all_file = os.path.join(sketch_folder, "chunk_{0}".format(ci), 'chunk_all.msh')
+            write_msh(all_file, [ref_of(i) for i in members], MASH_K, MASH_s, MASH_SEED)
+            alls.append(all_file)
+        write_msh(os.path.join(MASH_folder, 'ALL.msh'), [ref_of(i) for i in range(N)],
+                  MASH_K, MASH_s, MASH_SEED)
+    return SketchSet(names, locations, hashes, nhash, length, MASH_s)
+
+
+@dataclass
+class CondensedMash:
+    names: List[str]
+    locations: List[str]
+    common: np.ndarray     # uint16, condensed i<j (scipy squareform order)
+    denom: np.ndarray      # uint16, same layout
+    nhash: np.ndarray
+    length: np.ndarray
+    s: int
+
+
+def all_vs_all_MASH_condensed(Bdb, data_folder, **kwargs) -> CondensedMash:
+    """Sketch (or load cached sketches) and run the HIP all-pairs kernel;
+    return the condensed shared-hash counts instead of an N^2-row table."""
+    sk = sketch_genomes(Bdb, data_folder, **kwargs)
+    device = int(kwargs.get('gpu', os.environ.get('DREPHIP_DEVICE', 0)))
+    with _lib.Context(device=device, k=MASH_K, s=sk.s, seed=MASH_SEED) as ctx:
+        common, denom = ctx.allpairs(sk.hashes, sk.nhash)
+    return CondensedMash(sk.names, sk.locations, common, denom, sk.nhash, sk.length, sk.s)
+
+
+def all_vs_all_MASH(Bdb, data_folder, **kwargs):
+    """
+    Run MASH pairwise within all samples in Bdb (reference
+    drep/d_cluster.py:481-596), with sketching and the all-vs-all distance on
+    the GPU.
+
+    Args:
+        Bdb: dataframe with genome, location
+        data_folder: location to store output files
+
+    Keyword Args:
+        MASH_sketch: size of mash sketches (int or str, as the CLI passes it)
+        dry: dont actually run anything (parses an existing MASH_table.tsv, as
+            the reference does after printing its commands)
+        processors: CPU threads for FASTA ingest
+        groupSize: max number of mash sketches to hold in each folder
+        debug / wd: accepted for compatibility (no external commands to log)
+        exe_loc / mash_exe: accepted and ignored (no mash executable is used)
+        gpu: HIP device index (default $DREPHIP_DEVICE or 0)
+        write_sketches: write the .msh files (default True)
+        write_table: also write MASH_table.tsv like `mash dist` (default False)
+
+    Returns:
+        Mdb DataFrame [genome1, genome2, dist, similarity]
+    """
+    MASH_folder = os.path.join(data_folder, 'MASH_files/')
+    if kwargs.get('dry', False):
+        table = MASH_folder + 'MASH_table.tsv'
+        print("# drep_amd: dry run -- would sketch %d genomes and run all-pairs on HIP device %s"
+              % (len(Bdb), kwargs.get('gpu', os.environ.get('DREPHIP_DEVICE', 0))))
+        return _parse_mash_table(table, Bdb)
+
+    cm = all_vs_all_MASH_condensed(Bdb, data_folder, **kwargs)
+    if kwargs.get('write_table', False):
+        write_mash_table(MASH_folder + 'MASH_table.tsv', cm)
+    Mdb = mdb_from_condensed(cm.names, cm.common, cm.denom, cm.nhash, cm.s)
+
+    # Filter out those genomes that are not in Bdb (reference 586-594)
+    genomes = Bdb['genome'].unique()
+    Mdb = Mdb[Mdb['genome1'].isin(genomes)]
+    Mdb = Mdb[Mdb['genome2'].isin(genomes)]
+    for g in ['genome1', 'genome2']:
+        Mdb[g] = Mdb[g].cat.remove_unused_categories()
+        Mdb[g] = Mdb[g].cat.reorder_categories(sorted((Mdb[g].unique())), ordered=True)
+    return Mdb
+
+
+def _parse_mash_table(file, Bdb):
+    """The reference's TSV -> Mdb parse (d_cluster.py:575-596)."""
+    iniCols = ['genome1', 'genome2', 'dist', 'p', 'kmers']
+    uCols = ['genome1', 'genome2', 'dist']
+    dTypes = {'genome1': 'category', 'genome2': 'category', 'dist': np.float32}
+    Mdb = pd.read_csv(file, names=iniCols, usecols=uCols, dtype=dTypes, sep='\t')
+    Mdb['genome1'] = Mdb['genome1'].apply(_get_genome_name_from_fasta)
+    Mdb['genome2'] = Mdb['genome2'].apply(_get_genome_name_from_fasta)
+    Mdb['similarity'] = 1 - Mdb['dist']
+    genomes = Bdb['genome'].unique()
+    Mdb = Mdb[Mdb['genome1'].isin(genomes)]
+    Mdb = Mdb[Mdb['genome2'].isin(genomes)]
+    for g in ['genome1', 'genome2']:
+        Mdb[g] = Mdb[g].astype('category').cat.remove_unused_categories()
+        Mdb[g] = Mdb[g].cat.reorder_categories(sorted((Mdb[g].unique())), ordered=True)
+    return Mdb
+
+
+def mash_pvalue(common: np.ndarray, len_r: np.ndarray, len_q: np.ndarray, s: int,
+                k: int = MASH_K) -> np.ndarray:
+    """Mash's p-value column (binomial upper tail; Mash uses GSL's
+    gsl_cdf_binomial_Q, restated with scipy): 1 if common == 0, else
+    Q(common-1; r, trunc(min(M, s)))."""
+    from scipy.stats import binom
+    kspace = 4.0 ** k
+    px = 1.0 / (1.0 + kspace / np.asarray(len_r, dtype=np.float64))
+    py = 1.0 / (1.0 + kspace / np.asarray(len_q, dtype=np.float64))
+    r = px * py / (px + py - px * py)
+    M = kspace * (px + py) / (1.0 + r)
+    n = np.floor(np.minimum(M, s))
+    c = np.asarray(common, dtype=np.float64)
+    p = binom.sf(c - 1, n, r)
+    return np.where(c == 0, 1.0, p)
+
+
+def write_mash_table(path: str, cm: CondensedMash) -> None:
+    """MASH_table.tsv as `mash dist ALL ALL` prints it (d_cluster.py:570-572):
+    reference, query, %g distance, %g p-value, common/denom; outer loop over
+    queries.  N^2 lines -- only sensible for small N."""
+    N = len(cm.names)
+    nh = np.minimum(cm.nhash.astype(np.int64), cm.s)
+    Cm = _square(cm.common, N, nh.astype(np.uint16)).astype(np.int64)
+    Dm = _square(cm.denom, N, nh.astype(np.uint16)).astype(np.int64)
+    with open(path, 'w') as fh:
+        for q in range(N):
+            lut = {}
+            dist = np.empty(N)
+            for r in range(N):
+                key = (Cm[q, r], Dm[q, r])
+                if key not in lut:
+                    lut[key] = _lib.distance_lut(int(key[1]), MASH_K)[key[0]] if key[1] else 0.0
+                dist[r] = lut[key]
+            p = mash_pvalue(Cm[q], cm.length, np.full(N, cm.length[q]), cm.s)
+            for r in range(N):
+                fh.write("%s\t%s\t%s\t%s\t%d/%d\n" % (cm.locations[r], cm.locations[q], "%g" % dist[r],
+                                                     "%g" % p[r], Cm[q, r], Dm[q, r]))
+
+
+# ------------------------------------------------------ primary clustering
+def cluster_hierarchical(db, linkage_method='single', linkage_cutoff=0.10):
+    """Hierarchical clustering of a square distance DataFrame (reference
+    drep/d_cluster.py:429-461)."""
+    names = list(db.columns)
+    arr = np.asarray(db)
+    try:
+        arr = ssd.squareform(arr)
+    except Exception:
+        logging.error("The database passed in is not symmetrical!")
+        logging.error(arr)
+        logging.error(names)
+        raise
+    linkage = scipy.cluster.hierarchy.linkage(arr, method=linkage_method)
+    fclust = scipy.cluster.hierarchy.fcluster(linkage, linkage_cutoff, criterion='distance')
+    Cdb = _gen_cdb_from_fclust(fclust, names)
+    return Cdb, linkage
+
+
+def _gen_cdb_from_fclust(fclust, names):
+    """fcluster labels -> Cdb [cluster, genome] (reference d_cluster.py:463-479)."""
+    Table = {'cluster': [], 'genome': []}
+    for i, c in enumerate(fclust):
+        Table['cluster'].append(c)
+        Table['genome'].append(names[i])
+    return pd.DataFrame(Table)
+
+
+def cluster_mash_database(db, **kwargs):
+    """
+    From a Mash database, cluster and return Cdb (reference
+    drep/d_cluster.py:598-630).  Same in-place update of db['dist'] from
+    db['similarity'] as the reference; ``pivot`` is called with keywords
+    (pandas >= 2 rejects the reference's positional form).
+
+    Keyword arguments:
+        clusterAlg: how to cluster database (default = single)
+        P_ani: threshold to cluster at (default = 0.9)
+
+    Returns:
+        list: [Cdb, [linkage, linkage_db, arguments]]
+    """
+    logging.debug('Clustering MASH database')
+    P_Lmethod = kwargs.get('clusterAlg', 'single')
+    P_Lcutoff = 1 - kwargs.get('P_ani', .9)
+    db['dist'] = 1 - db['similarity']
+    linkage_db = db.pivot(index="genome1", columns="genome2", values="dist")
+    Cdb, linkage = cluster_hierarchical(linkage_db, linkage_method=P_Lmethod,
+                                        linkage_cutoff=P_Lcutoff)
+    Cdb = Cdb.rename(columns={'cluster': 'primary_cluster'})
+    arguments = {'linkage_method': P_Lmethod, 'linkage_cutoff': P_Lcutoff,
+                 'comparison_algorithm': 'MASH'}
+    return Cdb, [linkage, linkage_db, arguments]
+
+
+def condensed_cluster_distances(cm: CondensedMash) -> np.ndarray:
+    """float64 condensed distances bit-identical to what the reference feeds
+    scipy: dist32 -> 1 - (1 - dist32) in float32 (d_cluster.py:584, 619) ->
+    float64.  Rows/columns in sorted-name order (the pivot's order)."""
+    N = len(cm.names)
+    d32 = mash_distance_float32(cm.common, cm.denom)
+    one = np.float32(1)
+    after = (one - (one - d32)).astype(np.float32)
+    order = np.argsort(np.array(cm.names, dtype=object), kind='stable')
+    if np.all(order == np.arange(N)):
+        return after.astype(np.float64)
+    M = _square(after, N, np.zeros(N, dtype=np.float32))
+    M = M[np.ix_(order, order)]
+    return ssd.squareform(M, checks=False).astype(np.float64)
+
+
+def cluster_mash_condensed(cm: CondensedMash, **kwargs):
+    """Primary clustering straight from the condensed result (no N^2 Mdb):
+    same linkage input as cluster_mash_database builds via pivot+squareform."""
+    P_Lmethod = kwargs.get('clusterAlg', 'single')
+    P_Lcutoff = 1 - kwargs.get('P_ani', .9)
+    arr = condensed_cluster_distances(cm)
+    names = sorted(cm.names)
+    linkage = scipy.cluster.hierarchy.linkage(arr, method=P_Lmethod)
+    fclust = scipy.cluster.hierarchy.fcluster(linkage, P_Lcutoff, criterion='distance')
+    Cdb = _gen_cdb_from_fclust(fclust, names).rename(columns={'cluster': 'primary_cluster'})
+    arguments = {'linkage_method': P_Lmethod, 'linkage_cutoff': P_Lcutoff,
+                 'comparison_algorithm': 'MASH'}
+    return Cdb, [linkage, None, arguments]

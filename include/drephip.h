@@ -1,0 +1,169 @@
+/*
+ * drephip.h -- C ABI of libdrephip.so, the MI355X (gfx950) implementation of
+ * dRep's primary-clustering hot path: Mash sketch + all-vs-all Mash dist.
+ *
+ * The reference does this step by shelling out to the external Mash binary
+ * (drep/d_cluster.py:481-596, all_vs_all_MASH).  Each entry point below names
+ * the reference interface it replaces.  Conventions:
+ *   - every function returns 0 on success and a negative DREPHIP_ERR_* code on
+ *     failure (the reference ignored mash's exit codes, drep/__init__.py:44-48;
+ *     here failures are reported) -- drephip_last_error() gives the message
+ *     (thread-local);
+ *   - host buffers are owned by the caller (numpy arrays via ctypes); device
+ *     memory passed in (d_ prefix) is owned by the caller too; the library owns
+ *     its own device scratch, kept in the context;
+ *   - calls are blocking and a context is single-caller; no C++ exception
+ *     crosses the ABI.
+ *
+ * Sketch definition (bit-exact with `mash sketch -k 21 -s S`, seed 42):
+ *   canonical k-mer (memcmp(fwd, revcomp) <= 0 ? fwd : revcomp) hashed with
+ *   MurmurHash3_x64_128(seed).h1 over its ASCII bytes; k-mers containing a
+ *   non-ACGT byte (after upper-casing) or spanning two records are skipped;
+ *   sketch = the s smallest distinct hashes, ascending, one sketch per file.
+ * hashes_out rows are s wide; entries past nhash are UINT64_MAX.
+ *
+ * Pair output: condensed upper triangle (i < j, row-major; scipy squareform
+ * order): index(i, j) = i*N - i*(i+1)/2 + (j - i - 1).
+ *   common = Mash's shared-hash count (the "c" of "c/denom" in MASH_table.tsv),
+ *   denom  = s when both sketches are full, else min(s, |A u B|).
+ */
+#ifndef DREPHIP_H
+#define DREPHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DREPHIP_OK               0
+#define DREPHIP_ERR_ARG         -1
+#define DREPHIP_ERR_HIP         -2
+#define DREPHIP_ERR_IO          -3
+#define DREPHIP_ERR_NOMEM       -4
+#define DREPHIP_ERR_UNSUPPORTED -5
+#define DREPHIP_ERR_INTERNAL    -6
+
+typedef struct drephip_ctx drephip_ctx;
+
+/* Library/ABI version (major*10000 + minor*100 + patch). */
+int drephip_version(void);
+
+/* Last error message of the calling thread ("" if none). */
+const char *drephip_last_error(void);
+
+/* Number of visible HIP devices. */
+int drephip_device_count(int *n);
+
+/* Create a context on HIP device `device` for k-mer size k (1..32), sketch
+ * size s (1..DREPHIP_MAX_SKETCH) and Murmur seed.
+ * Replaces: the `mash` executable lookup + parameters,
+ *   drep/d_cluster.py:499-515 (MASH_sketch, exe_loc/get_exe), drep/__init__.py:88-101. */
+int drephip_create(int device, int k, uint32_t s, uint32_t seed, drephip_ctx **out);
+int drephip_destroy(drephip_ctx *ctx);
+
+/* Largest supported sketch size. */
+uint32_t drephip_max_sketch(void);
+
+/* ---------------------------------------------------------------- layout
+ * Packed genome set in HBM: 2-bit base codes (A0 C1 G2 T3), 16 bases per
+ * uint32 (base p at bits 2*(p%16)); validity bitmap, 32 bases per uint32 (bit
+ * p%32 of word p/32).  Genome g occupies bases [base_off[g], base_off[g] +
+ * padded[g]); base_off[0] = tile, base_off and padded are multiples of
+ * drephip_tile_bases(); records are separated by one invalid base and every
+ * genome is followed by at least one invalid base; bases [0, tile) are
+ * invalid. */
+uint64_t drephip_tile_bases(void);
+
+/* Padded size (in bases) of a genome whose records have the given lengths. */
+uint64_t drephip_padded_bases(const uint64_t *rec_len, uint32_t n_rec);
+
+/* Parse a FASTA file (plain or gzip; kseq semantics as in Mash) -- what
+ * `mash sketch <fasta>` reads (drep/d_cluster.py:543-544).  Outputs the sum of
+ * record lengths, the padded size, the record count and the number of valid
+ * k-mer positions. */
+int drephip_fasta_info(const char *path, int k, uint64_t *length, uint64_t *padded,
+                       uint32_t *n_records, uint64_t *n_kmers);
+
+/* Pack a FASTA into the layout at base offset `base_off` of caller-owned host
+ * arrays (codes/valid sized for at least base_off+padded bases; the genome's
+ * padded region must be zero on entry). */
+int drephip_fasta_pack(const char *path, int k, uint32_t *codes, uint32_t *valid,
+                       uint64_t base_off, uint64_t cap_bases, uint64_t *length,
+                       uint64_t *n_kmers);
+
+/* ---------------------------------------------------------------- sketch
+ * Replaces: `mash sketch <fa> -s S -o <out>` per genome on a thread pool
+ * (drep/d_cluster.py:531-549, drep/__init__.py:53-59) and `mash paste`
+ * (d_cluster.py:551-567): one call sketches a whole genome set into one
+ * row-major uint64[n_genomes][s] matrix.
+ * Input: concatenated sequence bytes (any case) of every record of every
+ * genome; rec_off[n_rec+1] record boundaries into seq; genome g owns records
+ * [genome_rec_off[g], genome_rec_off[g+1]). */
+int drephip_sketch(drephip_ctx *ctx, const uint8_t *seq, const uint64_t *rec_off, uint32_t n_rec,
+                   const uint64_t *genome_rec_off, uint32_t n_genomes,
+                   uint64_t *hashes_out, uint32_t *nhash_out, uint64_t *length_out);
+
+/* Same, reading FASTA files (host ingest on `threads` CPU threads, 0 = all;
+ * batches are streamed through the device). */
+int drephip_sketch_files(drephip_ctx *ctx, const char *const *paths, uint32_t n_genomes,
+                         int threads, uint64_t *hashes_out, uint32_t *nhash_out,
+                         uint64_t *length_out);
+
+/* Device-resident sketch: packed genome set already in HBM (see layout).
+ * h_base_off/h_padded/h_nkmers are host arrays of n_genomes entries
+ * (h_nkmers: valid k-mer positions, used only to seed the candidate
+ * threshold).  d_hashes: uint64[n_genomes][s]; d_nhash: uint32[n_genomes].
+ * stream: a hipStream_t (NULL = the context's stream).  Blocking. */
+int drephip_sketch_device(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t *d_valid,
+                          const uint64_t *h_base_off, const uint64_t *h_padded,
+                          const uint64_t *h_nkmers, uint32_t n_genomes,
+                          uint64_t *d_hashes, uint32_t *d_nhash, void *stream);
+
+/* Bench/test input: write synthetic genomes g0..g0+n-1 (each length L, one
+ * record; family = g / family_size) into the packed layout with
+ * genome i at base_off = tile + i*drephip_padded_bases(&L, 1).
+ * d_codes/d_valid must hold tile + n*padded bases. */
+int drephip_synth_device(drephip_ctx *ctx, uint64_t seed, uint32_t g0, uint32_t n,
+                         uint32_t family_size, uint64_t L, uint32_t *d_codes, uint32_t *d_valid,
+                         void *stream);
+
+/* ---------------------------------------------------------------- dist
+ * Replaces: `mash dist -p P ALL.msh ALL.msh > MASH_table.tsv`
+ * (drep/d_cluster.py:569-573) for the integer part of every row: the shared-
+ * hash count and its denominator.  Distances are a pure function of
+ * (common, denom) and are formed on the host (drephip_distance_lut). */
+int drephip_allpairs(drephip_ctx *ctx, const uint64_t *hashes, const uint32_t *nhash, uint32_t N,
+                     uint16_t *common_out, uint16_t *denom_out /* nullable */);
+
+/* Device-resident all-pairs over rows [row0, row1) of the upper triangle
+ * (columns row+1..N-1).  d_common/d_denom receive the condensed segment that
+ * starts at index(row0, row0+1).  d_denom may be NULL. Blocking. */
+int drephip_allpairs_device(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash,
+                            uint32_t N, uint32_t row0, uint32_t row1, uint16_t *d_common,
+                            uint16_t *d_denom, void *stream);
+
+/* Reference all-pairs kernel (one lane per pair, literal Mash merge loop).
+ * Same contract as drephip_allpairs_device; slower; used for cross-checks. */
+int drephip_allpairs_merge_device(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash,
+                                  uint32_t N, uint32_t row0, uint32_t row1, uint16_t *d_common,
+                                  uint16_t *d_denom, void *stream);
+
+/* Mash distance for common = 0..denom at the given denominator (host, libm):
+ * J = c/denom; d = c==denom ? 0 : c==0 ? 1 : min(1, -ln(2J/(1+J))/k).
+ * Reference: the "dist" column of MASH_table.tsv parsed at d_cluster.py:581. */
+int drephip_distance_lut(int k, uint32_t denom, double *lut /* denom+1 */);
+
+/* Enable (1) / disable (0) HIP-event timing of every kernel launch. */
+int drephip_set_timing(drephip_ctx *ctx, int enable);
+
+/* Per-launch timing of the last sketch/allpairs call on this context
+ * (milliseconds, from HIP events on the launch stream): which = 0 sketch hash
+ * kernel, 1 sketch finalize kernel, 2 allpairs kernel, 3 table build kernel.
+ * Returns the count of launches summed into *ms. */
+int drephip_last_kernel_ms(drephip_ctx *ctx, int which, double *ms, int *launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DREPHIP_H */

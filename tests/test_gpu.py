@@ -1,0 +1,289 @@
+"""Parity of the HIP path (libdrephip.so via its C ABI) with the oracle and the
+reference fixtures.  Integer outputs are compared bit-exactly."""
+import glob
+import os
+import shutil
+
+import numpy as np
+import pandas as pd
+import pytest
+
+import oracle
+from drep_amd import _lib
+from drep_amd.mash_io import read_msh
+
+pytestmark = pytest.mark.gpu
+S = 1000
+UMAX = np.iinfo(np.uint64).max
+
+
+def _pad(h, s):
+    out = np.full(s, UMAX, dtype=np.uint64)
+    out[:len(h)] = h
+    return out
+
+
+# ------------------------------------------------------------------ sketch
+def test_sketch_reference_genomes_bitexact(golden, ctx1000):
+    fas = sorted(glob.glob(os.path.join(golden, "genomes", "*.gz")))
+    h, nh, ln = ctx1000.sketch_files(fas, threads=4)
+    for i, fa in enumerate(fas):
+        ref = read_msh(os.path.join(golden, "MASH_files", "sketches",
+                                    os.path.basename(fa)[:-3] + ".msh")).references[0]
+        assert nh[i] == len(ref.hashes) == S
+        assert np.array_equal(h[i], ref.hashes)
+        assert int(ln[i]) == ref.length
+
+
+def _records_case(rng, kind):
+    A = np.frombuffer(b"ACGT", dtype=np.uint8)
+    if kind == "nruns_lower_multirecord":
+        recs = []
+        for L in rng.integers(1, 60000, 9):
+            b = A[rng.integers(0, 4, int(L))].copy()
+            b[rng.random(int(L)) < 0.002] = ord("N")
+            low = rng.random(int(L)) < 0.3
+            b[low] += 32
+            recs.append(b)
+        recs += [A[rng.integers(0, 4, 20)], A[rng.integers(0, 4, 21)], np.zeros(0, np.uint8)]
+        return recs
+    if kind == "iupac_and_junk":
+        b = A[rng.integers(0, 4, 50000)].copy()
+        junk = np.frombuffer(b"RYKMSWBDHVN-*xU u", dtype=np.uint8)
+        pos = rng.integers(0, 50000, 300)
+        b[pos] = junk[rng.integers(0, len(junk), 300)]
+        return [b]
+    if kind == "tiny":               # fewer than s distinct k-mers: partial sketch
+        return [A[rng.integers(0, 4, 400)]]
+    if kind == "empty":
+        return [np.zeros(0, np.uint8)]
+    if kind == "all_n":
+        return [np.full(5000, ord("N"), np.uint8)]
+    if kind == "repeats_up":         # heavy repeats: threshold must be raised
+        unit = A[rng.integers(0, 4, 3000)]
+        return [np.tile(unit, 300)]
+    if kind == "repeats_bisect":     # first raise overshoots the LDS sort -> bisection
+        unit = A[rng.integers(0, 4, 300_000)]
+        return [np.concatenate([unit, unit, unit, unit[:100_000]])]
+    if kind == "tandem":
+        return [np.tile(np.frombuffer(b"AT", np.uint8), 40000), A[rng.integers(0, 4, 100000)]]
+    raise KeyError(kind)
+
+
+CASES = ["nruns_lower_multirecord", "iupac_and_junk", "tiny", "empty", "all_n", "repeats_up",
+         "repeats_bisect", "tandem"]
+
+
+def test_sketch_edge_cases_vs_oracle(ctx1000):
+    rng = np.random.default_rng(11)
+    genomes = [_records_case(rng, k) for k in CASES]
+    recs = [r for g in genomes for r in g]
+    seq = np.concatenate(recs).astype(np.uint8) if recs else np.zeros(0, np.uint8)
+    rec_off = np.concatenate([[0], np.cumsum([len(r) for r in recs])]).astype(np.uint64)
+    gro = np.concatenate([[0], np.cumsum([len(g) for g in genomes])]).astype(np.uint64)
+    h, nh, ln = ctx1000.sketch_records(seq, rec_off, gro)
+    upper = np.where((seq >= 97) & (seq <= 122), seq - 32, seq).astype(np.uint8)
+    for gi, kind in enumerate(CASES):
+        r0, r1 = int(gro[gi]), int(gro[gi + 1])
+        sub = upper[int(rec_off[r0]):int(rec_off[r1])]
+        off = (rec_off[r0:r1 + 1] - rec_off[r0]).astype(np.uint64)
+        want = oracle.sketch_records(sub, off, 21, S, 42)
+        assert nh[gi] == len(want), kind
+        assert np.array_equal(h[gi, :nh[gi]], want), kind
+        assert (h[gi, nh[gi]:] == UMAX).all(), kind
+        assert int(ln[gi]) == int(off[-1]), kind
+
+
+@pytest.mark.parametrize("s", [1, 64, 4096, 12000])
+def test_sketch_sizes_vs_oracle(s):
+    rng = np.random.default_rng(s)
+    A = np.frombuffer(b"ACGT", dtype=np.uint8)
+    recs = [A[rng.integers(0, 4, 250_000)], A[rng.integers(0, 4, 3000)], A[rng.integers(0, 4, 900_000)]]
+    seq = np.concatenate(recs)
+    rec_off = np.concatenate([[0], np.cumsum([len(r) for r in recs])]).astype(np.uint64)
+    gro = np.arange(len(recs) + 1, dtype=np.uint64)
+    with _lib.Context(0, 21, s, 42) as ctx:
+        h, nh, _ = ctx.sketch_records(seq, rec_off, gro)
+    for g in range(len(recs)):
+        want = oracle.sketch_records(recs[g], np.array([0, len(recs[g])], np.uint64), 21, s, 42)
+        assert np.array_equal(h[g, :nh[g]], want)
+
+
+def test_synth_device_matches_oracle_generator(ctx1000):
+    """The bench's on-device generator + device sketch == oracle generator +
+    oracle sketch (5 Mbp genomes, the BASELINE genome size)."""
+    import torch
+    n, L, fam, seed = 6, 5_000_000, 3, 9
+    tile = _lib.tile_bases()
+    P = _lib.padded_bases([L])
+    total = tile + n * P
+    codes = torch.zeros(total // 16, dtype=torch.int32, device="cuda")
+    valid = torch.zeros(total // 32, dtype=torch.int32, device="cuda")
+    ctx1000.synth_device(seed, 0, n, fam, L, codes.data_ptr(), valid.data_ptr())
+    hashes = torch.zeros((n, S), dtype=torch.int64, device="cuda")
+    nhash = torch.zeros(n, dtype=torch.int32, device="cuda")
+    off = np.array([tile + i * P for i in range(n)], np.uint64)
+    ctx1000.sketch_device(codes.data_ptr(), valid.data_ptr(), off, np.full(n, P, np.uint64),
+                          np.full(n, L - 20, np.uint64), n, hashes.data_ptr(), nhash.data_ptr())
+    torch.cuda.synchronize()
+    h = hashes.cpu().numpy().view(np.uint64)
+    nh = nhash.cpu().numpy().view(np.uint32)
+    oh, onh = oracle.sketch_synth(0, n, L, seed=seed, family_size=fam, threads=6)
+    assert np.array_equal(nh, onh)
+    assert np.array_equal(h, oh)
+    # the packed bases themselves
+    asc = oracle.synth_ascii(4, L, seed=seed, family_size=fam)
+    code = np.frombuffer(bytes(256), np.uint8).copy()
+    code[[65, 67, 71, 84]] = [0, 1, 2, 3]
+    c = code[asc]
+    words = codes[(tile + 4 * P) // 16:(tile + 4 * P) // 16 + L // 16].cpu().numpy().view(np.uint32)
+    unpacked = ((words[:, None] >> (2 * np.arange(16, dtype=np.uint32))) & 3).reshape(-1)
+    assert np.array_equal(unpacked, c[:len(unpacked)])
+
+
+# --------------------------------------------------------------- all-pairs
+def _ref_sketches(golden):
+    refs = read_msh(os.path.join(golden, "MASH_files", "ALL.msh")).references
+    H = np.stack([_pad(r.hashes, S) for r in refs])
+    NH = np.array([len(r.hashes) for r in refs], np.uint32)
+    return refs, H, NH
+
+
+def test_allpairs_reference_table(golden, ctx1000):
+    """Shared-hash counts of the 5 reference genomes == MASH_table.tsv."""
+    refs, H, NH = _ref_sketches(golden)
+    c, d = ctx1000.allpairs(H, NH)
+    rows = [l.split("\t") for l in open(os.path.join(golden, "MASH_files", "MASH_table.tsv"))]
+    names = [r.name for r in refs]
+    N = len(refs)
+    for row in rows:
+        i, j = names.index(row[0]), names.index(row[1])
+        if i == j:
+            continue
+        a, b = min(i, j), max(i, j)
+        k = a * N - a * (a + 1) // 2 + (b - a - 1)
+        cc, dd = row[4].strip().split("/")
+        assert (int(c[k]), int(d[k])) == (int(cc), int(dd))
+
+
+def _family_sketches(n, L, fam, seed):
+    return oracle.sketch_synth(0, n, L, seed=seed, family_size=fam, threads=8)
+
+
+@pytest.fixture(scope="module")
+def family():
+    return _family_sketches(160, 400_000, 20, 5)
+
+
+def test_allpairs_family_vs_oracle(family, ctx1000):
+    h, nh = family
+    c, d = ctx1000.allpairs(h, nh)
+    oc, od = oracle.allpairs(h, nh, S, threads=8)
+    assert np.array_equal(c, oc) and np.array_equal(d, od)
+    assert c.max() > 500          # similar pairs are exercised
+
+
+def test_allpairs_partial_sketches_vs_oracle(ctx1000):
+    rng = np.random.default_rng(3)
+    A = np.frombuffer(b"ACGT", dtype=np.uint8)
+    base = A[rng.integers(0, 4, 600_000)]
+    recs = []
+    for i in range(40):
+        L = int(rng.choice([60, 300, 700, 1200, 5000, 600_000]))
+        x = base[:L].copy()
+        m = rng.random(L) < rng.choice([0.0, 0.01, 0.05])
+        x[m] = A[rng.integers(0, 4, int(m.sum()))]
+        recs.append(x)
+    seq = np.concatenate(recs)
+    rec_off = np.concatenate([[0], np.cumsum([len(r) for r in recs])]).astype(np.uint64)
+    gro = np.arange(len(recs) + 1, dtype=np.uint64)
+    h, nh, _ = ctx1000.sketch_records(seq, rec_off, gro)
+    assert (nh < S).any() and (nh == S).any()
+    c, d = ctx1000.allpairs(h, nh)
+    oc, od = oracle.allpairs(h, nh, S)
+    assert np.array_equal(c, oc) and np.array_equal(d, od)
+
+
+@pytest.mark.parametrize("s", [1, 16, 100, 513, 4096, 5000])
+def test_allpairs_sketch_sizes(s):
+    h, nh = oracle.sketch_synth(0, 48, 120_000, seed=s, family_size=12, s=s, threads=8)
+    with _lib.Context(0, 21, s, 42) as ctx:
+        c, d = ctx.allpairs(h, nh)
+    oc, od = oracle.allpairs(h, nh, s, threads=8)
+    assert np.array_equal(c, oc) and np.array_equal(d, od)
+
+
+def test_allpairs_row_segments_and_merge_kernel(family, ctx1000):
+    """Row-range sharding (the multi-GPU split) and the literal-merge kernel
+    agree with the full triangle."""
+    import torch
+    h, nh = family
+    N = len(nh)
+    dh = torch.from_numpy(h.view(np.int64)).cuda()
+    dn = torch.from_numpy(nh.view(np.int32)).cuda()
+    full = np.zeros(N * (N - 1) // 2, np.uint16)
+    oc, _ = oracle.allpairs(h, nh, S, threads=8)
+
+    def start(i):
+        return i * N - i * (i + 1) // 2
+
+    bounds = [0, 1, 17, 64, 100, N - 2, N]
+    for r0, r1 in zip(bounds[:-1], bounds[1:]):
+        n = start(min(r1, N - 1)) - start(r0) if r0 < N - 1 else 0
+        if n <= 0:
+            continue
+        out = torch.zeros(n, dtype=torch.int16, device="cuda")
+        ctx1000.allpairs_device(dh.data_ptr(), dn.data_ptr(), N, r0, r1, out.data_ptr())
+        full[start(r0):start(r0) + n] = out.cpu().numpy().view(np.uint16)
+    assert np.array_equal(full, oc)
+    out = torch.zeros(N * (N - 1) // 2, dtype=torch.int16, device="cuda")
+    ctx1000.allpairs_device(dh.data_ptr(), dn.data_ptr(), N, 0, N, out.data_ptr(), merge=True)
+    assert np.array_equal(out.cpu().numpy().view(np.uint16), oc)
+
+
+# ---------------------------------------------------------------- drop-in
+def test_all_vs_all_MASH_dropin_reproduces_reference(golden, tmp_path):
+    """all_vs_all_MASH on the reference's test genomes (Sakai from its cached
+    .msh, as the reference's own sketch cache would) -> Mdb bit-identical to
+    the reference's parse of its fixture MASH_table.tsv, then primary
+    clustering identical to the reference's Cdb / linkage."""
+    import json
+    from drep_amd import d_cluster
+    fas = sorted(glob.glob(os.path.join(golden, "genomes", "*.gz")))
+    gdir = tmp_path / "genomes"
+    gdir.mkdir()
+    locs = []
+    for fa in fas:
+        dst = gdir / os.path.basename(fa)[:-3]
+        import gzip
+        dst.write_bytes(gzip.open(fa).read())
+        locs.append(str(dst))
+    sakai = str(gdir / "Escherichia_coli_Sakai.fna")
+    locs.append(sakai)
+    Bdb = pd.DataFrame({"genome": [os.path.basename(x) for x in locs], "location": locs})
+    wd = tmp_path / "wd"
+    chunk = wd / "MASH_files" / "sketches" / "chunk_0"
+    chunk.mkdir(parents=True)
+    shutil.copy(os.path.join(golden, "MASH_files", "sketches", "Escherichia_coli_Sakai.fna.msh"),
+                chunk / "Escherichia_coli_Sakai.fna.msh")
+    Mdb = d_cluster.all_vs_all_MASH(Bdb, str(wd), processors=4)
+    meta = json.load(open(os.path.join(golden, "ref", "mdb_parsed_dtypes.json")))
+    exp = pd.read_csv(os.path.join(golden, "ref", "mdb_parsed.csv"))
+    assert len(Mdb) == 25
+    assert {c: str(t) for c, t in Mdb.dtypes.items()} == meta["dtypes"]
+    for g in ("genome1", "genome2"):
+        assert list(Mdb[g].cat.categories) == meta["categories"][g]
+        assert Mdb[g].cat.ordered
+        assert list(Mdb[g].astype(str)) == list(exp[g])
+    assert list(Mdb["dist"].to_numpy().view(np.uint32)) == meta["dist_bits"]
+    assert list(Mdb["similarity"].to_numpy().view(np.uint32)) == meta["similarity_bits"]
+    # reference layout: one chunk dir with 5 .msh + chunk_all.msh
+    assert len(glob.glob(str(wd / "MASH_files" / "sketches" / "*"))) == 1
+    assert len(glob.glob(str(wd / "MASH_files" / "sketches" / "*" / "*"))) == 6
+    for alg in ("average", "single"):
+        Cdb, ret = d_cluster.cluster_mash_database(Mdb.copy(), clusterAlg=alg, P_ani=0.9)
+        exp_c = pd.read_csv(os.path.join(golden, "ref", "cdb_%s.csv" % alg))
+        assert Cdb.to_dict("list") == exp_c.to_dict("list")
+        link = json.load(open(os.path.join(golden, "ref", "linkage_%s.json" % alg)))
+        got = [[float(v).hex() for v in row] for row in ret[0]]
+        assert got == link["linkage"]

@@ -1,0 +1,191 @@
+"""CPU-only tests: the C ABI library loads and exports every declared symbol,
+host-side layout/ingest helpers, .msh I/O, and the Mdb / primary-clustering
+host logic against the reference-derived golden vectors (shared-hash counts
+from the oracle; no GPU needed)."""
+import json
+import os
+import re
+
+import numpy as np
+import pandas as pd
+import pytest
+
+import oracle
+from drep_amd import _lib
+from drep_amd import d_cluster
+from drep_amd.mash_io import MashReference, read_msh, write_msh
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+S = 1000
+
+
+def test_library_exports_every_header_symbol():
+    hdr = open(os.path.join(ROOT, "include", "drephip.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    declared = set(re.findall(r"\b(drephip_[a-z0-9_]+)\s*\(", hdr))
+    assert declared == set(_lib.SIGNATURES), declared ^ set(_lib.SIGNATURES)
+    L = _lib.lib()
+    for name in declared:
+        assert getattr(L, name) is not None
+    assert L.drephip_version() >= 100
+
+
+def test_no_cpu_fallback(monkeypatch):
+    """The product path fails loudly when the HIP library is missing."""
+    import importlib
+    monkeypatch.setenv("DREPHIP_LIB", "/nonexistent/libdrephip.so")
+    mod = importlib.reload(_lib)
+    try:
+        with pytest.raises(mod.DrepHipError):
+            mod.Context(0, 21, S, 42)
+    finally:
+        monkeypatch.delenv("DREPHIP_LIB")
+        importlib.reload(_lib)
+
+
+def test_layout_helpers():
+    tile = _lib.tile_bases()
+    assert tile == 32768
+    assert _lib.padded_bases([tile - 1]) == tile
+    assert _lib.padded_bases([tile]) == 2 * tile          # >= 1 invalid base after
+    assert _lib.padded_bases([10, 20]) == tile
+    assert _lib.padded_bases([]) == tile
+
+
+def test_distance_lut_matches_oracle():
+    lut = _lib.distance_lut(S)
+    for c in (0, 1, 3, 500, 561, 905, 999, 1000):
+        assert lut[c] == oracle.mash_distance(c, S)
+
+
+def test_fasta_info_matches_oracle_reader(golden):
+    import glob
+    for fa in sorted(glob.glob(os.path.join(golden, "genomes", "*.gz"))):
+        info = _lib.fasta_info(fa)
+        seq, off, ln = oracle.read_fasta(fa)
+        assert info["length"] == ln
+        assert info["n_records"] == len(off) - 1
+        reclen = np.diff(off)
+        assert info["padded"] == _lib.padded_bases(reclen)
+
+
+def test_fasta_parser_edge_cases(tmp_path):
+    """kseq semantics: text before the first header ignored, CRLF, blank
+    lines, lowercase, empty records, gzip."""
+    import gzip
+    txt = b"junk line\n>r1 desc\r\nACGTac\r\n\r\ngtNN\n>r2\n>r3\nTTTT\n"
+    p = tmp_path / "x.fa"
+    p.write_bytes(txt)
+    pg = tmp_path / "x.fa.gz"
+    pg.write_bytes(gzip.compress(txt))
+    for path in (p, pg):
+        info = _lib.fasta_info(str(path))
+        seq, off, ln = oracle.read_fasta(str(path))
+        assert bytes(seq) == b"ACGTACGTNNTTTT"
+        assert list(off) == [0, 10, 10, 14]
+        assert info["length"] == 14 and info["n_records"] == 3
+
+
+def test_msh_roundtrip_and_fixture(golden, tmp_path):
+    m = read_msh(os.path.join(golden, "MASH_files", "ALL.msh"))
+    assert (m.kmer, m.sketch_size, m.seed) == (21, S, 42)
+    assert len(m.references) == 5
+    out = tmp_path / "copy.msh"
+    write_msh(str(out), m.references, 21, S, 42)
+    m2 = read_msh(str(out))
+    assert len(m2.references) == 5
+    for a, b in zip(m.references, m2.references):
+        assert (a.name, a.comment, a.length) == (b.name, b.comment, b.length)
+        assert np.array_equal(a.hashes, b.hashes)
+    one = tmp_path / "one.msh"
+    write_msh(str(one), [MashReference("x", "", 7, np.array([], np.uint64))], 21, 3, 7)
+    r = read_msh(str(one))
+    assert (r.kmer, r.sketch_size, r.seed, len(r.references[0].hashes)) == (21, 3, 7, 0)
+
+
+def _fixture_condensed(golden):
+    refs = read_msh(os.path.join(golden, "MASH_files", "ALL.msh")).references
+    H = np.stack([r.hashes for r in refs])
+    NH = np.full(len(refs), S, np.uint32)
+    c, d = oracle.allpairs(H, NH, S)
+    names = [os.path.basename(r.name) for r in refs]
+    return d_cluster.CondensedMash(names, [r.name for r in refs], c, d, NH,
+                                   np.array([r.length for r in refs], np.uint64), S)
+
+
+def test_mdb_from_condensed_matches_reference_parse(golden):
+    cm = _fixture_condensed(golden)
+    Mdb = d_cluster.mdb_from_condensed(cm.names, cm.common, cm.denom, cm.nhash, cm.s)
+    meta = json.load(open(os.path.join(golden, "ref", "mdb_parsed_dtypes.json")))
+    exp = pd.read_csv(os.path.join(golden, "ref", "mdb_parsed.csv"))
+    assert {c: str(t) for c, t in Mdb.dtypes.items()} == meta["dtypes"]
+    for g in ("genome1", "genome2"):
+        assert list(Mdb[g].cat.categories) == meta["categories"][g]
+        assert list(Mdb[g].astype(str)) == list(exp[g])
+    assert list(Mdb["dist"].to_numpy().view(np.uint32)) == meta["dist_bits"]
+    assert list(Mdb["similarity"].to_numpy().view(np.uint32)) == meta["similarity_bits"]
+
+
+@pytest.mark.parametrize("alg", ["average", "single"])
+def test_cluster_mash_database_matches_reference(golden, alg):
+    cm = _fixture_condensed(golden)
+    Mdb = d_cluster.mdb_from_condensed(cm.names, cm.common, cm.denom, cm.nhash, cm.s)
+    Cdb, ret = d_cluster.cluster_mash_database(Mdb, clusterAlg=alg, P_ani=0.9)
+    exp = pd.read_csv(os.path.join(golden, "ref", "cdb_%s.csv" % alg))
+    assert Cdb.to_dict("list") == exp.to_dict("list")
+    link = json.load(open(os.path.join(golden, "ref", "linkage_%s.json" % alg)))
+    assert [[float(v).hex() for v in row] for row in ret[0]] == link["linkage"]
+    assert ret[2] == link["arguments"]
+    # in-place update of Mdb['dist'] exactly as the reference leaves it
+    assert list(Mdb["dist"].to_numpy().view(np.uint32)) == link["dist_bits_after"]
+    # the condensed path (no N^2 table) gives the same linkage and clusters
+    Cdb2, ret2 = d_cluster.cluster_mash_condensed(cm, clusterAlg=alg, P_ani=0.9)
+    assert Cdb2.to_dict("list") == exp.to_dict("list")
+    assert np.array_equal(ret2[0], ret[0])
+
+
+def test_condensed_clustering_equals_pivot_path_unsorted_names():
+    """Random synthetic family, names deliberately not in sorted order."""
+    n = 30
+    h, nh = oracle.sketch_synth(0, n, 150_000, seed=21, family_size=8, threads=4)
+    c, d = oracle.allpairs(h, nh, S)
+    names = ["g%03d.fa" % ((i * 7) % n) for i in range(n)]
+    cm = d_cluster.CondensedMash(names, names, c, d, nh, np.full(n, 150_000, np.uint64), S)
+    Mdb = d_cluster.mdb_from_condensed(names, c, d, nh, S)
+    for alg in ("average", "single", "complete"):
+        Cdb, ret = d_cluster.cluster_mash_database(Mdb.copy(), clusterAlg=alg, P_ani=0.95)
+        Cdb2, ret2 = d_cluster.cluster_mash_condensed(cm, clusterAlg=alg, P_ani=0.95)
+        assert np.array_equal(ret[0], ret2[0])
+        assert Cdb.to_dict("list") == Cdb2.to_dict("list")
+
+
+def test_write_mash_table_matches_fixture(golden, tmp_path):
+    cm = _fixture_condensed(golden)
+    out = tmp_path / "MASH_table.tsv"
+    d_cluster.write_mash_table(str(out), cm)
+    assert out.read_text() == open(os.path.join(golden, "MASH_files", "MASH_table.tsv")).read()
+
+
+def test_dry_run_parses_existing_table(golden, tmp_path):
+    import shutil
+    os.makedirs(tmp_path / "MASH_files")
+    shutil.copy(os.path.join(golden, "MASH_files", "MASH_table.tsv"), tmp_path / "MASH_files")
+    names = sorted(os.path.basename(r.name) for r in
+                   read_msh(os.path.join(golden, "MASH_files", "ALL.msh")).references)
+    Bdb = pd.DataFrame({"genome": names, "location": ["/x/" + n for n in names]})
+    Mdb = d_cluster.all_vs_all_MASH(Bdb, str(tmp_path), dry=True)
+    meta = json.load(open(os.path.join(golden, "ref", "mdb_parsed_dtypes.json")))
+    assert list(Mdb["dist"].to_numpy().view(np.uint32)) == meta["dist_bits"]
+
+
+def test_load_genomes(tmp_path):
+    a = tmp_path / "a.fa"
+    b = tmp_path / "b.fna"
+    a.write_text(">x\nACGT\n")
+    b.write_text(">y\nACGT\n")
+    Bdb = d_cluster.load_genomes([str(a), str(b)])
+    assert list(Bdb["genome"]) == ["a.fa", "b.fna"]
+    lst = tmp_path / "list.txt"
+    lst.write_text("%s\n%s\n" % (a, b))
+    Bdb2 = d_cluster.load_genomes([str(lst)])
+    assert list(Bdb2["location"]) == [str(a), str(b)]
