@@ -1,0 +1,283 @@
+#!/usr/bin/env python3
+"""Benchmark of the dRep primary-clustering hot path on MI355X.
+
+One *step* = one pass of the hot path over the synthetic genome set, inputs
+already resident in HBM (2-bit packed, generated on device):
+  1. sketch every genome of this rank's shard  (replaces `mash sketch`, d_cluster.py:543)
+  2. RCCL all-gather of the sketch shards       (replaces `mash paste`,  d_cluster.py:551-567)
+  3. all-pairs shared-hash counts for this rank's balanced row range of the
+     upper triangle                             (replaces `mash dist`,   d_cluster.py:570-573)
+value = N(N-1)/2 genome pairs / step time, whole job (all ranks; max over ranks).
+
+Default workload = BASELINE.json configs[1]: 1,000 synthetic 5 Mbp genomes,
+k=21, s=1000.  The same total workload is used at every GPU count (strong
+scaling).  Launch: `python bench.py` (1 GPU) or
+`python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--genomes", type=int, default=1000)
+    ap.add_argument("--genome-bp", type=int, default=5_000_000)
+    ap.add_argument("--sketch", type=int, default=1000)
+    ap.add_argument("--family-size", type=int, default=100)
+    ap.add_argument("--seed", type=int, default=0xD2E9)
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the C oracle on host cores (rank 0)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_sketch_traffic.json"))
+    return ap.parse_args()
+
+
+def row_partition(N, world):
+    """Balanced contiguous row ranges of the upper triangle (pairs per row = N-1-i)."""
+    pairs = np.arange(N - 1, -1, -1, dtype=np.float64)
+    cum = np.concatenate([[0.0], np.cumsum(pairs)])
+    total = cum[-1]
+    bounds = [0]
+    for r in range(1, world):
+        bounds.append(int(np.searchsorted(cum, total * r / world)))
+    bounds.append(N)
+    return [(bounds[r], bounds[r + 1]) for r in range(world)]
+
+
+def cond_start(i, N):
+    return i * N - i * (i + 1) // 2
+
+
+def cpu_baseline(args, threads):
+    """Bounded sample of the same whole job on the host with the C oracle
+    (Mash-equivalent restatement, OpenMP): sketch 2*threads genomes, dist
+    2e6 pairs; extrapolate to the full N-genome job."""
+    import oracle
+    N, L, s = args.genomes, args.genome_bp, args.sketch
+    ns = max(2, 2 * threads)
+    t0 = time.perf_counter()
+    h, nh = oracle.sketch_synth(0, ns, L, seed=args.seed, family_size=args.family_size, s=s, threads=threads)
+    t_sk = time.perf_counter() - t0
+    rng = np.random.default_rng(1)
+    npairs = 2_000_000
+    pi = rng.integers(0, ns, npairs).astype(np.uint32)
+    pj = ((pi + 1 + rng.integers(0, ns - 1, npairs)) % ns).astype(np.uint32)
+    t0 = time.perf_counter()
+    oracle.dist_pairs_list(h, nh, s, pi, pj, threads=threads)
+    t_d = time.perf_counter() - t0
+    per_genome = t_sk / ns
+    per_pair = t_d / npairs
+    job = N * per_genome + (N * (N - 1) / 2) * per_pair
+    return {
+        "value": (N * (N - 1) / 2) / job,
+        "unit": "genome pairs/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": ("C oracle (Mash-equivalent restatement, OpenMP %d threads): sketch of %d synthetic "
+                   "%d bp genomes in %.2f s + %d random pairs of mash dist in %.2f s, extrapolated to "
+                   "the %d-genome job (%.1f s sketch + %.1f s dist)"
+                   % (threads, ns, L, t_sk, npairs, t_d, N, N * per_genome, N * (N - 1) / 2 * per_pair)),
+        "sketch_Mbp_per_s": ns * L / t_sk / 1e6,
+        "dist_pairs_per_s": npairs / t_d,
+    }
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from drep_amd import _lib
+
+    N, L, s = args.genomes, args.genome_bp, args.sketch
+    ctx = _lib.Context(device=local, k=21, s=s, seed=42)
+    ctx.set_timing(True)
+    dev = torch.device("cuda", local)
+
+    # ---- this rank's genome shard, generated on device (untimed)
+    nmax = (N + world - 1) // world
+    g0 = min(N, rank * nmax)
+    g1 = min(N, g0 + nmax)
+    nloc = g1 - g0
+    tile = _lib.tile_bases()
+    P = _lib.padded_bases([L])
+    total_bases = tile + max(nloc, 1) * P
+    codes = torch.zeros(total_bases // 16, dtype=torch.int32, device=dev)
+    valid = torch.zeros(total_bases // 32, dtype=torch.int32, device=dev)
+    if nloc:
+        ctx.synth_device(args.seed, g0, nloc, args.family_size, L, codes.data_ptr(), valid.data_ptr())
+    base_off = np.array([tile + i * P for i in range(nloc)], np.uint64)
+    padded = np.full(nloc, P, np.uint64)
+    nkmers = np.full(nloc, L - 20, np.uint64)
+    loc_h = torch.full((nmax, s), -1, dtype=torch.int64, device=dev)
+    loc_n = torch.zeros(nmax, dtype=torch.int32, device=dev)
+    all_h = torch.empty((world * nmax, s), dtype=torch.int64, device=dev)
+    all_n = torch.empty(world * nmax, dtype=torch.int32, device=dev)
+    r0, r1 = row_partition(N, world)[rank]
+    seg = cond_start(min(r1, N - 1), N) - cond_start(min(r0, N - 1), N) if r0 < N - 1 else 0
+    d_common = torch.zeros(max(seg, 1), dtype=torch.int16, device=dev)
+
+    stage = {"sketch": 0.0, "gather": 0.0, "dist": 0.0}
+    kms = {0: [0.0, 0], 1: [0.0, 0], 2: [0.0, 0], 3: [0.0, 0]}
+
+    def step(record):
+        t0 = time.perf_counter()
+        if nloc:
+            ctx.sketch_device(codes.data_ptr(), valid.data_ptr(), base_off, padded, nkmers, nloc,
+                              loc_h.data_ptr(), loc_n.data_ptr())
+            if record:
+                for w in (0, 1):
+                    ms, n = ctx.kernel_ms(w)
+                    kms[w][0] += ms
+                    kms[w][1] += n
+        t1 = time.perf_counter()
+        if world > 1:
+            dist.all_gather_into_tensor(all_h, loc_h)
+            dist.all_gather_into_tensor(all_n, loc_n)
+            torch.cuda.synchronize()
+            hh, nn = all_h, all_n
+        else:
+            hh, nn = loc_h, loc_n
+        t2 = time.perf_counter()
+        if seg:
+            ctx.allpairs_device(hh.data_ptr(), nn.data_ptr(), N, r0, r1, d_common.data_ptr())
+            if record:
+                for w in (2, 3):
+                    ms, n = ctx.kernel_ms(w)
+                    kms[w][0] += ms
+                    kms[w][1] += n
+        t3 = time.perf_counter()
+        if record:
+            stage["sketch"] += t1 - t0
+            stage["gather"] += t2 - t1
+            stage["dist"] += t3 - t2
+
+    for _ in range(args.warmup):
+        step(False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        st = torch.tensor([stage["sketch"], stage["gather"], stage["dist"]], dtype=torch.float64, device=dev)
+        dist.all_reduce(st, op=dist.ReduceOp.MAX)
+        stage = dict(zip(["sketch", "gather", "dist"], st.tolist()))
+
+    K = args.steps
+    ms_step = elapsed / K * 1e3
+    pairs = N * (N - 1) / 2
+    value = pairs / (elapsed / K)
+
+    # ---- roofline of the dominant kernel (sketch hash), this rank's launches
+    sk_ms, sk_n = kms[0]
+    avg_launch_s = (sk_ms / max(sk_n, 1)) / 1e3
+    alg_bytes = nloc * P * 3 / 8                     # 2-bit codes + 1 validity bit per base
+    achieved = alg_bytes / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get("genomes_per_launch") == nloc:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    kmers_per_s = nloc * (L - 20) / avg_launch_s if avg_launch_s > 0 else 0.0
+
+    # ---- output segment D2H (PCIe-inclusive leg; not part of `value`)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    host_seg = d_common.cpu()
+    d2h_ms = (time.perf_counter() - t0) * 1e3
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+        threads = max(1, min(threads, 16))
+        cpu = cpu_baseline(args, threads)
+
+    if rank == 0:
+        out = {
+            "metric": "genome pairs/sec (mash dist, k=21 s=1000) + sketch GB/s, at 1/2/4/8 GPUs",
+            "value": value,
+            "unit": "genome pairs/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (on-device splitmix64 genome families, 2-bit packed; see DESIGN.md)",
+            "config": {
+                "workload": "%d synthetic %d bp genomes, k=21, s=%d (BASELINE.json configs[1]); "
+                            "step = sketch + RCCL all-gather + all-pairs" % (N, L, s),
+                "genomes": N, "genome_bp": L, "k": 21, "sketch": s, "family_size": args.family_size,
+                "parallelism": "sketch: genome shards; all-pairs: balanced row shards; RCCL all-gather",
+            },
+            "stages": {
+                "sketch_ms_per_step": stage["sketch"] / K * 1e3,
+                "allgather_ms_per_step": stage["gather"] / K * 1e3,
+                "dist_ms_per_step": stage["dist"] / K * 1e3,
+                "sketch_GBps": N * L / (stage["sketch"] / K) / 1e9 if stage["sketch"] else None,
+                "sketch_packed_GBps": N * P * 3 / 8 / (stage["sketch"] / K) / 1e9 if stage["sketch"] else None,
+                "dist_pairs_per_s": pairs / (stage["dist"] / K) if stage["dist"] else None,
+                "output_d2h_ms_rank0": d2h_ms,
+                "output_bytes_rank0": int(host_seg.numel() * 2),
+            },
+            "kernels_rank0": {
+                "sketch_hash_ms_avg": sk_ms / max(sk_n, 1),
+                "sketch_finalize_ms_avg": kms[1][0] / max(kms[1][1], 1),
+                "allpairs_ms_avg": kms[2][0] / max(kms[2][1], 1),
+                "cuckoo_build_ms_avg": kms[3][0] / max(kms[3][1], 1),
+                "launches": {"sketch_hash": sk_n, "finalize": kms[1][1], "allpairs": kms[2][1],
+                             "build": kms[3][1]},
+            },
+            "roofline": {
+                "kernel": "k_sketch_hash<21>",
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBPS,
+                "traffic": traffic,
+                "note": "algorithmic bytes = 0.375 B/base (2-bit code + validity bit) x bases per "
+                        "launch; the binding limit is integer VALU (Murmur3 64-bit multiplies), "
+                        "see valu_model",
+                "valu_model": {"kmers_per_s": kmers_per_s},
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -6,21 +6,22 @@
 // of the s smallest elements of A u B.  For v = A[i] = B[j] its union rank is
 // i + j - m, m = shared hashes below v, hence
 //     common(A,B) = #{ j : B[j] = A[i]  and  i + j - m_j < s },
-// m_j = number of matches among B[0..j).  A wave streams B in 64-element
-// chunks (one element per lane, coalesced 512-B loads); membership and i come
-// from a two-choice cuckoo table of A (2H key slots + a parallel u16 index
-// array, H = nextpow2(2s), load <= 1/4) built once per row (k_build_cuckoo);
-// m_j is the running match count plus a ballot/popcount prefix within the
-// chunk.  Elements past A's largest hash (A full) cannot match, which ends the
-// scan.  A membership test is two independent ds_read_b64 and two 64-bit
-// compares: no probe loop, no divergence.  R row tables live in LDS per
-// workgroup; results are staged in LDS and written as contiguous runs of the
-// condensed triangle.
+// m_j = number of matches among B[0..j).  A wave holds a whole column sketch B
+// in registers (64-element chunks, one element per lane, coalesced 512-B loads,
+// the next column prefetched while this one is processed); membership and i
+// come from a quotiented two-choice cuckoo table of A (2H slots, H >= 2s, load
+// <= 1/4; the slot position implies B key bits, which the stored word reuses
+// for i) built once per row (k_build_qcuckoo); m_j is the running match count
+// plus a ballot/popcount prefix within the chunk.  Elements past A's largest
+// hash (A full) cannot match, which ends the scan.  A membership test is two
+// independent ds_read_b64 and two 64-bit compares: no probe loop, no
+// divergence.  R row tables live in LDS per workgroup; results are staged in
+// LDS and written as contiguous runs of the condensed triangle.
 // Roofline: LDS random-read throughput + VALU (integer compare/select); no
 // MFMA (set intersection is not a dense contraction).
 //
 // k_allpairs_merge is the literal Mash merge, one lane per pair: any s, used
-// for s > 4096 and as an in-library cross-check.
+// for s > 2048 and as an in-library cross-check.
 
 #include "ctx.h"
 #include "../../include/drephip.h"
@@ -40,71 +41,81 @@ __host__ __device__ __forceinline__ uint64_t cond_index(uint64_t i, uint64_t j, 
     return i * N - i * (i + 1) / 2 + (j - i - 1);
 }
 
-__device__ __forceinline__ void ck_slots(uint64_t x, uint32_t fam, uint32_t hmask, uint32_t &s1,
-                                         uint32_t &s2) {
-    uint32_t m = (uint32_t)x ^ ((uint32_t)(x >> 32) * 0x9E3779B1u);
-    const uint32_t r = fam * 5u;
-    m = r ? ((m << r) | (m >> (32u - r))) : m;
-    s1 = m & hmask;
-    s2 = (m >> 16) & hmask;
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
 }
 
-// One workgroup per row genome: parallel cuckoo insertion in LDS (64-bit
-// atomic exchange), verified by looking every key up again; on failure the
-// next hash family is tried.
-__global__ __launch_bounds__(256) void k_build_cuckoo(const uint64_t *__restrict__ hashes,
-                                                      const uint32_t *__restrict__ nhash, uint32_t s,
-                                                      uint32_t row0, uint32_t H,
-                                                      uint64_t *__restrict__ tabs,
-                                                      uint16_t *__restrict__ tidx,
-                                                      uint8_t *__restrict__ fam_out,
-                                                      uint32_t *__restrict__ nfail) {
+// --------------------------------------------------------------- v2
+// Quotiented two-choice cuckoo table: choice 1 sits at T[f1(x)], choice 2 at
+// T[H + f2(x)], where f1/f2 are disjoint B-bit fields of the key (family f
+// picks the fields).  Because a slot's position fixes those B bits, the stored
+// word replaces them with the key's sketch position i, so one ds_read_b64
+// returns membership AND i:  e = (x & ~F) | (i << o),  match iff
+// (e & ~F) == (x & ~F) and i < nA (the all-ones empty word decodes to
+// i = 2^B-1 >= nA).  Exact for every key.
+struct QFields { uint32_t o1, o2; };
+__host__ __device__ __forceinline__ QFields qfields(uint32_t fam) {
+    // disjoint field offsets inside the low 44 key bits (bottom-s hashes of
+    // genomes up to ~4 Gbp have uniformly random low 44 bits)
+    const uint32_t o1[6] = {0, 22, 5, 27, 11, 33};
+    const uint32_t o2[6] = {22, 0, 27, 5, 33, 11};
+    return {o1[fam], o2[fam]};
+}
+
+__global__ __launch_bounds__(256) void k_build_qcuckoo(const uint64_t *__restrict__ hashes,
+                                                       const uint32_t *__restrict__ nhash, uint32_t s,
+                                                       uint32_t row0, uint32_t B,
+                                                       uint64_t *__restrict__ tabs,
+                                                       uint8_t *__restrict__ fam_out,
+                                                       uint32_t *__restrict__ nfail) {
     extern __shared__ unsigned long long T[];
     __shared__ int fail;
+    const uint32_t H = 1u << B, hm = H - 1;
     const uint32_t r = blockIdx.x;
     const uint32_t g = row0 + r;
     const uint32_t n = nhash[g];
     const uint64_t *A = hashes + (uint64_t)g * s;
-    const uint32_t hmask = H - 1;
-    const uint32_t TS = 2 * H;
     for (uint32_t fam = 0; fam < kMaxFam; fam++) {
-        for (uint32_t i = threadIdx.x; i < TS; i += blockDim.x) T[i] = kEmpty;
+        const QFields q = qfields(fam);
+        const uint64_t F1 = (uint64_t)hm << q.o1, F2 = (uint64_t)hm << q.o2;
+        for (uint32_t i = threadIdx.x; i < 2 * H; i += blockDim.x) T[i] = kEmpty;
         if (threadIdx.x == 0) fail = 0;
         __syncthreads();
+        // insert (key, position) pairs; an entry travels as (x, i)
         for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-            unsigned long long x = A[i];
-            uint32_t p1, p2;
-            ck_slots(x, fam, hmask, p1, p2);
-            uint32_t pos = p1;
+            uint64_t x = A[i];
+            uint32_t ix = i;
+            uint32_t pos = (uint32_t)(x >> q.o1) & hm;
             bool placed = false;
             for (int kick = 0; kick < 96; kick++) {
-                const unsigned long long old = atomicExch(&T[pos], x);
+                const bool second = pos >= H;
+                const uint64_t e = second ? ((x & ~F2) | ((uint64_t)ix << q.o2))
+                                          : ((x & ~F1) | ((uint64_t)ix << q.o1));
+                const unsigned long long old = atomicExch(&T[pos], e);
                 if (old == kEmpty) { placed = true; break; }
-                x = old;
-                ck_slots(x, fam, hmask, p1, p2);
-                pos = (pos == p1) ? (H + p2) : p1;
+                // decode the evicted entry back to (key, position)
+                const uint32_t lp = second ? pos - H : pos;
+                if (second) { ix = (uint32_t)(old >> q.o2) & hm; x = (old & ~F2) | ((uint64_t)lp << q.o2); }
+                else        { ix = (uint32_t)(old >> q.o1) & hm; x = (old & ~F1) | ((uint64_t)lp << q.o1); }
+                pos = second ? ((uint32_t)(x >> q.o1) & hm) : (H + ((uint32_t)(x >> q.o2) & hm));
             }
             if (!placed) fail = 1;
         }
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
             const uint64_t x = A[i];
-            uint32_t p1, p2;
-            ck_slots(x, fam, hmask, p1, p2);
-            if (T[p1] != x && T[H + p2] != x) fail = 1;
+            const uint64_t e1 = T[(uint32_t)(x >> q.o1) & hm];
+            const uint64_t e2 = T[H + ((uint32_t)(x >> q.o2) & hm)];
+            const bool ok1 = (e1 & ~F1) == (x & ~F1) && ((uint32_t)(e1 >> q.o1) & hm) == i;
+            const bool ok2 = (e2 & ~F2) == (x & ~F2) && ((uint32_t)(e2 >> q.o2) & hm) == i;
+            if (!(ok1 || ok2)) fail = 1;
         }
         __syncthreads();
         if (!fail) {
-            uint64_t *o = tabs + (uint64_t)r * TS;
-            uint16_t *oi = tidx + (uint64_t)r * TS;
-            for (uint32_t i = threadIdx.x; i < TS; i += blockDim.x) { o[i] = T[i]; oi[i] = 0xFFFF; }
-            __syncthreads();
-            for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-                const uint64_t x = A[i];
-                uint32_t p1, p2;
-                ck_slots(x, fam, hmask, p1, p2);
-                oi[T[p1] == x ? p1 : H + p2] = (uint16_t)i;
-            }
+            uint64_t *o = tabs + (uint64_t)r * 2 * H;
+            for (uint32_t i = threadIdx.x; i < 2 * H; i += blockDim.x) o[i] = T[i];
             if (threadIdx.x == 0) fam_out[r] = (uint8_t)fam;
             return;
         }
@@ -113,85 +124,93 @@ __global__ __launch_bounds__(256) void k_build_cuckoo(const uint64_t *__restrict
     if (threadIdx.x == 0) { fam_out[r] = 0xFF; atomicAdd(nfail, 1u); }
 }
 
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-template <int R>
-__global__ __launch_bounds__(kApWG) void k_allpairs_ck(
+// R rows (tables in LDS) x kApCols columns per workgroup; each wave walks its
+// columns with the whole column sketch in registers (NCH 64-element chunks,
+// double-buffered: the next column's loads are in flight while this one is
+// processed).
+template <int R, int NCH>
+__global__ __launch_bounds__(kApWG) void k_allpairs_q(
     const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ nhash,
-    const uint64_t *__restrict__ tabs, const uint16_t *__restrict__ tidx,
-    const uint8_t *__restrict__ fam, uint32_t s, uint32_t N, uint32_t row0, uint32_t row1, uint32_t H,
-    const uint2 *__restrict__ items, uint16_t *__restrict__ common, uint16_t *__restrict__ denom,
-    uint64_t seg0) {
+    const uint64_t *__restrict__ tabs, const uint8_t *__restrict__ fam, uint32_t s, uint32_t N,
+    uint32_t row0, uint32_t row1, uint32_t B, const uint2 *__restrict__ items,
+    uint16_t *__restrict__ common, uint16_t *__restrict__ denom, uint64_t seg0) {
     extern __shared__ uint64_t lds[];
-    const uint32_t TS = 2 * H;
-    const uint32_t hmask = H - 1;
-    uint64_t *T = lds;                                              // [R][TS] keys
-    uint16_t *I = (uint16_t *)(lds + (uint64_t)R * TS);             // [R][TS] positions
-    uint16_t *res_c = I + (uint64_t)R * TS;                         // [R][kApCols]
+    const uint32_t H = 1u << B, hm = H - 1, TS = 2 * H;
+    uint64_t *T = lds;
+    uint16_t *res_c = (uint16_t *)(lds + (uint64_t)R * TS);
     uint16_t *res_d = res_c + R * kApCols;
     const uint32_t i0 = items[blockIdx.x].x;
     const uint32_t c0 = items[blockIdx.x].y;
     const uint32_t nrows = min((uint32_t)R, row1 - i0);
     const uint32_t cend = min(c0 + kApCols, N);
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-
     for (uint32_t r = 0; r < nrows; r++) {
         const uint4 *src = (const uint4 *)(tabs + (uint64_t)(i0 - row0 + r) * TS);
         uint4 *dst = (uint4 *)(T + (uint64_t)r * TS);
         for (uint32_t i = tid; i < TS / 2; i += kApWG) dst[i] = src[i];
-        const uint4 *isrc = (const uint4 *)(tidx + (uint64_t)(i0 - row0 + r) * TS);
-        uint4 *idst = (uint4 *)(I + (uint64_t)r * TS);
-        for (uint32_t i = tid; i < TS / 8; i += kApWG) idst[i] = isrc[i];
     }
-    uint32_t nA[R], fm[R];
-    uint64_t alast[R];
+    uint32_t nA[R], o1[R], o2[R];
+    uint64_t alast[R], nF1[R], nF2[R];
     bool any_partial_row = false;
 #pragma unroll
     for (int r = 0; r < R; r++) {
         const bool ok = (uint32_t)r < nrows;
         nA[r] = ok ? nhash[i0 + r] : s;
-        fm[r] = ok ? fam[i0 - row0 + r] : 0;
-        // largest hash of a full row sketch: no larger B element can match
+        const QFields q = qfields(ok ? fam[i0 - row0 + r] : 0);
+        o1[r] = q.o1; o2[r] = q.o2;
+        nF1[r] = ~((uint64_t)hm << q.o1);
+        nF2[r] = ~((uint64_t)hm << q.o2);
         alast[r] = (ok && nA[r] >= s) ? hashes[(uint64_t)(i0 + r) * s + s - 1] : kEmpty;
         any_partial_row |= nA[r] < s;
     }
-    __syncthreads();
     const uint64_t lt_mask = (1ull << lane) - 1;
+    const uint32_t nch = (s + 63) / 64;
 
-    for (uint32_t c = c0 + wave; c < cend; c += kApWG / 64) {
+    uint64_t cur[NCH], nxt[NCH];
+    uint32_t c = c0 + wave;
+    if (c < cend) {
+        const uint64_t *Bc = hashes + (uint64_t)c * s;
+#pragma unroll
+        for (int k = 0; k < NCH; k++) { const uint32_t j = k * 64 + lane; nxt[k] = (k < (int)nch && j < s) ? Bc[j] : kEmpty; }
+    }
+    __syncthreads();
+    for (; c < cend; c += kApWG / 64) {
+#pragma unroll
+        for (int k = 0; k < NCH; k++) cur[k] = nxt[k];
+        const uint32_t cn = c + kApWG / 64;
+        if (cn < cend) {
+            const uint64_t *Bn = hashes + (uint64_t)cn * s;
+#pragma unroll
+            for (int k = 0; k < NCH; k++) { const uint32_t j = k * 64 + lane; nxt[k] = (k < (int)nch && j < s) ? Bn[j] : kEmpty; }
+        }
         const uint32_t nB = nhash[c];
-        const uint64_t *B = hashes + (uint64_t)c * s;
         const bool partial = any_partial_row || nB < s;
         uint32_t cnt[R], mrun[R];
 #pragma unroll
         for (int r = 0; r < R; r++) { cnt[r] = 0; mrun[r] = 0; }
-        for (uint32_t jb = 0; jb < nB; jb += 64) {
-            const uint32_t j = jb + lane;
-            const uint64_t b = j < nB ? B[j] : kEmpty;
-            uint32_t p1, p2;
-            ck_slots(b, 0, hmask, p1, p2);
-            uint32_t pf = 0;
+#pragma unroll
+        for (int k = 0; k < NCH; k++) {
+            if (k >= (int)nch) break;
+            const uint32_t j = k * 64 + lane;
+            const uint64_t b = cur[k];
             bool more = false;
 #pragma unroll
             for (int r = 0; r < R; r++) {
                 if ((uint32_t)r >= nrows || i0 + r >= c) continue;        // wave-uniform
                 const bool in = b <= alast[r] && b != kEmpty;
-                if (fm[r] != pf) { ck_slots(b, fm[r], hmask, p1, p2); pf = fm[r]; }
                 const uint64_t *Tr = T + (uint64_t)r * TS;
-                const uint32_t q1 = p1, q2 = H + p2;
-                const bool f1 = in && Tr[q1] == b;
-                const bool f2 = in && !f1 && Tr[q2] == b;
-                const bool found = f1 || f2;
-                const uint64_t mask = __ballot(found);
-                uint32_t i = 0xFFFFu;
-                if (found) i = I[(uint64_t)r * TS + (f1 ? q1 : q2)];
-                const uint32_t mbefore = mrun[r] + (uint32_t)__popcll(mask & lt_mask);
-                cnt[r] += (found && i + j - mbefore < s) ? 1u : 0u;
-                mrun[r] += (uint32_t)__popcll(mask);
+                const uint64_t e1 = Tr[(uint32_t)(b >> o1[r]) & hm];
+                const uint64_t e2 = Tr[H + ((uint32_t)(b >> o2[r]) & hm)];
+                const uint32_t i1 = (uint32_t)(e1 >> o1[r]) & hm;
+                const uint32_t i2 = (uint32_t)(e2 >> o2[r]) & hm;
+                const bool f1 = ((e1 ^ b) & nF1[r]) == 0 && i1 < nA[r];
+                const bool f2 = ((e2 ^ b) & nF2[r]) == 0 && i2 < nA[r];
+                const bool found = in && (f1 || f2);
+                const uint32_t i = f1 ? i1 : i2;
+                const uint64_t m = __ballot(found);
+                const uint32_t mb = mrun[r] + (uint32_t)__popcll(m & lt_mask);
+                cnt[r] += (found && i + j - mb < s) ? 1u : 0u;
+                mrun[r] += (uint32_t)__popcll(m);
                 more |= in;
             }
             if (__ballot(more) == 0) break;
@@ -202,7 +221,7 @@ __global__ __launch_bounds__(kApWG) void k_allpairs_ck(
             const uint32_t cc = wave_sum(cnt[r]);
             uint32_t dd = s;
             if (partial) {
-                const uint32_t u = nA[r] + nB - mrun[r];      // |A u B|; mrun = |A n B| here
+                const uint32_t u = nA[r] + nB - mrun[r];
                 dd = u < s ? u : s;
             }
             if (lane == 0) { res_c[r * kApCols + (c - c0)] = (uint16_t)cc; res_d[r * kApCols + (c - c0)] = (uint16_t)dd; }
@@ -269,16 +288,15 @@ static int launch_merge(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32
     return DREPHIP_OK;
 }
 
-template <int R>
-static int launch_ck(drephip_ctx *ctx, uint32_t nitems, size_t lds, hipStream_t st, const uint64_t *h,
-                     const uint32_t *nh, const uint64_t *tabs, const uint16_t *tidx, const uint8_t *fam,
-                     uint32_t N, uint32_t row0, uint32_t row1, uint32_t H, const uint2 *items, uint16_t *cm,
-                     uint16_t *dn, uint64_t seg0) {
-    HIPC(hipFuncSetAttribute((const void *)k_allpairs_ck<R>, hipFuncAttributeMaxDynamicSharedMemorySize,
+template <int R, int NCH>
+static int launch_q(drephip_ctx *ctx, uint32_t nitems, size_t lds, hipStream_t st, const uint64_t *h,
+                    const uint32_t *nh, const uint64_t *tabs, const uint8_t *fam, uint32_t N, uint32_t row0,
+                    uint32_t row1, uint32_t B, const uint2 *items, uint16_t *cm, uint16_t *dn, uint64_t seg0) {
+    HIPC(hipFuncSetAttribute((const void *)k_allpairs_q<R, NCH>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)lds));
     timing_mark(ctx, 2, st, true);
-    hipLaunchKernelGGL(k_allpairs_ck<R>, dim3(nitems), dim3(kApWG), lds, st, h, nh, tabs, tidx, fam, ctx->s,
-                       N, row0, row1, H, items, cm, dn, seg0);
+    hipLaunchKernelGGL((k_allpairs_q<R, NCH>), dim3(nitems), dim3(kApWG), lds, st, h, nh, tabs, fam, ctx->s, N,
+                       row0, row1, B, items, cm, dn, seg0);
     timing_mark(ctx, 2, st, false);
     HIPC(hipGetLastError());
     return DREPHIP_OK;
@@ -294,38 +312,35 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
     const uint64_t seg0 = cond_index(row0, row0 + 1, N);
     const uint64_t seg1 = row1 < N - 1 ? cond_index(row1, row1 + 1, N) : (uint64_t)N * (N - 1) / 2;
     const uint64_t npairs = seg1 - seg0;
-    uint32_t H = 16;
-    while (H < 2 * s) H <<= 1;
-    const uint64_t TS = 2ull * H;
-    const uint64_t row_bytes = TS * 10;             // keys + u16 positions
-    if (force_merge || row_bytes > kLdsTables || s > 65535)
+    // table: 2H slots, H = 2^B >= 2s (load <= 1/4) and 2^B > s (positions fit the field)
+    uint32_t B = 4;
+    while ((1u << B) < 2 * s) B++;
+    const uint64_t TS = 2ull << B;
+    if (force_merge || s > 2048 || TS * 8 > kLdsTables)
         return launch_merge(ctx, d_hashes, d_nhash, N, seg0, npairs, d_common, d_denom, st);
 
     const uint32_t nrows = row1 - row0;
     uint64_t *d_tabs;
-    uint16_t *d_tidx;
     uint8_t *d_fam;
     uint32_t *d_nfail;
     uint2 *d_items;
     int rc;
     if ((rc = scratch(ctx, "ap_tabs", (uint64_t)nrows * TS * 8, (void **)&d_tabs))) return rc;
-    if ((rc = scratch(ctx, "ap_tidx", (uint64_t)nrows * TS * 2, (void **)&d_tidx))) return rc;
     if ((rc = scratch(ctx, "ap_fam", nrows, (void **)&d_fam))) return rc;
     if ((rc = scratch(ctx, "ap_nfail", 4, (void **)&d_nfail))) return rc;
     HIPC(hipMemsetAsync(d_nfail, 0, 4, st));
     const size_t blds = TS * 8;
-    HIPC(hipFuncSetAttribute((const void *)k_build_cuckoo, hipFuncAttributeMaxDynamicSharedMemorySize,
+    HIPC(hipFuncSetAttribute((const void *)k_build_qcuckoo, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)blds));
     timing_mark(ctx, 3, st, true);
-    hipLaunchKernelGGL(k_build_cuckoo, dim3(nrows), dim3(256), blds, st, d_hashes, d_nhash, s, row0, H,
-                       d_tabs, d_tidx, d_fam, d_nfail);
+    hipLaunchKernelGGL(k_build_qcuckoo, dim3(nrows), dim3(256), blds, st, d_hashes, d_nhash, s, row0, B,
+                       d_tabs, d_fam, d_nfail);
     timing_mark(ctx, 3, st, false);
     HIPC(hipGetLastError());
 
-    // rows per workgroup: as many tables as fit the LDS budget
-    static const uint32_t kR[] = {8, 6, 4, 3, 2, 1};
+    static const uint32_t kR[] = {8, 4, 2, 1};
     uint32_t R = 1;
-    for (uint32_t r : kR) if ((uint64_t)r * row_bytes <= kLdsTables) { R = r; break; }
+    for (uint32_t r : kR) if ((uint64_t)r * TS * 8 <= kLdsTables) { R = r; break; }
     std::vector<uint2> items;
     for (uint32_t i0 = row0; i0 < row1; i0 += R)
         for (uint32_t c0 = i0 + 1; c0 < N; c0 += kApCols) items.push_back(make_uint2(i0, c0));
@@ -334,21 +349,27 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
     uint32_t nfail = 0;
     HIPC(hipMemcpyAsync(&nfail, d_nfail, 4, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));
-    if (nfail)   // a row table could not be built with any hash family: exact merge kernel instead
+    if (nfail)   // a row table could not be built with any field pair: exact merge kernel instead
         return launch_merge(ctx, d_hashes, d_nhash, N, seg0, npairs, d_common, d_denom, st);
 
-    const size_t lds = (size_t)R * row_bytes + (size_t)R * kApCols * 4;
+    const size_t lds = (size_t)R * TS * 8 + (size_t)R * kApCols * 4;
     const uint32_t ni = (uint32_t)items.size();
-#define DREPHIP_CK(RR) launch_ck<RR>(ctx, ni, lds, st, d_hashes, d_nhash, d_tabs, d_tidx, d_fam, N, row0, row1, H, d_items, d_common, d_denom, seg0)
-    switch (R) {
-        case 8: rc = DREPHIP_CK(8); break;
-        case 6: rc = DREPHIP_CK(6); break;
-        case 4: rc = DREPHIP_CK(4); break;
-        case 3: rc = DREPHIP_CK(3); break;
-        case 2: rc = DREPHIP_CK(2); break;
-        default: rc = DREPHIP_CK(1); break;
+    const bool big = s > 1024;
+#define DREPHIP_Q(RR, NC) launch_q<RR, NC>(ctx, ni, lds, st, d_hashes, d_nhash, d_tabs, d_fam, N, row0, row1, B, d_items, d_common, d_denom, seg0)
+    if (!big) {
+        switch (R) {
+            case 8: rc = DREPHIP_Q(8, 16); break;
+            case 4: rc = DREPHIP_Q(4, 16); break;
+            case 2: rc = DREPHIP_Q(2, 16); break;
+            default: rc = DREPHIP_Q(1, 16); break;
+        }
+    } else {
+        switch (R) {
+            case 2: rc = DREPHIP_Q(2, 32); break;
+            default: rc = DREPHIP_Q(1, 32); break;
+        }
     }
-#undef DREPHIP_CK
+#undef DREPHIP_Q
     if (rc) return rc;
     HIPC(hipStreamSynchronize(st));
     return DREPHIP_OK;

@@ -131,6 +131,141 @@ __global__ __launch_bounds__(kSketchWG) void k_sketch_hash(
     }
 }
 
+// ---------------------------------------------- v2: instruction-lean kernel
+// Same contract as k_sketch_hash.  The window is kept as 32-bit words rolled
+// with v_alignbit_b32 (one instruction per word per base), the canonical k-mer
+// is hashed for every window end (no per-k-mer branch; invalid windows are
+// masked in the admit test), rotations are two v_alignbit_b32 and h*5+c is one
+// v_lshl_add_u64.  K = 21 only (3 Murmur words: 16-byte block + 5-byte tail).
+__device__ __forceinline__ uint64_t rotl64_ab(uint64_t x, int r) {
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    uint32_t nlo, nhi;
+    if (r < 32) {
+        nhi = __builtin_amdgcn_alignbit(hi, lo, 32 - r);
+        nlo = __builtin_amdgcn_alignbit(lo, hi, 32 - r);
+    } else {
+        nhi = __builtin_amdgcn_alignbit(lo, hi, 64 - r);
+        nlo = __builtin_amdgcn_alignbit(hi, lo, 64 - r);
+    }
+    return ((uint64_t)nhi << 32) | nlo;
+}
+__device__ __forceinline__ uint64_t x5_plus(uint64_t x, uint64_t c) {
+    uint64_t y;
+    asm volatile("v_lshl_add_u64 %0, %1, 2, %1" : "=v"(y) : "v"(x));
+    return y + c;
+}
+__device__ __forceinline__ uint64_t fmix64_v(uint64_t k) {
+    k ^= k >> 33; k *= 0xff51afd7ed558ccdULL;
+    k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ULL;
+    k ^= k >> 33; return k;
+}
+__device__ __forceinline__ uint64_t murmur21(uint64_t k1, uint64_t k2, uint64_t k3, uint32_t seed) {
+    constexpr uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
+    uint64_t h1 = seed, h2 = seed;
+    k1 *= c1; k1 = rotl64_ab(k1, 31); k1 *= c2; h1 ^= k1;
+    h1 = rotl64_ab(h1, 27); h1 += h2; h1 = x5_plus(h1, 0x52dce729);
+    k2 *= c2; k2 = rotl64_ab(k2, 33); k2 *= c1; h2 ^= k2;
+    h2 = rotl64_ab(h2, 31); h2 += h1; h2 = x5_plus(h2, 0x38495ab5);
+    k3 *= c1; k3 = rotl64_ab(k3, 31); k3 *= c2; h1 ^= k3;
+    h1 ^= 21u; h2 ^= 21u;
+    h1 += h2; h2 += h1;
+    return fmix64_v(h1) + fmix64_v(h2);
+}
+
+struct Window21 {
+    uint32_t f[6];      // forward ASCII, bytes 0..20 (word 5 holds byte 20)
+    uint32_t r[6];      // reverse-complement ASCII
+    uint64_t fc, rc;    // 2-bit codes, first character most significant
+    uint32_t run;
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int i = 0; i < 6; i++) { f[i] = 0; r[i] = 0; }
+        fc = rc = 0; run = 0;
+    }
+    __device__ __forceinline__ void push(uint32_t c, uint32_t v) {
+        run = v ? run + 1 : 0;
+        fc = ((fc << 2) | c) & ((1ull << 42) - 1);
+        rc = (rc >> 2) | ((uint64_t)(3u - c) << 40);
+        const uint32_t a = __builtin_amdgcn_perm(0u, 0x54474341u, c | 0x0c0c0c00u);   // A C G T
+        const uint32_t ca = __builtin_amdgcn_perm(0u, 0x41434754u, c | 0x0c0c0c00u);  // T G C A
+#pragma unroll
+        for (int i = 0; i < 5; i++) f[i] = __builtin_amdgcn_alignbit(f[i + 1], f[i], 8);
+        f[5] = a;
+        r[5] = r[4] >> 24;
+#pragma unroll
+        for (int i = 4; i > 0; i--) r[i] = __builtin_amdgcn_alignbit(r[i], r[i - 1], 24);
+        r[0] = (r[0] << 8) | ca;
+    }
+    __device__ __forceinline__ uint64_t hash(uint32_t seed) const {
+        const bool fwd = fc <= rc;
+        uint32_t w[6];
+#pragma unroll
+        for (int i = 0; i < 6; i++) w[i] = fwd ? f[i] : r[i];
+        return murmur21(((uint64_t)w[1] << 32) | w[0], ((uint64_t)w[3] << 32) | w[2],
+                        ((uint64_t)w[5] << 32) | w[4], seed);
+    }
+};
+
+// Candidates are staged in an LDS buffer (wave-aggregated LDS atomic) and only
+// flushed to the per-genome set after the tile, so the hot loop issues no
+// global memory operation with a wait; a full buffer spills to the set
+// directly.
+constexpr uint32_t kStage = 1024;
+
+__global__ __launch_bounds__(kSketchWG) void k_sketch_hash21_v2(
+    const uint32_t *__restrict__ codes, const uint32_t *__restrict__ valid,
+    const uint64_t *__restrict__ tile_base, const uint32_t *__restrict__ tile_genome,
+    const uint64_t *__restrict__ thr, unsigned long long *__restrict__ sets,
+    uint32_t *__restrict__ cnt, uint32_t set_log2, uint32_t limit, uint32_t seed) {
+    constexpr int K = 21;
+    __shared__ uint64_t stage[kStage];
+    __shared__ uint32_t nstage;
+    const uint32_t t = blockIdx.x;
+    const uint32_t g = tile_genome[t];
+    const uint64_t T = thr[g];
+    const uint64_t start = tile_base[t] + (uint64_t)threadIdx.x * kLaneBases;
+    const uint32_t mask = (1u << set_log2) - 1;
+    unsigned long long *S = sets + ((uint64_t)g << set_log2);
+    uint32_t *C = cnt + g;
+    if (threadIdx.x == 0) nstage = 0;
+    const uint32_t *cw = codes + (start - kWarm) / 16;
+    const uint32_t *vw = valid + (start - kWarm) / 32;
+    Window21 w;
+    w.init();
+    {
+        const uint32_t v0 = vw[0];
+        const uint32_t c0 = cw[0], c1 = cw[1];
+#pragma unroll
+        for (int b = 0; b < 16; b++) w.push((c0 >> (2 * b)) & 3u, (v0 >> b) & 1u);
+#pragma unroll
+        for (int b = 0; b < 16; b++) w.push((c1 >> (2 * b)) & 3u, (v0 >> (16 + b)) & 1u);
+    }
+    __syncthreads();
+    uint32_t cnext = cw[2];
+    uint32_t vcur = vw[1];
+    for (int wi = 0; wi < (int)(kLaneBases / 16); wi++) {
+        const uint32_t c = cnext;
+        const uint32_t vbits = vcur >> ((wi & 1) * 16);
+        if (wi + 1 < (int)(kLaneBases / 16)) {
+            cnext = cw[3 + wi];
+            if (wi & 1) vcur = vw[2 + (wi >> 1)];
+        }
+#pragma unroll
+        for (int b = 0; b < 16; b++) {
+            w.push((c >> (2 * b)) & 3u, (vbits >> b) & 1u);
+            const uint64_t h = w.hash(seed);
+            if (__builtin_expect(h <= T && w.run >= (uint32_t)K, 0)) {
+                const uint32_t slot = atomicAdd(&nstage, 1u);
+                if (slot < kStage) stage[slot] = h;
+                else set_insert(S, mask, C, limit, h);
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t n = min(nstage, kStage);
+    for (uint32_t i = threadIdx.x; i < n; i += kSketchWG) set_insert(S, mask, C, limit, stage[i]);
+}
+
 // ----------------------------------------------------------------- finalize
 enum : uint8_t { ST_OK = 0, ST_UP = 1, ST_DOWN = 2 };
 
@@ -333,8 +468,13 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
         }
         if (nt > 0) {
             timing_mark(ctx, 0, st, true);
-            launch_hash<21>(nt, st, d_codes, d_valid, tb_tiles_b, tb_tiles_g, d_thr, d_sets, d_cnt,
-                            plan.set_log2, limit, ctx->seed);
+            if (ctx->sketch_variant == 1)
+                launch_hash<21>(nt, st, d_codes, d_valid, tb_tiles_b, tb_tiles_g, d_thr, d_sets, d_cnt,
+                                plan.set_log2, limit, ctx->seed);
+            else
+                hipLaunchKernelGGL(k_sketch_hash21_v2, dim3(nt), dim3(kSketchWG), 0, st, d_codes, d_valid,
+                                   tb_tiles_b, tb_tiles_g, d_thr, d_sets, d_cnt, plan.set_log2, limit,
+                                   ctx->seed);
             timing_mark(ctx, 0, st, false);
         }
         timing_mark(ctx, 1, st, true);
