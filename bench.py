@@ -43,22 +43,6 @@ def parse():
     return ap.parse_args()
 
 
-def row_partition(N, world):
-    """Balanced contiguous row ranges of the upper triangle (pairs per row = N-1-i)."""
-    pairs = np.arange(N - 1, -1, -1, dtype=np.float64)
-    cum = np.concatenate([[0.0], np.cumsum(pairs)])
-    total = cum[-1]
-    bounds = [0]
-    for r in range(1, world):
-        bounds.append(int(np.searchsorted(cum, total * r / world)))
-    bounds.append(N)
-    return [(bounds[r], bounds[r + 1]) for r in range(world)]
-
-
-def cond_start(i, N):
-    return i * N - i * (i + 1) // 2
-
-
 def cpu_baseline(args, threads):
     """Bounded sample of the same whole job on the host with the C oracle
     (Mash-equivalent restatement, OpenMP): sketch 2*threads genomes, dist
@@ -104,16 +88,18 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     from drep_amd import _lib
+    from drep_amd.parallel import genome_shard, row_partition, segment_size, gather_sketches
 
     N, L, s = args.genomes, args.genome_bp, args.sketch
     ctx = _lib.Context(device=local, k=21, s=s, seed=42)
     ctx.set_timing(True)
     dev = torch.device("cuda", local)
+    # every library call runs on torch's stream, so it is ordered after the
+    # tensor fills / all-gathers that torch issues there
+    stream = torch.cuda.current_stream(dev).cuda_stream
 
     # ---- this rank's genome shard, generated on device (untimed)
-    nmax = (N + world - 1) // world
-    g0 = min(N, rank * nmax)
-    g1 = min(N, g0 + nmax)
+    g0, g1, nmax = genome_shard(N, world, rank)
     nloc = g1 - g0
     tile = _lib.tile_bases()
     P = _lib.padded_bases([L])
@@ -121,16 +107,14 @@ def main():
     codes = torch.zeros(total_bases // 16, dtype=torch.int32, device=dev)
     valid = torch.zeros(total_bases // 32, dtype=torch.int32, device=dev)
     if nloc:
-        ctx.synth_device(args.seed, g0, nloc, args.family_size, L, codes.data_ptr(), valid.data_ptr())
+        ctx.synth_device(args.seed, g0, nloc, args.family_size, L, codes.data_ptr(), valid.data_ptr(), stream)
     base_off = np.array([tile + i * P for i in range(nloc)], np.uint64)
     padded = np.full(nloc, P, np.uint64)
     nkmers = np.full(nloc, L - 20, np.uint64)
     loc_h = torch.full((nmax, s), -1, dtype=torch.int64, device=dev)
     loc_n = torch.zeros(nmax, dtype=torch.int32, device=dev)
-    all_h = torch.empty((world * nmax, s), dtype=torch.int64, device=dev)
-    all_n = torch.empty(world * nmax, dtype=torch.int32, device=dev)
     r0, r1 = row_partition(N, world)[rank]
-    seg = cond_start(min(r1, N - 1), N) - cond_start(min(r0, N - 1), N) if r0 < N - 1 else 0
+    seg = segment_size(N, r0, r1)
     d_common = torch.zeros(max(seg, 1), dtype=torch.int16, device=dev)
 
     stage = {"sketch": 0.0, "gather": 0.0, "dist": 0.0}
@@ -140,7 +124,7 @@ def main():
         t0 = time.perf_counter()
         if nloc:
             ctx.sketch_device(codes.data_ptr(), valid.data_ptr(), base_off, padded, nkmers, nloc,
-                              loc_h.data_ptr(), loc_n.data_ptr())
+                              loc_h.data_ptr(), loc_n.data_ptr(), stream)
             if record:
                 for w in (0, 1):
                     ms, n = ctx.kernel_ms(w)
@@ -148,15 +132,13 @@ def main():
                     kms[w][1] += n
         t1 = time.perf_counter()
         if world > 1:
-            dist.all_gather_into_tensor(all_h, loc_h)
-            dist.all_gather_into_tensor(all_n, loc_n)
+            hh, nn = gather_sketches(loc_h, loc_n)     # RCCL over xGMI
             torch.cuda.synchronize()
-            hh, nn = all_h, all_n
         else:
             hh, nn = loc_h, loc_n
         t2 = time.perf_counter()
         if seg:
-            ctx.allpairs_device(hh.data_ptr(), nn.data_ptr(), N, r0, r1, d_common.data_ptr())
+            ctx.allpairs_device(hh.data_ptr(), nn.data_ptr(), N, r0, r1, d_common.data_ptr(), None, stream)
             if record:
                 for w in (2, 3):
                     ms, n = ctx.kernel_ms(w)

@@ -188,9 +188,10 @@ __global__ __launch_bounds__(kApWG) void k_allpairs_q(
         uint32_t cnt[R], mrun[R];
 #pragma unroll
         for (int r = 0; r < R; r++) { cnt[r] = 0; mrun[r] = 0; }
+bool alive = true;
 #pragma unroll
         for (int k = 0; k < NCH; k++) {
-            if (k >= (int)nch) break;
+            if (!alive || k >= (int)nch) continue;      // wave-uniform
             const uint32_t j = k * 64 + lane;
             const uint64_t b = cur[k];
             bool more = false;
@@ -213,7 +214,7 @@ __global__ __launch_bounds__(kApWG) void k_allpairs_q(
                 mrun[r] += (uint32_t)__popcll(m);
                 more |= in;
             }
-            if (__ballot(more) == 0) break;
+            alive = __ballot(more) != 0;
         }
 #pragma unroll
         for (int r = 0; r < R; r++) {

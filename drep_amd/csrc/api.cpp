@@ -92,9 +92,10 @@ using namespace drephip;
         HIPC(hipSetDevice((ctx)->device));                          \
     } while (0)
 
-static hipStream_t pick_stream(drephip_ctx *ctx, void *stream) {
-    return stream ? (hipStream_t)stream : ctx->stream;
-}
+// Device-pointer entry points run on the caller's stream.  0 is the HIP null
+// stream (also torch's default stream handle), exactly as in the HIP API, so
+// work is ordered after whatever the caller queued there.
+static hipStream_t pick_stream(drephip_ctx *, void *stream) { return (hipStream_t)stream; }
 
 DREPHIP_EXPORT int drephip_version(void) { return 100; }
 
@@ -131,7 +132,6 @@ DREPHIP_EXPORT int drephip_create(int device, int k, uint32_t s, uint32_t seed, 
     drephip_ctx *c = new (std::nothrow) drephip_ctx();
     if (!c) { set_error("out of host memory"); return DREPHIP_ERR_NOMEM; }
     c->device = device; c->k = k; c->s = s; c->seed = seed;
-    if (const char *v = getenv("DREPHIP_SKETCH_VARIANT")) c->sketch_variant = atoi(v);
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) { delete c; set_error(hipGetErrorString(e)); return DREPHIP_ERR_HIP; }
     *out = c;

@@ -20,7 +20,6 @@ struct drephip_ctx {
     uint32_t seed = 42;
     hipStream_t stream = nullptr;
     bool timing = false;
-    int sketch_variant = 0;   // 0 = v2 (default), 1 = generic template kernel (A/B)
     // named grow-only device scratch buffers
     std::map<std::string, DevBuf> bufs;
     // per-kernel timing of the last call: {sum ms, launches}

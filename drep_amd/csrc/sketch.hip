@@ -2,15 +2,15 @@
 // genome (drep/d_cluster.py:531-549) and `mash paste` (551-567).
 //
 // Three kernels, one pass over the packed genome set per round:
-//   k_sketch_hash     one workgroup per 32768-base tile; each lane rolls a
+//   k_sketch_hash21   one workgroup per 32768-base tile; each lane rolls a
 //                     k-mer window over 128 window ends (2-bit codes +
-//                     validity from HBM, one 64-bit load pair per 16 bases),
-//                     keeps forward/reverse-complement ASCII windows in
-//                     registers, hashes the canonical k-mer with
-//                     MurmurHash3_x64_128 and admits it only if h <= T[g]
-//                     (per-genome candidate threshold).  Candidates go into a
-//                     per-genome open-addressing set in HBM (64-bit CAS), so
-//                     duplicates are dropped at insert time.
+//                     validity from HBM, one load per 16 bases), keeps
+//                     forward/reverse-complement ASCII windows in registers,
+//                     hashes the canonical k-mer with MurmurHash3_x64_128 and
+//                     admits it only if h <= T[g] (per-genome candidate
+//                     threshold).  Admitted hashes are staged in LDS and, after
+//                     the tile, inserted into a per-genome open-addressing set
+//                     in HBM (64-bit CAS), so duplicates drop out at insert.
 //   k_sketch_finalize one workgroup per genome: compacts the set into LDS,
 //                     bitonic-sorts it and writes the s smallest.
 //   k_synth           bench input generator (not on the product path).
@@ -27,50 +27,12 @@
 #include "../../include/drephip.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
 namespace drephip {
-
-// ------------------------------------------------------------ k-mer window
-template <int K>
-struct Window {
-    static constexpr int NW = (K + 7) / 8;
-    static constexpr int LASTB = (K - 1) % 8;
-    static constexpr uint64_t LASTMASK = (K % 8 == 0) ? ~0ull : ((1ull << (8 * (K % 8))) - 1);
-    static constexpr uint64_t CMASK = (K == 32) ? ~0ull : ((1ull << (2 * K)) - 1);
-    uint64_t f[NW];     // forward k-mer, ASCII, byte j = base (end-K+1+j)
-    uint64_t r[NW];     // reverse complement, ASCII, byte j = comp(base end-j)
-    uint64_t fc, rc;    // 2-bit codes, first character most significant
-    uint32_t run;       // consecutive valid bases ending here
-
-    __device__ __forceinline__ void init() {
-#pragma unroll
-        for (int i = 0; i < NW; i++) { f[i] = 0; r[i] = 0; }
-        fc = rc = 0; run = 0;
-    }
-    __device__ __forceinline__ void push(uint32_t c, uint32_t v) {
-        run = v ? run + 1 : 0;
-        fc = ((fc << 2) | c) & CMASK;
-        rc = (rc >> 2) | ((uint64_t)(3u - c) << (2 * (K - 1)));
-        const uint64_t a = (0x54474341u >> (8 * c)) & 0xffu;          // A C G T
-        const uint64_t ca = (0x41434754u >> (8 * c)) & 0xffu;         // T G C A
-#pragma unroll
-        for (int i = 0; i < NW - 1; i++) f[i] = (f[i] >> 8) | (f[i + 1] << 56);
-        f[NW - 1] = (f[NW - 1] >> 8) | (a << (8 * LASTB));
-#pragma unroll
-        for (int i = NW - 1; i > 0; i--) r[i] = (r[i] << 8) | (r[i - 1] >> 56);
-        r[0] = (r[0] << 8) | ca;
-        r[NW - 1] &= LASTMASK;
-    }
-    __device__ __forceinline__ uint64_t hash(uint32_t seed) const {
-        uint64_t w[NW];
-        const bool fwd = fc <= rc;   // memcmp(fwd, rev, K) <= 0
-#pragma unroll
-        for (int i = 0; i < NW; i++) w[i] = fwd ? f[i] : r[i];
-        return murmur3_h1_words<K>(w, seed);
-    }
-};
 
 __device__ __forceinline__ void set_insert(unsigned long long *S, uint32_t mask, uint32_t *cnt,
                                            uint32_t limit, uint64_t h) {
@@ -84,59 +46,14 @@ __device__ __forceinline__ void set_insert(unsigned long long *S, uint32_t mask,
     }
 }
 
-template <int K>
-__global__ __launch_bounds__(kSketchWG) void k_sketch_hash(
-    const uint32_t *__restrict__ codes, const uint32_t *__restrict__ valid,
-    const uint64_t *__restrict__ tile_base, const uint32_t *__restrict__ tile_genome,
-    const uint64_t *__restrict__ thr, unsigned long long *__restrict__ sets,
-    uint32_t *__restrict__ cnt, uint32_t set_log2, uint32_t limit, uint32_t seed) {
-    const uint32_t t = blockIdx.x;
-    const uint32_t g = tile_genome[t];
-    const uint64_t T = thr[g];
-    const uint64_t start = tile_base[t] + (uint64_t)threadIdx.x * kLaneBases;
-    const uint32_t mask = (1u << set_log2) - 1;
-    unsigned long long *S = sets + ((uint64_t)g << set_log2);
-    uint32_t *C = cnt + g;
-
-    // window ends [start - 32, start) warm the window; [start, start+128) emit
-    const uint32_t *cw = codes + (start - kWarm) / 16;
-    const uint32_t *vw = valid + (start - kWarm) / 32;
-    Window<K> w;
-    w.init();
-    {
-        const uint32_t v0 = vw[0];
-        const uint32_t c0 = cw[0], c1 = cw[1];
-#pragma unroll
-        for (int b = 0; b < 16; b++) w.push((c0 >> (2 * b)) & 3u, (v0 >> b) & 1u);
-#pragma unroll
-        for (int b = 0; b < 16; b++) w.push((c1 >> (2 * b)) & 3u, (v0 >> (16 + b)) & 1u);
-    }
-    uint32_t cnext = cw[2];
-    uint32_t vcur = vw[1];
-    for (int wi = 0; wi < (int)(kLaneBases / 16); wi++) {
-        const uint32_t c = cnext;
-        const uint32_t vbits = vcur >> ((wi & 1) * 16);
-        if (wi + 1 < (int)(kLaneBases / 16)) {
-            cnext = cw[3 + wi];
-            if (wi & 1) vcur = vw[2 + (wi >> 1)];
-        }
-#pragma unroll
-        for (int b = 0; b < 16; b++) {
-            w.push((c >> (2 * b)) & 3u, (vbits >> b) & 1u);
-            if (w.run >= (uint32_t)K) {
-                const uint64_t h = w.hash(seed);
-                if (__builtin_expect(h <= T, 0)) set_insert(S, mask, C, limit, h);
-            }
-        }
-    }
-}
-
-// ---------------------------------------------- v2: instruction-lean kernel
-// Same contract as k_sketch_hash.  The window is kept as 32-bit words rolled
-// with v_alignbit_b32 (one instruction per word per base), the canonical k-mer
-// is hashed for every window end (no per-k-mer branch; invalid windows are
-// masked in the admit test), rotations are two v_alignbit_b32 and h*5+c is one
-// v_lshl_add_u64.  K = 21 only (3 Murmur words: 16-byte block + 5-byte tail).
+// ------------------------------------------------------------- hash kernel
+// The k-mer window is kept as 32-bit words rolled with v_alignbit_b32 (one
+// instruction per word per base); the canonical k-mer is hashed for every
+// window end (no per-k-mer branch; invalid windows are masked in the admit
+// test); rotations are two v_alignbit_b32 and h*5+c is one v_lshl_add_u64.
+// K = 21 (Mash/dRep default): 3 Murmur words = one 16-byte block + 5-byte tail.
+// Measured (tools/sketch_ab.py, PMC): ~117 VALU instructions per window end,
+// 0.25 wave-instructions/SIMD/cycle; no memory waits in the loop.
 __device__ __forceinline__ uint64_t rotl64_ab(uint64_t x, int r) {
     const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
     uint32_t nlo, nhi;
@@ -197,8 +114,8 @@ struct Window21 {
         r[0] = (r[0] << 8) | ca;
     }
     __device__ __forceinline__ uint64_t hash(uint32_t seed) const {
-        const bool fwd = fc <= rc;
         uint32_t w[6];
+        const bool fwd = fc <= rc;   // memcmp(fwd, rev, K) <= 0
 #pragma unroll
         for (int i = 0; i < 6; i++) w[i] = fwd ? f[i] : r[i];
         return murmur21(((uint64_t)w[1] << 32) | w[0], ((uint64_t)w[3] << 32) | w[2],
@@ -212,18 +129,20 @@ struct Window21 {
 // directly.
 constexpr uint32_t kStage = 1024;
 
-__global__ __launch_bounds__(kSketchWG) void k_sketch_hash21_v2(
+template <int LANE>   // window ends per lane; the workgroup (kTile / LANE lanes) covers one tile
+__global__ __launch_bounds__(kTile / LANE) void k_sketch_hash21(
     const uint32_t *__restrict__ codes, const uint32_t *__restrict__ valid,
     const uint64_t *__restrict__ tile_base, const uint32_t *__restrict__ tile_genome,
     const uint64_t *__restrict__ thr, unsigned long long *__restrict__ sets,
     uint32_t *__restrict__ cnt, uint32_t set_log2, uint32_t limit, uint32_t seed) {
     constexpr int K = 21;
+    constexpr uint32_t WG = kTile / LANE;
     __shared__ uint64_t stage[kStage];
     __shared__ uint32_t nstage;
     const uint32_t t = blockIdx.x;
     const uint32_t g = tile_genome[t];
     const uint64_t T = thr[g];
-    const uint64_t start = tile_base[t] + (uint64_t)threadIdx.x * kLaneBases;
+    const uint64_t start = tile_base[t] + (uint64_t)threadIdx.x * LANE;
     const uint32_t mask = (1u << set_log2) - 1;
     unsigned long long *S = sets + ((uint64_t)g << set_log2);
     uint32_t *C = cnt + g;
@@ -243,10 +162,10 @@ __global__ __launch_bounds__(kSketchWG) void k_sketch_hash21_v2(
     __syncthreads();
     uint32_t cnext = cw[2];
     uint32_t vcur = vw[1];
-    for (int wi = 0; wi < (int)(kLaneBases / 16); wi++) {
+    for (int wi = 0; wi < (int)(LANE / 16); wi++) {
         const uint32_t c = cnext;
         const uint32_t vbits = vcur >> ((wi & 1) * 16);
-        if (wi + 1 < (int)(kLaneBases / 16)) {
+        if (wi + 1 < (int)(LANE / 16)) {
             cnext = cw[3 + wi];
             if (wi & 1) vcur = vw[2 + (wi >> 1)];
         }
@@ -263,7 +182,7 @@ __global__ __launch_bounds__(kSketchWG) void k_sketch_hash21_v2(
     }
     __syncthreads();
     const uint32_t n = min(nstage, kStage);
-    for (uint32_t i = threadIdx.x; i < n; i += kSketchWG) set_insert(S, mask, C, limit, stage[i]);
+    for (uint32_t i = threadIdx.x; i < n; i += WG) set_insert(S, mask, C, limit, stage[i]);
 }
 
 // ----------------------------------------------------------------- finalize
@@ -382,14 +301,6 @@ static SketchPlan plan_for(uint32_t s) {
     return p;
 }
 
-template <int K>
-static void launch_hash(uint32_t ntiles, hipStream_t st, const uint32_t *codes, const uint32_t *valid,
-                        const uint64_t *tb, const uint32_t *tg, const uint64_t *thr,
-                        unsigned long long *sets, uint32_t *cnt, uint32_t sl, uint32_t limit, uint32_t seed) {
-    hipLaunchKernelGGL(k_sketch_hash<K>, dim3(ntiles), dim3(kSketchWG), 0, st, codes, valid, tb, tg,
-                       thr, sets, cnt, sl, limit, seed);
-}
-
 int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t *d_valid,
                        const uint64_t *base_off, const uint64_t *padded, const uint64_t *nkmers,
                        uint32_t n, uint64_t *d_hashes, uint32_t *d_nhash, hipStream_t st) {
@@ -468,13 +379,9 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
         }
         if (nt > 0) {
             timing_mark(ctx, 0, st, true);
-            if (ctx->sketch_variant == 1)
-                launch_hash<21>(nt, st, d_codes, d_valid, tb_tiles_b, tb_tiles_g, d_thr, d_sets, d_cnt,
-                                plan.set_log2, limit, ctx->seed);
-            else
-                hipLaunchKernelGGL(k_sketch_hash21_v2, dim3(nt), dim3(kSketchWG), 0, st, d_codes, d_valid,
-                                   tb_tiles_b, tb_tiles_g, d_thr, d_sets, d_cnt, plan.set_log2, limit,
-                                   ctx->seed);
+            hipLaunchKernelGGL((k_sketch_hash21<kLaneBases>), dim3(nt), dim3(kTile / kLaneBases), 0, st,
+                               d_codes, d_valid, tb_tiles_b, tb_tiles_g, d_thr, d_sets, d_cnt, plan.set_log2,
+                               limit, ctx->seed);
             timing_mark(ctx, 0, st, false);
         }
         timing_mark(ctx, 1, st, true);
@@ -489,6 +396,13 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
         HIPC(hipMemcpyAsync(status.data(), d_st, n, hipMemcpyDeviceToHost, st));
         HIPC(hipStreamSynchronize(st));
         first = false;
+        if (getenv("DREPHIP_DEBUG")) {
+            uint32_t nu = 0, nd = 0;
+            for (uint32_t g : todo) { nu += status[g] == ST_UP; nd += status[g] == ST_DOWN; }
+            fprintf(stderr, "[drephip] sketch round %d: %zu genomes, %u up, %u down\n", round, todo.size(), nu, nd);
+            for (uint32_t g : todo) if (status[g] != ST_OK && nu + nd <= 8)
+                fprintf(stderr, "[drephip]   genome %u status %d T=%llu\n", g, status[g], (unsigned long long)T[g]);
+        }
         std::vector<uint32_t> next;
         for (uint32_t g : todo) {
             if (status[g] == ST_OK) continue;

@@ -1,0 +1,91 @@
+"""Multi-GPU sharding of the Mash step: one process per GPU (torchrun).
+
+The reference runs everything in one process (mash dist -p threads,
+d_cluster.py:570); it has no distributed code.  On a node of MI355X the step
+splits as:
+
+* sketch: genome shards (contiguous, equal count) -- each rank sketches its
+  own genomes;
+* exchange: ONE collective, an all-gather of the uint64[N/W][s] sketch shards
+  and their nhash counts (RCCL over xGMI with the "nccl" backend; gloo on CPU
+  in the tests);
+* all-pairs: contiguous row ranges of the upper triangle balanced by pair
+  count; each rank writes one contiguous segment of the condensed output, so
+  the result needs no collective (segments are concatenated on the host).
+"""
+from __future__ import annotations
+
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+
+def genome_shard(N: int, world: int, rank: int) -> Tuple[int, int, int]:
+    """(g0, g1, nmax): rank's contiguous genome range and the padded shard size
+    every rank uses so the all-gather chunks are equal."""
+    nmax = (N + world - 1) // world
+    g0 = min(N, rank * nmax)
+    g1 = min(N, g0 + nmax)
+    return g0, g1, nmax
+
+
+def cond_start(i: int, N: int) -> int:
+    """Condensed index of pair (i, i+1) (scipy squareform order)."""
+    return i * N - i * (i + 1) // 2
+
+
+def row_partition(N: int, world: int) -> List[Tuple[int, int]]:
+    """Contiguous row ranges [r0, r1) of the upper triangle with near-equal
+    pair counts (row i has N-1-i pairs)."""
+    pairs = np.arange(N - 1, -1, -1, dtype=np.float64)
+    cum = np.concatenate([[0.0], np.cumsum(pairs)])
+    total = cum[-1]
+    bounds = [0]
+    for r in range(1, world):
+        t = total * r / world
+        i = int(np.searchsorted(cum, t))
+        if i > 0 and abs(cum[i - 1] - t) <= abs(cum[min(i, N)] - t):
+            i -= 1                                   # nearest row boundary
+        bounds.append(i)
+    bounds.append(N)
+    for r in range(1, len(bounds)):
+        bounds[r] = max(bounds[r], bounds[r - 1])
+    return [(bounds[r], bounds[r + 1]) for r in range(world)]
+
+
+def segment_size(N: int, r0: int, r1: int) -> int:
+    """Number of condensed pairs in rows [r0, r1)."""
+    if N < 2 or r0 >= min(r1, N - 1):
+        return 0
+    return cond_start(min(r1, N - 1), N) - cond_start(r0, N)
+
+
+def gather_sketches(local_h, local_n, group=None):
+    """All-gather equal-size sketch shards (torch tensors on the process's
+    device: int64 [nmax, s] viewed as uint64, int32 [nmax]).  Returns the
+    gathered [world*nmax, s] and [world*nmax] tensors; rows >= N are padding."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    all_h = torch.empty((world * local_h.shape[0],) + tuple(local_h.shape[1:]),
+                        dtype=local_h.dtype, device=local_h.device)
+    all_n = torch.empty(world * local_n.shape[0], dtype=local_n.dtype, device=local_n.device)
+    dist.all_gather_into_tensor(all_h, local_h.contiguous(), group=group)
+    dist.all_gather_into_tensor(all_n, local_n.contiguous(), group=group)
+    return all_h, all_n
+
+
+def assemble_condensed(N: int, segments: Sequence[np.ndarray], world: int) -> np.ndarray:
+    """Concatenate per-rank condensed segments (rank order) into the full
+    condensed vector, checking every segment has its expected size."""
+    parts = row_partition(N, world)
+    out = []
+    for (r0, r1), seg in zip(parts, segments):
+        want = segment_size(N, r0, r1)
+        if len(seg) != want:
+            raise ValueError("segment for rows [%d,%d) has %d pairs, expected %d" % (r0, r1, len(seg), want))
+        out.append(np.asarray(seg))
+    full = np.concatenate(out) if out else np.zeros(0, np.uint16)
+    if len(full) != N * (N - 1) // 2:
+        raise ValueError("segments do not cover the triangle")
+    return full

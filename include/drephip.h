@@ -114,7 +114,9 @@ int drephip_sketch_files(drephip_ctx *ctx, const char *const *paths, uint32_t n_
  * h_base_off/h_padded/h_nkmers are host arrays of n_genomes entries
  * (h_nkmers: valid k-mer positions, used only to seed the candidate
  * threshold).  d_hashes: uint64[n_genomes][s]; d_nhash: uint32[n_genomes].
- * stream: a hipStream_t (NULL = the context's stream).  Blocking. */
+ * stream: a hipStream_t; 0 is the HIP null stream (as everywhere in HIP).
+ * Every device-pointer entry point runs on the stream it is given, so it is
+ * ordered after work the caller queued there.  Blocking. */
 int drephip_sketch_device(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t *d_valid,
                           const uint64_t *h_base_off, const uint64_t *h_padded,
                           const uint64_t *h_nkmers, uint32_t n_genomes,

@@ -119,12 +119,13 @@ def test_synth_device_matches_oracle_generator(ctx1000):
     total = tile + n * P
     codes = torch.zeros(total // 16, dtype=torch.int32, device="cuda")
     valid = torch.zeros(total // 32, dtype=torch.int32, device="cuda")
-    ctx1000.synth_device(seed, 0, n, fam, L, codes.data_ptr(), valid.data_ptr())
+    st = torch.cuda.current_stream().cuda_stream    # order after torch's fills
+    ctx1000.synth_device(seed, 0, n, fam, L, codes.data_ptr(), valid.data_ptr(), st)
     hashes = torch.zeros((n, S), dtype=torch.int64, device="cuda")
     nhash = torch.zeros(n, dtype=torch.int32, device="cuda")
     off = np.array([tile + i * P for i in range(n)], np.uint64)
     ctx1000.sketch_device(codes.data_ptr(), valid.data_ptr(), off, np.full(n, P, np.uint64),
-                          np.full(n, L - 20, np.uint64), n, hashes.data_ptr(), nhash.data_ptr())
+                          np.full(n, L - 20, np.uint64), n, hashes.data_ptr(), nhash.data_ptr(), st)
     torch.cuda.synchronize()
     h = hashes.cpu().numpy().view(np.uint64)
     nh = nhash.cpu().numpy().view(np.uint32)
@@ -233,11 +234,13 @@ def test_allpairs_row_segments_and_merge_kernel(family, ctx1000):
         if n <= 0:
             continue
         out = torch.zeros(n, dtype=torch.int16, device="cuda")
-        ctx1000.allpairs_device(dh.data_ptr(), dn.data_ptr(), N, r0, r1, out.data_ptr())
+        ctx1000.allpairs_device(dh.data_ptr(), dn.data_ptr(), N, r0, r1, out.data_ptr(), None,
+                                torch.cuda.current_stream().cuda_stream)
         full[start(r0):start(r0) + n] = out.cpu().numpy().view(np.uint16)
     assert np.array_equal(full, oc)
     out = torch.zeros(N * (N - 1) // 2, dtype=torch.int16, device="cuda")
-    ctx1000.allpairs_device(dh.data_ptr(), dn.data_ptr(), N, 0, N, out.data_ptr(), merge=True)
+    ctx1000.allpairs_device(dh.data_ptr(), dn.data_ptr(), N, 0, N, out.data_ptr(), None,
+                            torch.cuda.current_stream().cuda_stream, merge=True)
     assert np.array_equal(out.cpu().numpy().view(np.uint16), oc)
 
 
@@ -287,3 +290,24 @@ def test_all_vs_all_MASH_dropin_reproduces_reference(golden, tmp_path):
         link = json.load(open(os.path.join(golden, "ref", "linkage_%s.json" % alg)))
         got = [[float(v).hex() for v in row] for row in ret[0]]
         assert got == link["linkage"]
+
+
+def test_device_calls_follow_callers_stream(ctx1000):
+    """Device-pointer calls run on the caller's stream: a synth issued right
+    after torch's (asynchronous) zero-fill of a multi-GB buffer on torch's
+    default stream (handle 0) must not be overwritten by that fill."""
+    import torch
+    n, L = 1200, 5_000_000               # ~2.3 GB packed: the fill outlasts a launch
+    tile = _lib.tile_bases()
+    P = _lib.padded_bases([L])
+    total = tile + n * P
+    st = torch.cuda.current_stream().cuda_stream
+    codes = torch.zeros(total // 16, dtype=torch.int32, device="cuda")
+    valid = torch.zeros(total // 32, dtype=torch.int32, device="cuda")
+    ctx1000.synth_device(1, 0, n, 100, L, codes.data_ptr(), valid.data_ptr(), st)
+    torch.cuda.synchronize()
+    for g in (0, n // 2, n - 1):
+        w0 = (tile + g * P) // 32
+        assert int((valid[w0:w0 + L // 32] != -1).sum()) == 0, g
+    del codes, valid
+    torch.cuda.empty_cache()

@@ -6,10 +6,14 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
+#include <vector>
+#include <algorithm>
 
 #define CHAINS 8
 template <int OP>
-__global__ __launch_bounds__(256) void mb(uint32_t *out, int iters, uint32_t c) {
+__global__ __launch_bounds__(256) void mb(uint32_t *out, int iters, uint32_t c, unsigned long long *cyc) {
+    unsigned long long t0;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0) :: "memory");
     uint32_t a[CHAINS];
     uint64_t b[CHAINS];
     for (int j = 0; j < CHAINS; j++) { a[j] = threadIdx.x * 7 + j; b[j] = ((uint64_t)a[j] << 32) | (a[j] * 3); }
@@ -37,6 +41,9 @@ __global__ __launch_bounds__(256) void mb(uint32_t *out, int iters, uint32_t c) 
     uint32_t s = 0;
     for (int j = 0; j < CHAINS; j++) s += a[j] + (uint32_t)b[j] + (uint32_t)(b[j] >> 32);
     out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+    unsigned long long t1;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1) :: "memory");
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
 static const char *names[] = {"v_xor_b32", "v_mul_lo_u32", "v_mul_hi_u32", "v_mad_u64_u32", "v_lshlrev_b64",
@@ -44,16 +51,22 @@ static const char *names[] = {"v_xor_b32", "v_mul_lo_u32", "v_mul_hi_u32", "v_ma
                               "v_cmp_gt_u64", "v_mov_b32", "v_perm_b32", "v_mul_u32_u24", "v_mad_u32_u24",
                               "v_bitop3_b32"};
 
+static unsigned long long *g_cyc;
+static double g_med_cycles;
 template <int OP>
 static float run(uint32_t *d, int blocks, int iters, hipEvent_t e0, hipEvent_t e1) {
-    hipLaunchKernelGGL(mb<OP>, dim3(blocks), dim3(256), 0, 0, d, 4, 12345u);
+    hipLaunchKernelGGL(mb<OP>, dim3(blocks), dim3(256), 0, 0, d, 4, 12345u, g_cyc);
     (void)hipDeviceSynchronize();
     (void)hipEventRecord(e0, 0);
-    hipLaunchKernelGGL(mb<OP>, dim3(blocks), dim3(256), 0, 0, d, iters, 12345u);
+    hipLaunchKernelGGL(mb<OP>, dim3(blocks), dim3(256), 0, 0, d, iters, 12345u, g_cyc);
     (void)hipEventRecord(e1, 0);
     (void)hipEventSynchronize(e1);
     float ms = 0;
     (void)hipEventElapsedTime(&ms, e0, e1);
+    std::vector<unsigned long long> h(blocks);
+    (void)hipMemcpy(h.data(), g_cyc, blocks * 8, hipMemcpyDeviceToHost);
+    std::sort(h.begin(), h.end());
+    g_med_cycles = (double)h[blocks / 2];
     return ms;
 }
 
@@ -65,25 +78,24 @@ int main() {
     const int iters = 20000;
     uint32_t *d;
     (void)hipMalloc(&d, (size_t)blocks * 256 * 4);
+    (void)hipMalloc(&g_cyc, (size_t)blocks * 8);
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     float ms[16];
-    ms[0] = run<0>(d, blocks, iters, e0, e1);   ms[1] = run<1>(d, blocks, iters, e0, e1);
-    ms[2] = run<2>(d, blocks, iters, e0, e1);   ms[3] = run<3>(d, blocks, iters, e0, e1);
-    ms[4] = run<4>(d, blocks, iters, e0, e1);   ms[5] = run<5>(d, blocks, iters, e0, e1);
-    ms[6] = run<6>(d, blocks, iters, e0, e1);   ms[7] = run<7>(d, blocks, iters, e0, e1);
-    ms[8] = run<8>(d, blocks, iters, e0, e1);   ms[9] = run<9>(d, blocks, iters, e0, e1);
-    ms[10] = run<10>(d, blocks, iters, e0, e1); ms[11] = run<11>(d, blocks, iters, e0, e1);
-    ms[12] = run<12>(d, blocks, iters, e0, e1); ms[13] = run<13>(d, blocks, iters, e0, e1);
-    ms[14] = run<14>(d, blocks, iters, e0, e1); ms[15] = run<15>(d, blocks, iters, e0, e1);
+    double cy[16];
+#define RUN(i) ms[i] = run<i>(d, blocks, iters, e0, e1); cy[i] = g_med_cycles;
+    RUN(0) RUN(1) RUN(2) RUN(3) RUN(4) RUN(5) RUN(6) RUN(7)
+    RUN(8) RUN(9) RUN(10) RUN(11) RUN(12) RUN(13) RUN(14) RUN(15)
     // wave-instructions per SIMD = waves per SIMD (8) * iters * CHAINS
     const double winst = 8.0 * iters * CHAINS;
     printf("{\"cus\": %d, \"clock_mhz\": %d, \"results\": [\n", cus, p.clockRate / 1000);
     for (int i = 0; i < 16; i++) {
         const double ns_per = ms[i] * 1e6 / winst;
-        printf("  {\"inst\": \"%s\", \"ms\": %.3f, \"ns_per_wave_inst_per_simd\": %.4f, \"rel_to_xor\": %.2f}%s\n",
-               names[i], ms[i], ns_per, ms[i] / ms[0], i < 15 ? "," : "");
+        // a block's 4 waves sit on 4 SIMDs; 8 blocks per CU -> 8 waves per SIMD run together
+        const double cyc_per = cy[i] / (8.0 * iters * CHAINS);
+        printf("  {\"inst\": \"%s\", \"ms\": %.3f, \"ns_per_wave_inst_per_simd\": %.4f, \"cycles_per_wave_inst_per_simd\": %.3f, \"rel_to_xor\": %.2f}%s\n",
+               names[i], ms[i], ns_per, cyc_per, ms[i] / ms[0], i < 15 ? "," : "");
     }
     printf("]}\n");
     return 0;
