@@ -32,8 +32,8 @@
 
 namespace drephip {
 
-constexpr int kApWG = 512;                      // 8 waves
-constexpr uint32_t kApCols = 64;                // columns per work item
+constexpr int kApWG = 1024;                     // 16 waves: 4 per SIMD at 1 workgroup/CU
+constexpr uint32_t kApCols = 128;               // columns per work item
 constexpr uint32_t kMaxFam = 6;                 // cuckoo hash families tried per row
 constexpr uint32_t kLdsTables = 128 * 1024;     // LDS bytes for row tables per workgroup
 
@@ -57,10 +57,11 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 // i = 2^B-1 >= nA).  Exact for every key.
 struct QFields { uint32_t o1, o2; };
 __host__ __device__ __forceinline__ QFields qfields(uint32_t fam) {
-    // disjoint field offsets inside the low 44 key bits (bottom-s hashes of
-    // genomes up to ~4 Gbp have uniformly random low 44 bits)
-    const uint32_t o1[6] = {0, 22, 5, 27, 11, 33};
-    const uint32_t o2[6] = {22, 0, 27, 5, 33, 11};
+    // disjoint field offsets inside the low 36 key bits (bottom-s hashes of
+    // any genome below ~2^28 bases have uniformly random low 36 bits).
+    // Family 0 keeps both fields in the low 32 bits (kernel fast path).
+    const uint32_t o1[6] = {0, 16, 3, 19, 6, 22};
+    const uint32_t o2[6] = {16, 0, 19, 3, 22, 6};
     return {o1[fam], o2[fam]};
 }
 
@@ -124,10 +125,115 @@ __global__ __launch_bounds__(256) void k_build_qcuckoo(const uint64_t *__restric
     if (threadIdx.x == 0) { fam_out[r] = 0xFF; atomicAdd(nfail, 1u); }
 }
 
-// R rows (tables in LDS) x kApCols columns per workgroup; each wave walks its
-// columns with the whole column sketch in registers (NCH 64-element chunks,
-// double-buffered: the next column's loads are in flight while this one is
-// processed).
+// One membership test of B element b (this lane) against row table Tr.
+// FAST: family 0 (fields at bits [0,B) and [16,16+B), slots shared by all
+// rows and computed once per chunk); otherwise generic 64-bit field shifts.
+template <bool FAST>
+__device__ __forceinline__ bool q_lookup(const uint64_t *Tr, uint32_t H, uint32_t hm, uint64_t b,
+                                         uint32_t s1, uint32_t s2, uint32_t bm1, uint32_t bm2,
+                                         uint32_t o1, uint32_t o2, uint32_t nA, uint32_t &i) {
+    if (FAST) {
+        const uint64_t e1 = Tr[s1], e2 = Tr[H + s2];
+        const uint32_t bhi = (uint32_t)(b >> 32);
+        const bool m1 = (uint32_t)(e1 >> 32) == bhi && ((uint32_t)e1 & ~hm) == bm1;
+        const bool m2 = (uint32_t)(e2 >> 32) == bhi && ((uint32_t)e2 & ~(hm << 16)) == bm2;
+        i = m1 ? ((uint32_t)e1 & hm) : (((uint32_t)e2 >> 16) & hm);
+        return (m1 || m2) && i < nA;
+    } else {
+        const uint64_t F1 = (uint64_t)hm << o1, F2 = (uint64_t)hm << o2;
+        const uint64_t e1 = Tr[(uint32_t)(b >> o1) & hm];
+        const uint64_t e2 = Tr[H + ((uint32_t)(b >> o2) & hm)];
+        const bool m1 = ((e1 ^ b) & ~F1) == 0;
+        const bool m2 = ((e2 ^ b) & ~F2) == 0;
+        i = m1 ? ((uint32_t)(e1 >> o1) & hm) : ((uint32_t)(e2 >> o2) & hm);
+        return (m1 || m2) && i < nA;
+    }
+}
+
+// The columns of one work item, processed by one wave (double-buffered column
+// sketches in registers; see the header comment for the counting rule).
+template <int R, int NCH, bool FAST>
+__device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ nhash,
+                                           const uint64_t *T, uint32_t TS, uint32_t H, uint32_t hm, uint32_t s,
+                                           uint32_t i0, uint32_t nrows, uint32_t c0, uint32_t cend, uint32_t c_first,
+                                           uint32_t c_step, const uint32_t (&nA)[R], const uint32_t (&o1)[R],
+                                           const uint32_t (&o2)[R], const uint64_t (&alast)[R],
+                                           bool any_partial_row, uint16_t *res_c, uint16_t *res_d) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t lt_mask = (1ull << lane) - 1;
+    const uint32_t nch = (s + 63) / 64;
+    uint64_t cur[NCH], nxt[NCH];
+    uint32_t c = c_first;
+    if (c < cend) {
+        const uint64_t *Bc = hashes + (uint64_t)c * s;
+#pragma unroll
+        for (int k = 0; k < NCH; k++) { const uint32_t j = k * 64 + lane; nxt[k] = (k < (int)nch && j < s) ? Bc[j] : kEmpty; }
+    }
+    for (; c < cend; c += c_step) {
+#pragma unroll
+        for (int k = 0; k < NCH; k++) cur[k] = nxt[k];
+        const uint32_t cn = c + c_step;
+        if (cn < cend) {
+            const uint64_t *Bn = hashes + (uint64_t)cn * s;
+#pragma unroll
+            for (int k = 0; k < NCH; k++) { const uint32_t j = k * 64 + lane; nxt[k] = (k < (int)nch && j < s) ? Bn[j] : kEmpty; }
+        }
+        const uint32_t nB = nhash[c];
+        const bool partial = any_partial_row || nB < s;
+        uint32_t cnt[R], mrun[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) { cnt[r] = 0; mrun[r] = 0; }
+        bool alive = true;
+#pragma unroll
+        for (int k = 0; k < NCH; k++) {
+            if (!alive || k >= (int)nch) continue;                        // wave-uniform
+            const uint64_t b = cur[k];
+            // smallest element of the chunk (lane 0); elements past every
+            // active row's largest hash cannot match -- end of the scan
+            // (readfirstlane returns int: go through uint32_t so the low word
+            // is not sign-extended into the high one)
+            const uint64_t b0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                                (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+            bool more = false;
+#pragma unroll
+            for (int r = 0; r < R; r++)
+                if ((uint32_t)r < nrows && i0 + r < c) more |= b0 <= alast[r];
+            if (b0 == kEmpty || !more) { alive = false; continue; }
+            const uint32_t j = k * 64 + lane;
+            const uint32_t blo = (uint32_t)b;
+            const uint32_t s1 = blo & hm, s2 = (blo >> 16) & hm;
+            const uint32_t bm1 = blo & ~hm, bm2 = blo & ~(hm << 16);
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                if ((uint32_t)r >= nrows || i0 + r >= c) continue;        // wave-uniform
+                uint32_t i;
+                const bool found = q_lookup<FAST>(T + (uint64_t)r * TS, H, hm, b, s1, s2, bm1, bm2, o1[r], o2[r],
+                                                  nA[r], i);
+                const uint64_t m = __ballot(found);
+                // s + matches below this lane (running count + in-chunk prefix)
+                const uint32_t lim = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, s + mrun[r]));
+                cnt[r] += (found && i + j < lim) ? 1u : 0u;
+                mrun[r] += (uint32_t)__popcll(m);
+            }
+        }
+        (void)lt_mask;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            if ((uint32_t)r >= nrows || i0 + r >= c) continue;
+            const uint32_t cc = wave_sum(cnt[r]);
+            uint32_t dd = s;
+            if (partial) {
+                const uint32_t u = nA[r] + nB - mrun[r];      // |A u B|; mrun = |A n B| when partial
+                dd = u < s ? u : s;
+            }
+            if (lane == 0) { res_c[r * kApCols + (c - c0)] = (uint16_t)cc; res_d[r * kApCols + (c - c0)] = (uint16_t)dd; }
+        }
+    }
+}
+
+// R rows (tables in LDS) x kApCols columns per workgroup of kApWG lanes; each
+// wave walks every (kApWG/64)-th column of the item.
 template <int R, int NCH>
 __global__ __launch_bounds__(kApWG) void k_allpairs_q(
     const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ nhash,
@@ -143,91 +249,33 @@ __global__ __launch_bounds__(kApWG) void k_allpairs_q(
     const uint32_t c0 = items[blockIdx.x].y;
     const uint32_t nrows = min((uint32_t)R, row1 - i0);
     const uint32_t cend = min(c0 + kApCols, N);
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t tid = threadIdx.x, wave = tid >> 6;
     for (uint32_t r = 0; r < nrows; r++) {
         const uint4 *src = (const uint4 *)(tabs + (uint64_t)(i0 - row0 + r) * TS);
         uint4 *dst = (uint4 *)(T + (uint64_t)r * TS);
         for (uint32_t i = tid; i < TS / 2; i += kApWG) dst[i] = src[i];
     }
     uint32_t nA[R], o1[R], o2[R];
-    uint64_t alast[R], nF1[R], nF2[R];
-    bool any_partial_row = false;
+    uint64_t alast[R];
+    bool any_partial_row = false, fast = true;
 #pragma unroll
     for (int r = 0; r < R; r++) {
         const bool ok = (uint32_t)r < nrows;
         nA[r] = ok ? nhash[i0 + r] : s;
-        const QFields q = qfields(ok ? fam[i0 - row0 + r] : 0);
+        const uint32_t f = ok ? fam[i0 - row0 + r] : 0;
+        const QFields q = qfields(f);
         o1[r] = q.o1; o2[r] = q.o2;
-        nF1[r] = ~((uint64_t)hm << q.o1);
-        nF2[r] = ~((uint64_t)hm << q.o2);
+        fast &= f == 0;
         alast[r] = (ok && nA[r] >= s) ? hashes[(uint64_t)(i0 + r) * s + s - 1] : kEmpty;
         any_partial_row |= nA[r] < s;
     }
-    const uint64_t lt_mask = (1ull << lane) - 1;
-    const uint32_t nch = (s + 63) / 64;
-
-    uint64_t cur[NCH], nxt[NCH];
-    uint32_t c = c0 + wave;
-    if (c < cend) {
-        const uint64_t *Bc = hashes + (uint64_t)c * s;
-#pragma unroll
-        for (int k = 0; k < NCH; k++) { const uint32_t j = k * 64 + lane; nxt[k] = (k < (int)nch && j < s) ? Bc[j] : kEmpty; }
-    }
     __syncthreads();
-    for (; c < cend; c += kApWG / 64) {
-#pragma unroll
-        for (int k = 0; k < NCH; k++) cur[k] = nxt[k];
-        const uint32_t cn = c + kApWG / 64;
-        if (cn < cend) {
-            const uint64_t *Bn = hashes + (uint64_t)cn * s;
-#pragma unroll
-            for (int k = 0; k < NCH; k++) { const uint32_t j = k * 64 + lane; nxt[k] = (k < (int)nch && j < s) ? Bn[j] : kEmpty; }
-        }
-        const uint32_t nB = nhash[c];
-        const bool partial = any_partial_row || nB < s;
-        uint32_t cnt[R], mrun[R];
-#pragma unroll
-        for (int r = 0; r < R; r++) { cnt[r] = 0; mrun[r] = 0; }
-bool alive = true;
-#pragma unroll
-        for (int k = 0; k < NCH; k++) {
-            if (!alive || k >= (int)nch) continue;      // wave-uniform
-            const uint32_t j = k * 64 + lane;
-            const uint64_t b = cur[k];
-            bool more = false;
-#pragma unroll
-            for (int r = 0; r < R; r++) {
-                if ((uint32_t)r >= nrows || i0 + r >= c) continue;        // wave-uniform
-                const bool in = b <= alast[r] && b != kEmpty;
-                const uint64_t *Tr = T + (uint64_t)r * TS;
-                const uint64_t e1 = Tr[(uint32_t)(b >> o1[r]) & hm];
-                const uint64_t e2 = Tr[H + ((uint32_t)(b >> o2[r]) & hm)];
-                const uint32_t i1 = (uint32_t)(e1 >> o1[r]) & hm;
-                const uint32_t i2 = (uint32_t)(e2 >> o2[r]) & hm;
-                const bool f1 = ((e1 ^ b) & nF1[r]) == 0 && i1 < nA[r];
-                const bool f2 = ((e2 ^ b) & nF2[r]) == 0 && i2 < nA[r];
-                const bool found = in && (f1 || f2);
-                const uint32_t i = f1 ? i1 : i2;
-                const uint64_t m = __ballot(found);
-                const uint32_t mb = mrun[r] + (uint32_t)__popcll(m & lt_mask);
-                cnt[r] += (found && i + j - mb < s) ? 1u : 0u;
-                mrun[r] += (uint32_t)__popcll(m);
-                more |= in;
-            }
-            alive = __ballot(more) != 0;
-        }
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-            if ((uint32_t)r >= nrows || i0 + r >= c) continue;
-            const uint32_t cc = wave_sum(cnt[r]);
-            uint32_t dd = s;
-            if (partial) {
-                const uint32_t u = nA[r] + nB - mrun[r];
-                dd = u < s ? u : s;
-            }
-            if (lane == 0) { res_c[r * kApCols + (c - c0)] = (uint16_t)cc; res_d[r * kApCols + (c - c0)] = (uint16_t)dd; }
-        }
-    }
+    if (fast)
+        ap_columns<R, NCH, true>(hashes, nhash, T, TS, H, hm, s, i0, nrows, c0, cend, c0 + wave, kApWG / 64,
+                                 nA, o1, o2, alast, any_partial_row, res_c, res_d);
+    else
+        ap_columns<R, NCH, false>(hashes, nhash, T, TS, H, hm, s, i0, nrows, c0, cend, c0 + wave, kApWG / 64,
+                                  nA, o1, o2, alast, any_partial_row, res_c, res_d);
     __syncthreads();
     for (uint32_t r = 0; r < nrows; r++) {
         const uint32_t i = i0 + r;

@@ -185,6 +185,123 @@ __global__ __launch_bounds__(kTile / LANE) void k_sketch_hash21(
     for (uint32_t i = threadIdx.x; i < n; i += WG) set_insert(S, mask, C, limit, stage[i]);
 }
 
+// --------------------------------------------------------------- v3 kernel
+// Batches the 16 window ends of one code word: the window rolls serially, the
+// 16 canonical hashes are independent (the compiler interleaves them), and a
+// single admit test per batch replaces 16 per-k-mer branches.  Codes are kept
+// top-aligned (fc: newest base at bits 23:22, older bases fall off bit 63), so
+// no masking is needed: when the top 42 bits of fc and rc are equal the two
+// strings are identical and either choice hashes the same bytes.  Window
+// validity (run of >= 21 valid bases) is evaluated only inside the rare admit
+// branch, from a 64-base validity history.
+struct Window21v3 {
+    uint32_t f[6], r[6];
+    uint64_t fc, rc;
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int i = 0; i < 6; i++) { f[i] = 0; r[i] = 0; }
+        fc = rc = 0;
+    }
+    __device__ __forceinline__ void push(uint32_t c) {
+        fc = (fc << 2) | ((uint64_t)c << 22);
+        rc = (rc >> 2) | ((uint64_t)(c ^ 3u) << 62);
+        const uint32_t sel = c | 0x06050400u;        // byte0 <- LUT[c], bytes1..3 <- src0 bytes 0..2
+#pragma unroll
+        for (int i = 0; i < 5; i++) f[i] = __builtin_amdgcn_alignbit(f[i + 1], f[i], 8);
+        f[5] = __builtin_amdgcn_perm(0u, 0x54474341u, sel);              // ASCII of the new base
+        r[5] = r[4] >> 24;
+#pragma unroll
+        for (int i = 4; i > 0; i--) r[i] = __builtin_amdgcn_alignbit(r[i], r[i - 1], 24);
+        r[0] = __builtin_amdgcn_perm(r[0], 0x41434754u, sel);            // (r0 << 8) | comp ASCII
+    }
+    __device__ __forceinline__ uint64_t hash(uint32_t seed) const {
+        uint32_t w[6];
+        const bool fwd = fc <= rc;
+#pragma unroll
+        for (int i = 0; i < 6; i++) w[i] = fwd ? f[i] : r[i];
+        return murmur21(((uint64_t)w[1] << 32) | w[0], ((uint64_t)w[3] << 32) | w[2],
+                        ((uint64_t)w[5] << 32) | w[4], seed);
+    }
+};
+
+// bit i of the result: the 21 bases ending at history bit i are all valid
+__device__ __forceinline__ uint64_t run21(uint64_t v) {
+    const uint64_t r2 = v & (v << 1);
+    const uint64_t r4 = r2 & (r2 << 2);
+    const uint64_t r8 = r4 & (r4 << 4);
+    const uint64_t r16 = r8 & (r8 << 8);
+    return r16 & (r4 << 16) & (v << 20);
+}
+
+template <int LANE, int BATCH>   // BATCH window ends hashed per admit test (8 or 16)
+__global__ __launch_bounds__(kTile / LANE) void k_sketch_hash21_v3(
+    const uint32_t *__restrict__ codes, const uint32_t *__restrict__ valid,
+    const uint64_t *__restrict__ tile_base, const uint32_t *__restrict__ tile_genome,
+    const uint64_t *__restrict__ thr, unsigned long long *__restrict__ sets,
+    uint32_t *__restrict__ cnt, uint32_t set_log2, uint32_t limit, uint32_t seed) {
+    constexpr uint32_t WG = kTile / LANE;
+    __shared__ uint64_t stage[kStage];
+    __shared__ uint32_t nstage;
+    const uint32_t t = blockIdx.x;
+    const uint32_t g = tile_genome[t];
+    const uint64_t T = thr[g];
+    const uint64_t start = tile_base[t] + (uint64_t)threadIdx.x * LANE;
+    const uint32_t mask = (1u << set_log2) - 1;
+    unsigned long long *S = sets + ((uint64_t)g << set_log2);
+    uint32_t *C = cnt + g;
+    if (threadIdx.x == 0) nstage = 0;
+    const uint32_t *cw = codes + (start - kWarm) / 16;
+    const uint32_t *vw = valid + (start - kWarm) / 32;
+    Window21v3 w;
+    w.init();
+    const uint32_t v0 = vw[0];
+    {
+        const uint32_t c0 = cw[0], c1 = cw[1];
+#pragma unroll
+        for (int b = 0; b < 16; b++) w.push((c0 >> (2 * b)) & 3u);
+#pragma unroll
+        for (int b = 0; b < 16; b++) w.push((c1 >> (2 * b)) & 3u);
+    }
+    uint64_t vhist = (uint64_t)v0 << 32;              // bit 63 = newest base
+    __syncthreads();
+    uint32_t cnext = cw[2];
+    uint32_t vcur = vw[1];
+    for (int wi = 0; wi < (int)(LANE / 16); wi++) {
+        const uint32_t c = cnext;
+        const uint32_t vbits = (vcur >> ((wi & 1) * 16)) & 0xffffu;
+        if (wi + 1 < (int)(LANE / 16)) {
+            cnext = cw[3 + wi];
+            if (wi & 1) vcur = vw[2 + (wi >> 1)];
+        }
+        vhist = (vhist >> 16) | ((uint64_t)vbits << 48);
+#pragma unroll
+        for (int b0 = 0; b0 < 16; b0 += BATCH) {
+            uint64_t h[BATCH];
+            bool hit = false;
+#pragma unroll
+            for (int b = 0; b < BATCH; b++) {
+                w.push((c >> (2 * (b0 + b))) & 3u);
+                h[b] = w.hash(seed);
+                hit |= h[b] <= T;
+            }
+            if (__builtin_expect(hit, 0)) {
+                const uint64_t ok = run21(vhist);
+#pragma unroll
+                for (int b = 0; b < BATCH; b++) {
+                    if (h[b] <= T && ((ok >> (48 + b0 + b)) & 1)) {
+                        const uint32_t slot = atomicAdd(&nstage, 1u);
+                        if (slot < kStage) stage[slot] = h[b];
+                        else set_insert(S, mask, C, limit, h[b]);
+                    }
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t n = min(nstage, kStage);
+    for (uint32_t i = threadIdx.x; i < n; i += WG) set_insert(S, mask, C, limit, stage[i]);
+}
+
 // ----------------------------------------------------------------- finalize
 enum : uint8_t { ST_OK = 0, ST_UP = 1, ST_DOWN = 2 };
 
@@ -379,9 +496,14 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
         }
         if (nt > 0) {
             timing_mark(ctx, 0, st, true);
-            hipLaunchKernelGGL((k_sketch_hash21<kLaneBases>), dim3(nt), dim3(kTile / kLaneBases), 0, st,
-                               d_codes, d_valid, tb_tiles_b, tb_tiles_g, d_thr, d_sets, d_cnt, plan.set_log2,
-                               limit, ctx->seed);
+            if (ctx->sketch_kernel == 2)
+                hipLaunchKernelGGL((k_sketch_hash21<kLaneBases>), dim3(nt), dim3(kTile / kLaneBases), 0, st,
+                                   d_codes, d_valid, tb_tiles_b, tb_tiles_g, d_thr, d_sets, d_cnt, plan.set_log2,
+                                   limit, ctx->seed);
+            else
+                hipLaunchKernelGGL((k_sketch_hash21_v3<kLaneBases, 8>), dim3(nt), dim3(kTile / kLaneBases), 0, st,
+                                   d_codes, d_valid, tb_tiles_b, tb_tiles_g, d_thr, d_sets, d_cnt, plan.set_log2,
+                                   limit, ctx->seed);
             timing_mark(ctx, 0, st, false);
         }
         timing_mark(ctx, 1, st, true);

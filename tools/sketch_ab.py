@@ -13,10 +13,10 @@ from drep_amd import _lib
 N = int(os.environ.get("AB_GENOMES", 200))
 L = 5_000_000
 rounds = int(os.environ.get("AB_ROUNDS", 5))
-variants = [int(v) for v in os.environ.get("AB_VARIANTS", "0").split(",")]
+variants = [int(v) for v in os.environ.get("AB_VARIANTS", "3,2").split(",")]
 ctxs = {}
 for v in variants:
-    os.environ["DREPHIP_SKETCH_VARIANT"] = str(v)
+    os.environ["DREPHIP_SKETCH_KERNEL"] = str(v)
     ctxs[v] = _lib.Context(0, 21, 1000, 42)
     ctxs[v].set_timing(True)
 tile = _lib.tile_bases()
