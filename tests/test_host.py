@@ -189,3 +189,57 @@ def test_load_genomes(tmp_path):
     lst.write_text("%s\n%s\n" % (a, b))
     Bdb2 = d_cluster.load_genomes([str(lst)])
     assert list(Bdb2["location"]) == [str(a), str(b)]
+
+
+def _np_pack(recs, tile):
+    """numpy restatement of the packed layout (include/drephip.h) for one genome."""
+    span = sum(len(r) for r in recs) + max(len(recs) - 1, 0)
+    P = ((span + 1 + tile - 1) // tile) * tile
+    bases = np.full(P, 255, np.uint8)
+    pos = 0
+    for i, r in enumerate(recs):
+        bases[pos:pos + len(r)] = r
+        pos += len(r) + 1
+    lut = np.full(256, 4, np.uint8)
+    for ch, c in zip(b"ACGTacgt", [0, 1, 2, 3, 0, 1, 2, 3]):
+        lut[ch] = c
+    code = lut[bases]
+    ok = code < 4
+    c2 = np.where(ok, code, 0).astype(np.uint32).reshape(-1, 16)
+    codes = (c2 << (2 * np.arange(16, dtype=np.uint32))).sum(axis=1, dtype=np.uint64).astype(np.uint32)
+    v = ok.astype(np.uint32).reshape(-1, 32)
+    valid = (v << np.arange(32, dtype=np.uint32)).sum(axis=1, dtype=np.uint64).astype(np.uint32)
+    return P, codes, valid
+
+
+def test_fasta_pack_matches_numpy_layout(tmp_path, golden):
+    """Host packer (drephip_fasta_pack) == numpy restatement of the layout, on
+    a real multi-record genome with N runs and on a synthetic edge case file."""
+    import ctypes as C
+    import glob
+    rng = np.random.default_rng(2)
+    A = np.frombuffer(b"ACGTacgtNRY", dtype=np.uint8)
+    recs = [A[rng.integers(0, len(A), n)] for n in (1, 31, 32, 33, 5000, 0, 70000)]
+    txt = b"".join(b">r%d\n" % i + b"\n".join(bytes(r[j:j + 61]) for j in range(0, len(r), 61)) + b"\n"
+                   for i, r in enumerate(recs))
+    p = tmp_path / "e.fa"
+    p.write_bytes(txt)
+    fas = [str(p)] + sorted(glob.glob(os.path.join(golden, "genomes", "*.gz")))[1:2]
+    tile = _lib.tile_bases()
+    L = _lib.lib()
+    for fa in fas:
+        seq, off, ln = oracle.read_fasta(fa)
+        recs_o = [seq[off[i]:off[i + 1]] for i in range(len(off) - 1)]
+        if fa == str(p):   # oracle upper-cases; the packer accepts either case
+            recs_o = [np.array(r) for r in recs]
+        P, want_c, want_v = _np_pack(recs_o, tile)
+        codes = np.zeros((tile + P) // 16, np.uint32)
+        valid = np.zeros((tile + P) // 32, np.uint32)
+        length = C.c_uint64(0)
+        nk = C.c_uint64(0)
+        rc = L.drephip_fasta_pack(fa.encode(), 21, codes, valid, tile, tile + P, C.byref(length), C.byref(nk))
+        assert rc == 0
+        assert np.array_equal(codes[tile // 16:], want_c)
+        assert np.array_equal(valid[tile // 32:], want_v)
+        assert not codes[:tile // 16].any() and not valid[:tile // 32].any()
+        assert length.value == sum(len(r) for r in recs_o)
