@@ -26,6 +26,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+VALU_PEAK_TINST = 256 * 4 * 16 * 2.4e9 / 1e12   # full-rate VALU lane-instructions/s (MI355X_MICROARCH.md: 256 CU, 2.4 GHz)
+SKETCH_DEFAULT_VARIANT = "4"   # must match drephip_ctx::sketch_kernel default (ctx.h)
 
 
 def parse():
@@ -189,6 +191,20 @@ def main():
         except Exception:
             traffic = None
     kmers_per_s = nloc * (L - 20) / avg_launch_s if avg_launch_s > 0 else 0.0
+    valu = {"kmers_per_s": kmers_per_s}
+    isa_path = os.path.join(ROOT, "profiles", "sketch_isa.json")
+    variant = os.environ.get("DREPHIP_SKETCH_KERNEL", SKETCH_DEFAULT_VARIANT)
+    if os.path.exists(isa_path):
+        isa = json.load(open(isa_path))["variants"].get(variant)
+        if isa:
+            # lane-instructions issued per second vs the full-rate VALU issue peak
+            # (256 CU x 4 SIMD x 16 lanes x 2.4 GHz); 64-bit multiply-class ops
+            # issue slower than full rate, so frac < 1 at saturation
+            ach = kmers_per_s * isa["valu_per_kmer"] / 1e12
+            valu.update({"kernel": isa["kernel"], "valu_per_kmer": isa["valu_per_kmer"],
+                         "mul_per_kmer": isa["mul_per_kmer"], "achieved": ach,
+                         "peak": VALU_PEAK_TINST, "unit": "T lane-inst/s", "frac": ach / VALU_PEAK_TINST,
+                         "source": "profiles/sketch_isa.json (tools/isa_count.py)"})
 
     # ---- output segment D2H (PCIe-inclusive leg; not part of `value`)
     torch.cuda.synchronize()
@@ -241,7 +257,7 @@ def main():
                              "build": kms[3][1]},
             },
             "roofline": {
-                "kernel": "k_sketch_hash<21>",
+                "kernel": valu.get("kernel", "k_sketch_hash21"),
                 "bound": "hbm",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBPS,
@@ -251,7 +267,7 @@ def main():
                 "note": "algorithmic bytes = 0.375 B/base (2-bit code + validity bit) x bases per "
                         "launch; the binding limit is integer VALU (Murmur3 64-bit multiplies), "
                         "see valu_model",
-                "valu_model": {"kmers_per_s": kmers_per_s},
+                "valu_model": valu,
             },
             "cpu_baseline": cpu,
         }

@@ -33,6 +33,9 @@
 namespace drephip {
 
 constexpr int kApWG = 1024;                     // 16 waves: 4 per SIMD at 1 workgroup/CU
+// 32 chunks (s > 1024) double-buffered take 128 VGPRs of sketch alone: half the
+// waves, twice the registers
+__host__ __device__ constexpr int ap_wg(int nch) { return nch > 16 ? kApWG / 2 : kApWG; }
 constexpr uint32_t kApCols = 128;               // columns per work item
 constexpr uint32_t kMaxFam = 6;                 // cuckoo hash families tried per row
 constexpr uint32_t kLdsTables = 128 * 1024;     // LDS bytes for row tables per workgroup
@@ -125,29 +128,36 @@ __global__ __launch_bounds__(256) void k_build_qcuckoo(const uint64_t *__restric
     if (threadIdx.x == 0) { fam_out[r] = 0xFF; atomicAdd(nfail, 1u); }
 }
 
-// One membership test of B element b (this lane) against row table Tr.
-// FAST: family 0 (fields at bits [0,B) and [16,16+B), slots shared by all
-// rows and computed once per chunk); otherwise generic 64-bit field shifts.
+// Membership test of B element b (this lane) against a row table, from the
+// two slot words e1 = Tr[s1], e2 = Tr[H + s2] (read beforehand for every row
+// of the chunk so the 2R LDS reads are in flight together).  Branch-free: the
+// match tests are integer xor/or, i is one select.
+// FAST: family 0 (fields at bits [0,B) and [16,16+B)); otherwise generic
+// 64-bit field shifts.
 template <bool FAST>
-__device__ __forceinline__ bool q_lookup(const uint64_t *Tr, uint32_t H, uint32_t hm, uint64_t b,
-                                         uint32_t s1, uint32_t s2, uint32_t bm1, uint32_t bm2,
-                                         uint32_t o1, uint32_t o2, uint32_t nA, uint32_t &i) {
+__device__ __forceinline__ bool q_match(uint64_t e1, uint64_t e2, uint32_t hm, uint64_t b, uint32_t o1,
+                                        uint32_t o2, uint32_t nA, uint32_t &i) {
+    // x = residual of the non-field bits (0 iff the slot holds b); a slot's
+    // candidate position is pushed past any nA when x != 0:
+    //   i_k = field_k + min(x_k, 1) << 16,   i = min(i_1, i_2),   found = i < nA
+    // (at most one slot holds b; the empty word decodes to 2^B - 1 >= nA)
+    uint32_t x1, x2, f1, f2;
     if (FAST) {
-        const uint64_t e1 = Tr[s1], e2 = Tr[H + s2];
-        const uint32_t bhi = (uint32_t)(b >> 32);
-        const bool m1 = (uint32_t)(e1 >> 32) == bhi && ((uint32_t)e1 & ~hm) == bm1;
-        const bool m2 = (uint32_t)(e2 >> 32) == bhi && ((uint32_t)e2 & ~(hm << 16)) == bm2;
-        i = m1 ? ((uint32_t)e1 & hm) : (((uint32_t)e2 >> 16) & hm);
-        return (m1 || m2) && i < nA;
+        const uint32_t bhi = (uint32_t)(b >> 32), blo = (uint32_t)b;
+        x1 = ((uint32_t)(e1 >> 32) ^ bhi) | (((uint32_t)e1 ^ blo) & ~hm);
+        x2 = ((uint32_t)(e2 >> 32) ^ bhi) | (((uint32_t)e2 ^ blo) & ~(hm << 16));
+        f1 = (uint32_t)e1 & hm;
+        f2 = ((uint32_t)e2 >> 16) & hm;
     } else {
         const uint64_t F1 = (uint64_t)hm << o1, F2 = (uint64_t)hm << o2;
-        const uint64_t e1 = Tr[(uint32_t)(b >> o1) & hm];
-        const uint64_t e2 = Tr[H + ((uint32_t)(b >> o2) & hm)];
-        const bool m1 = ((e1 ^ b) & ~F1) == 0;
-        const bool m2 = ((e2 ^ b) & ~F2) == 0;
-        i = m1 ? ((uint32_t)(e1 >> o1) & hm) : ((uint32_t)(e2 >> o2) & hm);
-        return (m1 || m2) && i < nA;
+        const uint64_t y1 = (e1 ^ b) & ~F1, y2 = (e2 ^ b) & ~F2;
+        x1 = (uint32_t)y1 | (uint32_t)(y1 >> 32);
+        x2 = (uint32_t)y2 | (uint32_t)(y2 >> 32);
+        f1 = (uint32_t)(e1 >> o1) & hm;
+        f2 = (uint32_t)(e2 >> o2) & hm;
     }
+    i = min(f1 + (min(x1, 1u) << 16), f2 + (min(x2, 1u) << 16));
+    return i < nA;
 }
 
 // The columns of one work item, processed by one wave (double-buffered column
@@ -160,10 +170,9 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
                                            const uint32_t (&o2)[R], const uint64_t (&alast)[R],
                                            bool any_partial_row, uint16_t *res_c, uint16_t *res_d) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t lt_mask = (1ull << lane) - 1;
     const uint32_t nch = (s + 63) / 64;
     uint64_t cur[NCH], nxt[NCH];
-    uint32_t c = c_first;
+    uint32_t c = __builtin_amdgcn_readfirstlane(c_first);        // wave-uniform: scalar column loop
     if (c < cend) {
         const uint64_t *Bc = hashes + (uint64_t)c * s;
 #pragma unroll
@@ -201,23 +210,39 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
             if (b0 == kEmpty || !more) { alive = false; continue; }
             const uint32_t j = k * 64 + lane;
             const uint32_t blo = (uint32_t)b;
-            const uint32_t s1 = blo & hm, s2 = (blo >> 16) & hm;
-            const uint32_t bm1 = blo & ~hm, bm2 = blo & ~(hm << 16);
+            constexpr int G = R < 4 ? R : 4;                                 // rows per read group
 #pragma unroll
-            for (int r = 0; r < R; r++) {
-                if ((uint32_t)r >= nrows || i0 + r >= c) continue;        // wave-uniform
-                uint32_t i;
-                const bool found = q_lookup<FAST>(T + (uint64_t)r * TS, H, hm, b, s1, s2, bm1, bm2, o1[r], o2[r],
-                                                  nA[r], i);
-                const uint64_t m = __ballot(found);
-                // s + matches below this lane (running count + in-chunk prefix)
-                const uint32_t lim = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, s + mrun[r]));
-                cnt[r] += (found && i + j < lim) ? 1u : 0u;
-                mrun[r] += (uint32_t)__popcll(m);
+            for (int r0 = 0; r0 < R; r0 += G) {
+                uint64_t e1[G], e2[G];
+#pragma unroll
+                for (int g = 0; g < G; g++) {
+                    const int r = r0 + g;
+                    if ((uint32_t)r >= nrows || i0 + r >= c) continue;    // wave-uniform
+                    const uint64_t *Tr = T + (uint64_t)r * TS;
+                    if (FAST) {
+                        e1[g] = Tr[blo & hm];
+                        e2[g] = Tr[H + ((blo >> 16) & hm)];
+                    } else {
+                        e1[g] = Tr[(uint32_t)(b >> o1[r]) & hm];
+                        e2[g] = Tr[H + ((uint32_t)(b >> o2[r]) & hm)];
+                    }
+                    asm volatile("" ::"v"(e1[g]), "v"(e2[g]));            // all reads issued before any test
+                }
+#pragma unroll
+                for (int g = 0; g < G; g++) {
+                    const int r = r0 + g;
+                    if ((uint32_t)r >= nrows || i0 + r >= c) continue;    // wave-uniform
+                    uint32_t i;
+                    const bool found = q_match<FAST>(e1[g], e2[g], hm, b, o1[r], o2[r], nA[r], i);
+                    const uint64_t m = __ballot(found);
+                    // s + matches below this lane (running count + in-chunk prefix)
+                    const uint32_t lim = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, s + mrun[r]));
+                    cnt[r] += (uint32_t)found & (uint32_t)(i + j < lim);
+                    mrun[r] += (uint32_t)__popcll(m);
+                }
             }
         }
-        (void)lt_mask;
 #pragma unroll
         for (int r = 0; r < R; r++) {
             if ((uint32_t)r >= nrows || i0 + r >= c) continue;
@@ -232,14 +257,15 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
     }
 }
 
-// R rows (tables in LDS) x kApCols columns per workgroup of kApWG lanes; each
-// wave walks every (kApWG/64)-th column of the item.
+// R rows (tables in LDS) x kApCols columns per workgroup of ap_wg(NCH) lanes; each
+// wave walks every (WG/64)-th column of the item.
 template <int R, int NCH>
-__global__ __launch_bounds__(kApWG) void k_allpairs_q(
+__global__ __launch_bounds__(ap_wg(NCH)) void k_allpairs_q(
     const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ nhash,
     const uint64_t *__restrict__ tabs, const uint8_t *__restrict__ fam, uint32_t s, uint32_t N,
     uint32_t row0, uint32_t row1, uint32_t B, const uint2 *__restrict__ items,
     uint16_t *__restrict__ common, uint16_t *__restrict__ denom, uint64_t seg0) {
+    constexpr int WG = ap_wg(NCH);
     extern __shared__ uint64_t lds[];
     const uint32_t H = 1u << B, hm = H - 1, TS = 2 * H;
     uint64_t *T = lds;
@@ -253,7 +279,7 @@ __global__ __launch_bounds__(kApWG) void k_allpairs_q(
     for (uint32_t r = 0; r < nrows; r++) {
         const uint4 *src = (const uint4 *)(tabs + (uint64_t)(i0 - row0 + r) * TS);
         uint4 *dst = (uint4 *)(T + (uint64_t)r * TS);
-        for (uint32_t i = tid; i < TS / 2; i += kApWG) dst[i] = src[i];
+        for (uint32_t i = tid; i < TS / 2; i += WG) dst[i] = src[i];
     }
     uint32_t nA[R], o1[R], o2[R];
     uint64_t alast[R];
@@ -271,10 +297,10 @@ __global__ __launch_bounds__(kApWG) void k_allpairs_q(
     }
     __syncthreads();
     if (fast)
-        ap_columns<R, NCH, true>(hashes, nhash, T, TS, H, hm, s, i0, nrows, c0, cend, c0 + wave, kApWG / 64,
+        ap_columns<R, NCH, true>(hashes, nhash, T, TS, H, hm, s, i0, nrows, c0, cend, c0 + wave, WG / 64,
                                  nA, o1, o2, alast, any_partial_row, res_c, res_d);
     else
-        ap_columns<R, NCH, false>(hashes, nhash, T, TS, H, hm, s, i0, nrows, c0, cend, c0 + wave, kApWG / 64,
+        ap_columns<R, NCH, false>(hashes, nhash, T, TS, H, hm, s, i0, nrows, c0, cend, c0 + wave, WG / 64,
                                   nA, o1, o2, alast, any_partial_row, res_c, res_d);
     __syncthreads();
     for (uint32_t r = 0; r < nrows; r++) {
@@ -282,7 +308,7 @@ __global__ __launch_bounds__(kApWG) void k_allpairs_q(
         const uint32_t cs = max(c0, i + 1);
         if (cs >= cend) continue;
         const uint64_t base = cond_index(i, cs, N) - seg0;
-        for (uint32_t t = tid; t < cend - cs; t += kApWG) {
+        for (uint32_t t = tid; t < cend - cs; t += WG) {
             common[base + t] = res_c[r * kApCols + (cs - c0) + t];
             if (denom) denom[base + t] = res_d[r * kApCols + (cs - c0) + t];
         }
@@ -344,7 +370,7 @@ static int launch_q(drephip_ctx *ctx, uint32_t nitems, size_t lds, hipStream_t s
     HIPC(hipFuncSetAttribute((const void *)k_allpairs_q<R, NCH>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)lds));
     timing_mark(ctx, 2, st, true);
-    hipLaunchKernelGGL((k_allpairs_q<R, NCH>), dim3(nitems), dim3(kApWG), lds, st, h, nh, tabs, fam, ctx->s, N,
+    hipLaunchKernelGGL((k_allpairs_q<R, NCH>), dim3(nitems), dim3(ap_wg(NCH)), lds, st, h, nh, tabs, fam, ctx->s, N,
                        row0, row1, B, items, cm, dn, seg0);
     timing_mark(ctx, 2, st, false);
     HIPC(hipGetLastError());

@@ -20,7 +20,7 @@ struct drephip_ctx {
     uint32_t seed = 42;
     hipStream_t stream = nullptr;
     bool timing = false;
-    int sketch_kernel = 3;    // 3 = batched v3 (default), 2 = per-k-mer v2; env DREPHIP_SKETCH_KERNEL (A/B)
+    int sketch_kernel = 4;    // 4 = table-driven v4 (default), 3 = rolled-window v3; env DREPHIP_SKETCH_KERNEL (A/B)
     // named grow-only device scratch buffers
     std::map<std::string, DevBuf> bufs;
     // per-kernel timing of the last call: {sum ms, launches}

@@ -2,15 +2,16 @@
 // genome (drep/d_cluster.py:531-549) and `mash paste` (551-567).
 //
 // Three kernels, one pass over the packed genome set per round:
-//   k_sketch_hash21   one workgroup per 32768-base tile; each lane rolls a
-//                     k-mer window over 128 window ends (2-bit codes +
-//                     validity from HBM, one load per 16 bases), keeps
-//                     forward/reverse-complement ASCII windows in registers,
-//                     hashes the canonical k-mer with MurmurHash3_x64_128 and
-//                     admits it only if h <= T[g] (per-genome candidate
-//                     threshold).  Admitted hashes are staged in LDS and, after
-//                     the tile, inserted into a per-genome open-addressing set
-//                     in HBM (64-bit CAS), so duplicates drop out at insert.
+//   k_sketch_hash21_v4  one workgroup per 32768-base tile; each lane covers 128
+//                     window ends (2-bit codes + validity from HBM, one load
+//                     per 16 bases), cuts the forward and reverse-complement
+//                     k-mers out of the code stream, hashes the canonical one
+//                     with MurmurHash3_x64_128 (seed 42, h1) using per-workgroup
+//                     LDS tables for the base-local parts, and admits it only if
+//                     h <= T[g] (per-genome candidate threshold).  Admitted
+//                     hashes are staged in LDS and, after the tile, inserted
+//                     into a per-genome open-addressing set in HBM (64-bit CAS),
+//                     so duplicates drop out at insert.
 //   k_sketch_finalize one workgroup per genome: compacts the set into LDS,
 //                     bitonic-sorts it and writes the s smallest.
 //   k_synth           bench input generator (not on the product path).
@@ -19,9 +20,9 @@
 // low) or more than the LDS sort holds (T too high) is re-run with a bisected
 // T -- exact for every input, normally a single round.
 //
-// Roofline: integer VALU (≈40 quarter-rate 32-bit multiplies per k-mer for the
-// two 64-bit Murmur mixes); HBM traffic is 3 bits/base (0.375 B/base) plus the
-// candidate sets.
+// Roofline: integer VALU issue (v4: ~76 VALU instructions per k-mer, 18 of
+// them multiply-class, tools/isa_count.py); HBM traffic is 3 bits/base
+// (0.375 B/base) plus the candidate sets.
 
 #include "ctx.h"
 #include "../../include/drephip.h"
@@ -46,14 +47,9 @@ __device__ __forceinline__ void set_insert(unsigned long long *S, uint32_t mask,
     }
 }
 
-// ------------------------------------------------------------- hash kernel
-// The k-mer window is kept as 32-bit words rolled with v_alignbit_b32 (one
-// instruction per word per base); the canonical k-mer is hashed for every
-// window end (no per-k-mer branch; invalid windows are masked in the admit
-// test); rotations are two v_alignbit_b32 and h*5+c is one v_lshl_add_u64.
+// ------------------------------------------------------------- Murmur parts
 // K = 21 (Mash/dRep default): 3 Murmur words = one 16-byte block + 5-byte tail.
-// Measured (tools/sketch_ab.py, PMC): ~117 VALU instructions per window end,
-// 0.25 wave-instructions/SIMD/cycle; no memory waits in the loop.
+// Rotations are two v_alignbit_b32 and h*5+c is one v_lshl_add_u64.
 __device__ __forceinline__ uint64_t rotl64_ab(uint64_t x, int r) {
     const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
     uint32_t nlo, nhi;
@@ -89,104 +85,16 @@ __device__ __forceinline__ uint64_t murmur21(uint64_t k1, uint64_t k2, uint64_t 
     return fmix64_v(h1) + fmix64_v(h2);
 }
 
-struct Window21 {
-    uint32_t f[6];      // forward ASCII, bytes 0..20 (word 5 holds byte 20)
-    uint32_t r[6];      // reverse-complement ASCII
-    uint64_t fc, rc;    // 2-bit codes, first character most significant
-    uint32_t run;
-    __device__ __forceinline__ void init() {
-#pragma unroll
-        for (int i = 0; i < 6; i++) { f[i] = 0; r[i] = 0; }
-        fc = rc = 0; run = 0;
-    }
-    __device__ __forceinline__ void push(uint32_t c, uint32_t v) {
-        run = v ? run + 1 : 0;
-        fc = ((fc << 2) | c) & ((1ull << 42) - 1);
-        rc = (rc >> 2) | ((uint64_t)(3u - c) << 40);
-        const uint32_t a = __builtin_amdgcn_perm(0u, 0x54474341u, c | 0x0c0c0c00u);   // A C G T
-        const uint32_t ca = __builtin_amdgcn_perm(0u, 0x41434754u, c | 0x0c0c0c00u);  // T G C A
-#pragma unroll
-        for (int i = 0; i < 5; i++) f[i] = __builtin_amdgcn_alignbit(f[i + 1], f[i], 8);
-        f[5] = a;
-        r[5] = r[4] >> 24;
-#pragma unroll
-        for (int i = 4; i > 0; i--) r[i] = __builtin_amdgcn_alignbit(r[i], r[i - 1], 24);
-        r[0] = (r[0] << 8) | ca;
-    }
-    __device__ __forceinline__ uint64_t hash(uint32_t seed) const {
-        uint32_t w[6];
-        const bool fwd = fc <= rc;   // memcmp(fwd, rev, K) <= 0
-#pragma unroll
-        for (int i = 0; i < 6; i++) w[i] = fwd ? f[i] : r[i];
-        return murmur21(((uint64_t)w[1] << 32) | w[0], ((uint64_t)w[3] << 32) | w[2],
-                        ((uint64_t)w[5] << 32) | w[4], seed);
-    }
-};
-
 // Candidates are staged in an LDS buffer (wave-aggregated LDS atomic) and only
 // flushed to the per-genome set after the tile, so the hot loop issues no
 // global memory operation with a wait; a full buffer spills to the set
 // directly.
 constexpr uint32_t kStage = 1024;
 
-template <int LANE>   // window ends per lane; the workgroup (kTile / LANE lanes) covers one tile
-__global__ __launch_bounds__(kTile / LANE) void k_sketch_hash21(
-    const uint32_t *__restrict__ codes, const uint32_t *__restrict__ valid,
-    const uint64_t *__restrict__ tile_base, const uint32_t *__restrict__ tile_genome,
-    const uint64_t *__restrict__ thr, unsigned long long *__restrict__ sets,
-    uint32_t *__restrict__ cnt, uint32_t set_log2, uint32_t limit, uint32_t seed) {
-    constexpr int K = 21;
-    constexpr uint32_t WG = kTile / LANE;
-    __shared__ uint64_t stage[kStage];
-    __shared__ uint32_t nstage;
-    const uint32_t t = blockIdx.x;
-    const uint32_t g = tile_genome[t];
-    const uint64_t T = thr[g];
-    const uint64_t start = tile_base[t] + (uint64_t)threadIdx.x * LANE;
-    const uint32_t mask = (1u << set_log2) - 1;
-    unsigned long long *S = sets + ((uint64_t)g << set_log2);
-    uint32_t *C = cnt + g;
-    if (threadIdx.x == 0) nstage = 0;
-    const uint32_t *cw = codes + (start - kWarm) / 16;
-    const uint32_t *vw = valid + (start - kWarm) / 32;
-    Window21 w;
-    w.init();
-    {
-        const uint32_t v0 = vw[0];
-        const uint32_t c0 = cw[0], c1 = cw[1];
-#pragma unroll
-        for (int b = 0; b < 16; b++) w.push((c0 >> (2 * b)) & 3u, (v0 >> b) & 1u);
-#pragma unroll
-        for (int b = 0; b < 16; b++) w.push((c1 >> (2 * b)) & 3u, (v0 >> (16 + b)) & 1u);
-    }
-    __syncthreads();
-    uint32_t cnext = cw[2];
-    uint32_t vcur = vw[1];
-    for (int wi = 0; wi < (int)(LANE / 16); wi++) {
-        const uint32_t c = cnext;
-        const uint32_t vbits = vcur >> ((wi & 1) * 16);
-        if (wi + 1 < (int)(LANE / 16)) {
-            cnext = cw[3 + wi];
-            if (wi & 1) vcur = vw[2 + (wi >> 1)];
-        }
-#pragma unroll
-        for (int b = 0; b < 16; b++) {
-            w.push((c >> (2 * b)) & 3u, (vbits >> b) & 1u);
-            const uint64_t h = w.hash(seed);
-            if (__builtin_expect(h <= T && w.run >= (uint32_t)K, 0)) {
-                const uint32_t slot = atomicAdd(&nstage, 1u);
-                if (slot < kStage) stage[slot] = h;
-                else set_insert(S, mask, C, limit, h);
-            }
-        }
-    }
-    __syncthreads();
-    const uint32_t n = min(nstage, kStage);
-    for (uint32_t i = threadIdx.x; i < n; i += WG) set_insert(S, mask, C, limit, stage[i]);
-}
-
-// --------------------------------------------------------------- v3 kernel
-// Batches the 16 window ends of one code word: the window rolls serially, the
+// ------------------------------------------------------- hash kernel (v3)
+// Kept for A/B against v4 (DREPHIP_SKETCH_KERNEL=3).  Rolls forward and
+// reverse-complement ASCII windows (one v_alignbit_b32 per word per base) and
+// batches the 16 window ends of one code word: the window rolls serially, the
 // 16 canonical hashes are independent (the compiler interleaves them), and a
 // single admit test per batch replaces 16 per-k-mer branches.  Codes are kept
 // top-aligned (fc: newest base at bits 23:22, older bases fall off bit 63), so
@@ -296,6 +204,169 @@ __global__ __launch_bounds__(kTile / LANE) void k_sketch_hash21_v3(
                 }
             }
         }
+    }
+    __syncthreads();
+    const uint32_t n = min(nstage, kStage);
+    for (uint32_t i = threadIdx.x; i < n; i += WG) set_insert(S, mask, C, limit, stage[i]);
+}
+
+// ------------------------------------------------------- hash kernel (v4)
+// No rolled ASCII windows: the forward and reverse-complement k-mers are cut
+// out of the 2-bit code stream with two v_alignbit_b32 each (no loop-carried
+// state), the canonical one is chosen on the codes, and the parts of Murmur
+// that depend only on a few bases come from LDS tables built per workgroup:
+//   k1*c1 = TA1[bases 0-3] + TB1[bases 4-7] << 32     (k1 = ASCII bytes 0-7)
+//   k2*c2 = TA2[bases 8-11] + TB2[bases 12-15] << 32  (k2 = ASCII bytes 8-15)
+//   tail  = T3[bases 16-20] = rotl31(k3*c1)*c2 ^ 21   (k3 = ASCII bytes 16-20;
+//                                                       ^21 = Murmur's h1 ^= len)
+// (a 64-bit product k*c splits as lo*c + (hi*(uint32)c) << 32).  Of Murmur's
+// ten 64-bit multiplies six remain (two in the body, four in fmix).
+//
+// Streams (code word j holds bases 16j..16j+15, base i at bits 2i):
+//   NF[j] = ~F[j]: a 64-bit little-endian cut holding bases q-31..q has base q
+//     in the top bits, i.e. it is the reverse complement read MSB-first --
+//     top-aligned (bases of the k-mer in bits 22..63, junk below);
+//   R[j] = F[j] with its 16 fields reversed: a big-endian cut of R starting at
+//     base q-20 is the forward k-mer MSB-first, top-aligned the same way.
+// memcmp order of the ASCII k-mers = unsigned order of those top-aligned values
+// (A<C<G<T = 0<1<2<3; junk bits never decide: k is odd, so no k-mer equals its
+// reverse complement).
+struct SketchTables {
+    uint64_t ta1[256], ta2[256], t3[1024];
+    uint32_t tb1[256], tb2[256];
+};
+
+__device__ __forceinline__ uint32_t ascii4(uint32_t x) {      // 4 bases, base 0 in bits 6-7
+    const uint32_t sel = ((x >> 6) & 3u) | (((x >> 4) & 3u) << 8) | (((x >> 2) & 3u) << 16) | ((x & 3u) << 24);
+    return __builtin_amdgcn_perm(0u, 0x54474341u, sel);
+}
+
+__device__ void build_tables(SketchTables &tb, uint32_t tid, uint32_t nthreads) {
+    constexpr uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
+    for (uint32_t x = tid; x < 256; x += nthreads) {
+        const uint32_t a = ascii4(x);
+        tb.ta1[x] = (uint64_t)a * c1;
+        tb.tb1[x] = a * (uint32_t)c1;
+        tb.ta2[x] = (uint64_t)a * c2;
+        tb.tb2[x] = a * (uint32_t)c2;
+    }
+    for (uint32_t y = tid; y < 1024; y += nthreads) {
+        // bases 16..19 = bits 9..2, base 20 = bits 1..0
+        const uint64_t k3 = (uint64_t)ascii4(y >> 2) | ((uint64_t)ascii4((y & 3u) << 6) & 0xffu) << 32;
+        tb.t3[y] = (rotl64_ab(k3 * c1, 31) * c2) ^ 21u;   // tail mix, with h1 ^= len folded in
+    }
+}
+
+__device__ __forceinline__ uint32_t rev_fields16(uint32_t x) {     // reverse the 16 2-bit fields
+    const uint32_t y = __builtin_bitreverse32(x);
+    return ((y >> 1) & 0x55555555u) | ((y & 0x55555555u) << 1);
+}
+
+__device__ __forceinline__ uint64_t murmur21_tab(const SketchTables &tb, uint32_t hi, uint32_t lo,
+                                                 uint32_t seed) {
+    constexpr uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
+    const uint64_t a1 = tb.ta1[hi >> 24] + ((uint64_t)tb.tb1[(hi >> 16) & 0xffu] << 32);
+    const uint64_t a2 = tb.ta2[(hi >> 8) & 0xffu] + ((uint64_t)tb.tb2[hi & 0xffu] << 32);
+    const uint64_t k3 = tb.t3[lo >> 22];
+    uint64_t h1 = (uint64_t)seed ^ (rotl64_ab(a1, 31) * c2);
+    h1 = x5_plus(rotl64_ab(h1, 27), 5ull * seed + 0x52dce729);   // (rotl + seed) * 5 + c
+    uint64_t h2 = (uint64_t)seed ^ (rotl64_ab(a2, 33) * c1);
+    h2 = rotl64_ab(h2, 31) + h1;
+    h2 = x5_plus(h2, 0x38495ab5);
+    h1 ^= k3;
+    h2 ^= 21u;
+    h1 += h2; h2 += h1;
+    return fmix64_v(h1) + fmix64_v(h2);
+}
+
+template <int LANE, int BATCH>
+__global__ __launch_bounds__(kTile / LANE) void k_sketch_hash21_v4(
+    const uint32_t *__restrict__ codes, const uint32_t *__restrict__ valid,
+    const uint64_t *__restrict__ tile_base, const uint32_t *__restrict__ tile_genome,
+    const uint64_t *__restrict__ thr, unsigned long long *__restrict__ sets,
+    uint32_t *__restrict__ cnt, uint32_t set_log2, uint32_t limit, uint32_t seed, uint64_t wlast) {
+    constexpr uint32_t WG = kTile / LANE;
+    constexpr int NCH = LANE / 16;
+    __shared__ SketchTables tb;
+    __shared__ uint64_t stage[kStage];
+    __shared__ uint32_t nstage;
+    const uint32_t t = blockIdx.x;
+    const uint32_t g = tile_genome[t];
+    const uint64_t T = thr[g];
+    const uint64_t start = tile_base[t] + (uint64_t)threadIdx.x * LANE;
+    const uint32_t mask = (1u << set_log2) - 1;
+    unsigned long long *S = sets + ((uint64_t)g << set_log2);
+    uint32_t *C = cnt + g;
+    if (threadIdx.x == 0) nstage = 0;
+    build_tables(tb, threadIdx.x, WG);
+
+    const uint64_t m0 = start / 16;                  // code word of the lane's first window end
+    auto ld = [&](int j) -> uint32_t {               // clamp: the cut after the last word is junk
+        const uint64_t w = m0 + j;
+        return codes[w < wlast ? w : wlast];
+    };
+    // registers: F words m-2..m (complemented), R words m-2..m+1
+    uint32_t nf0 = ~ld(-2), nf1 = ~ld(-1), nf2 = ~ld(0);
+    uint32_t r0 = rev_fields16(~nf0), r1 = rev_fields16(~nf1), r2 = rev_fields16(~nf2);
+    uint32_t f3 = ld(1);                             // raw F[m+1]
+    uint32_t r3 = rev_fields16(f3);
+    uint32_t fnext = ld(2);
+    const uint32_t *vw = valid + (start - kWarm) / 32;
+    uint64_t vhist = (uint64_t)vw[0] << 32;          // bit 63 = newest base
+    uint32_t vcur = vw[1];
+    __syncthreads();
+
+#pragma unroll 1
+    for (int wi = 0; wi < NCH; wi++) {
+        const uint32_t vbits = (vcur >> ((wi & 1) * 16)) & 0xffffu;
+        if (wi + 1 < NCH && (wi & 1)) vcur = vw[2 + (wi >> 1)];
+        vhist = (vhist >> 16) | ((uint64_t)vbits << 48);
+#pragma unroll
+        for (int b0 = 0; b0 < 16; b0 += BATCH) {
+            uint64_t h[BATCH];
+            bool hit = false;
+#pragma unroll
+            for (int b = 0; b < BATCH; b++) {
+                const int r = b0 + b;                // window end q = 16m + r
+                uint32_t chi, clo, fhi, flo;
+                if (r == 15) { chi = nf2; clo = nf1; }
+                else {
+                    chi = __builtin_amdgcn_alignbit(nf2, nf1, 2 * (r + 1));
+                    clo = __builtin_amdgcn_alignbit(nf1, nf0, 2 * (r + 1));
+                }
+                if (r < 4) {                         // k-mer starts in word m-2 at field r+12
+                    fhi = __builtin_amdgcn_alignbit(r0, r1, 32 - 2 * (r + 12));
+                    flo = __builtin_amdgcn_alignbit(r1, r2, 32 - 2 * (r + 12));
+                } else if (r == 4) {
+                    fhi = r1; flo = r2;
+                } else {                             // starts in word m-1 at field r-4
+                    fhi = __builtin_amdgcn_alignbit(r1, r2, 32 - 2 * (r - 4));
+                    flo = __builtin_amdgcn_alignbit(r2, r3, 32 - 2 * (r - 4));
+                }
+                const uint64_t fw = ((uint64_t)fhi << 32) | flo;
+                const uint64_t rc = ((uint64_t)chi << 32) | clo;
+                const uint64_t cc = fw <= rc ? fw : rc;
+                h[b] = murmur21_tab(tb, (uint32_t)(cc >> 32), (uint32_t)cc, seed);
+                hit |= h[b] <= T;
+            }
+            if (__builtin_expect(hit, 0)) {
+                const uint64_t ok = run21(vhist);
+#pragma unroll
+                for (int b = 0; b < BATCH; b++) {
+                    if (h[b] <= T && ((ok >> (48 + b0 + b)) & 1)) {
+                        const uint32_t slot = atomicAdd(&nstage, 1u);
+                        if (slot < kStage) stage[slot] = h[b];
+                        else set_insert(S, mask, C, limit, h[b]);
+                    }
+                }
+            }
+        }
+        // slide one code word
+        nf0 = nf1; nf1 = nf2; nf2 = ~f3;
+        r0 = r1; r1 = r2; r2 = r3;
+        f3 = fnext;
+        r3 = rev_fields16(f3);
+        fnext = ld(wi + 3);
     }
     __syncthreads();
     const uint32_t n = min(nstage, kStage);
@@ -443,6 +514,8 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
             tgen.push_back(g);
         }
     }
+    uint64_t wlast = 0;                                // last code word any tile may touch
+    for (uint32_t g = 0; g < n; g++) wlast = std::max(wlast, (base_off[g] + padded[g]) / 16 - 1);
     std::vector<uint64_t> T(n), lo(n, 0), hi(n, 0);   // hi == 0: unknown
     for (uint32_t g = 0; g < n; g++) T[g] = initial_threshold(nkmers[g], s, plan.F);
 
@@ -496,10 +569,10 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
         }
         if (nt > 0) {
             timing_mark(ctx, 0, st, true);
-            if (ctx->sketch_kernel == 2)
-                hipLaunchKernelGGL((k_sketch_hash21<kLaneBases>), dim3(nt), dim3(kTile / kLaneBases), 0, st,
+            if (ctx->sketch_kernel != 3)
+                hipLaunchKernelGGL((k_sketch_hash21_v4<kLaneBases, 8>), dim3(nt), dim3(kTile / kLaneBases), 0, st,
                                    d_codes, d_valid, tb_tiles_b, tb_tiles_g, d_thr, d_sets, d_cnt, plan.set_log2,
-                                   limit, ctx->seed);
+                                   limit, ctx->seed, wlast);
             else
                 hipLaunchKernelGGL((k_sketch_hash21_v3<kLaneBases, 8>), dim3(nt), dim3(kTile / kLaneBases), 0, st,
                                    d_codes, d_valid, tb_tiles_b, tb_tiles_g, d_thr, d_sets, d_cnt, plan.set_log2,

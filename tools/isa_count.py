@@ -1,0 +1,52 @@
+"""Static instruction mix of the sketch hash kernels' hot loop (not part of the
+product).  Compiles drep_amd/csrc/sketch.hip to gfx950 assembly, finds each
+kernel's unrolled loop blocks (the ones holding the BATCH-wide hash code) and
+reports VALU instructions per window end.  Output feeds bench.py's VALU
+roofline: python tools/isa_count.py > profiles/sketch_isa.json"""
+import collections
+import json
+import os
+import re
+import subprocess
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNELS = {"3": ("k_sketch_hash21_v3", 8), "4": ("k_sketch_hash21_v4", 8)}   # variant: (name, k-mers/block)
+
+
+def main():
+    with tempfile.TemporaryDirectory() as td:
+        asm = os.path.join(td, "sk.s")
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                        "--cuda-device-only", "-S", "-o", asm,
+                        os.path.join(ROOT, "drep_amd/csrc/sketch.hip"),
+                        "-I" + os.path.join(ROOT, "drep_amd/csrc")], check=True,
+                       stderr=subprocess.DEVNULL)
+        s = open(asm).read()
+    out = {"arch": "gfx950", "source": "drep_amd/csrc/sketch.hip", "variants": {}}
+    for var, (name, per) in KERNELS.items():
+        m = re.search(r"^(_ZN7drephip\d+" + name + r"\S*):", s, re.M)
+        body = s[m.start():s.index(".Lfunc_end", m.start())]
+        blocks, cur = [], None
+        for line in body.split("\n"):
+            if re.match(r"^\.LBB\S+:", line):
+                cur = collections.Counter()
+                blocks.append(cur)
+            elif cur is not None and line.startswith("\t") and not line.strip().startswith((".", ";")):
+                cur[line.strip().split()[0]] += 1
+        # the hash blocks: those with the 64-bit multiply chains (mad_u64 per k-mer)
+        hot = [b for b in blocks if b["v_mad_u64_u32"] >= 4 * per]
+        valu = [sum(v for k, v in b.items() if k.startswith("v_")) for b in hot]
+        mul = [b["v_mul_lo_u32"] + b["v_mad_u64_u32"] + b["v_mul_hi_u32"] for b in hot]
+        lds = [sum(v for k, v in b.items() if k.startswith("ds_read")) for b in hot]
+        out["variants"][var] = {
+            "kernel": name, "kmers_per_block": per, "blocks": len(hot),
+            "valu_per_kmer": sum(valu) / len(hot) / per,
+            "mul_per_kmer": sum(mul) / len(hot) / per,
+            "lds_reads_per_kmer": sum(lds) / len(hot) / per,
+        }
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -13,7 +13,7 @@ from drep_amd import _lib
 N = int(os.environ.get("AB_GENOMES", 200))
 L = 5_000_000
 rounds = int(os.environ.get("AB_ROUNDS", 5))
-variants = [int(v) for v in os.environ.get("AB_VARIANTS", "3,2").split(",")]
+variants = [int(v) for v in os.environ.get("AB_VARIANTS", "4,3").split(",")]
 ctxs = {}
 for v in variants:
     os.environ["DREPHIP_SKETCH_KERNEL"] = str(v)
