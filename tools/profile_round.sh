@@ -14,3 +14,4 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 400 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_$c -o pmc -- \
       python bench.py --steps 1 --warmup 0 --cpu-baseline 0 > $OUT/pmc_$c.json 2> $OUT/pmc_$c.err || exit 1
 done
+python3 tools/traffic_json.py $OUT ${GENOMES:-1000} ${GENOME_BP:-5000000} > $OUT/sketch_traffic.json || exit 1
