@@ -64,8 +64,19 @@ __device__ __forceinline__ uint64_t rotl64_ab(uint64_t x, int r) {
 }
 __device__ __forceinline__ uint64_t x5_plus(uint64_t x, uint64_t c) {
     uint64_t y;
-    asm volatile("v_lshl_add_u64 %0, %1, 2, %1" : "=v"(y) : "v"(x));
+    asm("v_lshl_add_u64 %0, %1, 2, %1" : "=v"(y) : "v"(x));
     return y + c;
+}
+__device__ __forceinline__ uint64_t add64(uint64_t a, uint64_t b) {   // one v_lshl_add_u64
+    uint64_t y;
+    asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(y) : "v"(a), "v"(b));
+    return y;
+}
+// fmix64 without its last `k ^= k >> 33`, which only changes the low word
+__device__ __forceinline__ uint64_t fmix64_pre(uint64_t k) {
+    k ^= k >> 33; k *= 0xff51afd7ed558ccdULL;
+    k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ULL;
+    return k;
 }
 __device__ __forceinline__ uint64_t fmix64_v(uint64_t k) {
     k ^= k >> 33; k *= 0xff51afd7ed558ccdULL;
@@ -262,8 +273,15 @@ __device__ __forceinline__ uint32_t rev_fields16(uint32_t x) {     // reverse th
     return ((y >> 1) & 0x55555555u) | ((y & 0x55555555u) << 1);
 }
 
-__device__ __forceinline__ uint64_t murmur21_tab(const SketchTables &tb, uint32_t hi, uint32_t lo,
-                                                 uint32_t seed) {
+// Murmur h1 of the canonical k-mer (top-aligned codes hi:lo), returned as the
+// two fmix64 states before their final xorshift: h1 = fin(p1) + fin(p2) with
+// fin(k) = k ^ (k >> 33).  fin leaves the high word unchanged, so
+//     h1 <= T  implies  hi(p1) + hi(p2) + 1  <=  hi(T) + 1   (mod 2^32)
+// (the low-word sum carries at most 1 into the high word; both sides are
+// taken one past so a wrapping 0xFFFFFFFF + carry = 0 is kept): a one-add,
+// one-compare prefilter; the exact test runs in the rare admit branch.
+__device__ __forceinline__ void murmur21_tab(const SketchTables &tb, uint32_t hi, uint32_t lo, uint32_t seed,
+                                             uint64_t &p1, uint64_t &p2) {
     constexpr uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
     const uint64_t a1 = tb.ta1[hi >> 24] + ((uint64_t)tb.tb1[(hi >> 16) & 0xffu] << 32);
     const uint64_t a2 = tb.ta2[(hi >> 8) & 0xffu] + ((uint64_t)tb.tb2[hi & 0xffu] << 32);
@@ -271,12 +289,16 @@ __device__ __forceinline__ uint64_t murmur21_tab(const SketchTables &tb, uint32_
     uint64_t h1 = (uint64_t)seed ^ (rotl64_ab(a1, 31) * c2);
     h1 = x5_plus(rotl64_ab(h1, 27), 5ull * seed + 0x52dce729);   // (rotl + seed) * 5 + c
     uint64_t h2 = (uint64_t)seed ^ (rotl64_ab(a2, 33) * c1);
-    h2 = rotl64_ab(h2, 31) + h1;
-    h2 = x5_plus(h2, 0x38495ab5);
+    h2 = x5_plus(add64(rotl64_ab(h2, 31), h1), 0x38495ab5);
     h1 ^= k3;
     h2 ^= 21u;
-    h1 += h2; h2 += h1;
-    return fmix64_v(h1) + fmix64_v(h2);
+    h1 = add64(h1, h2);
+    h2 = add64(h2, h1);
+    p1 = fmix64_pre(h1);
+    p2 = fmix64_pre(h2);
+}
+__device__ __forceinline__ uint64_t murmur_fin(uint64_t p1, uint64_t p2) {
+    return add64(p1 ^ (p1 >> 33), p2 ^ (p2 >> 33));
 }
 
 template <int LANE, int BATCH>
@@ -293,6 +315,8 @@ __global__ __launch_bounds__(kTile / LANE) void k_sketch_hash21_v4(
     const uint32_t t = blockIdx.x;
     const uint32_t g = tile_genome[t];
     const uint64_t T = thr[g];
+    const uint32_t Thi = (uint32_t)(T >> 32);
+    const uint32_t Tp = Thi == 0xFFFFFFFFu ? Thi : Thi + 1;     // prefilter bound (see murmur21_tab)
     const uint64_t start = tile_base[t] + (uint64_t)threadIdx.x * LANE;
     const uint32_t mask = (1u << set_log2) - 1;
     unsigned long long *S = sets + ((uint64_t)g << set_log2);
@@ -323,7 +347,7 @@ __global__ __launch_bounds__(kTile / LANE) void k_sketch_hash21_v4(
         vhist = (vhist >> 16) | ((uint64_t)vbits << 48);
 #pragma unroll
         for (int b0 = 0; b0 < 16; b0 += BATCH) {
-            uint64_t h[BATCH];
+            uint64_t p1[BATCH], p2[BATCH];
             bool hit = false;
 #pragma unroll
             for (int b = 0; b < BATCH; b++) {
@@ -346,17 +370,18 @@ __global__ __launch_bounds__(kTile / LANE) void k_sketch_hash21_v4(
                 const uint64_t fw = ((uint64_t)fhi << 32) | flo;
                 const uint64_t rc = ((uint64_t)chi << 32) | clo;
                 const uint64_t cc = fw <= rc ? fw : rc;
-                h[b] = murmur21_tab(tb, (uint32_t)(cc >> 32), (uint32_t)cc, seed);
-                hit |= h[b] <= T;
+                murmur21_tab(tb, (uint32_t)(cc >> 32), (uint32_t)cc, seed, p1[b], p2[b]);
+                hit |= (uint32_t)(p1[b] >> 32) + (uint32_t)(p2[b] >> 32) + 1u <= Tp;
             }
             if (__builtin_expect(hit, 0)) {
                 const uint64_t ok = run21(vhist);
 #pragma unroll
                 for (int b = 0; b < BATCH; b++) {
-                    if (h[b] <= T && ((ok >> (48 + b0 + b)) & 1)) {
+                    const uint64_t h = murmur_fin(p1[b], p2[b]);
+                    if (h <= T && ((ok >> (48 + b0 + b)) & 1)) {
                         const uint32_t slot = atomicAdd(&nstage, 1u);
-                        if (slot < kStage) stage[slot] = h[b];
-                        else set_insert(S, mask, C, limit, h[b]);
+                        if (slot < kStage) stage[slot] = h;
+                        else set_insert(S, mask, C, limit, h);
                     }
                 }
             }
