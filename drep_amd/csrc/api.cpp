@@ -24,13 +24,14 @@ int scratch(drephip_ctx *ctx, const char *name, size_t bytes, void **out) {
     DevBuf &b = ctx->bufs[name];
     if (bytes == 0) bytes = 8;
     if (b.bytes < bytes) {
+        const size_t want = std::max(bytes, b.bytes + b.bytes / 4);
         if (b.ptr) {
             HIPC(hipStreamSynchronize(ctx->stream));
             HIPC(hipDeviceSynchronize());
             HIPC(hipFree(b.ptr));
             b.ptr = nullptr; b.bytes = 0;
         }
-        const size_t want = std::max(bytes, b.bytes + b.bytes / 4);
+        ctx->alloc_gen++;                      // invalidates contents cached in scratch
         hipError_t e = hipMalloc(&b.ptr, want);
         if (e != hipSuccess) {
             set_error(std::string("hipMalloc(") + std::to_string(want) + ") for " + name + ": " +

@@ -30,6 +30,11 @@ struct drephip_ctx {
     size_t ev_used = 0;
     struct Span { int which; hipEvent_t a, b; };
     std::vector<Span> spans;
+    uint64_t alloc_gen = 1;   // bumped by every scratch (re)allocation
+    // sketch tile table of the last call (reused while the genome layout is the
+    // same and no scratch buffer has been reallocated since: sk_gen == alloc_gen)
+    std::vector<uint64_t> sk_off, sk_pad;
+    uint64_t sk_gen = 0;
 };
 
 namespace drephip {

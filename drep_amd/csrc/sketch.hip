@@ -524,23 +524,19 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
     const uint64_t slots = 1ull << plan.set_log2;
     const uint32_t limit = (uint32_t)(slots * 3 / 4);
 
-    // tile table + initial thresholds (host)
-    std::vector<uint64_t> tbase;
-    std::vector<uint32_t> tgen;
-    std::vector<std::vector<uint32_t>> tiles_of(n);
+    // tile table (tile -> base, genome), reused across calls on the same layout
+    std::vector<uint64_t> tfirst(n + 1, 0);           // first tile of each genome
+    uint64_t wlast = 0;                                // last code word any tile may touch
     for (uint32_t g = 0; g < n; g++) {
         if (base_off[g] % kTile || padded[g] % kTile || base_off[g] < kTile) {
             set_error("genome base_off/padded must be tile multiples and base_off >= tile");
             return DREPHIP_ERR_ARG;
         }
-        for (uint64_t t = 0; t < padded[g] / kTile; t++) {
-            tiles_of[g].push_back((uint32_t)tbase.size());
-            tbase.push_back(base_off[g] + t * kTile);
-            tgen.push_back(g);
-        }
+        tfirst[g + 1] = tfirst[g] + padded[g] / kTile;
+        wlast = std::max(wlast, (base_off[g] + padded[g]) / 16 - 1);
     }
-    uint64_t wlast = 0;                                // last code word any tile may touch
-    for (uint32_t g = 0; g < n; g++) wlast = std::max(wlast, (base_off[g] + padded[g]) / 16 - 1);
+    if (tfirst[n] >= (1ull << 31)) { set_error("too many tiles in one sketch call"); return DREPHIP_ERR_ARG; }
+    const uint32_t ntiles = (uint32_t)tfirst[n];
     std::vector<uint64_t> T(n), lo(n, 0), hi(n, 0);   // hi == 0: unknown
     for (uint32_t g = 0; g < n; g++) T[g] = initial_threshold(nkmers[g], s, plan.F);
 
@@ -549,7 +545,6 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
     unsigned long long *d_sets;
     uint8_t *d_st;
     int rc;
-    const uint32_t ntiles = (uint32_t)tbase.size();
     if ((rc = scratch(ctx, "sk_tb", ntiles * 8ull, (void **)&d_tb))) return rc;
     if ((rc = scratch(ctx, "sk_tg", ntiles * 4ull, (void **)&d_tg))) return rc;
     if ((rc = scratch(ctx, "sk_tbsub", ntiles * 8ull, (void **)&d_tbsub))) return rc;
@@ -560,8 +555,25 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
     if ((rc = scratch(ctx, "sk_st", n * 1ull, (void **)&d_st))) return rc;
     if ((rc = scratch(ctx, "sk_sets", (uint64_t)n * slots * 8ull, (void **)&d_sets))) return rc;
 
-    HIPC(hipMemcpyAsync(d_tb, tbase.data(), ntiles * 8ull, hipMemcpyHostToDevice, st));
-    HIPC(hipMemcpyAsync(d_tg, tgen.data(), ntiles * 4ull, hipMemcpyHostToDevice, st));
+    const bool cached = ctx->sk_gen == ctx->alloc_gen && ctx->sk_off.size() == n &&
+                        !memcmp(ctx->sk_off.data(), base_off, n * 8ull) &&
+                        !memcmp(ctx->sk_pad.data(), padded, n * 8ull);
+    if (!cached) {
+        std::vector<uint64_t> tbase(ntiles);
+        std::vector<uint32_t> tgen(ntiles);
+        for (uint32_t g = 0; g < n; g++)
+            for (uint64_t t = tfirst[g]; t < tfirst[g + 1]; t++) {
+                tbase[t] = base_off[g] + (t - tfirst[g]) * kTile;
+                tgen[t] = g;
+            }
+        ctx->sk_gen = 0;
+        HIPC(hipMemcpyAsync(d_tb, tbase.data(), ntiles * 8ull, hipMemcpyHostToDevice, st));
+        HIPC(hipMemcpyAsync(d_tg, tgen.data(), ntiles * 4ull, hipMemcpyHostToDevice, st));
+        HIPC(hipStreamSynchronize(st));                // host vectors die here
+        ctx->sk_off.assign(base_off, base_off + n);
+        ctx->sk_pad.assign(padded, padded + n);
+        ctx->sk_gen = ctx->alloc_gen;
+    }
     HIPC(hipMemcpyAsync(d_thr, T.data(), n * 8ull, hipMemcpyHostToDevice, st));
     HIPC(hipMemsetAsync(d_sets, 0xFF, (uint64_t)n * slots * 8ull, st));
     HIPC(hipMemsetAsync(d_cnt, 0, n * 4ull, st));
@@ -581,7 +593,10 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
             std::vector<uint64_t> sb;
             std::vector<uint32_t> sg;
             for (uint32_t g : todo)
-                for (uint32_t t : tiles_of[g]) { sb.push_back(tbase[t]); sg.push_back(g); }
+                for (uint64_t t = tfirst[g]; t < tfirst[g + 1]; t++) {
+                    sb.push_back(base_off[g] + (t - tfirst[g]) * kTile);
+                    sg.push_back(g);
+                }
             nt = (uint32_t)sb.size();
             HIPC(hipMemcpyAsync(d_tbsub, sb.data(), nt * 8ull, hipMemcpyHostToDevice, st));
             HIPC(hipMemcpyAsync(d_tgsub, sg.data(), nt * 4ull, hipMemcpyHostToDevice, st));

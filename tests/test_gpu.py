@@ -311,3 +311,33 @@ def test_device_calls_follow_callers_stream(ctx1000):
         assert int((valid[w0:w0 + L // 32] != -1).sum()) == 0, g
     del codes, valid
     torch.cuda.empty_cache()
+
+
+@pytest.mark.gpu
+def test_sketch_layout_cache_follows_layout_changes(ctx1000):
+    """The tile table is cached on the context between calls with the same
+    layout; a call with a different layout (same genome count) must not reuse
+    it.  Sketch A B C, then the same genomes listed as C A B, then A B C again."""
+    import torch
+    n, L, seed = 3, 300_000, 21
+    tile = _lib.tile_bases()
+    P = _lib.padded_bases([L])
+    total = tile + n * P
+    st = torch.cuda.current_stream().cuda_stream
+    codes = torch.zeros(total // 16, dtype=torch.int32, device="cuda")
+    valid = torch.zeros(total // 32, dtype=torch.int32, device="cuda")
+    ctx1000.synth_device(seed, 0, n, 1, L, codes.data_ptr(), valid.data_ptr(), st)
+    oh, onh = oracle.sketch_synth(0, n, L, seed=seed, family_size=1, threads=3)
+
+    def run(order):
+        off = np.array([tile + i * P for i in order], np.uint64)
+        h = torch.zeros((n, S), dtype=torch.int64, device="cuda")
+        nh = torch.zeros(n, dtype=torch.int32, device="cuda")
+        ctx1000.sketch_device(codes.data_ptr(), valid.data_ptr(), off, np.full(n, P, np.uint64),
+                              np.full(n, L - 20, np.uint64), n, h.data_ptr(), nh.data_ptr(), st)
+        torch.cuda.synchronize()
+        return h.cpu().numpy().view(np.uint64), nh.cpu().numpy().view(np.uint32)
+
+    for order in ([0, 1, 2], [2, 0, 1], [2, 0, 1], [0, 1, 2]):
+        h, nh = run(order)
+        assert np.array_equal(h, oh[order]) and np.array_equal(nh, onh[order]), order
