@@ -50,15 +50,19 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
-// --------------------------------------------------------------- v2
+// ------------------------------------------------------- row tables
 // Quotiented two-choice cuckoo table: choice 1 sits at T[f1(x)], choice 2 at
-// T[H + f2(x)], where f1/f2 are disjoint B-bit fields of the key (family f
-// picks the fields).  Because a slot's position fixes those B bits, the stored
-// word replaces them with the key's sketch position i, so one ds_read_b64
-// returns membership AND i:  e = (x & ~F) | (i << o),  match iff
-// (e & ~F) == (x & ~F) and i < nA (the all-ones empty word decodes to
-// i = 2^B-1 >= nA).  Exact for every key.
+// T[H + f2(x)], where f1/f2 are disjoint B-bit fields of the key at offsets
+// o1/o2 (family f picks them).  Because a slot's position fixes those B bits,
+// the stored word replaces them with the key's sketch position i, and is kept
+// rotated right by the field offset:  e = rotr((x & ~F) | (i << o), o), so the
+// field sits at bits [0, B); one 8-byte read returns membership AND i:
+// match iff (e ^ rotr(x, o)) < 2^B, i = e & (2^B - 1) (the all-ones empty
+// word decodes to i = 2^B-1 >= nA).  Exact for every key.
 struct QFields { uint32_t o1, o2; };
+__host__ __device__ __forceinline__ uint64_t rotr64(uint64_t x, uint32_t r) {
+    return r ? (x >> r) | (x << (64 - r)) : x;
+}
 __host__ __device__ __forceinline__ QFields qfields(uint32_t fam) {
     // disjoint field offsets inside the low 36 key bits (bottom-s hashes of
     // any genome below ~2^28 bases have uniformly random low 36 bits).
@@ -97,9 +101,11 @@ __global__ __launch_bounds__(256) void k_build_qcuckoo(const uint64_t *__restric
                 const bool second = pos >= H;
                 const uint64_t e = second ? ((x & ~F2) | ((uint64_t)ix << q.o2))
                                           : ((x & ~F1) | ((uint64_t)ix << q.o1));
-                const unsigned long long old = atomicExch(&T[pos], e);
-                if (old == kEmpty) { placed = true; break; }
+                // stored rotated right by the field offset: field at bits [0, B)
+                const unsigned long long oldr = atomicExch(&T[pos], rotr64(e, second ? q.o2 : q.o1));
+                if (oldr == kEmpty) { placed = true; break; }
                 // decode the evicted entry back to (key, position)
+                const uint64_t old = rotr64(oldr, 64 - (second ? q.o2 : q.o1));
                 const uint32_t lp = second ? pos - H : pos;
                 if (second) { ix = (uint32_t)(old >> q.o2) & hm; x = (old & ~F2) | ((uint64_t)lp << q.o2); }
                 else        { ix = (uint32_t)(old >> q.o1) & hm; x = (old & ~F1) | ((uint64_t)lp << q.o1); }
@@ -110,8 +116,8 @@ __global__ __launch_bounds__(256) void k_build_qcuckoo(const uint64_t *__restric
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
             const uint64_t x = A[i];
-            const uint64_t e1 = T[(uint32_t)(x >> q.o1) & hm];
-            const uint64_t e2 = T[H + ((uint32_t)(x >> q.o2) & hm)];
+            const uint64_t e1 = rotr64(T[(uint32_t)(x >> q.o1) & hm], 64 - q.o1);
+            const uint64_t e2 = rotr64(T[H + ((uint32_t)(x >> q.o2) & hm)], 64 - q.o2);
             const bool ok1 = (e1 & ~F1) == (x & ~F1) && ((uint32_t)(e1 >> q.o1) & hm) == i;
             const bool ok2 = (e2 & ~F2) == (x & ~F2) && ((uint32_t)(e2 >> q.o2) & hm) == i;
             if (!(ok1 || ok2)) fail = 1;
@@ -134,30 +140,18 @@ __global__ __launch_bounds__(256) void k_build_qcuckoo(const uint64_t *__restric
 // match tests are integer xor/or, i is one select.
 // FAST: family 0 (fields at bits [0,B) and [16,16+B)); otherwise generic
 // 64-bit field shifts.
-template <bool FAST>
-__device__ __forceinline__ bool q_match(uint64_t e1, uint64_t e2, uint32_t hm, uint64_t b, uint32_t o1,
-                                        uint32_t o2, uint32_t nA, uint32_t &i) {
-    // x = residual of the non-field bits (0 iff the slot holds b); a slot's
-    // candidate position is pushed past any nA when x != 0:
-    //   i_k = field_k + min(x_k, 1) << 16,   i = min(i_1, i_2),   found = i < nA
-    // (at most one slot holds b; the empty word decodes to 2^B - 1 >= nA)
-    uint32_t x1, x2, f1, f2;
-    if (FAST) {
-        const uint32_t bhi = (uint32_t)(b >> 32), blo = (uint32_t)b;
-        x1 = ((uint32_t)(e1 >> 32) ^ bhi) | (((uint32_t)e1 ^ blo) & ~hm);
-        x2 = ((uint32_t)(e2 >> 32) ^ bhi) | (((uint32_t)e2 ^ blo) & ~(hm << 16));
-        f1 = (uint32_t)e1 & hm;
-        f2 = ((uint32_t)e2 >> 16) & hm;
-    } else {
-        const uint64_t F1 = (uint64_t)hm << o1, F2 = (uint64_t)hm << o2;
-        const uint64_t y1 = (e1 ^ b) & ~F1, y2 = (e2 ^ b) & ~F2;
-        x1 = (uint32_t)y1 | (uint32_t)(y1 >> 32);
-        x2 = (uint32_t)y2 | (uint32_t)(y2 >> 32);
-        f1 = (uint32_t)(e1 >> o1) & hm;
-        f2 = (uint32_t)(e2 >> o2) & hm;
-    }
-    i = min(f1 + (min(x1, 1u) << 16), f2 + (min(x2, 1u) << 16));
-    return i < nA;
+// Slot words are stored rotated right by their field offset (field at bits
+// [0, B)), so slot k holds b iff (e_k ^ rotr(b, o_k)) <= 2^B - 1, and the
+// field -- b's sketch position i in A -- is e_k & hm.  br_k = rotr(b, o_k) is
+// per chunk (FAST, family 0: o = 0 and 16 for every row) or per row.  Bitwise
+// |/& keep it branch-free.  The empty word (all ones) matches only the
+// all-ones padding key and decodes to i = 2^B - 1 >= nA, so `found` is exact.
+__device__ __forceinline__ bool q_match(uint64_t e1, uint64_t e2, uint64_t br1, uint64_t br2, uint32_t hm,
+                                        uint32_t nA, uint32_t &i) {
+    const bool m1 = (e1 ^ br1) <= (uint64_t)hm;
+    const bool m2 = (e2 ^ br2) <= (uint64_t)hm;
+    i = (m1 ? (uint32_t)e1 : (uint32_t)e2) & hm;
+    return (m1 | m2) & (i < nA);
 }
 
 // The columns of one work item, processed by one wave (double-buffered column
@@ -210,37 +204,47 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
             if (b0 == kEmpty || !more) { alive = false; continue; }
             const uint32_t j = k * 64 + lane;
             const uint32_t blo = (uint32_t)b;
-            constexpr int G = R < 4 ? R : 4;                                 // rows per read group
+            const uint64_t b16 = rotr64(b, 16);                          // family 0's second field
+            // row tables are interleaved in LDS (slot k of row r at k*R + r), so
+            // one slot address serves all R rows: R/2 ds_read_b128 per choice
+            uint64_t e1[R], e2[R];
+            if (FAST) {
+                const uint64_t *p1 = T + (uint64_t)(blo & hm) * R;
+                const uint64_t *p2 = T + (uint64_t)(H + ((blo >> 16) & hm)) * R;
+                if constexpr (R == 1) {
+                    e1[0] = p1[0]; e2[0] = p2[0];
+                } else {
 #pragma unroll
-            for (int r0 = 0; r0 < R; r0 += G) {
-                uint64_t e1[G], e2[G];
-#pragma unroll
-                for (int g = 0; g < G; g++) {
-                    const int r = r0 + g;
-                    if ((uint32_t)r >= nrows || i0 + r >= c) continue;    // wave-uniform
-                    const uint64_t *Tr = T + (uint64_t)r * TS;
-                    if (FAST) {
-                        e1[g] = Tr[blo & hm];
-                        e2[g] = Tr[H + ((blo >> 16) & hm)];
-                    } else {
-                        e1[g] = Tr[(uint32_t)(b >> o1[r]) & hm];
-                        e2[g] = Tr[H + ((uint32_t)(b >> o2[r]) & hm)];
+                    for (int r = 0; r < R; r += 2) {
+                        const ulonglong2 v1 = *(const ulonglong2 *)(p1 + r);
+                        const ulonglong2 v2 = *(const ulonglong2 *)(p2 + r);
+                        e1[r] = v1.x; e1[r + 1] = v1.y; e2[r] = v2.x; e2[r + 1] = v2.y;
                     }
-                    asm volatile("" ::"v"(e1[g]), "v"(e2[g]));            // all reads issued before any test
                 }
+            } else {
 #pragma unroll
-                for (int g = 0; g < G; g++) {
-                    const int r = r0 + g;
-                    if ((uint32_t)r >= nrows || i0 + r >= c) continue;    // wave-uniform
-                    uint32_t i;
-                    const bool found = q_match<FAST>(e1[g], e2[g], hm, b, o1[r], o2[r], nA[r], i);
-                    const uint64_t m = __ballot(found);
-                    // s + matches below this lane (running count + in-chunk prefix)
-                    const uint32_t lim = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, s + mrun[r]));
-                    cnt[r] += (uint32_t)found & (uint32_t)(i + j < lim);
-                    mrun[r] += (uint32_t)__popcll(m);
+                for (int r = 0; r < R; r++) {                            // rows past nrows read empty words
+                    e1[r] = T[(uint64_t)((uint32_t)(b >> o1[r]) & hm) * R + r];
+                    e2[r] = T[(uint64_t)(H + ((uint32_t)(b >> o2[r]) & hm)) * R + r];
                 }
+            }
+            // every row is tested unconditionally (no branch for the reads to
+            // sink into); an inactive row (past nrows, or not above the
+            // diagonal) has found = false, so its ballot is 0 and it is skipped
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                uint32_t i;
+                const bool act = (uint32_t)r < nrows && i0 + r < c;       // wave-uniform
+                const bool found = (FAST ? q_match(e1[r], e2[r], b, b16, hm, nA[r], i)
+                                         : q_match(e1[r], e2[r], rotr64(b, o1[r]), rotr64(b, o2[r]), hm, nA[r], i)) &
+                                   act;
+                const uint64_t m = __ballot(found);
+                if (m == 0) continue;                                    // wave-uniform: no shared hash here
+                // s + matches below this lane (running count + in-chunk prefix)
+                const uint32_t lim = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, s + mrun[r]));
+                cnt[r] += (uint32_t)found & (uint32_t)(i + j < lim);
+                mrun[r] += (uint32_t)__popcll(m);
             }
         }
 #pragma unroll
@@ -276,10 +280,11 @@ __global__ __launch_bounds__(ap_wg(NCH)) void k_allpairs_q(
     const uint32_t nrows = min((uint32_t)R, row1 - i0);
     const uint32_t cend = min(c0 + kApCols, N);
     const uint32_t tid = threadIdx.x, wave = tid >> 6;
-    for (uint32_t r = 0; r < nrows; r++) {
-        const uint4 *src = (const uint4 *)(tabs + (uint64_t)(i0 - row0 + r) * TS);
-        uint4 *dst = (uint4 *)(T + (uint64_t)r * TS);
-        for (uint32_t i = tid; i < TS / 2; i += WG) dst[i] = src[i];
+    // interleave the R row tables: slot k of row r at k*R + r (rows past nrows empty)
+    for (uint32_t k = tid; k < TS; k += WG) {
+#pragma unroll
+        for (int r = 0; r < R; r++)
+            T[(uint64_t)k * R + r] = (uint32_t)r < nrows ? tabs[(uint64_t)(i0 - row0 + r) * TS + k] : kEmpty;
     }
     uint32_t nA[R], o1[R], o2[R];
     uint64_t alast[R];
@@ -433,7 +438,7 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
 #define DREPHIP_Q(RR, NC) launch_q<RR, NC>(ctx, ni, lds, st, d_hashes, d_nhash, d_tabs, d_fam, N, row0, row1, B, d_items, d_common, d_denom, seg0)
     if (!big) {
         switch (R) {
-            case 8: rc = DREPHIP_Q(8, 16); break;
+            case 8: rc = DREPHIP_Q(8, 8); break;       // R = 8 only when H <= 1024, i.e. s <= 512
             case 4: rc = DREPHIP_Q(4, 16); break;
             case 2: rc = DREPHIP_Q(2, 16); break;
             default: rc = DREPHIP_Q(1, 16); break;
