@@ -26,7 +26,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
-VALU_PEAK_TINST = 256 * 4 * 16 * 2.4e9 / 1e12   # full-rate VALU lane-instructions/s (MI355X_MICROARCH.md: 256 CU, 2.4 GHz)
+# VALU issue peak: 256 CU x 4 SIMD-32 x 32 lanes/cycle x 2.4 GHz (a wave64 VALU
+# instruction issues over 2 cycles, MI355X_MICROARCH.md)
+VALU_PEAK_TINST = 256 * 4 * 32 * 2.4e9 / 1e12
+# measured throughput cost of the integer VOP3 ops that make up the Murmur loop
+# (v_mul_lo_u32, v_mad_u64_u32, v_alignbit_b32, v_add3_u32, v_lshl_add_u64 ...):
+# 2.85-3.1 cycles per wave-instruction at 8 waves/SIMD (tools/valu_microbench.hip,
+# profiles/r01_valu_microbench.json) -> attainable ~2/2.9 of the issue peak
+VALU_VOP3_CYCLES = 2.9
 SKETCH_DEFAULT_VARIANT = "4"   # must match drephip_ctx::sketch_kernel default (ctx.h)
 
 
@@ -197,14 +204,18 @@ def main():
     if os.path.exists(isa_path):
         isa = json.load(open(isa_path))["variants"].get(variant)
         if isa:
-            # lane-instructions issued per second vs the full-rate VALU issue peak
-            # (256 CU x 4 SIMD x 16 lanes x 2.4 GHz); 64-bit multiply-class ops
-            # issue slower than full rate, so frac < 1 at saturation
+            # lane-instructions issued per second vs the VALU issue peak (2-cycle
+            # wave64 issue at 2.4 GHz); "attainable" prices every instruction at
+            # the measured integer-VOP3 cost instead
             ach = kmers_per_s * isa["valu_per_kmer"] / 1e12
+            attain = VALU_PEAK_TINST * 2.0 / VALU_VOP3_CYCLES
             valu.update({"kernel": isa["kernel"], "valu_per_kmer": isa["valu_per_kmer"],
                          "mul_per_kmer": isa["mul_per_kmer"], "achieved": ach,
                          "peak": VALU_PEAK_TINST, "unit": "T lane-inst/s", "frac": ach / VALU_PEAK_TINST,
-                         "source": "profiles/sketch_isa.json (tools/isa_count.py)"})
+                         "attainable": attain, "frac_of_attainable": ach / attain,
+                         "source": "profiles/sketch_isa.json (tools/isa_count.py); attainable = peak x 2 / "
+                                   "%.1f measured cycles per integer VOP3 wave-instruction "
+                                   "(profiles/r01_valu_microbench.json)" % VALU_VOP3_CYCLES})
 
     # ---- output segment D2H (PCIe-inclusive leg; not part of `value`)
     torch.cuda.synchronize()

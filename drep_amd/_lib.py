@@ -64,6 +64,7 @@ SIGNATURES = {
     "drephip_allpairs_device": (C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp]),
     "drephip_allpairs_merge_device": (C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp]),
     "drephip_distance_lut": (C.c_int, [C.c_int, C.c_uint32, f64p]),
+    "drephip_set_allpairs_path": (C.c_int, [vp, C.c_int, C.c_uint32]),
     "drephip_set_timing": (C.c_int, [vp, C.c_int]),
     "drephip_last_kernel_ms": (C.c_int, [vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
 }
@@ -181,6 +182,12 @@ class Context:
     @property
     def handle(self):
         return self._h
+
+    # all-pairs kernel selection (include/drephip.h DREPHIP_AP_*)
+    AP_AUTO, AP_TABLE, AP_BAND, AP_MERGE = 0, 1, 2, 3
+
+    def set_allpairs_path(self, path: int, band_cap: int = 1024) -> None:
+        check(lib().drephip_set_allpairs_path(self._h, path, band_cap), "drephip_set_allpairs_path")
 
     def set_timing(self, on: bool = True) -> None:
         check(lib().drephip_set_timing(self._h, 1 if on else 0), "drephip_set_timing")

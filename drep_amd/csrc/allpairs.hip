@@ -354,6 +354,321 @@ __global__ __launch_bounds__(256) void k_allpairs_merge(const uint64_t *__restri
     if (denom) denom[t] = (uint16_t)d;
 }
 
+// ------------------------------------------------------- banded all-pairs
+// Large sketches (s > 2048, up to kMaxSketch): a whole-row table no longer fits
+// LDS, so the hash range is cut into value bands per row tile.  Band k of a
+// tile of R rows is [lo_k, hi_k) with hi_k = min over rows of A_r[p_r + cap]
+// (p_r = the row's first element >= lo_k), so every row has <= cap elements in
+// the band; those get an LDS cuckoo table (same quotiented format as above,
+// storing the element's position *within the band*, at most cap - 1 < H - 1,
+// so the empty word still decodes to "absent").  Every column of the tile
+// keeps a cursor into its sketch (first element >= lo_k, in LDS); a wave
+// streams the column's elements in [lo_k, hi_k) in 64-element chunks and
+// counts, per row, shared elements whose union rank
+//     i + j - m_j < s          (i = p_r + band position, j = column position)
+// is below s -- the same rule as k_allpairs_q, with the running match count
+// m and the partial counts carried across bands in LDS.  Bands run until
+// every row is exhausted; column elements past the rows' largest element end
+// the last band.  Tables are rebuilt per band by the whole workgroup (every
+// key verified; up to kMaxFam field families, then the host falls back to the
+// literal merge); a band's build is amortised over kBandCols columns.
+// Roofline: as k_allpairs_q (LDS random reads + VALU); column chunks are read
+// once per band per tile, i.e. s * 8 / R bytes per pair from L2.
+constexpr uint32_t kBandCols = 256;
+constexpr uint32_t kBandB = 11;                       // H = 2048 slots per choice
+constexpr uint32_t kBandCapMax = (1u << kBandB) / 2;  // <= 1024 elements per row per band
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t w = __shfl_xor(v, o, 64);
+        v = w < v ? w : v;
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
+    return ((uint64_t)rfl((uint32_t)(v >> 32)) << 32) | rfl((uint32_t)v);
+}
+
+// One 64-element chunk of a column against the R band tables.  Returns the
+// number of chunk elements inside the band (< 64: the column's band segment
+// ends in this chunk).  mrun[r] (wave-uniform) and cntl[r] (per lane) carry
+// the running match count and the partial common count.
+template <int R, bool FAST>
+__device__ __forceinline__ uint32_t band_chunk(uint64_t b, uint32_t j, uint64_t hi, const uint64_t *T,
+                                               uint32_t fam, uint32_t s, const uint32_t (&pr)[R],
+                                               uint32_t actmask, uint32_t (&mrun)[R], uint32_t (&cntl)[R]) {
+    constexpr uint32_t H = 1u << kBandB, hm = H - 1;
+    const QFields qf = qfields(fam);
+    const bool inb = b < hi;
+    const uint32_t blo = (uint32_t)b;
+    uint64_t e1[R], e2[R];
+    if (FAST) {
+        const uint64_t *p1 = T + (uint64_t)(blo & hm) * R;
+        const uint64_t *p2 = T + (uint64_t)(H + ((blo >> 16) & hm)) * R;
+        if constexpr (R == 1) {
+            e1[0] = p1[0]; e2[0] = p2[0];
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; r += 2) {
+                const ulonglong2 v1 = *(const ulonglong2 *)(p1 + r);
+                const ulonglong2 v2 = *(const ulonglong2 *)(p2 + r);
+                e1[r] = v1.x; e1[r + 1] = v1.y; e2[r] = v2.x; e2[r + 1] = v2.y;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            e1[r] = T[(uint64_t)((uint32_t)(b >> qf.o1) & hm) * R + r];
+            e2[r] = T[(uint64_t)(H + ((uint32_t)(b >> qf.o2) & hm)) * R + r];
+        }
+    }
+    const uint64_t br1 = FAST ? b : rotr64(b, qf.o1);
+    const uint64_t br2 = rotr64(b, FAST ? 16 : qf.o2);
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        uint32_t li;
+        const bool found = q_match(e1[r], e2[r], br1, br2, hm, kBandCapMax, li) & inb &
+                           (((actmask >> r) & 1u) != 0);
+        const uint64_t m = __ballot(found);
+        if (m == 0) continue;                                      // wave-uniform
+        const uint32_t lim = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, s + mrun[r]));
+        cntl[r] += (uint32_t)found & (uint32_t)(pr[r] + li + j < lim);
+        mrun[r] += (uint32_t)__popcll(m);
+    }
+    return (uint32_t)__popcll(__ballot(inb));
+}
+
+// A column's band segment: the first NCH chunks from registers (loaded while
+// the previous column was processed); a segment longer than NCH chunks
+// continues from memory one chunk at a time.  Returns the new cursor.
+template <int R, int NCH, bool FAST>
+__device__ __forceinline__ uint32_t band_column(const uint64_t *__restrict__ Bc, uint32_t nB, uint32_t q,
+                                                const uint64_t (&seg)[NCH], uint64_t hi, const uint64_t *T,
+                                                uint32_t fam, uint32_t s, const uint32_t (&pr)[R],
+                                                uint32_t actmask, uint32_t (&mrun)[R], uint32_t (&cntl)[R]) {
+    const uint32_t lane = threadIdx.x & 63;
+    bool more = true;
+#pragma unroll
+    for (int k = 0; k < NCH; k++) {
+        if (!more) continue;                                       // wave-uniform
+        const uint32_t nin = band_chunk<R, FAST>(seg[k], q + lane, hi, T, fam, s, pr, actmask, mrun, cntl);
+        q += nin;
+        more = nin == 64;
+    }
+    if (!more) return q;
+    uint64_t b = q + lane < nB ? Bc[q + lane] : kEmpty;
+    for (;;) {
+        const uint32_t jn = q + 64 + lane;
+        const uint64_t bn = jn < nB ? Bc[jn] : kEmpty;
+        const uint32_t nin = band_chunk<R, FAST>(b, q + lane, hi, T, fam, s, pr, actmask, mrun, cntl);
+        q += nin;
+        if (nin < 64) break;
+        b = bn;
+    }
+    return q;
+}
+
+template <int R, int NCH, int WG>
+__global__ __launch_bounds__(WG) void k_allpairs_band(
+    const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ nhash, uint32_t s, uint32_t N,
+    uint32_t row1, uint32_t cap, const uint2 *__restrict__ items, uint16_t *__restrict__ common,
+    uint16_t *__restrict__ denom, uint64_t seg0, uint32_t *__restrict__ nfail) {
+    constexpr uint32_t H = 1u << kBandB, hm = H - 1, TS = 2 * H;
+    constexpr uint32_t NW = WG / 64;
+    extern __shared__ uint64_t lds[];
+    uint64_t *T = lds;                                               // R*TS, interleaved
+    uint32_t *cur = (uint32_t *)(T + (uint64_t)R * TS);              // [kBandCols] column cursors
+    uint32_t *pcnt = cur + kBandCols;                                // [R][kBandCols] counts
+    uint32_t *pm = pcnt + R * kBandCols;                             // [R][kBandCols] shared so far
+    __shared__ uint32_t s_p[R], s_q[R];
+    __shared__ uint64_t s_hi;
+    __shared__ int s_done, s_fail, s_abort;
+
+    const uint32_t i0 = items[blockIdx.x].x;
+    const uint32_t c0 = items[blockIdx.x].y;
+    const uint32_t nrows = min((uint32_t)R, row1 - i0);
+    const uint32_t cend = min(c0 + kBandCols, N);
+    const uint32_t ncols = cend - c0;
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+
+    uint32_t nA[R];
+    bool any_partial_row = false;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        nA[r] = (uint32_t)r < nrows ? nhash[i0 + r] : 0;
+        any_partial_row |= (uint32_t)r < nrows && nA[r] < s;
+    }
+    // largest element over the tile's rows: column elements past it cannot match
+    uint64_t maxlast = 0;
+#pragma unroll
+    for (int r = 0; r < R; r++)
+        if (nA[r]) { const uint64_t v = hashes[(uint64_t)(i0 + r) * s + nA[r] - 1]; maxlast = v > maxlast ? v : maxlast; }
+    for (uint32_t k = tid; k < kBandCols; k += WG) cur[k] = 0;
+    for (uint32_t k = tid; k < R * kBandCols; k += WG) { pcnt[k] = 0; pm[k] = 0; }
+    if (tid < (uint32_t)R) s_p[tid] = 0;
+    if (tid == 0) s_abort = 0;
+
+    for (;;) {
+        __syncthreads();
+        if (wave == 0) {
+            // band bound: the (cap+1)-th remaining element of the tightest row
+            uint64_t v = kEmpty;
+            bool left = false;
+            if (lane < (uint32_t)R && lane < nrows) {
+                uint32_t nl = 0;
+#pragma unroll
+                for (int r = 0; r < R; r++) if ((uint32_t)r == lane) nl = nA[r];
+                const uint32_t p = s_p[lane];
+                left = p < nl;
+                if (p + cap < nl) v = hashes[(uint64_t)(i0 + lane) * s + p + cap];
+            }
+            v = wave_min_u64(v);
+            const bool any_left = __ballot(left) != 0;
+            if (lane == 0) {
+                s_hi = v < maxlast + 1 ? v : maxlast + 1;
+                s_done = !any_left;
+                s_fail = 0;
+            }
+            if (lane < (uint32_t)R) s_q[lane] = 0;
+        }
+        __syncthreads();
+        if (s_done) break;
+        const uint64_t hi = s_hi;
+        uint32_t pr[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) pr[r] = s_p[r];
+
+        // ---- build the R band tables (quotiented cuckoo, band positions)
+        uint32_t fam = 0;
+        for (; fam < kMaxFam; fam++) {
+            const QFields qf = qfields(fam);
+            const uint64_t F1 = (uint64_t)hm << qf.o1, F2 = (uint64_t)hm << qf.o2;
+            for (uint32_t k = tid; k < R * TS; k += WG) T[k] = kEmpty;
+            if (tid == 0) s_fail = 0;
+            __syncthreads();
+            for (uint32_t idx = tid; idx < R * cap; idx += WG) {
+                const uint32_t r = idx / cap, t = idx - r * cap;
+                uint32_t p = 0, nl = 0;
+#pragma unroll
+                for (int rr = 0; rr < R; rr++) if ((uint32_t)rr == r) { p = pr[rr]; nl = nA[rr]; }
+                if (p + t >= nl) continue;
+                uint64_t x = hashes[(uint64_t)(i0 + r) * s + p + t];
+                if (x >= hi) continue;
+                uint32_t ix = t;
+                uint32_t pos = (uint32_t)(x >> qf.o1) & hm;
+                bool placed = false;
+                for (int kick = 0; kick < 96; kick++) {
+                    const bool second = pos >= H;
+                    const uint64_t e = second ? ((x & ~F2) | ((uint64_t)ix << qf.o2))
+                                              : ((x & ~F1) | ((uint64_t)ix << qf.o1));
+                    const unsigned long long oldr = atomicExch((unsigned long long *)&T[(uint64_t)pos * R + r],
+                                                               (unsigned long long)rotr64(e, second ? qf.o2 : qf.o1));
+                    if (oldr == kEmpty) { placed = true; break; }
+                    const uint64_t old = rotr64(oldr, 64 - (second ? qf.o2 : qf.o1));
+                    const uint32_t lp = second ? pos - H : pos;
+                    if (second) { ix = (uint32_t)(old >> qf.o2) & hm; x = (old & ~F2) | ((uint64_t)lp << qf.o2); }
+                    else        { ix = (uint32_t)(old >> qf.o1) & hm; x = (old & ~F1) | ((uint64_t)lp << qf.o1); }
+                    pos = second ? ((uint32_t)(x >> qf.o1) & hm) : (H + ((uint32_t)(x >> qf.o2) & hm));
+                }
+                if (!placed) s_fail = 1;
+            }
+            __syncthreads();
+            // verify every key of the band; count the band's elements per row
+            for (uint32_t idx = tid; idx < R * cap; idx += WG) {
+                const uint32_t r = idx / cap, t = idx - r * cap;
+                uint32_t p = 0, nl = 0;
+#pragma unroll
+                for (int rr = 0; rr < R; rr++) if ((uint32_t)rr == r) { p = pr[rr]; nl = nA[rr]; }
+                if (p + t >= nl) continue;
+                const uint64_t x = hashes[(uint64_t)(i0 + r) * s + p + t];
+                if (x >= hi) continue;
+                const uint64_t e1 = rotr64(T[(uint64_t)((uint32_t)(x >> qf.o1) & hm) * R + r], 64 - qf.o1);
+                const uint64_t e2 = rotr64(T[(uint64_t)(H + ((uint32_t)(x >> qf.o2) & hm)) * R + r], 64 - qf.o2);
+                const bool ok1 = (e1 & ~F1) == (x & ~F1) && ((uint32_t)(e1 >> qf.o1) & hm) == t;
+                const bool ok2 = (e2 & ~F2) == (x & ~F2) && ((uint32_t)(e2 >> qf.o2) & hm) == t;
+                if (!(ok1 || ok2)) s_fail = 1;
+                if (fam == 0) atomicAdd(&s_q[r], 1u);
+            }
+            __syncthreads();
+            if (!s_fail) break;
+        }
+        if (fam == kMaxFam) {                       // no field family worked: host reruns with the merge kernel
+            if (tid == 0) { s_abort = 1; atomicAdd(nfail, 1u); }
+            break;
+        }
+
+        // ---- columns: wave w takes columns w, w+NW, ...; next column's first chunk prefetched
+        uint32_t ci = wave;
+        uint64_t nseg[NCH];
+        uint32_t nq = 0, nnB = 0;
+        auto load_seg = [&](uint32_t cc) {
+            nq = rfl(cur[cc]);
+            nnB = nhash[c0 + cc];
+            const uint64_t *Bn = hashes + (uint64_t)(c0 + cc) * s;
+#pragma unroll
+            for (int k = 0; k < NCH; k++) {
+                const uint32_t j = nq + 64 * k + lane;
+                nseg[k] = j < nnB ? Bn[j] : kEmpty;
+            }
+        };
+        if (ci < ncols) load_seg(ci);
+        for (; ci < ncols; ci += NW) {
+            const uint32_t c = c0 + ci;
+            const uint32_t q0 = nq, nB = nnB;
+            uint64_t seg[NCH];
+#pragma unroll
+            for (int k = 0; k < NCH; k++) seg[k] = nseg[k];
+            if (ci + NW < ncols) load_seg(ci + NW);
+            uint32_t actmask = 0;
+#pragma unroll
+            for (int r = 0; r < R; r++) actmask |= (uint32_t)((uint32_t)r < nrows && i0 + r < c) << r;
+            if (!actmask) continue;
+            uint32_t mrun[R], cntl[R];
+#pragma unroll
+            for (int r = 0; r < R; r++) { mrun[r] = rfl(pm[r * kBandCols + ci]); cntl[r] = 0; }
+            const uint64_t *Bc = hashes + (uint64_t)c * s;
+            const uint32_t q = fam == 0
+                ? band_column<R, NCH, true>(Bc, nB, q0, seg, hi, T, fam, s, pr, actmask, mrun, cntl)
+                : band_column<R, NCH, false>(Bc, nB, q0, seg, hi, T, fam, s, pr, actmask, mrun, cntl);
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const uint32_t cc = wave_sum(cntl[r]);
+                if (lane == 0) { pcnt[r * kBandCols + ci] += cc; pm[r * kBandCols + ci] = mrun[r]; }
+            }
+            if (lane == 0) cur[ci] = q;
+        }
+        __syncthreads();
+        if (tid < (uint32_t)R) s_p[tid] += s_q[tid];
+    }
+    __syncthreads();
+    if (s_abort) return;
+    for (uint32_t r = 0; r < nrows; r++) {
+        const uint32_t i = i0 + r;
+        const uint32_t cs = max(c0, i + 1);
+        if (cs >= cend) continue;
+        uint32_t nl = 0;
+#pragma unroll
+        for (int rr = 0; rr < R; rr++) if ((uint32_t)rr == r) nl = nA[rr];
+        const uint64_t base = cond_index(i, cs, N) - seg0;
+        for (uint32_t t = tid; t < cend - cs; t += WG) {
+            const uint32_t ci = cs - c0 + t;
+            common[base + t] = (uint16_t)pcnt[r * kBandCols + ci];
+            if (denom) {
+                const uint32_t nB = nhash[cs + t];
+                uint32_t dd = s;
+                if (any_partial_row || nB < s) {
+                    const uint32_t u = nl + nB - pm[r * kBandCols + ci];
+                    dd = u < s ? u : s;
+                }
+                denom[base + t] = (uint16_t)dd;
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------- host driver
 static int launch_merge(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N,
                         uint64_t seg0, uint64_t npairs, uint16_t *d_common, uint16_t *d_denom,
@@ -365,6 +680,48 @@ static int launch_merge(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32
     timing_mark(ctx, 2, st, false);
     HIPC(hipGetLastError());
     HIPC(hipStreamSynchronize(st));
+    return DREPHIP_OK;
+}
+
+static int launch_band(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N,
+                       uint32_t row0, uint32_t row1, uint64_t seg0, uint64_t npairs, uint16_t *d_common,
+                       uint16_t *d_denom, hipStream_t st) {
+    constexpr int R = 4;
+    const uint32_t cap = std::min(std::max(ctx->band_cap, 1u), kBandCapMax);
+    std::vector<uint2> items;
+    for (uint32_t i0 = row0; i0 < row1; i0 += R)
+        for (uint32_t c0 = i0 + 1; c0 < N; c0 += kBandCols) items.push_back(make_uint2(i0, c0));
+    if (items.empty()) return DREPHIP_OK;
+    uint2 *d_items;
+    uint32_t *d_nfail;
+    int rc;
+    if ((rc = scratch(ctx, "apb_items", items.size() * sizeof(uint2), (void **)&d_items))) return rc;
+    if ((rc = scratch(ctx, "ap_nfail", 4, (void **)&d_nfail))) return rc;
+    HIPC(hipMemsetAsync(d_nfail, 0, 4, st));
+    HIPC(hipMemcpyAsync(d_items, items.data(), items.size() * sizeof(uint2), hipMemcpyHostToDevice, st));
+    const size_t lds = (size_t)R * (2u << kBandB) * 8 + kBandCols * 4 + 2ull * R * kBandCols * 4;
+    // geometry: 16 waves x 8 register chunks (default) or 8 waves x 16 chunks
+    // (DREPHIP_BAND_GEOM=1, A/B); one workgroup per CU either way (LDS)
+    const char *geom = getenv("DREPHIP_BAND_GEOM");
+    const bool wide = geom && geom[0] == '1';
+    if (!wide) {
+        HIPC(hipFuncSetAttribute((const void *)k_allpairs_band<R, 8, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        timing_mark(ctx, 2, st, true);
+        hipLaunchKernelGGL((k_allpairs_band<R, 8, 1024>), dim3((uint32_t)items.size()), dim3(1024), lds, st, d_hashes,
+                           d_nhash, ctx->s, N, row1, cap, d_items, d_common, d_denom, seg0, d_nfail);
+    } else {
+        HIPC(hipFuncSetAttribute((const void *)k_allpairs_band<R, 16, 512>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        timing_mark(ctx, 2, st, true);
+        hipLaunchKernelGGL((k_allpairs_band<R, 16, 512>), dim3((uint32_t)items.size()), dim3(512), lds, st, d_hashes,
+                           d_nhash, ctx->s, N, row1, cap, d_items, d_common, d_denom, seg0, d_nfail);
+    }
+    timing_mark(ctx, 2, st, false);
+    HIPC(hipGetLastError());
+    uint32_t nfail = 0;
+    HIPC(hipMemcpyAsync(&nfail, d_nfail, 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    if (nfail)   // a band table could not be built with any field pair: exact merge kernel instead
+        return launch_merge(ctx, d_hashes, d_nhash, N, seg0, npairs, d_common, d_denom, st);
     return DREPHIP_OK;
 }
 
@@ -396,8 +753,17 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
     uint32_t B = 4;
     while ((1u << B) < 2 * s) B++;
     const uint64_t TS = 2ull << B;
-    if (force_merge || s > 2048 || TS * 8 > kLdsTables)
+    const bool fits = s <= 2048 && TS * 8 <= kLdsTables;
+    int path = force_merge ? DREPHIP_AP_MERGE : ctx->ap_path;
+    if (path == DREPHIP_AP_AUTO) path = fits ? DREPHIP_AP_TABLE : DREPHIP_AP_BAND;
+    if (path == DREPHIP_AP_TABLE && !fits) {
+        set_error("whole-row table all-pairs kernel needs s <= 2048");
+        return DREPHIP_ERR_UNSUPPORTED;
+    }
+    if (path == DREPHIP_AP_MERGE)
         return launch_merge(ctx, d_hashes, d_nhash, N, seg0, npairs, d_common, d_denom, st);
+    if (path == DREPHIP_AP_BAND)
+        return launch_band(ctx, d_hashes, d_nhash, N, row0, row1, seg0, npairs, d_common, d_denom, st);
 
     const uint32_t nrows = row1 - row0;
     uint64_t *d_tabs;

@@ -157,6 +157,15 @@ DREPHIP_EXPORT int drephip_set_timing(drephip_ctx *ctx, int enable) {
     return DREPHIP_OK;
 }
 
+DREPHIP_EXPORT int drephip_set_allpairs_path(drephip_ctx *ctx, int path, uint32_t band_cap) {
+    if (!ctx) { set_error("null context"); return DREPHIP_ERR_ARG; }
+    if (path < DREPHIP_AP_AUTO || path > DREPHIP_AP_MERGE) { set_error("unknown all-pairs path"); return DREPHIP_ERR_ARG; }
+    if (band_cap < 1 || band_cap > 1024) { set_error("band_cap must be in 1..1024"); return DREPHIP_ERR_ARG; }
+    ctx->ap_path = path;
+    ctx->band_cap = band_cap;
+    return DREPHIP_OK;
+}
+
 DREPHIP_EXPORT int drephip_last_kernel_ms(drephip_ctx *ctx, int which, double *ms, int *launches) {
     if (!ctx || which < 0 || which > 3 || !ms) { set_error("bad argument"); return DREPHIP_ERR_ARG; }
     *ms = ctx->kms[which];

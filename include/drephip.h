@@ -156,6 +156,20 @@ int drephip_allpairs_merge_device(drephip_ctx *ctx, const uint64_t *d_hashes, co
  * Reference: the "dist" column of MASH_table.tsv parsed at d_cluster.py:581. */
 int drephip_distance_lut(int k, uint32_t denom, double *lut /* denom+1 */);
 
+/* All-pairs kernel selection (no CPU path exists; every choice is a HIP kernel
+ * with the same bit-exact result):
+ *   DREPHIP_AP_AUTO  whole-row LDS tables for s <= 2048, value bands above;
+ *   DREPHIP_AP_TABLE k_allpairs_q (s <= 2048);
+ *   DREPHIP_AP_BAND  k_allpairs_band, band_cap (1..1024) elements per row per
+ *                    band (the default 1024 is the production setting; small
+ *                    caps exercise many bands on small sketches in tests);
+ *   DREPHIP_AP_MERGE k_allpairs_merge (literal merge, cross-check only). */
+#define DREPHIP_AP_AUTO 0
+#define DREPHIP_AP_TABLE 1
+#define DREPHIP_AP_BAND 2
+#define DREPHIP_AP_MERGE 3
+int drephip_set_allpairs_path(drephip_ctx *ctx, int path, uint32_t band_cap);
+
 /* Enable (1) / disable (0) HIP-event timing of every kernel launch. */
 int drephip_set_timing(drephip_ctx *ctx, int enable);
 

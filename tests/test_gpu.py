@@ -205,13 +205,73 @@ def test_allpairs_partial_sketches_vs_oracle(ctx1000):
     assert np.array_equal(c, oc) and np.array_equal(d, od)
 
 
-@pytest.mark.parametrize("s", [1, 16, 100, 513, 1024, 1025, 2048, 4096])
+@pytest.mark.parametrize("s", [1, 16, 100, 513, 1024, 1025, 2048, 2049, 4096, 10000, 12000])
 def test_allpairs_sketch_sizes(s):
     h, nh = oracle.sketch_synth(0, 48, 120_000, seed=s, family_size=12, s=s, threads=8)
     with _lib.Context(0, 21, s, 42) as ctx:
         c, d = ctx.allpairs(h, nh)
     oc, od = oracle.allpairs(h, nh, s, threads=8)
     assert np.array_equal(c, oc) and np.array_equal(d, od)
+
+
+@pytest.mark.parametrize("s,cap", [(1, 1), (100, 7), (1000, 64), (1000, 1024), (4096, 300),
+                                   (10000, 1024), (12000, 1000)])
+def test_allpairs_band_kernel_vs_oracle(s, cap):
+    """Value-banded kernel (production path for s > 2048): many bands per row
+    tile at small caps, bit-exact counts and denominators."""
+    h, nh = oracle.sketch_synth(0, 40, 150_000, seed=s + cap, family_size=10, s=s, threads=8)
+    with _lib.Context(0, 21, s, 42) as ctx:
+        ctx.set_allpairs_path(ctx.AP_BAND, cap)
+        c, d = ctx.allpairs(h, nh, want_denom=True)
+    oc, od = oracle.allpairs(h, nh, s, threads=8)
+    assert np.array_equal(c, oc) and np.array_equal(d, od)
+    if s >= 1000:
+        assert c.max() > s // 2
+
+
+def test_allpairs_band_partial_and_segments(family, ctx1000):
+    """Band kernel on partial sketches (denominator from the full intersection)
+    and on row-range segments."""
+    import torch
+    rng = np.random.default_rng(11)
+    A = np.frombuffer(b"ACGT", dtype=np.uint8)
+    base = A[rng.integers(0, 4, 300_000)]
+    recs = []
+    for i in range(36):
+        L = int(rng.choice([0, 60, 300, 700, 1200, 5000, 300_000]))
+        x = base[:L].copy()
+        m = rng.random(L) < rng.choice([0.0, 0.01, 0.05])
+        x[m] = A[rng.integers(0, 4, int(m.sum()))]
+        recs.append(x)
+    seq = np.concatenate(recs)
+    rec_off = np.concatenate([[0], np.cumsum([len(r) for r in recs])]).astype(np.uint64)
+    gro = np.arange(len(recs) + 1, dtype=np.uint64)
+    with _lib.Context(0, 21, S, 42) as ctx:
+        h, nh, _ = ctx.sketch_records(seq, rec_off, gro)
+        assert (nh < S).any() and (nh == S).any() and (nh == 0).any()
+        ctx.set_allpairs_path(ctx.AP_BAND, 50)
+        c, d = ctx.allpairs(h, nh, want_denom=True)
+        oc, od = oracle.allpairs(h, nh, S)
+        assert np.array_equal(c, oc) and np.array_equal(d, od)
+        # row segments of the family set, band path
+        h, nh = family
+        N = len(nh)
+        dh = torch.from_numpy(h.view(np.int64)).cuda()
+        dn = torch.from_numpy(nh.view(np.int32)).cuda()
+        oc, _ = oracle.allpairs(h, nh, S, threads=8)
+        full = np.zeros(N * (N - 1) // 2, np.uint16)
+
+        def start(i):
+            return i * N - i * (i + 1) // 2
+
+        ctx.set_allpairs_path(ctx.AP_BAND, 200)
+        for r0, r1 in zip([0, 3, 61, N - 2], [3, 61, N - 2, N]):
+            n = start(min(r1, N - 1)) - start(r0)
+            out = torch.zeros(n, dtype=torch.int16, device="cuda")
+            ctx.allpairs_device(dh.data_ptr(), dn.data_ptr(), N, r0, r1, out.data_ptr(), None,
+                                torch.cuda.current_stream().cuda_stream)
+            full[start(r0):start(r0) + n] = out.cpu().numpy().view(np.uint16)
+        assert np.array_equal(full, oc)
 
 
 def test_allpairs_row_segments_and_merge_kernel(family, ctx1000):

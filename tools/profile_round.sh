@@ -1,7 +1,8 @@
 #!/bin/bash
 # Collects the round's profiles on the GPU box (run from the repo root):
-#   kernel trace + stats of the default bench, and HBM traffic PMC passes
-#   (FETCH_SIZE and WRITE_SIZE in separate passes, MI355X_MICROARCH.md HBM).
+#   kernel trace + stats of the default bench, HBM traffic PMC passes
+#   (FETCH_SIZE and WRITE_SIZE in separate passes, MI355X_MICROARCH.md HBM),
+#   and SQ issue/stall counter passes (<= 8 SQ + 2 GRBM counters per pass).
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-.}
 export TMPDIR=/tmp
@@ -15,3 +16,11 @@ for c in FETCH_SIZE WRITE_SIZE; do
       python bench.py --steps 1 --warmup 0 --cpu-baseline 0 > $OUT/pmc_$c.json 2> $OUT/pmc_$c.err || exit 1
 done
 python3 tools/traffic_json.py $OUT ${GENOMES:-1000} ${GENOME_BP:-5000000} > $OUT/sketch_traffic.json || exit 1
+i=0
+for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_INSTS_SMEM GRBM_GUI_ACTIVE" \
+           "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
+           "SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/sq$i -o pmc -- \
+      python bench.py --steps 1 --warmup 0 --cpu-baseline 0 > $OUT/sq$i.json 2> $OUT/sq$i.err || exit 1
+done

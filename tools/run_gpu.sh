@@ -1,5 +1,8 @@
 #!/bin/bash
 # GPU-box check used during development: parity tests, then the default bench.
 cd ${GRAFT_REPO_ROOT:-.}
-timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/gpu_tests.log 2>&1 || { echo "tests failed"; exit 1; }
-timeout -k 10 300 python bench.py > gpurun_out/bench.log 2> gpurun_out/bench.err || { echo "bench failed"; exit 1; }
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/gpu_tests.log; exit 1; }
+tail -3 gpurun_out/gpu_tests.log
+timeout -k 10 300 python bench.py > gpurun_out/bench.log 2> gpurun_out/bench.err || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }
+cat gpurun_out/bench.log
