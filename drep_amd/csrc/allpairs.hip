@@ -28,6 +28,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 namespace drephip {
@@ -44,11 +46,6 @@ __host__ __device__ __forceinline__ uint64_t cond_index(uint64_t i, uint64_t j, 
     return i * N - i * (i + 1) / 2 + (j - i - 1);
 }
 
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
 
 // ------------------------------------------------------- row tables
 // Quotiented two-choice cuckoo table: choice 1 sits at T[f1(x)], choice 2 at
@@ -134,24 +131,65 @@ __global__ __launch_bounds__(256) void k_build_qcuckoo(const uint64_t *__restric
     if (threadIdx.x == 0) { fam_out[r] = 0xFF; atomicAdd(nfail, 1u); }
 }
 
-// Membership test of B element b (this lane) against a row table, from the
-// two slot words e1 = Tr[s1], e2 = Tr[H + s2] (read beforehand for every row
-// of the chunk so the 2R LDS reads are in flight together).  Branch-free: the
-// match tests are integer xor/or, i is one select.
-// FAST: family 0 (fields at bits [0,B) and [16,16+B)); otherwise generic
-// 64-bit field shifts.
 // Slot words are stored rotated right by their field offset (field at bits
 // [0, B)), so slot k holds b iff (e_k ^ rotr(b, o_k)) <= 2^B - 1, and the
-// field -- b's sketch position i in A -- is e_k & hm.  br_k = rotr(b, o_k) is
-// per chunk (FAST, family 0: o = 0 and 16 for every row) or per row.  Bitwise
-// |/& keep it branch-free.  The empty word (all ones) matches only the
-// all-ones padding key and decodes to i = 2^B - 1 >= nA, so `found` is exact.
-__device__ __forceinline__ bool q_match(uint64_t e1, uint64_t e2, uint64_t br1, uint64_t br2, uint32_t hm,
-                                        uint32_t nA, uint32_t &i) {
-    const bool m1 = (e1 ^ br1) <= (uint64_t)hm;
-    const bool m2 = (e2 ^ br2) <= (uint64_t)hm;
-    i = (m1 ? (uint32_t)e1 : (uint32_t)e2) & hm;
-    return (m1 | m2) & (i < nA);
+// field -- b's sketch position i in A -- is e_k & hm.  The empty word (all
+// ones) matches only the all-ones padding key and decodes to 2^B - 1, past
+// every real position, so the ilim test below keeps `found` exact.
+// One 64-element chunk of column elements (one per lane; position j) against
+// R row tables, with wave-level lane masks kept in SGPRs: per row the two
+// slot words are compared and their ballots OR-ed; only a row with a match in
+// the chunk (uniform branch) selects i, checks it against ilim (the empty
+// word decodes past it) and applies the union-rank rule
+//     i + j < s + mrun + (matches in lower lanes)
+// with scalar popcounts -- counts stay in SGPRs, no per-lane reduction.
+// i = ibase[r] + field.  lanemask drops lanes (band kernel: outside the band).
+// Row tables are interleaved in LDS (slot k of row r at k*R + r), so in the
+// FAST layout (family 0 for every row) one slot address serves all R rows:
+// R/2 ds_read_b128 per choice.
+template <int R, bool FAST>
+__device__ __forceinline__ void probe_chunk(uint64_t b, uint32_t j, const uint64_t *T, uint32_t H, uint32_t hm,
+                                            const uint32_t (&o1)[R], const uint32_t (&o2)[R], uint32_t actmask,
+                                            uint64_t lanemask, const uint32_t (&ibase)[R],
+                                            const uint32_t (&ilim)[R], uint32_t s, uint32_t (&mrun)[R],
+                                            uint32_t (&cnt)[R]) {
+    const uint32_t blo = (uint32_t)b;
+    uint64_t e1[R], e2[R];
+    if (FAST) {
+        const uint64_t *p1 = T + (uint64_t)(blo & hm) * R;
+        const uint64_t *p2 = T + (uint64_t)(H + ((blo >> 16) & hm)) * R;
+        if constexpr (R == 1) {
+            e1[0] = p1[0]; e2[0] = p2[0];
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; r += 2) {
+                const ulonglong2 v1 = *(const ulonglong2 *)(p1 + r);
+                const ulonglong2 v2 = *(const ulonglong2 *)(p2 + r);
+                e1[r] = v1.x; e1[r + 1] = v1.y; e2[r] = v2.x; e2[r + 1] = v2.y;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < R; r++) {                                // inactive rows read empty words
+            e1[r] = T[(uint64_t)((uint32_t)(b >> o1[r]) & hm) * R + r];
+            e2[r] = T[(uint64_t)(H + ((uint32_t)(b >> o2[r]) & hm)) * R + r];
+        }
+    }
+    const uint64_t b16 = rotr64(b, 16);                              // family 0's second field
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        if (!((actmask >> r) & 1u)) continue;                        // wave-uniform
+        const bool c1 = (e1[r] ^ (FAST ? b : rotr64(b, o1[r]))) <= (uint64_t)hm;
+        const bool c2 = (e2[r] ^ (FAST ? b16 : rotr64(b, o2[r]))) <= (uint64_t)hm;
+        uint64_t m = (__builtin_amdgcn_ballot_w64(c1) | __builtin_amdgcn_ballot_w64(c2)) & lanemask;
+        if (m == 0) continue;                                        // wave-uniform: no shared hash here
+        const uint32_t f = (c1 ? (uint32_t)e1[r] : (uint32_t)e2[r]) & hm;
+        m &= __builtin_amdgcn_ballot_w64(f < ilim[r]);
+        const uint32_t lim = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, s + mrun[r]));
+        cnt[r] += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(ibase[r] + f + j < lim) & m);
+        mrun[r] += (uint32_t)__popcll(m);
+    }
 }
 
 // The columns of one work item, processed by one wave (double-buffered column
@@ -183,74 +221,36 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
         }
         const uint32_t nB = nhash[c];
         const bool partial = any_partial_row || nB < s;
-        uint32_t cnt[R], mrun[R];
+        uint32_t cnt[R], mrun[R], actmask = 0;
+        // elements past every active row's largest hash cannot match: the
+        // scan ends at the first chunk whose smallest element is past them
+        uint64_t amax = 0;
 #pragma unroll
-        for (int r = 0; r < R; r++) { cnt[r] = 0; mrun[r] = 0; }
+        for (int r = 0; r < R; r++) {
+            cnt[r] = 0; mrun[r] = 0;
+            const bool act = (uint32_t)r < nrows && i0 + r < c;
+            actmask |= (uint32_t)act << r;
+            if (act) amax = alast[r] > amax ? alast[r] : amax;
+        }
+        uint32_t zero[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) zero[r] = 0;
         bool alive = true;
 #pragma unroll
         for (int k = 0; k < NCH; k++) {
             if (!alive || k >= (int)nch) continue;                        // wave-uniform
             const uint64_t b = cur[k];
-            // smallest element of the chunk (lane 0); elements past every
-            // active row's largest hash cannot match -- end of the scan
-            // (readfirstlane returns int: go through uint32_t so the low word
-            // is not sign-extended into the high one)
+            // smallest element of the chunk (lane 0; readfirstlane returns
+            // int: through uint32_t so the low word is not sign-extended)
             const uint64_t b0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
                                 (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
-            bool more = false;
-#pragma unroll
-            for (int r = 0; r < R; r++)
-                if ((uint32_t)r < nrows && i0 + r < c) more |= b0 <= alast[r];
-            if (b0 == kEmpty || !more) { alive = false; continue; }
-            const uint32_t j = k * 64 + lane;
-            const uint32_t blo = (uint32_t)b;
-            const uint64_t b16 = rotr64(b, 16);                          // family 0's second field
-            // row tables are interleaved in LDS (slot k of row r at k*R + r), so
-            // one slot address serves all R rows: R/2 ds_read_b128 per choice
-            uint64_t e1[R], e2[R];
-            if (FAST) {
-                const uint64_t *p1 = T + (uint64_t)(blo & hm) * R;
-                const uint64_t *p2 = T + (uint64_t)(H + ((blo >> 16) & hm)) * R;
-                if constexpr (R == 1) {
-                    e1[0] = p1[0]; e2[0] = p2[0];
-                } else {
-#pragma unroll
-                    for (int r = 0; r < R; r += 2) {
-                        const ulonglong2 v1 = *(const ulonglong2 *)(p1 + r);
-                        const ulonglong2 v2 = *(const ulonglong2 *)(p2 + r);
-                        e1[r] = v1.x; e1[r + 1] = v1.y; e2[r] = v2.x; e2[r + 1] = v2.y;
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int r = 0; r < R; r++) {                            // rows past nrows read empty words
-                    e1[r] = T[(uint64_t)((uint32_t)(b >> o1[r]) & hm) * R + r];
-                    e2[r] = T[(uint64_t)(H + ((uint32_t)(b >> o2[r]) & hm)) * R + r];
-                }
-            }
-            // every row is tested unconditionally (no branch for the reads to
-            // sink into); an inactive row (past nrows, or not above the
-            // diagonal) has found = false, so its ballot is 0 and it is skipped
-#pragma unroll
-            for (int r = 0; r < R; r++) {
-                uint32_t i;
-                const bool act = (uint32_t)r < nrows && i0 + r < c;       // wave-uniform
-                const bool found = (FAST ? q_match(e1[r], e2[r], b, b16, hm, nA[r], i)
-                                         : q_match(e1[r], e2[r], rotr64(b, o1[r]), rotr64(b, o2[r]), hm, nA[r], i)) &
-                                   act;
-                const uint64_t m = __ballot(found);
-                if (m == 0) continue;                                    // wave-uniform: no shared hash here
-                // s + matches below this lane (running count + in-chunk prefix)
-                const uint32_t lim = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, s + mrun[r]));
-                cnt[r] += (uint32_t)found & (uint32_t)(i + j < lim);
-                mrun[r] += (uint32_t)__popcll(m);
-            }
+            if (b0 == kEmpty || b0 > amax) { alive = false; continue; }
+            probe_chunk<R, FAST>(b, k * 64 + lane, T, H, hm, o1, o2, actmask, ~0ull, zero, nA, s, mrun, cnt);
         }
 #pragma unroll
         for (int r = 0; r < R; r++) {
             if ((uint32_t)r >= nrows || i0 + r >= c) continue;
-            const uint32_t cc = wave_sum(cnt[r]);
+            const uint32_t cc = cnt[r];
             uint32_t dd = s;
             if (partial) {
                 const uint32_t u = nA[r] + nB - mrun[r];      // |A u B|; mrun = |A n B| when partial
@@ -270,7 +270,7 @@ __global__ __launch_bounds__(ap_wg(NCH)) void k_allpairs_q(
     uint32_t row0, uint32_t row1, uint32_t B, const uint2 *__restrict__ items,
     uint16_t *__restrict__ common, uint16_t *__restrict__ denom, uint64_t seg0) {
     constexpr int WG = ap_wg(NCH);
-    extern __shared__ uint64_t lds[];
+    extern __shared__ __align__(16) uint64_t lds[];    // 16-B aligned: the tables are read with ds_read_b128
     const uint32_t H = 1u << B, hm = H - 1, TS = 2 * H;
     uint64_t *T = lds;
     uint16_t *res_c = (uint16_t *)(lds + (uint64_t)R * TS);
@@ -386,59 +386,32 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
     }
     return v;
 }
+// Column element j (kEmpty past nB): an unconditional load clamped to the
+// row (no branch around it), then a select.
+__device__ __forceinline__ uint64_t ld_col(const uint64_t *__restrict__ Bc, uint32_t j, uint32_t nB, uint32_t s) {
+    const uint64_t v = Bc[j < s ? j : s - 1];
+    return j < nB ? v : kEmpty;
+}
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint64_t rfl64(uint64_t v) {
     return ((uint64_t)rfl((uint32_t)(v >> 32)) << 32) | rfl((uint32_t)v);
 }
 
-// One 64-element chunk of a column against the R band tables.  Returns the
+// One 64-element chunk of a column inside the current band.  Returns the
 // number of chunk elements inside the band (< 64: the column's band segment
-// ends in this chunk).  mrun[r] (wave-uniform) and cntl[r] (per lane) carry
-// the running match count and the partial common count.
+// ends in this chunk).
 template <int R, bool FAST>
 __device__ __forceinline__ uint32_t band_chunk(uint64_t b, uint32_t j, uint64_t hi, const uint64_t *T,
-                                               uint32_t fam, uint32_t s, const uint32_t (&pr)[R],
-                                               uint32_t actmask, uint32_t (&mrun)[R], uint32_t (&cntl)[R]) {
+                                               const uint32_t (&o1)[R], const uint32_t (&o2)[R], uint32_t s,
+                                               const uint32_t (&pr)[R], uint32_t actmask, uint32_t (&mrun)[R],
+                                               uint32_t (&cnt)[R]) {
     constexpr uint32_t H = 1u << kBandB, hm = H - 1;
-    const QFields qf = qfields(fam);
-    const bool inb = b < hi;
-    const uint32_t blo = (uint32_t)b;
-    uint64_t e1[R], e2[R];
-    if (FAST) {
-        const uint64_t *p1 = T + (uint64_t)(blo & hm) * R;
-        const uint64_t *p2 = T + (uint64_t)(H + ((blo >> 16) & hm)) * R;
-        if constexpr (R == 1) {
-            e1[0] = p1[0]; e2[0] = p2[0];
-        } else {
+    uint32_t cap[R];
 #pragma unroll
-            for (int r = 0; r < R; r += 2) {
-                const ulonglong2 v1 = *(const ulonglong2 *)(p1 + r);
-                const ulonglong2 v2 = *(const ulonglong2 *)(p2 + r);
-                e1[r] = v1.x; e1[r + 1] = v1.y; e2[r] = v2.x; e2[r + 1] = v2.y;
-            }
-        }
-    } else {
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-            e1[r] = T[(uint64_t)((uint32_t)(b >> qf.o1) & hm) * R + r];
-            e2[r] = T[(uint64_t)(H + ((uint32_t)(b >> qf.o2) & hm)) * R + r];
-        }
-    }
-    const uint64_t br1 = FAST ? b : rotr64(b, qf.o1);
-    const uint64_t br2 = rotr64(b, FAST ? 16 : qf.o2);
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-        uint32_t li;
-        const bool found = q_match(e1[r], e2[r], br1, br2, hm, kBandCapMax, li) & inb &
-                           (((actmask >> r) & 1u) != 0);
-        const uint64_t m = __ballot(found);
-        if (m == 0) continue;                                      // wave-uniform
-        const uint32_t lim = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, s + mrun[r]));
-        cntl[r] += (uint32_t)found & (uint32_t)(pr[r] + li + j < lim);
-        mrun[r] += (uint32_t)__popcll(m);
-    }
-    return (uint32_t)__popcll(__ballot(inb));
+    for (int r = 0; r < R; r++) cap[r] = kBandCapMax;
+    const uint64_t inb = __builtin_amdgcn_ballot_w64(b < hi);
+    probe_chunk<R, FAST>(b, j, T, H, hm, o1, o2, actmask, inb, pr, cap, s, mrun, cnt);
+    return (uint32_t)__popcll(inb);
 }
 
 // A column's band segment: the first NCH chunks from registers (loaded while
@@ -447,23 +420,24 @@ __device__ __forceinline__ uint32_t band_chunk(uint64_t b, uint32_t j, uint64_t 
 template <int R, int NCH, bool FAST>
 __device__ __forceinline__ uint32_t band_column(const uint64_t *__restrict__ Bc, uint32_t nB, uint32_t q,
                                                 const uint64_t (&seg)[NCH], uint64_t hi, const uint64_t *T,
-                                                uint32_t fam, uint32_t s, const uint32_t (&pr)[R],
+                                                const uint32_t (&o1)[R], const uint32_t (&o2)[R], uint32_t s,
+                                                const uint32_t (&pr)[R],
                                                 uint32_t actmask, uint32_t (&mrun)[R], uint32_t (&cntl)[R]) {
     const uint32_t lane = threadIdx.x & 63;
     bool more = true;
 #pragma unroll
     for (int k = 0; k < NCH; k++) {
         if (!more) continue;                                       // wave-uniform
-        const uint32_t nin = band_chunk<R, FAST>(seg[k], q + lane, hi, T, fam, s, pr, actmask, mrun, cntl);
+        const uint32_t nin = band_chunk<R, FAST>(seg[k], q + lane, hi, T, o1, o2, s, pr, actmask, mrun, cntl);
         q += nin;
         more = nin == 64;
     }
     if (!more) return q;
-    uint64_t b = q + lane < nB ? Bc[q + lane] : kEmpty;
+    uint64_t b = ld_col(Bc, q + lane, nB, s);
     for (;;) {
         const uint32_t jn = q + 64 + lane;
-        const uint64_t bn = jn < nB ? Bc[jn] : kEmpty;
-        const uint32_t nin = band_chunk<R, FAST>(b, q + lane, hi, T, fam, s, pr, actmask, mrun, cntl);
+        const uint64_t bn = ld_col(Bc, jn, nB, s);
+        const uint32_t nin = band_chunk<R, FAST>(b, q + lane, hi, T, o1, o2, s, pr, actmask, mrun, cntl);
         q += nin;
         if (nin < 64) break;
         b = bn;
@@ -475,10 +449,10 @@ template <int R, int NCH, int WG>
 __global__ __launch_bounds__(WG) void k_allpairs_band(
     const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ nhash, uint32_t s, uint32_t N,
     uint32_t row1, uint32_t cap, const uint2 *__restrict__ items, uint16_t *__restrict__ common,
-    uint16_t *__restrict__ denom, uint64_t seg0, uint32_t *__restrict__ nfail) {
+    uint16_t *__restrict__ denom, uint64_t seg0, uint32_t *__restrict__ nfail, uint64_t *__restrict__ prof) {
     constexpr uint32_t H = 1u << kBandB, hm = H - 1, TS = 2 * H;
     constexpr uint32_t NW = WG / 64;
-    extern __shared__ uint64_t lds[];
+    extern __shared__ __align__(16) uint64_t lds[];    // 16-B aligned: the tables are read with ds_read_b128
     uint64_t *T = lds;                                               // R*TS, interleaved
     uint32_t *cur = (uint32_t *)(T + (uint64_t)R * TS);              // [kBandCols] column cursors
     uint32_t *pcnt = cur + kBandCols;                                // [R][kBandCols] counts
@@ -492,7 +466,8 @@ __global__ __launch_bounds__(WG) void k_allpairs_band(
     const uint32_t nrows = min((uint32_t)R, row1 - i0);
     const uint32_t cend = min(c0 + kBandCols, N);
     const uint32_t ncols = cend - c0;
-    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t wave = rfl(tid >> 6);          // wave-uniform for the compiler: scalar column loop
 
     uint32_t nA[R];
     bool any_partial_row = false;
@@ -541,6 +516,7 @@ __global__ __launch_bounds__(WG) void k_allpairs_band(
 #pragma unroll
         for (int r = 0; r < R; r++) pr[r] = s_p[r];
 
+        uint64_t t_b0 = prof ? wall_clock64() : 0;
         // ---- build the R band tables (quotiented cuckoo, band positions)
         uint32_t fam = 0;
         for (; fam < kMaxFam; fam++) {
@@ -600,6 +576,7 @@ __global__ __launch_bounds__(WG) void k_allpairs_band(
             break;
         }
 
+        uint64_t t_c0 = prof ? wall_clock64() : 0;
         // ---- columns: wave w takes columns w, w+NW, ...; next column's first chunk prefetched
         uint32_t ci = wave;
         uint64_t nseg[NCH];
@@ -611,7 +588,7 @@ __global__ __launch_bounds__(WG) void k_allpairs_band(
 #pragma unroll
             for (int k = 0; k < NCH; k++) {
                 const uint32_t j = nq + 64 * k + lane;
-                nseg[k] = j < nnB ? Bn[j] : kEmpty;
+                nseg[k] = ld_col(Bn, j, nnB, s);
             }
         };
         if (ci < ncols) load_seg(ci);
@@ -628,20 +605,28 @@ __global__ __launch_bounds__(WG) void k_allpairs_band(
             if (!actmask) continue;
             uint32_t mrun[R], cntl[R];
 #pragma unroll
-            for (int r = 0; r < R; r++) { mrun[r] = rfl(pm[r * kBandCols + ci]); cntl[r] = 0; }
+            for (int r = 0; r < R; r++) { mrun[r] = rfl(pm[r * kBandCols + ci]); cntl[r] = 0; }   // scalar counters
             const uint64_t *Bc = hashes + (uint64_t)c * s;
-            const uint32_t q = fam == 0
-                ? band_column<R, NCH, true>(Bc, nB, q0, seg, hi, T, fam, s, pr, actmask, mrun, cntl)
-                : band_column<R, NCH, false>(Bc, nB, q0, seg, hi, T, fam, s, pr, actmask, mrun, cntl);
+            uint32_t o1[R], o2[R];
+            const QFields qf = qfields(fam);
 #pragma unroll
-            for (int r = 0; r < R; r++) {
-                const uint32_t cc = wave_sum(cntl[r]);
-                if (lane == 0) { pcnt[r * kBandCols + ci] += cc; pm[r * kBandCols + ci] = mrun[r]; }
-            }
+            for (int r = 0; r < R; r++) { o1[r] = qf.o1; o2[r] = qf.o2; }
+            const uint32_t q = fam == 0
+                ? band_column<R, NCH, true>(Bc, nB, q0, seg, hi, T, o1, o2, s, pr, actmask, mrun, cntl)
+                : band_column<R, NCH, false>(Bc, nB, q0, seg, hi, T, o1, o2, s, pr, actmask, mrun, cntl);
+#pragma unroll
+            for (int r = 0; r < R; r++)
+                if (lane == 0) { pcnt[r * kBandCols + ci] += cntl[r]; pm[r * kBandCols + ci] = mrun[r]; }
             if (lane == 0) cur[ci] = q;
         }
         __syncthreads();
         if (tid < (uint32_t)R) s_p[tid] += s_q[tid];
+        if (prof && tid == 0) {
+            const uint64_t t_e = wall_clock64();
+            atomicAdd((unsigned long long *)&prof[0], (unsigned long long)(t_c0 - t_b0));
+            atomicAdd((unsigned long long *)&prof[1], (unsigned long long)(t_e - t_c0));
+            atomicAdd((unsigned long long *)&prof[2], 1ull);
+        }
     }
     __syncthreads();
     if (s_abort) return;
@@ -699,27 +684,30 @@ static int launch_band(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_
     if ((rc = scratch(ctx, "ap_nfail", 4, (void **)&d_nfail))) return rc;
     HIPC(hipMemsetAsync(d_nfail, 0, 4, st));
     HIPC(hipMemcpyAsync(d_items, items.data(), items.size() * sizeof(uint2), hipMemcpyHostToDevice, st));
-    const size_t lds = (size_t)R * (2u << kBandB) * 8 + kBandCols * 4 + 2ull * R * kBandCols * 4;
-    // geometry: 16 waves x 8 register chunks (default) or 8 waves x 16 chunks
-    // (DREPHIP_BAND_GEOM=1, A/B); one workgroup per CU either way (LDS)
-    const char *geom = getenv("DREPHIP_BAND_GEOM");
-    const bool wide = geom && geom[0] == '1';
-    if (!wide) {
-        HIPC(hipFuncSetAttribute((const void *)k_allpairs_band<R, 8, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        timing_mark(ctx, 2, st, true);
-        hipLaunchKernelGGL((k_allpairs_band<R, 8, 1024>), dim3((uint32_t)items.size()), dim3(1024), lds, st, d_hashes,
-                           d_nhash, ctx->s, N, row1, cap, d_items, d_common, d_denom, seg0, d_nfail);
-    } else {
-        HIPC(hipFuncSetAttribute((const void *)k_allpairs_band<R, 16, 512>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        timing_mark(ctx, 2, st, true);
-        hipLaunchKernelGGL((k_allpairs_band<R, 16, 512>), dim3((uint32_t)items.size()), dim3(512), lds, st, d_hashes,
-                           d_nhash, ctx->s, N, row1, cap, d_items, d_common, d_denom, seg0, d_nfail);
+    uint64_t *d_prof = nullptr;                      // DREPHIP_BAND_PROF=1: per-phase wall-clock sums
+    const bool prof = getenv("DREPHIP_BAND_PROF") != nullptr;
+    if (prof) {
+        if ((rc = scratch(ctx, "apb_prof", 64, (void **)&d_prof))) return rc;
+        HIPC(hipMemsetAsync(d_prof, 0, 64, st));
     }
+    const size_t lds = (size_t)R * (2u << kBandB) * 8 + kBandCols * 4 + 2ull * R * kBandCols * 4;
+    // 16 waves x 8 register chunks per band segment (8 waves x 16 chunks,
+    // 512-lane workgroups, measured 1.35x slower at s = 10^4)
+    HIPC(hipFuncSetAttribute((const void *)k_allpairs_band<R, 8, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    timing_mark(ctx, 2, st, true);
+    hipLaunchKernelGGL((k_allpairs_band<R, 8, 1024>), dim3((uint32_t)items.size()), dim3(1024), lds, st, d_hashes,
+                       d_nhash, ctx->s, N, row1, cap, d_items, d_common, d_denom, seg0, d_nfail, d_prof);
     timing_mark(ctx, 2, st, false);
     HIPC(hipGetLastError());
     uint32_t nfail = 0;
     HIPC(hipMemcpyAsync(&nfail, d_nfail, 4, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));
+    if (prof) {
+        uint64_t h[3];
+        HIPC(hipMemcpy(h, d_prof, 24, hipMemcpyDeviceToHost));
+        fprintf(stderr, "[drephip] band kernel: %llu bands over %zu items; per band: build %.2f us, columns %.2f us (100 MHz wall clock)\n",
+                (unsigned long long)h[2], items.size(), h[2] ? h[0] / 100.0 / h[2] : 0.0, h[2] ? h[1] / 100.0 / h[2] : 0.0);
+    }
     if (nfail)   // a band table could not be built with any field pair: exact merge kernel instead
         return launch_merge(ctx, d_hashes, d_nhash, N, seg0, npairs, d_common, d_denom, st);
     return DREPHIP_OK;
