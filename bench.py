@@ -52,6 +52,20 @@ def parse():
     return ap.parse_args()
 
 
+def config_name(N, L, s):
+    """Which BASELINE.json config a run measures (the default is configs[1])."""
+    if L == 5_000_000:
+        if (N, s) == (1000, 1000):
+            return "BASELINE.json configs[1]"
+        if (N, s) == (10000, 1000):
+            return "BASELINE.json configs[2]"
+        if (N, s) == (100000, 1000):
+            return "BASELINE.json configs[3]"
+        if (N, s) == (10000, 10000):
+            return "BASELINE.json configs[4]"
+    return "custom size"
+
+
 def cpu_baseline(args, threads):
     """Bounded sample of the same whole job on the host with the C oracle
     (Mash-equivalent restatement, OpenMP): sketch 2*threads genomes, dist
@@ -244,8 +258,8 @@ def main():
             "dtype": "u64",
             "data": "synthetic (on-device splitmix64 genome families, 2-bit packed; see DESIGN.md)",
             "config": {
-                "workload": "%d synthetic %d bp genomes, k=21, s=%d (BASELINE.json configs[1]); "
-                            "step = sketch + RCCL all-gather + all-pairs" % (N, L, s),
+                "workload": "%d synthetic %d bp genomes, k=21, s=%d (%s); "
+                            "step = sketch + RCCL all-gather + all-pairs" % (N, L, s, config_name(N, L, s)),
                 "genomes": N, "genome_bp": L, "k": 21, "sketch": s, "family_size": args.family_size,
                 "parallelism": "sketch: genome shards; all-pairs: balanced row shards; RCCL all-gather",
             },

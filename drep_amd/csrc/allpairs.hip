@@ -9,19 +9,22 @@
 // m_j = number of matches among B[0..j).  A wave holds a whole column sketch B
 // in registers (64-element chunks, one element per lane, coalesced 512-B loads,
 // the next column prefetched while this one is processed); membership and i
-// come from a quotiented two-choice cuckoo table of A (2H slots, H >= 2s, load
-// <= 1/4; the slot position implies B key bits, which the stored word reuses
-// for i) built once per row (k_build_qcuckoo); m_j is the running match count
-// plus a ballot/popcount prefix within the chunk.  Elements past A's largest
-// hash (A full) cannot match, which ends the scan.  A membership test is two
-// independent ds_read_b64 and two 64-bit compares: no probe loop, no
-// divergence.  R row tables live in LDS per workgroup; results are staged in
-// LDS and written as contiguous runs of the condensed triangle.
+// come from a quotiented two-choice cuckoo table of A's low words (2H 32-bit
+// slots, H >= 2s, load <= 1/4; the slot position implies B bits of the low
+// word, which the stored word reuses for i), plus A's high words by position
+// (V[i]) to confirm a hit; m_j is the running match count plus a
+// ballot/popcount prefix within the chunk.  Elements past A's largest hash
+// (A full) cannot match, which ends the scan.  A membership test is two
+// independent 4-byte LDS reads (for four interleaved rows: two ds_read_b128)
+// and two 32-bit compares; only a row with a hit in the chunk reads V.  The
+// next chunk's slot words are read before the current chunk is tested.  R row
+// tables live in LDS per workgroup; results are staged in LDS and written as
+// contiguous runs of the condensed triangle.
 // Roofline: LDS random-read throughput + VALU (integer compare/select); no
 // MFMA (set intersection is not a dense contraction).
 //
-// k_allpairs_merge is the literal Mash merge, one lane per pair: any s, used
-// for s > 2048 and as an in-library cross-check.
+// k_allpairs_band (value bands, s > 2048) and k_allpairs_merge (the literal
+// Mash merge, one lane per pair; cross-check and fallback) are further down.
 
 #include "ctx.h"
 #include "../../include/drephip.h"
@@ -34,48 +37,77 @@
 
 namespace drephip {
 
-constexpr int kApWG = 1024;                     // 16 waves: 4 per SIMD at 1 workgroup/CU
-// 32 chunks (s > 1024) double-buffered take 128 VGPRs of sketch alone: half the
-// waves, twice the registers
-__host__ __device__ constexpr int ap_wg(int nch) { return nch > 16 ? kApWG / 2 : kApWG; }
+constexpr int kApWG = 1024;                     // 16 waves per workgroup
 constexpr uint32_t kApCols = 128;               // columns per work item
-constexpr uint32_t kMaxFam = 6;                 // cuckoo hash families tried per row
-constexpr uint32_t kLdsTables = 128 * 1024;     // LDS bytes for row tables per workgroup
+constexpr uint32_t kMaxFam = 6;                 // cuckoo field families tried per table
+constexpr uint32_t kLdsBudget = 156 * 1024;     // dynamic LDS per workgroup
+constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;      // empty slot word
 
 __host__ __device__ __forceinline__ uint64_t cond_index(uint64_t i, uint64_t j, uint64_t N) {
     return i * N - i * (i + 1) / 2 + (j - i - 1);
 }
-
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
 
 // ------------------------------------------------------- row tables
-// Quotiented two-choice cuckoo table: choice 1 sits at T[f1(x)], choice 2 at
-// T[H + f2(x)], where f1/f2 are disjoint B-bit fields of the key at offsets
-// o1/o2 (family f picks them).  Because a slot's position fixes those B bits,
-// the stored word replaces them with the key's sketch position i, and is kept
-// rotated right by the field offset:  e = rotr((x & ~F) | (i << o), o), so the
-// field sits at bits [0, B); one 8-byte read returns membership AND i:
-// match iff (e ^ rotr(x, o)) < 2^B, i = e & (2^B - 1) (the all-ones empty
-// word decodes to i = 2^B-1 >= nA).  Exact for every key.
+// Quotiented two-choice cuckoo table over the keys' low words x = lo32(key):
+// choice 1 sits at T[f1(x)], choice 2 at T[H + f2(x)], where f1/f2 are
+// disjoint B-bit fields of x at offsets o1/o2 (family f picks them).  Because
+// a slot's position fixes those B bits, the stored word replaces them with
+// the key's position i, and is kept rotated right by the field offset:
+//     e = rotr32((x & ~F) | (i << o), o)       (field at bits [0, B))
+// so one 4-byte read answers "does this slot hold low word x" --
+// (e ^ rotr32(x, o)) < 2^B -- and gives i = e & (2^B - 1).  The key's high
+// word is then compared with V[i] = hi32(A[i]).  The all-ones empty word
+// decodes to i = 2^B - 1, past every real position (H >= 2s), and no stored
+// word is all ones (i <= s - 1 < 2^B - 1).  Two keys of one row with equal low
+// words occupy the two slots they share; a hit whose high word does not match
+// retries the other choice.  Exact for every key.
 struct QFields { uint32_t o1, o2; };
-__host__ __device__ __forceinline__ uint64_t rotr64(uint64_t x, uint32_t r) {
-    return r ? (x >> r) | (x << (64 - r)) : x;
+__host__ __device__ __forceinline__ uint32_t rotr32(uint32_t x, uint32_t r) {
+    return r ? (x >> r) | (x << (32 - r)) : x;
 }
 __host__ __device__ __forceinline__ QFields qfields(uint32_t fam) {
-    // disjoint field offsets inside the low 36 key bits (bottom-s hashes of
-    // any genome below ~2^28 bases have uniformly random low 36 bits).
-    // Family 0 keeps both fields in the low 32 bits (kernel fast path).
-    const uint32_t o1[6] = {0, 16, 3, 19, 6, 22};
-    const uint32_t o2[6] = {16, 0, 19, 3, 22, 6};
+    // disjoint fields inside the low word for B <= 12 (o + B <= 32)
+    const uint32_t o1[6] = {0, 16, 2, 18, 4, 20};
+    const uint32_t o2[6] = {16, 0, 18, 2, 20, 4};
     return {o1[fam], o2[fam]};
 }
 
-__global__ __launch_bounds__(256) void k_build_qcuckoo(const uint64_t *__restrict__ hashes,
-                                                       const uint32_t *__restrict__ nhash, uint32_t s,
-                                                       uint32_t row0, uint32_t B,
-                                                       uint64_t *__restrict__ tabs,
-                                                       uint8_t *__restrict__ fam_out,
-                                                       uint32_t *__restrict__ nfail) {
-    extern __shared__ unsigned long long T[];
+// Insert (x, ix) into an LDS table whose slot p lives at T[p * stride + col]
+// (stride R, col r: the interleaved band tables; stride 1: one row).
+__device__ __forceinline__ bool cuckoo_insert32(uint32_t *T, uint32_t stride, uint32_t col, uint32_t H,
+                                                uint32_t hm, QFields q, uint32_t x, uint32_t ix) {
+    const uint32_t F1 = hm << q.o1, F2 = hm << q.o2;
+    uint32_t pos = (x >> q.o1) & hm;
+    for (int kick = 0; kick < 96; kick++) {
+        const bool second = pos >= H;
+        const uint32_t o = second ? q.o2 : q.o1, F = second ? F2 : F1;
+        const uint32_t old_r = atomicExch(&T[pos * stride + col], rotr32((x & ~F) | (ix << o), o));
+        if (old_r == kEmpty32) return true;
+        const uint32_t old = rotr32(old_r, (32 - o) & 31);      // decode the evicted entry
+        const uint32_t lp = second ? pos - H : pos;
+        ix = (old >> o) & hm;
+        x = (old & ~F) | (lp << o);
+        pos = second ? ((x >> q.o1) & hm) : (H + ((x >> q.o2) & hm));
+    }
+    return false;
+}
+// (x, ix) is stored in one of its two slots
+__device__ __forceinline__ bool cuckoo_has32(const uint32_t *T, uint32_t stride, uint32_t col, uint32_t H,
+                                             uint32_t hm, QFields q, uint32_t x, uint32_t ix) {
+    const uint32_t e1 = T[((x >> q.o1) & hm) * stride + col];
+    const uint32_t e2 = T[(H + ((x >> q.o2) & hm)) * stride + col];
+    const bool ok1 = (e1 ^ rotr32(x, q.o1)) <= hm && (e1 & hm) == ix;
+    const bool ok2 = (e2 ^ rotr32(x, q.o2)) <= hm && (e2 & hm) == ix;
+    return ok1 || ok2;
+}
+
+// One table per row g in [row0, row0 + gridDim.x): 2H words to tabs.
+__global__ __launch_bounds__(256) void k_build_q32(const uint64_t *__restrict__ hashes,
+                                                   const uint32_t *__restrict__ nhash, uint32_t s,
+                                                   uint32_t row0, uint32_t B, uint32_t *__restrict__ tabs,
+                                                   uint8_t *__restrict__ fam_out, uint32_t *__restrict__ nfail) {
+    extern __shared__ uint32_t Tb[];
     __shared__ int fail;
     const uint32_t H = 1u << B, hm = H - 1;
     const uint32_t r = blockIdx.x;
@@ -84,45 +116,18 @@ __global__ __launch_bounds__(256) void k_build_qcuckoo(const uint64_t *__restric
     const uint64_t *A = hashes + (uint64_t)g * s;
     for (uint32_t fam = 0; fam < kMaxFam; fam++) {
         const QFields q = qfields(fam);
-        const uint64_t F1 = (uint64_t)hm << q.o1, F2 = (uint64_t)hm << q.o2;
-        for (uint32_t i = threadIdx.x; i < 2 * H; i += blockDim.x) T[i] = kEmpty;
+        for (uint32_t i = threadIdx.x; i < 2 * H; i += blockDim.x) Tb[i] = kEmpty32;
         if (threadIdx.x == 0) fail = 0;
         __syncthreads();
-        // insert (key, position) pairs; an entry travels as (x, i)
-        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-            uint64_t x = A[i];
-            uint32_t ix = i;
-            uint32_t pos = (uint32_t)(x >> q.o1) & hm;
-            bool placed = false;
-            for (int kick = 0; kick < 96; kick++) {
-                const bool second = pos >= H;
-                const uint64_t e = second ? ((x & ~F2) | ((uint64_t)ix << q.o2))
-                                          : ((x & ~F1) | ((uint64_t)ix << q.o1));
-                // stored rotated right by the field offset: field at bits [0, B)
-                const unsigned long long oldr = atomicExch(&T[pos], rotr64(e, second ? q.o2 : q.o1));
-                if (oldr == kEmpty) { placed = true; break; }
-                // decode the evicted entry back to (key, position)
-                const uint64_t old = rotr64(oldr, 64 - (second ? q.o2 : q.o1));
-                const uint32_t lp = second ? pos - H : pos;
-                if (second) { ix = (uint32_t)(old >> q.o2) & hm; x = (old & ~F2) | ((uint64_t)lp << q.o2); }
-                else        { ix = (uint32_t)(old >> q.o1) & hm; x = (old & ~F1) | ((uint64_t)lp << q.o1); }
-                pos = second ? ((uint32_t)(x >> q.o1) & hm) : (H + ((uint32_t)(x >> q.o2) & hm));
-            }
-            if (!placed) fail = 1;
-        }
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+            if (!cuckoo_insert32(Tb, 1, 0, H, hm, q, (uint32_t)A[i], i)) fail = 1;
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-            const uint64_t x = A[i];
-            const uint64_t e1 = rotr64(T[(uint32_t)(x >> q.o1) & hm], 64 - q.o1);
-            const uint64_t e2 = rotr64(T[H + ((uint32_t)(x >> q.o2) & hm)], 64 - q.o2);
-            const bool ok1 = (e1 & ~F1) == (x & ~F1) && ((uint32_t)(e1 >> q.o1) & hm) == i;
-            const bool ok2 = (e2 & ~F2) == (x & ~F2) && ((uint32_t)(e2 >> q.o2) & hm) == i;
-            if (!(ok1 || ok2)) fail = 1;
-        }
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+            if (!cuckoo_has32(Tb, 1, 0, H, hm, q, (uint32_t)A[i], i)) fail = 1;
         __syncthreads();
         if (!fail) {
-            uint64_t *o = tabs + (uint64_t)r * 2 * H;
-            for (uint32_t i = threadIdx.x; i < 2 * H; i += blockDim.x) o[i] = T[i];
+            uint32_t *o = tabs + (uint64_t)r * 2 * H;
+            for (uint32_t i = threadIdx.x; i < 2 * H; i += blockDim.x) o[i] = Tb[i];
             if (threadIdx.x == 0) fam_out[r] = (uint8_t)fam;
             return;
         }
@@ -131,60 +136,79 @@ __global__ __launch_bounds__(256) void k_build_qcuckoo(const uint64_t *__restric
     if (threadIdx.x == 0) { fam_out[r] = 0xFF; atomicAdd(nfail, 1u); }
 }
 
-// Slot words are stored rotated right by their field offset (field at bits
-// [0, B)), so slot k holds b iff (e_k ^ rotr(b, o_k)) <= 2^B - 1, and the
-// field -- b's sketch position i in A -- is e_k & hm.  The empty word (all
-// ones) matches only the all-ones padding key and decodes to 2^B - 1, past
-// every real position, so the ilim test below keeps `found` exact.
-// One 64-element chunk of column elements (one per lane; position j) against
-// R row tables, with wave-level lane masks kept in SGPRs: per row the two
-// slot words are compared and their ballots OR-ed; only a row with a match in
-// the chunk (uniform branch) selects i, checks it against ilim (the empty
-// word decodes past it) and applies the union-rank rule
-//     i + j < s + mrun + (matches in lower lanes)
-// with scalar popcounts -- counts stay in SGPRs, no per-lane reduction.
-// i = ibase[r] + field.  lanemask drops lanes (band kernel: outside the band).
-// Row tables are interleaved in LDS (slot k of row r at k*R + r), so in the
-// FAST layout (family 0 for every row) one slot address serves all R rows:
-// R/2 ds_read_b128 per choice.
+// ------------------------------------------------------- probe
+// Slot words of one chunk element (this lane) for R interleaved row tables
+// (slot k of row r at T[k * R + r]): in the FAST layout (family 0 for every
+// row) one slot address serves all R rows -- R = 4: one ds_read_b128 per
+// choice.
+template <int R>
+struct Slots { uint32_t e1[R], e2[R]; };
+
 template <int R, bool FAST>
-__device__ __forceinline__ void probe_chunk(uint64_t b, uint32_t j, const uint64_t *T, uint32_t H, uint32_t hm,
-                                            const uint32_t (&o1)[R], const uint32_t (&o2)[R], uint32_t actmask,
-                                            uint64_t lanemask, const uint32_t (&ibase)[R],
-                                            const uint32_t (&ilim)[R], uint32_t s, uint32_t (&mrun)[R],
-                                            uint32_t (&cnt)[R]) {
-    const uint32_t blo = (uint32_t)b;
-    uint64_t e1[R], e2[R];
+__device__ __forceinline__ Slots<R> read_slots(uint32_t blo, const uint32_t *T, uint32_t H, uint32_t hm,
+                                               const uint32_t (&o1)[R], const uint32_t (&o2)[R]) {
+    Slots<R> sl;
     if (FAST) {
-        const uint64_t *p1 = T + (uint64_t)(blo & hm) * R;
-        const uint64_t *p2 = T + (uint64_t)(H + ((blo >> 16) & hm)) * R;
-        if constexpr (R == 1) {
-            e1[0] = p1[0]; e2[0] = p2[0];
-        } else {
+        const uint32_t *p1 = T + (blo & hm) * R;
+        const uint32_t *p2 = T + (H + ((blo >> 16) & hm)) * R;
+        if constexpr (R >= 4) {
 #pragma unroll
-            for (int r = 0; r < R; r += 2) {
-                const ulonglong2 v1 = *(const ulonglong2 *)(p1 + r);
-                const ulonglong2 v2 = *(const ulonglong2 *)(p2 + r);
-                e1[r] = v1.x; e1[r + 1] = v1.y; e2[r] = v2.x; e2[r + 1] = v2.y;
+            for (int r = 0; r < R; r += 4) {
+                const uint4 v1 = *(const uint4 *)(p1 + r);
+                const uint4 v2 = *(const uint4 *)(p2 + r);
+                sl.e1[r] = v1.x; sl.e1[r + 1] = v1.y; sl.e1[r + 2] = v1.z; sl.e1[r + 3] = v1.w;
+                sl.e2[r] = v2.x; sl.e2[r + 1] = v2.y; sl.e2[r + 2] = v2.z; sl.e2[r + 3] = v2.w;
             }
+        } else if constexpr (R == 2) {
+            const uint2 v1 = *(const uint2 *)p1, v2 = *(const uint2 *)p2;
+            sl.e1[0] = v1.x; sl.e1[1] = v1.y; sl.e2[0] = v2.x; sl.e2[1] = v2.y;
+        } else {
+            sl.e1[0] = p1[0]; sl.e2[0] = p2[0];
         }
     } else {
 #pragma unroll
         for (int r = 0; r < R; r++) {                                // inactive rows read empty words
-            e1[r] = T[(uint64_t)((uint32_t)(b >> o1[r]) & hm) * R + r];
-            e2[r] = T[(uint64_t)(H + ((uint32_t)(b >> o2[r]) & hm)) * R + r];
+            sl.e1[r] = T[((blo >> o1[r]) & hm) * R + r];
+            sl.e2[r] = T[(H + ((blo >> o2[r]) & hm)) * R + r];
         }
     }
-    const uint64_t b16 = rotr64(b, 16);                              // family 0's second field
+    return sl;
+}
+
+// One 64-element chunk of column elements (one per lane; position j) against
+// R row tables, with wave-level lane masks kept in SGPRs: per row the two
+// slot words are compared and their ballots OR-ed; only a row with a hit in
+// the chunk (uniform branch) selects i, confirms the high word against
+// V[r * vs + i] and applies the union-rank rule
+//     i + j < s + mrun + (matches in lower lanes)
+// with scalar popcounts -- counts stay in SGPRs, no per-lane reduction.
+// i = ibase[r] + field, valid below ilim[r].  lanemask drops lanes (band
+// kernel: outside the band).
+template <int R, bool FAST>
+__device__ __forceinline__ void probe_rows(const Slots<R> &sl, uint64_t b, uint32_t j, const uint32_t *V,
+                                           uint32_t vs, uint32_t hm, const uint32_t (&o1)[R],
+                                           const uint32_t (&o2)[R], uint32_t actmask, uint64_t lanemask,
+                                           const uint32_t (&ibase)[R], const uint32_t (&ilim)[R], uint32_t s,
+                                           uint32_t (&mrun)[R], uint32_t (&cnt)[R]) {
+    const uint32_t blo = (uint32_t)b, bhi = (uint32_t)(b >> 32);
+    const uint32_t b16 = rotr32(blo, 16);                            // family 0's second field
 #pragma unroll
     for (int r = 0; r < R; r++) {
         if (!((actmask >> r) & 1u)) continue;                        // wave-uniform
-        const bool c1 = (e1[r] ^ (FAST ? b : rotr64(b, o1[r]))) <= (uint64_t)hm;
-        const bool c2 = (e2[r] ^ (FAST ? b16 : rotr64(b, o2[r]))) <= (uint64_t)hm;
+        const bool c1 = (sl.e1[r] ^ (FAST ? blo : rotr32(blo, o1[r]))) <= hm;
+        const bool c2 = (sl.e2[r] ^ (FAST ? b16 : rotr32(blo, o2[r]))) <= hm;
         uint64_t m = (__builtin_amdgcn_ballot_w64(c1) | __builtin_amdgcn_ballot_w64(c2)) & lanemask;
-        if (m == 0) continue;                                        // wave-uniform: no shared hash here
-        const uint32_t f = (c1 ? (uint32_t)e1[r] : (uint32_t)e2[r]) & hm;
-        m &= __builtin_amdgcn_ballot_w64(f < ilim[r]);
+        if (m == 0) continue;                                        // wave-uniform: no hit in this row
+        uint32_t f = (c1 ? sl.e1[r] : sl.e2[r]) & hm;
+        bool ok = f < ilim[r] && V[r * vs + (f < ilim[r] ? f : 0)] == bhi;
+        const bool retry = c1 && c2 && !ok;                          // two keys share this low word
+        if (__builtin_amdgcn_ballot_w64(retry) != 0) {
+            const uint32_t f2 = sl.e2[r] & hm;
+            const bool ok2 = retry && f2 < ilim[r] && V[r * vs + (f2 < ilim[r] ? f2 : 0)] == bhi;
+            f = ok2 ? f2 : f;
+            ok = ok || ok2;
+        }
+        m &= __builtin_amdgcn_ballot_w64(ok);
         const uint32_t lim = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, s + mrun[r]));
         cnt[r] += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(ibase[r] + f + j < lim) & m);
@@ -192,32 +216,47 @@ __device__ __forceinline__ void probe_chunk(uint64_t b, uint32_t j, const uint64
     }
 }
 
-// The columns of one work item, processed by one wave (double-buffered column
-// sketches in registers; see the header comment for the counting rule).
+// ------------------------------------------------------- whole-row tables
+// The columns of one work item, processed by one wave.  The column elements
+// stream through a ring of kRing chunks in registers, loaded kRing chunks
+// ahead of use (the next column's first kRing chunks are loaded when a column
+// starts), so a wave holds ~16 VGPRs of sketch instead of whole columns and
+// two workgroups fit a CU.  Slot words are read one chunk ahead of the tests.
+// Counts go straight to the condensed output (lane 0).
+constexpr int kRing = 4;
+
 template <int R, int NCH, bool FAST>
 __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ nhash,
-                                           const uint64_t *T, uint32_t TS, uint32_t H, uint32_t hm, uint32_t s,
-                                           uint32_t i0, uint32_t nrows, uint32_t c0, uint32_t cend, uint32_t c_first,
+                                           const uint32_t *T, const uint32_t *V, uint32_t H, uint32_t hm, uint32_t s,
+                                           uint32_t N, uint32_t i0, uint32_t nrows, uint32_t cend, uint32_t c_first,
                                            uint32_t c_step, const uint32_t (&nA)[R], const uint32_t (&o1)[R],
                                            const uint32_t (&o2)[R], const uint64_t (&alast)[R],
-                                           bool any_partial_row, uint16_t *res_c, uint16_t *res_d) {
+                                           bool any_partial_row, uint16_t *__restrict__ common,
+                                           uint16_t *__restrict__ denom, uint64_t seg0) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nch = (s + 63) / 64;
-    uint64_t cur[NCH], nxt[NCH];
-    uint32_t c = __builtin_amdgcn_readfirstlane(c_first);        // wave-uniform: scalar column loop
-    if (c < cend) {
-        const uint64_t *Bc = hashes + (uint64_t)c * s;
+    auto ld = [&](const uint64_t *Bc, int k) -> uint64_t {     // clamped load + select: no branch
+        const uint32_t j = k * 64 + lane;
+        const uint64_t v = Bc[j < s ? j : s - 1];
+        return j < s ? v : kEmpty;
+    };
+    uint64_t rg[kRing], nx[kRing];
+    uint32_t zero[R];
 #pragma unroll
-        for (int k = 0; k < NCH; k++) { const uint32_t j = k * 64 + lane; nxt[k] = (k < (int)nch && j < s) ? Bc[j] : kEmpty; }
+    for (int r = 0; r < R; r++) zero[r] = 0;
+    uint32_t c = rfl(c_first);                                       // wave-uniform: scalar column loop
+    if (c < cend) {
+#pragma unroll
+        for (int k = 0; k < kRing; k++) nx[k] = ld(hashes + (uint64_t)c * s, k);
     }
     for (; c < cend; c += c_step) {
+        const uint64_t *Bc = hashes + (uint64_t)c * s;
 #pragma unroll
-        for (int k = 0; k < NCH; k++) cur[k] = nxt[k];
+        for (int k = 0; k < kRing; k++) rg[k] = nx[k];
         const uint32_t cn = c + c_step;
         if (cn < cend) {
-            const uint64_t *Bn = hashes + (uint64_t)cn * s;
 #pragma unroll
-            for (int k = 0; k < NCH; k++) { const uint32_t j = k * 64 + lane; nxt[k] = (k < (int)nch && j < s) ? Bn[j] : kEmpty; }
+            for (int k = 0; k < kRing; k++) nx[k] = ld(hashes + (uint64_t)cn * s, k);
         }
         const uint32_t nB = nhash[c];
         const bool partial = any_partial_row || nB < s;
@@ -232,60 +271,76 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
             actmask |= (uint32_t)act << r;
             if (act) amax = alast[r] > amax ? alast[r] : amax;
         }
-        uint32_t zero[R];
-#pragma unroll
-        for (int r = 0; r < R; r++) zero[r] = 0;
+        if (!actmask) continue;                                       // column at or left of the tile's rows
+        Slots<R> sn = read_slots<R, FAST>((uint32_t)rg[0], T, H, hm, o1, o2);
         bool alive = true;
+        // runtime loop over groups of kRing chunks; ring slots are static
+        for (uint32_t kb = 0; kb < nch && alive; kb += kRing) {
 #pragma unroll
-        for (int k = 0; k < NCH; k++) {
-            if (!alive || k >= (int)nch) continue;                        // wave-uniform
-            const uint64_t b = cur[k];
-            // smallest element of the chunk (lane 0; readfirstlane returns
-            // int: through uint32_t so the low word is not sign-extended)
-            const uint64_t b0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
-                                (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
-            if (b0 == kEmpty || b0 > amax) { alive = false; continue; }
-            probe_chunk<R, FAST>(b, k * 64 + lane, T, H, hm, o1, o2, actmask, ~0ull, zero, nA, s, mrun, cnt);
-        }
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-            if ((uint32_t)r >= nrows || i0 + r >= c) continue;
-            const uint32_t cc = cnt[r];
-            uint32_t dd = s;
-            if (partial) {
-                const uint32_t u = nA[r] + nB - mrun[r];      // |A u B|; mrun = |A n B| when partial
-                dd = u < s ? u : s;
+            for (int u = 0; u < kRing; u++) {
+                const uint32_t k = kb + u;
+                if (!alive || k >= nch) continue;                        // wave-uniform
+                const uint64_t b = rg[u];
+                const Slots<R> sl = sn;
+                if (k + kRing < nch) rg[u] = ld(Bc, k + kRing);          // refill the ring
+                sn = read_slots<R, FAST>((uint32_t)rg[(u + 1) % kRing], T, H, hm, o1, o2);
+                // smallest element of the chunk (lane 0; readfirstlane returns
+                // int: through uint32_t so the low word is not sign-extended)
+                const uint64_t b0 = ((uint64_t)rfl((uint32_t)(b >> 32)) << 32) | rfl((uint32_t)b);
+                if (b0 == kEmpty || b0 > amax) { alive = false; continue; }
+                probe_rows<R, FAST>(sl, b, k * 64 + lane, V, s, hm, o1, o2, actmask, ~0ull, zero, nA, s, mrun, cnt);
             }
-            if (lane == 0) { res_c[r * kApCols + (c - c0)] = (uint16_t)cc; res_d[r * kApCols + (c - c0)] = (uint16_t)dd; }
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                if (!((actmask >> r) & 1u)) continue;
+                const uint64_t o = cond_index(i0 + r, c, N) - seg0;
+                common[o] = (uint16_t)cnt[r];
+                if (denom) {
+                    uint32_t dd = s;
+                    if (partial) {
+                        const uint32_t u = nA[r] + nB - mrun[r];  // |A u B|; mrun = |A n B| when partial
+                        dd = u < s ? u : s;
+                    }
+                    denom[o] = (uint16_t)dd;
+                }
+            }
         }
     }
 }
 
-// R rows (tables in LDS) x kApCols columns per workgroup of ap_wg(NCH) lanes; each
-// wave walks every (WG/64)-th column of the item.
-template <int R, int NCH>
-__global__ __launch_bounds__(ap_wg(NCH)) void k_allpairs_q(
+__host__ __device__ constexpr size_t q_lds_bytes(uint32_t R, uint32_t TS, uint32_t s) {
+    return (size_t)R * TS * 4 + (size_t)R * s * 4;
+}
+
+// R rows (tables in LDS) x kApCols columns per workgroup of kApWG lanes; each
+// wave walks every 16th column of the item.  MINW = 8: two workgroups per CU
+// (LDS <= 80 KiB, <= 64 VGPRs).
+template <int R, int NCH, int MINW>
+__global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
     const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ nhash,
-    const uint64_t *__restrict__ tabs, const uint8_t *__restrict__ fam, uint32_t s, uint32_t N,
+    const uint32_t *__restrict__ tabs, const uint8_t *__restrict__ fam, uint32_t s, uint32_t N,
     uint32_t row0, uint32_t row1, uint32_t B, const uint2 *__restrict__ items,
     uint16_t *__restrict__ common, uint16_t *__restrict__ denom, uint64_t seg0) {
-    constexpr int WG = ap_wg(NCH);
-    extern __shared__ __align__(16) uint64_t lds[];    // 16-B aligned: the tables are read with ds_read_b128
+    constexpr int WG = kApWG;
+    extern __shared__ __align__(16) uint32_t lds[];    // 16-B aligned: slot words are read with ds_read_b128
     const uint32_t H = 1u << B, hm = H - 1, TS = 2 * H;
-    uint64_t *T = lds;
-    uint16_t *res_c = (uint16_t *)(lds + (uint64_t)R * TS);
-    uint16_t *res_d = res_c + R * kApCols;
+    uint32_t *T = lds;                                  // [TS][R] interleaved slot words
+    uint32_t *V = T + R * TS;                           // [R][s] high words by position
     const uint32_t i0 = items[blockIdx.x].x;
     const uint32_t c0 = items[blockIdx.x].y;
+    if (i0 == 0xFFFFFFFFu) return;                      // idle padding item (make_items)
     const uint32_t nrows = min((uint32_t)R, row1 - i0);
     const uint32_t cend = min(c0 + kApCols, N);
     const uint32_t tid = threadIdx.x, wave = tid >> 6;
-    // interleave the R row tables: slot k of row r at k*R + r (rows past nrows empty)
     for (uint32_t k = tid; k < TS; k += WG) {
 #pragma unroll
         for (int r = 0; r < R; r++)
-            T[(uint64_t)k * R + r] = (uint32_t)r < nrows ? tabs[(uint64_t)(i0 - row0 + r) * TS + k] : kEmpty;
+            T[k * R + r] = (uint32_t)r < nrows ? tabs[(uint64_t)(i0 - row0 + r) * TS + k] : kEmpty32;
     }
+    for (uint32_t r = 0; r < nrows; r++)
+        for (uint32_t i = tid; i < s; i += WG) V[r * s + i] = (uint32_t)(hashes[(uint64_t)(i0 + r) * s + i] >> 32);
     uint32_t nA[R], o1[R], o2[R];
     uint64_t alast[R];
     bool any_partial_row = false, fast = true;
@@ -302,24 +357,14 @@ __global__ __launch_bounds__(ap_wg(NCH)) void k_allpairs_q(
     }
     __syncthreads();
     if (fast)
-        ap_columns<R, NCH, true>(hashes, nhash, T, TS, H, hm, s, i0, nrows, c0, cend, c0 + wave, WG / 64,
-                                 nA, o1, o2, alast, any_partial_row, res_c, res_d);
+        ap_columns<R, NCH, true>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend, c0 + wave, WG / 64,
+                                 nA, o1, o2, alast, any_partial_row, common, denom, seg0);
     else
-        ap_columns<R, NCH, false>(hashes, nhash, T, TS, H, hm, s, i0, nrows, c0, cend, c0 + wave, WG / 64,
-                                  nA, o1, o2, alast, any_partial_row, res_c, res_d);
-    __syncthreads();
-    for (uint32_t r = 0; r < nrows; r++) {
-        const uint32_t i = i0 + r;
-        const uint32_t cs = max(c0, i + 1);
-        if (cs >= cend) continue;
-        const uint64_t base = cond_index(i, cs, N) - seg0;
-        for (uint32_t t = tid; t < cend - cs; t += WG) {
-            common[base + t] = res_c[r * kApCols + (cs - c0) + t];
-            if (denom) denom[base + t] = res_d[r * kApCols + (cs - c0) + t];
-        }
-    }
+        ap_columns<R, NCH, false>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend, c0 + wave, WG / 64,
+                                  nA, o1, o2, alast, any_partial_row, common, denom, seg0);
 }
 
+// ------------------------------------------------------- literal merge
 // Literal Mash merge, one lane per pair of the condensed segment.
 __global__ __launch_bounds__(256) void k_allpairs_merge(const uint64_t *__restrict__ hashes,
                                                         const uint32_t *__restrict__ nhash, uint32_t s,
@@ -361,10 +406,10 @@ __global__ __launch_bounds__(256) void k_allpairs_merge(const uint64_t *__restri
 // (p_r = the row's first element >= lo_k), so every row has <= cap elements in
 // the band; those get an LDS cuckoo table (same quotiented format as above,
 // storing the element's position *within the band*, at most cap - 1 < H - 1,
-// so the empty word still decodes to "absent").  Every column of the tile
-// keeps a cursor into its sketch (first element >= lo_k, in LDS); a wave
-// streams the column's elements in [lo_k, hi_k) in 64-element chunks and
-// counts, per row, shared elements whose union rank
+// so the empty word still decodes to "absent") and their high words V.  Every
+// column of the tile keeps a cursor into its sketch (first element >= lo_k, in
+// LDS); a wave streams the column's elements in [lo_k, hi_k) in 64-element
+// chunks and counts, per row, shared elements whose union rank
 //     i + j - m_j < s          (i = p_r + band position, j = column position)
 // is below s -- the same rule as k_allpairs_q, with the running match count
 // m and the partial counts carried across bands in LDS.  Bands run until
@@ -392,57 +437,52 @@ __device__ __forceinline__ uint64_t ld_col(const uint64_t *__restrict__ Bc, uint
     const uint64_t v = Bc[j < s ? j : s - 1];
     return j < nB ? v : kEmpty;
 }
-__device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
-    return ((uint64_t)rfl((uint32_t)(v >> 32)) << 32) | rfl((uint32_t)v);
-}
 
-// One 64-element chunk of a column inside the current band.  Returns the
-// number of chunk elements inside the band (< 64: the column's band segment
-// ends in this chunk).
-template <int R, bool FAST>
-__device__ __forceinline__ uint32_t band_chunk(uint64_t b, uint32_t j, uint64_t hi, const uint64_t *T,
-                                               const uint32_t (&o1)[R], const uint32_t (&o2)[R], uint32_t s,
-                                               const uint32_t (&pr)[R], uint32_t actmask, uint32_t (&mrun)[R],
-                                               uint32_t (&cnt)[R]) {
+// A column's band segment: the first NCH chunks from registers (loaded while
+// the previous column was processed), slot words read one chunk ahead; a
+// segment longer than NCH chunks continues from memory one chunk at a time.
+// Returns the new cursor.
+template <int R, int NCH, bool FAST>
+__device__ __forceinline__ uint32_t band_column(const uint64_t *__restrict__ Bc, uint32_t nB, uint32_t q,
+                                                const uint64_t (&seg)[NCH], uint64_t hi, const uint32_t *T,
+                                                const uint32_t *V, const uint32_t (&o1)[R],
+                                                const uint32_t (&o2)[R], uint32_t s, const uint32_t (&pr)[R],
+                                                uint32_t actmask, uint32_t (&mrun)[R], uint32_t (&cnt)[R]) {
     constexpr uint32_t H = 1u << kBandB, hm = H - 1;
+    const uint32_t lane = threadIdx.x & 63;
     uint32_t cap[R];
 #pragma unroll
     for (int r = 0; r < R; r++) cap[r] = kBandCapMax;
-    const uint64_t inb = __builtin_amdgcn_ballot_w64(b < hi);
-    probe_chunk<R, FAST>(b, j, T, H, hm, o1, o2, actmask, inb, pr, cap, s, mrun, cnt);
-    return (uint32_t)__popcll(inb);
-}
-
-// A column's band segment: the first NCH chunks from registers (loaded while
-// the previous column was processed); a segment longer than NCH chunks
-// continues from memory one chunk at a time.  Returns the new cursor.
-template <int R, int NCH, bool FAST>
-__device__ __forceinline__ uint32_t band_column(const uint64_t *__restrict__ Bc, uint32_t nB, uint32_t q,
-                                                const uint64_t (&seg)[NCH], uint64_t hi, const uint64_t *T,
-                                                const uint32_t (&o1)[R], const uint32_t (&o2)[R], uint32_t s,
-                                                const uint32_t (&pr)[R],
-                                                uint32_t actmask, uint32_t (&mrun)[R], uint32_t (&cntl)[R]) {
-    const uint32_t lane = threadIdx.x & 63;
     bool more = true;
+    Slots<R> sn = read_slots<R, FAST>((uint32_t)seg[0], T, H, hm, o1, o2);
 #pragma unroll
     for (int k = 0; k < NCH; k++) {
         if (!more) continue;                                       // wave-uniform
-        const uint32_t nin = band_chunk<R, FAST>(seg[k], q + lane, hi, T, o1, o2, s, pr, actmask, mrun, cntl);
+        const Slots<R> sl = sn;
+        if (k + 1 < NCH) sn = read_slots<R, FAST>((uint32_t)seg[k + 1], T, H, hm, o1, o2);
+        const uint64_t inb = __builtin_amdgcn_ballot_w64(seg[k] < hi);
+        probe_rows<R, FAST>(sl, seg[k], q + lane, V, kBandCapMax, hm, o1, o2, actmask, inb, pr, cap, s, mrun, cnt);
+        const uint32_t nin = (uint32_t)__popcll(inb);
         q += nin;
         more = nin == 64;
     }
     if (!more) return q;
     uint64_t b = ld_col(Bc, q + lane, nB, s);
     for (;;) {
-        const uint32_t jn = q + 64 + lane;
-        const uint64_t bn = ld_col(Bc, jn, nB, s);
-        const uint32_t nin = band_chunk<R, FAST>(b, q + lane, hi, T, o1, o2, s, pr, actmask, mrun, cntl);
+        const uint64_t bn = ld_col(Bc, q + 64 + lane, nB, s);
+        const Slots<R> sl = read_slots<R, FAST>((uint32_t)b, T, H, hm, o1, o2);
+        const uint64_t inb = __builtin_amdgcn_ballot_w64(b < hi);
+        probe_rows<R, FAST>(sl, b, q + lane, V, kBandCapMax, hm, o1, o2, actmask, inb, pr, cap, s, mrun, cnt);
+        const uint32_t nin = (uint32_t)__popcll(inb);
         q += nin;
         if (nin < 64) break;
         b = bn;
     }
     return q;
+}
+
+__host__ __device__ constexpr size_t band_lds_bytes(uint32_t R) {
+    return (size_t)R * (2u << kBandB) * 4 + (size_t)R * kBandCapMax * 4 + kBandCols * 4 + 2ull * R * kBandCols * 4;
 }
 
 template <int R, int NCH, int WG>
@@ -452,9 +492,10 @@ __global__ __launch_bounds__(WG) void k_allpairs_band(
     uint16_t *__restrict__ denom, uint64_t seg0, uint32_t *__restrict__ nfail, uint64_t *__restrict__ prof) {
     constexpr uint32_t H = 1u << kBandB, hm = H - 1, TS = 2 * H;
     constexpr uint32_t NW = WG / 64;
-    extern __shared__ __align__(16) uint64_t lds[];    // 16-B aligned: the tables are read with ds_read_b128
-    uint64_t *T = lds;                                               // R*TS, interleaved
-    uint32_t *cur = (uint32_t *)(T + (uint64_t)R * TS);              // [kBandCols] column cursors
+    extern __shared__ __align__(16) uint32_t lds[];    // 16-B aligned: slot words are read with ds_read_b128
+    uint32_t *T = lds;                                               // [TS][R] interleaved slot words
+    uint32_t *V = T + R * TS;                                        // [R][kBandCapMax] high words
+    uint32_t *cur = V + R * kBandCapMax;                             // [kBandCols] column cursors
     uint32_t *pcnt = cur + kBandCols;                                // [R][kBandCols] counts
     uint32_t *pm = pcnt + R * kBandCols;                             // [R][kBandCols] shared so far
     __shared__ uint32_t s_p[R], s_q[R];
@@ -463,6 +504,7 @@ __global__ __launch_bounds__(WG) void k_allpairs_band(
 
     const uint32_t i0 = items[blockIdx.x].x;
     const uint32_t c0 = items[blockIdx.x].y;
+    if (i0 == 0xFFFFFFFFu) return;                      // idle padding item (make_items)
     const uint32_t nrows = min((uint32_t)R, row1 - i0);
     const uint32_t cend = min(c0 + kBandCols, N);
     const uint32_t ncols = cend - c0;
@@ -517,12 +559,11 @@ __global__ __launch_bounds__(WG) void k_allpairs_band(
         for (int r = 0; r < R; r++) pr[r] = s_p[r];
 
         uint64_t t_b0 = prof ? wall_clock64() : 0;
-        // ---- build the R band tables (quotiented cuckoo, band positions)
+        // ---- build the R band tables (quotiented cuckoo, band positions) and V
         uint32_t fam = 0;
         for (; fam < kMaxFam; fam++) {
             const QFields qf = qfields(fam);
-            const uint64_t F1 = (uint64_t)hm << qf.o1, F2 = (uint64_t)hm << qf.o2;
-            for (uint32_t k = tid; k < R * TS; k += WG) T[k] = kEmpty;
+            for (uint32_t k = tid; k < R * TS; k += WG) T[k] = kEmpty32;
             if (tid == 0) s_fail = 0;
             __syncthreads();
             for (uint32_t idx = tid; idx < R * cap; idx += WG) {
@@ -531,25 +572,10 @@ __global__ __launch_bounds__(WG) void k_allpairs_band(
 #pragma unroll
                 for (int rr = 0; rr < R; rr++) if ((uint32_t)rr == r) { p = pr[rr]; nl = nA[rr]; }
                 if (p + t >= nl) continue;
-                uint64_t x = hashes[(uint64_t)(i0 + r) * s + p + t];
+                const uint64_t x = hashes[(uint64_t)(i0 + r) * s + p + t];
                 if (x >= hi) continue;
-                uint32_t ix = t;
-                uint32_t pos = (uint32_t)(x >> qf.o1) & hm;
-                bool placed = false;
-                for (int kick = 0; kick < 96; kick++) {
-                    const bool second = pos >= H;
-                    const uint64_t e = second ? ((x & ~F2) | ((uint64_t)ix << qf.o2))
-                                              : ((x & ~F1) | ((uint64_t)ix << qf.o1));
-                    const unsigned long long oldr = atomicExch((unsigned long long *)&T[(uint64_t)pos * R + r],
-                                                               (unsigned long long)rotr64(e, second ? qf.o2 : qf.o1));
-                    if (oldr == kEmpty) { placed = true; break; }
-                    const uint64_t old = rotr64(oldr, 64 - (second ? qf.o2 : qf.o1));
-                    const uint32_t lp = second ? pos - H : pos;
-                    if (second) { ix = (uint32_t)(old >> qf.o2) & hm; x = (old & ~F2) | ((uint64_t)lp << qf.o2); }
-                    else        { ix = (uint32_t)(old >> qf.o1) & hm; x = (old & ~F1) | ((uint64_t)lp << qf.o1); }
-                    pos = second ? ((uint32_t)(x >> qf.o1) & hm) : (H + ((uint32_t)(x >> qf.o2) & hm));
-                }
-                if (!placed) s_fail = 1;
+                if (fam == 0) V[r * kBandCapMax + t] = (uint32_t)(x >> 32);
+                if (!cuckoo_insert32(T, R, r, H, hm, qf, (uint32_t)x, t)) s_fail = 1;
             }
             __syncthreads();
             // verify every key of the band; count the band's elements per row
@@ -561,11 +587,7 @@ __global__ __launch_bounds__(WG) void k_allpairs_band(
                 if (p + t >= nl) continue;
                 const uint64_t x = hashes[(uint64_t)(i0 + r) * s + p + t];
                 if (x >= hi) continue;
-                const uint64_t e1 = rotr64(T[(uint64_t)((uint32_t)(x >> qf.o1) & hm) * R + r], 64 - qf.o1);
-                const uint64_t e2 = rotr64(T[(uint64_t)(H + ((uint32_t)(x >> qf.o2) & hm)) * R + r], 64 - qf.o2);
-                const bool ok1 = (e1 & ~F1) == (x & ~F1) && ((uint32_t)(e1 >> qf.o1) & hm) == t;
-                const bool ok2 = (e2 & ~F2) == (x & ~F2) && ((uint32_t)(e2 >> qf.o2) & hm) == t;
-                if (!(ok1 || ok2)) s_fail = 1;
+                if (!cuckoo_has32(T, R, r, H, hm, qf, (uint32_t)x, t)) s_fail = 1;
                 if (fam == 0) atomicAdd(&s_q[r], 1u);
             }
             __syncthreads();
@@ -577,7 +599,8 @@ __global__ __launch_bounds__(WG) void k_allpairs_band(
         }
 
         uint64_t t_c0 = prof ? wall_clock64() : 0;
-        // ---- columns: wave w takes columns w, w+NW, ...; next column's first chunk prefetched
+        // ---- columns: wave w takes columns w, w+NW, ...; the next column's
+        // segment is loaded while this one is processed
         uint32_t ci = wave;
         uint64_t nseg[NCH];
         uint32_t nq = 0, nnB = 0;
@@ -586,12 +609,13 @@ __global__ __launch_bounds__(WG) void k_allpairs_band(
             nnB = nhash[c0 + cc];
             const uint64_t *Bn = hashes + (uint64_t)(c0 + cc) * s;
 #pragma unroll
-            for (int k = 0; k < NCH; k++) {
-                const uint32_t j = nq + 64 * k + lane;
-                nseg[k] = ld_col(Bn, j, nnB, s);
-            }
+            for (int k = 0; k < NCH; k++) nseg[k] = ld_col(Bn, nq + 64 * k + lane, nnB, s);
         };
         if (ci < ncols) load_seg(ci);
+        uint32_t o1[R], o2[R];
+        const QFields qf = qfields(fam);
+#pragma unroll
+        for (int r = 0; r < R; r++) { o1[r] = qf.o1; o2[r] = qf.o2; }
         for (; ci < ncols; ci += NW) {
             const uint32_t c = c0 + ci;
             const uint32_t q0 = nq, nB = nnB;
@@ -603,20 +627,16 @@ __global__ __launch_bounds__(WG) void k_allpairs_band(
 #pragma unroll
             for (int r = 0; r < R; r++) actmask |= (uint32_t)((uint32_t)r < nrows && i0 + r < c) << r;
             if (!actmask) continue;
-            uint32_t mrun[R], cntl[R];
+            uint32_t mrun[R], cnt[R];
 #pragma unroll
-            for (int r = 0; r < R; r++) { mrun[r] = rfl(pm[r * kBandCols + ci]); cntl[r] = 0; }   // scalar counters
+            for (int r = 0; r < R; r++) { mrun[r] = rfl(pm[r * kBandCols + ci]); cnt[r] = 0; }   // scalar counters
             const uint64_t *Bc = hashes + (uint64_t)c * s;
-            uint32_t o1[R], o2[R];
-            const QFields qf = qfields(fam);
-#pragma unroll
-            for (int r = 0; r < R; r++) { o1[r] = qf.o1; o2[r] = qf.o2; }
             const uint32_t q = fam == 0
-                ? band_column<R, NCH, true>(Bc, nB, q0, seg, hi, T, o1, o2, s, pr, actmask, mrun, cntl)
-                : band_column<R, NCH, false>(Bc, nB, q0, seg, hi, T, o1, o2, s, pr, actmask, mrun, cntl);
+                ? band_column<R, NCH, true>(Bc, nB, q0, seg, hi, T, V, o1, o2, s, pr, actmask, mrun, cnt)
+                : band_column<R, NCH, false>(Bc, nB, q0, seg, hi, T, V, o1, o2, s, pr, actmask, mrun, cnt);
 #pragma unroll
             for (int r = 0; r < R; r++)
-                if (lane == 0) { pcnt[r * kBandCols + ci] += cntl[r]; pm[r * kBandCols + ci] = mrun[r]; }
+                if (lane == 0) { pcnt[r * kBandCols + ci] += cnt[r]; pm[r * kBandCols + ci] = mrun[r]; }
             if (lane == 0) cur[ci] = q;
         }
         __syncthreads();
@@ -655,6 +675,49 @@ __global__ __launch_bounds__(WG) void k_allpairs_band(
 }
 
 // ------------------------------------------------------------- host driver
+// Work items (row tile i0, column tile c0) of the upper triangle in an
+// XCD-aware order.  Column tiles are aligned (c0 = ct * C) so every row tile
+// shares them; tiles are dealt to the 8 XCDs (largest first, least-loaded
+// XCD) and the per-XCD lists are interleaved so that workgroup b -- which the
+// dispatcher places on XCD b % 8 -- comes from XCD (b % 8)'s list: the
+// workgroups running on one XCD then stream the same ~C column sketches,
+// which stay in that XCD's L2 (the mapping is a speed hint only; any
+// placement gives the same result).  Lists are padded with idle items
+// (i0 = kIdleItem).
+constexpr uint32_t kXcds = 8;
+constexpr uint32_t kIdleItem = 0xFFFFFFFFu;
+
+static std::vector<uint2> make_items(uint32_t row0, uint32_t row1, uint32_t N, uint32_t R, uint32_t C) {
+    const uint32_t nct = (N + C - 1) / C;
+    std::vector<std::vector<uint2>> tiles(nct);
+    size_t total = 0;
+    for (uint32_t i0 = row0; i0 < row1; i0 += R)
+        for (uint32_t ct = (i0 + 1) / C; ct < nct; ct++) { tiles[ct].push_back(make_uint2(i0, ct * C)); total++; }
+    // groups: runs of one column tile's items, at most ~1/16 of an XCD's share,
+    // so that dealing them largest-first balances the XCDs
+    const size_t gmax = std::max<size_t>(1, total / (kXcds * 16));
+    std::vector<std::pair<uint32_t, uint32_t>> groups;              // (tile, first item) -> size via gmax
+    for (uint32_t t = 0; t < nct; t++)
+        for (size_t i = 0; i < tiles[t].size(); i += gmax) groups.push_back({t, (uint32_t)i});
+    auto gsize = [&](const std::pair<uint32_t, uint32_t> &g) {
+        return std::min(gmax, tiles[g.first].size() - g.second);
+    };
+    std::stable_sort(groups.begin(), groups.end(), [&](const auto &a, const auto &b) { return gsize(a) > gsize(b); });
+    std::vector<std::vector<uint2>> lists(kXcds);
+    for (const auto &g : groups) {
+        uint32_t best = 0;
+        for (uint32_t x = 1; x < kXcds; x++) if (lists[x].size() < lists[best].size()) best = x;
+        const auto &tl = tiles[g.first];
+        lists[best].insert(lists[best].end(), tl.begin() + g.second, tl.begin() + g.second + gsize(g));
+    }
+    size_t len = 0;
+    for (auto &l : lists) len = std::max(len, l.size());
+    std::vector<uint2> items(len * kXcds, make_uint2(kIdleItem, 0));
+    for (uint32_t x = 0; x < kXcds; x++)
+        for (size_t i = 0; i < lists[x].size(); i++) items[i * kXcds + x] = lists[x][i];
+    return items;
+}
+
 static int launch_merge(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N,
                         uint64_t seg0, uint64_t npairs, uint16_t *d_common, uint16_t *d_denom,
                         hipStream_t st) {
@@ -673,9 +736,7 @@ static int launch_band(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_
                        uint16_t *d_denom, hipStream_t st) {
     constexpr int R = 4;
     const uint32_t cap = std::min(std::max(ctx->band_cap, 1u), kBandCapMax);
-    std::vector<uint2> items;
-    for (uint32_t i0 = row0; i0 < row1; i0 += R)
-        for (uint32_t c0 = i0 + 1; c0 < N; c0 += kBandCols) items.push_back(make_uint2(i0, c0));
+    const std::vector<uint2> items = make_items(row0, row1, N, R, kBandCols);
     if (items.empty()) return DREPHIP_OK;
     uint2 *d_items;
     uint32_t *d_nfail;
@@ -690,7 +751,7 @@ static int launch_band(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_
         if ((rc = scratch(ctx, "apb_prof", 64, (void **)&d_prof))) return rc;
         HIPC(hipMemsetAsync(d_prof, 0, 64, st));
     }
-    const size_t lds = (size_t)R * (2u << kBandB) * 8 + kBandCols * 4 + 2ull * R * kBandCols * 4;
+    const size_t lds = band_lds_bytes(R);
     // 16 waves x 8 register chunks per band segment (8 waves x 16 chunks,
     // 512-lane workgroups, measured 1.35x slower at s = 10^4)
     HIPC(hipFuncSetAttribute((const void *)k_allpairs_band<R, 8, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -713,15 +774,15 @@ static int launch_band(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_
     return DREPHIP_OK;
 }
 
-template <int R, int NCH>
+template <int R, int NCH, int MINW>
 static int launch_q(drephip_ctx *ctx, uint32_t nitems, size_t lds, hipStream_t st, const uint64_t *h,
-                    const uint32_t *nh, const uint64_t *tabs, const uint8_t *fam, uint32_t N, uint32_t row0,
+                    const uint32_t *nh, const uint32_t *tabs, const uint8_t *fam, uint32_t N, uint32_t row0,
                     uint32_t row1, uint32_t B, const uint2 *items, uint16_t *cm, uint16_t *dn, uint64_t seg0) {
-    HIPC(hipFuncSetAttribute((const void *)k_allpairs_q<R, NCH>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    HIPC(hipFuncSetAttribute((const void *)k_allpairs_q<R, NCH, MINW>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)lds));
     timing_mark(ctx, 2, st, true);
-    hipLaunchKernelGGL((k_allpairs_q<R, NCH>), dim3(nitems), dim3(ap_wg(NCH)), lds, st, h, nh, tabs, fam, ctx->s, N,
-                       row0, row1, B, items, cm, dn, seg0);
+    hipLaunchKernelGGL((k_allpairs_q<R, NCH, MINW>), dim3(nitems), dim3(kApWG), lds, st, h, nh, tabs, fam, ctx->s,
+                       N, row0, row1, B, items, cm, dn, seg0);
     timing_mark(ctx, 2, st, false);
     HIPC(hipGetLastError());
     return DREPHIP_OK;
@@ -737,11 +798,12 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
     const uint64_t seg0 = cond_index(row0, row0 + 1, N);
     const uint64_t seg1 = row1 < N - 1 ? cond_index(row1, row1 + 1, N) : (uint64_t)N * (N - 1) / 2;
     const uint64_t npairs = seg1 - seg0;
-    // table: 2H slots, H = 2^B >= 2s (load <= 1/4) and 2^B > s (positions fit the field)
+    // table: 2H slots, H = 2^B >= 2s (load <= 1/4, and every position and the
+    // empty word's 2^B - 1 fit the field); 32-bit families need B <= 12
     uint32_t B = 4;
     while ((1u << B) < 2 * s) B++;
-    const uint64_t TS = 2ull << B;
-    const bool fits = s <= 2048 && TS * 8 <= kLdsTables;
+    const uint32_t TS = 2u << B;
+    const bool fits = B <= 12 && q_lds_bytes(1, TS, s) <= kLdsBudget;
     int path = force_merge ? DREPHIP_AP_MERGE : ctx->ap_path;
     if (path == DREPHIP_AP_AUTO) path = fits ? DREPHIP_AP_TABLE : DREPHIP_AP_BAND;
     if (path == DREPHIP_AP_TABLE && !fits) {
@@ -754,30 +816,28 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
         return launch_band(ctx, d_hashes, d_nhash, N, row0, row1, seg0, npairs, d_common, d_denom, st);
 
     const uint32_t nrows = row1 - row0;
-    uint64_t *d_tabs;
+    uint32_t *d_tabs;
     uint8_t *d_fam;
     uint32_t *d_nfail;
     uint2 *d_items;
     int rc;
-    if ((rc = scratch(ctx, "ap_tabs", (uint64_t)nrows * TS * 8, (void **)&d_tabs))) return rc;
+    if ((rc = scratch(ctx, "ap_tabs", (uint64_t)nrows * TS * 4, (void **)&d_tabs))) return rc;
     if ((rc = scratch(ctx, "ap_fam", nrows, (void **)&d_fam))) return rc;
     if ((rc = scratch(ctx, "ap_nfail", 4, (void **)&d_nfail))) return rc;
     HIPC(hipMemsetAsync(d_nfail, 0, 4, st));
-    const size_t blds = TS * 8;
-    HIPC(hipFuncSetAttribute((const void *)k_build_qcuckoo, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)blds));
+    const size_t blds = (size_t)TS * 4;
+    HIPC(hipFuncSetAttribute((const void *)k_build_q32, hipFuncAttributeMaxDynamicSharedMemorySize, (int)blds));
     timing_mark(ctx, 3, st, true);
-    hipLaunchKernelGGL(k_build_qcuckoo, dim3(nrows), dim3(256), blds, st, d_hashes, d_nhash, s, row0, B,
-                       d_tabs, d_fam, d_nfail);
+    hipLaunchKernelGGL(k_build_q32, dim3(nrows), dim3(256), blds, st, d_hashes, d_nhash, s, row0, B, d_tabs, d_fam,
+                       d_nfail);
     timing_mark(ctx, 3, st, false);
     HIPC(hipGetLastError());
 
+    // rows per workgroup: the most (8, 4, 2, 1) whose tables + high words fit
     static const uint32_t kR[] = {8, 4, 2, 1};
     uint32_t R = 1;
-    for (uint32_t r : kR) if ((uint64_t)r * TS * 8 <= kLdsTables) { R = r; break; }
-    std::vector<uint2> items;
-    for (uint32_t i0 = row0; i0 < row1; i0 += R)
-        for (uint32_t c0 = i0 + 1; c0 < N; c0 += kApCols) items.push_back(make_uint2(i0, c0));
+    for (uint32_t r : kR) if (q_lds_bytes(r, TS, s) <= kLdsBudget) { R = r; break; }
+    const std::vector<uint2> items = make_items(row0, row1, N, R, kApCols);
     if ((rc = scratch(ctx, "ap_items", items.size() * sizeof(uint2), (void **)&d_items))) return rc;
     HIPC(hipMemcpyAsync(d_items, items.data(), items.size() * sizeof(uint2), hipMemcpyHostToDevice, st));
     uint32_t nfail = 0;
@@ -786,19 +846,30 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
     if (nfail)   // a row table could not be built with any field pair: exact merge kernel instead
         return launch_merge(ctx, d_hashes, d_nhash, N, seg0, npairs, d_common, d_denom, st);
 
-    const size_t lds = (size_t)R * TS * 8 + (size_t)R * kApCols * 4;
+    const size_t lds = q_lds_bytes(R, TS, s);
     const uint32_t ni = (uint32_t)items.size();
-    const bool big = s > 1024;
-#define DREPHIP_Q(RR, NC) launch_q<RR, NC>(ctx, ni, lds, st, d_hashes, d_nhash, d_tabs, d_fam, N, row0, row1, B, d_items, d_common, d_denom, seg0)
-    if (!big) {
+    const uint32_t nch = (s + 63) / 64;
+    // two workgroups per CU when the LDS allows (DREPHIP_AP_ONEWG=1: one, A/B)
+    const bool two = lds <= 80 * 1024 && !getenv("DREPHIP_AP_ONEWG");
+#define DREPHIP_Q(RR, NC) (two ? launch_q<RR, NC, 8>(ctx, ni, lds, st, d_hashes, d_nhash, d_tabs, d_fam, N, row0, row1, B, d_items, d_common, d_denom, seg0) \
+                               : launch_q<RR, NC, 4>(ctx, ni, lds, st, d_hashes, d_nhash, d_tabs, d_fam, N, row0, row1, B, d_items, d_common, d_denom, seg0))
+    if (nch <= 8) {
         switch (R) {
-            case 8: rc = DREPHIP_Q(8, 8); break;       // R = 8 only when H <= 1024, i.e. s <= 512
+            case 8: rc = DREPHIP_Q(8, 8); break;
+            case 4: rc = DREPHIP_Q(4, 8); break;
+            case 2: rc = DREPHIP_Q(2, 8); break;
+            default: rc = DREPHIP_Q(1, 8); break;
+        }
+    } else if (nch <= 16) {
+        switch (R) {
+            case 8: rc = DREPHIP_Q(8, 16); break;
             case 4: rc = DREPHIP_Q(4, 16); break;
             case 2: rc = DREPHIP_Q(2, 16); break;
             default: rc = DREPHIP_Q(1, 16); break;
         }
     } else {
         switch (R) {
+            case 4: rc = DREPHIP_Q(4, 32); break;
             case 2: rc = DREPHIP_Q(2, 32); break;
             default: rc = DREPHIP_Q(1, 32); break;
         }

@@ -36,6 +36,10 @@ __global__ __launch_bounds__(256) void mb(uint32_t *out, int iters, uint32_t c, 
             if constexpr (OP == 13) asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(a[j]) : "v"(c));
             if constexpr (OP == 14) asm volatile("v_mad_u32_u24 %0, %0, %1, %0" : "+v"(a[j]) : "v"(c));
             if constexpr (OP == 15) asm volatile("v_bitop3_b32 %0, %0, %1, %1 bitop3:0x96" : "+v"(a[j]) : "v"(c));
+            if constexpr (OP == 16) asm volatile("v_xor_b32_e64 %0, %1, %0" : "+v"(a[j]) : "v"(c));
+            if constexpr (OP == 17) asm volatile("v_add_u32_e32 %0, %1, %0" : "+v"(a[j]) : "v"(c));
+            if constexpr (OP == 18) asm volatile("v_add_u32_e64 %0, %1, %0" : "+v"(a[j]) : "v"(c));
+            if constexpr (OP == 19) asm volatile("v_xor_b32_e32 %0, %1, %0\n\tv_xor_b32_e64 %0, %1, %0" : "+v"(a[j]) : "v"(c));
         }
     }
     uint32_t s = 0;
@@ -49,7 +53,7 @@ __global__ __launch_bounds__(256) void mb(uint32_t *out, int iters, uint32_t c, 
 static const char *names[] = {"v_xor_b32", "v_mul_lo_u32", "v_mul_hi_u32", "v_mad_u64_u32", "v_lshlrev_b64",
                               "v_lshl_add_u64", "v_alignbit_b32", "v_add3_u32", "v_cndmask_b32", "v_lshrrev_b64",
                               "v_cmp_gt_u64", "v_mov_b32", "v_perm_b32", "v_mul_u32_u24", "v_mad_u32_u24",
-                              "v_bitop3_b32"};
+                              "v_bitop3_b32", "v_xor_b32_e64", "v_add_u32_e32", "v_add_u32_e64", "xor_e32+xor_e64 (2 instr)"};
 
 static unsigned long long *g_cyc;
 static double g_med_cycles;
@@ -82,20 +86,21 @@ int main() {
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
-    float ms[16];
-    double cy[16];
+    float ms[20];
+    double cy[20];
 #define RUN(i) ms[i] = run<i>(d, blocks, iters, e0, e1); cy[i] = g_med_cycles;
     RUN(0) RUN(1) RUN(2) RUN(3) RUN(4) RUN(5) RUN(6) RUN(7)
     RUN(8) RUN(9) RUN(10) RUN(11) RUN(12) RUN(13) RUN(14) RUN(15)
+    RUN(16) RUN(17) RUN(18) RUN(19)
     // wave-instructions per SIMD = waves per SIMD (8) * iters * CHAINS
     const double winst = 8.0 * iters * CHAINS;
     printf("{\"cus\": %d, \"clock_mhz\": %d, \"results\": [\n", cus, p.clockRate / 1000);
-    for (int i = 0; i < 16; i++) {
+    for (int i = 0; i < 20; i++) {
         const double ns_per = ms[i] * 1e6 / winst;
         // a block's 4 waves sit on 4 SIMDs; 8 blocks per CU -> 8 waves per SIMD run together
         const double cyc_per = cy[i] / (8.0 * iters * CHAINS);
         printf("  {\"inst\": \"%s\", \"ms\": %.3f, \"ns_per_wave_inst_per_simd\": %.4f, \"cycles_per_wave_inst_per_simd\": %.3f, \"rel_to_xor\": %.2f}%s\n",
-               names[i], ms[i], ns_per, cyc_per, ms[i] / ms[0], i < 15 ? "," : "");
+               names[i], ms[i], ns_per, cyc_per, ms[i] / ms[0], i < 19 ? "," : "");
     }
     printf("]}\n");
     return 0;
