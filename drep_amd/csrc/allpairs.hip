@@ -419,9 +419,9 @@ __global__ __launch_bounds__(256) void k_allpairs_merge(const uint64_t *__restri
 // literal merge); a band's build is amortised over kBandCols columns.
 // Roofline: as k_allpairs_q (LDS random reads + VALU); column chunks are read
 // once per band per tile, i.e. s * 8 / R bytes per pair from L2.
-constexpr uint32_t kBandCols = 256;
+constexpr uint32_t kBandCols = 128;
 constexpr uint32_t kBandB = 11;                       // H = 2048 slots per choice
-constexpr uint32_t kBandCapMax = (1u << kBandB) / 2;  // <= 1024 elements per row per band
+constexpr uint32_t kBandCapMax = 768;                 // elements per row per band (<= H/2): LDS for 2 workgroups/CU
 
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 #pragma unroll
@@ -438,55 +438,82 @@ __device__ __forceinline__ uint64_t ld_col(const uint64_t *__restrict__ Bc, uint
     return j < nB ? v : kEmpty;
 }
 
-// A column's band segment: the first NCH chunks from registers (loaded while
-// the previous column was processed), slot words read one chunk ahead; a
-// segment longer than NCH chunks continues from memory one chunk at a time.
-// Returns the new cursor.
-template <int R, int NCH, bool FAST>
-__device__ __forceinline__ uint32_t band_column(const uint64_t *__restrict__ Bc, uint32_t nB, uint32_t q,
-                                                const uint64_t (&seg)[NCH], uint64_t hi, const uint32_t *T,
-                                                const uint32_t *V, const uint32_t (&o1)[R],
-                                                const uint32_t (&o2)[R], uint32_t s, const uint32_t (&pr)[R],
-                                                uint32_t actmask, uint32_t (&mrun)[R], uint32_t (&cnt)[R]) {
+// The column phase of one band: wave w takes columns w, w+NW, ... of the
+// item.  A column's band segment streams through a ring of kRing chunks in
+// registers, loaded kRing chunks ahead (the next column's first kRing chunks
+// when a column starts); slot words are read one chunk ahead of the tests.
+template <int R, uint32_t NW, bool FAST>
+__device__ __forceinline__ void band_columns(const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ nhash,
+                                             uint32_t s, const uint32_t *T, const uint32_t *V, uint32_t *cur,
+                                             uint16_t *pcnt, uint16_t *pm, uint32_t c0, uint32_t ncols, uint32_t i0,
+                                             uint32_t nrows, uint32_t wave, uint64_t hi, uint32_t fam,
+                                             const uint32_t (&pr)[R]) {
     constexpr uint32_t H = 1u << kBandB, hm = H - 1;
     const uint32_t lane = threadIdx.x & 63;
-    uint32_t cap[R];
+    uint32_t ci = wave;
+    uint64_t nx[kRing];
+    uint32_t nq = 0, nnB = 0;
+    auto load_first = [&](uint32_t cc) {
+        nq = rfl(cur[cc]);
+        nnB = nhash[c0 + cc];
+        const uint64_t *Bn = hashes + (uint64_t)(c0 + cc) * s;
 #pragma unroll
-    for (int r = 0; r < R; r++) cap[r] = kBandCapMax;
-    bool more = true;
-    Slots<R> sn = read_slots<R, FAST>((uint32_t)seg[0], T, H, hm, o1, o2);
+        for (int k = 0; k < kRing; k++) nx[k] = ld_col(Bn, nq + 64 * k + lane, nnB, s);
+    };
+    if (ci < ncols) load_first(ci);
+    uint32_t o1[R], o2[R], cap_r[R];
+    const QFields qf = qfields(fam);
 #pragma unroll
-    for (int k = 0; k < NCH; k++) {
-        if (!more) continue;                                       // wave-uniform
-        const Slots<R> sl = sn;
-        if (k + 1 < NCH) sn = read_slots<R, FAST>((uint32_t)seg[k + 1], T, H, hm, o1, o2);
-        const uint64_t inb = __builtin_amdgcn_ballot_w64(seg[k] < hi);
-        probe_rows<R, FAST>(sl, seg[k], q + lane, V, kBandCapMax, hm, o1, o2, actmask, inb, pr, cap, s, mrun, cnt);
-        const uint32_t nin = (uint32_t)__popcll(inb);
-        q += nin;
-        more = nin == 64;
+    for (int r = 0; r < R; r++) { o1[r] = qf.o1; o2[r] = qf.o2; cap_r[r] = kBandCapMax; }
+    for (; ci < ncols; ci += NW) {
+        const uint32_t c = c0 + ci;
+        const uint32_t q0 = nq, nB = nnB;
+        uint64_t rg[kRing];
+#pragma unroll
+        for (int k = 0; k < kRing; k++) rg[k] = nx[k];
+        if (ci + NW < ncols) load_first(ci + NW);
+        uint32_t actmask = 0;
+#pragma unroll
+        for (int r = 0; r < R; r++) actmask |= (uint32_t)((uint32_t)r < nrows && i0 + r < c) << r;
+        if (!actmask) continue;
+        uint32_t mrun[R], cnt[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) { mrun[r] = rfl(pm[r * kBandCols + ci]); cnt[r] = 0; }   // scalar counters
+        const uint64_t *Bc = hashes + (uint64_t)c * s;
+        uint32_t q = q0;
+        bool more = true;
+        Slots<R> sn = read_slots<R, FAST>((uint32_t)rg[0], T, H, hm, o1, o2);
+        for (uint32_t kb = 0; more; kb += kRing) {
+#pragma unroll
+            for (int u = 0; u < kRing; u++) {
+                if (!more) continue;                                  // wave-uniform
+                const uint64_t b = rg[u];
+                const Slots<R> sl = sn;
+                rg[u] = ld_col(Bc, q0 + 64 * (kb + u + kRing) + lane, nB, s);   // refill the ring
+                const uint32_t bn = (uint32_t)rg[(u + 1) % kRing];
+                const uint64_t inb = __builtin_amdgcn_ballot_w64(b < hi);
+                sn = read_slots<R, FAST>(bn, T, H, hm, o1, o2);
+                probe_rows<R, FAST>(sl, b, q + lane, V, kBandCapMax, hm, o1, o2, actmask, inb, pr, cap_r,
+                                    s, mrun, cnt);
+                const uint32_t nin = (uint32_t)__popcll(inb);
+                q += nin;
+                more = nin == 64;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; r++)
+            if (lane == 0) { pcnt[r * kBandCols + ci] += cnt[r]; pm[r * kBandCols + ci] = mrun[r]; }
+        if (lane == 0) cur[ci] = q;
     }
-    if (!more) return q;
-    uint64_t b = ld_col(Bc, q + lane, nB, s);
-    for (;;) {
-        const uint64_t bn = ld_col(Bc, q + 64 + lane, nB, s);
-        const Slots<R> sl = read_slots<R, FAST>((uint32_t)b, T, H, hm, o1, o2);
-        const uint64_t inb = __builtin_amdgcn_ballot_w64(b < hi);
-        probe_rows<R, FAST>(sl, b, q + lane, V, kBandCapMax, hm, o1, o2, actmask, inb, pr, cap, s, mrun, cnt);
-        const uint32_t nin = (uint32_t)__popcll(inb);
-        q += nin;
-        if (nin < 64) break;
-        b = bn;
-    }
-    return q;
 }
 
 __host__ __device__ constexpr size_t band_lds_bytes(uint32_t R) {
-    return (size_t)R * (2u << kBandB) * 4 + (size_t)R * kBandCapMax * 4 + kBandCols * 4 + 2ull * R * kBandCols * 4;
+    return (size_t)R * (2u << kBandB) * 4 + (size_t)R * kBandCapMax * 4 + kBandCols * 4 + 2ull * R * kBandCols * 2;
 }
+static_assert(band_lds_bytes(4) <= 80 * 1024, "band kernel LDS must allow two workgroups per CU");
 
-template <int R, int NCH, int WG>
-__global__ __launch_bounds__(WG) void k_allpairs_band(
+template <int R, int WG, int MINW>
+__global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
     const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ nhash, uint32_t s, uint32_t N,
     uint32_t row1, uint32_t cap, const uint2 *__restrict__ items, uint16_t *__restrict__ common,
     uint16_t *__restrict__ denom, uint64_t seg0, uint32_t *__restrict__ nfail, uint64_t *__restrict__ prof) {
@@ -496,8 +523,8 @@ __global__ __launch_bounds__(WG) void k_allpairs_band(
     uint32_t *T = lds;                                               // [TS][R] interleaved slot words
     uint32_t *V = T + R * TS;                                        // [R][kBandCapMax] high words
     uint32_t *cur = V + R * kBandCapMax;                             // [kBandCols] column cursors
-    uint32_t *pcnt = cur + kBandCols;                                // [R][kBandCols] counts
-    uint32_t *pm = pcnt + R * kBandCols;                             // [R][kBandCols] shared so far
+    uint16_t *pcnt = (uint16_t *)(cur + kBandCols);                  // [R][kBandCols] counts (<= s)
+    uint16_t *pm = pcnt + R * kBandCols;                             // [R][kBandCols] shared so far (<= s)
     __shared__ uint32_t s_p[R], s_q[R];
     __shared__ uint64_t s_hi;
     __shared__ int s_done, s_fail, s_abort;
@@ -599,46 +626,11 @@ __global__ __launch_bounds__(WG) void k_allpairs_band(
         }
 
         uint64_t t_c0 = prof ? wall_clock64() : 0;
-        // ---- columns: wave w takes columns w, w+NW, ...; the next column's
-        // segment is loaded while this one is processed
-        uint32_t ci = wave;
-        uint64_t nseg[NCH];
-        uint32_t nq = 0, nnB = 0;
-        auto load_seg = [&](uint32_t cc) {
-            nq = rfl(cur[cc]);
-            nnB = nhash[c0 + cc];
-            const uint64_t *Bn = hashes + (uint64_t)(c0 + cc) * s;
-#pragma unroll
-            for (int k = 0; k < NCH; k++) nseg[k] = ld_col(Bn, nq + 64 * k + lane, nnB, s);
-        };
-        if (ci < ncols) load_seg(ci);
-        uint32_t o1[R], o2[R];
-        const QFields qf = qfields(fam);
-#pragma unroll
-        for (int r = 0; r < R; r++) { o1[r] = qf.o1; o2[r] = qf.o2; }
-        for (; ci < ncols; ci += NW) {
-            const uint32_t c = c0 + ci;
-            const uint32_t q0 = nq, nB = nnB;
-            uint64_t seg[NCH];
-#pragma unroll
-            for (int k = 0; k < NCH; k++) seg[k] = nseg[k];
-            if (ci + NW < ncols) load_seg(ci + NW);
-            uint32_t actmask = 0;
-#pragma unroll
-            for (int r = 0; r < R; r++) actmask |= (uint32_t)((uint32_t)r < nrows && i0 + r < c) << r;
-            if (!actmask) continue;
-            uint32_t mrun[R], cnt[R];
-#pragma unroll
-            for (int r = 0; r < R; r++) { mrun[r] = rfl(pm[r * kBandCols + ci]); cnt[r] = 0; }   // scalar counters
-            const uint64_t *Bc = hashes + (uint64_t)c * s;
-            const uint32_t q = fam == 0
-                ? band_column<R, NCH, true>(Bc, nB, q0, seg, hi, T, V, o1, o2, s, pr, actmask, mrun, cnt)
-                : band_column<R, NCH, false>(Bc, nB, q0, seg, hi, T, V, o1, o2, s, pr, actmask, mrun, cnt);
-#pragma unroll
-            for (int r = 0; r < R; r++)
-                if (lane == 0) { pcnt[r * kBandCols + ci] += cnt[r]; pm[r * kBandCols + ci] = mrun[r]; }
-            if (lane == 0) cur[ci] = q;
-        }
+        // ---- columns: wave w takes columns w, w+NW, ...
+        if (fam == 0)
+            band_columns<R, NW, true>(hashes, nhash, s, T, V, cur, pcnt, pm, c0, ncols, i0, nrows, wave, hi, fam, pr);
+        else
+            band_columns<R, NW, false>(hashes, nhash, s, T, V, cur, pcnt, pm, c0, ncols, i0, nrows, wave, hi, fam, pr);
         __syncthreads();
         if (tid < (uint32_t)R) s_p[tid] += s_q[tid];
         if (prof && tid == 0) {
@@ -751,12 +743,10 @@ static int launch_band(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_
         if ((rc = scratch(ctx, "apb_prof", 64, (void **)&d_prof))) return rc;
         HIPC(hipMemsetAsync(d_prof, 0, 64, st));
     }
-    const size_t lds = band_lds_bytes(R);
-    // 16 waves x 8 register chunks per band segment (8 waves x 16 chunks,
-    // 512-lane workgroups, measured 1.35x slower at s = 10^4)
-    HIPC(hipFuncSetAttribute((const void *)k_allpairs_band<R, 8, 1024>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const size_t lds = band_lds_bytes(R);         // <= 80 KiB: two workgroups per CU
+    HIPC(hipFuncSetAttribute((const void *)k_allpairs_band<R, 1024, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     timing_mark(ctx, 2, st, true);
-    hipLaunchKernelGGL((k_allpairs_band<R, 8, 1024>), dim3((uint32_t)items.size()), dim3(1024), lds, st, d_hashes,
+    hipLaunchKernelGGL((k_allpairs_band<R, 1024, 8>), dim3((uint32_t)items.size()), dim3(1024), lds, st, d_hashes,
                        d_nhash, ctx->s, N, row1, cap, d_items, d_common, d_denom, seg0, d_nfail, d_prof);
     timing_mark(ctx, 2, st, false);
     HIPC(hipGetLastError());

@@ -161,8 +161,9 @@ int drephip_distance_lut(int k, uint32_t denom, double *lut /* denom+1 */);
  *   DREPHIP_AP_AUTO  whole-row LDS tables for s <= 2048, value bands above;
  *   DREPHIP_AP_TABLE k_allpairs_q (s <= 2048);
  *   DREPHIP_AP_BAND  k_allpairs_band, band_cap (1..1024) elements per row per
- *                    band (the default 1024 is the production setting; small
- *                    caps exercise many bands on small sketches in tests);
+ *                    band, clamped to the kernel's LDS budget (768; the
+ *                    default is the production setting; small caps exercise
+ *                    many bands on small sketches in tests);
  *   DREPHIP_AP_MERGE k_allpairs_merge (literal merge, cross-check only). */
 #define DREPHIP_AP_AUTO 0
 #define DREPHIP_AP_TABLE 1
