@@ -26,15 +26,21 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
-# VALU issue peak: 256 CU x 4 SIMD-32 x 32 lanes/cycle x 2.4 GHz (a wave64 VALU
-# instruction issues over 2 cycles, MI355X_MICROARCH.md)
+# VALU issue peak: 256 CU x 4 SIMD-32 x 32 lanes/cycle x 2.4 GHz (a wave64
+# instruction issues over 2 cycles, MI355X_MICROARCH.md; two-operand 32-bit
+# ops measure 1.0 ns per wave-instruction per SIMD under load).  The Murmur
+# loop is mostly three-operand / 64-bit / multiply ops, which measure
+# 1.7-2.0 ns (tools/valu_microbench.hip, profiles/r01_valu_microbench.json):
+# the binding model is the measured cost of the loop's own instruction mix
+# (valu_model.mix_ns_per_wave_inst_per_simd / frac_of_mix_throughput).
 VALU_PEAK_TINST = 256 * 4 * 32 * 2.4e9 / 1e12
-# measured throughput cost of the integer VOP3 ops that make up the Murmur loop
-# (v_mul_lo_u32, v_mad_u64_u32, v_alignbit_b32, v_add3_u32, v_lshl_add_u64 ...):
-# 2.85-3.1 cycles per wave-instruction at 8 waves/SIMD (tools/valu_microbench.hip,
-# profiles/r01_valu_microbench.json) -> attainable ~2/2.9 of the issue peak
-VALU_VOP3_CYCLES = 2.9
-SKETCH_DEFAULT_VARIANT = "4"   # must match drephip_ctx::sketch_kernel default (ctx.h)
+N_SIMD = 256 * 4
+# measured throughput (ns per wave64 instruction per SIMD, 8 waves/SIMD) of the
+# integer instructions the Murmur loop is made of; instructions the microbench
+# does not cover are priced as v_xor (its v_cndmask figure is a VCC-hazard
+# artefact of the microbench loop and is not used)
+MICROBENCH = os.path.join(ROOT, "profiles", "r01_valu_microbench.json")
+SKETCH_DEFAULT_VARIANT = "5"   # must match drephip_ctx::sketch_kernel default (ctx.h)
 
 
 def parse():
@@ -218,18 +224,31 @@ def main():
     if os.path.exists(isa_path):
         isa = json.load(open(isa_path))["variants"].get(variant)
         if isa:
-            # lane-instructions issued per second vs the VALU issue peak (2-cycle
-            # wave64 issue at 2.4 GHz); "attainable" prices every instruction at
-            # the measured integer-VOP3 cost instead
+            # lane-instructions issued per second vs the VALU issue peak, and
+            # the issue time per wave-instruction vs the measured cost of the
+            # same instruction mix (microbench)
             ach = kmers_per_s * isa["valu_per_kmer"] / 1e12
-            attain = VALU_PEAK_TINST * 2.0 / VALU_VOP3_CYCLES
+            ns_inst = N_SIMD / (kmers_per_s * isa["valu_per_kmer"] / 64) * 1e9
             valu.update({"kernel": isa["kernel"], "valu_per_kmer": isa["valu_per_kmer"],
                          "mul_per_kmer": isa["mul_per_kmer"], "achieved": ach,
                          "peak": VALU_PEAK_TINST, "unit": "T lane-inst/s", "frac": ach / VALU_PEAK_TINST,
-                         "attainable": attain, "frac_of_attainable": ach / attain,
-                         "source": "profiles/sketch_isa.json (tools/isa_count.py); attainable = peak x 2 / "
-                                   "%.1f measured cycles per integer VOP3 wave-instruction "
-                                   "(profiles/r01_valu_microbench.json)" % VALU_VOP3_CYCLES})
+                         "ns_per_wave_inst_per_simd": ns_inst,
+                         "source": "profiles/sketch_isa.json (tools/isa_count.py)"})
+            mix = isa.get("valu_mix_per_kmer")
+            if mix and os.path.exists(MICROBENCH):
+                mb = {r["inst"]: r["ns_per_wave_inst_per_simd"] for r in json.load(open(MICROBENCH))["results"]}
+                base = mb["v_xor_b32"]
+
+                def cost(op):
+                    for name, ns in mb.items():
+                        if op.startswith(name) and not name.startswith("v_cndmask"):
+                            return ns
+                    return base
+                mix_ns = sum(n * cost(op) for op, n in mix.items()) / sum(mix.values())
+                valu.update({"mix_ns_per_wave_inst_per_simd": mix_ns,
+                             "frac_of_mix_throughput": mix_ns / ns_inst,
+                             "mix_source": "profiles/r01_valu_microbench.json (8 waves/SIMD, "
+                                           "independent chains), weighted by the hot-loop mix"})
 
     # ---- output segment D2H (PCIe-inclusive leg; not part of `value`)
     torch.cuda.synchronize()

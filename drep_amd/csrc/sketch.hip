@@ -100,7 +100,7 @@ __device__ __forceinline__ uint64_t murmur21(uint64_t k1, uint64_t k2, uint64_t 
 // flushed to the per-genome set after the tile, so the hot loop issues no
 // global memory operation with a wait; a full buffer spills to the set
 // directly.
-constexpr uint32_t kStage = 1024;
+constexpr uint32_t kStage = 512;      // 4 KiB: with the tables, 8 workgroups (32 waves) per CU
 
 // ------------------------------------------------------- hash kernel (v3)
 // Kept for A/B against v4 (DREPHIP_SKETCH_KERNEL=3).  Rolls forward and
@@ -398,6 +398,172 @@ __global__ __launch_bounds__(kTile / LANE) void k_sketch_hash21_v4(
     for (uint32_t i = threadIdx.x; i < n; i += WG) set_insert(S, mask, C, limit, stage[i]);
 }
 
+// ------------------------------------------------------- hash kernel (v5)
+// v4 with the two Murmur body multiplies folded into tables.  For block word
+// k1 (bases 0-7): X = k1*c1 = TA1[x] + TB1[y] << 32, so Xlo = lo(TA1[x]) and
+// Xhi = hi(TA1[x]) + TB1[y]; rotl(X, 31) is the disjoint bit sum
+//     (Xhi >> 1) + (Xlo << 31) + ((Xhi & 1) << 63)
+// and, c2 being odd,
+//     rotl(X, 31) * c2 = (Xhi >> 1) * c2 + TT1[x] + ((Xhi & 1) << 63),
+//     TT1[x] = (Xlo << 31) * c2                      (one table per 4 bases)
+//     -> one v_mad_u64_u32 (h * lo(c2) + TT1) and a high-word fix
+//        h * hi(c2) + (Xhi << 31).
+// For k2 (bases 8-15): X = k2*c2, rotl(X, 33) = ((Xlo & 0x7fffffff) << 33) +
+// (Xlo >> 31) + 2 Xhi, so
+//     rotl(X, 33) * c1 = Xhi * (2 c1) + TT2[x'],
+//     TT2[x'] = ((Xlo & 0x7fffffff) << 33) * c1 + (Xlo >> 31) * c1.
+// Saves two rotates, a 32x32 multiply and an add per block word (measured-cost
+// model: ~9 % of the k-mer's VALU time) for two more LDS reads per k-mer.
+struct SketchTables5 {
+    uint64_t tt1[256], tt2[256], t3[1024];
+    uint32_t ta1[256], ta2[256], tb1[256], tb2[256];   // ta = hi(a * c)
+};
+
+__device__ void build_tables5(SketchTables5 &tb, uint32_t tid, uint32_t nthreads) {
+    constexpr uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
+    for (uint32_t x = tid; x < 256; x += nthreads) {
+        const uint32_t a = ascii4(x);
+        const uint64_t A1 = (uint64_t)a * c1, A2 = (uint64_t)a * c2;
+        const uint32_t x1 = (uint32_t)A1, x2 = (uint32_t)A2;
+        tb.tt1[x] = ((uint64_t)x1 << 31) * c2;
+        tb.tt2[x] = ((uint64_t)(x2 & 0x7fffffffu) << 33) * c1 + (uint64_t)(x2 >> 31) * c1;
+        tb.ta1[x] = (uint32_t)(A1 >> 32);
+        tb.ta2[x] = (uint32_t)(A2 >> 32);
+        tb.tb1[x] = a * (uint32_t)c1;
+        tb.tb2[x] = a * (uint32_t)c2;
+    }
+    for (uint32_t y = tid; y < 1024; y += nthreads) {
+        const uint64_t k3 = (uint64_t)ascii4(y >> 2) | ((uint64_t)ascii4((y & 3u) << 6) & 0xffu) << 32;
+        tb.t3[y] = (rotl64_ab(k3 * c1, 31) * c2) ^ 21u;
+    }
+}
+
+__device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {   // one v_mad_u64_u32
+    return (uint64_t)a * b + c;
+}
+
+__device__ __forceinline__ void murmur21_tab5(const SketchTables5 &tb, uint32_t hi, uint32_t lo, uint32_t seed,
+                                              uint64_t &p1, uint64_t &p2) {
+    constexpr uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
+    constexpr uint64_t d1 = c1 * 2;                                  // 2 c1 mod 2^64
+    const uint32_t x = hi >> 24, xp = (hi >> 8) & 0xffu;
+    const uint32_t X1 = tb.ta1[x] + tb.tb1[(hi >> 16) & 0xffu];        // hi(k1 * c1)
+    const uint32_t X2 = tb.ta2[xp] + tb.tb2[hi & 0xffu];               // hi(k2 * c2)
+    const uint64_t k3 = tb.t3[lo >> 22];
+    // rotl(k1 c1, 31) c2 ^ seed
+    const uint32_t h = X1 >> 1;
+    const uint64_t P1 = mad64(h, (uint32_t)c2, tb.tt1[x]);
+    const uint32_t g1hi = (uint32_t)(P1 >> 32) + h * (uint32_t)(c2 >> 32) + (X1 << 31);
+    uint64_t h1 = ((uint64_t)g1hi << 32) | ((uint32_t)P1 ^ seed);
+    h1 = x5_plus(rotl64_ab(h1, 27), 5ull * seed + 0x52dce729);   // (rotl + seed) * 5 + c
+    // rotl(k2 c2, 33) c1 ^ seed
+    const uint64_t P2 = mad64(X2, (uint32_t)d1, tb.tt2[xp]);
+    const uint32_t g2hi = (uint32_t)(P2 >> 32) + X2 * (uint32_t)(d1 >> 32);
+    uint64_t h2 = ((uint64_t)g2hi << 32) | ((uint32_t)P2 ^ seed);
+    h2 = x5_plus(add64(rotl64_ab(h2, 31), h1), 0x38495ab5);
+    h1 ^= k3;
+    h2 ^= 21u;
+    h1 = add64(h1, h2);
+    h2 = add64(h2, h1);
+    p1 = fmix64_pre(h1);
+    p2 = fmix64_pre(h2);
+}
+
+template <int LANE, int BATCH>
+__global__ __launch_bounds__(kTile / LANE) void k_sketch_hash21_v5(
+    const uint32_t *__restrict__ codes, const uint32_t *__restrict__ valid,
+    const uint64_t *__restrict__ tile_base, const uint32_t *__restrict__ tile_genome,
+    const uint64_t *__restrict__ thr, unsigned long long *__restrict__ sets,
+    uint32_t *__restrict__ cnt, uint32_t set_log2, uint32_t limit, uint32_t seed, uint64_t wlast) {
+    constexpr uint32_t WG = kTile / LANE;
+    constexpr int NCH = LANE / 16;
+    __shared__ SketchTables5 tb;
+    __shared__ uint64_t stage[kStage];
+    __shared__ uint32_t nstage;
+    const uint32_t t = blockIdx.x;
+    const uint32_t g = tile_genome[t];
+    const uint64_t T = thr[g];
+    const uint32_t Thi = (uint32_t)(T >> 32);
+    const uint32_t Tp = Thi == 0xFFFFFFFFu ? Thi : Thi + 1;     // prefilter bound (see murmur21_tab)
+    const uint64_t start = tile_base[t] + (uint64_t)threadIdx.x * LANE;
+    const uint32_t mask = (1u << set_log2) - 1;
+    unsigned long long *S = sets + ((uint64_t)g << set_log2);
+    uint32_t *C = cnt + g;
+    if (threadIdx.x == 0) nstage = 0;
+    build_tables5(tb, threadIdx.x, WG);
+
+    const uint64_t m0 = start / 16;
+    auto ld = [&](int j) -> uint32_t {
+        const uint64_t w = m0 + j;
+        return codes[w < wlast ? w : wlast];
+    };
+    uint32_t nf0 = ~ld(-2), nf1 = ~ld(-1), nf2 = ~ld(0);
+    uint32_t r0 = rev_fields16(~nf0), r1 = rev_fields16(~nf1), r2 = rev_fields16(~nf2);
+    uint32_t f3 = ld(1);
+    uint32_t r3 = rev_fields16(f3);
+    uint32_t fnext = ld(2);
+    const uint32_t *vw = valid + (start - kWarm) / 32;
+    uint64_t vhist = (uint64_t)vw[0] << 32;
+    uint32_t vcur = vw[1];
+    __syncthreads();
+
+#pragma unroll 1
+    for (int wi = 0; wi < NCH; wi++) {
+        const uint32_t vbits = (vcur >> ((wi & 1) * 16)) & 0xffffu;
+        if (wi + 1 < NCH && (wi & 1)) vcur = vw[2 + (wi >> 1)];
+        vhist = (vhist >> 16) | ((uint64_t)vbits << 48);
+#pragma unroll
+        for (int b0 = 0; b0 < 16; b0 += BATCH) {
+            uint64_t p1[BATCH], p2[BATCH];
+            bool hit = false;
+#pragma unroll
+            for (int b = 0; b < BATCH; b++) {
+                const int r = b0 + b;
+                uint32_t chi, clo, fhi, flo;
+                if (r == 15) { chi = nf2; clo = nf1; }
+                else {
+                    chi = __builtin_amdgcn_alignbit(nf2, nf1, 2 * (r + 1));
+                    clo = __builtin_amdgcn_alignbit(nf1, nf0, 2 * (r + 1));
+                }
+                if (r < 4) {
+                    fhi = __builtin_amdgcn_alignbit(r0, r1, 32 - 2 * (r + 12));
+                    flo = __builtin_amdgcn_alignbit(r1, r2, 32 - 2 * (r + 12));
+                } else if (r == 4) {
+                    fhi = r1; flo = r2;
+                } else {
+                    fhi = __builtin_amdgcn_alignbit(r1, r2, 32 - 2 * (r - 4));
+                    flo = __builtin_amdgcn_alignbit(r2, r3, 32 - 2 * (r - 4));
+                }
+                const uint64_t fw = ((uint64_t)fhi << 32) | flo;
+                const uint64_t rc = ((uint64_t)chi << 32) | clo;
+                const uint64_t cc = fw <= rc ? fw : rc;
+                murmur21_tab5(tb, (uint32_t)(cc >> 32), (uint32_t)cc, seed, p1[b], p2[b]);
+                hit |= (uint32_t)(p1[b] >> 32) + (uint32_t)(p2[b] >> 32) + 1u <= Tp;
+            }
+            if (__builtin_expect(hit, 0)) {
+                const uint64_t ok = run21(vhist);
+#pragma unroll
+                for (int b = 0; b < BATCH; b++) {
+                    const uint64_t h = murmur_fin(p1[b], p2[b]);
+                    if (h <= T && ((ok >> (48 + b0 + b)) & 1)) {
+                        const uint32_t slot = atomicAdd(&nstage, 1u);
+                        if (slot < kStage) stage[slot] = h;
+                        else set_insert(S, mask, C, limit, h);
+                    }
+                }
+            }
+        }
+        nf0 = nf1; nf1 = nf2; nf2 = ~f3;
+        r0 = r1; r1 = r2; r2 = r3;
+        f3 = fnext;
+        r3 = rev_fields16(f3);
+        fnext = ld(wi + 3);
+    }
+    __syncthreads();
+    const uint32_t n = min(nstage, kStage);
+    for (uint32_t i = threadIdx.x; i < n; i += WG) set_insert(S, mask, C, limit, stage[i]);
+}
+
 // ----------------------------------------------------------------- finalize
 enum : uint8_t { ST_OK = 0, ST_UP = 1, ST_DOWN = 2 };
 
@@ -609,7 +775,11 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
         }
         if (nt > 0) {
             timing_mark(ctx, 0, st, true);
-            if (ctx->sketch_kernel != 3)
+            if (ctx->sketch_kernel == 5)
+                hipLaunchKernelGGL((k_sketch_hash21_v5<kLaneBases, 8>), dim3(nt), dim3(kTile / kLaneBases), 0, st,
+                                   d_codes, d_valid, tb_tiles_b, tb_tiles_g, d_thr, d_sets, d_cnt, plan.set_log2,
+                                   limit, ctx->seed, wlast);
+            else if (ctx->sketch_kernel != 3)
                 hipLaunchKernelGGL((k_sketch_hash21_v4<kLaneBases, 8>), dim3(nt), dim3(kTile / kLaneBases), 0, st,
                                    d_codes, d_valid, tb_tiles_b, tb_tiles_g, d_thr, d_sets, d_cnt, plan.set_log2,
                                    limit, ctx->seed, wlast);

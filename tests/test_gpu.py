@@ -109,6 +109,31 @@ def test_sketch_sizes_vs_oracle(s):
         assert np.array_equal(h[g, :nh[g]], want)
 
 
+@pytest.mark.parametrize("variant", ["3", "4", "5"])
+def test_sketch_kernel_variants_vs_oracle(variant, monkeypatch):
+    """Every hash-kernel variant (DREPHIP_SKETCH_KERNEL, read at context
+    creation; 5 is the default) gives the oracle's sketches, including
+    lower case, N runs, multi-record genomes and a partial sketch."""
+    monkeypatch.setenv("DREPHIP_SKETCH_KERNEL", variant)
+    rng = np.random.default_rng(int(variant))
+    A = np.frombuffer(b"ACGTacgtN", dtype=np.uint8)
+    recs = [A[rng.choice(9, 300_000, p=[.24, .24, .24, .24, .01, .01, .01, .01, 0])],
+            A[rng.choice(9, 50_000, p=[.2, .2, .2, .2, 0, 0, 0, 0, .2])],
+            A[rng.integers(0, 4, 700)]]
+    seq = np.concatenate(recs)
+    rec_off = np.concatenate([[0], np.cumsum([len(r) for r in recs])]).astype(np.uint64)
+    gro = np.array([0, 2, 3], dtype=np.uint64)           # genome 0 = records 0-1, genome 1 = record 2
+    with _lib.Context(0, 21, S, 42) as ctx:
+        h, nh, _ = ctx.sketch_records(seq, rec_off, gro)
+    for g, (a, b) in enumerate([(0, 2), (2, 3)]):
+        sub = np.concatenate(recs[a:b])
+        sub = np.where((sub >= 97) & (sub <= 122), sub - 32, sub).astype(np.uint8)   # the oracle takes upper case
+        off = np.concatenate([[0], np.cumsum([len(r) for r in recs[a:b]])]).astype(np.uint64)
+        want = oracle.sketch_records(sub, off, 21, S, 42)
+        assert nh[g] == len(want) and np.array_equal(h[g, :nh[g]], want)
+    assert nh[1] < S
+
+
 def test_synth_device_matches_oracle_generator(ctx1000):
     """The bench's on-device generator + device sketch == oracle generator +
     oracle sketch (5 Mbp genomes, the BASELINE genome size)."""

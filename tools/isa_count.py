@@ -11,7 +11,7 @@ import subprocess
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = {"3": ("k_sketch_hash21_v3", 8), "4": ("k_sketch_hash21_v4", 8)}   # variant: (name, k-mers/block)
+KERNELS = {"3": ("k_sketch_hash21_v3", 8), "4": ("k_sketch_hash21_v4", 8), "5": ("k_sketch_hash21_v5", 8)}   # variant: (name, k-mers/block)
 
 
 def main():
@@ -35,15 +35,22 @@ def main():
             elif cur is not None and line.startswith("\t") and not line.strip().startswith((".", ";")):
                 cur[line.strip().split()[0]] += 1
         # the hash blocks: those with the 64-bit multiply chains (mad_u64 per k-mer)
-        hot = [b for b in blocks if b["v_mad_u64_u32"] >= 4 * per]
+        hot = [b for b in blocks if b["v_mad_u64_u32"] >= 4 * per or
+               (b["v_mad_u64_u32"] >= 3 * per and b["ds_read_b128"] >= 2 * per)]
         valu = [sum(v for k, v in b.items() if k.startswith("v_")) for b in hot]
         mul = [b["v_mul_lo_u32"] + b["v_mad_u64_u32"] + b["v_mul_hi_u32"] for b in hot]
         lds = [sum(v for k, v in b.items() if k.startswith("ds_read")) for b in hot]
+        mix = collections.Counter()
+        for b in hot:
+            for k, v in b.items():
+                if k.startswith("v_"):
+                    mix[k] += v
         out["variants"][var] = {
             "kernel": name, "kmers_per_block": per, "blocks": len(hot),
             "valu_per_kmer": sum(valu) / len(hot) / per,
             "mul_per_kmer": sum(mul) / len(hot) / per,
             "lds_reads_per_kmer": sum(lds) / len(hot) / per,
+            "valu_mix_per_kmer": {k: v / len(hot) / per for k, v in sorted(mix.items())},
         }
     print(json.dumps(out, indent=1))
 

@@ -10,6 +10,7 @@
 #include <algorithm>
 
 #define CHAINS 8
+#define REPS 8      // CHAINS*REPS instructions per loop iteration: loop overhead < 5 %
 template <int OP>
 __global__ __launch_bounds__(256) void mb(uint32_t *out, int iters, uint32_t c, unsigned long long *cyc) {
     unsigned long long t0;
@@ -19,7 +20,8 @@ __global__ __launch_bounds__(256) void mb(uint32_t *out, int iters, uint32_t c, 
     for (int j = 0; j < CHAINS; j++) { a[j] = threadIdx.x * 7 + j; b[j] = ((uint64_t)a[j] << 32) | (a[j] * 3); }
     for (int i = 0; i < iters; i++) {
 #pragma unroll
-        for (int j = 0; j < CHAINS; j++) {
+        for (int jj = 0; jj < CHAINS * REPS; jj++) {
+            const int j = jj % CHAINS;
             if constexpr (OP == 0) asm volatile("v_xor_b32 %0, %1, %0" : "+v"(a[j]) : "v"(c));
             if constexpr (OP == 1) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a[j]) : "v"(c));
             if constexpr (OP == 2) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(a[j]) : "v"(c));
@@ -40,6 +42,9 @@ __global__ __launch_bounds__(256) void mb(uint32_t *out, int iters, uint32_t c, 
             if constexpr (OP == 17) asm volatile("v_add_u32_e32 %0, %1, %0" : "+v"(a[j]) : "v"(c));
             if constexpr (OP == 18) asm volatile("v_add_u32_e64 %0, %1, %0" : "+v"(a[j]) : "v"(c));
             if constexpr (OP == 19) asm volatile("v_xor_b32_e32 %0, %1, %0\n\tv_xor_b32_e64 %0, %1, %0" : "+v"(a[j]) : "v"(c));
+            if constexpr (OP == 20) asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(a[j]) : "v"(c));
+            if constexpr (OP == 21) asm volatile("v_add_f32_e32 %0, %1, %0" : "+v"(a[j]) : "v"(c));
+            if constexpr (OP == 22) asm volatile("v_pk_fma_f32 %0, %0, %1, %1" : "+v"(b[j]) : "v"(b[(j + 1) % CHAINS]));
         }
     }
     uint32_t s = 0;
@@ -53,7 +58,8 @@ __global__ __launch_bounds__(256) void mb(uint32_t *out, int iters, uint32_t c, 
 static const char *names[] = {"v_xor_b32", "v_mul_lo_u32", "v_mul_hi_u32", "v_mad_u64_u32", "v_lshlrev_b64",
                               "v_lshl_add_u64", "v_alignbit_b32", "v_add3_u32", "v_cndmask_b32", "v_lshrrev_b64",
                               "v_cmp_gt_u64", "v_mov_b32", "v_perm_b32", "v_mul_u32_u24", "v_mad_u32_u24",
-                              "v_bitop3_b32", "v_xor_b32_e64", "v_add_u32_e32", "v_add_u32_e64", "xor_e32+xor_e64 (2 instr)"};
+                              "v_bitop3_b32", "v_xor_b32_e64", "v_add_u32_e32", "v_add_u32_e64", "xor_e32+xor_e64 (2 instr)",
+                              "v_fma_f32", "v_add_f32", "v_pk_fma_f32"};
 
 static unsigned long long *g_cyc;
 static double g_med_cycles;
@@ -79,28 +85,28 @@ int main() {
     (void)hipGetDeviceProperties(&p, 0);
     const int cus = p.multiProcessorCount;
     const int blocks = cus * 8;          // 8 blocks x 4 waves = 32 waves / CU = 8 per SIMD
-    const int iters = 20000;
+    const int iters = 2500;
     uint32_t *d;
     (void)hipMalloc(&d, (size_t)blocks * 256 * 4);
     (void)hipMalloc(&g_cyc, (size_t)blocks * 8);
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
-    float ms[20];
-    double cy[20];
+    float ms[23];
+    double cy[23];
 #define RUN(i) ms[i] = run<i>(d, blocks, iters, e0, e1); cy[i] = g_med_cycles;
     RUN(0) RUN(1) RUN(2) RUN(3) RUN(4) RUN(5) RUN(6) RUN(7)
     RUN(8) RUN(9) RUN(10) RUN(11) RUN(12) RUN(13) RUN(14) RUN(15)
-    RUN(16) RUN(17) RUN(18) RUN(19)
+    RUN(16) RUN(17) RUN(18) RUN(19) RUN(20) RUN(21) RUN(22)
     // wave-instructions per SIMD = waves per SIMD (8) * iters * CHAINS
-    const double winst = 8.0 * iters * CHAINS;
+    const double winst = 8.0 * iters * CHAINS * REPS;
     printf("{\"cus\": %d, \"clock_mhz\": %d, \"results\": [\n", cus, p.clockRate / 1000);
-    for (int i = 0; i < 20; i++) {
+    for (int i = 0; i < 23; i++) {
         const double ns_per = ms[i] * 1e6 / winst;
         // a block's 4 waves sit on 4 SIMDs; 8 blocks per CU -> 8 waves per SIMD run together
-        const double cyc_per = cy[i] / (8.0 * iters * CHAINS);
+        const double cyc_per = cy[i] / (8.0 * iters * CHAINS * REPS);
         printf("  {\"inst\": \"%s\", \"ms\": %.3f, \"ns_per_wave_inst_per_simd\": %.4f, \"cycles_per_wave_inst_per_simd\": %.3f, \"rel_to_xor\": %.2f}%s\n",
-               names[i], ms[i], ns_per, cyc_per, ms[i] / ms[0], i < 19 ? "," : "");
+               names[i], ms[i], ns_per, cyc_per, ms[i] / ms[0], i < 22 ? "," : "");
     }
     printf("]}\n");
     return 0;
