@@ -65,6 +65,10 @@ SIGNATURES = {
     "drephip_allpairs_merge_device": (C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp]),
     "drephip_distance_lut": (C.c_int, [C.c_int, C.c_uint32, f64p]),
     "drephip_set_allpairs_path": (C.c_int, [vp, C.c_int, C.c_uint32]),
+    "drephip_linkage": (C.c_int, [vp, f64p, C.c_uint32, C.c_int, f64p]),
+    "drephip_linkage_counts_device": (C.c_int, [vp, vp, vp, C.c_uint32, u32p, f64p, C.c_uint32,
+                                                np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS"),
+                                                C.c_int, f64p]),
     "drephip_set_timing": (C.c_int, [vp, C.c_int]),
     "drephip_last_kernel_ms": (C.c_int, [vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
 }
@@ -188,6 +192,35 @@ class Context:
 
     def set_allpairs_path(self, path: int, band_cap: int = 1024) -> None:
         check(lib().drephip_set_allpairs_path(self._h, path, band_cap), "drephip_set_allpairs_path")
+
+    # scipy linkage method codes (include/drephip.h DREPHIP_LINK_*)
+    LINK_METHODS = {"single": 0, "complete": 1, "average": 2, "weighted": 6}
+
+    def linkage(self, y: np.ndarray, method: str) -> np.ndarray:
+        """scipy.cluster.hierarchy.linkage(y, method) on the GPU, bit-identical
+        (y: condensed float64 distances)."""
+        y = np.ascontiguousarray(y, dtype=np.float64)
+        n = int(round((1 + (1 + 8 * len(y)) ** 0.5) / 2))
+        if n * (n - 1) // 2 != len(y):
+            raise ValueError("y is not a condensed distance vector")
+        Z = np.zeros((max(n - 1, 0), 4), dtype=np.float64)
+        if n >= 2:
+            check(lib().drephip_linkage(self._h, y, n, self.LINK_METHODS[method], Z.reshape(-1)),
+                  "drephip_linkage")
+        return Z
+
+    def linkage_counts_device(self, d_common: int, d_denom: Optional[int], n: int, perm: np.ndarray,
+                              lut: np.ndarray, lut_off: np.ndarray, method: str) -> np.ndarray:
+        """linkage() of the distances given by device-resident all-pairs counts
+        (see drephip_linkage_counts_device)."""
+        Z = np.zeros((max(n - 1, 0), 4), dtype=np.float64)
+        if n >= 2:
+            check(lib().drephip_linkage_counts_device(
+                self._h, d_common, d_denom, n, np.ascontiguousarray(perm, dtype=np.uint32),
+                np.ascontiguousarray(lut, dtype=np.float64), len(lut),
+                np.ascontiguousarray(lut_off, dtype=np.int32), self.LINK_METHODS[method], Z.reshape(-1)),
+                "drephip_linkage_counts_device")
+        return Z
 
     def set_timing(self, on: bool = True) -> None:
         check(lib().drephip_set_timing(self._h, 1 if on else 0), "drephip_set_timing")

@@ -12,6 +12,7 @@
 #include <cstring>
 #include <new>
 #include <thread>
+#include <vector>
 
 #define DREPHIP_EXPORT extern "C" __attribute__((visibility("default")))
 
@@ -433,5 +434,44 @@ DREPHIP_EXPORT int drephip_distance_lut(int k, uint32_t denom, double *lut) {
         }
         lut[c] = d;
     }
+    return DREPHIP_OK;
+}
+
+DREPHIP_EXPORT int drephip_linkage(drephip_ctx *ctx, const double *y, uint32_t n, int method, double *Z) {
+    GUARD_CTX(ctx);
+    if (n < 2) return DREPHIP_OK;
+    if (!y || !Z) { set_error("null argument"); return DREPHIP_ERR_ARG; }
+    if (n > 200000) { set_error("linkage supports n <= 200000 (n x n f64 matrix in HBM)"); return DREPHIP_ERR_UNSUPPORTED; }
+    timing_begin(ctx);
+    double *d_D;
+    int rc = dist_from_condensed_impl(ctx, y, n, &d_D, ctx->stream);
+    if (rc) return rc;
+    rc = linkage_device_impl(ctx, d_D, n, method, Z, ctx->stream);
+    if (rc) return rc;
+    timing_collect(ctx);
+    return DREPHIP_OK;
+}
+
+DREPHIP_EXPORT int drephip_linkage_counts_device(drephip_ctx *ctx, const uint16_t *d_common, const uint16_t *d_denom,
+                                                 uint32_t n, const uint32_t *perm, const double *lut,
+                                                 uint32_t lut_len, const int32_t *lut_off, int method, double *Z) {
+    GUARD_CTX(ctx);
+    if (n < 2) return DREPHIP_OK;
+    if (!d_common || !perm || !lut || !lut_off || !Z) { set_error("null argument"); return DREPHIP_ERR_ARG; }
+    if (n > 200000) { set_error("linkage supports n <= 200000 (n x n f64 matrix in HBM)"); return DREPHIP_ERR_UNSUPPORTED; }
+    for (uint32_t d = 0; d <= ctx->s; d++)
+        if (lut_off[d] >= 0 && (uint64_t)lut_off[d] + d + 1 > lut_len) { set_error("lut_off/lut_len mismatch"); return DREPHIP_ERR_ARG; }
+    std::vector<char> seen(n, 0);
+    for (uint32_t i = 0; i < n; i++) {
+        if (perm[i] >= n || seen[perm[i]]) { set_error("perm is not a permutation of 0..n-1"); return DREPHIP_ERR_ARG; }
+        seen[perm[i]] = 1;
+    }
+    timing_begin(ctx);
+    double *d_D;
+    int rc = dist_matrix_impl(ctx, d_common, d_denom, n, perm, lut, lut_len, lut_off, &d_D, ctx->stream);
+    if (rc) return rc;
+    rc = linkage_device_impl(ctx, d_D, n, method, Z, ctx->stream);
+    if (rc) return rc;
+    timing_collect(ctx);
     return DREPHIP_OK;
 }

@@ -70,6 +70,13 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
                          uint32_t N, uint32_t row0, uint32_t row1, uint16_t *d_common,
                          uint16_t *d_denom, hipStream_t st, bool force_merge);
 
+// Primary clustering (linkage.hip).
+int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, double *Z_out, hipStream_t st);
+int dist_matrix_impl(drephip_ctx *ctx, const uint16_t *d_common, const uint16_t *d_denom, uint32_t n,
+                     const uint32_t *perm, const double *lut, uint32_t lut_len, const int32_t *lut_off,
+                     double **d_D_out, hipStream_t st);
+int dist_from_condensed_impl(drephip_ctx *ctx, const double *y, uint32_t n, double **d_D_out, hipStream_t st);
+
 // Host ingest (ingest.cpp).
 struct Genome {
     std::vector<uint8_t> seq;        // concatenated record bytes (raw case)

@@ -1,0 +1,386 @@
+// linkage.hip -- primary clustering at scale: scipy.cluster.hierarchy.linkage
+// (the call dRep's cluster_hierarchical makes, drep/d_cluster.py:453, on the
+// distances built at 447) restated on the GPU, bit-identical to scipy:
+//   complete / average / weighted : scipy's nn_chain (nearest-neighbour chain
+//                                   with the previous chain element preferred
+//                                   on ties, Lance-Williams updates in f64);
+//   single                        : scipy's mst_single_linkage (Prim).
+// Then, on the host as scipy does: stable sort of the merges by distance and
+// the union-find relabel (scipy's `label`).
+//
+// The distance matrix lives in HBM as a full symmetric n x n f64 matrix (80 GB
+// at n = 10^5 -- one MI355X holds it), built on the device straight from the
+// all-pairs shared-hash counts through a per-(denominator, common) table of
+// the exact float64 values dRep feeds scipy; nothing n^2 crosses PCIe.  Each
+// step of the (inherently sequential) chain is one grid-wide argmin over a row
+// (contiguous reads) whose last workgroup makes the chain decision, and each
+// merge one grid-wide row + column update.  Steps are launched in batches
+// captured in a hipGraph; kernels after the last merge exit at once.
+// Roofline: HBM -- a search reads one 8n-byte row, an update reads two rows
+// and writes a row and a column (strided); launch latency dominates below
+// n ~ 3*10^4.
+
+#include "ctx.h"
+#include "../../include/drephip.h"
+
+#include <algorithm>
+#include <cmath>
+#include <numeric>
+#include <vector>
+
+namespace drephip {
+
+constexpr int kLkWG = 256;
+
+struct LinkState {
+    int32_t chain_len;
+    int32_t first_active;    // smallest index with size > 0 (non-decreasing)
+    int32_t k;               // merges done
+    int32_t pend;            // 1: the update kernel applies merge (px <- py)
+    int32_t px, py, pnx, pny;
+    double pd;
+    uint32_t ticket;         // last-workgroup detection of the search kernel
+    int32_t x;               // MST: current vertex
+};
+
+struct MinIdx { double v; int32_t i; };
+
+__device__ __forceinline__ bool better(double v, int32_t i, double bv, int32_t bi) {
+    return v < bv || (v == bv && i < bi);
+}
+
+// Lance-Williams updates exactly as scipy's _hierarchy_distance_update.pxi:
+// every operation rounded on its own, as in scipy's x86-64 build (this file is
+// compiled with -ffp-contract=off; see the Makefile)
+__device__ __forceinline__ double lw_update(int method, double dxi, double dyi, int32_t nx, int32_t ny) {
+    if (method == DREPHIP_LINK_COMPLETE) return fmax(dxi, dyi);
+    if (method == DREPHIP_LINK_WEIGHTED) return __dmul_rn(0.5, __dadd_rn(dxi, dyi));
+    // average: (size_x * d_xi + size_y * d_yi) / (size_x + size_y)
+    return __ddiv_rn(__dadd_rn(__dmul_rn((double)nx, dxi), __dmul_rn((double)ny, dyi)), (double)(nx + ny));
+}
+
+// Block argmin (smallest index among equal minima); result valid in thread 0.
+__device__ MinIdx block_argmin(double v, int32_t i) {
+    __shared__ double sv[kLkWG / 64];
+    __shared__ int32_t si[kLkWG / 64];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double ov = __shfl_xor(v, o, 64);
+        const int32_t oi = __shfl_xor(i, o, 64);
+        if (better(ov, oi, v, i)) { v = ov; i = oi; }
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { sv[w] = v; si[w] = i; }
+    __syncthreads();
+    MinIdx r{INFINITY, 0x7fffffff};
+    if (threadIdx.x == 0)
+        for (int k = 0; k < kLkWG / 64; k++)
+            if (better(sv[k], si[k], r.v, r.i)) { r.v = sv[k]; r.i = si[k]; }
+    return r;
+}
+
+// Last workgroup of a grid: every workgroup publishes its partial, then one
+// agent-scope acq_rel ticket; the workgroup that draws the last ticket reads
+// all partials (agent-scope loads).
+__device__ bool last_block(MinIdx part, MinIdx *parts, LinkState *st, MinIdx &out) {
+    __shared__ int is_last;
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(&parts[blockIdx.x].v, part.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&parts[blockIdx.x].i, part.i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t t = __hip_atomic_fetch_add(&st->ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        is_last = t == gridDim.x - 1;
+        if (is_last) {
+            MinIdx r{INFINITY, 0x7fffffff};
+            for (uint32_t b = 0; b < gridDim.x; b++) {
+                const double v = __hip_atomic_load(&parts[b].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const int32_t i = __hip_atomic_load(&parts[b].i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (better(v, i, r.v, r.i)) { r.v = v; r.i = i; }
+            }
+            out = r;
+            st->ticket = 0;
+        }
+    }
+    __syncthreads();
+    return is_last;
+}
+
+// ---------------------------------------------------------------- nn_chain
+__global__ __launch_bounds__(kLkWG) void k_nn_update(double *__restrict__ D, uint32_t n, int method,
+                                                    const int32_t *__restrict__ size, const LinkState *__restrict__ st) {
+    if (!st->pend) return;
+    const int32_t x = st->px, y = st->py, nx = st->pnx, ny = st->pny;
+    const double *Dx = D + (uint64_t)x * n;
+    double *Dy = D + (uint64_t)y * n;
+    for (uint32_t i = blockIdx.x * kLkWG + threadIdx.x; i < n; i += gridDim.x * kLkWG) {
+        if (size[i] == 0 || (int32_t)i == y) continue;
+        const double d = lw_update(method, Dx[i], Dy[i], nx, ny);
+        Dy[i] = d;
+        D[(uint64_t)i * n + y] = d;
+    }
+}
+
+__global__ __launch_bounds__(kLkWG) void k_nn_search(const double *__restrict__ D, uint32_t n,
+                                                    int32_t *__restrict__ size, int32_t *__restrict__ chain,
+                                                    LinkState *__restrict__ st, MinIdx *__restrict__ parts,
+                                                    double *__restrict__ Z) {
+    if (st->k >= (int32_t)n - 1) return;                       // all merged: the rest of the batch idles
+    const int32_t x = chain[st->chain_len - 1];
+    const double *Dx = D + (uint64_t)x * n;
+    double bv = INFINITY;
+    int32_t bi = 0x7fffffff;
+    for (uint32_t i = blockIdx.x * kLkWG + threadIdx.x; i < n; i += gridDim.x * kLkWG) {
+        if (size[i] == 0 || (int32_t)i == x) continue;
+        const double v = Dx[i];
+        if (v < bv) { bv = v; bi = (int32_t)i; }                // ascending i per thread: first minimum kept
+    }
+    const MinIdx part = block_argmin(bv, bi);
+    MinIdx g;
+    if (!last_block(part, parts, st, g)) return;
+    if (threadIdx.x != 0) return;
+    // chain decision (scipy nn_chain): the previous chain element wins ties
+    st->pend = 0;
+    const int32_t len = st->chain_len;
+    int32_t y = g.i;
+    double cur = g.v;
+    bool merge = false;
+    if (len > 1) {
+        const int32_t yp = chain[len - 2];
+        const double dp = Dx[yp];
+        if (!(g.v < dp)) { y = yp; cur = dp; merge = true; }
+    }
+    if (!merge) {
+        chain[len] = y;
+        st->chain_len = len + 1;
+        return;
+    }
+    int32_t a = x, b = y;
+    if (a > b) { const int32_t t = a; a = b; b = t; }
+    const int32_t na = size[a], nb = size[b];
+    const int32_t k = st->k;
+    Z[4 * k + 0] = a; Z[4 * k + 1] = b; Z[4 * k + 2] = cur; Z[4 * k + 3] = na + nb;
+    size[a] = 0;
+    size[b] = na + nb;
+    st->pend = 1; st->px = a; st->py = b; st->pnx = na; st->pny = nb; st->pd = cur;
+    st->k = k + 1;
+    st->chain_len = len - 2;
+    if (st->chain_len == 0 && k + 1 < (int32_t)n - 1) {
+        int32_t f = st->first_active;
+        while (size[f] == 0) f++;
+        st->first_active = f;
+        chain[0] = f;
+        st->chain_len = 1;
+    }
+}
+
+// ------------------------------------------------------------ MST (single)
+__global__ __launch_bounds__(kLkWG) void k_mst_step(const double *__restrict__ D, uint32_t n,
+                                                   int32_t *__restrict__ merged, double *__restrict__ Dmin,
+                                                   LinkState *__restrict__ st, MinIdx *__restrict__ parts,
+                                                   double *__restrict__ Z) {
+    if (st->k >= (int32_t)n - 1) return;
+    const int32_t x = st->x;
+    const double *Dx = D + (uint64_t)x * n;
+    double bv = INFINITY;
+    int32_t bi = 0x7fffffff;
+    for (uint32_t i = blockIdx.x * kLkWG + threadIdx.x; i < n; i += gridDim.x * kLkWG) {
+        if (merged[i]) continue;
+        const double d = Dx[i];
+        double m = Dmin[i];
+        if (m > d) { m = d; Dmin[i] = d; }
+        if (m < bv) { bv = m; bi = (int32_t)i; }
+    }
+    const MinIdx part = block_argmin(bv, bi);
+    MinIdx g;
+    if (!last_block(part, parts, st, g)) return;
+    if (threadIdx.x != 0) return;
+    const int32_t k = st->k;
+    Z[4 * k + 0] = x; Z[4 * k + 1] = g.i; Z[4 * k + 2] = g.v; Z[4 * k + 3] = 0;
+    merged[g.i] = 1;
+    st->x = g.i;
+    st->k = k + 1;
+}
+
+// ------------------------------------------------------------ matrix build
+// D[p(i)][p(j)] = D[p(j)][p(i)] = lut[off[denom] + common] for the condensed
+// pair (i, j) of the all-pairs output (denom = s when d_denom is null).
+__global__ __launch_bounds__(kLkWG) void k_dist_matrix(const uint16_t *__restrict__ common,
+                                                      const uint16_t *__restrict__ denom, uint32_t s, uint32_t n,
+                                                      const uint32_t *__restrict__ perm, const double *__restrict__ lut,
+                                                      const int32_t *__restrict__ off, double *__restrict__ D) {
+    const uint32_t i = blockIdx.x;
+    const uint64_t base = (uint64_t)i * n - (uint64_t)i * (i + 1) / 2;   // condensed index of (i, i+1), minus 1
+    const uint32_t pi = perm[i];
+    if (threadIdx.x == 0) D[(uint64_t)pi * n + pi] = 0.0;
+    for (uint32_t j = i + 1 + threadIdx.x; j < n; j += kLkWG) {
+        const uint64_t t = base + (j - i - 1);
+        const uint32_t dn = denom ? denom[t] : s;
+        const double v = lut[off[dn] + common[t]];
+        const uint32_t pj = perm[j];
+        D[(uint64_t)pi * n + pj] = v;
+        D[(uint64_t)pj * n + pi] = v;
+    }
+}
+
+__global__ __launch_bounds__(kLkWG) void k_dist_from_condensed(const double *__restrict__ y, uint32_t n,
+                                                              double *__restrict__ D) {
+    const uint32_t i = blockIdx.x;
+    const uint64_t base = (uint64_t)i * n - (uint64_t)i * (i + 1) / 2;
+    if (threadIdx.x == 0) D[(uint64_t)i * n + i] = 0.0;
+    for (uint32_t j = i + 1 + threadIdx.x; j < n; j += kLkWG) {
+        const double v = y[base + (j - i - 1)];
+        D[(uint64_t)i * n + j] = v;
+        D[(uint64_t)j * n + i] = v;
+    }
+}
+
+// ------------------------------------------------------------- host driver
+// scipy: Z sorted by distance (np.argsort kind='mergesort': stable), then
+// `label` (union-find over 2n-1 nodes; the smaller root first; sizes).
+static void sort_and_label(std::vector<double> &Z, uint32_t n) {
+    const uint32_t m = n - 1;
+    std::vector<uint32_t> order(m);
+    std::iota(order.begin(), order.end(), 0u);
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return Z[4 * a + 2] < Z[4 * b + 2]; });
+    std::vector<double> S(4ull * m);
+    for (uint32_t r = 0; r < m; r++)
+        for (int c = 0; c < 4; c++) S[4ull * r + c] = Z[4ull * order[r] + c];
+    std::vector<int64_t> parent(2ull * n - 1);
+    std::iota(parent.begin(), parent.end(), 0);
+    std::vector<int64_t> sz(2ull * n - 1, 1);
+    auto find = [&](int64_t x) {
+        int64_t p = x;
+        while (parent[p] != p) p = parent[p];
+        while (parent[x] != p) { const int64_t nx = parent[x]; parent[x] = p; x = nx; }
+        return p;
+    };
+    int64_t next = n;
+    for (uint32_t r = 0; r < m; r++) {
+        const int64_t xr = find((int64_t)S[4ull * r]), yr = find((int64_t)S[4ull * r + 1]);
+        S[4ull * r] = (double)std::min(xr, yr);
+        S[4ull * r + 1] = (double)std::max(xr, yr);
+        parent[xr] = next; parent[yr] = next;
+        sz[next] = sz[xr] + sz[yr];
+        S[4ull * r + 3] = (double)sz[next];
+        next++;
+    }
+    Z.swap(S);
+}
+
+int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, double *Z_out, hipStream_t st) {
+    if (n < 2) return DREPHIP_OK;
+    if (method != DREPHIP_LINK_SINGLE && method != DREPHIP_LINK_COMPLETE && method != DREPHIP_LINK_AVERAGE &&
+        method != DREPHIP_LINK_WEIGHTED) {
+        set_error("linkage method must be single, complete, average or weighted");
+        return DREPHIP_ERR_UNSUPPORTED;
+    }
+    const uint32_t grid = std::max(1u, std::min(1024u, (n + kLkWG * 4 - 1) / (kLkWG * 4)));
+    int32_t *d_size, *d_chain;
+    double *d_Z, *d_Dmin;
+    LinkState *d_st;
+    MinIdx *d_parts;
+    int rc;
+    if ((rc = scratch(ctx, "lk_size", n * 4ull, (void **)&d_size))) return rc;
+    if ((rc = scratch(ctx, "lk_chain", n * 4ull, (void **)&d_chain))) return rc;
+    if ((rc = scratch(ctx, "lk_Z", (n - 1) * 32ull, (void **)&d_Z))) return rc;
+    if ((rc = scratch(ctx, "lk_st", sizeof(LinkState), (void **)&d_st))) return rc;
+    if ((rc = scratch(ctx, "lk_parts", grid * sizeof(MinIdx), (void **)&d_parts))) return rc;
+    const bool mst = method == DREPHIP_LINK_SINGLE;
+    if (mst && (rc = scratch(ctx, "lk_dmin", n * 8ull, (void **)&d_Dmin))) return rc;
+
+    LinkState h{};
+    std::vector<int32_t> init(n, 1);
+    if (mst) {
+        std::vector<double> inf(n, INFINITY);
+        std::vector<int32_t> mg(n, 0);
+        mg[0] = 1;                                            // scipy: x = 0, merged[x] = 1
+        HIPC(hipMemcpyAsync(d_size, mg.data(), n * 4ull, hipMemcpyHostToDevice, st));
+        HIPC(hipMemcpyAsync(d_Dmin, inf.data(), n * 8ull, hipMemcpyHostToDevice, st));
+        h.x = 0;
+    } else {
+        HIPC(hipMemcpyAsync(d_size, init.data(), n * 4ull, hipMemcpyHostToDevice, st));
+        int32_t zero = 0;
+        HIPC(hipMemcpyAsync(d_chain, &zero, 4, hipMemcpyHostToDevice, st));
+        h.chain_len = 1;                                      // chain starts at the first active cluster, 0
+    }
+    HIPC(hipMemcpyAsync(d_st, &h, sizeof(h), hipMemcpyHostToDevice, st));
+
+    // batches of steps captured once in a graph, replayed until every merge is done
+    constexpr int kBatch = 256;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    HIPC(hipStreamSynchronize(st));
+    HIPC(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    for (int b = 0; b < kBatch; b++) {
+        if (mst) {
+            hipLaunchKernelGGL(k_mst_step, dim3(grid), dim3(kLkWG), 0, st, d_D, n, d_size, d_Dmin, d_st, d_parts, d_Z);
+        } else {
+            hipLaunchKernelGGL(k_nn_update, dim3(grid), dim3(kLkWG), 0, st, d_D, n, method, d_size, d_st);
+            hipLaunchKernelGGL(k_nn_search, dim3(grid), dim3(kLkWG), 0, st, d_D, n, d_size, d_chain, d_st, d_parts, d_Z);
+        }
+    }
+    HIPC(hipStreamEndCapture(st, &graph));
+    hipError_t e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    if (e != hipSuccess) { (void)hipGraphDestroy(graph); HIPC(e); }
+    // every search step either extends the chain or merges; the chain is at
+    // most n long, so 3n steps always suffice (the bound only guards a hang)
+    const uint64_t max_batches = (3ull * n) / kBatch + 2;
+    int32_t done = 0;
+    timing_mark(ctx, 2, st, true);
+    for (uint64_t it = 0; it < max_batches; it++) {
+        e = hipGraphLaunch(exec, st);
+        if (e != hipSuccess) break;
+        if ((it & 3) == 3 || it + 1 == max_batches) {
+            e = hipMemcpyAsync(&done, &d_st->k, 4, hipMemcpyDeviceToHost, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess || done >= (int32_t)n - 1) break;
+        }
+    }
+    timing_mark(ctx, 2, st, false);
+    (void)hipGraphExecDestroy(exec);
+    (void)hipGraphDestroy(graph);
+    HIPC(e);
+    HIPC(hipMemcpyAsync(&done, &d_st->k, 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    if (done != (int32_t)n - 1) { set_error("linkage did not finish"); return DREPHIP_ERR_INTERNAL; }
+    std::vector<double> Z(4ull * (n - 1));
+    HIPC(hipMemcpy(Z.data(), d_Z, Z.size() * 8, hipMemcpyDeviceToHost));
+    sort_and_label(Z, n);
+    std::copy(Z.begin(), Z.end(), Z_out);
+    return DREPHIP_OK;
+}
+
+int dist_matrix_impl(drephip_ctx *ctx, const uint16_t *d_common, const uint16_t *d_denom, uint32_t n,
+                     const uint32_t *perm, const double *lut, uint32_t lut_len, const int32_t *lut_off,
+                     double **d_D_out, hipStream_t st) {
+    const uint32_t s = ctx->s;
+    double *d_D, *d_lut;
+    uint32_t *d_perm;
+    int32_t *d_off;
+    int rc;
+    if ((rc = scratch(ctx, "lk_D", (uint64_t)n * n * 8, (void **)&d_D))) return rc;
+    if ((rc = scratch(ctx, "lk_perm", n * 4ull, (void **)&d_perm))) return rc;
+    if ((rc = scratch(ctx, "lk_lut", lut_len * 8ull, (void **)&d_lut))) return rc;
+    if ((rc = scratch(ctx, "lk_off", (s + 1) * 4ull, (void **)&d_off))) return rc;
+    HIPC(hipMemcpyAsync(d_perm, perm, n * 4ull, hipMemcpyHostToDevice, st));
+    HIPC(hipMemcpyAsync(d_lut, lut, lut_len * 8ull, hipMemcpyHostToDevice, st));
+    HIPC(hipMemcpyAsync(d_off, lut_off, (s + 1) * 4ull, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_dist_matrix, dim3(n), dim3(kLkWG), 0, st, d_common, d_denom, s, n, d_perm, d_lut, d_off, d_D);
+    HIPC(hipGetLastError());
+    *d_D_out = d_D;
+    return DREPHIP_OK;
+}
+
+int dist_from_condensed_impl(drephip_ctx *ctx, const double *y, uint32_t n, double **d_D_out, hipStream_t st) {
+    double *d_D, *d_y;
+    int rc;
+    const uint64_t np = (uint64_t)n * (n - 1) / 2;
+    if ((rc = scratch(ctx, "lk_D", (uint64_t)n * n * 8, (void **)&d_D))) return rc;
+    if ((rc = scratch(ctx, "lk_y", np * 8, (void **)&d_y))) return rc;
+    HIPC(hipMemcpyAsync(d_y, y, np * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_dist_from_condensed, dim3(n), dim3(kLkWG), 0, st, d_y, n, d_D);
+    HIPC(hipGetLastError());
+    *d_D_out = d_D;
+    return DREPHIP_OK;
+}
+
+}  // namespace drephip

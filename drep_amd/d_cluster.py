@@ -20,7 +20,8 @@ Beyond the reference (needed at 10^4-10^5 genomes, where an N^2-row Mdb does
 not fit): :func:`all_vs_all_MASH_condensed` returns the condensed
 ``common``/``denom`` vectors and :func:`mdb_from_condensed` /
 :func:`cluster_mash_condensed` build the Mdb / primary clusters from them with
-the same float32 arithmetic the reference applies.
+the same float32 arithmetic the reference applies; with ``gpu=`` the linkage
+itself (scipy's algorithm, bit-identical Z) runs on the GPU.
 """
 from __future__ import annotations
 
@@ -405,30 +406,82 @@ def cluster_mash_database(db, **kwargs):
     return Cdb, [linkage, linkage_db, arguments]
 
 
-def condensed_cluster_distances(cm: CondensedMash) -> np.ndarray:
-    """float64 condensed distances bit-identical to what the reference feeds
-    scipy: dist32 -> 1 - (1 - dist32) in float32 (d_cluster.py:584, 619) ->
-    float64.  Rows/columns in sorted-name order (the pivot's order)."""
-    N = len(cm.names)
-    d32 = mash_distance_float32(cm.common, cm.denom)
+def _linkage_values(common: np.ndarray, denom: np.ndarray) -> np.ndarray:
+    """float64 linkage input for (common, denom) pairs, bit-identical to what
+    the reference feeds scipy: dist32 (the %g / read_csv path) -> 1 - (1 -
+    dist32) in float32 (d_cluster.py:584, 619) -> float64."""
+    d32 = mash_distance_float32(common, denom)
     one = np.float32(1)
-    after = (one - (one - d32)).astype(np.float32)
+    return (one - (one - d32)).astype(np.float32).astype(np.float64)
+
+
+def condensed_cluster_distances(cm: CondensedMash) -> np.ndarray:
+    """float64 condensed linkage input, rows/columns in sorted-name order (the
+    pivot's order)."""
+    N = len(cm.names)
+    after = _linkage_values(cm.common, cm.denom)
     order = np.argsort(np.array(cm.names, dtype=object), kind='stable')
     if np.all(order == np.arange(N)):
-        return after.astype(np.float64)
-    M = _square(after, N, np.zeros(N, dtype=np.float32))
+        return after
+    M = _square(after, N, np.zeros(N, dtype=np.float64))
     M = M[np.ix_(order, order)]
     return ssd.squareform(M, checks=False).astype(np.float64)
 
 
+def linkage_tables(denominators: np.ndarray, s: int):
+    """(lut, lut_off) for drephip_linkage_counts_device: for every denominator
+    d that occurs, lut[lut_off[d] + c] = linkage input value of (c, d)."""
+    lut_off = np.full(s + 1, -1, dtype=np.int32)
+    parts, pos = [], 0
+    for d in np.unique(np.asarray(denominators)):
+        d = int(d)
+        c = np.arange(d + 1)
+        parts.append(_linkage_values(c, np.full(d + 1, d)))
+        lut_off[d] = pos
+        pos += d + 1
+    lut = np.concatenate(parts) if parts else np.zeros(1)
+    return lut, lut_off
+
+
+def linkage_order(names: Sequence[str]) -> np.ndarray:
+    """perm[i] = row of genome i in the linkage input (sorted names, as the
+    reference's pivot orders them)."""
+    order = np.argsort(np.array(names, dtype=object), kind='stable')
+    perm = np.empty(len(names), dtype=np.uint32)
+    perm[order] = np.arange(len(names), dtype=np.uint32)
+    return perm
+
+
+GPU_LINKAGE_METHODS = ('single', 'complete', 'average', 'weighted')
+
+
 def cluster_mash_condensed(cm: CondensedMash, **kwargs):
     """Primary clustering straight from the condensed result (no N^2 Mdb):
-    same linkage input as cluster_mash_database builds via pivot+squareform."""
+    same linkage input as cluster_mash_database builds via pivot+squareform.
+
+    gpu=<device> runs the linkage itself on the GPU (libdrephip
+    drephip_linkage_counts_device: scipy's nn_chain / MST restated, Z
+    bit-identical; the n x n matrix is built in HBM from the counts); other
+    methods, or gpu=None, use scipy on the host."""
     P_Lmethod = kwargs.get('clusterAlg', 'single')
     P_Lcutoff = 1 - kwargs.get('P_ani', .9)
-    arr = condensed_cluster_distances(cm)
+    gpu = kwargs.get('gpu', None)
     names = sorted(cm.names)
-    linkage = scipy.cluster.hierarchy.linkage(arr, method=P_Lmethod)
+    N = len(cm.names)
+    if gpu is not None and P_Lmethod in GPU_LINKAGE_METHODS and N >= 2:
+        import torch
+        dev = torch.device('cuda', int(gpu))
+        lut, lut_off = linkage_tables(cm.denom, cm.s)
+        d_c = torch.from_numpy(np.ascontiguousarray(cm.common, dtype=np.uint16).view(np.int16)).to(dev)
+        full = bool((cm.denom == cm.s).all())
+        d_d = None if full else torch.from_numpy(np.ascontiguousarray(cm.denom, dtype=np.uint16).view(np.int16)).to(dev)
+        torch.cuda.synchronize(dev)
+        with _lib.Context(device=int(gpu), k=MASH_K, s=cm.s, seed=MASH_SEED) as ctx:
+            linkage = ctx.linkage_counts_device(d_c.data_ptr(), None if d_d is None else d_d.data_ptr(), N,
+                                                linkage_order(cm.names), lut, lut_off, P_Lmethod)
+    else:
+        arr = condensed_cluster_distances(cm)
+        linkage = scipy.cluster.hierarchy.linkage(arr, method=P_Lmethod)
     fclust = scipy.cluster.hierarchy.fcluster(linkage, P_Lcutoff, criterion='distance')
     Cdb = _gen_cdb_from_fclust(fclust, names).rename(columns={'cluster': 'primary_cluster'})
     arguments = {'linkage_method': P_Lmethod, 'linkage_cutoff': P_Lcutoff,

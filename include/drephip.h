@@ -171,6 +171,28 @@ int drephip_distance_lut(int k, uint32_t denom, double *lut /* denom+1 */);
 #define DREPHIP_AP_MERGE 3
 int drephip_set_allpairs_path(drephip_ctx *ctx, int path, uint32_t band_cap);
 
+/* ---------------------------------------------------------- primary clustering
+ * Replaces: scipy.cluster.hierarchy.linkage(squareform(dist), method) in
+ * cluster_hierarchical (drep/d_cluster.py:447-453), called from
+ * cluster_mash_database (598-630) -- the O(n^2) step of primary clustering.
+ * Result: the (n-1) x 4 linkage matrix Z, bit-identical to scipy's (its
+ * nn_chain for complete/average/weighted, mst_single_linkage for single,
+ * then its stable sort and relabel).  Method codes are scipy's. */
+#define DREPHIP_LINK_SINGLE 0
+#define DREPHIP_LINK_COMPLETE 1
+#define DREPHIP_LINK_AVERAGE 2
+#define DREPHIP_LINK_WEIGHTED 6
+/* From a host condensed distance vector y (n(n-1)/2 doubles, scipy order). */
+int drephip_linkage(drephip_ctx *ctx, const double *y, uint32_t n, int method, double *Z /* (n-1)*4 */);
+/* From the device-resident all-pairs output of drephip_allpairs_device (rows
+ * 0..n-1 in one segment): distance of pair (i, j) = lut[lut_off[denom] +
+ * common] (denom = s when d_denom is NULL; lut_off has s+1 entries, -1 for a
+ * denominator that does not occur), placed at row/column perm[i], perm[j] of
+ * the linkage input.  Blocking. */
+int drephip_linkage_counts_device(drephip_ctx *ctx, const uint16_t *d_common, const uint16_t *d_denom,
+                                  uint32_t n, const uint32_t *perm, const double *lut, uint32_t lut_len,
+                                  const int32_t *lut_off, int method, double *Z /* (n-1)*4 */);
+
 /* Enable (1) / disable (0) HIP-event timing of every kernel launch. */
 int drephip_set_timing(drephip_ctx *ctx, int enable);
 

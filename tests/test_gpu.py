@@ -426,3 +426,47 @@ def test_sketch_layout_cache_follows_layout_changes(ctx1000):
     for order in ([0, 1, 2], [2, 0, 1], [2, 0, 1], [0, 1, 2]):
         h, nh = run(order)
         assert np.array_equal(h, oh[order]) and np.array_equal(nh, onh[order]), order
+
+
+# ------------------------------------------------------ primary clustering
+@pytest.mark.parametrize("method", ["single", "complete", "average", "weighted"])
+@pytest.mark.parametrize("n,kind", [(2, "ties"), (3, "ties"), (17, "ties"), (257, "ties"), (300, "cont"),
+                                    (64, "equal")])
+def test_gpu_linkage_matches_scipy(method, n, kind):
+    """drephip_linkage == scipy.cluster.hierarchy.linkage bit for bit, with
+    Mash-like ties (a few distinct distances, many 1.0), continuous values and
+    all-equal distances."""
+    import scipy.cluster.hierarchy as sch
+    rng = np.random.default_rng(n * 31 + len(method))
+    m = n * (n - 1) // 2
+    if kind == "ties":
+        vals = np.array([0.0, 0.00243596, 0.0157245, 0.0157245, 0.05, 0.1, 0.243761, 1.0, 1.0, 1.0])
+        y = vals[rng.integers(0, len(vals), m)]
+    elif kind == "cont":
+        y = rng.random(m)
+    else:
+        y = np.full(m, 0.5)
+    with _lib.Context(0, 21, S, 42) as ctx:
+        Z = ctx.linkage(y, method)
+    Zs = sch.linkage(y, method=method)
+    assert Z.shape == Zs.shape
+    assert np.array_equal(Z, Zs), np.argwhere(Z != Zs)[:5]
+
+
+@pytest.mark.parametrize("method", ["average", "single"])
+def test_cluster_mash_condensed_gpu_equals_reference_path(family, ctx1000, method):
+    """Primary clustering from device-resident all-pairs counts (GPU linkage)
+    gives the reference path's linkage matrix and Cdb (scipy on the float32
+    Mdb distances), with names in a shuffled order."""
+    from drep_amd.d_cluster import CondensedMash, cluster_mash_condensed
+    h, nh = family
+    N = len(nh)
+    c, d = ctx1000.allpairs(h, nh)
+    rng = np.random.default_rng(5)
+    names = ["g%04d.fna" % i for i in rng.permutation(N)]
+    cm = CondensedMash(names, names, c, d, nh, np.full(N, 400_000, np.uint64), S)
+    cdb_cpu, (z_cpu, _, _) = cluster_mash_condensed(cm, clusterAlg=method, P_ani=0.95)
+    cdb_gpu, (z_gpu, _, _) = cluster_mash_condensed(cm, clusterAlg=method, P_ani=0.95, gpu=0)
+    assert np.array_equal(z_gpu, z_cpu)
+    assert cdb_gpu.equals(cdb_cpu)
+    assert cdb_gpu['primary_cluster'].nunique() > 1
