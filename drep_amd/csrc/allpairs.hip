@@ -273,21 +273,26 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
         }
         if (!actmask) continue;                                       // column at or left of the tile's rows
         Slots<R> sn = read_slots<R, FAST>((uint32_t)rg[0], T, H, hm, o1, o2);
-        bool alive = true;
-        // runtime loop over groups of kRing chunks; ring slots are static
-        for (uint32_t kb = 0; kb < nch && alive; kb += kRing) {
+        // runtime loop over groups of kRing chunks; ring slots are static.  The
+        // scan-end test runs once per group, on the group's first chunk (a
+        // chunk past every row's largest hash cannot hit, so finishing the
+        // group is only wasted work, never a wrong count)
+        for (uint32_t kb = 0; kb < nch; kb += kRing) {
+            {
+                const uint64_t b = rg[0];
+                // smallest element of the group (lane 0; readfirstlane returns
+                // int: through uint32_t so the low word is not sign-extended)
+                const uint64_t b0 = ((uint64_t)rfl((uint32_t)(b >> 32)) << 32) | rfl((uint32_t)b);
+                if (b0 == kEmpty || b0 > amax) break;
+            }
 #pragma unroll
             for (int u = 0; u < kRing; u++) {
                 const uint32_t k = kb + u;
-                if (!alive || k >= nch) continue;                        // wave-uniform
+                if (k >= nch) continue;                                   // wave-uniform
                 const uint64_t b = rg[u];
                 const Slots<R> sl = sn;
                 if (k + kRing < nch) rg[u] = ld(Bc, k + kRing);          // refill the ring
                 sn = read_slots<R, FAST>((uint32_t)rg[(u + 1) % kRing], T, H, hm, o1, o2);
-                // smallest element of the chunk (lane 0; readfirstlane returns
-                // int: through uint32_t so the low word is not sign-extended)
-                const uint64_t b0 = ((uint64_t)rfl((uint32_t)(b >> 32)) << 32) | rfl((uint32_t)b);
-                if (b0 == kEmpty || b0 > amax) { alive = false; continue; }
                 probe_rows<R, FAST>(sl, b, k * 64 + lane, V, s, hm, o1, o2, actmask, ~0ull, zero, nA, s, mrun, cnt);
             }
         }

@@ -779,6 +779,18 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
                 hipLaunchKernelGGL((k_sketch_hash21_v5<kLaneBases, 8>), dim3(nt), dim3(kTile / kLaneBases), 0, st,
                                    d_codes, d_valid, tb_tiles_b, tb_tiles_g, d_thr, d_sets, d_cnt, plan.set_log2,
                                    limit, ctx->seed, wlast);
+            else if (ctx->sketch_kernel == 6)      // A/B: 4 k-mers per admit test
+                hipLaunchKernelGGL((k_sketch_hash21_v5<kLaneBases, 4>), dim3(nt), dim3(kTile / kLaneBases), 0, st,
+                                   d_codes, d_valid, tb_tiles_b, tb_tiles_g, d_thr, d_sets, d_cnt, plan.set_log2,
+                                   limit, ctx->seed, wlast);
+            else if (ctx->sketch_kernel == 7)      // A/B: 64 window ends per lane, 512-lane workgroups
+                hipLaunchKernelGGL((k_sketch_hash21_v5<kLaneBases / 2, 8>), dim3(nt), dim3(kTile / (kLaneBases / 2)), 0,
+                                   st, d_codes, d_valid, tb_tiles_b, tb_tiles_g, d_thr, d_sets, d_cnt, plan.set_log2,
+                                   limit, ctx->seed, wlast);
+            else if (ctx->sketch_kernel == 8)      // A/B: 256 window ends per lane, 128-lane workgroups
+                hipLaunchKernelGGL((k_sketch_hash21_v5<kLaneBases * 2, 8>), dim3(nt), dim3(kTile / (kLaneBases * 2)), 0,
+                                   st, d_codes, d_valid, tb_tiles_b, tb_tiles_g, d_thr, d_sets, d_cnt, plan.set_log2,
+                                   limit, ctx->seed, wlast);
             else if (ctx->sketch_kernel != 3)
                 hipLaunchKernelGGL((k_sketch_hash21_v4<kLaneBases, 8>), dim3(nt), dim3(kTile / kLaneBases), 0, st,
                                    d_codes, d_valid, tb_tiles_b, tb_tiles_g, d_thr, d_sets, d_cnt, plan.set_log2,
