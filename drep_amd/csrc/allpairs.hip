@@ -195,10 +195,12 @@ __device__ __forceinline__ void probe_rows(const Slots<R> &sl, uint64_t b, uint3
 #pragma unroll
     for (int r = 0; r < R; r++) {
         if (!((actmask >> r) & 1u)) continue;                        // wave-uniform
-        const bool c1 = (sl.e1[r] ^ (FAST ? blo : rotr32(blo, o1[r]))) <= hm;
-        const bool c2 = (sl.e2[r] ^ (FAST ? b16 : rotr32(blo, o2[r]))) <= hm;
-        uint64_t m = (__builtin_amdgcn_ballot_w64(c1) | __builtin_amdgcn_ballot_w64(c2)) & lanemask;
+        const uint32_t x1 = sl.e1[r] ^ (FAST ? blo : rotr32(blo, o1[r]));
+        const uint32_t x2 = sl.e2[r] ^ (FAST ? b16 : rotr32(blo, o2[r]));
+        // one compare, one mask: a hit in either slot <=> min(x1, x2) <= hm
+        uint64_t m = __builtin_amdgcn_ballot_w64(min(x1, x2) <= hm) & lanemask;
         if (m == 0) continue;                                        // wave-uniform: no hit in this row
+        const bool c1 = x1 <= hm, c2 = x2 <= hm;
         uint32_t f = (c1 ? sl.e1[r] : sl.e2[r]) & hm;
         bool ok = f < ilim[r] && V[r * vs + (f < ilim[r] ? f : 0)] == bhi;
         const bool retry = c1 && c2 && !ok;                          // two keys share this low word
