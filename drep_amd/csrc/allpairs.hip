@@ -720,10 +720,13 @@ static std::vector<uint2> make_items(uint32_t row0, uint32_t row1, uint32_t N, u
 static int launch_merge(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N,
                         uint64_t seg0, uint64_t npairs, uint16_t *d_common, uint16_t *d_denom,
                         hipStream_t st) {
-    const uint64_t blocks = (npairs + 255) / 256;
+    const uint64_t per = max_blocks(256) * 256;      // pairs per dispatch
     timing_mark(ctx, 2, st, true);
-    hipLaunchKernelGGL(k_allpairs_merge, dim3((uint32_t)blocks), dim3(256), 0, st, d_hashes, d_nhash,
-                       ctx->s, N, seg0, npairs, d_common, d_denom);
+    for (uint64_t p0 = 0; p0 < npairs; p0 += per) {
+        const uint64_t np = std::min(per, npairs - p0);
+        hipLaunchKernelGGL(k_allpairs_merge, dim3((uint32_t)((np + 255) / 256)), dim3(256), 0, st, d_hashes, d_nhash,
+                           ctx->s, N, seg0 + p0, np, d_common + p0, d_denom ? d_denom + p0 : nullptr);
+    }
     timing_mark(ctx, 2, st, false);
     HIPC(hipGetLastError());
     HIPC(hipStreamSynchronize(st));
@@ -753,8 +756,10 @@ static int launch_band(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_
     const size_t lds = band_lds_bytes(R);         // <= 80 KiB: two workgroups per CU
     HIPC(hipFuncSetAttribute((const void *)k_allpairs_band<R, 1024, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     timing_mark(ctx, 2, st, true);
-    hipLaunchKernelGGL((k_allpairs_band<R, 1024, 8>), dim3((uint32_t)items.size()), dim3(1024), lds, st, d_hashes,
-                       d_nhash, ctx->s, N, row1, cap, d_items, d_common, d_denom, seg0, d_nfail, d_prof);
+    for (size_t i0 = 0; i0 < items.size(); i0 += max_blocks(1024))
+        hipLaunchKernelGGL((k_allpairs_band<R, 1024, 8>), dim3((uint32_t)std::min<size_t>(items.size() - i0, max_blocks(1024))),
+                           dim3(1024), lds, st, d_hashes, d_nhash, ctx->s, N, row1, cap, d_items + i0, d_common,
+                           d_denom, seg0, d_nfail, d_prof);
     timing_mark(ctx, 2, st, false);
     HIPC(hipGetLastError());
     uint32_t nfail = 0;
@@ -778,8 +783,9 @@ static int launch_q(drephip_ctx *ctx, uint32_t nitems, size_t lds, hipStream_t s
     HIPC(hipFuncSetAttribute((const void *)k_allpairs_q<R, NCH, MINW>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)lds));
     timing_mark(ctx, 2, st, true);
-    hipLaunchKernelGGL((k_allpairs_q<R, NCH, MINW>), dim3(nitems), dim3(kApWG), lds, st, h, nh, tabs, fam, ctx->s,
-                       N, row0, row1, B, items, cm, dn, seg0);
+    for (uint32_t i0 = 0; i0 < nitems; i0 += (uint32_t)max_blocks(kApWG))
+        hipLaunchKernelGGL((k_allpairs_q<R, NCH, MINW>), dim3(std::min<uint32_t>(nitems - i0, (uint32_t)max_blocks(kApWG))),
+                           dim3(kApWG), lds, st, h, nh, tabs, fam, ctx->s, N, row0, row1, B, items + i0, cm, dn, seg0);
     timing_mark(ctx, 2, st, false);
     HIPC(hipGetLastError());
     return DREPHIP_OK;

@@ -24,6 +24,14 @@ constexpr uint32_t kMaxSketch = 12000;        // finalize sorts <= 16384 candida
 
 inline uint64_t round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }
 
+// One dispatch covers fewer than 2^32 work-items (the AQL grid size is a
+// 32-bit work-item count; a larger grid is silently truncated), so every
+// launch whose grid scales with N is issued in pieces of at most
+// kMaxLaunchItems work-items.  A multiple of 8 workgroups per piece keeps the
+// XCD-interleaved item order of the all-pairs kernels intact.
+constexpr uint64_t kMaxLaunchItems = 1ull << 31;
+inline uint64_t max_blocks(uint32_t wg) { return kMaxLaunchItems / wg / 8 * 8; }
+
 // padded footprint of a genome whose records (incl. the 1-base separators)
 // span `span` bases: at least one invalid base after it, rounded to a tile.
 inline uint64_t padded_span(uint64_t span) { return round_up(span + 1, kTile); }

@@ -625,8 +625,8 @@ __global__ void k_reset_sets(unsigned long long *__restrict__ sets, uint32_t *__
 // One thread per 32-base word pair (two code words + one validity word).
 __global__ void k_synth(uint64_t seed, uint32_t g0, uint32_t n, uint32_t fam, uint64_t L,
                         uint64_t P, uint32_t *__restrict__ codes, uint32_t *__restrict__ valid,
-                        uint64_t nwords32) {
-    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                        uint64_t nwords32, uint64_t w0) {
+    const uint64_t w = w0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= nwords32) return;
     const uint64_t p0 = w * 32;
     uint32_t c_lo = 0, c_hi = 0, v = 0;
@@ -775,30 +775,35 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
         }
         if (nt > 0) {
             timing_mark(ctx, 0, st, true);
-            if (ctx->sketch_kernel == 5)
-                hipLaunchKernelGGL((k_sketch_hash21_v5<kLaneBases, 8>), dim3(nt), dim3(kTile / kLaneBases), 0, st,
-                                   d_codes, d_valid, tb_tiles_b, tb_tiles_g, d_thr, d_sets, d_cnt, plan.set_log2,
-                                   limit, ctx->seed, wlast);
-            else if (ctx->sketch_kernel == 6)      // A/B: 4 k-mers per admit test
-                hipLaunchKernelGGL((k_sketch_hash21_v5<kLaneBases, 4>), dim3(nt), dim3(kTile / kLaneBases), 0, st,
-                                   d_codes, d_valid, tb_tiles_b, tb_tiles_g, d_thr, d_sets, d_cnt, plan.set_log2,
-                                   limit, ctx->seed, wlast);
-            else if (ctx->sketch_kernel == 7)      // A/B: 64 window ends per lane, 512-lane workgroups
-                hipLaunchKernelGGL((k_sketch_hash21_v5<kLaneBases / 2, 8>), dim3(nt), dim3(kTile / (kLaneBases / 2)), 0,
-                                   st, d_codes, d_valid, tb_tiles_b, tb_tiles_g, d_thr, d_sets, d_cnt, plan.set_log2,
-                                   limit, ctx->seed, wlast);
-            else if (ctx->sketch_kernel == 8)      // A/B: 256 window ends per lane, 128-lane workgroups
-                hipLaunchKernelGGL((k_sketch_hash21_v5<kLaneBases * 2, 8>), dim3(nt), dim3(kTile / (kLaneBases * 2)), 0,
-                                   st, d_codes, d_valid, tb_tiles_b, tb_tiles_g, d_thr, d_sets, d_cnt, plan.set_log2,
-                                   limit, ctx->seed, wlast);
-            else if (ctx->sketch_kernel != 3)
-                hipLaunchKernelGGL((k_sketch_hash21_v4<kLaneBases, 8>), dim3(nt), dim3(kTile / kLaneBases), 0, st,
-                                   d_codes, d_valid, tb_tiles_b, tb_tiles_g, d_thr, d_sets, d_cnt, plan.set_log2,
-                                   limit, ctx->seed, wlast);
-            else
-                hipLaunchKernelGGL((k_sketch_hash21_v3<kLaneBases, 8>), dim3(nt), dim3(kTile / kLaneBases), 0, st,
-                                   d_codes, d_valid, tb_tiles_b, tb_tiles_g, d_thr, d_sets, d_cnt, plan.set_log2,
-                                   limit, ctx->seed);
+            for (uint32_t t0 = 0; t0 < nt; t0 += (uint32_t)max_blocks(kTile / (kLaneBases / 2))) {
+                const uint32_t ntc = std::min<uint32_t>(nt - t0, (uint32_t)max_blocks(kTile / (kLaneBases / 2)));
+                const uint64_t *tbb = tb_tiles_b + t0;
+                const uint32_t *tbg = tb_tiles_g + t0;
+                if (ctx->sketch_kernel == 5)
+                    hipLaunchKernelGGL((k_sketch_hash21_v5<kLaneBases, 8>), dim3(ntc), dim3(kTile / kLaneBases), 0, st,
+                                       d_codes, d_valid, tbb, tbg, d_thr, d_sets, d_cnt, plan.set_log2, limit,
+                                       ctx->seed, wlast);
+                else if (ctx->sketch_kernel == 6)      // A/B: 4 k-mers per admit test
+                    hipLaunchKernelGGL((k_sketch_hash21_v5<kLaneBases, 4>), dim3(ntc), dim3(kTile / kLaneBases), 0, st,
+                                       d_codes, d_valid, tbb, tbg, d_thr, d_sets, d_cnt, plan.set_log2, limit,
+                                       ctx->seed, wlast);
+                else if (ctx->sketch_kernel == 7)      // A/B: 64 window ends per lane, 512-lane workgroups
+                    hipLaunchKernelGGL((k_sketch_hash21_v5<kLaneBases / 2, 8>), dim3(ntc),
+                                       dim3(kTile / (kLaneBases / 2)), 0, st, d_codes, d_valid, tbb, tbg, d_thr,
+                                       d_sets, d_cnt, plan.set_log2, limit, ctx->seed, wlast);
+                else if (ctx->sketch_kernel == 8)      // A/B: 256 window ends per lane, 128-lane workgroups
+                    hipLaunchKernelGGL((k_sketch_hash21_v5<kLaneBases * 2, 8>), dim3(ntc),
+                                       dim3(kTile / (kLaneBases * 2)), 0, st, d_codes, d_valid, tbb, tbg, d_thr,
+                                       d_sets, d_cnt, plan.set_log2, limit, ctx->seed, wlast);
+                else if (ctx->sketch_kernel != 3)
+                    hipLaunchKernelGGL((k_sketch_hash21_v4<kLaneBases, 8>), dim3(ntc), dim3(kTile / kLaneBases), 0, st,
+                                       d_codes, d_valid, tbb, tbg, d_thr, d_sets, d_cnt, plan.set_log2, limit,
+                                       ctx->seed, wlast);
+                else
+                    hipLaunchKernelGGL((k_sketch_hash21_v3<kLaneBases, 8>), dim3(ntc), dim3(kTile / kLaneBases), 0, st,
+                                       d_codes, d_valid, tbb, tbg, d_thr, d_sets, d_cnt, plan.set_log2, limit,
+                                       ctx->seed);
+            }
             timing_mark(ctx, 0, st, false);
         }
         timing_mark(ctx, 1, st, true);
@@ -852,9 +857,10 @@ int synth_device_impl(drephip_ctx *ctx, uint64_t seed, uint32_t g0, uint32_t n, 
     const uint64_t P = padded_span(L);
     const uint64_t total = kTile + (uint64_t)n * P;
     const uint64_t nw32 = total / 32;
-    const uint32_t blocks = (uint32_t)((nw32 + 255) / 256);
-    hipLaunchKernelGGL(k_synth, dim3(blocks), dim3(256), 0, st, seed, g0, n, family_size, L, P, d_codes,
-                       d_valid, nw32);
+    const uint64_t blocks = (nw32 + 255) / 256;
+    for (uint64_t b0 = 0; b0 < blocks; b0 += max_blocks(256))
+        hipLaunchKernelGGL(k_synth, dim3((uint32_t)std::min<uint64_t>(blocks - b0, max_blocks(256))), dim3(256), 0, st,
+                           seed, g0, n, family_size, L, P, d_codes, d_valid, nw32, b0 * 256);
     HIPC(hipGetLastError());
     HIPC(hipStreamSynchronize(st));
     return DREPHIP_OK;
