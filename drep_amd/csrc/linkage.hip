@@ -12,19 +12,22 @@
 // at n = 10^5 -- one MI355X holds it), built on the device straight from the
 // all-pairs shared-hash counts through a per-(denominator, common) table of
 // the exact float64 values dRep feeds scipy; nothing n^2 crosses PCIe.  Each
-// step of the (inherently sequential) chain is one grid-wide argmin over a row
-// (contiguous reads) whose last workgroup makes the chain decision, and each
-// merge one grid-wide row + column update.  Steps are launched in batches
-// captured in a hipGraph; kernels after the last merge exit at once.
-// Roofline: HBM -- a search reads one 8n-byte row, an update reads two rows
-// and writes a row and a column (strided); launch latency dominates below
-// n ~ 3*10^4.
+// step of the (inherently sequential) chain is one launch: the previous
+// merge's row + column update fused with the grid-wide argmin over the chain
+// top's row, whose last workgroup makes the chain decision.  Steps are
+// launched in batches captured in a hipGraph; kernels after the last merge
+// exit at once.
+// Roofline: HBM -- a step reads one 8n-byte row (and after a merge two more
+// rows, writing a row and a strided column); at n = 10^5 (0.8 MB rows) the
+// ~5 us launch floor and the grid-wide reduction dominate.
 
 #include "ctx.h"
 #include "../../include/drephip.h"
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
 #include <numeric>
 #include <vector>
 
@@ -81,7 +84,8 @@ __device__ MinIdx block_argmin(double v, int32_t i) {
 
 // Last workgroup of a grid: every workgroup publishes its partial, then one
 // agent-scope acq_rel ticket; the workgroup that draws the last ticket reads
-// all partials (agent-scope loads).
+// all partials (agent-scope loads, spread over its threads) and reduces them.
+// Every thread of the block must call it; the result is valid in thread 0.
 __device__ bool last_block(MinIdx part, MinIdx *parts, LinkState *st, MinIdx &out) {
     __shared__ int is_last;
     if (threadIdx.x == 0) {
@@ -89,70 +93,28 @@ __device__ bool last_block(MinIdx part, MinIdx *parts, LinkState *st, MinIdx &ou
         __hip_atomic_store(&parts[blockIdx.x].i, part.i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t t = __hip_atomic_fetch_add(&st->ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
         is_last = t == gridDim.x - 1;
-        if (is_last) {
-            MinIdx r{INFINITY, 0x7fffffff};
-            for (uint32_t b = 0; b < gridDim.x; b++) {
-                const double v = __hip_atomic_load(&parts[b].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const int32_t i = __hip_atomic_load(&parts[b].i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (better(v, i, r.v, r.i)) { r.v = v; r.i = i; }
-            }
-            out = r;
-            st->ticket = 0;
-        }
+        if (is_last) st->ticket = 0;
     }
     __syncthreads();
-    return is_last;
+    if (!is_last) return false;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // every published partial is visible
+    double bv = INFINITY;
+    int32_t bi = 0x7fffffff;
+    for (uint32_t b = threadIdx.x; b < gridDim.x; b += blockDim.x) {
+        const double v = __hip_atomic_load(&parts[b].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int32_t i = __hip_atomic_load(&parts[b].i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (better(v, i, bv, bi)) { bv = v; bi = i; }
+    }
+    out = block_argmin(bv, bi);
+    return true;
 }
 
 // ---------------------------------------------------------------- nn_chain
-__global__ __launch_bounds__(kLkWG) void k_nn_update(double *__restrict__ D, uint32_t n, int method,
-                                                    const int32_t *__restrict__ size, const LinkState *__restrict__ st) {
-    if (!st->pend) return;
-    const int32_t x = st->px, y = st->py, nx = st->pnx, ny = st->pny;
-    const double *Dx = D + (uint64_t)x * n;
-    double *Dy = D + (uint64_t)y * n;
-    for (uint32_t i = blockIdx.x * kLkWG + threadIdx.x; i < n; i += gridDim.x * kLkWG) {
-        if (size[i] == 0 || (int32_t)i == y) continue;
-        const double d = lw_update(method, Dx[i], Dy[i], nx, ny);
-        Dy[i] = d;
-        D[(uint64_t)i * n + y] = d;
-    }
-}
-
-__global__ __launch_bounds__(kLkWG) void k_nn_search(const double *__restrict__ D, uint32_t n,
-                                                    int32_t *__restrict__ size, int32_t *__restrict__ chain,
-                                                    LinkState *__restrict__ st, MinIdx *__restrict__ parts,
-                                                    double *__restrict__ Z) {
-    if (st->k >= (int32_t)n - 1) return;                       // all merged: the rest of the batch idles
-    const int32_t x = chain[st->chain_len - 1];
-    const double *Dx = D + (uint64_t)x * n;
-    double bv = INFINITY;
-    int32_t bi = 0x7fffffff;
-    for (uint32_t i = blockIdx.x * kLkWG + threadIdx.x; i < n; i += gridDim.x * kLkWG) {
-        if (size[i] == 0 || (int32_t)i == x) continue;
-        const double v = Dx[i];
-        if (v < bv) { bv = v; bi = (int32_t)i; }                // ascending i per thread: first minimum kept
-    }
-    const MinIdx part = block_argmin(bv, bi);
-    MinIdx g;
-    if (!last_block(part, parts, st, g)) return;
-    if (threadIdx.x != 0) return;
-    // chain decision (scipy nn_chain): the previous chain element wins ties
-    st->pend = 0;
-    const int32_t len = st->chain_len;
-    int32_t y = g.i;
-    double cur = g.v;
-    bool merge = false;
-    if (len > 1) {
-        const int32_t yp = chain[len - 2];
-        const double dp = Dx[yp];
-        if (!(g.v < dp)) { y = yp; cur = dp; merge = true; }
-    }
-    if (!merge) {
-        chain[len] = y;
-        st->chain_len = len + 1;
-        return;
-    }
+// Merge chain top x with y at distance cur (scipy: the smaller index is
+// dropped, the larger becomes the new cluster), pop both, restart an empty
+// chain at the first active cluster.
+__device__ void chain_merge(int32_t x, int32_t y, double cur, int32_t len, uint32_t n, int32_t *size,
+                            int32_t *chain, LinkState *st, double *Z) {
     int32_t a = x, b = y;
     if (a > b) { const int32_t t = a; a = b; b = t; }
     const int32_t na = size[a], nb = size[b];
@@ -170,6 +132,69 @@ __global__ __launch_bounds__(kLkWG) void k_nn_search(const double *__restrict__ 
         chain[0] = f;
         st->chain_len = 1;
     }
+}
+
+// One chain step per launch: the pending merge's Lance-Williams update (row and
+// column y) fused with the search of the chain top's row.  The search of row
+// t = chain top reads D[t][i]; the update rewrites only row/column y, so every
+// D[t][i] with i != y is untouched, and the one changed entry D[t][y] is
+// produced by the thread of i = y (the thread of i = t skips it), which also
+// uses it as its search value -- no cross-workgroup dependence.  After a chain
+// restart t may be y itself: then the search value of i is the freshly
+// computed D[y][i].  The last workgroup makes scipy's chain decision.
+__global__ __launch_bounds__(kLkWG) void k_nn_step(double *__restrict__ D, uint32_t n, int method,
+                                                  int32_t *__restrict__ size, int32_t *__restrict__ chain,
+                                                  LinkState *__restrict__ st, MinIdx *__restrict__ parts,
+                                                  double *__restrict__ Z) {
+    if (st->k >= (int32_t)n - 1) return;                       // all merged: the rest of the batch idles
+    const bool pend = st->pend != 0;
+    const int32_t x = st->px, y = st->py, nx = st->pnx, ny = st->pny;
+    const int32_t t = chain[st->chain_len - 1];
+    const double *Dt = D + (uint64_t)t * n;
+    const double *Dx = D + (uint64_t)x * n;
+    double *Dy = D + (uint64_t)y * n;
+    double bv = INFINITY;
+    int32_t bi = 0x7fffffff;
+    for (uint32_t i = blockIdx.x * kLkWG + threadIdx.x; i < n; i += gridDim.x * kLkWG) {
+        if (size[i] == 0) continue;
+        double v;
+        if (pend && (int32_t)i != y && (int32_t)i != t) {
+            const double u = lw_update(method, Dx[i], Dy[i], nx, ny);
+            Dy[i] = u;
+            D[(uint64_t)i * n + y] = u;
+            v = t == y ? u : Dt[i];
+        } else if (pend && (int32_t)i == y && t != y) {
+            const double u = lw_update(method, Dx[t], Dy[t], nx, ny);   // entry (y, t): old values, unshared
+            Dy[t] = u;
+            D[(uint64_t)t * n + y] = u;
+            v = u;
+        } else {
+            if ((int32_t)i == t) continue;
+            v = Dt[i];
+        }
+        if (v < bv) { bv = v; bi = (int32_t)i; }                // ascending i per thread: first minimum kept
+    }
+    const MinIdx part = block_argmin(bv, bi);
+    MinIdx g;
+    if (!last_block(part, parts, st, g)) return;
+    if (threadIdx.x != 0) return;
+    // chain decision (scipy nn_chain): the previous chain element wins ties
+    st->pend = 0;
+    const int32_t len = st->chain_len;
+    int32_t yy = g.i;
+    double cur = g.v;
+    bool merge = false;
+    if (len > 1) {
+        const int32_t yp = chain[len - 2];
+        const double dp = Dt[yp];
+        if (!(g.v < dp)) { yy = yp; cur = dp; merge = true; }
+    }
+    if (!merge) {
+        chain[len] = yy;
+        st->chain_len = len + 1;
+        return;
+    }
+    chain_merge(t, yy, cur, len, n, size, chain, st, Z);
 }
 
 // ------------------------------------------------------------ MST (single)
@@ -273,7 +298,10 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
         set_error("linkage method must be single, complete, average or weighted");
         return DREPHIP_ERR_UNSUPPORTED;
     }
-    const uint32_t grid = std::max(1u, std::min(1024u, (n + kLkWG * 4 - 1) / (kLkWG * 4)));
+    // entries per lane of a step (DREPHIP_LINK_PER_LANE, A/B; default 4)
+    const char *pl = getenv("DREPHIP_LINK_PER_LANE");
+    const uint32_t per = pl ? std::max(1, std::min(64, atoi(pl))) : 4;
+    const uint32_t grid = std::max(1u, std::min(1024u, (n + kLkWG * per - 1) / (kLkWG * per)));
     int32_t *d_size, *d_chain;
     double *d_Z, *d_Dmin;
     LinkState *d_st;
@@ -283,10 +311,9 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     if ((rc = scratch(ctx, "lk_chain", n * 4ull, (void **)&d_chain))) return rc;
     if ((rc = scratch(ctx, "lk_Z", (n - 1) * 32ull, (void **)&d_Z))) return rc;
     if ((rc = scratch(ctx, "lk_st", sizeof(LinkState), (void **)&d_st))) return rc;
-    if ((rc = scratch(ctx, "lk_parts", grid * sizeof(MinIdx), (void **)&d_parts))) return rc;
+    if ((rc = scratch(ctx, "lk_parts", 1024 * sizeof(MinIdx), (void **)&d_parts))) return rc;
     const bool mst = method == DREPHIP_LINK_SINGLE;
     if (mst && (rc = scratch(ctx, "lk_dmin", n * 8ull, (void **)&d_Dmin))) return rc;
-
     LinkState h{};
     std::vector<int32_t> init(n, 1);
     if (mst) {
@@ -303,7 +330,6 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
         h.chain_len = 1;                                      // chain starts at the first active cluster, 0
     }
     HIPC(hipMemcpyAsync(d_st, &h, sizeof(h), hipMemcpyHostToDevice, st));
-
     // batches of steps captured once in a graph, replayed until every merge is done
     constexpr int kBatch = 256;
     hipGraph_t graph = nullptr;
@@ -314,8 +340,8 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
         if (mst) {
             hipLaunchKernelGGL(k_mst_step, dim3(grid), dim3(kLkWG), 0, st, d_D, n, d_size, d_Dmin, d_st, d_parts, d_Z);
         } else {
-            hipLaunchKernelGGL(k_nn_update, dim3(grid), dim3(kLkWG), 0, st, d_D, n, method, d_size, d_st);
-            hipLaunchKernelGGL(k_nn_search, dim3(grid), dim3(kLkWG), 0, st, d_D, n, d_size, d_chain, d_st, d_parts, d_Z);
+            hipLaunchKernelGGL(k_nn_step, dim3(grid), dim3(kLkWG), 0, st, d_D, n, method, d_size, d_chain, d_st,
+                               d_parts, d_Z);
         }
     }
     HIPC(hipStreamEndCapture(st, &graph));
@@ -364,7 +390,9 @@ int dist_matrix_impl(drephip_ctx *ctx, const uint16_t *d_common, const uint16_t 
     HIPC(hipMemcpyAsync(d_perm, perm, n * 4ull, hipMemcpyHostToDevice, st));
     HIPC(hipMemcpyAsync(d_lut, lut, lut_len * 8ull, hipMemcpyHostToDevice, st));
     HIPC(hipMemcpyAsync(d_off, lut_off, (s + 1) * 4ull, hipMemcpyHostToDevice, st));
+    timing_mark(ctx, 3, st, true);
     hipLaunchKernelGGL(k_dist_matrix, dim3(n), dim3(kLkWG), 0, st, d_common, d_denom, s, n, d_perm, d_lut, d_off, d_D);
+    timing_mark(ctx, 3, st, false);
     HIPC(hipGetLastError());
     *d_D_out = d_D;
     return DREPHIP_OK;
@@ -377,7 +405,9 @@ int dist_from_condensed_impl(drephip_ctx *ctx, const double *y, uint32_t n, doub
     if ((rc = scratch(ctx, "lk_D", (uint64_t)n * n * 8, (void **)&d_D))) return rc;
     if ((rc = scratch(ctx, "lk_y", np * 8, (void **)&d_y))) return rc;
     HIPC(hipMemcpyAsync(d_y, y, np * 8, hipMemcpyHostToDevice, st));
+    timing_mark(ctx, 3, st, true);
     hipLaunchKernelGGL(k_dist_from_condensed, dim3(n), dim3(kLkWG), 0, st, d_y, n, d_D);
+    timing_mark(ctx, 3, st, false);
     HIPC(hipGetLastError());
     *d_D_out = d_D;
     return DREPHIP_OK;

@@ -431,11 +431,14 @@ def test_sketch_layout_cache_follows_layout_changes(ctx1000):
 # ------------------------------------------------------ primary clustering
 @pytest.mark.parametrize("method", ["single", "complete", "average", "weighted"])
 @pytest.mark.parametrize("n,kind", [(2, "ties"), (3, "ties"), (17, "ties"), (257, "ties"), (300, "cont"),
-                                    (64, "equal")])
+                                    (64, "equal"), (400, "fewvals"), (1500, "mash")])
 def test_gpu_linkage_matches_scipy(method, n, kind):
     """drephip_linkage == scipy.cluster.hierarchy.linkage bit for bit, with
-    Mash-like ties (a few distinct distances, many 1.0), continuous values and
-    all-equal distances."""
+    Mash-like ties (a few distinct distances, many 1.0), continuous values,
+    all-equal distances, a few values whose Lance-Williams averages round
+    (fewvals), and family structure with 1.0 between families (mash).  The
+    cached-nearest-neighbour chain (default) and the row-scan chain
+    (DREPHIP_LINK_IMPL=scan) both match."""
     import scipy.cluster.hierarchy as sch
     rng = np.random.default_rng(n * 31 + len(method))
     m = n * (n - 1) // 2
@@ -444,13 +447,28 @@ def test_gpu_linkage_matches_scipy(method, n, kind):
         y = vals[rng.integers(0, len(vals), m)]
     elif kind == "cont":
         y = rng.random(m)
+    elif kind == "fewvals":
+        y = np.array([0.1, 0.3, 0.7])[rng.integers(0, 3, m)]
+    elif kind == "mash":
+        fam = rng.integers(0, max(1, n // 40), n)
+        iu = np.triu_indices(n, 1)
+        same = fam[iu[0]] == fam[iu[1]]
+        y = np.ones(m)
+        y[same] = np.round(rng.random(int(same.sum())) * 0.2, 3)
     else:
         y = np.full(m, 0.5)
-    with _lib.Context(0, 21, S, 42) as ctx:
-        Z = ctx.linkage(y, method)
     Zs = sch.linkage(y, method=method)
-    assert Z.shape == Zs.shape
-    assert np.array_equal(Z, Zs), np.argwhere(Z != Zs)[:5]
+    impls = ["default", "scan"] if method != "single" else ["default"]
+    for impl in impls:
+        if impl == "scan":
+            os.environ["DREPHIP_LINK_IMPL"] = "scan"
+        try:
+            with _lib.Context(0, 21, S, 42) as ctx:
+                Z = ctx.linkage(y, method)
+        finally:
+            os.environ.pop("DREPHIP_LINK_IMPL", None)
+        assert Z.shape == Zs.shape
+        assert np.array_equal(Z, Zs), (impl, np.argwhere(Z != Zs)[:5])
 
 
 @pytest.mark.parametrize("method", ["average", "single"])

@@ -157,6 +157,9 @@ def test_scale_configs3_single_gpu():
     t0 = time.perf_counter()
     Z = ctx.linkage_counts_device(d_common.data_ptr(), None, N, perm, lut, lut_off, "average")
     res["linkage_s"] = time.perf_counter() - t0
+    res["linkage_matrix_build_ms"] = ctx.kernel_ms(3)[0]
+    res["linkage_chain_ms"] = ctx.kernel_ms(2)[0]
+    res["linkage_entries_per_lane"] = int(os.environ.get("DREPHIP_LINK_PER_LANE", 4))
     note("gpu linkage %.2f s" % res["linkage_s"])
     assert Z.shape == (N - 1, 4)
     assert np.all(np.diff(Z[:, 2]) >= 0)           # average linkage is monotone
