@@ -436,9 +436,8 @@ def test_gpu_linkage_matches_scipy(method, n, kind):
     """drephip_linkage == scipy.cluster.hierarchy.linkage bit for bit, with
     Mash-like ties (a few distinct distances, many 1.0), continuous values,
     all-equal distances, a few values whose Lance-Williams averages round
-    (fewvals), and family structure with 1.0 between families (mash).  The
-    cached-nearest-neighbour chain (default) and the row-scan chain
-    (DREPHIP_LINK_IMPL=scan) both match."""
+    (fewvals), and family structure with 1.0 between families (mash), at two
+    grid densities of the chain-step kernel."""
     import scipy.cluster.hierarchy as sch
     rng = np.random.default_rng(n * 31 + len(method))
     m = n * (n - 1) // 2
@@ -458,17 +457,15 @@ def test_gpu_linkage_matches_scipy(method, n, kind):
     else:
         y = np.full(m, 0.5)
     Zs = sch.linkage(y, method=method)
-    impls = ["default", "scan"] if method != "single" else ["default"]
-    for impl in impls:
-        if impl == "scan":
-            os.environ["DREPHIP_LINK_IMPL"] = "scan"
+    for per_lane in ("4", "1"):                      # grid densities of the chain-step kernel
+        os.environ["DREPHIP_LINK_PER_LANE"] = per_lane
         try:
             with _lib.Context(0, 21, S, 42) as ctx:
                 Z = ctx.linkage(y, method)
         finally:
-            os.environ.pop("DREPHIP_LINK_IMPL", None)
+            os.environ.pop("DREPHIP_LINK_PER_LANE", None)
         assert Z.shape == Zs.shape
-        assert np.array_equal(Z, Zs), (impl, np.argwhere(Z != Zs)[:5])
+        assert np.array_equal(Z, Zs), (per_lane, np.argwhere(Z != Zs)[:5])
 
 
 @pytest.mark.parametrize("method", ["average", "single"])
