@@ -237,11 +237,11 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
                                            uint16_t *__restrict__ denom, uint64_t seg0) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nch = (s + 63) / 64;
-    auto ld = [&](const uint64_t *Bc, int k) -> uint64_t {     // clamped load + select: no branch
-        const uint32_t j = k * 64 + lane;
-        const uint64_t v = Bc[j < s ? j : s - 1];
-        return j < s ? v : kEmpty;
-    };
+    // clamped raw load: no select, so the ring refill never waits on its own
+    // load; lanes past s in the last chunk are masked where the chunk is used
+    auto ld = [&](const uint64_t *Bc, int k) -> uint64_t { return Bc[min(k * 64 + lane, s - 1)]; };
+    const uint32_t tail = s - (nch - 1) * 64;                        // valid lanes of the last chunk
+    const uint64_t tailmask = tail >= 64 ? ~0ull : (1ull << tail) - 1;
     uint64_t rg[kRing], nx[kRing];
     uint32_t zero[R];
 #pragma unroll
@@ -260,8 +260,6 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
 #pragma unroll
             for (int k = 0; k < kRing; k++) nx[k] = ld(hashes + (uint64_t)cn * s, k);
         }
-        const uint32_t nB = nhash[c];
-        const bool partial = any_partial_row || nB < s;
         uint32_t cnt[R], mrun[R], actmask = 0;
         // elements past every active row's largest hash cannot match: the
         // scan ends at the first chunk whose smallest element is past them
@@ -274,7 +272,10 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
             if (act) amax = alast[r] > amax ? alast[r] : amax;
         }
         if (!actmask) continue;                                       // column at or left of the tile's rows
-        Slots<R> sn = read_slots<R, FAST>((uint32_t)rg[0], T, H, hm, o1, o2);
+        // slot words of chunk k live in sb[k & 1] (kRing is even): read one
+        // chunk ahead into the other half, no register copies
+        Slots<R> sb[2];
+        sb[0] = read_slots<R, FAST>((uint32_t)rg[0], T, H, hm, o1, o2);
         // runtime loop over groups of kRing chunks; ring slots are static.  The
         // scan-end test runs once per group, on the group's first chunk (a
         // chunk past every row's largest hash cannot hit, so finishing the
@@ -292,13 +293,22 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
                 const uint32_t k = kb + u;
                 if (k >= nch) continue;                                   // wave-uniform
                 const uint64_t b = rg[u];
-                const Slots<R> sl = sn;
-                if (k + kRing < nch) rg[u] = ld(Bc, k + kRing);          // refill the ring
-                sn = read_slots<R, FAST>((uint32_t)rg[(u + 1) % kRing], T, H, hm, o1, o2);
-                probe_rows<R, FAST>(sl, b, k * 64 + lane, V, s, hm, o1, o2, actmask, ~0ull, zero, nA, s, mrun, cnt);
+                // lanes past s in the last chunk hold clamped copies: masked out
+                const uint64_t lm = k == nch - 1 ? tailmask : ~0ull;
+                // refill the ring unconditionally (past the end: the last chunk
+                // again): a conditional element update would make the register
+                // tuple a phi whose merge waits on the load
+                rg[u] = ld(Bc, min(k + kRing, nch - 1));
+                sb[(u + 1) & 1] = read_slots<R, FAST>((uint32_t)rg[(u + 1) % kRing], T, H, hm, o1, o2);
+                probe_rows<R, FAST>(sb[u & 1], b, k * 64 + lane, V, s, hm, o1, o2, actmask, lm, zero, nA, s,
+                                    mrun, cnt);
             }
         }
         if (lane == 0) {
+            // the column's count is read only here: a scalar load left in flight
+            // across the chunk loop would force every LDS wait there to lgkmcnt(0)
+            const uint32_t nB = nhash[c];
+            const bool partial = any_partial_row || nB < s;
 #pragma unroll
             for (int r = 0; r < R; r++) {
                 if (!((actmask >> r) & 1u)) continue;

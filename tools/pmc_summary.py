@@ -5,6 +5,7 @@ import csv
 import json
 import sys
 
+N_CU, N_SIMD = 256, 1024          # MI355X
 
 def main():
     key, files = sys.argv[1], sys.argv[2:]
@@ -29,6 +30,21 @@ def main():
         out.setdefault("derived", {})["lds_bank_conflict_frac"] = c.get("SQ_LDS_BANK_CONFLICT", 0) / c["SQ_LDS_IDX_ACTIVE"]
     if c.get("SQ_WAVES"):
         out.setdefault("derived", {})["valu_insts_per_wave"] = c.get("SQ_INSTS_VALU", 0) / c["SQ_WAVES"]
+    # GRBM_GUI_ACTIVE rides along in every pass and rocprofv3 sums it over the 8
+    # XCDs: kernel cycles = sum / passes / 8.  A wave64 VALU instruction holds a
+    # SIMD for 4 cycles (SQ_ACTIVE_INST_VALU counts 1 per instruction here);
+    # SQ_LDS_IDX_ACTIVE counts LDS-array cycles per CU.
+    npass = len(disp.get("GRBM_GUI_ACTIVE", ())) or 1
+    npass = max(1, sum(1 for f in files if any(key in r["Kernel_Name"] and r["Counter_Name"] == "GRBM_GUI_ACTIVE"
+                                               for r in csv.DictReader(open(f)))))
+    if c.get("GRBM_GUI_ACTIVE"):
+        cyc = c["GRBM_GUI_ACTIVE"] / npass / 8
+        d = out.setdefault("derived", {})
+        d["kernel_cycles"] = cyc
+        if c.get("SQ_ACTIVE_INST_VALU"):
+            d["valu_busy_frac"] = c["SQ_ACTIVE_INST_VALU"] * 4 / (N_SIMD * cyc)
+        if c.get("SQ_LDS_IDX_ACTIVE"):
+            d["lds_busy_frac"] = c["SQ_LDS_IDX_ACTIVE"] / (N_CU * cyc)
     print(json.dumps(out, indent=1))
 
 
