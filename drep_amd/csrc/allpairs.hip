@@ -448,34 +448,38 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
     }
     return v;
 }
-// Column element j (kEmpty past nB): an unconditional load clamped to the
-// row (no branch around it), then a select.
-__device__ __forceinline__ uint64_t ld_col(const uint64_t *__restrict__ Bc, uint32_t j, uint32_t nB, uint32_t s) {
-    const uint64_t v = Bc[j < s ? j : s - 1];
-    return j < nB ? v : kEmpty;
+// Column element j: an unconditional load clamped to the row, no select (a
+// select would wait on the load right where it is issued).  Elements past nB
+// are kEmpty in the sketch matrix and fail every band test (b < hi <= the
+// rows' largest element + 1); lanes past s hold clamped copies and are masked
+// by tail_mask.
+__device__ __forceinline__ uint64_t ld_col(const uint64_t *__restrict__ Bc, uint32_t j, uint32_t s) {
+    return Bc[j < s ? j : s - 1];
+}
+__device__ __forceinline__ uint64_t tail_mask(uint32_t j0, uint32_t s) {     // lanes with j0 + lane < s
+    return j0 + 64 <= s ? ~0ull : j0 >= s ? 0ull : (1ull << (s - j0)) - 1;
 }
 
 // The column phase of one band: wave w takes columns w, w+NW, ... of the
 // item.  A column's band segment streams through a ring of kRing chunks in
 // registers, loaded kRing chunks ahead (the next column's first kRing chunks
-// when a column starts); slot words are read one chunk ahead of the tests.
+// when a column starts); slot words are read one chunk ahead of the tests
+// into the other half of a two-entry buffer.
 template <int R, uint32_t NW, bool FAST>
-__device__ __forceinline__ void band_columns(const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ nhash,
-                                             uint32_t s, const uint32_t *T, const uint32_t *V, uint32_t *cur,
-                                             uint16_t *pcnt, uint16_t *pm, uint32_t c0, uint32_t ncols, uint32_t i0,
-                                             uint32_t nrows, uint32_t wave, uint64_t hi, uint32_t fam,
-                                             const uint32_t (&pr)[R]) {
+__device__ __forceinline__ void band_columns(const uint64_t *__restrict__ hashes, uint32_t s, const uint32_t *T,
+                                             const uint32_t *V, uint32_t *cur, uint16_t *pcnt, uint16_t *pm,
+                                             uint32_t c0, uint32_t ncols, uint32_t i0, uint32_t nrows, uint32_t wave,
+                                             uint64_t hi, uint32_t fam, const uint32_t (&pr)[R]) {
     constexpr uint32_t H = 1u << kBandB, hm = H - 1;
     const uint32_t lane = threadIdx.x & 63;
     uint32_t ci = wave;
     uint64_t nx[kRing];
-    uint32_t nq = 0, nnB = 0;
+    uint32_t nq = 0;
     auto load_first = [&](uint32_t cc) {
         nq = rfl(cur[cc]);
-        nnB = nhash[c0 + cc];
         const uint64_t *Bn = hashes + (uint64_t)(c0 + cc) * s;
 #pragma unroll
-        for (int k = 0; k < kRing; k++) nx[k] = ld_col(Bn, nq + 64 * k + lane, nnB, s);
+        for (int k = 0; k < kRing; k++) nx[k] = ld_col(Bn, nq + 64 * k + lane, s);
     };
     if (ci < ncols) load_first(ci);
     uint32_t o1[R], o2[R], cap_r[R];
@@ -484,7 +488,7 @@ __device__ __forceinline__ void band_columns(const uint64_t *__restrict__ hashes
     for (int r = 0; r < R; r++) { o1[r] = qf.o1; o2[r] = qf.o2; cap_r[r] = kBandCapMax; }
     for (; ci < ncols; ci += NW) {
         const uint32_t c = c0 + ci;
-        const uint32_t q0 = nq, nB = nnB;
+        const uint32_t q0 = nq;
         uint64_t rg[kRing];
 #pragma unroll
         for (int k = 0; k < kRing; k++) rg[k] = nx[k];
@@ -499,18 +503,18 @@ __device__ __forceinline__ void band_columns(const uint64_t *__restrict__ hashes
         const uint64_t *Bc = hashes + (uint64_t)c * s;
         uint32_t q = q0;
         bool more = true;
-        Slots<R> sn = read_slots<R, FAST>((uint32_t)rg[0], T, H, hm, o1, o2);
+        Slots<R> sb[2];
+        sb[0] = read_slots<R, FAST>((uint32_t)rg[0], T, H, hm, o1, o2);
         for (uint32_t kb = 0; more; kb += kRing) {
 #pragma unroll
             for (int u = 0; u < kRing; u++) {
                 if (!more) continue;                                  // wave-uniform
                 const uint64_t b = rg[u];
-                const Slots<R> sl = sn;
-                rg[u] = ld_col(Bc, q0 + 64 * (kb + u + kRing) + lane, nB, s);   // refill the ring
-                const uint32_t bn = (uint32_t)rg[(u + 1) % kRing];
-                const uint64_t inb = __builtin_amdgcn_ballot_w64(b < hi);
-                sn = read_slots<R, FAST>(bn, T, H, hm, o1, o2);
-                probe_rows<R, FAST>(sl, b, q + lane, V, kBandCapMax, hm, o1, o2, actmask, inb, pr, cap_r,
+                const uint32_t j0 = q0 + 64 * (kb + u);
+                rg[u] = ld_col(Bc, j0 + 64 * kRing + lane, s);       // refill the ring
+                const uint64_t inb = __builtin_amdgcn_ballot_w64(b < hi) & tail_mask(j0, s);
+                sb[(u + 1) & 1] = read_slots<R, FAST>((uint32_t)rg[(u + 1) % kRing], T, H, hm, o1, o2);
+                probe_rows<R, FAST>(sb[u & 1], b, q + lane, V, kBandCapMax, hm, o1, o2, actmask, inb, pr, cap_r,
                                     s, mrun, cnt);
                 const uint32_t nin = (uint32_t)__popcll(inb);
                 q += nin;
@@ -645,9 +649,9 @@ __global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
         uint64_t t_c0 = prof ? wall_clock64() : 0;
         // ---- columns: wave w takes columns w, w+NW, ...
         if (fam == 0)
-            band_columns<R, NW, true>(hashes, nhash, s, T, V, cur, pcnt, pm, c0, ncols, i0, nrows, wave, hi, fam, pr);
+            band_columns<R, NW, true>(hashes, s, T, V, cur, pcnt, pm, c0, ncols, i0, nrows, wave, hi, fam, pr);
         else
-            band_columns<R, NW, false>(hashes, nhash, s, T, V, cur, pcnt, pm, c0, ncols, i0, nrows, wave, hi, fam, pr);
+            band_columns<R, NW, false>(hashes, s, T, V, cur, pcnt, pm, c0, ncols, i0, nrows, wave, hi, fam, pr);
         __syncthreads();
         if (tid < (uint32_t)R) s_p[tid] += s_q[tid];
         if (prof && tid == 0) {

@@ -399,6 +399,12 @@ DREPHIP_EXPORT int drephip_allpairs(drephip_ctx *ctx, const uint64_t *hashes, co
     GUARD_CTX(ctx);
     if (N < 2) return DREPHIP_OK;
     if (!hashes || !nhash || !common_out) { set_error("null argument"); return DREPHIP_ERR_ARG; }
+    for (uint32_t i = 0; i < N; i++) {                    // the kernels read rows past nhash: must be padding
+        if (nhash[i] > ctx->s) { set_error("nhash[i] > s"); return DREPHIP_ERR_ARG; }
+        const uint64_t *row = hashes + (uint64_t)i * ctx->s;
+        for (uint32_t j = nhash[i]; j < ctx->s; j++)
+            if (row[j] != ~0ull) { set_error("sketch rows must be UINT64_MAX past nhash[i]"); return DREPHIP_ERR_ARG; }
+    }
     const uint64_t npairs = (uint64_t)N * (N - 1) / 2;
     hipStream_t st = ctx->stream;
     uint64_t *d_h;

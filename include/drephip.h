@@ -134,7 +134,10 @@ int drephip_synth_device(drephip_ctx *ctx, uint64_t seed, uint32_t g0, uint32_t 
  * Replaces: `mash dist -p P ALL.msh ALL.msh > MASH_table.tsv`
  * (drep/d_cluster.py:569-573) for the integer part of every row: the shared-
  * hash count and its denominator.  Distances are a pure function of
- * (common, denom) and are formed on the host (drephip_distance_lut). */
+ * (common, denom) and are formed on the host (drephip_distance_lut).
+ * Input: N rows of s hashes, ascending and distinct; entries past nhash[i] are
+ * UINT64_MAX (as drephip_sketch* write them -- the kernels read whole rows;
+ * drephip_allpairs checks this, the device entry points assume it). */
 int drephip_allpairs(drephip_ctx *ctx, const uint64_t *hashes, const uint32_t *nhash, uint32_t N,
                      uint16_t *common_out, uint16_t *denom_out /* nullable */);
 

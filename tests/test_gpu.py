@@ -209,6 +209,19 @@ def test_allpairs_family_vs_oracle(family, ctx1000):
     assert c.max() > 500          # similar pairs are exercised
 
 
+def test_allpairs_rejects_unpadded_rows(ctx1000):
+    """Rows past nhash must be UINT64_MAX (the kernels read whole rows): the
+    host entry point checks and reports instead of miscounting."""
+    h = np.full((3, S), UMAX, dtype=np.uint64)
+    h[:, :10] = np.arange(10, dtype=np.uint64) + 1
+    nh = np.array([10, 10, 10], np.uint32)
+    c, _ = ctx1000.allpairs(h, nh)
+    assert list(c) == [10, 10, 10]
+    h[1, 20] = 5
+    with pytest.raises(_lib.DrepHipError, match="UINT64_MAX"):
+        ctx1000.allpairs(h, nh)
+
+
 def test_allpairs_partial_sketches_vs_oracle(ctx1000):
     rng = np.random.default_rng(3)
     A = np.frombuffer(b"ACGT", dtype=np.uint8)
