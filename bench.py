@@ -41,6 +41,26 @@ N_SIMD = 256 * 4
 # artefact of the microbench loop and is not used)
 MICROBENCH = os.path.join(ROOT, "profiles", "r01_valu_microbench.json")
 SKETCH_DEFAULT_VARIANT = "5"   # must match drephip_ctx::sketch_kernel default (ctx.h)
+# committed PMC summaries (tools/pmc_summary.py): VALU / LDS utilisation of the
+# two kernels, reported next to the live timings
+SKETCH_PMC = os.path.join(ROOT, "profiles", "r01_sketch_pmc_sq.json")
+DIST_PMC = os.path.join(ROOT, "profiles", "r01_allpairs_pmc_sq_N6000.json")
+
+
+def pmc_block(path):
+    """Utilisation fractions from a committed PMC summary, or None."""
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+    except Exception:
+        return None
+    keep = ("valu_busy_frac", "lds_busy_frac", "lds_bank_conflict_frac", "wait_any_frac",
+            "wait_inst_any_frac", "active_inst_any_frac")
+    out = {k: d["derived"][k] for k in keep if k in d.get("derived", {})}
+    out["source"] = os.path.relpath(path, ROOT)
+    out["profiled_kernel"] = (d.get("kernel") or "")[:80]
+    return out
 
 
 def parse():
@@ -309,9 +329,19 @@ def main():
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": traffic,
                 "note": "algorithmic bytes = 0.375 B/base (2-bit code + validity bit) x bases per "
-                        "launch; the binding limit is integer VALU (Murmur3 64-bit multiplies), "
-                        "see valu_model",
+                        "launch; the binding limit is VALU issue (Murmur3, ~67 instructions per "
+                        "k-mer) with the LDS table lookups as a co-limit: see valu_model and pmc",
                 "valu_model": valu,
+                "pmc": pmc_block(SKETCH_PMC),
+            },
+            "dist_kernel": {
+                "kernel": "k_allpairs_q (s <= 2048) / k_allpairs_band",
+                "bound": "VALU + LDS (random slot reads); integer set intersection, no MFMA",
+                "ms_per_launch": kms[2][0] / max(kms[2][1], 1),
+                "pairs_per_launch": segment_size(N, r0, r1),
+                "pairs_per_s_per_gpu": (segment_size(N, r0, r1) / (kms[2][0] / max(kms[2][1], 1) / 1e3)
+                                        if kms[2][0] else None),
+                "pmc": pmc_block(DIST_PMC),
             },
             "cpu_baseline": cpu,
         }

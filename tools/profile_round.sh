@@ -24,3 +24,5 @@ for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_I
   timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/sq$i -o pmc -- \
       python bench.py --steps 1 --warmup 0 --cpu-baseline 0 > $OUT/sq$i.json 2> $OUT/sq$i.err || exit 1
 done
+python3 tools/pmc_summary.py k_sketch_hash21 $OUT/sq*/pmc_counter_collection.csv > $OUT/sketch_pmc_sq.json || exit 1
+python3 tools/pmc_summary.py k_allpairs_q $OUT/sq*/pmc_counter_collection.csv > $OUT/allpairs_pmc_sq_N1000.json || exit 1
