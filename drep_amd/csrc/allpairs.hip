@@ -454,7 +454,7 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 // rows' largest element + 1); lanes past s hold clamped copies and are masked
 // by tail_mask.
 __device__ __forceinline__ uint64_t ld_col(const uint64_t *__restrict__ Bc, uint32_t j, uint32_t s) {
-    return Bc[j < s ? j : s - 1];
+    return Bc[min(j, s - 1)];
 }
 __device__ __forceinline__ uint64_t tail_mask(uint32_t j0, uint32_t s) {     // lanes with j0 + lane < s
     return j0 + 64 <= s ? ~0ull : j0 >= s ? 0ull : (1ull << (s - j0)) - 1;
