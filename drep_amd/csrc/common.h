@@ -7,6 +7,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
 #include <string>
 
 namespace drephip {
@@ -29,8 +30,17 @@ inline uint64_t round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }
 // launch whose grid scales with N is issued in pieces of at most
 // kMaxLaunchItems work-items.  A multiple of 8 workgroups per piece keeps the
 // XCD-interleaved item order of the all-pairs kernels intact.
+// DREPHIP_MAX_LAUNCH_ITEMS (tests only) lowers the cap so the split runs at
+// small sizes too.
 constexpr uint64_t kMaxLaunchItems = 1ull << 31;
-inline uint64_t max_blocks(uint32_t wg) { return kMaxLaunchItems / wg / 8 * 8; }
+inline uint64_t max_blocks(uint32_t wg) {
+    uint64_t cap = kMaxLaunchItems;
+    if (const char *e = std::getenv("DREPHIP_MAX_LAUNCH_ITEMS")) {
+        const uint64_t v = std::strtoull(e, nullptr, 10);
+        if (v) cap = v < 8ull * wg ? 8ull * wg : v > kMaxLaunchItems ? kMaxLaunchItems : v;
+    }
+    return cap / wg / 8 * 8;
+}
 
 // padded footprint of a genome whose records (incl. the 1-base separators)
 // span `span` bases: at least one invalid base after it, rounded to a tile.

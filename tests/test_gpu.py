@@ -342,6 +342,47 @@ def test_allpairs_row_segments_and_merge_kernel(family, ctx1000):
     assert np.array_equal(out.cpu().numpy().view(np.uint16), oc)
 
 
+def test_split_launches_match_oracle(family, monkeypatch):
+    """Every N-scaled launch is issued in pieces of < 2^32 work-items
+    (kMaxLaunchItems; at N = 10^5 the all-pairs grid needs 5).  A tiny cap
+    (DREPHIP_MAX_LAUNCH_ITEMS) forces dozens of pieces at test sizes: table,
+    band and merge all-pairs, the sketch hash kernel and the synthetic
+    generator must still match the oracle exactly."""
+    import torch
+    monkeypatch.setenv("DREPHIP_MAX_LAUNCH_ITEMS", "8192")
+    h, nh = family
+    N = len(nh)
+    oc, _ = oracle.allpairs(h, nh, S, threads=8)
+    with _lib.Context(0, 21, S, 42) as ctx:
+        c, _ = ctx.allpairs(h, nh)                                   # table path
+        assert np.array_equal(c, oc)
+        ctx.set_allpairs_path(ctx.AP_BAND, 64)
+        c, _ = ctx.allpairs(h, nh)
+        assert np.array_equal(c, oc)
+        dh = torch.from_numpy(h.view(np.int64)).cuda()
+        dn = torch.from_numpy(nh.view(np.int32)).cuda()
+        out = torch.zeros(N * (N - 1) // 2, dtype=torch.int16, device="cuda")
+        ctx.allpairs_device(dh.data_ptr(), dn.data_ptr(), N, 0, N, out.data_ptr(), None,
+                            torch.cuda.current_stream().cuda_stream, merge=True)
+        assert np.array_equal(out.cpu().numpy().view(np.uint16), oc)
+        # sketch + synth: 3 genomes of 300 kbp = ~30 tiles, 16 per piece
+        n, L, seed, fam = 3, 300_000, 11, 2
+        tile = _lib.tile_bases()
+        P = _lib.padded_bases([L])
+        codes = torch.zeros((tile + n * P) // 16, dtype=torch.int32, device="cuda")
+        valid = torch.zeros((tile + n * P) // 32, dtype=torch.int32, device="cuda")
+        st = torch.cuda.current_stream().cuda_stream
+        ctx.synth_device(seed, 0, n, fam, L, codes.data_ptr(), valid.data_ptr(), st)
+        hh = torch.zeros((n, S), dtype=torch.int64, device="cuda")
+        nn = torch.zeros(n, dtype=torch.int32, device="cuda")
+        ctx.sketch_device(codes.data_ptr(), valid.data_ptr(), np.array([tile + i * P for i in range(n)], np.uint64),
+                          np.full(n, P, np.uint64), np.full(n, L - 20, np.uint64), n, hh.data_ptr(), nn.data_ptr(), st)
+        torch.cuda.synchronize()
+    oh, onh = oracle.sketch_synth(0, n, L, seed=seed, family_size=fam, threads=3)
+    assert np.array_equal(hh.cpu().numpy().view(np.uint64), oh)
+    assert np.array_equal(nn.cpu().numpy().view(np.uint32), onh)
+
+
 # ---------------------------------------------------------------- drop-in
 def test_all_vs_all_MASH_dropin_reproduces_reference(golden, tmp_path):
     """all_vs_all_MASH on the reference's test genomes (Sakai from its cached
