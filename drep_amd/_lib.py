@@ -61,6 +61,7 @@ SIGNATURES = {
     "drephip_synth_device": (C.c_int, [vp, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64,
                                        vp, vp, vp]),
     "drephip_allpairs": (C.c_int, [vp, u64p, u32p, C.c_uint32, u16p, vp]),
+    "drephip_allpairs_rows": (C.c_int, [vp, u64p, u32p, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp]),
     "drephip_allpairs_device": (C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp]),
     "drephip_allpairs_merge_device": (C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp]),
     "drephip_distance_lut": (C.c_int, [C.c_int, C.c_uint32, f64p]),
@@ -294,6 +295,30 @@ class Context:
         else:
             denom = denom[:npairs]
         return common, denom
+
+    def allpairs_rows(self, hashes: np.ndarray, nhash: np.ndarray, row0: int, row1: int,
+                      common_out: np.ndarray, denom_out: Optional[np.ndarray] = None) -> None:
+        """Rows [row0, row1) of the triangle into the given condensed segment
+        views (uint16, contiguous; length = pairs of those rows)."""
+        hashes = np.ascontiguousarray(hashes, dtype=np.uint64)
+        nhash = np.ascontiguousarray(nhash, dtype=np.uint32)
+        N = len(nhash)
+        if hashes.shape != (N, self.s):
+            raise ValueError("hashes must be [N, s] = [%d, %d], got %s" % (N, self.s, hashes.shape))
+        r1 = min(row1, N - 1)
+
+        def start(i):
+            return i * N - i * (i + 1) // 2
+        n = max(0, start(r1) - start(row0)) if row0 < r1 else 0
+        for arr in (common_out, denom_out):
+            if arr is not None and (arr.dtype != np.uint16 or not arr.flags.c_contiguous or len(arr) < n):
+                raise ValueError("segment buffers must be contiguous uint16 of length >= %d" % n)
+        if n == 0:
+            return
+        check(lib().drephip_allpairs_rows(self._h, hashes.reshape(-1), nhash, N, row0, row1,
+                                          common_out.ctypes.data,
+                                          denom_out.ctypes.data if denom_out is not None else None),
+              "drephip_allpairs_rows")
 
     def allpairs_device(self, d_hashes: int, d_nhash: int, N: int, row0: int, row1: int, d_common: int,
                         d_denom: Optional[int] = None, stream: Optional[int] = None, merge: bool = False):

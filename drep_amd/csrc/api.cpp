@@ -394,18 +394,21 @@ DREPHIP_EXPORT int drephip_allpairs_merge_device(drephip_ctx *ctx, const uint64_
     return DREPHIP_OK;
 }
 
-DREPHIP_EXPORT int drephip_allpairs(drephip_ctx *ctx, const uint64_t *hashes, const uint32_t *nhash, uint32_t N,
-                                    uint16_t *common_out, uint16_t *denom_out) {
-    GUARD_CTX(ctx);
-    if (N < 2) return DREPHIP_OK;
+// Host-buffer all-pairs over rows [row0, row1): stage the sketch matrix, run
+// the kernels on the context's stream, copy the condensed segment back.
+static int allpairs_host_rows(drephip_ctx *ctx, const uint64_t *hashes, const uint32_t *nhash, uint32_t N,
+                              uint32_t row0, uint32_t row1, uint16_t *common_out, uint16_t *denom_out) {
     if (!hashes || !nhash || !common_out) { set_error("null argument"); return DREPHIP_ERR_ARG; }
+    if (row1 > N) row1 = N;
+    if (N < 2 || row0 >= row1 || row0 >= N - 1) return DREPHIP_OK;
     for (uint32_t i = 0; i < N; i++) {                    // the kernels read rows past nhash: must be padding
         if (nhash[i] > ctx->s) { set_error("nhash[i] > s"); return DREPHIP_ERR_ARG; }
         const uint64_t *row = hashes + (uint64_t)i * ctx->s;
         for (uint32_t j = nhash[i]; j < ctx->s; j++)
             if (row[j] != ~0ull) { set_error("sketch rows must be UINT64_MAX past nhash[i]"); return DREPHIP_ERR_ARG; }
     }
-    const uint64_t npairs = (uint64_t)N * (N - 1) / 2;
+    auto start = [&](uint64_t i) { return i * N - i * (i + 1) / 2; };
+    const uint64_t npairs = start(std::min(row1, N - 1)) - start(row0);
     hipStream_t st = ctx->stream;
     uint64_t *d_h;
     uint32_t *d_n;
@@ -418,13 +421,25 @@ DREPHIP_EXPORT int drephip_allpairs(drephip_ctx *ctx, const uint64_t *hashes, co
     HIPC(hipMemcpyAsync(d_h, hashes, (uint64_t)N * ctx->s * 8, hipMemcpyHostToDevice, st));
     HIPC(hipMemcpyAsync(d_n, nhash, N * 4ull, hipMemcpyHostToDevice, st));
     timing_begin(ctx);
-    rc = allpairs_device_impl(ctx, d_h, d_n, N, 0, N, d_c, d_d, st, false);
+    rc = allpairs_device_impl(ctx, d_h, d_n, N, row0, row1, d_c, d_d, st, false);
     if (rc) return rc;
     timing_collect(ctx);
     HIPC(hipMemcpyAsync(common_out, d_c, npairs * 2, hipMemcpyDeviceToHost, st));
     if (denom_out) HIPC(hipMemcpyAsync(denom_out, d_d, npairs * 2, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));
     return DREPHIP_OK;
+}
+
+DREPHIP_EXPORT int drephip_allpairs(drephip_ctx *ctx, const uint64_t *hashes, const uint32_t *nhash, uint32_t N,
+                                    uint16_t *common_out, uint16_t *denom_out) {
+    GUARD_CTX(ctx);
+    return allpairs_host_rows(ctx, hashes, nhash, N, 0, N, common_out, denom_out);
+}
+
+DREPHIP_EXPORT int drephip_allpairs_rows(drephip_ctx *ctx, const uint64_t *hashes, const uint32_t *nhash, uint32_t N,
+                                         uint32_t row0, uint32_t row1, uint16_t *common_out, uint16_t *denom_out) {
+    GUARD_CTX(ctx);
+    return allpairs_host_rows(ctx, hashes, nhash, N, row0, row1, common_out, denom_out);
 }
 
 DREPHIP_EXPORT int drephip_distance_lut(int k, uint32_t denom, double *lut) {

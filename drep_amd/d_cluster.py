@@ -38,6 +38,7 @@ import scipy.spatial.distance as ssd
 
 from . import _lib
 from .mash_io import MashReference, read_msh, write_msh
+from .parallel import cond_start, row_partition, segment_size
 
 MASH_K = 21          # Mash default, never overridden by dRep (d_cluster.py:543)
 MASH_SEED = 42       # Mash default hash seed
@@ -135,6 +136,41 @@ def mdb_from_condensed(names: Sequence[str], common: np.ndarray, denom: np.ndarr
     return Mdb
 
 
+# ---------------------------------------------------------- devices
+def _devices(kwargs) -> List[int]:
+    """HIP devices for the Mash step: kwargs `gpus` (a count, a list, or
+    "0,1,..."), else $DREPHIP_DEVICES, else the single `gpu` /
+    $DREPHIP_DEVICE (default 0)."""
+    g = kwargs.get('gpus', os.environ.get('DREPHIP_DEVICES'))
+    if g is None or g == '':
+        return [int(kwargs.get('gpu', os.environ.get('DREPHIP_DEVICE', 0)))]
+    if isinstance(g, int):
+        return list(range(g))
+    if isinstance(g, str):
+        return [int(x) for x in g.split(',') if x.strip() != '']
+    return [int(x) for x in g]
+
+
+def _on_devices(devs: Sequence[int], fn) -> list:
+    """fn(i, device) for every device, one host thread each (the C ABI calls
+    release the GIL); first exception re-raised."""
+    from concurrent.futures import ThreadPoolExecutor
+    if len(devs) == 1:
+        return [fn(0, devs[0])]
+    with ThreadPoolExecutor(max_workers=len(devs)) as ex:
+        futs = [ex.submit(fn, i, d) for i, d in enumerate(devs)]
+        return [f.result() for f in futs]
+
+
+def _balanced_shards(weights: Sequence[int], n: int) -> List[List[int]]:
+    """Contiguous index shards with near-equal total weight (genome bytes)."""
+    w = np.asarray(weights, dtype=np.float64)
+    cum = np.concatenate([[0.0], np.cumsum(w)])
+    cuts = [0] + [int(np.searchsorted(cum, cum[-1] * k / n)) for k in range(1, n)] + [len(w)]
+    cuts = np.maximum.accumulate(np.minimum(cuts, len(w)))
+    return [list(range(cuts[k], cuts[k + 1])) for k in range(n)]
+
+
 # ---------------------------------------------------------- sketch cache
 def _load_cached(path: str, s: int) -> Optional[MashReference]:
     try:
@@ -164,7 +200,6 @@ def sketch_genomes(Bdb: pd.DataFrame, data_folder: str, **kwargs) -> SketchSet:
     MASH_s = int(kwargs.get('MASH_sketch', 1000))
     p = int(kwargs.get('processors', 6))
     groupSize = int(kwargs.get('groupSize', 1000))
-    device = int(kwargs.get('gpu', os.environ.get('DREPHIP_DEVICE', 0)))
     write_sketches = kwargs.get('write_sketches', True)
 
     MASH_folder = os.path.join(data_folder, 'MASH_files/')
@@ -203,12 +238,21 @@ def sketch_genomes(Bdb: pd.DataFrame, data_folder: str, **kwargs) -> SketchSet:
         chunk_members.append(members)
 
     if todo:
-        with _lib.Context(device=device, k=MASH_K, s=MASH_s, seed=MASH_SEED) as ctx:
-            h, nh, ln = ctx.sketch_files([locations[i] for i in todo], threads=p)
-        hashes[todo] = h
-        nhash[todo] = nh
-        length[todo] = ln
-        logging.debug("sketched %d genomes on HIP device %d", len(todo), device)
+        devs = _devices(kwargs)
+        sizes = [os.path.getsize(locations[i]) if os.path.exists(locations[i]) else 1 for i in todo]
+        shards = [[todo[j] for j in sh] for sh in _balanced_shards(sizes, len(devs))]
+        threads = max(1, p // len(devs))
+
+        def run(k, dev):
+            if not shards[k]:
+                return
+            with _lib.Context(device=dev, k=MASH_K, s=MASH_s, seed=MASH_SEED) as ctx:
+                h, nh, ln = ctx.sketch_files([locations[i] for i in shards[k]], threads=threads)
+            hashes[shards[k]] = h
+            nhash[shards[k]] = nh
+            length[shards[k]] = ln
+        _on_devices(devs, run)
+        logging.debug("sketched %d genomes on HIP devices %s", len(todo), devs)
 
     if write_sketches:
         def ref_of(i):
@@ -240,10 +284,35 @@ def all_vs_all_MASH_condensed(Bdb, data_folder, **kwargs) -> CondensedMash:
     """Sketch (or load cached sketches) and run the HIP all-pairs kernel;
     return the condensed shared-hash counts instead of an N^2-row table."""
     sk = sketch_genomes(Bdb, data_folder, **kwargs)
-    device = int(kwargs.get('gpu', os.environ.get('DREPHIP_DEVICE', 0)))
-    with _lib.Context(device=device, k=MASH_K, s=sk.s, seed=MASH_SEED) as ctx:
-        common, denom = ctx.allpairs(sk.hashes, sk.nhash)
+    common, denom = condensed_allpairs(sk.hashes, sk.nhash, sk.s, _devices(kwargs))
     return CondensedMash(sk.names, sk.locations, common, denom, sk.nhash, sk.length, sk.s)
+
+
+def condensed_allpairs(hashes: np.ndarray, nhash: np.ndarray, s: int, devices: Sequence[int] = (0,)):
+    """(common, denom) for the whole condensed triangle.  With several devices
+    the rows are split into contiguous ranges of near-equal pair count
+    (parallel.row_partition), one context and host thread per device, each
+    writing its own segment of the host buffers (no collective)."""
+    N = len(nhash)
+    npairs = N * (N - 1) // 2
+    partial = bool((np.asarray(nhash) < s).any())
+    common = np.zeros(npairs, dtype=np.uint16)
+    denom = np.zeros(npairs, dtype=np.uint16) if partial else None
+    parts = row_partition(N, len(devices))
+
+    def run(k, dev):
+        r0, r1 = parts[k]
+        a = cond_start(r0, N)
+        b = a + segment_size(N, r0, r1)
+        if b <= a:
+            return
+        with _lib.Context(device=dev, k=MASH_K, s=s, seed=MASH_SEED) as ctx:
+            ctx.allpairs_rows(hashes, nhash, r0, r1, common[a:b], denom[a:b] if denom is not None else None)
+    if npairs:
+        _on_devices(list(devices), run)
+    if denom is None:
+        denom = np.full(npairs, s, dtype=np.uint16)
+    return common, denom
 
 
 def all_vs_all_MASH(Bdb, data_folder, **kwargs):
@@ -265,6 +334,9 @@ def all_vs_all_MASH(Bdb, data_folder, **kwargs):
         debug / wd: accepted for compatibility (no external commands to log)
         exe_loc / mash_exe: accepted and ignored (no mash executable is used)
         gpu: HIP device index (default $DREPHIP_DEVICE or 0)
+        gpus: several HIP devices (count, list or "0,1,..."; default
+            $DREPHIP_DEVICES): sketch shards and all-pairs row ranges run on
+            all of them from this process, one host thread per device
         write_sketches: write the .msh files (default True)
         write_table: also write MASH_table.tsv like `mash dist` (default False)
 

@@ -141,6 +141,14 @@ int drephip_synth_device(drephip_ctx *ctx, uint64_t seed, uint32_t g0, uint32_t 
 int drephip_allpairs(drephip_ctx *ctx, const uint64_t *hashes, const uint32_t *nhash, uint32_t N,
                      uint16_t *common_out, uint16_t *denom_out /* nullable */);
 
+/* drephip_allpairs restricted to rows [row0, row1) of the upper triangle
+ * (columns row+1..N-1): common_out/denom_out receive the condensed segment
+ * that starts at index(row0, row0+1), i.e. row0*N - row0*(row0+1)/2.  One call
+ * per device (one context each) splits the triangle across GPUs inside one
+ * process -- the multi-device form of the same `mash dist` step. */
+int drephip_allpairs_rows(drephip_ctx *ctx, const uint64_t *hashes, const uint32_t *nhash, uint32_t N,
+                          uint32_t row0, uint32_t row1, uint16_t *common_out, uint16_t *denom_out /* nullable */);
+
 /* Device-resident all-pairs over rows [row0, row1) of the upper triangle
  * (columns row+1..N-1).  d_common/d_denom receive the condensed segment that
  * starts at index(row0, row0+1).  d_denom may be NULL. Blocking. */

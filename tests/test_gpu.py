@@ -342,6 +342,25 @@ def test_allpairs_row_segments_and_merge_kernel(family, ctx1000):
     assert np.array_equal(out.cpu().numpy().view(np.uint16), oc)
 
 
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0, 0, 0]])
+def test_condensed_allpairs_multi_device(family, devices):
+    """In-process multi-device all-pairs (drephip_allpairs_rows per device on
+    balanced row ranges, threads) assembles the same triangle, with partial
+    sketches (denominators) too."""
+    from drep_amd.d_cluster import condensed_allpairs
+    h, nh = family
+    oc, od = oracle.allpairs(h, nh, S, threads=8)
+    c, d = condensed_allpairs(h, nh, S, devices)
+    assert np.array_equal(c, oc) and (d == S).all()
+    h2, nh2 = h.copy(), nh.copy()
+    nh2[::7] = 500
+    for i in range(0, len(nh2), 7):
+        h2[i, 500:] = UMAX
+    oc, od = oracle.allpairs(h2, nh2, S, threads=8)
+    c, d = condensed_allpairs(h2, nh2, S, devices)
+    assert np.array_equal(c, oc) and np.array_equal(d, od)
+
+
 def test_split_launches_match_oracle(family, monkeypatch):
     """Every N-scaled launch is issued in pieces of < 2^32 work-items
     (kMaxLaunchItems; at N = 10^5 the all-pairs grid needs 5).  A tiny cap
@@ -384,11 +403,14 @@ def test_split_launches_match_oracle(family, monkeypatch):
 
 
 # ---------------------------------------------------------------- drop-in
-def test_all_vs_all_MASH_dropin_reproduces_reference(golden, tmp_path):
+@pytest.mark.parametrize("gpus", [None, "0,0,0"])
+def test_all_vs_all_MASH_dropin_reproduces_reference(golden, tmp_path, gpus):
     """all_vs_all_MASH on the reference's test genomes (Sakai from its cached
     .msh, as the reference's own sketch cache would) -> Mdb bit-identical to
     the reference's parse of its fixture MASH_table.tsv, then primary
-    clustering identical to the reference's Cdb / linkage."""
+    clustering identical to the reference's Cdb / linkage.  gpus="0,0,0" runs
+    the multi-device path (sketch shards and all-pairs row ranges on three
+    contexts, one host thread each) on the one device of the test box."""
     import json
     from drep_amd import d_cluster
     fas = sorted(glob.glob(os.path.join(golden, "genomes", "*.gz")))
@@ -408,7 +430,7 @@ def test_all_vs_all_MASH_dropin_reproduces_reference(golden, tmp_path):
     chunk.mkdir(parents=True)
     shutil.copy(os.path.join(golden, "MASH_files", "sketches", "Escherichia_coli_Sakai.fna.msh"),
                 chunk / "Escherichia_coli_Sakai.fna.msh")
-    Mdb = d_cluster.all_vs_all_MASH(Bdb, str(wd), processors=4)
+    Mdb = d_cluster.all_vs_all_MASH(Bdb, str(wd), processors=4, **({"gpus": gpus} if gpus else {}))
     meta = json.load(open(os.path.join(golden, "ref", "mdb_parsed_dtypes.json")))
     exp = pd.read_csv(os.path.join(golden, "ref", "mdb_parsed.csv"))
     assert len(Mdb) == 25

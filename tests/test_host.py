@@ -243,3 +243,27 @@ def test_fasta_pack_matches_numpy_layout(tmp_path, golden):
         assert np.array_equal(valid[tile // 32:], want_v)
         assert not codes[:tile // 16].any() and not valid[:tile // 32].any()
         assert length.value == sum(len(r) for r in recs_o)
+
+
+def test_device_list_and_balanced_shards(monkeypatch):
+    """Multi-device drop-in plumbing (no GPU): the `gpus` kwarg forms and the
+    byte-balanced contiguous genome shards."""
+    from drep_amd.d_cluster import _balanced_shards, _devices
+    monkeypatch.delenv("DREPHIP_DEVICES", raising=False)
+    monkeypatch.delenv("DREPHIP_DEVICE", raising=False)
+    assert _devices({}) == [0]
+    assert _devices({"gpu": 3}) == [3]
+    assert _devices({"gpus": 4}) == [0, 1, 2, 3]
+    assert _devices({"gpus": "0,2,5"}) == [0, 2, 5]
+    assert _devices({"gpus": [1, 1]}) == [1, 1]
+    monkeypatch.setenv("DREPHIP_DEVICES", "6,7")
+    assert _devices({"gpu": 0}) == [6, 7]
+    rng = np.random.default_rng(0)
+    for n_items, n_dev in [(0, 3), (1, 4), (5, 5), (100, 8), (1000, 3)]:
+        w = rng.integers(1, 1000, n_items)
+        sh = _balanced_shards(w, n_dev)
+        assert len(sh) == n_dev
+        assert sum(sh, []) == list(range(n_items))           # contiguous cover, in order
+        if n_items >= 100:
+            tot = [w[s].sum() for s in sh]
+            assert max(tot) - min(tot) <= 2 * w.max()
