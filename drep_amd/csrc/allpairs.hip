@@ -38,7 +38,8 @@
 namespace drephip {
 
 constexpr int kApWG = 1024;                     // 16 waves per workgroup
-constexpr uint32_t kApCols = 128;               // columns per work item
+constexpr uint32_t kApCols = 128;               // columns per work item (fewer when the grid would not fill the chip)
+constexpr uint32_t kApMinCols = 16;             // one column per wave
 constexpr uint32_t kMaxFam = 6;                 // cuckoo field families tried per table
 constexpr uint32_t kLdsBudget = 156 * 1024;     // dynamic LDS per workgroup
 constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;      // empty slot word
@@ -338,7 +339,7 @@ template <int R, int NCH, int MINW>
 __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
     const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ nhash,
     const uint32_t *__restrict__ tabs, const uint8_t *__restrict__ fam, uint32_t s, uint32_t N,
-    uint32_t row0, uint32_t row1, uint32_t B, const uint2 *__restrict__ items,
+    uint32_t row0, uint32_t row1, uint32_t B, const uint2 *__restrict__ items, uint32_t ncol_item,
     uint16_t *__restrict__ common, uint16_t *__restrict__ denom, uint64_t seg0) {
     constexpr int WG = kApWG;
     extern __shared__ __align__(16) uint32_t lds[];    // 16-B aligned: slot words are read with ds_read_b128
@@ -349,7 +350,7 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
     const uint32_t c0 = items[blockIdx.x].y;
     if (i0 == 0xFFFFFFFFu) return;                      // idle padding item (make_items)
     const uint32_t nrows = min((uint32_t)R, row1 - i0);
-    const uint32_t cend = min(c0 + kApCols, N);
+    const uint32_t cend = min(c0 + ncol_item, N);
     const uint32_t tid = threadIdx.x, wave = tid >> 6;
     for (uint32_t k = tid; k < TS; k += WG) {
 #pragma unroll
@@ -365,7 +366,8 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
     for (int r = 0; r < R; r++) {
         const bool ok = (uint32_t)r < nrows;
         nA[r] = ok ? nhash[i0 + r] : s;
-        const uint32_t f = ok ? fam[i0 - row0 + r] : 0;
+        uint32_t f = ok ? fam[i0 - row0 + r] : 0;
+        f = f < kMaxFam ? f : 0;        // failed table (0xFF): output discarded, the host reruns the merge kernel
         const QFields q = qfields(f);
         o1[r] = q.o1; o2[r] = q.o2;
         fast &= f == 0;
@@ -793,13 +795,15 @@ static int launch_band(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_
 template <int R, int NCH, int MINW>
 static int launch_q(drephip_ctx *ctx, uint32_t nitems, size_t lds, hipStream_t st, const uint64_t *h,
                     const uint32_t *nh, const uint32_t *tabs, const uint8_t *fam, uint32_t N, uint32_t row0,
-                    uint32_t row1, uint32_t B, const uint2 *items, uint16_t *cm, uint16_t *dn, uint64_t seg0) {
+                    uint32_t row1, uint32_t B, const uint2 *items, uint32_t C, uint16_t *cm, uint16_t *dn,
+                    uint64_t seg0) {
     HIPC(hipFuncSetAttribute((const void *)k_allpairs_q<R, NCH, MINW>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)lds));
     timing_mark(ctx, 2, st, true);
     for (uint32_t i0 = 0; i0 < nitems; i0 += (uint32_t)max_blocks(kApWG))
         hipLaunchKernelGGL((k_allpairs_q<R, NCH, MINW>), dim3(std::min<uint32_t>(nitems - i0, (uint32_t)max_blocks(kApWG))),
-                           dim3(kApWG), lds, st, h, nh, tabs, fam, ctx->s, N, row0, row1, B, items + i0, cm, dn, seg0);
+                           dim3(kApWG), lds, st, h, nh, tabs, fam, ctx->s, N, row0, row1, B, items + i0, C, cm, dn,
+                           seg0);
     timing_mark(ctx, 2, st, false);
     HIPC(hipGetLastError());
     return DREPHIP_OK;
@@ -854,22 +858,31 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
     static const uint32_t kR[] = {8, 4, 2, 1};
     uint32_t R = 1;
     for (uint32_t r : kR) if (q_lds_bytes(r, TS, s) <= kLdsBudget) { R = r; break; }
-    const std::vector<uint2> items = make_items(row0, row1, N, R, kApCols);
+    // column tile: the widest (<= kApCols) whose item count still gives every
+    // workgroup slot of the chip (256 CUs x 2) about four items; small
+    // problems (a rank's shard on 8 GPUs, N ~ 10^3) get narrower items
+    uint32_t C = kApCols;
+    auto nitems_for = [&](uint32_t c) {
+        uint64_t n = 0;
+        const uint32_t nct = (N + c - 1) / c;
+        for (uint32_t i0 = row0; i0 < row1; i0 += R) n += nct - (i0 + 1) / c;
+        return n;
+    };
+    while (C > kApMinCols && nitems_for(C) < 4ull * 2 * 256) C /= 2;
+    const std::vector<uint2> items = make_items(row0, row1, N, R, C);
     if ((rc = scratch(ctx, "ap_items", items.size() * sizeof(uint2), (void **)&d_items))) return rc;
     HIPC(hipMemcpyAsync(d_items, items.data(), items.size() * sizeof(uint2), hipMemcpyHostToDevice, st));
-    uint32_t nfail = 0;
-    HIPC(hipMemcpyAsync(&nfail, d_nfail, 4, hipMemcpyDeviceToHost, st));
-    HIPC(hipStreamSynchronize(st));
-    if (nfail)   // a row table could not be built with any field pair: exact merge kernel instead
-        return launch_merge(ctx, d_hashes, d_nhash, N, seg0, npairs, d_common, d_denom, st);
+    // the main kernel is queued without waiting for the build's failure count;
+    // in the (never observed) case of a row with no working field family its
+    // output is discarded and the merge kernel recomputes the segment
 
     const size_t lds = q_lds_bytes(R, TS, s);
     const uint32_t ni = (uint32_t)items.size();
     const uint32_t nch = (s + 63) / 64;
     // two workgroups per CU when the LDS allows (DREPHIP_AP_ONEWG=1: one, A/B)
     const bool two = lds <= 80 * 1024 && !getenv("DREPHIP_AP_ONEWG");
-#define DREPHIP_Q(RR, NC) (two ? launch_q<RR, NC, 8>(ctx, ni, lds, st, d_hashes, d_nhash, d_tabs, d_fam, N, row0, row1, B, d_items, d_common, d_denom, seg0) \
-                               : launch_q<RR, NC, 4>(ctx, ni, lds, st, d_hashes, d_nhash, d_tabs, d_fam, N, row0, row1, B, d_items, d_common, d_denom, seg0))
+#define DREPHIP_Q(RR, NC) (two ? launch_q<RR, NC, 8>(ctx, ni, lds, st, d_hashes, d_nhash, d_tabs, d_fam, N, row0, row1, B, d_items, C, d_common, d_denom, seg0) \
+                               : launch_q<RR, NC, 4>(ctx, ni, lds, st, d_hashes, d_nhash, d_tabs, d_fam, N, row0, row1, B, d_items, C, d_common, d_denom, seg0))
     if (nch <= 8) {
         switch (R) {
             case 8: rc = DREPHIP_Q(8, 8); break;
@@ -893,7 +906,11 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
     }
 #undef DREPHIP_Q
     if (rc) return rc;
-    HIPC(hipStreamSynchronize(st));
+    uint32_t nfail = 0;
+    HIPC(hipMemcpyAsync(&nfail, d_nfail, 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));                  // items (host vector) and nfail are safe past here
+    if (nfail)   // a row table could not be built with any field pair: exact merge kernel instead
+        return launch_merge(ctx, d_hashes, d_nhash, N, seg0, npairs, d_common, d_denom, st);
     return DREPHIP_OK;
 }
 

@@ -209,6 +209,36 @@ def test_allpairs_family_vs_oracle(family, ctx1000):
     assert c.max() > 500          # similar pairs are exercised
 
 
+@pytest.mark.parametrize("path", ["table", "band"])
+def test_allpairs_unbuildable_table_falls_back_to_merge(path):
+    """Three hashes of one row sharing their low 32 bits land in the same two
+    slots under every field family, so no cuckoo table exists for that row:
+    the host must discard the table kernel's output and rerun the segment with
+    the literal merge kernel -- counts still exact."""
+    rng = np.random.default_rng(3)
+    N = 24
+    base = np.sort(rng.choice(2 ** 62, size=(N, 2000), replace=False).astype(np.uint64), axis=1)
+    h = np.full((N, S), UMAX, dtype=np.uint64)
+    for i in range(N):                                   # families: shared prefixes
+        pool = base[i // 6]
+        keep = np.sort(rng.choice(len(pool), S, replace=False))
+        h[i] = pool[keep]
+    lo = np.uint64(0x12345678)
+    bad = np.array([(np.uint64(k) << np.uint64(40)) | lo for k in (1, 2, 3)], dtype=np.uint64)
+    for i in (0, 7):
+        row = np.unique(np.concatenate([h[i][:S - 3], bad]))
+        h[i] = row[:S]
+        h[i + 1] = np.unique(np.concatenate([h[i + 1][:S - 2], bad[:2]]))[:S]
+    nh = np.full(N, S, np.uint32)
+    oc, _ = oracle.allpairs(h, nh, S, threads=4)
+    with _lib.Context(0, 21, S, 42) as ctx:
+        if path == "band":
+            ctx.set_allpairs_path(ctx.AP_BAND, 256)
+        c, _ = ctx.allpairs(h, nh)
+    assert np.array_equal(c, oc)
+    assert c.max() >= 2
+
+
 def test_allpairs_rejects_unpadded_rows(ctx1000):
     """Rows past nhash must be UINT64_MAX (the kernels read whole rows): the
     host entry point checks and reports instead of miscounting."""
