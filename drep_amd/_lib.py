@@ -131,6 +131,11 @@ def device_count() -> int:
     return n.value if rc == 0 else 0
 
 
+def max_sketch() -> int:
+    """Largest supported sketch size s."""
+    return int(lib().drephip_max_sketch())
+
+
 def tile_bases() -> int:
     return int(lib().drephip_tile_bases())
 

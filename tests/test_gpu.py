@@ -483,6 +483,27 @@ def test_all_vs_all_MASH_dropin_reproduces_reference(golden, tmp_path, gpus):
         assert got == link["linkage"]
 
 
+def test_errors_are_reported_not_hidden(ctx1000, tmp_path):
+    """The reference ignores Mash's exit codes (drep/__init__.py:44-48); the
+    C ABI returns them: unreadable inputs, bad sizes and bad devices raise with
+    a message instead of producing missing or wrong rows."""
+    with pytest.raises(_lib.DrepHipError, match="nonexistent"):
+        ctx1000.sketch_files([str(tmp_path / "nonexistent.fna")])
+    bad = tmp_path / "broken.fa.gz"
+    bad.write_bytes(b"\x1f\x8b\x08\x00not really gzip")
+    with pytest.raises(_lib.DrepHipError):
+        ctx1000.sketch_files([str(bad)])
+    with pytest.raises(_lib.DrepHipError):
+        _lib.Context(device=0, k=21, s=0, seed=42)
+    with pytest.raises(_lib.DrepHipError):
+        _lib.Context(device=0, k=21, s=_lib.max_sketch() + 1, seed=42)
+    with pytest.raises(_lib.DrepHipError):
+        _lib.Context(device=1 << 20, k=21, s=1000, seed=42)
+    h = np.full((2, S), UMAX, dtype=np.uint64)
+    with pytest.raises(_lib.DrepHipError):
+        ctx1000.allpairs(h, np.array([S + 1, 0], np.uint32))
+
+
 def test_device_calls_follow_callers_stream(ctx1000):
     """Device-pointer calls run on the caller's stream: a synth issued right
     after torch's (asynchronous) zero-fill of a multi-GB buffer on torch's
