@@ -30,6 +30,7 @@
 #include "../../include/drephip.h"
 
 #include <algorithm>
+#include <cstring>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -869,15 +870,30 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
         return n;
     };
     while (C > kApMinCols && nitems_for(C) < 4ull * 2 * 256) C /= 2;
-    const std::vector<uint2> items = make_items(row0, row1, N, R, C);
-    if ((rc = scratch(ctx, "ap_items", items.size() * sizeof(uint2), (void **)&d_items))) return rc;
-    HIPC(hipMemcpyAsync(d_items, items.data(), items.size() * sizeof(uint2), hipMemcpyHostToDevice, st));
+    // the item list depends only on (N, rows, R, C): reused while the shape and
+    // the scratch allocation are unchanged (repeated calls: bench steps, shards)
+    const uint64_t key[5] = {N, row0, row1, R, C};
+    std::vector<uint2> items;
+    uint32_t ni = ctx->ap_items_n;
+    const bool reuse = ctx->ap_items_gen == ctx->alloc_gen && !memcmp(ctx->ap_items_key, key, sizeof(key));
+    if (!reuse) {
+        items = make_items(row0, row1, N, R, C);
+        ni = (uint32_t)items.size();
+    }
+    if ((rc = scratch(ctx, "ap_items", (uint64_t)ni * sizeof(uint2), (void **)&d_items))) return rc;
+    if (!reuse) {
+        HIPC(hipMemcpyAsync(d_items, items.data(), items.size() * sizeof(uint2), hipMemcpyHostToDevice, st));
+        memcpy(ctx->ap_items_key, key, sizeof(key));
+        ctx->ap_items_n = ni;
+        ctx->ap_items_gen = ctx->alloc_gen;
+    }
+    uint32_t *h_nfail;
+    if ((rc = pinned_host(ctx, "ap_nfail", 4, (void **)&h_nfail))) return rc;
     // the main kernel is queued without waiting for the build's failure count;
     // in the (never observed) case of a row with no working field family its
     // output is discarded and the merge kernel recomputes the segment
 
     const size_t lds = q_lds_bytes(R, TS, s);
-    const uint32_t ni = (uint32_t)items.size();
     const uint32_t nch = (s + 63) / 64;
     // two workgroups per CU when the LDS allows (DREPHIP_AP_ONEWG=1: one, A/B)
     const bool two = lds <= 80 * 1024 && !getenv("DREPHIP_AP_ONEWG");
@@ -906,10 +922,9 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
     }
 #undef DREPHIP_Q
     if (rc) return rc;
-    uint32_t nfail = 0;
-    HIPC(hipMemcpyAsync(&nfail, d_nfail, 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(h_nfail, d_nfail, 4, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));                  // items (host vector) and nfail are safe past here
-    if (nfail)   // a row table could not be built with any field pair: exact merge kernel instead
+    if (*h_nfail)   // a row table could not be built with any field pair: exact merge kernel instead
         return launch_merge(ctx, d_hashes, d_nhash, N, seg0, npairs, d_common, d_denom, st);
     return DREPHIP_OK;
 }

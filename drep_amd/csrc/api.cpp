@@ -46,6 +46,28 @@ int scratch(drephip_ctx *ctx, const char *name, size_t bytes, void **out) {
     return DREPHIP_OK;
 }
 
+int pinned_host(drephip_ctx *ctx, const char *name, size_t bytes, void **out) {
+    DevBuf &b = ctx->pinned[name];
+    if (bytes == 0) bytes = 8;
+    if (b.bytes < bytes) {
+        if (b.ptr) {
+            HIPC(hipStreamSynchronize(ctx->stream));
+            HIPC(hipHostFree(b.ptr));
+            b.ptr = nullptr; b.bytes = 0;
+        }
+        const size_t want = std::max(bytes, (size_t)4096);
+        hipError_t e = hipHostMalloc(&b.ptr, want, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            set_error(std::string("hipHostMalloc for ") + name + ": " + hipGetErrorString(e));
+            b.ptr = nullptr;
+            return DREPHIP_ERR_NOMEM;
+        }
+        b.bytes = want;
+    }
+    *out = b.ptr;
+    return DREPHIP_OK;
+}
+
 void timing_begin(drephip_ctx *ctx) {
     for (int i = 0; i < 4; i++) { ctx->kms[i] = 0; ctx->kn[i] = 0; }
     ctx->spans.clear();
@@ -146,6 +168,7 @@ DREPHIP_EXPORT int drephip_destroy(drephip_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     for (auto &kv : ctx->bufs) if (kv.second.ptr) (void)hipFree(kv.second.ptr);
+    for (auto &kv : ctx->pinned) if (kv.second.ptr) (void)hipHostFree(kv.second.ptr);
     for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;

@@ -35,8 +35,14 @@ struct drephip_ctx {
     uint64_t alloc_gen = 1;   // bumped by every scratch (re)allocation
     // sketch tile table of the last call (reused while the genome layout is the
     // same and no scratch buffer has been reallocated since: sk_gen == alloc_gen)
-    std::vector<uint64_t> sk_off, sk_pad;
+    std::vector<uint64_t> sk_off, sk_pad, sk_nk;
     uint64_t sk_gen = 0;
+    // pinned host staging for the small per-call readbacks (status, failure count)
+    std::map<std::string, DevBuf> pinned;
+    // all-pairs work-item list of the last call, reused on the same shape
+    uint64_t ap_items_key[5] = {0, 0, 0, 0, 0};
+    uint64_t ap_items_gen = 0;
+    uint32_t ap_items_n = 0;
 };
 
 namespace drephip {
@@ -53,6 +59,8 @@ namespace drephip {
 
 // Grow-only named scratch buffer on the context's device.
 int scratch(drephip_ctx *ctx, const char *name, size_t bytes, void **out);
+// Grow-only named pinned host buffer (hipHostMalloc) for async readbacks.
+int pinned_host(drephip_ctx *ctx, const char *name, size_t bytes, void **out);
 
 // Bracket kernel launches with events when ctx->timing is on; resolved by
 // timing_collect() after the stream is synchronised.

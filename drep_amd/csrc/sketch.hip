@@ -720,10 +720,18 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
     if ((rc = scratch(ctx, "sk_gl", n * 4ull, (void **)&d_gl))) return rc;
     if ((rc = scratch(ctx, "sk_st", n * 1ull, (void **)&d_st))) return rc;
     if ((rc = scratch(ctx, "sk_sets", (uint64_t)n * slots * 8ull, (void **)&d_sets))) return rc;
+    // first-round thresholds and genome list: device copies cached with the tile table
+    uint64_t *d_thr0;
+    uint32_t *d_gl0;
+    uint8_t *h_st;                                     // pinned: the per-round status readback
+    if ((rc = scratch(ctx, "sk_thr0", n * 8ull, (void **)&d_thr0))) return rc;
+    if ((rc = scratch(ctx, "sk_gl0", n * 4ull, (void **)&d_gl0))) return rc;
+    if ((rc = pinned_host(ctx, "sk_status", n, (void **)&h_st))) return rc;
 
     const bool cached = ctx->sk_gen == ctx->alloc_gen && ctx->sk_off.size() == n &&
                         !memcmp(ctx->sk_off.data(), base_off, n * 8ull) &&
-                        !memcmp(ctx->sk_pad.data(), padded, n * 8ull);
+                        !memcmp(ctx->sk_pad.data(), padded, n * 8ull) &&
+                        !memcmp(ctx->sk_nk.data(), nkmers, n * 8ull);
     if (!cached) {
         std::vector<uint64_t> tbase(ntiles);
         std::vector<uint32_t> tgen(ntiles);
@@ -732,27 +740,31 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
                 tbase[t] = base_off[g] + (t - tfirst[g]) * kTile;
                 tgen[t] = g;
             }
+        std::vector<uint32_t> glist(n);
+        for (uint32_t g = 0; g < n; g++) glist[g] = g;
         ctx->sk_gen = 0;
         HIPC(hipMemcpyAsync(d_tb, tbase.data(), ntiles * 8ull, hipMemcpyHostToDevice, st));
         HIPC(hipMemcpyAsync(d_tg, tgen.data(), ntiles * 4ull, hipMemcpyHostToDevice, st));
+        HIPC(hipMemcpyAsync(d_thr0, T.data(), n * 8ull, hipMemcpyHostToDevice, st));
+        HIPC(hipMemcpyAsync(d_gl0, glist.data(), n * 4ull, hipMemcpyHostToDevice, st));
         HIPC(hipStreamSynchronize(st));                // host vectors die here
         ctx->sk_off.assign(base_off, base_off + n);
         ctx->sk_pad.assign(padded, padded + n);
+        ctx->sk_nk.assign(nkmers, nkmers + n);
         ctx->sk_gen = ctx->alloc_gen;
     }
-    HIPC(hipMemcpyAsync(d_thr, T.data(), n * 8ull, hipMemcpyHostToDevice, st));
     HIPC(hipMemsetAsync(d_sets, 0xFF, (uint64_t)n * slots * 8ull, st));
     HIPC(hipMemsetAsync(d_cnt, 0, n * 4ull, st));
-    std::vector<uint32_t> glist(n);
-    for (uint32_t g = 0; g < n; g++) glist[g] = g;
-    HIPC(hipMemcpyAsync(d_gl, glist.data(), n * 4ull, hipMemcpyHostToDevice, st));
 
-    std::vector<uint8_t> status(n);
-    std::vector<uint32_t> todo = glist;
+    uint8_t *status = h_st;
+    std::vector<uint32_t> todo(n);
+    for (uint32_t g = 0; g < n; g++) todo[g] = g;
     bool first = true;
     for (int round = 0; round < 130 && !todo.empty(); round++) {
         const uint32_t *tb_tiles_g = d_tg;
         const uint64_t *tb_tiles_b = d_tb;
+        const uint64_t *thr_p = first ? d_thr0 : d_thr;   // round 0 reads the cached first-round values
+        const uint32_t *gl_p = first ? d_gl0 : d_gl;
         uint32_t nt = ntiles;
         if (!first) {
             // subset: reset sets of the retried genomes, gather their tiles
@@ -781,27 +793,27 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
                 const uint32_t *tbg = tb_tiles_g + t0;
                 if (ctx->sketch_kernel == 5)
                     hipLaunchKernelGGL((k_sketch_hash21_v5<kLaneBases, 8>), dim3(ntc), dim3(kTile / kLaneBases), 0, st,
-                                       d_codes, d_valid, tbb, tbg, d_thr, d_sets, d_cnt, plan.set_log2, limit,
+                                       d_codes, d_valid, tbb, tbg, thr_p, d_sets, d_cnt, plan.set_log2, limit,
                                        ctx->seed, wlast);
                 else if (ctx->sketch_kernel == 6)      // A/B: 4 k-mers per admit test
                     hipLaunchKernelGGL((k_sketch_hash21_v5<kLaneBases, 4>), dim3(ntc), dim3(kTile / kLaneBases), 0, st,
-                                       d_codes, d_valid, tbb, tbg, d_thr, d_sets, d_cnt, plan.set_log2, limit,
+                                       d_codes, d_valid, tbb, tbg, thr_p, d_sets, d_cnt, plan.set_log2, limit,
                                        ctx->seed, wlast);
                 else if (ctx->sketch_kernel == 7)      // A/B: 64 window ends per lane, 512-lane workgroups
                     hipLaunchKernelGGL((k_sketch_hash21_v5<kLaneBases / 2, 8>), dim3(ntc),
-                                       dim3(kTile / (kLaneBases / 2)), 0, st, d_codes, d_valid, tbb, tbg, d_thr,
+                                       dim3(kTile / (kLaneBases / 2)), 0, st, d_codes, d_valid, tbb, tbg, thr_p,
                                        d_sets, d_cnt, plan.set_log2, limit, ctx->seed, wlast);
                 else if (ctx->sketch_kernel == 8)      // A/B: 256 window ends per lane, 128-lane workgroups
                     hipLaunchKernelGGL((k_sketch_hash21_v5<kLaneBases * 2, 8>), dim3(ntc),
-                                       dim3(kTile / (kLaneBases * 2)), 0, st, d_codes, d_valid, tbb, tbg, d_thr,
+                                       dim3(kTile / (kLaneBases * 2)), 0, st, d_codes, d_valid, tbb, tbg, thr_p,
                                        d_sets, d_cnt, plan.set_log2, limit, ctx->seed, wlast);
                 else if (ctx->sketch_kernel != 3)
                     hipLaunchKernelGGL((k_sketch_hash21_v4<kLaneBases, 8>), dim3(ntc), dim3(kTile / kLaneBases), 0, st,
-                                       d_codes, d_valid, tbb, tbg, d_thr, d_sets, d_cnt, plan.set_log2, limit,
+                                       d_codes, d_valid, tbb, tbg, thr_p, d_sets, d_cnt, plan.set_log2, limit,
                                        ctx->seed, wlast);
                 else
                     hipLaunchKernelGGL((k_sketch_hash21_v3<kLaneBases, 8>), dim3(ntc), dim3(kTile / kLaneBases), 0, st,
-                                       d_codes, d_valid, tbb, tbg, d_thr, d_sets, d_cnt, plan.set_log2, limit,
+                                       d_codes, d_valid, tbb, tbg, thr_p, d_sets, d_cnt, plan.set_log2, limit,
                                        ctx->seed);
             }
             timing_mark(ctx, 0, st, false);
@@ -809,13 +821,13 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
         timing_mark(ctx, 1, st, true);
         if (plan.maxc <= 4096)
             hipLaunchKernelGGL(k_sketch_finalize<4096>, dim3((uint32_t)todo.size()), dim3(1024), 0, st,
-                               d_sets, d_cnt, d_thr, d_gl, plan.set_log2, plan.maxc, s, d_hashes, d_nhash, d_st);
+                               d_sets, d_cnt, thr_p, gl_p, plan.set_log2, plan.maxc, s, d_hashes, d_nhash, d_st);
         else
             hipLaunchKernelGGL(k_sketch_finalize<16384>, dim3((uint32_t)todo.size()), dim3(1024), 0, st,
-                               d_sets, d_cnt, d_thr, d_gl, plan.set_log2, plan.maxc, s, d_hashes, d_nhash, d_st);
+                               d_sets, d_cnt, thr_p, gl_p, plan.set_log2, plan.maxc, s, d_hashes, d_nhash, d_st);
         timing_mark(ctx, 1, st, false);
         HIPC(hipGetLastError());
-        HIPC(hipMemcpyAsync(status.data(), d_st, n, hipMemcpyDeviceToHost, st));
+        HIPC(hipMemcpyAsync(status, d_st, n, hipMemcpyDeviceToHost, st));
         HIPC(hipStreamSynchronize(st));
         first = false;
         if (getenv("DREPHIP_DEBUG")) {
