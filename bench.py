@@ -75,6 +75,10 @@ def parse():
     ap.add_argument("--seed", type=int, default=0xD2E9)
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the C oracle on host cores (rank 0)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_sketch_traffic.json"))
+    ap.add_argument("--verify", type=int, default=0,
+                    help="after timing, every rank re-sketches all genomes and recomputes the whole "
+                         "triangle on its own GPU and checks its gathered sketches and its segment "
+                         "(rehearsal of the sharded path; untimed)")
     return ap.parse_args()
 
 
@@ -133,11 +137,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", 0))
     import torch
     import torch.distributed as dist
+    # one rank per GPU; ranks beyond the visible GPUs wrap (only for rehearsing
+    # the multi-rank path on a smaller box, with DREPHIP_DIST_BACKEND=gloo)
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("DREPHIP_DIST_BACKEND", "nccl")          # nccl = RCCL over xGMI
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     from drep_amd import _lib
-    from drep_amd.parallel import genome_shard, row_partition, segment_size, gather_sketches
+    from drep_amd.parallel import cond_start, genome_shard, row_partition, segment_size, gather_sketches
 
     N, L, s = args.genomes, args.genome_bp, args.sketch
     ctx = _lib.Context(device=local, k=21, s=s, seed=42)
@@ -169,6 +180,8 @@ def main():
     stage = {"sketch": 0.0, "gather": 0.0, "dist": 0.0}
     kms = {0: [0.0, 0], 1: [0.0, 0], 2: [0.0, 0], 3: [0.0, 0]}
 
+    ev = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+
     def step(record):
         t0 = time.perf_counter()
         if nloc:
@@ -181,8 +194,11 @@ def main():
                     kms[w][1] += n
         t1 = time.perf_counter()
         if world > 1:
-            hh, nn = gather_sketches(loc_h, loc_n)     # RCCL over xGMI
-            torch.cuda.synchronize()
+            # RCCL over xGMI on torch's stream; the all-pairs call below is queued
+            # on the same stream, so no host sync in between (events time it)
+            ev[0].record()
+            hh, nn = gather_sketches(loc_h, loc_n)
+            ev[1].record()
         else:
             hh, nn = loc_h, loc_n
         t2 = time.perf_counter()
@@ -195,9 +211,12 @@ def main():
                     kms[w][1] += n
         t3 = time.perf_counter()
         if record:
+            if world > 1:
+                ev[1].synchronize()
+            g = ev[0].elapsed_time(ev[1]) / 1e3 if world > 1 else 0.0
             stage["sketch"] += t1 - t0
-            stage["gather"] += t2 - t1
-            stage["dist"] += t3 - t2
+            stage["gather"] += g
+            stage["dist"] += t3 - t2 - (g if world > 1 else 0.0)
 
     for _ in range(args.warmup):
         step(False)
@@ -276,6 +295,32 @@ def main():
     host_seg = d_common.cpu()
     d2h_ms = (time.perf_counter() - t0) * 1e3
 
+    verified = None
+    if args.verify:
+        # the sharded result against this GPU doing the whole job alone
+        tot = tile + N * P
+        codes_a = torch.zeros(tot // 16, dtype=torch.int32, device=dev)
+        valid_a = torch.zeros(tot // 32, dtype=torch.int32, device=dev)
+        ctx.synth_device(args.seed, 0, N, args.family_size, L, codes_a.data_ptr(), valid_a.data_ptr(), stream)
+        full_h = torch.full((N, s), -1, dtype=torch.int64, device=dev)
+        full_n = torch.zeros(N, dtype=torch.int32, device=dev)
+        ctx.sketch_device(codes_a.data_ptr(), valid_a.data_ptr(), np.array([tile + i * P for i in range(N)], np.uint64),
+                          np.full(N, P, np.uint64), np.full(N, L - 20, np.uint64), N,
+                          full_h.data_ptr(), full_n.data_ptr(), stream)
+        full_c = torch.zeros(max(N * (N - 1) // 2, 1), dtype=torch.int16, device=dev)
+        ctx.allpairs_device(full_h.data_ptr(), full_n.data_ptr(), N, 0, N, full_c.data_ptr(), None, stream)
+        torch.cuda.synchronize()
+        hh, nn = (gather_sketches(loc_h, loc_n) if world > 1 else (loc_h, loc_n))
+        a = cond_start(r0, N)
+        ok = (torch.equal(hh[:N], full_h) and torch.equal(nn[:N], full_n) and
+              torch.equal(d_common[:seg], full_c[a:a + seg]))
+        if world > 1:
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            ok = bool(flag.item())
+        verified = bool(ok)
+        del codes_a, valid_a, full_h, full_n, full_c
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
@@ -345,6 +390,8 @@ def main():
             },
             "cpu_baseline": cpu,
         }
+        if verified is not None:
+            out["verified_against_single_gpu"] = verified
         print(json.dumps(out))
     ctx.close()
     if world > 1:

@@ -63,15 +63,20 @@ def segment_size(N: int, r0: int, r1: int) -> int:
 def gather_sketches(local_h, local_n, group=None):
     """All-gather equal-size sketch shards (torch tensors on the process's
     device: int64 [nmax, s] viewed as uint64, int32 [nmax]).  Returns the
-    gathered [world*nmax, s] and [world*nmax] tensors; rows >= N are padding."""
+    gathered [world*nmax, s] and [world*nmax] tensors; rows >= N are padding.
+    One all-gather (RCCL over xGMI with the nccl backend) of [nmax, s+1]."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    all_h = torch.empty((world * local_h.shape[0],) + tuple(local_h.shape[1:]),
-                        dtype=local_h.dtype, device=local_h.device)
-    all_n = torch.empty(world * local_n.shape[0], dtype=local_n.dtype, device=local_n.device)
-    dist.all_gather_into_tensor(all_h, local_h.contiguous(), group=group)
-    dist.all_gather_into_tensor(all_n, local_n.contiguous(), group=group)
+    nmax, s = local_h.shape
+    # one collective: the count rides along as an extra int64 column
+    packed = torch.empty((nmax, s + 1), dtype=torch.int64, device=local_h.device)
+    packed[:, :s] = local_h
+    packed[:, s] = local_n.to(torch.int64)
+    gathered = torch.empty((world * nmax, s + 1), dtype=torch.int64, device=local_h.device)
+    dist.all_gather_into_tensor(gathered, packed, group=group)
+    all_h = gathered[:, :s].contiguous()
+    all_n = gathered[:, s].to(local_n.dtype).contiguous()
     return all_h, all_n
 
 
