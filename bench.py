@@ -40,7 +40,7 @@ N_SIMD = 256 * 4
 # does not cover are priced as v_xor (its v_cndmask figure is a VCC-hazard
 # artefact of the microbench loop and is not used)
 MICROBENCH = os.path.join(ROOT, "profiles", "r01_valu_microbench.json")
-SKETCH_DEFAULT_VARIANT = "5"   # must match drephip_ctx::sketch_kernel default (ctx.h)
+SKETCH_DEFAULT_VARIANT = "9"   # must match drephip_ctx::sketch_kernel default (ctx.h)
 # committed PMC summaries (tools/pmc_summary.py): VALU / LDS utilisation of the
 # two kernels, reported next to the live timings
 SKETCH_PMC = os.path.join(ROOT, "profiles", "r01_sketch_pmc_sq.json")

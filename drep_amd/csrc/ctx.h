@@ -22,7 +22,7 @@ struct drephip_ctx {
     bool timing = false;
     int ap_path = 0;          // DREPHIP_AP_*: 0 auto (table for s <= 2048, else band)
     uint32_t band_cap = 1024; // elements per row per band of the banded all-pairs kernel (clamped to its LDS budget)
-    int sketch_kernel = 5;    // 5 = v4 + body tables (default), 4 = table-driven v4, 3 = rolled-window v3; env DREPHIP_SKETCH_KERNEL (A/B)
+    int sketch_kernel = 9;    // 9 = v5 with split TT tables (default), 5 = v4 + body tables, 4 = table-driven v4, 3 = rolled-window v3; env DREPHIP_SKETCH_KERNEL (A/B)
     // named grow-only device scratch buffers
     std::map<std::string, DevBuf> bufs;
     // per-kernel timing of the last call: {sum ms, launches}

@@ -438,26 +438,72 @@ __device__ void build_tables5(SketchTables5 &tb, uint32_t tid, uint32_t nthreads
     }
 }
 
+// v6 layout (A/B): the 64-bit TT tables split into 32-bit halves so that TA,
+// lo(TT) and hi(TT) of one block word are read from ONE address (byte * 4)
+// with three offsets -- two index adds fewer per k-mer, two LDS reads more.
+struct SketchTables6 {
+    uint32_t tt1lo[256], tt1hi[256], ta1[256];
+    uint32_t tt2lo[256], tt2hi[256], ta2[256];
+    uint32_t tb1[256], tb2[256];
+    uint64_t t3[1024];
+};
+__device__ void build_tables(SketchTables5 &tb, uint32_t tid, uint32_t nthreads) { build_tables5(tb, tid, nthreads); }
+__device__ void build_tables(SketchTables6 &tb, uint32_t tid, uint32_t nthreads) {
+    constexpr uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
+    for (uint32_t x = tid; x < 256; x += nthreads) {
+        const uint32_t a = ascii4(x);
+        const uint64_t A1 = (uint64_t)a * c1, A2 = (uint64_t)a * c2;
+        const uint32_t x1 = (uint32_t)A1, x2 = (uint32_t)A2;
+        const uint64_t t1 = ((uint64_t)x1 << 31) * c2;
+        const uint64_t t2 = ((uint64_t)(x2 & 0x7fffffffu) << 33) * c1 + (uint64_t)(x2 >> 31) * c1;
+        tb.tt1lo[x] = (uint32_t)t1; tb.tt1hi[x] = (uint32_t)(t1 >> 32); tb.ta1[x] = (uint32_t)(A1 >> 32);
+        tb.tt2lo[x] = (uint32_t)t2; tb.tt2hi[x] = (uint32_t)(t2 >> 32); tb.ta2[x] = (uint32_t)(A2 >> 32);
+        tb.tb1[x] = a * (uint32_t)c1;
+        tb.tb2[x] = a * (uint32_t)c2;
+    }
+    for (uint32_t y = tid; y < 1024; y += nthreads) {
+        const uint64_t k3 = (uint64_t)ascii4(y >> 2) | ((uint64_t)ascii4((y & 3u) << 6) & 0xffu) << 32;
+        tb.t3[y] = (rotl64_ab(k3 * c1, 31) * c2) ^ 21u;
+    }
+}
+__device__ __forceinline__ void tab_k1(const SketchTables5 &tb, uint32_t x, uint32_t &ta, uint64_t &tt) {
+    ta = tb.ta1[x]; tt = tb.tt1[x];
+}
+__device__ __forceinline__ void tab_k2(const SketchTables5 &tb, uint32_t x, uint32_t &ta, uint64_t &tt) {
+    ta = tb.ta2[x]; tt = tb.tt2[x];
+}
+__device__ __forceinline__ void tab_k1(const SketchTables6 &tb, uint32_t x, uint32_t &ta, uint64_t &tt) {
+    ta = tb.ta1[x]; tt = ((uint64_t)tb.tt1hi[x] << 32) | tb.tt1lo[x];
+}
+__device__ __forceinline__ void tab_k2(const SketchTables6 &tb, uint32_t x, uint32_t &ta, uint64_t &tt) {
+    ta = tb.ta2[x]; tt = ((uint64_t)tb.tt2hi[x] << 32) | tb.tt2lo[x];
+}
+
 __device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {   // one v_mad_u64_u32
     return (uint64_t)a * b + c;
 }
 
-__device__ __forceinline__ void murmur21_tab5(const SketchTables5 &tb, uint32_t hi, uint32_t lo, uint32_t seed,
+template <class TB>
+__device__ __forceinline__ void murmur21_tab5(const TB &tb, uint32_t hi, uint32_t lo, uint32_t seed,
                                               uint64_t &p1, uint64_t &p2) {
     constexpr uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
     constexpr uint64_t d1 = c1 * 2;                                  // 2 c1 mod 2^64
     const uint32_t x = hi >> 24, xp = (hi >> 8) & 0xffu;
-    const uint32_t X1 = tb.ta1[x] + tb.tb1[(hi >> 16) & 0xffu];        // hi(k1 * c1)
-    const uint32_t X2 = tb.ta2[xp] + tb.tb2[hi & 0xffu];               // hi(k2 * c2)
+    uint32_t ta1, ta2;
+    uint64_t tt1, tt2;
+    tab_k1(tb, x, ta1, tt1);
+    tab_k2(tb, xp, ta2, tt2);
+    const uint32_t X1 = ta1 + tb.tb1[(hi >> 16) & 0xffu];              // hi(k1 * c1)
+    const uint32_t X2 = ta2 + tb.tb2[hi & 0xffu];                      // hi(k2 * c2)
     const uint64_t k3 = tb.t3[lo >> 22];
     // rotl(k1 c1, 31) c2 ^ seed
     const uint32_t h = X1 >> 1;
-    const uint64_t P1 = mad64(h, (uint32_t)c2, tb.tt1[x]);
+    const uint64_t P1 = mad64(h, (uint32_t)c2, tt1);
     const uint32_t g1hi = (uint32_t)(P1 >> 32) + h * (uint32_t)(c2 >> 32) + (X1 << 31);
     uint64_t h1 = ((uint64_t)g1hi << 32) | ((uint32_t)P1 ^ seed);
     h1 = x5_plus(rotl64_ab(h1, 27), 5ull * seed + 0x52dce729);   // (rotl + seed) * 5 + c
     // rotl(k2 c2, 33) c1 ^ seed
-    const uint64_t P2 = mad64(X2, (uint32_t)d1, tb.tt2[xp]);
+    const uint64_t P2 = mad64(X2, (uint32_t)d1, tt2);
     const uint32_t g2hi = (uint32_t)(P2 >> 32) + X2 * (uint32_t)(d1 >> 32);
     uint64_t h2 = ((uint64_t)g2hi << 32) | ((uint32_t)P2 ^ seed);
     h2 = x5_plus(add64(rotl64_ab(h2, 31), h1), 0x38495ab5);
@@ -469,7 +515,7 @@ __device__ __forceinline__ void murmur21_tab5(const SketchTables5 &tb, uint32_t 
     p2 = fmix64_pre(h2);
 }
 
-template <int LANE, int BATCH>
+template <int LANE, int BATCH, class TB = SketchTables5>
 __global__ __launch_bounds__(kTile / LANE) void k_sketch_hash21_v5(
     const uint32_t *__restrict__ codes, const uint32_t *__restrict__ valid,
     const uint64_t *__restrict__ tile_base, const uint32_t *__restrict__ tile_genome,
@@ -477,7 +523,7 @@ __global__ __launch_bounds__(kTile / LANE) void k_sketch_hash21_v5(
     uint32_t *__restrict__ cnt, uint32_t set_log2, uint32_t limit, uint32_t seed, uint64_t wlast) {
     constexpr uint32_t WG = kTile / LANE;
     constexpr int NCH = LANE / 16;
-    __shared__ SketchTables5 tb;
+    __shared__ TB tb;
     __shared__ uint64_t stage[kStage];
     __shared__ uint32_t nstage;
     const uint32_t t = blockIdx.x;
@@ -490,7 +536,7 @@ __global__ __launch_bounds__(kTile / LANE) void k_sketch_hash21_v5(
     unsigned long long *S = sets + ((uint64_t)g << set_log2);
     uint32_t *C = cnt + g;
     if (threadIdx.x == 0) nstage = 0;
-    build_tables5(tb, threadIdx.x, WG);
+    build_tables(tb, threadIdx.x, WG);
 
     const uint64_t m0 = start / 16;
     auto ld = [&](int j) -> uint32_t {
@@ -795,6 +841,10 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
                     hipLaunchKernelGGL((k_sketch_hash21_v5<kLaneBases, 8>), dim3(ntc), dim3(kTile / kLaneBases), 0, st,
                                        d_codes, d_valid, tbb, tbg, thr_p, d_sets, d_cnt, plan.set_log2, limit,
                                        ctx->seed, wlast);
+                else if (ctx->sketch_kernel == 9)      // A/B: split 32-bit TT tables (SketchTables6)
+                    hipLaunchKernelGGL((k_sketch_hash21_v5<kLaneBases, 8, SketchTables6>), dim3(ntc),
+                                       dim3(kTile / kLaneBases), 0, st, d_codes, d_valid, tbb, tbg, thr_p, d_sets,
+                                       d_cnt, plan.set_log2, limit, ctx->seed, wlast);
                 else if (ctx->sketch_kernel == 6)      // A/B: 4 k-mers per admit test
                     hipLaunchKernelGGL((k_sketch_hash21_v5<kLaneBases, 4>), dim3(ntc), dim3(kTile / kLaneBases), 0, st,
                                        d_codes, d_valid, tbb, tbg, thr_p, d_sets, d_cnt, plan.set_log2, limit,

@@ -109,7 +109,7 @@ def test_sketch_sizes_vs_oracle(s):
         assert np.array_equal(h[g, :nh[g]], want)
 
 
-@pytest.mark.parametrize("variant", ["3", "4", "5"])
+@pytest.mark.parametrize("variant", ["3", "4", "5", "9"])
 def test_sketch_kernel_variants_vs_oracle(variant, monkeypatch):
     """Every hash-kernel variant (DREPHIP_SKETCH_KERNEL, read at context
     creation; 5 is the default) gives the oracle's sketches, including

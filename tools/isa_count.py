@@ -11,7 +11,10 @@ import subprocess
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = {"3": ("k_sketch_hash21_v3", 8), "4": ("k_sketch_hash21_v4", 8), "5": ("k_sketch_hash21_v5", 8)}   # variant: (name, k-mers/block)
+# variant: (mangled-name pattern, k-mers/block)
+KERNELS = {"3": ("k_sketch_hash21_v3", 8), "4": ("k_sketch_hash21_v4", 8),
+           "5": ("k_sketch_hash21_v5ILi128ELi8ENS_13SketchTables5E", 8),
+           "9": ("k_sketch_hash21_v5ILi128ELi8ENS_13SketchTables6E", 8)}
 
 
 def main():
@@ -45,8 +48,10 @@ def main():
             for k, v in b.items():
                 if k.startswith("v_"):
                     mix[k] += v
+        label = {"5": "k_sketch_hash21_v5<128,8,SketchTables5>",
+                 "9": "k_sketch_hash21_v5<128,8,SketchTables6>"}.get(var, name)
         out["variants"][var] = {
-            "kernel": name, "kmers_per_block": per, "blocks": len(hot),
+            "kernel": label, "kmers_per_block": per, "blocks": len(hot),
             "valu_per_kmer": sum(valu) / len(hot) / per,
             "mul_per_kmer": sum(mul) / len(hot) / per,
             "lds_reads_per_kmer": sum(lds) / len(hot) / per,
