@@ -240,21 +240,20 @@ DREPHIP_EXPORT int drephip_fasta_pack(const char *path, int k, uint32_t *codes, 
 }
 
 // Stage a packed genome set (already laid out on the host) and sketch it.
-static int sketch_packed_host(drephip_ctx *ctx, const std::vector<uint32_t> &codes,
-                              const std::vector<uint32_t> &valid, const std::vector<uint64_t> &off,
-                              const std::vector<uint64_t> &pad, const std::vector<uint64_t> &nk,
-                              uint64_t *hashes_out, uint32_t *nhash_out) {
+static int sketch_packed_host(drephip_ctx *ctx, const uint32_t *codes, uint64_t n_codes, const uint32_t *valid,
+                              uint64_t n_valid, const std::vector<uint64_t> &off, const std::vector<uint64_t> &pad,
+                              const std::vector<uint64_t> &nk, uint64_t *hashes_out, uint32_t *nhash_out) {
     const uint32_t n = (uint32_t)off.size();
     hipStream_t st = ctx->stream;
     uint32_t *d_codes, *d_valid, *d_nhash;
     uint64_t *d_hashes;
     int rc;
-    if ((rc = scratch(ctx, "in_codes", codes.size() * 4, (void **)&d_codes))) return rc;
-    if ((rc = scratch(ctx, "in_valid", valid.size() * 4, (void **)&d_valid))) return rc;
+    if ((rc = scratch(ctx, "in_codes", n_codes * 4, (void **)&d_codes))) return rc;
+    if ((rc = scratch(ctx, "in_valid", n_valid * 4, (void **)&d_valid))) return rc;
     if ((rc = scratch(ctx, "out_hashes", (uint64_t)n * ctx->s * 8, (void **)&d_hashes))) return rc;
     if ((rc = scratch(ctx, "out_nhash", n * 4ull, (void **)&d_nhash))) return rc;
-    HIPC(hipMemcpyAsync(d_codes, codes.data(), codes.size() * 4, hipMemcpyHostToDevice, st));
-    HIPC(hipMemcpyAsync(d_valid, valid.data(), valid.size() * 4, hipMemcpyHostToDevice, st));
+    HIPC(hipMemcpyAsync(d_codes, codes, n_codes * 4, hipMemcpyHostToDevice, st));
+    HIPC(hipMemcpyAsync(d_valid, valid, n_valid * 4, hipMemcpyHostToDevice, st));
     timing_begin(ctx);
     rc = sketch_device_impl(ctx, d_codes, d_valid, off.data(), pad.data(), nk.data(), n, d_hashes, d_nhash, st);
     if (rc) return rc;
@@ -311,7 +310,8 @@ DREPHIP_EXPORT int drephip_sketch(drephip_ctx *ctx, const uint8_t *seq, const ui
         nk[g] = pack_records(seq + (r1 > r0 ? rec_off[r0] : 0), reclen.data() + r0, (uint32_t)(r1 - r0),
                              ctx->k, codes.data(), valid.data(), off[g]);
     });
-    return sketch_packed_host(ctx, codes, valid, off, pad, nk, hashes_out, nhash_out);
+    return sketch_packed_host(ctx, codes.data(), codes.size(), valid.data(), valid.size(), off, pad, nk, hashes_out,
+                              nhash_out);
 }
 
 DREPHIP_EXPORT int drephip_sketch_files(drephip_ctx *ctx, const char *const *paths, uint32_t n_genomes,
@@ -350,14 +350,23 @@ DREPHIP_EXPORT int drephip_sketch_files(drephip_ctx *ctx, const char *const *pat
             cur += pad[i];
             if (length_out) length_out[g0 + i] = gs[i].length;
         }
-        std::vector<uint32_t> codes(cur / 16, 0), valid(cur / 32, 0);
+        // packed batch in pinned host memory (DMA'd without staging); every
+        // thread zeroes and packs its own genomes' slots
+        uint32_t *codes, *valid;
+        int rc;
+        if ((rc = pinned_host(ctx, "in_codes_h", cur / 16 * 4, (void **)&codes))) return rc;
+        if ((rc = pinned_host(ctx, "in_valid_h", cur / 32 * 4, (void **)&valid))) return rc;
+        memset(codes, 0, kTile / 16 * 4);
+        memset(valid, 0, kTile / 32 * 4);
         parallel_for(n, threads, [&](uint32_t i) {
+            memset(codes + off[i] / 16, 0, pad[i] / 16 * 4);
+            memset(valid + off[i] / 32, 0, pad[i] / 32 * 4);
             nk[i] = pack_records(gs[i].seq.data(), gs[i].rec_len.data(), (uint32_t)gs[i].rec_len.size(),
-                                 ctx->k, codes.data(), valid.data(), off[i]);
+                                 ctx->k, codes, valid, off[i]);
         });
         gs.clear();
-        const int rc = sketch_packed_host(ctx, codes, valid, off, pad, nk,
-                                          hashes_out + (uint64_t)g0 * ctx->s, nhash_out + g0);
+        rc = sketch_packed_host(ctx, codes, cur / 16, valid, cur / 32, off, pad, nk,
+                                hashes_out + (uint64_t)g0 * ctx->s, nhash_out + g0);
         if (rc) return rc;
         g0 = g1;
     }

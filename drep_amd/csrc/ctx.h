@@ -5,6 +5,8 @@
 
 #include <hip/hip_runtime.h>
 #include <map>
+#include <memory>
+#include <utility>
 #include <string>
 #include <vector>
 
@@ -86,8 +88,19 @@ int dist_matrix_impl(drephip_ctx *ctx, const uint16_t *d_common, const uint16_t 
 int dist_from_condensed_impl(drephip_ctx *ctx, const double *y, uint32_t n, double **d_D_out, hipStream_t st);
 
 // Host ingest (ingest.cpp).
+// std::allocator that leaves new elements uninitialised (resize() without the
+// memset: the FASTA reader writes every byte it keeps)
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    template <class U> struct rebind { using other = NoInitAlloc<U>; };
+    NoInitAlloc() = default;
+    template <class U> NoInitAlloc(const NoInitAlloc<U> &) {}
+    template <class U> void construct(U *) noexcept {}
+    template <class U, class... A> void construct(U *p, A &&...a) { ::new ((void *)p) U(std::forward<A>(a)...); }
+};
+
 struct Genome {
-    std::vector<uint8_t> seq;        // concatenated record bytes (raw case)
+    std::vector<uint8_t, NoInitAlloc<uint8_t>> seq;   // concatenated record bytes (raw case)
     std::vector<uint64_t> rec_len;   // record lengths
     uint64_t length = 0;             // sum of record lengths
 };

@@ -10,67 +10,132 @@
 //
 // Speed: the file is read in 4 MiB blocks, lines are found with memchr and
 // sequence lines appended with memcpy; packing builds each 32-base group
-// (two code words + one validity word) in registers from a byte LUT and
-// stores it once.
+// (two code words + one validity word) with SSE2 compares and BMI2 pext (a
+// byte LUT for the partial groups at record ends) and stores it once.
 #include "ctx.h"
 
 #include <zlib.h>
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <immintrin.h>
 
 namespace drephip {
+
+// 64-bit mask of the '\n' bytes among p[0..63] (SSE2)
+__attribute__((target("sse2"))) static inline uint64_t newline_mask64(const char *p) {
+    const __m128i nl = _mm_set1_epi8('\n');
+    uint64_t m = 0;
+#pragma GCC unroll 4
+    for (int h = 0; h < 4; h++)
+        m |= (uint64_t)(uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_loadu_si128((const __m128i *)(p + 16 * h)), nl))
+             << (16 * h);
+    return m;
+}
 
 int read_fasta(const char *path, Genome &g) {
     gzFile f = gzopen(path, "rb");
     if (!f) { set_error(std::string("cannot open ") + path); return -1; }
     gzbuffer(f, 1 << 20);
     g.seq.clear(); g.rec_len.clear(); g.length = 0;
-    if (FILE *fp = fopen(path, "rb")) {          // capacity hint: file size (x4 if gzip)
+    // the sequence buffer is sized once (file size; x4 if gzip) and written
+    // through a cursor, then trimmed at the end
+    size_t used = 0;
+    if (FILE *fp = fopen(path, "rb")) {
         fseek(fp, 0, SEEK_END);
         const long sz = ftell(fp);
         fclose(fp);
-        if (sz > 0) g.seq.reserve((size_t)sz * (gzdirect(f) ? 1 : 4));
+        if (sz > 0) g.seq.resize((size_t)sz * (gzdirect(f) ? 1 : 4));
     }
-    const size_t kBlock = 4u << 20;
-    std::vector<char> buf(kBlock + 1);
-    std::string carry;                    // partial line spanning blocks
-    bool in_seq = false;                  // inside a record's sequence lines
-
-    auto line = [&](const char *p, size_t n) {
-        if (n && p[n - 1] == '\r') n--;
-        if (n == 0) return;
-        const char c0 = p[0];
-        if (c0 == '>' || c0 == '@') { g.rec_len.push_back(0); in_seq = true; return; }
-        if (c0 == '+') { in_seq = false; return; }
-        if (!in_seq) return;
-        const size_t old = g.seq.size();
-        g.seq.resize(old + n);
-        memcpy(g.seq.data() + old, p, n);
+    auto append = [&](const char *p, size_t n) {
+        if (used + n > g.seq.size()) g.seq.resize(std::max(used + n, 2 * g.seq.size() + 64));
+        memcpy(g.seq.data() + used, p, n);
+        used += n;
         g.rec_len.back() += n;
     };
+    auto end_seq_line = [&] {                      // a line-final '\r' is dropped
+        if (used && g.seq[used - 1] == '\r' && g.rec_len.back()) { used--; g.rec_len.back()--; }
+    };
+    // Line state machine, carried across blocks: START (first byte of a line),
+    // SEQ (inside a sequence line: copied in 64-byte chunks up to the newline),
+    // SKIP (header / '+' / text outside a record: skipped to the newline).
+    enum { START, SEQ, SKIP } st = START;
+    bool in_seq = false;
+    const size_t kBlock = 4u << 20;
+    static thread_local std::vector<char> buf(kBlock + 64);   // reused across files (no 4 MiB memset each)
     for (;;) {
         const int got = gzread(f, buf.data(), (unsigned)kBlock);
         if (got < 0) { gzclose(f); set_error(std::string("read error in ") + path); return -1; }
         if (got == 0) break;
         const char *p = buf.data(), *end = p + got;
-        if (!carry.empty()) {
-            const char *nl = (const char *)memchr(p, '\n', end - p);
-            if (!nl) { carry.append(p, end - p); continue; }
-            carry.append(p, nl - p);
-            line(carry.data(), carry.size());
-            carry.clear();
-            p = nl + 1;
-        }
         while (p < end) {
-            const char *nl = (const char *)memchr(p, '\n', end - p);
-            if (!nl) { carry.assign(p, end - p); break; }
-            line(p, nl - p);
-            p = nl + 1;
+            if (st == START) {
+                const char c = *p;
+                if (c == '\n') { p++; continue; }                                     // empty line
+                if (c == '>' || c == '@') { g.rec_len.push_back(0); in_seq = true; st = SKIP; continue; }
+                if (c == '+') { in_seq = false; st = SKIP; continue; }
+                st = in_seq ? SEQ : SKIP;
+                continue;
+            }
+            if (st == SKIP) {
+                const char *nl = (const char *)memchr(p, '\n', end - p);
+                if (!nl) { p = end; break; }
+                p = nl + 1;
+                st = START;
+                continue;
+            }
+            // SEQ: 64-byte chunks; every sequence line inside a chunk is
+            // compacted with a fixed 64-byte copy (the output cursor advances by
+            // the line's length, later copies overwrite the excess); a line that
+            // starts with '>', '@' or '+' hands over to START
+            while (end - p >= 64) {
+                uint64_t m = newline_mask64(p);
+                if (used + 128 > g.seq.size()) g.seq.resize(std::max(used + 128, 2 * g.seq.size()));
+                uint8_t *out = g.seq.data();
+                int pos = 0;
+                bool handover = false;
+                while (m) {
+                    const int j = __builtin_ctzll(m);
+                    memcpy(out + used, p + pos, 64);
+                    used += (size_t)(j - pos);
+                    g.rec_len.back() += (uint64_t)(j - pos);
+                    // line-final '\r': inside this segment, or (newline first in
+                    // a chunk that continues a line) at the end of the previous one
+                    const bool cr = j > pos ? p[j - 1] == '\r' : (j == 0 && used && out[used - 1] == '\r');
+                    if (cr && g.rec_len.back()) { used--; g.rec_len.back()--; }
+                    pos = j + 1;
+                    m &= m - 1;
+                    if (pos < 64) {
+                        const char c = p[pos];
+                        if (c == '>' || c == '@' || c == '+') { handover = true; break; }
+                    } else {
+                        break;
+                    }
+                }
+                if (handover || pos == 64) {                // next byte starts a line
+                    p += pos;
+                    st = START;
+                    goto next_state;
+                }
+                memcpy(out + used, p + pos, 64);            // rest of the chunk: inside a sequence line
+                used += (size_t)(64 - pos);
+                g.rec_len.back() += (uint64_t)(64 - pos);
+                p += 64;
+            }
+            {
+                const char *nl = (const char *)memchr(p, '\n', end - p);
+                if (!nl) { append(p, end - p); p = end; break; }
+                append(p, nl - p);
+                p = nl + 1;
+            }
+            end_seq_line();
+            st = START;
+        next_state:;
         }
     }
-    if (!carry.empty()) line(carry.data(), carry.size());
+    if (st == SEQ) end_seq_line();
     gzclose(f);
+    g.seq.resize(used);
     for (uint64_t l : g.rec_len) g.length += l;
     return 0;
 }
@@ -94,6 +159,46 @@ static const uint8_t *code_lut() {
     return lut;
 }
 
+// 32 bases -> 64 code bits + 32 validity bits with SSE2 (+ BMI2 pext when the
+// host has it).  Codes: ((c >> 1) ^ (c >> 2)) & 3 maps A/C/G/T and a/c/g/t to
+// 0/1/2/3 (bits 1..3 of each byte; 16-bit shifts leak nothing into bits 0..1
+// of a byte); valid: (c & 0xDF) is one of 'A','C','G','T'; invalid bytes get
+// code 0, as in the scalar path.
+static inline uint64_t gather2_swar(uint64_t c) {      // 8 bytes of 2-bit values -> 16 bits
+    uint64_t t = (c | (c >> 6)) & 0x000F000F000F000Full;
+    t = (t | (t >> 12)) & 0x000000FF000000FFull;
+    return (t | (t >> 24)) & 0xFFFFull;
+}
+__attribute__((target("bmi2"))) static inline uint64_t gather2_pext(uint64_t c) {
+    return _pext_u64(c, 0x0303030303030303ull);
+}
+template <bool PEXT>
+__attribute__((target("sse2,bmi2"))) static inline void pack32(const uint8_t *s, uint64_t &codes, uint32_t &valid) {
+    const __m128i m3 = _mm_set1_epi8(3), mDF = _mm_set1_epi8((char)0xDF);
+    const __m128i A = _mm_set1_epi8('A'), Cc = _mm_set1_epi8('C'), G = _mm_set1_epi8('G'), T = _mm_set1_epi8('T');
+    uint64_t out = 0;
+    uint32_t vm = 0;
+#pragma GCC unroll 2
+    for (int h = 0; h < 2; h++) {
+        const __m128i v = _mm_loadu_si128((const __m128i *)(s + 16 * h));
+        const __m128i u = _mm_and_si128(v, mDF);
+        const __m128i ok = _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(u, A), _mm_cmpeq_epi8(u, Cc)),
+                                        _mm_or_si128(_mm_cmpeq_epi8(u, G), _mm_cmpeq_epi8(u, T)));
+        vm |= (uint32_t)_mm_movemask_epi8(ok) << (16 * h);
+        const __m128i c = _mm_and_si128(_mm_and_si128(_mm_xor_si128(_mm_srli_epi16(v, 1), _mm_srli_epi16(v, 2)), m3),
+                                        ok);                            // invalid bases: code 0 (layout contract)
+        const uint64_t lo = (uint64_t)_mm_cvtsi128_si64(c), hi = (uint64_t)_mm_cvtsi128_si64(_mm_unpackhi_epi64(c, c));
+        const uint64_t g = PEXT ? (gather2_pext(lo) | gather2_pext(hi) << 16) : (gather2_swar(lo) | gather2_swar(hi) << 16);
+        out |= g << (32 * h);
+    }
+    codes = out;
+    valid = vm;
+}
+static bool host_has_bmi2() {
+    static const bool b = __builtin_cpu_supports("bmi2");
+    return b;
+}
+
 // Mask of positions (bits) ending a run of >= k set bits in `v` (k <= 32),
 // by doubling: a1 = v, a2 = a1 & a1<<1, a4, a8, a16, then the binary digits of
 // k combined at growing offsets.
@@ -111,6 +216,7 @@ static inline uint64_t run_k_mask(uint64_t v, int k) {
 // Pack n bytes of one record starting at base position pos (any alignment).
 // Whole 32-base groups are built in registers; partial groups at either end
 // are OR-ed into the (zeroed) arrays.  Returns the valid k-mers ending in it.
+template <bool PEXT>
 static uint64_t pack_span(const uint8_t *s, uint64_t n, uint64_t pos, int k, const uint8_t *lut,
                           uint32_t *codes, uint32_t *valid) {
     uint64_t hist = 0;                  // validity of the previous group (bits 0..31)
@@ -123,12 +229,7 @@ static uint64_t pack_span(const uint8_t *s, uint64_t n, uint64_t pos, int k, con
         uint64_t clo = 0;
         uint32_t vw = 0;
         if (take == 32) {
-#pragma GCC unroll 32
-            for (uint32_t t = 0; t < 32; t++) {
-                const uint32_t c = lut[s[i + t]];
-                clo |= (uint64_t)(c & 3u) << (2 * t);
-                vw |= ((c >> 2) ^ 1u) << t;
-            }
+            pack32<PEXT>(s + i, clo, vw);
         } else {
             for (uint32_t t = 0; t < take; t++) {
                 const uint32_t c = lut[s[i + t]];
@@ -154,8 +255,10 @@ uint64_t pack_records(const uint8_t *seq, const uint64_t *rec_len, uint32_t n_re
     const uint8_t *lut = code_lut();
     uint64_t pos = base_off, nk = 0;
     const uint8_t *s = seq;
+    const bool pext = host_has_bmi2();
     for (uint32_t r = 0; r < n_rec; r++) {
-        nk += pack_span(s, rec_len[r], pos, k, lut, codes, valid);
+        nk += pext ? pack_span<true>(s, rec_len[r], pos, k, lut, codes, valid)
+                   : pack_span<false>(s, rec_len[r], pos, k, lut, codes, valid);
         s += rec_len[r];
         pos += rec_len[r] + 1;          // one invalid separator between records
     }

@@ -245,6 +245,62 @@ def test_fasta_pack_matches_numpy_layout(tmp_path, golden):
         assert length.value == sum(len(r) for r in recs_o)
 
 
+def _messy_fasta(rng, n_rec, big):
+    """FASTA bytes with kseq corner cases, and the records kseq reads from it:
+    random line lengths (1-300, so sequence lines straddle the reader's
+    64-byte chunks and 4 MiB blocks), CRLF on some lines, blank lines,
+    lowercase, N/IUPAC bytes, '\r' inside lines, long headers, text before the
+    first header, FASTQ records whose '+' line ends the sequence."""
+    A = np.frombuffer(b"ACGTacgtNRYKM", dtype=np.uint8)
+    out, recs = [b"preamble text\n\n"], []
+    for r in range(n_rec):
+        L = int(rng.integers(0, 3_000_000 if big else 20_000))
+        seq = A[rng.integers(0, len(A), L)].copy()
+        seq[rng.random(L) < 1e-4] = ord("\r")                  # '\r' inside a line is a (bad) base
+        fastq = r % 5 == 4
+        out.append((b"@" if fastq else b">") + b"rec%d " % r + b"x" * int(rng.integers(0, 500)) + b"\n")
+        kept, i = [], 0
+        while i < L:
+            w = int(rng.integers(1, 301))
+            line = seq[i:i + w].tobytes()
+            i += w
+            if line.endswith(b"\r"):                              # would be eaten as CRLF
+                line = line[:-1] + b"A"
+            kept.append(line)
+            out.append(line + (b"\r\n" if rng.random() < 0.2 else b"\n"))
+            if rng.random() < 0.02:
+                out.append(b"\n")
+        if fastq:
+            out.append(b"+\n" + b"I" * len(b"".join(kept)) + b"\n")
+        recs.append(np.frombuffer(b"".join(kept), dtype=np.uint8))
+    return b"".join(out), recs
+
+
+@pytest.mark.parametrize("seed,n_rec,big", [(1, 12, False), (2, 40, False), (3, 4, True)])
+def test_fasta_reader_and_packer_on_messy_files(tmp_path, seed, n_rec, big):
+    """The SIMD FASTA reader + packer (drephip_fasta_pack) against a direct
+    restatement of kseq's rules and the numpy layout, plain and gzip."""
+    import ctypes as C
+    import gzip
+    rng = np.random.default_rng(seed)
+    txt, recs = _messy_fasta(rng, n_rec, big)
+    tile = _lib.tile_bases()
+    P, want_c, want_v = _np_pack(recs, tile)
+    L = _lib.lib()
+    for name, data in (("m.fa", txt), ("m.fa.gz", gzip.compress(txt, 1))):
+        path = tmp_path / name
+        path.write_bytes(data)
+        codes = np.zeros((tile + P) // 16, np.uint32)
+        valid = np.zeros((tile + P) // 32, np.uint32)
+        length = C.c_uint64(0)
+        nk = C.c_uint64(0)
+        rc = L.drephip_fasta_pack(str(path).encode(), 21, codes, valid, tile, tile + P, C.byref(length), C.byref(nk))
+        assert rc == 0, name
+        assert length.value == sum(len(r) for r in recs), name
+        assert np.array_equal(codes[tile // 16:], want_c), name
+        assert np.array_equal(valid[tile // 32:], want_v), name
+
+
 def test_device_list_and_balanced_shards(monkeypatch):
     """Multi-device drop-in plumbing (no GPU): the `gpus` kwarg forms and the
     byte-balanced contiguous genome shards."""
