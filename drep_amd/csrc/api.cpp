@@ -157,6 +157,7 @@ DREPHIP_EXPORT int drephip_create(int device, int k, uint32_t s, uint32_t seed, 
     if (!c) { set_error("out of host memory"); return DREPHIP_ERR_NOMEM; }
     c->device = device; c->k = k; c->s = s; c->seed = seed;
     if (const char *v = getenv("DREPHIP_SKETCH_KERNEL")) c->sketch_kernel = atoi(v);
+    if (const char *v = getenv("DREPHIP_FINALIZE")) c->finalize_kernel = atoi(v);
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) { delete c; set_error(hipGetErrorString(e)); return DREPHIP_ERR_HIP; }
     *out = c;

@@ -24,6 +24,7 @@ struct drephip_ctx {
     bool timing = false;
     int ap_path = 0;          // DREPHIP_AP_*: 0 auto (table for s <= 2048, else band)
     uint32_t band_cap = 1024; // elements per row per band of the banded all-pairs kernel (clamped to its LDS budget)
+    int finalize_kernel = 1;  // 1 = bucket sort (default), 0 = bitonic sort (A/B); env DREPHIP_FINALIZE
     int sketch_kernel = 9;    // 9 = v5 with split TT tables (default), 5 = v4 + body tables, 4 = table-driven v4, 3 = rolled-window v3; env DREPHIP_SKETCH_KERNEL (A/B)
     // named grow-only device scratch buffers
     std::map<std::string, DevBuf> bufs;

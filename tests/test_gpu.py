@@ -134,6 +134,29 @@ def test_sketch_kernel_variants_vs_oracle(variant, monkeypatch):
     assert nh[1] < S
 
 
+@pytest.mark.parametrize("finalize", ["0", "1"])
+@pytest.mark.parametrize("s", [1, 1000, 12000])
+def test_sketch_finalize_variants_vs_oracle(finalize, s, monkeypatch):
+    """Both finalize kernels (DREPHIP_FINALIZE: 1 bucket sort, the default; 0
+    bitonic sort) give the oracle's sketches: full and partial sketches, the
+    4096- and 16384-candidate instantiations, and a low-complexity genome whose
+    candidates crowd few buckets."""
+    monkeypatch.setenv("DREPHIP_FINALIZE", finalize)
+    rng = np.random.default_rng(100 + s)
+    A = np.frombuffer(b"ACGT", dtype=np.uint8)
+    motif = A[rng.integers(0, 4, 40)]
+    recs = [A[rng.integers(0, 4, 400_000)], A[rng.integers(0, 4, 5000)],
+            np.tile(motif, 2000) if s > 1 else A[rng.integers(0, 4, 30)]]
+    seq = np.concatenate(recs)
+    rec_off = np.concatenate([[0], np.cumsum([len(r) for r in recs])]).astype(np.uint64)
+    gro = np.arange(len(recs) + 1, dtype=np.uint64)
+    with _lib.Context(0, 21, s, 42) as ctx:
+        h, nh, _ = ctx.sketch_records(seq, rec_off, gro)
+    for g in range(len(recs)):
+        want = oracle.sketch_records(recs[g], np.array([0, len(recs[g])], np.uint64), 21, s, 42)
+        assert nh[g] == len(want) and np.array_equal(h[g, :nh[g]], want), g
+
+
 def test_synth_device_matches_oracle_generator(ctx1000):
     """The bench's on-device generator + device sketch == oracle generator +
     oracle sketch (5 Mbp genomes, the BASELINE genome size)."""
