@@ -228,8 +228,11 @@ class Context:
                 "drephip_linkage_counts_device")
         return Z
 
-    def set_timing(self, on: bool = True) -> None:
-        check(lib().drephip_set_timing(self._h, 1 if on else 0), "drephip_set_timing")
+    def set_timing(self, on: bool = True, kernels=None) -> None:
+        """HIP-event timing of kernel launches: all kernels, or only the
+        `which` indices in `kernels` (see kernel_ms)."""
+        mask = 0 if not on else (-1 if kernels is None else sum(1 << int(w) for w in kernels))
+        check(lib().drephip_set_timing(self._h, mask), "drephip_set_timing")
 
     def kernel_ms(self, which: int):
         ms = C.c_double(0)

@@ -84,7 +84,7 @@ static hipEvent_t next_event(drephip_ctx *ctx) {
 }
 
 void timing_mark(drephip_ctx *ctx, int which, hipStream_t st, bool start) {
-    if (!ctx->timing) return;
+    if (!((ctx->timing >> which) & 1u)) return;
     hipEvent_t e = next_event(ctx);
     if (!e) return;
     (void)hipEventRecord(e, st);
@@ -176,9 +176,9 @@ DREPHIP_EXPORT int drephip_destroy(drephip_ctx *ctx) {
     return DREPHIP_OK;
 }
 
-DREPHIP_EXPORT int drephip_set_timing(drephip_ctx *ctx, int enable) {
+DREPHIP_EXPORT int drephip_set_timing(drephip_ctx *ctx, int kernels) {
     if (!ctx) { set_error("null context"); return DREPHIP_ERR_ARG; }
-    ctx->timing = enable != 0;
+    ctx->timing = (uint32_t)kernels & 0xFu;
     return DREPHIP_OK;
 }
 

@@ -21,7 +21,7 @@ struct drephip_ctx {
     uint32_t s = 1000;
     uint32_t seed = 42;
     hipStream_t stream = nullptr;
-    bool timing = false;
+    uint32_t timing = 0;      // bitmask of timed kernels (bit w = `which` w of drephip_last_kernel_ms)
     int ap_path = 0;          // DREPHIP_AP_*: 0 auto (table for s <= 2048, else band)
     uint32_t band_cap = 1024; // elements per row per band of the banded all-pairs kernel (clamped to its LDS budget)
     int finalize_kernel = 1;  // 1 = bucket sort (default), 0 = bitonic sort (A/B); env DREPHIP_FINALIZE
@@ -39,6 +39,12 @@ struct drephip_ctx {
     // sketch tile table of the last call (reused while the genome layout is the
     // same and no scratch buffer has been reallocated since: sk_gen == alloc_gen)
     std::vector<uint64_t> sk_off, sk_pad, sk_nk;
+    // candidate sets / counts known to be empty / zero: the first sk_clean_n
+    // genomes' slots of these buffers (every finalize resets what it read)
+    unsigned long long *sk_clean_sets = nullptr;
+    uint32_t *sk_clean_cnt = nullptr;
+    uint32_t sk_clean_n = 0;
+    uint64_t sk_clean_gen = 0;   // alloc_gen when they were last left clean
     uint64_t sk_gen = 0;
     // pinned host staging for the small per-call readbacks (status, failure count)
     std::map<std::string, DevBuf> pinned;
@@ -65,7 +71,7 @@ int scratch(drephip_ctx *ctx, const char *name, size_t bytes, void **out);
 // Grow-only named pinned host buffer (hipHostMalloc) for async readbacks.
 int pinned_host(drephip_ctx *ctx, const char *name, size_t bytes, void **out);
 
-// Bracket kernel launches with events when ctx->timing is on; resolved by
+// Bracket kernel launches with events when their bit of ctx->timing is set; resolved by
 // timing_collect() after the stream is synchronised.
 void timing_begin(drephip_ctx *ctx);
 void timing_mark(drephip_ctx *ctx, int which, hipStream_t st, bool start);

@@ -613,9 +613,18 @@ __global__ __launch_bounds__(kTile / LANE) void k_sketch_hash21_v5(
 // ----------------------------------------------------------------- finalize
 enum : uint8_t { ST_OK = 0, ST_UP = 1, ST_DOWN = 2 };
 
+// Every finalize leaves the genome's candidate set empty and its count zero
+// (the slots it reads are reset as it goes; a genome sent back for another
+// round is reset whole), so the next call needs no memset of the sets.
+__device__ __forceinline__ void finalize_reset(unsigned long long *S, uint32_t slots, uint32_t *cnt_g) {
+    for (uint32_t i = threadIdx.x; i < slots; i += blockDim.x) S[i] = kEmpty;
+    __syncthreads();                                   // every thread has read *cnt_g
+    if (threadIdx.x == 0) *cnt_g = 0;
+}
+
 template <int MAXC>
 __global__ __launch_bounds__(1024) void k_sketch_finalize(
-    const unsigned long long *__restrict__ sets, const uint32_t *__restrict__ cnt,
+    unsigned long long *__restrict__ sets, uint32_t *__restrict__ cnt,
     const uint64_t *__restrict__ thr, const uint32_t *__restrict__ glist, uint32_t set_log2,
     uint32_t maxc, uint32_t s, uint64_t *__restrict__ out, uint32_t *__restrict__ nhash,
     uint8_t *__restrict__ status) {
@@ -624,15 +633,19 @@ __global__ __launch_bounds__(1024) void k_sketch_finalize(
     const uint32_t g = glist[blockIdx.x];
     const uint32_t n = cnt[g];
     const uint32_t tid = threadIdx.x;
-    if (n > maxc) { if (tid == 0) status[g] = ST_DOWN; return; }
-    if (n < s && thr[g] < kMaxThr) { if (tid == 0) status[g] = ST_UP; return; }
+    unsigned long long *S = sets + ((uint64_t)g << set_log2);
+    const uint32_t slots = 1u << set_log2;
+    if (n > maxc || (n < s && thr[g] < kMaxThr)) {
+        if (tid == 0) status[g] = n > maxc ? ST_DOWN : ST_UP;
+        finalize_reset(S, slots, cnt + g);
+        return;
+    }
     if (tid == 0) pos = 0;
     __syncthreads();
-    const unsigned long long *S = sets + ((uint64_t)g << set_log2);
-    const uint32_t slots = 1u << set_log2;
+    if (tid == 0) cnt[g] = 0;                          // every thread has read it
     for (uint32_t i = tid; i < slots; i += blockDim.x) {
         const uint64_t v = S[i];
-        if (v != kEmpty) buf[atomicAdd(&pos, 1u)] = v;
+        if (v != kEmpty) { buf[atomicAdd(&pos, 1u)] = v; S[i] = kEmpty; }
     }
     __syncthreads();
     uint32_t P = 1;
@@ -667,7 +680,7 @@ __global__ __launch_bounds__(1024) void k_sketch_finalize(
 // 105 barrier-separated stages.
 template <int MAXC, int NB>
 __global__ __launch_bounds__(1024) void k_sketch_finalize_bucket(
-    const unsigned long long *__restrict__ sets, const uint32_t *__restrict__ cnt,
+    unsigned long long *__restrict__ sets, uint32_t *__restrict__ cnt,
     const uint64_t *__restrict__ thr, const uint32_t *__restrict__ glist, uint32_t set_log2,
     uint32_t maxc, uint32_t s, uint64_t *__restrict__ out, uint32_t *__restrict__ nhash,
     uint8_t *__restrict__ status) {
@@ -680,14 +693,18 @@ __global__ __launch_bounds__(1024) void k_sketch_finalize_bucket(
     const uint32_t n = cnt[g];
     const uint32_t tid = threadIdx.x;
     const uint64_t T = thr[g];
-    if (n > maxc) { if (tid == 0) status[g] = ST_DOWN; return; }
-    if (n < s && T < kMaxThr) { if (tid == 0) status[g] = ST_UP; return; }
+    unsigned long long *S = sets + ((uint64_t)g << set_log2);
+    const uint32_t slots = 1u << set_log2;
+    if (n > maxc || (n < s && T < kMaxThr)) {
+        if (tid == 0) status[g] = n > maxc ? ST_DOWN : ST_UP;
+        finalize_reset(S, slots, cnt + g);
+        return;
+    }
     const uint32_t tbits = 64 - __builtin_clzll(T | 1);
     const uint32_t shift = tbits > LOGNB ? tbits - LOGNB : 0;
     for (uint32_t i = tid; i < NB; i += WG) bk[i] = 0;
     __syncthreads();
-    const unsigned long long *S = sets + ((uint64_t)g << set_log2);
-    const uint32_t slots = 1u << set_log2;
+    if (tid == 0) cnt[g] = 0;                          // every thread has read it
     for (uint32_t i = tid; i < slots; i += WG) {
         const uint64_t v = S[i];
         if (v != kEmpty) atomicAdd(&bk[min((uint32_t)(v >> shift), (uint32_t)NB - 1u)], 1u);
@@ -714,7 +731,10 @@ __global__ __launch_bounds__(1024) void k_sketch_finalize_bucket(
     __syncthreads();
     for (uint32_t i = tid; i < slots; i += WG) {
         const uint64_t v = S[i];
-        if (v != kEmpty) buf[atomicAdd(&bk[min((uint32_t)(v >> shift), (uint32_t)NB - 1u)], 1u)] = v;
+        if (v != kEmpty) {
+            buf[atomicAdd(&bk[min((uint32_t)(v >> shift), (uint32_t)NB - 1u)], 1u)] = v;
+            S[i] = kEmpty;
+        }
     }
     __syncthreads();
     // bk[b] is now the end of bucket b (= the start of bucket b + 1)
@@ -875,8 +895,15 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
         ctx->sk_nk.assign(nkmers, nkmers + n);
         ctx->sk_gen = ctx->alloc_gen;
     }
-    HIPC(hipMemsetAsync(d_sets, 0xFF, (uint64_t)n * slots * 8ull, st));
-    HIPC(hipMemsetAsync(d_cnt, 0, n * 4ull, st));
+    // sets and counts: finalize leaves them empty, so only the part not known
+    // to be clean (new buffers, more genomes than before, a failed call) is reset
+    const uint32_t clean = (ctx->sk_clean_gen == ctx->alloc_gen && ctx->sk_clean_sets == d_sets &&
+                            ctx->sk_clean_cnt == d_cnt) ? ctx->sk_clean_n : 0;
+    ctx->sk_clean_n = 0;                               // dirty until this call completes
+    if (n > clean) {
+        HIPC(hipMemsetAsync(d_sets + (uint64_t)clean * slots, 0xFF, (uint64_t)(n - clean) * slots * 8ull, st));
+        HIPC(hipMemsetAsync(d_cnt + clean, 0, (n - clean) * 4ull, st));
+    }
 
     uint8_t *status = h_st;
     std::vector<uint32_t> todo(n);
@@ -992,6 +1019,10 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
         todo.swap(next);
     }
     if (!todo.empty()) { set_error("sketch did not converge"); return DREPHIP_ERR_INTERNAL; }
+    ctx->sk_clean_gen = ctx->alloc_gen;
+    ctx->sk_clean_sets = d_sets;
+    ctx->sk_clean_cnt = d_cnt;
+    ctx->sk_clean_n = std::max(clean, n);
     return DREPHIP_OK;
 }
 

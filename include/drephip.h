@@ -204,8 +204,11 @@ int drephip_linkage_counts_device(drephip_ctx *ctx, const uint16_t *d_common, co
                                   uint32_t n, const uint32_t *perm, const double *lut, uint32_t lut_len,
                                   const int32_t *lut_off, int method, double *Z /* (n-1)*4 */);
 
-/* Enable (1) / disable (0) HIP-event timing of every kernel launch. */
-int drephip_set_timing(drephip_ctx *ctx, int enable);
+/* HIP-event timing of kernel launches: `kernels` is a bitmask of the kernels
+ * to bracket with events (bit w = `which` w of drephip_last_kernel_ms; -1 =
+ * all, 0 = none).  Each event pair adds a few microseconds of idle time
+ * between dispatches, so a benchmark times only the kernel it reports. */
+int drephip_set_timing(drephip_ctx *ctx, int kernels);
 
 /* Per-launch timing of the last sketch/allpairs call on this context
  * (milliseconds, from HIP events on the launch stream): which = 0 sketch hash
