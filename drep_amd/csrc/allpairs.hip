@@ -104,18 +104,33 @@ __device__ __forceinline__ bool cuckoo_has32(const uint32_t *T, uint32_t stride,
     return ok1 || ok2;
 }
 
-// One table per row g in [row0, row0 + gridDim.x): 2H words to tabs.
-__global__ __launch_bounds__(256) void k_build_q32(const uint64_t *__restrict__ hashes,
+// One table per row g = row0 + blockIdx.x, written straight into the LDS
+// image of its row group (R consecutive rows, `stride` words per group): the
+// 2H slot words interleaved with the group's other rows (slot k of row r at
+// k*R + r), then the row's s high words at R*2H + r*s.  The main kernel copies
+// a group's image into LDS with 16-byte loads.  Rows past row1 (padding of the
+// last group) get empty slots.
+__global__ __launch_bounds__(1024) void k_build_q32(const uint64_t *__restrict__ hashes,
                                                    const uint32_t *__restrict__ nhash, uint32_t s,
-                                                   uint32_t row0, uint32_t B, uint32_t *__restrict__ tabs,
+                                                   uint32_t row0, uint32_t row1, uint32_t B, uint32_t R,
+                                                   uint32_t *__restrict__ blk, uint32_t stride,
                                                    uint8_t *__restrict__ fam_out, uint32_t *__restrict__ nfail) {
     extern __shared__ uint32_t Tb[];
     __shared__ int fail;
     const uint32_t H = 1u << B, hm = H - 1;
     const uint32_t r = blockIdx.x;
     const uint32_t g = row0 + r;
+    uint32_t *img = blk + (uint64_t)(r / R) * stride;
+    const uint32_t rr = r % R;
+    if (g >= row1) {
+        for (uint32_t i = threadIdx.x; i < 2 * H; i += blockDim.x) img[i * R + rr] = kEmpty32;
+        for (uint32_t i = threadIdx.x; i < s; i += blockDim.x) img[2 * H * R + rr * s + i] = 0;
+        if (threadIdx.x == 0) fam_out[r] = 0;
+        return;
+    }
     const uint32_t n = nhash[g];
     const uint64_t *A = hashes + (uint64_t)g * s;
+    for (uint32_t i = threadIdx.x; i < s; i += blockDim.x) img[2 * H * R + rr * s + i] = (uint32_t)(A[i] >> 32);
     for (uint32_t fam = 0; fam < kMaxFam; fam++) {
         const QFields q = qfields(fam);
         for (uint32_t i = threadIdx.x; i < 2 * H; i += blockDim.x) Tb[i] = kEmpty32;
@@ -128,8 +143,7 @@ __global__ __launch_bounds__(256) void k_build_q32(const uint64_t *__restrict__ 
             if (!cuckoo_has32(Tb, 1, 0, H, hm, q, (uint32_t)A[i], i)) fail = 1;
         __syncthreads();
         if (!fail) {
-            uint32_t *o = tabs + (uint64_t)r * 2 * H;
-            for (uint32_t i = threadIdx.x; i < 2 * H; i += blockDim.x) o[i] = Tb[i];
+            for (uint32_t i = threadIdx.x; i < 2 * H; i += blockDim.x) img[i * R + rr] = Tb[i];
             if (threadIdx.x == 0) fam_out[r] = (uint8_t)fam;
             return;
         }
@@ -339,7 +353,7 @@ __host__ __device__ constexpr size_t q_lds_bytes(uint32_t R, uint32_t TS, uint32
 template <int R, int NCH, int MINW>
 __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
     const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ nhash,
-    const uint32_t *__restrict__ tabs, const uint8_t *__restrict__ fam, uint32_t s, uint32_t N,
+    const uint32_t *__restrict__ blk, uint32_t stride, const uint8_t *__restrict__ fam, uint32_t s, uint32_t N,
     uint32_t row0, uint32_t row1, uint32_t B, const uint2 *__restrict__ items, uint32_t ncol_item,
     uint16_t *__restrict__ common, uint16_t *__restrict__ denom, uint64_t seg0) {
     constexpr int WG = kApWG;
@@ -353,13 +367,17 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
     const uint32_t nrows = min((uint32_t)R, row1 - i0);
     const uint32_t cend = min(c0 + ncol_item, N);
     const uint32_t tid = threadIdx.x, wave = tid >> 6;
-    for (uint32_t k = tid; k < TS; k += WG) {
-#pragma unroll
-        for (int r = 0; r < R; r++)
-            T[k * R + r] = (uint32_t)r < nrows ? tabs[(uint64_t)(i0 - row0 + r) * TS + k] : kEmpty32;
+    {   // the row group's LDS image (k_build_q32): 16-byte loads, four in flight per lane
+        const uint4 *src = (const uint4 *)(blk + (uint64_t)((i0 - row0) / R) * stride);
+        uint4 *dst = (uint4 *)lds;
+        const uint32_t n16 = stride / 4;
+        uint32_t i = tid;
+        for (; i + 3 * WG < n16; i += 4 * WG) {
+            const uint4 a = src[i], b = src[i + WG], c = src[i + 2 * WG], d = src[i + 3 * WG];
+            dst[i] = a; dst[i + WG] = b; dst[i + 2 * WG] = c; dst[i + 3 * WG] = d;
+        }
+        for (; i < n16; i += WG) dst[i] = src[i];
     }
-    for (uint32_t r = 0; r < nrows; r++)
-        for (uint32_t i = tid; i < s; i += WG) V[r * s + i] = (uint32_t)(hashes[(uint64_t)(i0 + r) * s + i] >> 32);
     uint32_t nA[R], o1[R], o2[R];
     uint64_t alast[R];
     bool any_partial_row = false, fast = true;
@@ -795,7 +813,7 @@ static int launch_band(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_
 
 template <int R, int NCH, int MINW>
 static int launch_q(drephip_ctx *ctx, uint32_t nitems, size_t lds, hipStream_t st, const uint64_t *h,
-                    const uint32_t *nh, const uint32_t *tabs, const uint8_t *fam, uint32_t N, uint32_t row0,
+                    const uint32_t *nh, const uint32_t *blk, uint32_t stride, const uint8_t *fam, uint32_t N, uint32_t row0,
                     uint32_t row1, uint32_t B, const uint2 *items, uint32_t C, uint16_t *cm, uint16_t *dn,
                     uint64_t seg0) {
     HIPC(hipFuncSetAttribute((const void *)k_allpairs_q<R, NCH, MINW>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -803,7 +821,7 @@ static int launch_q(drephip_ctx *ctx, uint32_t nitems, size_t lds, hipStream_t s
     timing_mark(ctx, 2, st, true);
     for (uint32_t i0 = 0; i0 < nitems; i0 += (uint32_t)max_blocks(kApWG))
         hipLaunchKernelGGL((k_allpairs_q<R, NCH, MINW>), dim3(std::min<uint32_t>(nitems - i0, (uint32_t)max_blocks(kApWG))),
-                           dim3(kApWG), lds, st, h, nh, tabs, fam, ctx->s, N, row0, row1, B, items + i0, C, cm, dn,
+                           dim3(kApWG), lds, st, h, nh, blk, stride, fam, ctx->s, N, row0, row1, B, items + i0, C, cm, dn,
                            seg0);
     timing_mark(ctx, 2, st, false);
     HIPC(hipGetLastError());
@@ -837,28 +855,31 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
     if (path == DREPHIP_AP_BAND)
         return launch_band(ctx, d_hashes, d_nhash, N, row0, row1, seg0, npairs, d_common, d_denom, st);
 
+    // rows per workgroup: the most (8, 4, 2, 1) whose tables + high words fit
+    static const uint32_t kR[] = {8, 4, 2, 1};
+    uint32_t R = 1;
+    for (uint32_t r : kR) if (q_lds_bytes(r, TS, s) + 16 <= kLdsBudget) { R = r; break; }
+
+    // row-group LDS images (tables + high words), built once per call
     const uint32_t nrows = row1 - row0;
-    uint32_t *d_tabs;
+    const uint32_t ngroups = (nrows + R - 1) / R;
+    const uint32_t stride = (uint32_t)((q_lds_bytes(R, TS, s) / 4 + 3) & ~3ull);   // words, 16-B multiple
+    uint32_t *d_blk;
     uint8_t *d_fam;
     uint32_t *d_nfail;
     uint2 *d_items;
     int rc;
-    if ((rc = scratch(ctx, "ap_tabs", (uint64_t)nrows * TS * 4, (void **)&d_tabs))) return rc;
-    if ((rc = scratch(ctx, "ap_fam", nrows, (void **)&d_fam))) return rc;
+    if ((rc = scratch(ctx, "ap_blk", (uint64_t)ngroups * stride * 4, (void **)&d_blk))) return rc;
+    if ((rc = scratch(ctx, "ap_fam", (uint64_t)ngroups * R, (void **)&d_fam))) return rc;
     if ((rc = scratch(ctx, "ap_nfail", 4, (void **)&d_nfail))) return rc;
     HIPC(hipMemsetAsync(d_nfail, 0, 4, st));
     const size_t blds = (size_t)TS * 4;
     HIPC(hipFuncSetAttribute((const void *)k_build_q32, hipFuncAttributeMaxDynamicSharedMemorySize, (int)blds));
     timing_mark(ctx, 3, st, true);
-    hipLaunchKernelGGL(k_build_q32, dim3(nrows), dim3(256), blds, st, d_hashes, d_nhash, s, row0, B, d_tabs, d_fam,
-                       d_nfail);
+    hipLaunchKernelGGL(k_build_q32, dim3(ngroups * R), dim3(1024), blds, st, d_hashes, d_nhash, s, row0, row1, B, R,
+                       d_blk, stride, d_fam, d_nfail);
     timing_mark(ctx, 3, st, false);
     HIPC(hipGetLastError());
-
-    // rows per workgroup: the most (8, 4, 2, 1) whose tables + high words fit
-    static const uint32_t kR[] = {8, 4, 2, 1};
-    uint32_t R = 1;
-    for (uint32_t r : kR) if (q_lds_bytes(r, TS, s) <= kLdsBudget) { R = r; break; }
     // column tile: the widest (<= kApCols) whose item count still gives every
     // workgroup slot of the chip (256 CUs x 2) about four items; small
     // problems (a rank's shard on 8 GPUs, N ~ 10^3) get narrower items
@@ -893,12 +914,12 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
     // in the (never observed) case of a row with no working field family its
     // output is discarded and the merge kernel recomputes the segment
 
-    const size_t lds = q_lds_bytes(R, TS, s);
+    const size_t lds = (size_t)stride * 4;
     const uint32_t nch = (s + 63) / 64;
     // two workgroups per CU when the LDS allows (DREPHIP_AP_ONEWG=1: one, A/B)
     const bool two = lds <= 80 * 1024 && !getenv("DREPHIP_AP_ONEWG");
-#define DREPHIP_Q(RR, NC) (two ? launch_q<RR, NC, 8>(ctx, ni, lds, st, d_hashes, d_nhash, d_tabs, d_fam, N, row0, row1, B, d_items, C, d_common, d_denom, seg0) \
-                               : launch_q<RR, NC, 4>(ctx, ni, lds, st, d_hashes, d_nhash, d_tabs, d_fam, N, row0, row1, B, d_items, C, d_common, d_denom, seg0))
+#define DREPHIP_Q(RR, NC) (two ? launch_q<RR, NC, 8>(ctx, ni, lds, st, d_hashes, d_nhash, d_blk, stride, d_fam, N, row0, row1, B, d_items, C, d_common, d_denom, seg0) \
+                               : launch_q<RR, NC, 4>(ctx, ni, lds, st, d_hashes, d_nhash, d_blk, stride, d_fam, N, row0, row1, B, d_items, C, d_common, d_denom, seg0))
     if (nch <= 8) {
         switch (R) {
             case 8: rc = DREPHIP_Q(8, 8); break;
