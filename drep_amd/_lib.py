@@ -58,6 +58,8 @@ SIGNATURES = {
     "drephip_sketch": (C.c_int, [vp, u8p, u64p, C.c_uint32, u64p, C.c_uint32, u64p, u32p, u64p]),
     "drephip_sketch_files": (C.c_int, [vp, C.POINTER(C.c_char_p), C.c_uint32, C.c_int, u64p, u32p, u64p]),
     "drephip_sketch_device": (C.c_int, [vp, vp, vp, u64p, u64p, u64p, C.c_uint32, vp, vp, vp]),
+    "drephip_sketch_device_async": (C.c_int, [vp, vp, vp, u64p, u64p, u64p, C.c_uint32, vp, vp, vp]),
+    "drephip_sketch_wait": (C.c_int, [vp, C.POINTER(C.c_int)]),
     "drephip_synth_device": (C.c_int, [vp, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64,
                                        vp, vp, vp]),
     "drephip_allpairs": (C.c_int, [vp, u64p, u32p, C.c_uint32, u16p, vp]),
@@ -275,6 +277,23 @@ class Context:
                                           np.ascontiguousarray(padded, dtype=np.uint64),
                                           np.ascontiguousarray(nkmers, dtype=np.uint64), n,
                                           d_hashes, d_nhash, stream), "drephip_sketch_device")
+
+    def sketch_device_async(self, d_codes: int, d_valid: int, base_off, padded, nkmers, n: int,
+                            d_hashes: int, d_nhash: int, stream: Optional[int] = None) -> None:
+        """sketch_device without the wait: the sketches are final after
+        sketch_wait() (include/drephip.h)."""
+        check(lib().drephip_sketch_device_async(self._h, d_codes, d_valid,
+                                                np.ascontiguousarray(base_off, dtype=np.uint64),
+                                                np.ascontiguousarray(padded, dtype=np.uint64),
+                                                np.ascontiguousarray(nkmers, dtype=np.uint64), n,
+                                                d_hashes, d_nhash, stream), "drephip_sketch_device_async")
+
+    def sketch_wait(self) -> bool:
+        """Completes sketch_device_async; True if the sketches were recomputed
+        (results derived from them in between must be recomputed)."""
+        redone = C.c_int(0)
+        check(lib().drephip_sketch_wait(self._h, C.byref(redone)), "drephip_sketch_wait")
+        return bool(redone.value)
 
     def synth_device(self, seed: int, g0: int, n: int, family_size: int, L: int, d_codes: int,
                      d_valid: int, stream: Optional[int] = None) -> None:

@@ -120,6 +120,7 @@ using namespace drephip;
 // stream (also torch's default stream handle), exactly as in the HIP API, so
 // work is ordered after whatever the caller queued there.
 static hipStream_t pick_stream(drephip_ctx *, void *stream) { return (hipStream_t)stream; }
+static void pend_release(drephip_ctx *ctx);
 
 DREPHIP_EXPORT int drephip_version(void) { return 100; }
 
@@ -170,6 +171,7 @@ DREPHIP_EXPORT int drephip_destroy(drephip_ctx *ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     for (auto &kv : ctx->bufs) if (kv.second.ptr) (void)hipFree(kv.second.ptr);
     for (auto &kv : ctx->pinned) if (kv.second.ptr) (void)hipHostFree(kv.second.ptr);
+    pend_release(ctx);
     for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -255,6 +257,7 @@ static int sketch_packed_host(drephip_ctx *ctx, const uint32_t *codes, uint64_t 
     if ((rc = scratch(ctx, "out_nhash", n * 4ull, (void **)&d_nhash))) return rc;
     HIPC(hipMemcpyAsync(d_codes, codes, n_codes * 4, hipMemcpyHostToDevice, st));
     HIPC(hipMemcpyAsync(d_valid, valid, n_valid * 4, hipMemcpyHostToDevice, st));
+    pend_release(ctx);
     timing_begin(ctx);
     rc = sketch_device_impl(ctx, d_codes, d_valid, off.data(), pad.data(), nk.data(), n, d_hashes, d_nhash, st);
     if (rc) return rc;
@@ -384,11 +387,79 @@ DREPHIP_EXPORT int drephip_sketch_device(drephip_ctx *ctx, const uint32_t *d_cod
         set_error("null argument"); return DREPHIP_ERR_ARG;
     }
     hipStream_t st = pick_stream(ctx, stream);
+    pend_release(ctx);
     timing_begin(ctx);
     int rc = sketch_device_impl(ctx, d_codes, d_valid, h_base_off, h_padded, h_nkmers, n_genomes, d_hashes,
                                 d_nhash, st);
     if (rc) return rc;
     timing_collect(ctx);
+    return DREPHIP_OK;
+}
+
+// Drop a deferred sketch's bookkeeping: its timing events go back to the pool.
+static void pend_release(drephip_ctx *ctx) {
+    auto &p = ctx->pend;
+    for (hipEvent_t e : p.events) ctx->ev_pool.push_back(e);
+    p.events.clear();
+    p.spans.clear();
+    p.active = false;
+}
+
+DREPHIP_EXPORT int drephip_sketch_device_async(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t *d_valid,
+                                               const uint64_t *h_base_off, const uint64_t *h_padded,
+                                               const uint64_t *h_nkmers, uint32_t n_genomes, uint64_t *d_hashes,
+                                               uint32_t *d_nhash, void *stream) {
+    GUARD_CTX(ctx);
+    pend_release(ctx);                                 // an earlier call never waited on: forget it
+    if (n_genomes == 0) return DREPHIP_OK;
+    if (!d_codes || !d_valid || !h_base_off || !h_padded || !h_nkmers || !d_hashes || !d_nhash) {
+        set_error("null argument"); return DREPHIP_ERR_ARG;
+    }
+    hipStream_t st = pick_stream(ctx, stream);
+    timing_begin(ctx);
+    int rc = sketch_device_impl(ctx, d_codes, d_valid, h_base_off, h_padded, h_nkmers, n_genomes, d_hashes,
+                                d_nhash, st, true);
+    if (rc) { ctx->pend.active = false; return rc; }
+    // the queued kernels' events leave the pool until drephip_sketch_wait reads them
+    auto &p = ctx->pend;
+    p.spans.swap(ctx->spans);
+    p.events.assign(ctx->ev_pool.begin(), ctx->ev_pool.begin() + ctx->ev_used);
+    ctx->ev_pool.erase(ctx->ev_pool.begin(), ctx->ev_pool.begin() + ctx->ev_used);
+    ctx->ev_used = 0;
+    return DREPHIP_OK;
+}
+
+DREPHIP_EXPORT int drephip_sketch_wait(drephip_ctx *ctx, int *redone) {
+    GUARD_CTX(ctx);
+    if (redone) *redone = 0;
+    auto &p = ctx->pend;
+    if (!p.active) return DREPHIP_OK;
+    HIPC(hipStreamSynchronize(p.st));
+    double kms[2] = {0, 0};
+    int kn[2] = {0, 0};
+    for (auto &sp : p.spans) {
+        float ms = 0;
+        if (sp.a && sp.b && sp.which < 2 && hipEventElapsedTime(&ms, sp.a, sp.b) == hipSuccess) {
+            kms[sp.which] += ms;
+            kn[sp.which] += 1;
+        }
+    }
+    bool ok = true;
+    for (uint32_t g = 0; g < p.n; g++) ok &= p.h_status[g] == 0;   // ST_OK
+    pend_release(ctx);
+    if (ok) {
+        for (int w = 0; w < 2; w++) { ctx->kms[w] = kms[w]; ctx->kn[w] = kn[w]; }
+        return DREPHIP_OK;
+    }
+    // a genome needs another threshold round: rerun the whole call synchronously
+    // (finalize left every set empty, so this starts from a clean state)
+    const auto off = p.off, pad = p.pad, nk = p.nk;
+    timing_begin(ctx);
+    int rc = sketch_device_impl(ctx, p.d_codes, p.d_valid, off.data(), pad.data(), nk.data(), p.n, p.d_hashes,
+                                p.d_nhash, p.st);
+    if (rc) return rc;
+    timing_collect(ctx);
+    if (redone) *redone = 1;
     return DREPHIP_OK;
 }
 

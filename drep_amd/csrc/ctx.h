@@ -52,6 +52,21 @@ struct drephip_ctx {
     uint64_t ap_items_key[5] = {0, 0, 0, 0, 0};
     uint64_t ap_items_gen = 0;
     uint32_t ap_items_n = 0;
+    // deferred sketch (drephip_sketch_device_async): the first round is queued
+    // without reading its status back; drephip_sketch_wait checks it (and
+    // reruns the call synchronously if a genome needs another threshold round)
+    struct PendingSketch {
+        bool active = false;
+        const uint32_t *d_codes = nullptr, *d_valid = nullptr;
+        std::vector<uint64_t> off, pad, nk;
+        uint32_t n = 0;
+        uint64_t *d_hashes = nullptr;
+        uint32_t *d_nhash = nullptr;
+        hipStream_t st = nullptr;
+        const uint8_t *h_status = nullptr;     // pinned, written by the queued copy
+        std::vector<Span> spans;               // timing spans of the queued kernels
+        std::vector<hipEvent_t> events;        // their events, out of ev_pool until collected
+    } pend;
 };
 
 namespace drephip {
@@ -80,7 +95,8 @@ void timing_collect(drephip_ctx *ctx);
 // Kernel drivers (sketch.hip / allpairs.hip).
 int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t *d_valid,
                        const uint64_t *base_off, const uint64_t *padded, const uint64_t *nkmers,
-                       uint32_t n, uint64_t *d_hashes, uint32_t *d_nhash, hipStream_t st);
+                       uint32_t n, uint64_t *d_hashes, uint32_t *d_nhash, hipStream_t st,
+                       bool defer = false);
 int synth_device_impl(drephip_ctx *ctx, uint64_t seed, uint32_t g0, uint32_t n, uint32_t family_size,
                       uint64_t L, uint32_t *d_codes, uint32_t *d_valid, hipStream_t st);
 int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash,

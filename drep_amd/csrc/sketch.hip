@@ -824,7 +824,8 @@ static SketchPlan plan_for(uint32_t s) {
 
 int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t *d_valid,
                        const uint64_t *base_off, const uint64_t *padded, const uint64_t *nkmers,
-                       uint32_t n, uint64_t *d_hashes, uint32_t *d_nhash, hipStream_t st) {
+                       uint32_t n, uint64_t *d_hashes, uint32_t *d_nhash, hipStream_t st,
+                       bool defer) {
     if (n == 0) return DREPHIP_OK;
     if (ctx->k != 21) { set_error("sketch kernel is instantiated for k=21 (Mash/dRep default) only"); return DREPHIP_ERR_UNSUPPORTED; }
     const uint32_t s = ctx->s;
@@ -987,6 +988,23 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
         timing_mark(ctx, 1, st, false);
         HIPC(hipGetLastError());
         HIPC(hipMemcpyAsync(status, d_st, n, hipMemcpyDeviceToHost, st));
+        if (defer) {
+            // deferred: the sets are left empty by finalize whatever the status
+            // (finalize_reset), so a rerun from scratch is always valid
+            auto &p = ctx->pend;
+            p.active = true;
+            p.d_codes = d_codes; p.d_valid = d_valid;
+            p.off.assign(base_off, base_off + n);
+            p.pad.assign(padded, padded + n);
+            p.nk.assign(nkmers, nkmers + n);
+            p.n = n; p.d_hashes = d_hashes; p.d_nhash = d_nhash; p.st = st;
+            p.h_status = status;
+            ctx->sk_clean_gen = ctx->alloc_gen;
+            ctx->sk_clean_sets = d_sets;
+            ctx->sk_clean_cnt = d_cnt;
+            ctx->sk_clean_n = std::max(clean, n);
+            return DREPHIP_OK;
+        }
         HIPC(hipStreamSynchronize(st));
         first = false;
         if (getenv("DREPHIP_DEBUG")) {

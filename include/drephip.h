@@ -122,6 +122,25 @@ int drephip_sketch_device(drephip_ctx *ctx, const uint32_t *d_codes, const uint3
                           const uint64_t *h_nkmers, uint32_t n_genomes,
                           uint64_t *d_hashes, uint32_t *d_nhash, void *stream);
 
+/* Same as drephip_sketch_device, but returns once the first threshold round
+ * is queued, without waiting for it: work the caller queues next on `stream`
+ * (the sketch all-gather, drephip_allpairs_device) runs right behind it.
+ * d_hashes/d_nhash are final only after drephip_sketch_wait, which must be
+ * called before the next sketch call on this context (a sketch call made
+ * first drops the pending check). */
+int drephip_sketch_device_async(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t *d_valid,
+                                const uint64_t *h_base_off, const uint64_t *h_padded,
+                                const uint64_t *h_nkmers, uint32_t n_genomes,
+                                uint64_t *d_hashes, uint32_t *d_nhash, void *stream);
+
+/* Completes a drephip_sketch_device_async call: waits for its stream, checks
+ * every genome's first-round status and, if any genome needs another
+ * threshold round (a genome with fewer distinct k-mers than expected, or
+ * heavy repeats), reruns the whole call synchronously and sets *redone = 1:
+ * anything the caller computed from the sketches in between must then be
+ * recomputed.  *redone = 0 otherwise (also when nothing is pending). */
+int drephip_sketch_wait(drephip_ctx *ctx, int *redone);
+
 /* Bench/test input: write synthetic genomes g0..g0+n-1 (each length L, one
  * record; family = g / family_size) into the packed layout with
  * genome i at base_off = tile + i*drephip_padded_bases(&L, 1).

@@ -635,3 +635,54 @@ def test_cluster_mash_condensed_gpu_equals_reference_path(family, ctx1000, metho
     assert np.array_equal(z_gpu, z_cpu)
     assert cdb_gpu.equals(cdb_cpu)
     assert cdb_gpu['primary_cluster'].nunique() > 1
+
+
+def test_sketch_device_async_wait(ctx1000):
+    """drephip_sketch_device_async queues the sketch without reading its
+    threshold status back; all-pairs queued behind it on the same stream sees
+    the final sketches, and drephip_sketch_wait reruns the call when a genome
+    needs another threshold round (forced here by overstating its k-mer count,
+    which seeds the threshold ~1000x too low)."""
+    import torch
+    n, L, fam, seed = 4, 300_000, 2, 5
+    tile = _lib.tile_bases()
+    P = _lib.padded_bases([L])
+    codes = torch.zeros((tile + n * P) // 16, dtype=torch.int32, device="cuda")
+    valid = torch.zeros((tile + n * P) // 32, dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    ctx1000.synth_device(seed, 0, n, fam, L, codes.data_ptr(), valid.data_ptr(), st)
+    off = np.array([tile + i * P for i in range(n)], np.uint64)
+    pad = np.full(n, P, np.uint64)
+    oh, onh = oracle.sketch_synth(0, n, L, seed=seed, family_size=fam)
+    oc, _ = oracle.allpairs(oh, onh, S)
+
+    def run(nk, wait=True, sync_after=False):
+        hashes = torch.zeros((n, S), dtype=torch.int64, device="cuda")
+        nhash = torch.zeros(n, dtype=torch.int32, device="cuda")
+        common = torch.zeros(n * (n - 1) // 2, dtype=torch.int16, device="cuda")
+        ctx1000.sketch_device_async(codes.data_ptr(), valid.data_ptr(), off, pad, nk, n,
+                                    hashes.data_ptr(), nhash.data_ptr(), st)
+        if sync_after:       # a sketch call before the wait drops the pending check
+            ctx1000.sketch_device(codes.data_ptr(), valid.data_ptr(), off, pad, nk, n,
+                                  hashes.data_ptr(), nhash.data_ptr(), st)
+        ctx1000.allpairs_device(hashes.data_ptr(), nhash.data_ptr(), n, 0, n, common.data_ptr(), None, st)
+        redone = ctx1000.sketch_wait() if wait else None
+        if redone:
+            ctx1000.allpairs_device(hashes.data_ptr(), nhash.data_ptr(), n, 0, n, common.data_ptr(), None, st)
+        torch.cuda.synchronize()
+        return (hashes.cpu().numpy().view(np.uint64), nhash.cpu().numpy().view(np.uint32),
+                common.cpu().numpy().view(np.uint16), redone)
+
+    good = np.full(n, L - 20, np.uint64)
+    h, nh, c, redone = run(good)
+    assert redone is False
+    assert np.array_equal(nh, onh) and np.array_equal(h, oh) and np.array_equal(c, oc)
+    bad = good.copy()
+    bad[1] *= 1000
+    h, nh, c, redone = run(bad)
+    assert redone is True
+    assert np.array_equal(nh, onh) and np.array_equal(h, oh) and np.array_equal(c, oc)
+    h, nh, c, redone = run(bad, sync_after=True)
+    assert redone is False
+    assert np.array_equal(h, oh) and np.array_equal(c, oc)
+    assert ctx1000.sketch_wait() is False          # nothing pending
