@@ -779,7 +779,7 @@ static int launch_band(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_
     uint32_t *d_nfail;
     int rc;
     if ((rc = scratch(ctx, "apb_items", items.size() * sizeof(uint2), (void **)&d_items))) return rc;
-    if ((rc = scratch(ctx, "ap_nfail", 4, (void **)&d_nfail))) return rc;
+    if ((rc = scratch(ctx, "ap_nfail_band", 4, (void **)&d_nfail))) return rc;
     HIPC(hipMemsetAsync(d_nfail, 0, 4, st));
     HIPC(hipMemcpyAsync(d_items, items.data(), items.size() * sizeof(uint2), hipMemcpyHostToDevice, st));
     uint64_t *d_prof = nullptr;                      // DREPHIP_BAND_PROF=1: per-phase wall-clock sums
@@ -872,7 +872,13 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
     if ((rc = scratch(ctx, "ap_blk", (uint64_t)ngroups * stride * 4, (void **)&d_blk))) return rc;
     if ((rc = scratch(ctx, "ap_fam", (uint64_t)ngroups * R, (void **)&d_fam))) return rc;
     if ((rc = scratch(ctx, "ap_nfail", 4, (void **)&d_nfail))) return rc;
-    HIPC(hipMemsetAsync(d_nfail, 0, 4, st));
+    // the failure counter is never reset: a call's failures are the growth
+    // since the value the previous call read back (zeroed once per allocation)
+    if (ctx->ap_nfail_ptr != d_nfail) {
+        HIPC(hipMemsetAsync(d_nfail, 0, 4, st));
+        ctx->ap_nfail_ptr = d_nfail;
+        ctx->ap_nfail_seen = 0;
+    }
     const size_t blds = (size_t)TS * 4;
     HIPC(hipFuncSetAttribute((const void *)k_build_q32, hipFuncAttributeMaxDynamicSharedMemorySize, (int)blds));
     timing_mark(ctx, 3, st, true);
@@ -945,7 +951,9 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
     if (rc) return rc;
     HIPC(hipMemcpyAsync(h_nfail, d_nfail, 4, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));                  // items (host vector) and nfail are safe past here
-    if (*h_nfail)   // a row table could not be built with any field pair: exact merge kernel instead
+    const uint32_t nfail = *h_nfail - ctx->ap_nfail_seen;
+    ctx->ap_nfail_seen = *h_nfail;
+    if (nfail)      // a row table could not be built with any field pair: exact merge kernel instead
         return launch_merge(ctx, d_hashes, d_nhash, N, seg0, npairs, d_common, d_denom, st);
     return DREPHIP_OK;
 }

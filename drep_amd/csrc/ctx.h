@@ -52,6 +52,9 @@ struct drephip_ctx {
     uint64_t ap_items_key[5] = {0, 0, 0, 0, 0};
     uint64_t ap_items_gen = 0;
     uint32_t ap_items_n = 0;
+    // table-build failure counter of the whole-row all-pairs path (never reset)
+    uint32_t *ap_nfail_ptr = nullptr;
+    uint32_t ap_nfail_seen = 0;
     // deferred sketch (drephip_sketch_device_async): the first round is queued
     // without reading its status back; drephip_sketch_wait checks it (and
     // reruns the call synchronously if a genome needs another threshold round)

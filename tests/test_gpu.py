@@ -254,11 +254,21 @@ def test_allpairs_unbuildable_table_falls_back_to_merge(path):
         h[i + 1] = np.unique(np.concatenate([h[i + 1][:S - 2], bad[:2]]))[:S]
     nh = np.full(N, S, np.uint32)
     oc, _ = oracle.allpairs(h, nh, S, threads=4)
+    good = h.copy()
+    for i in (0, 7, 1, 8):
+        good[i] = h[i + 2]
+    ogc, _ = oracle.allpairs(good, nh, S, threads=4)
     with _lib.Context(0, 21, S, 42) as ctx:
         if path == "band":
             ctx.set_allpairs_path(ctx.AP_BAND, 256)
         c, _ = ctx.allpairs(h, nh)
-    assert np.array_equal(c, oc)
+        # the failure counter is per context and never reset (the table path
+        # compares it with the last value read): a clean call, then a failing
+        # one again, on the same context
+        c2, _ = ctx.allpairs(good, nh)
+        c3, _ = ctx.allpairs(h, nh)
+    assert np.array_equal(c, oc) and np.array_equal(c3, oc)
+    assert np.array_equal(c2, ogc)
     assert c.max() >= 2
 
 
