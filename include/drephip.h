@@ -138,7 +138,8 @@ int drephip_sketch_device_async(drephip_ctx *ctx, const uint32_t *d_codes, const
  * threshold round (a genome with fewer distinct k-mers than expected, or
  * heavy repeats), reruns the whole call synchronously and sets *redone = 1:
  * anything the caller computed from the sketches in between must then be
- * recomputed.  *redone = 0 otherwise (also when nothing is pending). */
+ * recomputed.  *redone = 0 otherwise (also when nothing is pending).  The
+ * sketch kernels' drephip_last_kernel_ms entries (0, 1) are set here. */
 int drephip_sketch_wait(drephip_ctx *ctx, int *redone);
 
 /* Bench/test input: write synthetic genomes g0..g0+n-1 (each length L, one
