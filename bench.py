@@ -75,6 +75,8 @@ def parse():
     ap.add_argument("--family-size", type=int, default=100)
     ap.add_argument("--seed", type=int, default=0xD2E9)
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the C oracle on host cores (rank 0)")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="queue each step before checking the previous one (1) or one step at a time (0)")
     ap.add_argument("--defer-check", type=int, default=1,
                     help="check the sketch's threshold status after queuing the all-pairs (1) or before (0)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_sketch_traffic.json"))
@@ -233,15 +235,61 @@ def main():
                 ev[1].synchronize()
             stage["gather"] += ev[0].elapsed_time(ev[1]) / 1e3 if world > 1 else 0.0
 
+    def pipelined(nsteps, record):
+        """nsteps steps with the host one step ahead: step i's sketch is queued
+        before the host waits for step i-1's all-pairs, and every step's checks
+        (sketch threshold status, table-build failures) run while the next
+        step's kernels execute.  Same work per step as step()."""
+        gev = []
+
+        def check_sketch():
+            if nloc and ctx.sketch_wait():
+                redo["n"] += 1          # sketches rewritten after their all-pairs: re-time (below)
+            if record and nloc:
+                read_kms((0,))
+
+        for i in range(nsteps):
+            if i > 0:
+                check_sketch()
+            if nloc:
+                ctx.sketch_device_async(codes.data_ptr(), valid.data_ptr(), base_off, padded, nkmers, nloc,
+                                        loc_h.data_ptr(), loc_n.data_ptr(), stream)
+            if i > 0 and seg:
+                ctx.allpairs_wait()
+            if world > 1:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                hh, nn = gather_sketches(loc_h, loc_n)
+                e1.record()
+                gev.append((e0, e1))
+            else:
+                hh, nn = loc_h, loc_n
+            if seg:
+                ctx.allpairs_device_async(hh.data_ptr(), nn.data_ptr(), N, r0, r1, d_common.data_ptr(), None,
+                                          stream)
+        if nsteps:
+            check_sketch()
+            if seg:
+                ctx.allpairs_wait()
+        if record and gev:
+            gev[-1][1].synchronize()
+            stage["gather"] += sum(a.elapsed_time(b) for a, b in gev) / 1e3
+
     def timed():
-        for _ in range(args.warmup):
-            step(False)
+        if args.pipeline:
+            pipelined(args.warmup, False)
+        else:
+            for _ in range(args.warmup):
+                step(False)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step(True)
+        if args.pipeline:
+            pipelined(args.steps, True)
+        else:
+            for _ in range(args.steps):
+                step(True)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -253,12 +301,14 @@ def main():
         return el
 
     elapsed = timed()
-    if redo["n"] and world > 1:
+    if redo["n"] and (world > 1 or args.pipeline):
         # some rank redid its sketches inside a step: those steps' all-pairs
         # used stale sketches, so time again with the synchronous check
         print("bench: a sketch needed another threshold round; re-timing with the synchronous check",
               file=sys.stderr)
         args.defer_check = 0
+        args.pipeline = 0
+        redo["n"] = 0
         for w in kms:
             kms[w] = [0.0, 0]
         stage["gather"] = 0.0
@@ -393,6 +443,8 @@ def main():
                             "step = sketch + RCCL all-gather + all-pairs" % (N, L, s, config_name(N, L, s)),
                 "genomes": N, "genome_bp": L, "k": 21, "sketch": s, "family_size": args.family_size,
                 "parallelism": "sketch: genome shards; all-pairs: balanced row shards; RCCL all-gather",
+                "host_loop": ("pipelined: step i+1 queued before step i's checks" if args.pipeline
+                              else "one step at a time") + (", deferred sketch check" if args.defer_check else ""),
             },
             "stages": {
                 "sketch_ms_per_step": stage["sketch"] / K * 1e3,

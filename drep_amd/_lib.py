@@ -65,6 +65,8 @@ SIGNATURES = {
     "drephip_allpairs": (C.c_int, [vp, u64p, u32p, C.c_uint32, u16p, vp]),
     "drephip_allpairs_rows": (C.c_int, [vp, u64p, u32p, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp]),
     "drephip_allpairs_device": (C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp]),
+    "drephip_allpairs_device_async": (C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp]),
+    "drephip_allpairs_wait": (C.c_int, [vp]),
     "drephip_allpairs_merge_device": (C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp]),
     "drephip_distance_lut": (C.c_int, [C.c_int, C.c_uint32, f64p]),
     "drephip_set_allpairs_path": (C.c_int, [vp, C.c_int, C.c_uint32]),
@@ -352,3 +354,13 @@ class Context:
         fn = lib().drephip_allpairs_merge_device if merge else lib().drephip_allpairs_device
         check(fn(self._h, d_hashes, d_nhash, N, row0, row1, d_common, d_denom, stream),
               "drephip_allpairs_device")
+
+    def allpairs_device_async(self, d_hashes: int, d_nhash: int, N: int, row0: int, row1: int,
+                              d_common: int, d_denom: Optional[int] = None, stream: Optional[int] = None):
+        """allpairs_device whose failure-count check is deferred to
+        allpairs_wait() (include/drephip.h)."""
+        check(lib().drephip_allpairs_device_async(self._h, d_hashes, d_nhash, N, row0, row1, d_common,
+                                                  d_denom, stream), "drephip_allpairs_device_async")
+
+    def allpairs_wait(self) -> None:
+        check(lib().drephip_allpairs_wait(self._h), "drephip_allpairs_wait")

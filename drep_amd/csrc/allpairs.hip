@@ -830,7 +830,13 @@ static int launch_q(drephip_ctx *ctx, uint32_t nitems, size_t lds, hipStream_t s
 
 int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N,
                          uint32_t row0, uint32_t row1, uint16_t *d_common, uint16_t *d_denom,
-                         hipStream_t st, bool force_merge) {
+                         hipStream_t st, bool force_merge, bool defer) {
+    // a deferred call's failure count must be read before this call's build
+    // adds to the shared counter
+    if (ctx->apend.active) {
+        int rc = allpairs_wait_impl(ctx);
+        if (rc) return rc;
+    }
     if (row1 > N) row1 = N;
     if (N < 2 || row0 >= row1 || row0 >= N - 1) return DREPHIP_OK;
     if (row1 > N - 1) row1 = N - 1;
@@ -950,11 +956,39 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
 #undef DREPHIP_Q
     if (rc) return rc;
     HIPC(hipMemcpyAsync(h_nfail, d_nfail, 4, hipMemcpyDeviceToHost, st));
+    if (defer && reuse) {
+        // deferred: drephip_allpairs_wait reads the count (after this event)
+        // and runs the merge fallback if a table failed.  Only on a reused
+        // item list: a new one's host vector must outlive its copy (sync below)
+        auto &p = ctx->apend;
+        if (!p.ev) HIPC(hipEventCreateWithFlags(&p.ev, hipEventDisableTiming));
+        HIPC(hipEventRecord(p.ev, st));
+        p.active = true;
+        p.d_hashes = d_hashes; p.d_nhash = d_nhash; p.N = N; p.seg0 = seg0; p.npairs = npairs;
+        p.d_common = d_common; p.d_denom = d_denom; p.st = st; p.h_nfail = h_nfail;
+        return DREPHIP_OK;
+    }
     HIPC(hipStreamSynchronize(st));                  // items (host vector) and nfail are safe past here
     const uint32_t nfail = *h_nfail - ctx->ap_nfail_seen;
     ctx->ap_nfail_seen = *h_nfail;
     if (nfail)      // a row table could not be built with any field pair: exact merge kernel instead
         return launch_merge(ctx, d_hashes, d_nhash, N, seg0, npairs, d_common, d_denom, st);
+    return DREPHIP_OK;
+}
+
+// Completes a deferred table-path call (drephip_allpairs_device_async).
+int allpairs_wait_impl(drephip_ctx *ctx) {
+    auto &p = ctx->apend;
+    if (!p.active) return DREPHIP_OK;
+    p.active = false;
+    HIPC(hipEventSynchronize(p.ev));
+    const uint32_t nfail = *p.h_nfail - ctx->ap_nfail_seen;
+    ctx->ap_nfail_seen = *p.h_nfail;
+    if (nfail) {
+        int rc = launch_merge(ctx, p.d_hashes, p.d_nhash, p.N, p.seg0, p.npairs, p.d_common, p.d_denom, p.st);
+        if (rc) return rc;
+        HIPC(hipStreamSynchronize(p.st));
+    }
     return DREPHIP_OK;
 }
 

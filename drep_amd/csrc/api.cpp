@@ -169,10 +169,15 @@ DREPHIP_EXPORT int drephip_destroy(drephip_ctx *ctx) {
     if (!ctx) return DREPHIP_OK;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
+    // deferred calls may still be writing the pinned readback buffers
+    if (ctx->pend.active && ctx->pend.done) (void)hipEventSynchronize(ctx->pend.done);
+    if (ctx->apend.active && ctx->apend.ev) (void)hipEventSynchronize(ctx->apend.ev);
     for (auto &kv : ctx->bufs) if (kv.second.ptr) (void)hipFree(kv.second.ptr);
     for (auto &kv : ctx->pinned) if (kv.second.ptr) (void)hipHostFree(kv.second.ptr);
     pend_release(ctx);
     for (auto e : ctx->ev_pool) (void)hipEventDestroy(e);
+    if (ctx->pend.done) (void)hipEventDestroy(ctx->pend.done);
+    if (ctx->apend.ev) (void)hipEventDestroy(ctx->apend.ev);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return DREPHIP_OK;
@@ -434,7 +439,7 @@ DREPHIP_EXPORT int drephip_sketch_wait(drephip_ctx *ctx, int *redone) {
     if (redone) *redone = 0;
     auto &p = ctx->pend;
     if (!p.active) return DREPHIP_OK;
-    HIPC(hipStreamSynchronize(p.st));
+    HIPC(hipEventSynchronize(p.done));                 // the status copy (not what was queued after it)
     double kms[2] = {0, 0};
     int kn[2] = {0, 0};
     for (auto &sp : p.spans) {
@@ -482,6 +487,27 @@ DREPHIP_EXPORT int drephip_allpairs_device(drephip_ctx *ctx, const uint64_t *d_h
     if (rc) return rc;
     timing_collect(ctx);
     return DREPHIP_OK;
+}
+
+DREPHIP_EXPORT int drephip_allpairs_device_async(drephip_ctx *ctx, const uint64_t *d_hashes,
+                                                 const uint32_t *d_nhash, uint32_t N, uint32_t row0,
+                                                 uint32_t row1, uint16_t *d_common, uint16_t *d_denom,
+                                                 void *stream) {
+    GUARD_CTX(ctx);
+    if (!d_hashes || !d_nhash || !d_common) { set_error("null argument"); return DREPHIP_ERR_ARG; }
+    int rc = allpairs_wait_impl(ctx);                  // an earlier call's check comes first
+    if (rc) return rc;
+    timing_begin(ctx);
+    rc = allpairs_device_impl(ctx, d_hashes, d_nhash, N, row0, row1, d_common, d_denom,
+                              pick_stream(ctx, stream), false, true);
+    if (rc) { ctx->apend.active = false; return rc; }
+    if (!ctx->apend.active) timing_collect(ctx);      // the call completed synchronously
+    return DREPHIP_OK;
+}
+
+DREPHIP_EXPORT int drephip_allpairs_wait(drephip_ctx *ctx) {
+    GUARD_CTX(ctx);
+    return allpairs_wait_impl(ctx);
 }
 
 DREPHIP_EXPORT int drephip_allpairs_merge_device(drephip_ctx *ctx, const uint64_t *d_hashes,

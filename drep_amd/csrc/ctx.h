@@ -69,7 +69,20 @@ struct drephip_ctx {
         const uint8_t *h_status = nullptr;     // pinned, written by the queued copy
         std::vector<Span> spans;               // timing spans of the queued kernels
         std::vector<hipEvent_t> events;        // their events, out of ev_pool until collected
+        hipEvent_t done = nullptr;             // after the status copy
     } pend;
+    // deferred all-pairs check (drephip_allpairs_device_async, table path)
+    struct PendingAllpairs {
+        bool active = false;
+        hipEvent_t ev = nullptr;               // after the failure-count copy
+        const uint64_t *d_hashes = nullptr;
+        const uint32_t *d_nhash = nullptr;
+        uint32_t N = 0;
+        uint64_t seg0 = 0, npairs = 0;
+        uint16_t *d_common = nullptr, *d_denom = nullptr;
+        hipStream_t st = nullptr;
+        const uint32_t *h_nfail = nullptr;
+    } apend;
 };
 
 namespace drephip {
@@ -104,7 +117,8 @@ int synth_device_impl(drephip_ctx *ctx, uint64_t seed, uint32_t g0, uint32_t n, 
                       uint64_t L, uint32_t *d_codes, uint32_t *d_valid, hipStream_t st);
 int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash,
                          uint32_t N, uint32_t row0, uint32_t row1, uint16_t *d_common,
-                         uint16_t *d_denom, hipStream_t st, bool force_merge);
+                         uint16_t *d_denom, hipStream_t st, bool force_merge, bool defer = false);
+int allpairs_wait_impl(drephip_ctx *ctx);
 
 // Primary clustering (linkage.hip).
 int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, double *Z_out, hipStream_t st);

@@ -999,6 +999,8 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
             p.nk.assign(nkmers, nkmers + n);
             p.n = n; p.d_hashes = d_hashes; p.d_nhash = d_nhash; p.st = st;
             p.h_status = status;
+            if (!p.done) HIPC(hipEventCreateWithFlags(&p.done, hipEventDisableTiming));
+            HIPC(hipEventRecord(p.done, st));
             ctx->sk_clean_gen = ctx->alloc_gen;
             ctx->sk_clean_sets = d_sets;
             ctx->sk_clean_cnt = d_cnt;

@@ -176,6 +176,19 @@ int drephip_allpairs_device(drephip_ctx *ctx, const uint64_t *d_hashes, const ui
                             uint32_t N, uint32_t row0, uint32_t row1, uint16_t *d_common,
                             uint16_t *d_denom, void *stream);
 
+/* Same as drephip_allpairs_device, but on the whole-row table path (s <=
+ * 2048) it returns once the kernels and the table-build failure count's
+ * readback are queued: the host can queue the next step's work while these
+ * kernels run.  drephip_allpairs_wait (or any later all-pairs call on this
+ * context) completes it: reads the count and, if a row's table could not be
+ * built, recomputes the segment with the merge kernel before returning.  The
+ * output is final only after that.  Other paths run synchronously (the wait
+ * is then a no-op).  Kernel timings of a deferred call are not recorded. */
+int drephip_allpairs_device_async(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash,
+                                  uint32_t N, uint32_t row0, uint32_t row1, uint16_t *d_common,
+                                  uint16_t *d_denom, void *stream);
+int drephip_allpairs_wait(drephip_ctx *ctx);
+
 /* Reference all-pairs kernel (one lane per pair, literal Mash merge loop).
  * Same contract as drephip_allpairs_device; slower; used for cross-checks. */
 int drephip_allpairs_merge_device(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash,

@@ -238,21 +238,8 @@ def test_allpairs_unbuildable_table_falls_back_to_merge(path):
     slots under every field family, so no cuckoo table exists for that row:
     the host must discard the table kernel's output and rerun the segment with
     the literal merge kernel -- counts still exact."""
-    rng = np.random.default_rng(3)
-    N = 24
-    base = np.sort(rng.choice(2 ** 62, size=(N, 2000), replace=False).astype(np.uint64), axis=1)
-    h = np.full((N, S), UMAX, dtype=np.uint64)
-    for i in range(N):                                   # families: shared prefixes
-        pool = base[i // 6]
-        keep = np.sort(rng.choice(len(pool), S, replace=False))
-        h[i] = pool[keep]
-    lo = np.uint64(0x12345678)
-    bad = np.array([(np.uint64(k) << np.uint64(40)) | lo for k in (1, 2, 3)], dtype=np.uint64)
-    for i in (0, 7):
-        row = np.unique(np.concatenate([h[i][:S - 3], bad]))
-        h[i] = row[:S]
-        h[i + 1] = np.unique(np.concatenate([h[i + 1][:S - 2], bad[:2]]))[:S]
-    nh = np.full(N, S, np.uint32)
+    h, nh = _unbuildable_rows()
+    N = len(nh)
     oc, _ = oracle.allpairs(h, nh, S, threads=4)
     good = h.copy()
     for i in (0, 7, 1, 8):
@@ -270,6 +257,59 @@ def test_allpairs_unbuildable_table_falls_back_to_merge(path):
     assert np.array_equal(c, oc) and np.array_equal(c3, oc)
     assert np.array_equal(c2, ogc)
     assert c.max() >= 2
+
+
+def _unbuildable_rows():
+    """Rows 0 and 7 hold three hashes with one low word (no cuckoo table can
+    hold them); rows 1 and 8 share two of them."""
+    rng = np.random.default_rng(3)
+    N = 24
+    base = np.sort(rng.choice(2 ** 62, size=(N, 2000), replace=False).astype(np.uint64), axis=1)
+    h = np.full((N, S), UMAX, dtype=np.uint64)
+    for i in range(N):                                   # families: shared prefixes
+        pool = base[i // 6]
+        keep = np.sort(rng.choice(len(pool), S, replace=False))
+        h[i] = pool[keep]
+    lo = np.uint64(0x12345678)
+    bad = np.array([(np.uint64(k) << np.uint64(40)) | lo for k in (1, 2, 3)], dtype=np.uint64)
+    for i in (0, 7):
+        row = np.unique(np.concatenate([h[i][:S - 3], bad]))
+        h[i] = row[:S]
+        h[i + 1] = np.unique(np.concatenate([h[i + 1][:S - 2], bad[:2]]))[:S]
+    nh = np.full(N, S, np.uint32)
+    return h, nh
+
+
+def test_allpairs_device_async_wait():
+    """drephip_allpairs_device_async defers the table-build failure check to
+    drephip_allpairs_wait (or the next all-pairs call): a failing table is
+    still replaced by the merge kernel's exact counts, on either completion,
+    and a clean call between two failing ones is not mistaken for failing."""
+    import torch
+    h, nh = _unbuildable_rows()
+    N = len(nh)
+    good = h.copy()
+    for i in (0, 7, 1, 8):
+        good[i] = h[i + 2]
+    oc, _ = oracle.allpairs(h, nh, S, threads=4)
+    ogc, _ = oracle.allpairs(good, nh, S, threads=4)
+    st = torch.cuda.current_stream().cuda_stream
+    dn = torch.from_numpy(nh.view(np.int32)).cuda()
+    with _lib.Context(0, 21, S, 42) as ctx:
+        outs = []
+        for rows, how in ((h, "wait"), (good, "wait"), (h, "next_call"), (good, "wait"), (h, "wait")):
+            dh = torch.from_numpy(rows.view(np.int64)).cuda()
+            c = torch.zeros(N * (N - 1) // 2, dtype=torch.int16, device="cuda")
+            for _ in range(2):          # the second call reuses the item list: the deferred form
+                ctx.allpairs_device_async(dh.data_ptr(), dn.data_ptr(), N, 0, N, c.data_ptr(), None, st)
+                if how == "wait":
+                    ctx.allpairs_wait()
+                else:                   # completed by the next all-pairs call (a synchronous one)
+                    ctx.allpairs_device(dh.data_ptr(), dn.data_ptr(), N, N, N, c.data_ptr(), None, st)
+            torch.cuda.synchronize()
+            outs.append(c.cpu().numpy().view(np.uint16))
+    for c, want in zip(outs, (oc, ogc, oc, ogc, oc)):
+        assert np.array_equal(c, want)
 
 
 def test_allpairs_rejects_unpadded_rows(ctx1000):
