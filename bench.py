@@ -314,6 +314,9 @@ def main():
         stage["gather"] = 0.0
         elapsed = timed()
 
+    # the timed (possibly pipelined) steps' outputs, checked by --verify below
+    snap = (loc_h.clone(), loc_n.clone(), d_common.clone()) if args.verify else None
+
     # ---- the other kernels' times: PROFILE_STEPS extra steps, every kernel
     # bracketed by events (not part of the timed region)
     keep = (list(kms[0]), dict(stage))
@@ -407,10 +410,12 @@ def main():
         full_c = torch.zeros(max(N * (N - 1) // 2, 1), dtype=torch.int16, device=dev)
         ctx.allpairs_device(full_h.data_ptr(), full_n.data_ptr(), N, 0, N, full_c.data_ptr(), None, stream)
         torch.cuda.synchronize()
-        hh, nn = (gather_sketches(loc_h, loc_n) if world > 1 else (loc_h, loc_n))
         a = cond_start(r0, N)
-        ok = (torch.equal(hh[:N], full_h) and torch.equal(nn[:N], full_n) and
-              torch.equal(d_common[:seg], full_c[a:a + seg]))
+        ok = True
+        for lh, ln, dc in ((loc_h, loc_n, d_common), snap):     # after the extra steps; after the timed ones
+            hh, nn = (gather_sketches(lh, ln) if world > 1 else (lh, ln))
+            ok = ok and (torch.equal(hh[:N], full_h) and torch.equal(nn[:N], full_n) and
+                         torch.equal(dc[:seg], full_c[a:a + seg]))
         if world > 1:
             flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
             dist.all_reduce(flag, op=dist.ReduceOp.MIN)
