@@ -26,26 +26,21 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
-# VALU issue peak: 256 CU x 4 SIMD-32 x 32 lanes/cycle x 2.4 GHz (a wave64
-# instruction issues over 2 cycles, MI355X_MICROARCH.md; two-operand 32-bit
-# ops measure 1.0 ns per wave-instruction per SIMD under load).  The Murmur
-# loop is mostly three-operand / 64-bit / multiply ops, which measure
-# 1.7-2.0 ns (tools/valu_microbench.hip, profiles/r01_valu_microbench.json):
-# the binding model is the measured cost of the loop's own instruction mix
-# (valu_model.mix_ns_per_wave_inst_per_simd / frac_of_mix_throughput).
-VALU_PEAK_TINST = 256 * 4 * 32 * 2.4e9 / 1e12
+# VALU issue model: SQ_ACTIVE_INST_VALU counts quad-cycles (MI355X_MICROARCH.md,
+# "s_memtime tick vs SQ PMC units") and equals SQ_INSTS_VALU for the sketch
+# kernel, i.e. each of its wave64 VALU instructions holds a SIMD for 4 cycles:
+# peak = 1024 SIMDs x 2.4 GHz / 4 wave-instructions per second.
 N_SIMD = 256 * 4
-# measured throughput (ns per wave64 instruction per SIMD, 8 waves/SIMD) of the
-# integer instructions the Murmur loop is made of; instructions the microbench
-# does not cover are priced as v_xor (its v_cndmask figure is a VCC-hazard
-# artefact of the microbench loop and is not used)
-MICROBENCH = os.path.join(ROOT, "profiles", "r01_valu_microbench.json")
-SKETCH_DEFAULT_VARIANT = "9"   # must match drephip_ctx::sketch_kernel default (ctx.h)
+VALU_PEAK_WAVE_INST = N_SIMD * 2.4e9 / 4
+SKETCH_ISA = os.path.join(ROOT, "profiles", "r02_sketch_isa.json")
 # committed PMC summaries (tools/pmc_summary.py): VALU / LDS utilisation of the
 # two kernels, reported next to the live timings
-SKETCH_PMC = os.path.join(ROOT, "profiles", "r01_sketch_pmc_sq.json")
-DIST_PMC = os.path.join(ROOT, "profiles", "r01_allpairs_pmc_sq_N6000.json")
+SKETCH_PMC = os.path.join(ROOT, "profiles", "r02_sketch_pmc_sq.json")
+DIST_PMC = os.path.join(ROOT, "profiles", "r02_allpairs_pmc_sq_N6000.json")
+SKETCH_TRAFFIC = os.path.join(ROOT, "profiles", "r02_sketch_traffic.json")
 PROFILE_STEPS = 3              # untimed steps that time finalize / all-pairs / table build
+VERIFY_GENOMES = 16            # timed-step sketches re-derived by the C oracle (sampled, every run)
+VERIFY_PAIRS = 100_000         # timed-step counts re-derived by the C oracle (random pairs + one row)
 
 
 def pmc_block(path):
@@ -57,7 +52,7 @@ def pmc_block(path):
     except Exception:
         return None
     keep = ("valu_busy_frac", "lds_busy_frac", "lds_bank_conflict_frac", "wait_any_frac",
-            "wait_inst_any_frac", "active_inst_any_frac")
+            "wait_inst_any_frac", "active_inst_any_frac", "valu_insts_per_window_end", "effective_clock_ghz")
     out = {k: d["derived"][k] for k in keep if k in d.get("derived", {})}
     out["source"] = os.path.relpath(path, ROOT)
     out["profiled_kernel"] = (d.get("kernel") or "")[:80]
@@ -79,7 +74,11 @@ def parse():
                     help="queue each step before checking the previous one (1) or one step at a time (0)")
     ap.add_argument("--defer-check", type=int, default=1,
                     help="check the sketch's threshold status after queuing the all-pairs (1) or before (0)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_sketch_traffic.json"))
+    ap.add_argument("--traffic-json", default=SKETCH_TRAFFIC)
+    ap.add_argument("--check", type=int, default=1,
+                    help="after timing (untimed): check a sample of the timed steps' own sketches and "
+                         "shared-hash counts against the C oracle (test infrastructure); 'verified' in "
+                         "the JSON line")
     ap.add_argument("--verify", type=int, default=0,
                     help="after timing, every rank re-sketches all genomes and recomputes the whole "
                          "triangle on its own GPU and checks its gathered sketches and its segment "
@@ -101,18 +100,29 @@ def config_name(N, L, s):
     return "custom size"
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(args, threads):
     """Bounded sample of the same whole job on the host with the C oracle
-    (Mash-equivalent restatement, OpenMP): sketch 2*threads genomes, dist
-    2e6 pairs; extrapolate to the full N-genome job."""
+    (Mash-equivalent restatement, OpenMP): sketch a sample of the genomes
+    (about 4 s of wall time) and `mash dist` as many random pairs as the job
+    has; extrapolate the sketch part to all N genomes."""
     import oracle
     N, L, s = args.genomes, args.genome_bp, args.sketch
-    ns = max(2, 2 * threads)
+    ns = min(N, max(2, 16 * threads))
     t0 = time.perf_counter()
     h, nh = oracle.sketch_synth(0, ns, L, seed=args.seed, family_size=args.family_size, s=s, threads=threads)
     t_sk = time.perf_counter() - t0
     rng = np.random.default_rng(1)
-    npairs = 2_000_000
+    npairs = max(2, min(N * (N - 1) // 2, 5_000_000))
     pi = rng.integers(0, ns, npairs).astype(np.uint32)
     pj = ((pi + 1 + rng.integers(0, ns - 1, npairs)) % ns).astype(np.uint32)
     t0 = time.perf_counter()
@@ -121,18 +131,88 @@ def cpu_baseline(args, threads):
     per_genome = t_sk / ns
     per_pair = t_d / npairs
     job = N * per_genome + (N * (N - 1) / 2) * per_pair
+    visible = os.cpu_count() or threads
     return {
         "value": (N * (N - 1) / 2) / job,
         "unit": "genome pairs/s",
         "cores": threads,
         "kind": "port",
-        "sample": ("C oracle (Mash-equivalent restatement, OpenMP %d threads): sketch of %d synthetic "
-                   "%d bp genomes in %.2f s + %d random pairs of mash dist in %.2f s, extrapolated to "
-                   "the %d-genome job (%.1f s sketch + %.1f s dist)"
-                   % (threads, ns, L, t_sk, npairs, t_d, N, N * per_genome, N * (N - 1) / 2 * per_pair)),
+        "cpu_model": cpu_model(),
+        "host_cpus_visible": visible,
+        "sample": ("C oracle (Mash-equivalent restatement; Mash itself is absent), OpenMP %d threads = this job's "
+                   "host CPU share: sketch of %d of the %d synthetic %d bp genomes in %.2f s + %d random pairs of "
+                   "mash dist (the job's pair count, capped at 5e6) in %.2f s; job = %d x per-genome sketch + "
+                   "N(N-1)/2 x per-pair dist = %.1f s + %.2f s"
+                   % (threads, ns, N, L, t_sk, npairs, t_d, N, N * per_genome, N * (N - 1) / 2 * per_pair)),
         "sketch_Mbp_per_s": ns * L / t_sk / 1e6,
         "dist_pairs_per_s": npairs / t_d,
+        # mash dist -p <all host cores>: the sample's per-thread rate times the
+        # host's visible CPUs (linear scaling assumed; both legs are embarrassingly
+        # parallel), stated next to the measured share
+        "value_all_host_cpus_extrapolated": (N * (N - 1) / 2) / job * visible / threads,
     }
+
+
+def check_against_oracle(args, loc_h, loc_n, d_common, g0, nloc, N, r0, r1, world, gather_sketches):
+    """Sampled check of the timed steps' outputs (untimed; the C oracle is test
+    infrastructure): VERIFY_GENOMES of this rank's genomes regenerated and
+    sketched on the host must equal their rows of the sketch matrix, and the
+    shared-hash counts of VERIFY_PAIRS random pairs of this rank's segment plus
+    one whole row must equal Mash's merge of the gathered sketches."""
+    import torch
+    import oracle
+    from drep_amd.parallel import cond_start, segment_size
+    L, s = args.genome_bp, args.sketch
+    threads = max(1, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1))
+    rng = np.random.default_rng(12345 + g0)
+    res = {"genomes": 0, "pairs": 0, "mismatches": 0}
+    ok = True
+    if nloc:
+        k = min(VERIFY_GENOMES, nloc)
+        starts = sorted(set([0, nloc - 1] + [int(x) for x in rng.integers(0, nloc, k - 2)])) if k > 2 else list(range(k))
+        H = loc_h[:nloc].cpu().numpy().view(np.uint64)
+        NH = loc_n[:nloc].cpu().numpy().view(np.uint32)
+        for i in starts:
+            oh, onh = oracle.sketch_synth(g0 + i, 1, L, seed=args.seed, family_size=args.family_size, s=s,
+                                          threads=threads)
+            good = bool(np.array_equal(H[i], oh[0]) and NH[i] == onh[0])
+            ok &= good
+            res["mismatches"] += int(not good)
+        res["genomes"] = len(starts)
+    seg = segment_size(N, r0, r1)
+    if seg:
+        hh, nn = (gather_sketches(loc_h, loc_n) if world > 1 else (loc_h, loc_n))
+        HA = hh[:N].cpu().numpy().view(np.uint64)
+        NA = nn[:N].cpu().numpy().view(np.uint32)
+        C = d_common[:seg].cpu().numpy().view(np.uint16)
+        a = cond_start(r0, N)
+        t = rng.integers(0, seg, VERIFY_PAIRS) + a                     # condensed indices in this segment
+        row = int(rng.integers(r0, min(r1, N - 1)))                    # plus one whole row
+        t = np.concatenate([t, cond_start(row, N) + np.arange(N - 1 - row)])
+        # condensed index -> (i, j)
+        Mf = 2.0 * N - 1.0
+        i = np.floor((Mf - np.sqrt(np.maximum(Mf * Mf - 8.0 * t, 0.0))) / 2.0).astype(np.int64)
+        i = np.clip(i, 0, N - 2)
+        for _ in range(2):
+            i = np.where(i * N - i * (i + 1) // 2 > t, i - 1, i)
+            i = np.where((i + 1) * N - (i + 1) * (i + 2) // 2 <= t, i + 1, i)
+        j = t - (i * N - i * (i + 1) // 2) + i + 1
+        want = oracle.dist_pairs_list(HA, NA, s, i.astype(np.uint32), j.astype(np.uint32), threads=threads)
+        bad = int((C[t - a] != want).sum())
+        ok &= bad == 0
+        res["pairs"] = int(len(t))
+        res["mismatches"] += bad
+    if world > 1:
+        import torch.distributed as dist
+        flag = torch.tensor([1 if ok else 0, res["genomes"], res["pairs"], res["mismatches"]], dtype=torch.int64,
+                            device=loc_h.device)
+        f2 = flag.clone()
+        dist.all_reduce(flag[:1], op=dist.ReduceOp.MIN)
+        dist.all_reduce(f2[1:], op=dist.ReduceOp.SUM)
+        ok = bool(flag[0].item())
+        res.update(genomes=int(f2[1].item()), pairs=int(f2[2].item()), mismatches=int(f2[3].item()))
+    res["verified"] = bool(ok)
+    return res
 
 
 def main():
@@ -314,8 +394,9 @@ def main():
         stage["gather"] = 0.0
         elapsed = timed()
 
-    # the timed (possibly pipelined) steps' outputs, checked by --verify below
-    snap = (loc_h.clone(), loc_n.clone(), d_common.clone()) if args.verify else None
+    # the timed (possibly pipelined) steps' outputs, checked below (oracle
+    # sample by default; --verify: the whole job recomputed on this GPU)
+    snap = (loc_h.clone(), loc_n.clone(), d_common.clone()) if (args.verify or args.check) else None
 
     # ---- the other kernels' times: PROFILE_STEPS extra steps, every kernel
     # bracketed by events (not part of the timed region)
@@ -357,37 +438,27 @@ def main():
         except Exception:
             traffic = None
     kmers_per_s = nloc * (L - 20) / avg_launch_s if avg_launch_s > 0 else 0.0
+    window_ends = nloc * P                           # every padded position is a window end the kernel visits
     valu = {"kmers_per_s": kmers_per_s}
-    isa_path = os.path.join(ROOT, "profiles", "sketch_isa.json")
-    variant = os.environ.get("DREPHIP_SKETCH_KERNEL", SKETCH_DEFAULT_VARIANT)
-    if os.path.exists(isa_path):
-        isa = json.load(open(isa_path))["variants"].get(variant)
+    if os.path.exists(SKETCH_ISA):
+        isa = json.load(open(SKETCH_ISA))["variants"].get("default")
         if isa:
-            # lane-instructions issued per second vs the VALU issue peak, and
-            # the issue time per wave-instruction vs the measured cost of the
-            # same instruction mix (microbench)
-            ach = kmers_per_s * isa["valu_per_kmer"] / 1e12
-            ns_inst = N_SIMD / (kmers_per_s * isa["valu_per_kmer"] / 64) * 1e9
-            valu.update({"kernel": isa["kernel"], "valu_per_kmer": isa["valu_per_kmer"],
-                         "mul_per_kmer": isa["mul_per_kmer"], "achieved": ach,
-                         "peak": VALU_PEAK_TINST, "unit": "T lane-inst/s", "frac": ach / VALU_PEAK_TINST,
-                         "ns_per_wave_inst_per_simd": ns_inst,
-                         "source": "profiles/sketch_isa.json (tools/isa_count.py)"})
-            mix = isa.get("valu_mix_per_kmer")
-            if mix and os.path.exists(MICROBENCH):
-                mb = {r["inst"]: r["ns_per_wave_inst_per_simd"] for r in json.load(open(MICROBENCH))["results"]}
-                base = mb["v_xor_b32"]
-
-                def cost(op):
-                    for name, ns in mb.items():
-                        if op.startswith(name) and not name.startswith("v_cndmask"):
-                            return ns
-                    return base
-                mix_ns = sum(n * cost(op) for op, n in mix.items()) / sum(mix.values())
-                valu.update({"mix_ns_per_wave_inst_per_simd": mix_ns,
-                             "frac_of_mix_throughput": mix_ns / ns_inst,
-                             "mix_source": "profiles/r01_valu_microbench.json (8 waves/SIMD, "
-                                           "independent chains), weighted by the hot-loop mix"})
+            valu.update({"kernel": isa["kernel"], "valu_per_kmer_hot_loop": isa["valu_per_kmer"],
+                         "lds_reads_per_kmer": isa["lds_reads_per_kmer"],
+                         "isa_source": os.path.relpath(SKETCH_ISA, ROOT) + " (tools/isa_count.py)"})
+    pmc_sk = pmc_block(SKETCH_PMC)
+    if pmc_sk and pmc_sk.get("valu_insts_per_window_end"):
+        # wave64 VALU instructions per launch (PMC count per window end, the
+        # table copy and every loop overhead included) / launch time, against
+        # 1024 SIMDs x 2.4 GHz / 4 cycles per wave instruction
+        wi = pmc_sk["valu_insts_per_window_end"] * window_ends / 64
+        ach = wi / avg_launch_s if avg_launch_s > 0 else 0.0
+        valu.update({"bound": "valu_issue", "achieved": ach, "peak": VALU_PEAK_WAVE_INST,
+                     "unit": "wave64 VALU instructions/s", "frac": ach / VALU_PEAK_WAVE_INST,
+                     "valu_insts_per_kmer_measured": pmc_sk["valu_insts_per_window_end"],
+                     "note": "each VALU instruction of this kernel holds its SIMD one quad-cycle "
+                             "(SQ_ACTIVE_INST_VALU = SQ_INSTS_VALU); time follows the VALU count "
+                             "(profiles/r02_sketch_ab.json)"})
 
     # ---- output segment D2H (PCIe-inclusive leg; not part of `value`)
     torch.cuda.synchronize()
@@ -423,11 +494,16 @@ def main():
         verified = bool(ok)
         del codes_a, valid_a, full_h, full_n, full_c
 
+    checked = None
+    if args.check:
+        checked = check_against_oracle(args, snap[0], snap[1], snap[2], g0, nloc, N, r0, r1, world, gather_sketches)
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline:
+        # the host CPUs this job may use: OMP_NUM_THREADS (the GPU box sets it to
+        # the job's share, 16 per GPU), else every visible CPU
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-        threads = max(1, min(threads, 16))
-        cpu = cpu_baseline(args, threads)
+        cpu = cpu_baseline(args, max(1, threads))
 
     if rank == 0:
         out = {
@@ -444,8 +520,10 @@ def main():
             "dtype": "u64",
             "data": "synthetic (on-device splitmix64 genome families, 2-bit packed; see DESIGN.md)",
             "config": {
-                "workload": "%d synthetic %d bp genomes, k=21, s=%d (%s); "
-                            "step = sketch + RCCL all-gather + all-pairs" % (N, L, s, config_name(N, L, s)),
+                "workload": "%d synthetic %d bp genomes, k=21, s=%d (%s); step = %s"
+                            % (N, L, s, config_name(N, L, s),
+                               "sketch shard + RCCL all-gather of sketches + all-pairs row shard" if world > 1
+                               else "sketch + all-pairs (one GPU: no all-gather)"),
                 "genomes": N, "genome_bp": L, "k": 21, "sketch": s, "family_size": args.family_size,
                 "parallelism": "sketch: genome shards; all-pairs: balanced row shards; RCCL all-gather",
                 "host_loop": ("pipelined: step i+1 queued before step i's checks" if args.pipeline
@@ -480,10 +558,10 @@ def main():
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": traffic,
                 "note": "algorithmic bytes = 0.375 B/base (2-bit code + validity bit) x bases per "
-                        "launch; the binding limit is VALU issue (Murmur3, ~67 instructions per "
-                        "k-mer) with the LDS table lookups as a co-limit: see valu_model and pmc",
+                        "launch; HBM is not the limit: the kernel is VALU-issue bound (Murmur3, ~65 "
+                        "VALU instructions per k-mer), see valu_model",
                 "valu_model": valu,
-                "pmc": pmc_block(SKETCH_PMC),
+                "pmc": pmc_sk,
             },
             "dist_kernel": {
                 "kernel": "k_allpairs_q (s <= 2048) / k_allpairs_band",
@@ -496,6 +574,10 @@ def main():
             },
             "cpu_baseline": cpu,
         }
+        if checked is not None:
+            out["verified"] = checked["verified"]
+            out["verification"] = dict(checked, how="timed steps' outputs vs the C oracle: sampled genomes "
+                                       "re-sketched on the host; random pairs + one whole row re-merged")
         if verified is not None:
             out["verified_against_single_gpu"] = verified
         print(json.dumps(out))

@@ -73,7 +73,7 @@ SIGNATURES = {
     "drephip_linkage": (C.c_int, [vp, f64p, C.c_uint32, C.c_int, f64p]),
     "drephip_linkage_counts_device": (C.c_int, [vp, vp, vp, C.c_uint32, u32p, f64p, C.c_uint32,
                                                 np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS"),
-                                                C.c_int, f64p]),
+                                                C.c_int, f64p, vp]),
     "drephip_set_timing": (C.c_int, [vp, C.c_int]),
     "drephip_last_kernel_ms": (C.c_int, [vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
 }
@@ -220,15 +220,17 @@ class Context:
         return Z
 
     def linkage_counts_device(self, d_common: int, d_denom: Optional[int], n: int, perm: np.ndarray,
-                              lut: np.ndarray, lut_off: np.ndarray, method: str) -> np.ndarray:
+                              lut: np.ndarray, lut_off: np.ndarray, method: str,
+                              stream: Optional[int] = None) -> np.ndarray:
         """linkage() of the distances given by device-resident all-pairs counts
-        (see drephip_linkage_counts_device)."""
+        (see drephip_linkage_counts_device); the counts are read after the work
+        queued on `stream`."""
         Z = np.zeros((max(n - 1, 0), 4), dtype=np.float64)
         if n >= 2:
             check(lib().drephip_linkage_counts_device(
                 self._h, d_common, d_denom, n, np.ascontiguousarray(perm, dtype=np.uint32),
                 np.ascontiguousarray(lut, dtype=np.float64), len(lut),
-                np.ascontiguousarray(lut_off, dtype=np.int32), self.LINK_METHODS[method], Z.reshape(-1)),
+                np.ascontiguousarray(lut_off, dtype=np.int32), self.LINK_METHODS[method], Z.reshape(-1), stream),
                 "drephip_linkage_counts_device")
         return Z
 

@@ -114,7 +114,7 @@ __global__ __launch_bounds__(1024) void k_build_q32(const uint64_t *__restrict__
                                                    const uint32_t *__restrict__ nhash, uint32_t s,
                                                    uint32_t row0, uint32_t row1, uint32_t B, uint32_t R,
                                                    uint32_t *__restrict__ blk, uint32_t stride,
-                                                   uint8_t *__restrict__ fam_out, uint32_t *__restrict__ nfail) {
+                                                   uint8_t *__restrict__ fam_out) {
     extern __shared__ uint32_t Tb[];
     __shared__ int fail;
     const uint32_t H = 1u << B, hm = H - 1;
@@ -149,7 +149,30 @@ __global__ __launch_bounds__(1024) void k_build_q32(const uint64_t *__restrict__
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) { fam_out[r] = 0xFF; atomicAdd(nfail, 1u); }
+    if (threadIdx.x == 0) fam_out[r] = 0xFF;          // k_allpairs_q merges this row's pairs literally
+}
+
+// ------------------------------------------------------- literal merge
+// Mash's merge loop for one pair (oracle_dist_pair): walk the union of the two
+// sorted sketches for at most s elements; common = shared hashes seen, denom =
+// union elements seen (topped up from the unwalked tails when < s).
+__device__ __forceinline__ void merge_pair(const uint64_t *__restrict__ a, uint32_t na,
+                                           const uint64_t *__restrict__ b, uint32_t nb, uint32_t s,
+                                           uint32_t &common, uint32_t &denom) {
+    uint32_t x = 0, y = 0, c = 0, d = 0;
+    while (d < s && x < na && y < nb) {
+        const uint64_t u = a[x], v = b[y];
+        if (u < v) x++;
+        else if (v < u) y++;
+        else { x++; y++; c++; }
+        d++;
+    }
+    if (d < s) {
+        if (x < na) { const uint32_t r = na - x; d += (s - d < r) ? s - d : r; }
+        if (y < nb) { const uint32_t r = nb - y; d += (s - d < r) ? s - d : r; }
+    }
+    common = c;
+    denom = d;
 }
 
 // ------------------------------------------------------- probe
@@ -248,7 +271,7 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
                                            const uint32_t *T, const uint32_t *V, uint32_t H, uint32_t hm, uint32_t s,
                                            uint32_t N, uint32_t i0, uint32_t nrows, uint32_t cend, uint32_t c_first,
                                            uint32_t c_step, const uint32_t (&nA)[R], const uint32_t (&o1)[R],
-                                           const uint32_t (&o2)[R], const uint64_t (&alast)[R],
+                                           const uint32_t (&o2)[R], const uint64_t (&alast)[R], uint32_t okmask,
                                            bool any_partial_row, uint16_t *__restrict__ common,
                                            uint16_t *__restrict__ denom, uint64_t seg0) {
     const uint32_t lane = threadIdx.x & 63;
@@ -283,7 +306,7 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
 #pragma unroll
         for (int r = 0; r < R; r++) {
             cnt[r] = 0; mrun[r] = 0;
-            const bool act = (uint32_t)r < nrows && i0 + r < c;
+            const bool act = (uint32_t)r < nrows && i0 + r < c && ((okmask >> r) & 1u);
             actmask |= (uint32_t)act << r;
             if (act) amax = alast[r] > amax ? alast[r] : amax;
         }
@@ -380,13 +403,15 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
     }
     uint32_t nA[R], o1[R], o2[R];
     uint64_t alast[R];
+    uint32_t failmask = 0;
     bool any_partial_row = false, fast = true;
 #pragma unroll
     for (int r = 0; r < R; r++) {
         const bool ok = (uint32_t)r < nrows;
         nA[r] = ok ? nhash[i0 + r] : s;
         uint32_t f = ok ? fam[i0 - row0 + r] : 0;
-        f = f < kMaxFam ? f : 0;        // failed table (0xFF): output discarded, the host reruns the merge kernel
+        failmask |= (uint32_t)(f >= kMaxFam) << r;   // no field family worked: merged literally below
+        f = f < kMaxFam ? f : 0;
         const QFields q = qfields(f);
         o1[r] = q.o1; o2[r] = q.o2;
         fast &= f == 0;
@@ -396,10 +421,25 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
     __syncthreads();
     if (fast)
         ap_columns<R, NCH, true>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend, c0 + wave, WG / 64,
-                                 nA, o1, o2, alast, any_partial_row, common, denom, seg0);
+                                 nA, o1, o2, alast, ~failmask, any_partial_row, common, denom, seg0);
     else
         ap_columns<R, NCH, false>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend, c0 + wave, WG / 64,
-                                  nA, o1, o2, alast, any_partial_row, common, denom, seg0);
+                                  nA, o1, o2, alast, ~failmask, any_partial_row, common, denom, seg0);
+    if (failmask) {
+        // a row whose table could not be built (three of its keys share a low
+        // word under every field family; never observed on real sketches):
+        // its pairs of this item by Mash's literal merge, one lane per pair
+        const uint32_t ncol = cend - c0;
+        for (uint32_t t = tid; t < (uint32_t)R * ncol; t += WG) {
+            const uint32_t r = t / ncol, c = c0 + t % ncol, i = i0 + r;
+            if (!((failmask >> r) & 1u) || c <= i) continue;
+            uint32_t cm, dd;
+            merge_pair(hashes + (uint64_t)i * s, nhash[i], hashes + (uint64_t)c * s, nhash[c], s, cm, dd);
+            const uint64_t o = cond_index(i, c, N) - seg0;
+            common[o] = (uint16_t)cm;
+            if (denom) denom[o] = (uint16_t)dd;
+        }
+    }
 }
 
 // ------------------------------------------------------- literal merge
@@ -418,21 +458,8 @@ __global__ __launch_bounds__(256) void k_allpairs_merge(const uint64_t *__restri
     while (i > 0 && cond_index(i, i + 1, N) > idx) i--;
     while (i + 1 < (int64_t)N - 1 && cond_index(i + 1, i + 2, N) <= idx) i++;
     const uint64_t j = idx - cond_index(i, i + 1, N) + i + 1;
-    const uint64_t *a = hashes + (uint64_t)i * s;
-    const uint64_t *b = hashes + j * s;
-    const uint32_t na = nhash[i], nb = nhash[j];
-    uint32_t x = 0, y = 0, c = 0, d = 0;
-    while (d < s && x < na && y < nb) {
-        const uint64_t u = a[x], v = b[y];
-        if (u < v) x++;
-        else if (v < u) y++;
-        else { x++; y++; c++; }
-        d++;
-    }
-    if (d < s) {
-        if (x < na) { const uint32_t r = na - x; d += (s - d < r) ? s - d : r; }
-        if (y < nb) { const uint32_t r = nb - y; d += (s - d < r) ? s - d : r; }
-    }
+    uint32_t c, d;
+    merge_pair(hashes + (uint64_t)i * s, nhash[i], hashes + j * s, nhash[j], s, c, d);
     common[t] = (uint16_t)c;
     if (denom) denom[t] = (uint16_t)d;
 }
@@ -831,8 +858,8 @@ static int launch_q(drephip_ctx *ctx, uint32_t nitems, size_t lds, hipStream_t s
 int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N,
                          uint32_t row0, uint32_t row1, uint16_t *d_common, uint16_t *d_denom,
                          hipStream_t st, bool force_merge, bool defer) {
-    // a deferred call's failure count must be read before this call's build
-    // adds to the shared counter
+    // an earlier deferred call completes first (its queued item-list copy
+    // reads host memory this call may replace)
     if (ctx->apend.active) {
         int rc = allpairs_wait_impl(ctx);
         if (rc) return rc;
@@ -872,24 +899,15 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
     const uint32_t stride = (uint32_t)((q_lds_bytes(R, TS, s) / 4 + 3) & ~3ull);   // words, 16-B multiple
     uint32_t *d_blk;
     uint8_t *d_fam;
-    uint32_t *d_nfail;
     uint2 *d_items;
     int rc;
     if ((rc = scratch(ctx, "ap_blk", (uint64_t)ngroups * stride * 4, (void **)&d_blk))) return rc;
     if ((rc = scratch(ctx, "ap_fam", (uint64_t)ngroups * R, (void **)&d_fam))) return rc;
-    if ((rc = scratch(ctx, "ap_nfail", 4, (void **)&d_nfail))) return rc;
-    // the failure counter is never reset: a call's failures are the growth
-    // since the value the previous call read back (zeroed once per allocation)
-    if (ctx->ap_nfail_ptr != d_nfail) {
-        HIPC(hipMemsetAsync(d_nfail, 0, 4, st));
-        ctx->ap_nfail_ptr = d_nfail;
-        ctx->ap_nfail_seen = 0;
-    }
     const size_t blds = (size_t)TS * 4;
     HIPC(hipFuncSetAttribute((const void *)k_build_q32, hipFuncAttributeMaxDynamicSharedMemorySize, (int)blds));
     timing_mark(ctx, 3, st, true);
     hipLaunchKernelGGL(k_build_q32, dim3(ngroups * R), dim3(1024), blds, st, d_hashes, d_nhash, s, row0, row1, B, R,
-                       d_blk, stride, d_fam, d_nfail);
+                       d_blk, stride, d_fam);
     timing_mark(ctx, 3, st, false);
     HIPC(hipGetLastError());
     // column tile: the widest (<= kApCols) whose item count still gives every
@@ -904,32 +922,28 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
     };
     while (C > kApMinCols && nitems_for(C) < 4ull * 2 * 256) C /= 2;
     // the item list depends only on (N, rows, R, C): reused while the shape and
-    // the scratch allocation are unchanged (repeated calls: bench steps, shards)
+    // the scratch allocation are unchanged (repeated calls: bench steps, shards).
+    // Its host copy lives in the context until the next list replaces it (the
+    // queued H2D copy may still be reading it when a deferred call returns).
     const uint64_t key[5] = {N, row0, row1, R, C};
-    std::vector<uint2> items;
-    uint32_t ni = ctx->ap_items_n;
     const bool reuse = ctx->ap_items_gen == ctx->alloc_gen && !memcmp(ctx->ap_items_key, key, sizeof(key));
     if (!reuse) {
-        items = make_items(row0, row1, N, R, C);
-        ni = (uint32_t)items.size();
+        ctx->ap_items_host = make_items(row0, row1, N, R, C);
+        ctx->ap_items_gen = 0;
     }
+    const uint32_t ni = (uint32_t)ctx->ap_items_host.size();
     if ((rc = scratch(ctx, "ap_items", (uint64_t)ni * sizeof(uint2), (void **)&d_items))) return rc;
     if (!reuse) {
-        HIPC(hipMemcpyAsync(d_items, items.data(), items.size() * sizeof(uint2), hipMemcpyHostToDevice, st));
+        HIPC(hipMemcpyAsync(d_items, ctx->ap_items_host.data(), (uint64_t)ni * sizeof(uint2), hipMemcpyHostToDevice, st));
         memcpy(ctx->ap_items_key, key, sizeof(key));
-        ctx->ap_items_n = ni;
         ctx->ap_items_gen = ctx->alloc_gen;
     }
-    uint32_t *h_nfail;
-    if ((rc = pinned_host(ctx, "ap_nfail", 4, (void **)&h_nfail))) return rc;
-    // the main kernel is queued without waiting for the build's failure count;
-    // in the (never observed) case of a row with no working field family its
-    // output is discarded and the merge kernel recomputes the segment
-
+    // a row whose table cannot be built is merged literally inside the main
+    // kernel (k_allpairs_q): no host round trip, nothing to check afterwards
     const size_t lds = (size_t)stride * 4;
     const uint32_t nch = (s + 63) / 64;
-    // two workgroups per CU when the LDS allows (DREPHIP_AP_ONEWG=1: one, A/B)
-    const bool two = lds <= 80 * 1024 && !getenv("DREPHIP_AP_ONEWG");
+    // two workgroups per CU when the LDS allows
+    const bool two = lds <= 80 * 1024;
 #define DREPHIP_Q(RR, NC) (two ? launch_q<RR, NC, 8>(ctx, ni, lds, st, d_hashes, d_nhash, d_blk, stride, d_fam, N, row0, row1, B, d_items, C, d_common, d_denom, seg0) \
                                : launch_q<RR, NC, 4>(ctx, ni, lds, st, d_hashes, d_nhash, d_blk, stride, d_fam, N, row0, row1, B, d_items, C, d_common, d_denom, seg0))
     if (nch <= 8) {
@@ -955,40 +969,26 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
     }
 #undef DREPHIP_Q
     if (rc) return rc;
-    HIPC(hipMemcpyAsync(h_nfail, d_nfail, 4, hipMemcpyDeviceToHost, st));
-    if (defer && reuse) {
-        // deferred: drephip_allpairs_wait reads the count (after this event)
-        // and runs the merge fallback if a table failed.  Only on a reused
-        // item list: a new one's host vector must outlive its copy (sync below)
+    if (defer) {
+        // drephip_allpairs_wait (or the next all-pairs call) waits for this event
         auto &p = ctx->apend;
         if (!p.ev) HIPC(hipEventCreateWithFlags(&p.ev, hipEventDisableTiming));
         HIPC(hipEventRecord(p.ev, st));
         p.active = true;
-        p.d_hashes = d_hashes; p.d_nhash = d_nhash; p.N = N; p.seg0 = seg0; p.npairs = npairs;
-        p.d_common = d_common; p.d_denom = d_denom; p.st = st; p.h_nfail = h_nfail;
         return DREPHIP_OK;
     }
-    HIPC(hipStreamSynchronize(st));                  // items (host vector) and nfail are safe past here
-    const uint32_t nfail = *h_nfail - ctx->ap_nfail_seen;
-    ctx->ap_nfail_seen = *h_nfail;
-    if (nfail)      // a row table could not be built with any field pair: exact merge kernel instead
-        return launch_merge(ctx, d_hashes, d_nhash, N, seg0, npairs, d_common, d_denom, st);
+    HIPC(hipStreamSynchronize(st));
     return DREPHIP_OK;
 }
 
-// Completes a deferred table-path call (drephip_allpairs_device_async).
+// Completes a deferred table-path call (drephip_allpairs_device_async): waits
+// for its kernels.  Nothing is recomputed here -- the kernels themselves
+// handle every row, including rows whose table could not be built.
 int allpairs_wait_impl(drephip_ctx *ctx) {
     auto &p = ctx->apend;
     if (!p.active) return DREPHIP_OK;
     p.active = false;
     HIPC(hipEventSynchronize(p.ev));
-    const uint32_t nfail = *p.h_nfail - ctx->ap_nfail_seen;
-    ctx->ap_nfail_seen = *p.h_nfail;
-    if (nfail) {
-        int rc = launch_merge(ctx, p.d_hashes, p.d_nhash, p.N, p.seg0, p.npairs, p.d_common, p.d_denom, p.st);
-        if (rc) return rc;
-        HIPC(hipStreamSynchronize(p.st));
-    }
     return DREPHIP_OK;
 }
 

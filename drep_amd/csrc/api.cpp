@@ -122,6 +122,15 @@ using namespace drephip;
 static hipStream_t pick_stream(drephip_ctx *, void *stream) { return (hipStream_t)stream; }
 static void pend_release(drephip_ctx *ctx);
 
+// A deferred sketch (drephip_sketch_device_async) owns the sketch scratch and
+// its status check until drephip_sketch_wait: any other sketch call is refused
+// rather than dropping that check or reusing scratch its kernels still read.
+static int refuse_if_pending(drephip_ctx *ctx) {
+    if (!ctx->pend.active) return DREPHIP_OK;
+    set_error("a deferred sketch (drephip_sketch_device_async) is pending: call drephip_sketch_wait first");
+    return DREPHIP_ERR_ARG;
+}
+
 DREPHIP_EXPORT int drephip_version(void) { return 100; }
 
 DREPHIP_EXPORT const char *drephip_last_error(void) { return g_err.c_str(); }
@@ -157,8 +166,6 @@ DREPHIP_EXPORT int drephip_create(int device, int k, uint32_t s, uint32_t seed, 
     drephip_ctx *c = new (std::nothrow) drephip_ctx();
     if (!c) { set_error("out of host memory"); return DREPHIP_ERR_NOMEM; }
     c->device = device; c->k = k; c->s = s; c->seed = seed;
-    if (const char *v = getenv("DREPHIP_SKETCH_KERNEL")) c->sketch_kernel = atoi(v);
-    if (const char *v = getenv("DREPHIP_FINALIZE")) c->finalize_kernel = atoi(v);
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) { delete c; set_error(hipGetErrorString(e)); return DREPHIP_ERR_HIP; }
     *out = c;
@@ -256,13 +263,13 @@ static int sketch_packed_host(drephip_ctx *ctx, const uint32_t *codes, uint64_t 
     uint32_t *d_codes, *d_valid, *d_nhash;
     uint64_t *d_hashes;
     int rc;
+    if ((rc = refuse_if_pending(ctx))) return rc;
     if ((rc = scratch(ctx, "in_codes", n_codes * 4, (void **)&d_codes))) return rc;
     if ((rc = scratch(ctx, "in_valid", n_valid * 4, (void **)&d_valid))) return rc;
     if ((rc = scratch(ctx, "out_hashes", (uint64_t)n * ctx->s * 8, (void **)&d_hashes))) return rc;
     if ((rc = scratch(ctx, "out_nhash", n * 4ull, (void **)&d_nhash))) return rc;
     HIPC(hipMemcpyAsync(d_codes, codes, n_codes * 4, hipMemcpyHostToDevice, st));
     HIPC(hipMemcpyAsync(d_valid, valid, n_valid * 4, hipMemcpyHostToDevice, st));
-    pend_release(ctx);
     timing_begin(ctx);
     rc = sketch_device_impl(ctx, d_codes, d_valid, off.data(), pad.data(), nk.data(), n, d_hashes, d_nhash, st);
     if (rc) return rc;
@@ -391,11 +398,12 @@ DREPHIP_EXPORT int drephip_sketch_device(drephip_ctx *ctx, const uint32_t *d_cod
     if (!d_codes || !d_valid || !h_base_off || !h_padded || !h_nkmers || !d_hashes || !d_nhash) {
         set_error("null argument"); return DREPHIP_ERR_ARG;
     }
+    int rc;
+    if ((rc = refuse_if_pending(ctx))) return rc;
     hipStream_t st = pick_stream(ctx, stream);
-    pend_release(ctx);
     timing_begin(ctx);
-    int rc = sketch_device_impl(ctx, d_codes, d_valid, h_base_off, h_padded, h_nkmers, n_genomes, d_hashes,
-                                d_nhash, st);
+    rc = sketch_device_impl(ctx, d_codes, d_valid, h_base_off, h_padded, h_nkmers, n_genomes, d_hashes,
+                            d_nhash, st);
     if (rc) return rc;
     timing_collect(ctx);
     return DREPHIP_OK;
@@ -415,15 +423,16 @@ DREPHIP_EXPORT int drephip_sketch_device_async(drephip_ctx *ctx, const uint32_t 
                                                const uint64_t *h_nkmers, uint32_t n_genomes, uint64_t *d_hashes,
                                                uint32_t *d_nhash, void *stream) {
     GUARD_CTX(ctx);
-    pend_release(ctx);                                 // an earlier call never waited on: forget it
+    int rc;
+    if ((rc = refuse_if_pending(ctx))) return rc;
     if (n_genomes == 0) return DREPHIP_OK;
     if (!d_codes || !d_valid || !h_base_off || !h_padded || !h_nkmers || !d_hashes || !d_nhash) {
         set_error("null argument"); return DREPHIP_ERR_ARG;
     }
     hipStream_t st = pick_stream(ctx, stream);
     timing_begin(ctx);
-    int rc = sketch_device_impl(ctx, d_codes, d_valid, h_base_off, h_padded, h_nkmers, n_genomes, d_hashes,
-                                d_nhash, st, true);
+    rc = sketch_device_impl(ctx, d_codes, d_valid, h_base_off, h_padded, h_nkmers, n_genomes, d_hashes,
+                            d_nhash, st, true);
     if (rc) { ctx->pend.active = false; return rc; }
     // the queued kernels' events leave the pool until drephip_sketch_wait reads them
     auto &p = ctx->pend;
@@ -605,21 +614,31 @@ DREPHIP_EXPORT int drephip_linkage(drephip_ctx *ctx, const double *y, uint32_t n
 
 DREPHIP_EXPORT int drephip_linkage_counts_device(drephip_ctx *ctx, const uint16_t *d_common, const uint16_t *d_denom,
                                                  uint32_t n, const uint32_t *perm, const double *lut,
-                                                 uint32_t lut_len, const int32_t *lut_off, int method, double *Z) {
+                                                 uint32_t lut_len, const int32_t *lut_off, int method, double *Z,
+                                                 void *stream) {
     GUARD_CTX(ctx);
     if (n < 2) return DREPHIP_OK;
     if (!d_common || !perm || !lut || !lut_off || !Z) { set_error("null argument"); return DREPHIP_ERR_ARG; }
     if (n > 200000) { set_error("linkage supports n <= 200000 (n x n f64 matrix in HBM)"); return DREPHIP_ERR_UNSUPPORTED; }
     for (uint32_t d = 0; d <= ctx->s; d++)
         if (lut_off[d] >= 0 && (uint64_t)lut_off[d] + d + 1 > lut_len) { set_error("lut_off/lut_len mismatch"); return DREPHIP_ERR_ARG; }
+    if (!d_denom && lut_off[ctx->s] < 0) {
+        set_error("d_denom is NULL (every denominator is s) but lut_off[s] < 0");
+        return DREPHIP_ERR_ARG;
+    }
     std::vector<char> seen(n, 0);
     for (uint32_t i = 0; i < n; i++) {
         if (perm[i] >= n || seen[perm[i]]) { set_error("perm is not a permutation of 0..n-1"); return DREPHIP_ERR_ARG; }
         seen[perm[i]] = 1;
     }
+    // the counts are read after everything the caller queued on `stream`
+    // (e.g. the all-pairs call that wrote them, deferred or not)
+    int rc = allpairs_wait_impl(ctx);
+    if (rc) return rc;
+    HIPC(hipStreamSynchronize(pick_stream(ctx, stream)));
     timing_begin(ctx);
     double *d_D;
-    int rc = dist_matrix_impl(ctx, d_common, d_denom, n, perm, lut, lut_len, lut_off, &d_D, ctx->stream);
+    rc = dist_matrix_impl(ctx, d_common, d_denom, n, perm, lut, lut_len, lut_off, &d_D, ctx->stream);
     if (rc) return rc;
     rc = linkage_device_impl(ctx, d_D, n, method, Z, ctx->stream);
     if (rc) return rc;

@@ -24,8 +24,6 @@ struct drephip_ctx {
     uint32_t timing = 0;      // bitmask of timed kernels (bit w = `which` w of drephip_last_kernel_ms)
     int ap_path = 0;          // DREPHIP_AP_*: 0 auto (table for s <= 2048, else band)
     uint32_t band_cap = 1024; // elements per row per band of the banded all-pairs kernel (clamped to its LDS budget)
-    int finalize_kernel = 1;  // 1 = bucket sort (default), 0 = bitonic sort (A/B); env DREPHIP_FINALIZE
-    int sketch_kernel = 9;    // 9 = v5 with split TT tables (default), 5 = v4 + body tables, 4 = table-driven v4, 3 = rolled-window v3; env DREPHIP_SKETCH_KERNEL (A/B)
     // named grow-only device scratch buffers
     std::map<std::string, DevBuf> bufs;
     // per-kernel timing of the last call: {sum ms, launches}
@@ -46,18 +44,18 @@ struct drephip_ctx {
     uint32_t sk_clean_n = 0;
     uint64_t sk_clean_gen = 0;   // alloc_gen when they were last left clean
     uint64_t sk_gen = 0;
+    uint64_t sk_tab_gen = 0;     // alloc_gen when the Murmur table image was built
     // pinned host staging for the small per-call readbacks (status, failure count)
     std::map<std::string, DevBuf> pinned;
     // all-pairs work-item list of the last call, reused on the same shape
+    // (host copy kept: a deferred call's H2D copy of it may still be queued)
     uint64_t ap_items_key[5] = {0, 0, 0, 0, 0};
     uint64_t ap_items_gen = 0;
-    uint32_t ap_items_n = 0;
-    // table-build failure counter of the whole-row all-pairs path (never reset)
-    uint32_t *ap_nfail_ptr = nullptr;
-    uint32_t ap_nfail_seen = 0;
+    std::vector<uint2> ap_items_host;
     // deferred sketch (drephip_sketch_device_async): the first round is queued
     // without reading its status back; drephip_sketch_wait checks it (and
-    // reruns the call synchronously if a genome needs another threshold round)
+    // reruns the call synchronously if a genome needs another threshold round).
+    // While it is pending, every other sketch call on the context is refused.
     struct PendingSketch {
         bool active = false;
         const uint32_t *d_codes = nullptr, *d_valid = nullptr;
@@ -71,17 +69,11 @@ struct drephip_ctx {
         std::vector<hipEvent_t> events;        // their events, out of ev_pool until collected
         hipEvent_t done = nullptr;             // after the status copy
     } pend;
-    // deferred all-pairs check (drephip_allpairs_device_async, table path)
+    // deferred all-pairs call (drephip_allpairs_device_async, table path):
+    // an event after its kernels
     struct PendingAllpairs {
         bool active = false;
-        hipEvent_t ev = nullptr;               // after the failure-count copy
-        const uint64_t *d_hashes = nullptr;
-        const uint32_t *d_nhash = nullptr;
-        uint32_t N = 0;
-        uint64_t seg0 = 0, npairs = 0;
-        uint16_t *d_common = nullptr, *d_denom = nullptr;
-        hipStream_t st = nullptr;
-        const uint32_t *h_nfail = nullptr;
+        hipEvent_t ev = nullptr;
     } apend;
 };
 

@@ -227,11 +227,14 @@ __global__ __launch_bounds__(kLkWG) void k_mst_step(const double *__restrict__ D
 
 // ------------------------------------------------------------ matrix build
 // D[p(i)][p(j)] = D[p(j)][p(i)] = lut[off[denom] + common] for the condensed
-// pair (i, j) of the all-pairs output (denom = s when d_denom is null).
+// pair (i, j) of the all-pairs output (denom = s when d_denom is null).  A
+// pair whose denominator has no table (off < 0), or whose count exceeds its
+// denominator, sets *bad and gets NaN (the host then refuses the result).
 __global__ __launch_bounds__(kLkWG) void k_dist_matrix(const uint16_t *__restrict__ common,
                                                       const uint16_t *__restrict__ denom, uint32_t s, uint32_t n,
                                                       const uint32_t *__restrict__ perm, const double *__restrict__ lut,
-                                                      const int32_t *__restrict__ off, double *__restrict__ D) {
+                                                      const int32_t *__restrict__ off, double *__restrict__ D,
+                                                      uint32_t *__restrict__ bad) {
     const uint32_t i = blockIdx.x;
     const uint64_t base = (uint64_t)i * n - (uint64_t)i * (i + 1) / 2;   // condensed index of (i, i+1), minus 1
     const uint32_t pi = perm[i];
@@ -239,7 +242,11 @@ __global__ __launch_bounds__(kLkWG) void k_dist_matrix(const uint16_t *__restric
     for (uint32_t j = i + 1 + threadIdx.x; j < n; j += kLkWG) {
         const uint64_t t = base + (j - i - 1);
         const uint32_t dn = denom ? denom[t] : s;
-        const double v = lut[off[dn] + common[t]];
+        const uint32_t cm = common[t];
+        const int32_t o = dn <= s ? off[dn] : -1;
+        double v;
+        if (o >= 0 && cm <= dn) v = lut[o + cm];
+        else { v = __builtin_nan(""); atomicOr(bad, 1u); }
         const uint32_t pj = perm[j];
         D[(uint64_t)pi * n + pj] = v;
         D[(uint64_t)pj * n + pi] = v;
@@ -380,20 +387,30 @@ int dist_matrix_impl(drephip_ctx *ctx, const uint16_t *d_common, const uint16_t 
                      double **d_D_out, hipStream_t st) {
     const uint32_t s = ctx->s;
     double *d_D, *d_lut;
-    uint32_t *d_perm;
+    uint32_t *d_perm, *d_bad, *h_bad;
     int32_t *d_off;
     int rc;
     if ((rc = scratch(ctx, "lk_D", (uint64_t)n * n * 8, (void **)&d_D))) return rc;
     if ((rc = scratch(ctx, "lk_perm", n * 4ull, (void **)&d_perm))) return rc;
+    if ((rc = scratch(ctx, "lk_bad", 4, (void **)&d_bad))) return rc;
+    if ((rc = pinned_host(ctx, "lk_bad", 4, (void **)&h_bad))) return rc;
+    HIPC(hipMemsetAsync(d_bad, 0, 4, st));
     if ((rc = scratch(ctx, "lk_lut", lut_len * 8ull, (void **)&d_lut))) return rc;
     if ((rc = scratch(ctx, "lk_off", (s + 1) * 4ull, (void **)&d_off))) return rc;
     HIPC(hipMemcpyAsync(d_perm, perm, n * 4ull, hipMemcpyHostToDevice, st));
     HIPC(hipMemcpyAsync(d_lut, lut, lut_len * 8ull, hipMemcpyHostToDevice, st));
     HIPC(hipMemcpyAsync(d_off, lut_off, (s + 1) * 4ull, hipMemcpyHostToDevice, st));
     timing_mark(ctx, 3, st, true);
-    hipLaunchKernelGGL(k_dist_matrix, dim3(n), dim3(kLkWG), 0, st, d_common, d_denom, s, n, d_perm, d_lut, d_off, d_D);
+    hipLaunchKernelGGL(k_dist_matrix, dim3(n), dim3(kLkWG), 0, st, d_common, d_denom, s, n, d_perm, d_lut, d_off, d_D,
+                       d_bad);
     timing_mark(ctx, 3, st, false);
     HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(h_bad, d_bad, 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    if (*h_bad) {
+        set_error("a pair's denominator has no distance table (lut_off < 0) or its count exceeds it");
+        return DREPHIP_ERR_ARG;
+    }
     *d_D_out = d_D;
     return DREPHIP_OK;
 }

@@ -2,7 +2,7 @@
 // genome (drep/d_cluster.py:531-549) and `mash paste` (551-567).
 //
 // Three kernels, one pass over the packed genome set per round:
-//   k_sketch_hash21_v4  one workgroup per 32768-base tile; each lane covers 128
+//   k_sketch_hash21   one workgroup per 32768-base tile; each lane covers 128
 //                     window ends (2-bit codes + validity from HBM, one load
 //                     per 16 bases), cuts the forward and reverse-complement
 //                     k-mers out of the code stream, hashes the canonical one
@@ -12,17 +12,16 @@
 //                     hashes are staged in LDS and, after the tile, inserted
 //                     into a per-genome open-addressing set in HBM (64-bit CAS),
 //                     so duplicates drop out at insert.
-//   k_sketch_finalize_bucket one workgroup per genome: bucket-sorts the set in LDS
-//                     and writes the s smallest (k_sketch_finalize: bitonic, A/B).
+//   k_sketch_finalize_bucket one workgroup per genome: bucket-sorts the set in
+//                     LDS and writes the s smallest.
 //   k_synth           bench input generator (not on the product path).
 // The threshold is seeded from the k-mer count so ~F*s distinct candidates
 // survive; a genome whose set ends with fewer than s distinct hashes (T too
 // low) or more than the LDS sort holds (T too high) is re-run with a bisected
 // T -- exact for every input, normally a single round.
 //
-// Roofline: integer VALU issue (v4: ~76 VALU instructions per k-mer, 18 of
-// them multiply-class, tools/isa_count.py); HBM traffic is 3 bits/base
-// (0.375 B/base) plus the candidate sets.
+// Roofline: integer VALU issue and LDS table reads (see k_sketch_hash21);
+// HBM traffic is 3 bits/base (0.375 B/base) plus the candidate sets.
 
 #include "ctx.h"
 #include "../../include/drephip.h"
@@ -78,70 +77,14 @@ __device__ __forceinline__ uint64_t fmix64_pre(uint64_t k) {
     k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ULL;
     return k;
 }
-__device__ __forceinline__ uint64_t fmix64_v(uint64_t k) {
-    k ^= k >> 33; k *= 0xff51afd7ed558ccdULL;
-    k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ULL;
-    k ^= k >> 33; return k;
-}
-__device__ __forceinline__ uint64_t murmur21(uint64_t k1, uint64_t k2, uint64_t k3, uint32_t seed) {
-    constexpr uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
-    uint64_t h1 = seed, h2 = seed;
-    k1 *= c1; k1 = rotl64_ab(k1, 31); k1 *= c2; h1 ^= k1;
-    h1 = rotl64_ab(h1, 27); h1 += h2; h1 = x5_plus(h1, 0x52dce729);
-    k2 *= c2; k2 = rotl64_ab(k2, 33); k2 *= c1; h2 ^= k2;
-    h2 = rotl64_ab(h2, 31); h2 += h1; h2 = x5_plus(h2, 0x38495ab5);
-    k3 *= c1; k3 = rotl64_ab(k3, 31); k3 *= c2; h1 ^= k3;
-    h1 ^= 21u; h2 ^= 21u;
-    h1 += h2; h2 += h1;
-    return fmix64_v(h1) + fmix64_v(h2);
-}
-
 // Candidates are staged in an LDS buffer (wave-aggregated LDS atomic) and only
 // flushed to the per-genome set after the tile, so the hot loop issues no
 // global memory operation with a wait; a full buffer spills to the set
 // directly.
-constexpr uint32_t kStage = 512;      // 4 KiB: with the tables, 8 workgroups (32 waves) per CU
-
-// ------------------------------------------------------- hash kernel (v3)
-// Kept for A/B against v4 (DREPHIP_SKETCH_KERNEL=3).  Rolls forward and
-// reverse-complement ASCII windows (one v_alignbit_b32 per word per base) and
-// batches the 16 window ends of one code word: the window rolls serially, the
-// 16 canonical hashes are independent (the compiler interleaves them), and a
-// single admit test per batch replaces 16 per-k-mer branches.  Codes are kept
-// top-aligned (fc: newest base at bits 23:22, older bases fall off bit 63), so
-// no masking is needed: when the top 42 bits of fc and rc are equal the two
-// strings are identical and either choice hashes the same bytes.  Window
-// validity (run of >= 21 valid bases) is evaluated only inside the rare admit
-// branch, from a 64-base validity history.
-struct Window21v3 {
-    uint32_t f[6], r[6];
-    uint64_t fc, rc;
-    __device__ __forceinline__ void init() {
-#pragma unroll
-        for (int i = 0; i < 6; i++) { f[i] = 0; r[i] = 0; }
-        fc = rc = 0;
-    }
-    __device__ __forceinline__ void push(uint32_t c) {
-        fc = (fc << 2) | ((uint64_t)c << 22);
-        rc = (rc >> 2) | ((uint64_t)(c ^ 3u) << 62);
-        const uint32_t sel = c | 0x06050400u;        // byte0 <- LUT[c], bytes1..3 <- src0 bytes 0..2
-#pragma unroll
-        for (int i = 0; i < 5; i++) f[i] = __builtin_amdgcn_alignbit(f[i + 1], f[i], 8);
-        f[5] = __builtin_amdgcn_perm(0u, 0x54474341u, sel);              // ASCII of the new base
-        r[5] = r[4] >> 24;
-#pragma unroll
-        for (int i = 4; i > 0; i--) r[i] = __builtin_amdgcn_alignbit(r[i], r[i - 1], 24);
-        r[0] = __builtin_amdgcn_perm(r[0], 0x41434754u, sel);            // (r0 << 8) | comp ASCII
-    }
-    __device__ __forceinline__ uint64_t hash(uint32_t seed) const {
-        uint32_t w[6];
-        const bool fwd = fc <= rc;
-#pragma unroll
-        for (int i = 0; i < 6; i++) w[i] = fwd ? f[i] : r[i];
-        return murmur21(((uint64_t)w[1] << 32) | w[0], ((uint64_t)w[3] << 32) | w[2],
-                        ((uint64_t)w[5] << 32) | w[4], seed);
-    }
-};
+#ifndef DREPHIP_SK_STAGE
+#define DREPHIP_SK_STAGE 128       // ~13 admitted hashes per tile expected; overflow goes straight to the set
+#endif
+constexpr uint32_t kStage = DREPHIP_SK_STAGE;
 
 // bit i of the result: the 21 bases ending at history bit i are all valid
 __device__ __forceinline__ uint64_t run21(uint64_t v) {
@@ -152,86 +95,13 @@ __device__ __forceinline__ uint64_t run21(uint64_t v) {
     return r16 & (r4 << 16) & (v << 20);
 }
 
-template <int LANE, int BATCH>   // BATCH window ends hashed per admit test (8 or 16)
-__global__ __launch_bounds__(kTile / LANE) void k_sketch_hash21_v3(
-    const uint32_t *__restrict__ codes, const uint32_t *__restrict__ valid,
-    const uint64_t *__restrict__ tile_base, const uint32_t *__restrict__ tile_genome,
-    const uint64_t *__restrict__ thr, unsigned long long *__restrict__ sets,
-    uint32_t *__restrict__ cnt, uint32_t set_log2, uint32_t limit, uint32_t seed) {
-    constexpr uint32_t WG = kTile / LANE;
-    __shared__ uint64_t stage[kStage];
-    __shared__ uint32_t nstage;
-    const uint32_t t = blockIdx.x;
-    const uint32_t g = tile_genome[t];
-    const uint64_t T = thr[g];
-    const uint64_t start = tile_base[t] + (uint64_t)threadIdx.x * LANE;
-    const uint32_t mask = (1u << set_log2) - 1;
-    unsigned long long *S = sets + ((uint64_t)g << set_log2);
-    uint32_t *C = cnt + g;
-    if (threadIdx.x == 0) nstage = 0;
-    const uint32_t *cw = codes + (start - kWarm) / 16;
-    const uint32_t *vw = valid + (start - kWarm) / 32;
-    Window21v3 w;
-    w.init();
-    const uint32_t v0 = vw[0];
-    {
-        const uint32_t c0 = cw[0], c1 = cw[1];
-#pragma unroll
-        for (int b = 0; b < 16; b++) w.push((c0 >> (2 * b)) & 3u);
-#pragma unroll
-        for (int b = 0; b < 16; b++) w.push((c1 >> (2 * b)) & 3u);
-    }
-    uint64_t vhist = (uint64_t)v0 << 32;              // bit 63 = newest base
-    __syncthreads();
-    uint32_t cnext = cw[2];
-    uint32_t vcur = vw[1];
-    for (int wi = 0; wi < (int)(LANE / 16); wi++) {
-        const uint32_t c = cnext;
-        const uint32_t vbits = (vcur >> ((wi & 1) * 16)) & 0xffffu;
-        if (wi + 1 < (int)(LANE / 16)) {
-            cnext = cw[3 + wi];
-            if (wi & 1) vcur = vw[2 + (wi >> 1)];
-        }
-        vhist = (vhist >> 16) | ((uint64_t)vbits << 48);
-#pragma unroll
-        for (int b0 = 0; b0 < 16; b0 += BATCH) {
-            uint64_t h[BATCH];
-            bool hit = false;
-#pragma unroll
-            for (int b = 0; b < BATCH; b++) {
-                w.push((c >> (2 * (b0 + b))) & 3u);
-                h[b] = w.hash(seed);
-                hit |= h[b] <= T;
-            }
-            if (__builtin_expect(hit, 0)) {
-                const uint64_t ok = run21(vhist);
-#pragma unroll
-                for (int b = 0; b < BATCH; b++) {
-                    if (h[b] <= T && ((ok >> (48 + b0 + b)) & 1)) {
-                        const uint32_t slot = atomicAdd(&nstage, 1u);
-                        if (slot < kStage) stage[slot] = h[b];
-                        else set_insert(S, mask, C, limit, h[b]);
-                    }
-                }
-            }
-        }
-    }
-    __syncthreads();
-    const uint32_t n = min(nstage, kStage);
-    for (uint32_t i = threadIdx.x; i < n; i += WG) set_insert(S, mask, C, limit, stage[i]);
-}
-
-// ------------------------------------------------------- hash kernel (v4)
-// No rolled ASCII windows: the forward and reverse-complement k-mers are cut
-// out of the 2-bit code stream with two v_alignbit_b32 each (no loop-carried
-// state), the canonical one is chosen on the codes, and the parts of Murmur
-// that depend only on a few bases come from LDS tables built per workgroup:
-//   k1*c1 = TA1[bases 0-3] + TB1[bases 4-7] << 32     (k1 = ASCII bytes 0-7)
-//   k2*c2 = TA2[bases 8-11] + TB2[bases 12-15] << 32  (k2 = ASCII bytes 8-15)
-//   tail  = T3[bases 16-20] = rotl31(k3*c1)*c2 ^ 21   (k3 = ASCII bytes 16-20;
-//                                                       ^21 = Murmur's h1 ^= len)
-// (a 64-bit product k*c splits as lo*c + (hi*(uint32)c) << 32).  Of Murmur's
-// ten 64-bit multiplies six remain (two in the body, four in fmix).
+// ------------------------------------------------------------- hash kernel
+// One workgroup of 256 lanes per 32768-base tile; lane l owns the 128 window
+// ends [tile + 128 l, tile + 128 (l + 1)).  No per-base rolling state: the
+// forward and reverse-complement k-mers are cut out of the 2-bit code stream
+// with two v_alignbit_b32 each, the canonical one is chosen on the codes, and
+// the parts of MurmurHash3_x64_128 (seed 42, h1) that depend only on a few
+// bases come from per-workgroup LDS tables.
 //
 // Streams (code word j holds bases 16j..16j+15, base i at bits 2i):
 //   NF[j] = ~F[j]: a 64-bit little-endian cut holding bases q-31..q has base q
@@ -242,9 +112,45 @@ __global__ __launch_bounds__(kTile / LANE) void k_sketch_hash21_v3(
 // memcmp order of the ASCII k-mers = unsigned order of those top-aligned values
 // (A<C<G<T = 0<1<2<3; junk bits never decide: k is odd, so no k-mer equals its
 // reverse complement).
-struct SketchTables {
-    uint64_t ta1[256], ta2[256], t3[1024];
-    uint32_t tb1[256], tb2[256];
+//
+// Murmur's block words are k1 = ASCII of bases 0-7 and k2 = bases 8-15; the
+// tail k3 = bases 16-20.  A 64-bit product k * c splits as
+//     k * c = A03 * c + (A47 * lo(c)) << 32       (A03, A47: ASCII of 4 bases)
+// so X = k1 * c1 has lo(X) = lo(A03 c1) and hi(X) = hi(A03 c1) + A47 lo(c1).
+// Then rotl(X, 31) = (hi(X) >> 1) + (lo(X) << 31) + ((hi(X) & 1) << 63) is a
+// disjoint bit sum and, c2 being odd,
+//     rotl(X, 31) * c2 = (hi(X) >> 1) * c2 + TT1 + ((hi(X) & 1) << 63),
+//     TT1 = (lo(X) << 31) * c2,
+// one v_mad_u64_u32 plus a high-word fix.  Likewise for k2:
+//     rotl(X, 33) * c1 = hi(X) * (2 c1) + TT2,
+//     TT2 = ((lo(X) & 0x7fffffff) << 33) * c1 + (lo(X) >> 31) * c1.
+// The tail is one table entry, rotl31(k3 c1) c2 ^ 21 (Murmur's h1 ^= len).
+//
+// Cost model (measured, profiles/r02_sketch_ab.json): the loop is VALU-issue
+// bound -- its time follows the VALU instruction count (a layout with 17 %
+// more VALU instructions and half the LDS cycles ran 16 % slower), so the
+// tables exist to take VALU work off the loop.  Every lookup index is data
+// dependent: a wave's 64 reads of one instruction hit the LDS banks at
+// random, ~3.2x the conflict-free cycles for 4- and 8-byte reads and ~3x for
+// 16-byte reads (profiles/r02_lds_microbench.json).  Per dword fetched a
+// 16-byte read therefore costs half a 4-byte one, so what a block word needs
+// from its 4-base index is one 16-byte entry {lo(TT), hi(TT), hi(A03 c), 0}
+// (ds_read_b128; TT in the first two words lands in the register pair the
+// v_mad_u64_u32 adds), the A47 lo(c) terms are an 8- and a 4-byte read and
+// the tail one 8-byte read: five reads per k-mer.
+// The k1 word's high-word fix (X << 31) is folded into the tables: mod 2^32
+// it is (hi(A03 c1) << 31) + (A47 lo(c1) << 31), the first added to hi(TT1)
+// (a carry out of the 64-bit addend is discarded, as in the product), the
+// second stored next to A47 lo(c1): one v_add3_u32 instead of a move, a
+// v_mad_u64_u32 and a v_lshl_add_u32.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // one LDS vector load (a struct is split)
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+struct SketchTablesQ {
+    u32x4 e1[256];        // {lo(TT1), hi(TT1) + (hi(A03 c1) << 31), hi(A03 c1), 0}  by bases 0-3
+    u32x4 e2[256];        // {lo(TT2), hi(TT2), hi(A03 c2), 0}                       by bases 8-11
+    u32x2 b1[256];        // {A47 lo(c1), A47 lo(c1) << 31}                         by bases 4-7
+    uint32_t b2[256];     // A47 lo(c2)                                              by bases 12-15
+    uint64_t t3[1024];    // tail, by bases 16-20
 };
 
 __device__ __forceinline__ uint32_t ascii4(uint32_t x) {      // 4 bases, base 0 in bits 6-7
@@ -252,25 +158,50 @@ __device__ __forceinline__ uint32_t ascii4(uint32_t x) {      // 4 bases, base 0
     return __builtin_amdgcn_perm(0u, 0x54474341u, sel);
 }
 
-__device__ void build_tables(SketchTables &tb, uint32_t tid, uint32_t nthreads) {
+__device__ void build_tables(SketchTablesQ &tb, uint32_t tid, uint32_t nthreads) {
     constexpr uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
     for (uint32_t x = tid; x < 256; x += nthreads) {
         const uint32_t a = ascii4(x);
-        tb.ta1[x] = (uint64_t)a * c1;
-        tb.tb1[x] = a * (uint32_t)c1;
-        tb.ta2[x] = (uint64_t)a * c2;
-        tb.tb2[x] = a * (uint32_t)c2;
+        const uint64_t A1 = (uint64_t)a * c1, A2 = (uint64_t)a * c2;
+        const uint32_t x1 = (uint32_t)A1, x2 = (uint32_t)A2;
+        const uint32_t ta1 = (uint32_t)(A1 >> 32), ta2 = (uint32_t)(A2 >> 32);
+        const uint64_t t1 = ((uint64_t)x1 << 31) * c2 + ((uint64_t)(ta1 << 31) << 32);
+        const uint64_t t2 = ((uint64_t)(x2 & 0x7fffffffu) << 33) * c1 + (uint64_t)(x2 >> 31) * c1;
+        tb.e1[x] = u32x4{(uint32_t)t1, (uint32_t)(t1 >> 32), ta1, 0u};
+        tb.e2[x] = u32x4{(uint32_t)t2, (uint32_t)(t2 >> 32), ta2, 0u};
+        const uint32_t m1 = a * (uint32_t)c1;
+        tb.b1[x] = u32x2{m1, m1 << 31};
+        tb.b2[x] = a * (uint32_t)c2;
     }
     for (uint32_t y = tid; y < 1024; y += nthreads) {
         // bases 16..19 = bits 9..2, base 20 = bits 1..0
         const uint64_t k3 = (uint64_t)ascii4(y >> 2) | ((uint64_t)ascii4((y & 3u) << 6) & 0xffu) << 32;
-        tb.t3[y] = (rotl64_ab(k3 * c1, 31) * c2) ^ 21u;   // tail mix, with h1 ^= len folded in
+        tb.t3[y] = (rotl64_ab(k3 * c1, 31) * c2) ^ 21u;
     }
+}
+
+// The tables depend on nothing but the Murmur constants: built once per
+// context into a device image (k_sketch_tables), which every hash workgroup
+// copies into LDS with 16-byte loads (~5 per lane, L2-resident) instead of
+// recomputing ~1,300 entries (the build cost ~1.2 VALU instructions per k-mer).
+constexpr uint32_t kTabVec = sizeof(SketchTablesQ) / 16;
+static_assert(sizeof(SketchTablesQ) % 16 == 0, "table image is copied in 16-byte pieces");
+__global__ __launch_bounds__(256) void k_sketch_tables(SketchTablesQ *__restrict__ img) {
+    __shared__ SketchTablesQ tb;
+    build_tables(tb, threadIdx.x, 256);
+    __syncthreads();
+    const u32x4 *src = (const u32x4 *)&tb;
+    u32x4 *dst = (u32x4 *)img;
+    for (uint32_t i = threadIdx.x; i < kTabVec; i += 256) dst[i] = src[i];
 }
 
 __device__ __forceinline__ uint32_t rev_fields16(uint32_t x) {     // reverse the 16 2-bit fields
     const uint32_t y = __builtin_bitreverse32(x);
     return ((y >> 1) & 0x55555555u) | ((y & 0x55555555u) << 1);
+}
+
+__device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {   // one v_mad_u64_u32
+    return (uint64_t)a * b + c;
 }
 
 // Murmur h1 of the canonical k-mer (top-aligned codes hi:lo), returned as the
@@ -280,15 +211,29 @@ __device__ __forceinline__ uint32_t rev_fields16(uint32_t x) {     // reverse th
 // (the low-word sum carries at most 1 into the high word; both sides are
 // taken one past so a wrapping 0xFFFFFFFF + carry = 0 is kept): a one-add,
 // one-compare prefilter; the exact test runs in the rare admit branch.
-__device__ __forceinline__ void murmur21_tab(const SketchTables &tb, uint32_t hi, uint32_t lo, uint32_t seed,
-                                             uint64_t &p1, uint64_t &p2) {
+__device__ __forceinline__ void murmur21_q(const SketchTablesQ &tb, uint32_t hi, uint32_t lo, uint32_t seed,
+                                           uint64_t &p1, uint64_t &p2) {
     constexpr uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
-    const uint64_t a1 = tb.ta1[hi >> 24] + ((uint64_t)tb.tb1[(hi >> 16) & 0xffu] << 32);
-    const uint64_t a2 = tb.ta2[(hi >> 8) & 0xffu] + ((uint64_t)tb.tb2[hi & 0xffu] << 32);
+    constexpr uint64_t d1 = c1 * 2;                                  // 2 c1 mod 2^64
+    const u32x4 e1 = tb.e1[hi >> 24];
+    const u32x2 f1 = tb.b1[(hi >> 16) & 0xffu];
+    const u32x4 e2 = tb.e2[(hi >> 8) & 0xffu];
+    const uint32_t f2 = tb.b2[hi & 0xffu];
     const uint64_t k3 = tb.t3[lo >> 22];
-    uint64_t h1 = (uint64_t)seed ^ (rotl64_ab(a1, 31) * c2);
+    const uint32_t X1 = e1.z + f1.x;                                 // hi(k1 * c1)
+    const uint32_t X2 = e2.z + f2;                                   // hi(k2 * c2)
+    const uint64_t tt1 = ((uint64_t)e1.y << 32) | e1.x;
+    const uint64_t tt2 = ((uint64_t)e2.y << 32) | e2.x;
+    // rotl(k1 c1, 31) c2 ^ seed  (its (X1 << 31) term: in e1.y and f1.y)
+    const uint32_t h = X1 >> 1;
+    const uint64_t P1 = mad64(h, (uint32_t)c2, tt1);
+    const uint32_t g1hi = (uint32_t)(P1 >> 32) + h * (uint32_t)(c2 >> 32) + f1.y;
+    uint64_t h1 = ((uint64_t)g1hi << 32) | ((uint32_t)P1 ^ seed);
     h1 = x5_plus(rotl64_ab(h1, 27), 5ull * seed + 0x52dce729);   // (rotl + seed) * 5 + c
-    uint64_t h2 = (uint64_t)seed ^ (rotl64_ab(a2, 33) * c1);
+    // rotl(k2 c2, 33) c1 ^ seed
+    const uint64_t P2 = mad64(X2, (uint32_t)d1, tt2);
+    const uint32_t g2hi = (uint32_t)(P2 >> 32) + X2 * (uint32_t)(d1 >> 32);
+    uint64_t h2 = ((uint64_t)g2hi << 32) | ((uint32_t)P2 ^ seed);
     h2 = x5_plus(add64(rotl64_ab(h2, 31), h1), 0x38495ab5);
     h1 ^= k3;
     h2 ^= 21u;
@@ -301,28 +246,38 @@ __device__ __forceinline__ uint64_t murmur_fin(uint64_t p1, uint64_t p2) {
     return add64(p1 ^ (p1 >> 33), p2 ^ (p2 >> 33));
 }
 
+#ifndef DREPHIP_SK_BATCH
+#define DREPHIP_SK_BATCH 4          // k-mers per admit test: 50 VGPRs, 8 waves per SIMD (8: 70 VGPRs, 7 waves; 0.2-0.3 % slower)
+#endif
+#ifndef DREPHIP_SK_MINW
+#define DREPHIP_SK_MINW 1
+#endif
 template <int LANE, int BATCH>
-__global__ __launch_bounds__(kTile / LANE) void k_sketch_hash21_v4(
-    const uint32_t *__restrict__ codes, const uint32_t *__restrict__ valid,
+__global__ __launch_bounds__(kTile / LANE, DREPHIP_SK_MINW) void k_sketch_hash21(
+    const SketchTablesQ *__restrict__ img, const uint32_t *__restrict__ codes, const uint32_t *__restrict__ valid,
     const uint64_t *__restrict__ tile_base, const uint32_t *__restrict__ tile_genome,
     const uint64_t *__restrict__ thr, unsigned long long *__restrict__ sets,
     uint32_t *__restrict__ cnt, uint32_t set_log2, uint32_t limit, uint32_t seed, uint64_t wlast) {
     constexpr uint32_t WG = kTile / LANE;
     constexpr int NCH = LANE / 16;
-    __shared__ SketchTables tb;
+    __shared__ SketchTablesQ tb;
     __shared__ uint64_t stage[kStage];
     __shared__ uint32_t nstage;
     const uint32_t t = blockIdx.x;
     const uint32_t g = tile_genome[t];
     const uint64_t T = thr[g];
     const uint32_t Thi = (uint32_t)(T >> 32);
-    const uint32_t Tp = Thi == 0xFFFFFFFFu ? Thi : Thi + 1;     // prefilter bound (see murmur21_tab)
+    const uint32_t Tp = Thi == 0xFFFFFFFFu ? Thi : Thi + 1;     // prefilter bound (see murmur21_q)
     const uint64_t start = tile_base[t] + (uint64_t)threadIdx.x * LANE;
     const uint32_t mask = (1u << set_log2) - 1;
     unsigned long long *S = sets + ((uint64_t)g << set_log2);
     uint32_t *C = cnt + g;
     if (threadIdx.x == 0) nstage = 0;
-    build_tables(tb, threadIdx.x, WG);
+    {
+        const u32x4 *src = (const u32x4 *)img;
+        u32x4 *dst = (u32x4 *)&tb;
+        for (uint32_t i = threadIdx.x; i < kTabVec; i += WG) dst[i] = src[i];
+    }
 
     const uint64_t m0 = start / 16;                  // code word of the lane's first window end
     auto ld = [&](int j) -> uint32_t {               // clamp: the cut after the last word is junk
@@ -370,7 +325,7 @@ __global__ __launch_bounds__(kTile / LANE) void k_sketch_hash21_v4(
                 const uint64_t fw = ((uint64_t)fhi << 32) | flo;
                 const uint64_t rc = ((uint64_t)chi << 32) | clo;
                 const uint64_t cc = fw <= rc ? fw : rc;
-                murmur21_tab(tb, (uint32_t)(cc >> 32), (uint32_t)cc, seed, p1[b], p2[b]);
+                murmur21_q(tb, (uint32_t)(cc >> 32), (uint32_t)cc, seed, p1[b], p2[b]);
                 hit |= (uint32_t)(p1[b] >> 32) + (uint32_t)(p2[b] >> 32) + 1u <= Tp;
             }
             if (__builtin_expect(hit, 0)) {
@@ -398,218 +353,6 @@ __global__ __launch_bounds__(kTile / LANE) void k_sketch_hash21_v4(
     for (uint32_t i = threadIdx.x; i < n; i += WG) set_insert(S, mask, C, limit, stage[i]);
 }
 
-// ------------------------------------------------------- hash kernel (v5)
-// v4 with the two Murmur body multiplies folded into tables.  For block word
-// k1 (bases 0-7): X = k1*c1 = TA1[x] + TB1[y] << 32, so Xlo = lo(TA1[x]) and
-// Xhi = hi(TA1[x]) + TB1[y]; rotl(X, 31) is the disjoint bit sum
-//     (Xhi >> 1) + (Xlo << 31) + ((Xhi & 1) << 63)
-// and, c2 being odd,
-//     rotl(X, 31) * c2 = (Xhi >> 1) * c2 + TT1[x] + ((Xhi & 1) << 63),
-//     TT1[x] = (Xlo << 31) * c2                      (one table per 4 bases)
-//     -> one v_mad_u64_u32 (h * lo(c2) + TT1) and a high-word fix
-//        h * hi(c2) + (Xhi << 31).
-// For k2 (bases 8-15): X = k2*c2, rotl(X, 33) = ((Xlo & 0x7fffffff) << 33) +
-// (Xlo >> 31) + 2 Xhi, so
-//     rotl(X, 33) * c1 = Xhi * (2 c1) + TT2[x'],
-//     TT2[x'] = ((Xlo & 0x7fffffff) << 33) * c1 + (Xlo >> 31) * c1.
-// Saves two rotates, a 32x32 multiply and an add per block word (measured-cost
-// model: ~9 % of the k-mer's VALU time) for two more LDS reads per k-mer.
-struct SketchTables5 {
-    uint64_t tt1[256], tt2[256], t3[1024];
-    uint32_t ta1[256], ta2[256], tb1[256], tb2[256];   // ta = hi(a * c)
-};
-
-__device__ void build_tables5(SketchTables5 &tb, uint32_t tid, uint32_t nthreads) {
-    constexpr uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
-    for (uint32_t x = tid; x < 256; x += nthreads) {
-        const uint32_t a = ascii4(x);
-        const uint64_t A1 = (uint64_t)a * c1, A2 = (uint64_t)a * c2;
-        const uint32_t x1 = (uint32_t)A1, x2 = (uint32_t)A2;
-        tb.tt1[x] = ((uint64_t)x1 << 31) * c2;
-        tb.tt2[x] = ((uint64_t)(x2 & 0x7fffffffu) << 33) * c1 + (uint64_t)(x2 >> 31) * c1;
-        tb.ta1[x] = (uint32_t)(A1 >> 32);
-        tb.ta2[x] = (uint32_t)(A2 >> 32);
-        tb.tb1[x] = a * (uint32_t)c1;
-        tb.tb2[x] = a * (uint32_t)c2;
-    }
-    for (uint32_t y = tid; y < 1024; y += nthreads) {
-        const uint64_t k3 = (uint64_t)ascii4(y >> 2) | ((uint64_t)ascii4((y & 3u) << 6) & 0xffu) << 32;
-        tb.t3[y] = (rotl64_ab(k3 * c1, 31) * c2) ^ 21u;
-    }
-}
-
-// v6 layout (A/B): the 64-bit TT tables split into 32-bit halves so that TA,
-// lo(TT) and hi(TT) of one block word are read from ONE address (byte * 4)
-// with three offsets -- two index adds fewer per k-mer, two LDS reads more.
-struct SketchTables6 {
-    uint32_t tt1lo[256], tt1hi[256], ta1[256];
-    uint32_t tt2lo[256], tt2hi[256], ta2[256];
-    uint32_t tb1[256], tb2[256];
-    uint64_t t3[1024];
-};
-__device__ void build_tables(SketchTables5 &tb, uint32_t tid, uint32_t nthreads) { build_tables5(tb, tid, nthreads); }
-__device__ void build_tables(SketchTables6 &tb, uint32_t tid, uint32_t nthreads) {
-    constexpr uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
-    for (uint32_t x = tid; x < 256; x += nthreads) {
-        const uint32_t a = ascii4(x);
-        const uint64_t A1 = (uint64_t)a * c1, A2 = (uint64_t)a * c2;
-        const uint32_t x1 = (uint32_t)A1, x2 = (uint32_t)A2;
-        const uint64_t t1 = ((uint64_t)x1 << 31) * c2;
-        const uint64_t t2 = ((uint64_t)(x2 & 0x7fffffffu) << 33) * c1 + (uint64_t)(x2 >> 31) * c1;
-        tb.tt1lo[x] = (uint32_t)t1; tb.tt1hi[x] = (uint32_t)(t1 >> 32); tb.ta1[x] = (uint32_t)(A1 >> 32);
-        tb.tt2lo[x] = (uint32_t)t2; tb.tt2hi[x] = (uint32_t)(t2 >> 32); tb.ta2[x] = (uint32_t)(A2 >> 32);
-        tb.tb1[x] = a * (uint32_t)c1;
-        tb.tb2[x] = a * (uint32_t)c2;
-    }
-    for (uint32_t y = tid; y < 1024; y += nthreads) {
-        const uint64_t k3 = (uint64_t)ascii4(y >> 2) | ((uint64_t)ascii4((y & 3u) << 6) & 0xffu) << 32;
-        tb.t3[y] = (rotl64_ab(k3 * c1, 31) * c2) ^ 21u;
-    }
-}
-__device__ __forceinline__ void tab_k1(const SketchTables5 &tb, uint32_t x, uint32_t &ta, uint64_t &tt) {
-    ta = tb.ta1[x]; tt = tb.tt1[x];
-}
-__device__ __forceinline__ void tab_k2(const SketchTables5 &tb, uint32_t x, uint32_t &ta, uint64_t &tt) {
-    ta = tb.ta2[x]; tt = tb.tt2[x];
-}
-__device__ __forceinline__ void tab_k1(const SketchTables6 &tb, uint32_t x, uint32_t &ta, uint64_t &tt) {
-    ta = tb.ta1[x]; tt = ((uint64_t)tb.tt1hi[x] << 32) | tb.tt1lo[x];
-}
-__device__ __forceinline__ void tab_k2(const SketchTables6 &tb, uint32_t x, uint32_t &ta, uint64_t &tt) {
-    ta = tb.ta2[x]; tt = ((uint64_t)tb.tt2hi[x] << 32) | tb.tt2lo[x];
-}
-
-__device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {   // one v_mad_u64_u32
-    return (uint64_t)a * b + c;
-}
-
-template <class TB>
-__device__ __forceinline__ void murmur21_tab5(const TB &tb, uint32_t hi, uint32_t lo, uint32_t seed,
-                                              uint64_t &p1, uint64_t &p2) {
-    constexpr uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
-    constexpr uint64_t d1 = c1 * 2;                                  // 2 c1 mod 2^64
-    const uint32_t x = hi >> 24, xp = (hi >> 8) & 0xffu;
-    uint32_t ta1, ta2;
-    uint64_t tt1, tt2;
-    tab_k1(tb, x, ta1, tt1);
-    tab_k2(tb, xp, ta2, tt2);
-    const uint32_t X1 = ta1 + tb.tb1[(hi >> 16) & 0xffu];              // hi(k1 * c1)
-    const uint32_t X2 = ta2 + tb.tb2[hi & 0xffu];                      // hi(k2 * c2)
-    const uint64_t k3 = tb.t3[lo >> 22];
-    // rotl(k1 c1, 31) c2 ^ seed
-    const uint32_t h = X1 >> 1;
-    const uint64_t P1 = mad64(h, (uint32_t)c2, tt1);
-    const uint32_t g1hi = (uint32_t)(P1 >> 32) + h * (uint32_t)(c2 >> 32) + (X1 << 31);
-    uint64_t h1 = ((uint64_t)g1hi << 32) | ((uint32_t)P1 ^ seed);
-    h1 = x5_plus(rotl64_ab(h1, 27), 5ull * seed + 0x52dce729);   // (rotl + seed) * 5 + c
-    // rotl(k2 c2, 33) c1 ^ seed
-    const uint64_t P2 = mad64(X2, (uint32_t)d1, tt2);
-    const uint32_t g2hi = (uint32_t)(P2 >> 32) + X2 * (uint32_t)(d1 >> 32);
-    uint64_t h2 = ((uint64_t)g2hi << 32) | ((uint32_t)P2 ^ seed);
-    h2 = x5_plus(add64(rotl64_ab(h2, 31), h1), 0x38495ab5);
-    h1 ^= k3;
-    h2 ^= 21u;
-    h1 = add64(h1, h2);
-    h2 = add64(h2, h1);
-    p1 = fmix64_pre(h1);
-    p2 = fmix64_pre(h2);
-}
-
-template <int LANE, int BATCH, class TB = SketchTables5>
-__global__ __launch_bounds__(kTile / LANE) void k_sketch_hash21_v5(
-    const uint32_t *__restrict__ codes, const uint32_t *__restrict__ valid,
-    const uint64_t *__restrict__ tile_base, const uint32_t *__restrict__ tile_genome,
-    const uint64_t *__restrict__ thr, unsigned long long *__restrict__ sets,
-    uint32_t *__restrict__ cnt, uint32_t set_log2, uint32_t limit, uint32_t seed, uint64_t wlast) {
-    constexpr uint32_t WG = kTile / LANE;
-    constexpr int NCH = LANE / 16;
-    __shared__ TB tb;
-    __shared__ uint64_t stage[kStage];
-    __shared__ uint32_t nstage;
-    const uint32_t t = blockIdx.x;
-    const uint32_t g = tile_genome[t];
-    const uint64_t T = thr[g];
-    const uint32_t Thi = (uint32_t)(T >> 32);
-    const uint32_t Tp = Thi == 0xFFFFFFFFu ? Thi : Thi + 1;     // prefilter bound (see murmur21_tab)
-    const uint64_t start = tile_base[t] + (uint64_t)threadIdx.x * LANE;
-    const uint32_t mask = (1u << set_log2) - 1;
-    unsigned long long *S = sets + ((uint64_t)g << set_log2);
-    uint32_t *C = cnt + g;
-    if (threadIdx.x == 0) nstage = 0;
-    build_tables(tb, threadIdx.x, WG);
-
-    const uint64_t m0 = start / 16;
-    auto ld = [&](int j) -> uint32_t {
-        const uint64_t w = m0 + j;
-        return codes[w < wlast ? w : wlast];
-    };
-    uint32_t nf0 = ~ld(-2), nf1 = ~ld(-1), nf2 = ~ld(0);
-    uint32_t r0 = rev_fields16(~nf0), r1 = rev_fields16(~nf1), r2 = rev_fields16(~nf2);
-    uint32_t f3 = ld(1);
-    uint32_t r3 = rev_fields16(f3);
-    uint32_t fnext = ld(2);
-    const uint32_t *vw = valid + (start - kWarm) / 32;
-    uint64_t vhist = (uint64_t)vw[0] << 32;
-    uint32_t vcur = vw[1];
-    __syncthreads();
-
-#pragma unroll 1
-    for (int wi = 0; wi < NCH; wi++) {
-        const uint32_t vbits = (vcur >> ((wi & 1) * 16)) & 0xffffu;
-        if (wi + 1 < NCH && (wi & 1)) vcur = vw[2 + (wi >> 1)];
-        vhist = (vhist >> 16) | ((uint64_t)vbits << 48);
-#pragma unroll
-        for (int b0 = 0; b0 < 16; b0 += BATCH) {
-            uint64_t p1[BATCH], p2[BATCH];
-            bool hit = false;
-#pragma unroll
-            for (int b = 0; b < BATCH; b++) {
-                const int r = b0 + b;
-                uint32_t chi, clo, fhi, flo;
-                if (r == 15) { chi = nf2; clo = nf1; }
-                else {
-                    chi = __builtin_amdgcn_alignbit(nf2, nf1, 2 * (r + 1));
-                    clo = __builtin_amdgcn_alignbit(nf1, nf0, 2 * (r + 1));
-                }
-                if (r < 4) {
-                    fhi = __builtin_amdgcn_alignbit(r0, r1, 32 - 2 * (r + 12));
-                    flo = __builtin_amdgcn_alignbit(r1, r2, 32 - 2 * (r + 12));
-                } else if (r == 4) {
-                    fhi = r1; flo = r2;
-                } else {
-                    fhi = __builtin_amdgcn_alignbit(r1, r2, 32 - 2 * (r - 4));
-                    flo = __builtin_amdgcn_alignbit(r2, r3, 32 - 2 * (r - 4));
-                }
-                const uint64_t fw = ((uint64_t)fhi << 32) | flo;
-                const uint64_t rc = ((uint64_t)chi << 32) | clo;
-                const uint64_t cc = fw <= rc ? fw : rc;
-                murmur21_tab5(tb, (uint32_t)(cc >> 32), (uint32_t)cc, seed, p1[b], p2[b]);
-                hit |= (uint32_t)(p1[b] >> 32) + (uint32_t)(p2[b] >> 32) + 1u <= Tp;
-            }
-            if (__builtin_expect(hit, 0)) {
-                const uint64_t ok = run21(vhist);
-#pragma unroll
-                for (int b = 0; b < BATCH; b++) {
-                    const uint64_t h = murmur_fin(p1[b], p2[b]);
-                    if (h <= T && ((ok >> (48 + b0 + b)) & 1)) {
-                        const uint32_t slot = atomicAdd(&nstage, 1u);
-                        if (slot < kStage) stage[slot] = h;
-                        else set_insert(S, mask, C, limit, h);
-                    }
-                }
-            }
-        }
-        nf0 = nf1; nf1 = nf2; nf2 = ~f3;
-        r0 = r1; r1 = r2; r2 = r3;
-        f3 = fnext;
-        r3 = rev_fields16(f3);
-        fnext = ld(wi + 3);
-    }
-    __syncthreads();
-    const uint32_t n = min(nstage, kStage);
-    for (uint32_t i = threadIdx.x; i < n; i += WG) set_insert(S, mask, C, limit, stage[i]);
-}
-
 // ----------------------------------------------------------------- finalize
 enum : uint8_t { ST_OK = 0, ST_UP = 1, ST_DOWN = 2 };
 
@@ -622,56 +365,7 @@ __device__ __forceinline__ void finalize_reset(unsigned long long *S, uint32_t s
     if (threadIdx.x == 0) *cnt_g = 0;
 }
 
-template <int MAXC>
-__global__ __launch_bounds__(1024) void k_sketch_finalize(
-    unsigned long long *__restrict__ sets, uint32_t *__restrict__ cnt,
-    const uint64_t *__restrict__ thr, const uint32_t *__restrict__ glist, uint32_t set_log2,
-    uint32_t maxc, uint32_t s, uint64_t *__restrict__ out, uint32_t *__restrict__ nhash,
-    uint8_t *__restrict__ status) {
-    __shared__ uint64_t buf[MAXC];
-    __shared__ uint32_t pos;
-    const uint32_t g = glist[blockIdx.x];
-    const uint32_t n = cnt[g];
-    const uint32_t tid = threadIdx.x;
-    unsigned long long *S = sets + ((uint64_t)g << set_log2);
-    const uint32_t slots = 1u << set_log2;
-    if (n > maxc || (n < s && thr[g] < kMaxThr)) {
-        if (tid == 0) status[g] = n > maxc ? ST_DOWN : ST_UP;
-        finalize_reset(S, slots, cnt + g);
-        return;
-    }
-    if (tid == 0) pos = 0;
-    __syncthreads();
-    if (tid == 0) cnt[g] = 0;                          // every thread has read it
-    for (uint32_t i = tid; i < slots; i += blockDim.x) {
-        const uint64_t v = S[i];
-        if (v != kEmpty) { buf[atomicAdd(&pos, 1u)] = v; S[i] = kEmpty; }
-    }
-    __syncthreads();
-    uint32_t P = 1;
-    while (P < n) P <<= 1;
-    for (uint32_t i = n + tid; i < P; i += blockDim.x) buf[i] = kEmpty;
-    __syncthreads();
-    for (uint32_t k = 2; k <= P; k <<= 1) {
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = tid; i < P; i += blockDim.x) {
-                const uint32_t ixj = i ^ j;
-                if (ixj > i) {
-                    const uint64_t a = buf[i], b = buf[ixj];
-                    const bool up = (i & k) == 0;
-                    if ((a > b) == up) { buf[i] = b; buf[ixj] = a; }
-                }
-            }
-            __syncthreads();
-        }
-    }
-    const uint32_t m = n < s ? n : s;
-    uint64_t *o = out + (uint64_t)g * s;
-    for (uint32_t i = tid; i < s; i += blockDim.x) o[i] = i < m ? buf[i] : kEmpty;
-    if (tid == 0) { nhash[g] = m; status[g] = ST_OK; }
-}
-
-// Bucket-sort finalize (default).  The candidates of one genome are distinct
+// Bucket-sort finalize.  The candidates of one genome are distinct
 // hashes <= T spread evenly over [0, T], so a counting sort on their top bits
 // (NB buckets, bucket = h >> shift with T >> shift < NB; monotone in h) leaves
 // ~1-4 hashes per bucket, which one thread then insertion-sorts in LDS.  Exact
@@ -863,6 +557,14 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
     if ((rc = scratch(ctx, "sk_gl", n * 4ull, (void **)&d_gl))) return rc;
     if ((rc = scratch(ctx, "sk_st", n * 1ull, (void **)&d_st))) return rc;
     if ((rc = scratch(ctx, "sk_sets", (uint64_t)n * slots * 8ull, (void **)&d_sets))) return rc;
+    // Murmur table image (once per context; rebuilt after any reallocation)
+    SketchTablesQ *d_img;
+    if ((rc = scratch(ctx, "sk_tables", sizeof(SketchTablesQ), (void **)&d_img))) return rc;
+    if (ctx->sk_tab_gen != ctx->alloc_gen) {
+        hipLaunchKernelGGL(k_sketch_tables, dim3(1), dim3(256), 0, st, d_img);
+        HIPC(hipGetLastError());
+        ctx->sk_tab_gen = ctx->alloc_gen;
+    }
     // first-round thresholds and genome list: device copies cached with the tile table
     uint64_t *d_thr0;
     uint32_t *d_gl0;
@@ -937,54 +639,23 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
         }
         if (nt > 0) {
             timing_mark(ctx, 0, st, true);
-            for (uint32_t t0 = 0; t0 < nt; t0 += (uint32_t)max_blocks(kTile / (kLaneBases / 2))) {
-                const uint32_t ntc = std::min<uint32_t>(nt - t0, (uint32_t)max_blocks(kTile / (kLaneBases / 2)));
+            for (uint32_t t0 = 0; t0 < nt; t0 += (uint32_t)max_blocks(kTile / kLaneBases)) {
+                const uint32_t ntc = std::min<uint32_t>(nt - t0, (uint32_t)max_blocks(kTile / kLaneBases));
                 const uint64_t *tbb = tb_tiles_b + t0;
                 const uint32_t *tbg = tb_tiles_g + t0;
-                if (ctx->sketch_kernel == 5)
-                    hipLaunchKernelGGL((k_sketch_hash21_v5<kLaneBases, 8>), dim3(ntc), dim3(kTile / kLaneBases), 0, st,
-                                       d_codes, d_valid, tbb, tbg, thr_p, d_sets, d_cnt, plan.set_log2, limit,
-                                       ctx->seed, wlast);
-                else if (ctx->sketch_kernel == 9)      // A/B: split 32-bit TT tables (SketchTables6)
-                    hipLaunchKernelGGL((k_sketch_hash21_v5<kLaneBases, 8, SketchTables6>), dim3(ntc),
-                                       dim3(kTile / kLaneBases), 0, st, d_codes, d_valid, tbb, tbg, thr_p, d_sets,
-                                       d_cnt, plan.set_log2, limit, ctx->seed, wlast);
-                else if (ctx->sketch_kernel == 6)      // A/B: 4 k-mers per admit test
-                    hipLaunchKernelGGL((k_sketch_hash21_v5<kLaneBases, 4>), dim3(ntc), dim3(kTile / kLaneBases), 0, st,
-                                       d_codes, d_valid, tbb, tbg, thr_p, d_sets, d_cnt, plan.set_log2, limit,
-                                       ctx->seed, wlast);
-                else if (ctx->sketch_kernel == 7)      // A/B: 64 window ends per lane, 512-lane workgroups
-                    hipLaunchKernelGGL((k_sketch_hash21_v5<kLaneBases / 2, 8>), dim3(ntc),
-                                       dim3(kTile / (kLaneBases / 2)), 0, st, d_codes, d_valid, tbb, tbg, thr_p,
-                                       d_sets, d_cnt, plan.set_log2, limit, ctx->seed, wlast);
-                else if (ctx->sketch_kernel == 8)      // A/B: 256 window ends per lane, 128-lane workgroups
-                    hipLaunchKernelGGL((k_sketch_hash21_v5<kLaneBases * 2, 8>), dim3(ntc),
-                                       dim3(kTile / (kLaneBases * 2)), 0, st, d_codes, d_valid, tbb, tbg, thr_p,
-                                       d_sets, d_cnt, plan.set_log2, limit, ctx->seed, wlast);
-                else if (ctx->sketch_kernel != 3)
-                    hipLaunchKernelGGL((k_sketch_hash21_v4<kLaneBases, 8>), dim3(ntc), dim3(kTile / kLaneBases), 0, st,
-                                       d_codes, d_valid, tbb, tbg, thr_p, d_sets, d_cnt, plan.set_log2, limit,
-                                       ctx->seed, wlast);
-                else
-                    hipLaunchKernelGGL((k_sketch_hash21_v3<kLaneBases, 8>), dim3(ntc), dim3(kTile / kLaneBases), 0, st,
-                                       d_codes, d_valid, tbb, tbg, thr_p, d_sets, d_cnt, plan.set_log2, limit,
-                                       ctx->seed);
+                hipLaunchKernelGGL((k_sketch_hash21<kLaneBases, DREPHIP_SK_BATCH>), dim3(ntc), dim3(kTile / kLaneBases), 0, st,
+                                   d_img, d_codes, d_valid, tbb, tbg, thr_p, d_sets, d_cnt, plan.set_log2, limit,
+                                   ctx->seed, wlast);
             }
             timing_mark(ctx, 0, st, false);
         }
         timing_mark(ctx, 1, st, true);
-        if (ctx->finalize_kernel && plan.maxc <= 4096)
+        if (plan.maxc <= 4096)
             hipLaunchKernelGGL((k_sketch_finalize_bucket<4096, 4096>), dim3((uint32_t)todo.size()), dim3(1024), 0, st,
                                d_sets, d_cnt, thr_p, gl_p, plan.set_log2, plan.maxc, s, d_hashes, d_nhash, d_st);
-        else if (ctx->finalize_kernel)
+        else
             hipLaunchKernelGGL((k_sketch_finalize_bucket<16384, 4096>), dim3((uint32_t)todo.size()), dim3(1024), 0,
                                st, d_sets, d_cnt, thr_p, gl_p, plan.set_log2, plan.maxc, s, d_hashes, d_nhash, d_st);
-        else if (plan.maxc <= 4096)
-            hipLaunchKernelGGL(k_sketch_finalize<4096>, dim3((uint32_t)todo.size()), dim3(1024), 0, st,
-                               d_sets, d_cnt, thr_p, gl_p, plan.set_log2, plan.maxc, s, d_hashes, d_nhash, d_st);
-        else
-            hipLaunchKernelGGL(k_sketch_finalize<16384>, dim3((uint32_t)todo.size()), dim3(1024), 0, st,
-                               d_sets, d_cnt, thr_p, gl_p, plan.set_log2, plan.maxc, s, d_hashes, d_nhash, d_st);
         timing_mark(ctx, 1, st, false);
         HIPC(hipGetLastError());
         HIPC(hipMemcpyAsync(status, d_st, n, hipMemcpyDeviceToHost, st));

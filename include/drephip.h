@@ -126,8 +126,10 @@ int drephip_sketch_device(drephip_ctx *ctx, const uint32_t *d_codes, const uint3
  * is queued, without waiting for it: work the caller queues next on `stream`
  * (the sketch all-gather, drephip_allpairs_device) runs right behind it.
  * d_hashes/d_nhash are final only after drephip_sketch_wait, which must be
- * called before the next sketch call on this context (a sketch call made
- * first drops the pending check). */
+ * called before the next sketch call on this context: until then every other
+ * sketch call fails with DREPHIP_ERR_ARG (the pending check is kept).  The
+ * inputs (d_codes, d_valid) must stay unchanged until the wait, which may
+ * rerun the call from them. */
 int drephip_sketch_device_async(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t *d_valid,
                                 const uint64_t *h_base_off, const uint64_t *h_padded,
                                 const uint64_t *h_nkmers, uint32_t n_genomes,
@@ -177,13 +179,13 @@ int drephip_allpairs_device(drephip_ctx *ctx, const uint64_t *d_hashes, const ui
                             uint16_t *d_denom, void *stream);
 
 /* Same as drephip_allpairs_device, but on the whole-row table path (s <=
- * 2048) it returns once the kernels and the table-build failure count's
- * readback are queued: the host can queue the next step's work while these
- * kernels run.  drephip_allpairs_wait (or any later all-pairs call on this
- * context) completes it: reads the count and, if a row's table could not be
- * built, recomputes the segment with the merge kernel before returning.  The
- * output is final only after that.  Other paths run synchronously (the wait
- * is then a no-op).  Kernel timings of a deferred call are not recorded. */
+ * 2048) it returns once the kernels are queued: the host can queue the next
+ * step's work while they run.  The output is final once the work queued on
+ * `stream` before and by this call has run (the kernels handle every row
+ * themselves, including a row whose table cannot be built, which they merge
+ * literally); drephip_allpairs_wait (or any later all-pairs or linkage call on
+ * this context) waits for it.  Other paths run synchronously (the wait is
+ * then a no-op).  Kernel timings of a deferred call are not recorded. */
 int drephip_allpairs_device_async(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash,
                                   uint32_t N, uint32_t row0, uint32_t row1, uint16_t *d_common,
                                   uint16_t *d_denom, void *stream);
@@ -232,10 +234,13 @@ int drephip_linkage(drephip_ctx *ctx, const double *y, uint32_t n, int method, d
  * 0..n-1 in one segment): distance of pair (i, j) = lut[lut_off[denom] +
  * common] (denom = s when d_denom is NULL; lut_off has s+1 entries, -1 for a
  * denominator that does not occur), placed at row/column perm[i], perm[j] of
- * the linkage input.  Blocking. */
+ * the linkage input.  The counts are read after all work queued on `stream`
+ * (and after a pending drephip_allpairs_device_async on this context).  A pair
+ * whose denominator has no table, or whose count exceeds it, fails the call
+ * (DREPHIP_ERR_ARG).  Blocking. */
 int drephip_linkage_counts_device(drephip_ctx *ctx, const uint16_t *d_common, const uint16_t *d_denom,
                                   uint32_t n, const uint32_t *perm, const double *lut, uint32_t lut_len,
-                                  const int32_t *lut_off, int method, double *Z /* (n-1)*4 */);
+                                  const int32_t *lut_off, int method, double *Z /* (n-1)*4 */, void *stream);
 
 /* HIP-event timing of kernel launches: `kernels` is a bitmask of the kernels
  * to bracket with events (bit w = `which` w of drephip_last_kernel_ms; -1 =

@@ -109,13 +109,11 @@ def test_sketch_sizes_vs_oracle(s):
         assert np.array_equal(h[g, :nh[g]], want)
 
 
-@pytest.mark.parametrize("variant", ["3", "4", "5", "9"])
-def test_sketch_kernel_variants_vs_oracle(variant, monkeypatch):
-    """Every hash-kernel variant (DREPHIP_SKETCH_KERNEL, read at context
-    creation; 5 is the default) gives the oracle's sketches, including
-    lower case, N runs, multi-record genomes and a partial sketch."""
-    monkeypatch.setenv("DREPHIP_SKETCH_KERNEL", variant)
-    rng = np.random.default_rng(int(variant))
+@pytest.mark.parametrize("seed", [3, 4, 5, 9])
+def test_sketch_mixed_case_nruns_vs_oracle(seed):
+    """The hash kernel gives the oracle's sketches on lower case, N runs,
+    multi-record genomes and a partial sketch."""
+    rng = np.random.default_rng(seed)
     A = np.frombuffer(b"ACGTacgtN", dtype=np.uint8)
     recs = [A[rng.choice(9, 300_000, p=[.24, .24, .24, .24, .01, .01, .01, .01, 0])],
             A[rng.choice(9, 50_000, p=[.2, .2, .2, .2, 0, 0, 0, 0, .2])],
@@ -134,14 +132,11 @@ def test_sketch_kernel_variants_vs_oracle(variant, monkeypatch):
     assert nh[1] < S
 
 
-@pytest.mark.parametrize("finalize", ["0", "1"])
 @pytest.mark.parametrize("s", [1, 1000, 12000])
-def test_sketch_finalize_variants_vs_oracle(finalize, s, monkeypatch):
-    """Both finalize kernels (DREPHIP_FINALIZE: 1 bucket sort, the default; 0
-    bitonic sort) give the oracle's sketches: full and partial sketches, the
-    4096- and 16384-candidate instantiations, and a low-complexity genome whose
-    candidates crowd few buckets."""
-    monkeypatch.setenv("DREPHIP_FINALIZE", finalize)
+def test_sketch_finalize_vs_oracle(s):
+    """The bucket-sort finalize gives the oracle's sketches: full and partial
+    sketches, its 4096- and 16384-candidate instantiations, and a
+    low-complexity genome whose candidates crowd few buckets."""
     rng = np.random.default_rng(100 + s)
     A = np.frombuffer(b"ACGT", dtype=np.uint8)
     motif = A[rng.integers(0, 4, 40)]
@@ -155,6 +150,20 @@ def test_sketch_finalize_variants_vs_oracle(finalize, s, monkeypatch):
     for g in range(len(recs)):
         want = oracle.sketch_records(recs[g], np.array([0, len(recs[g])], np.uint64), 21, s, 42)
         assert nh[g] == len(want) and np.array_equal(h[g, :nh[g]], want), g
+
+
+def test_sketch_every_kmer_hash_vs_oracle():
+    """With s above the number of distinct k-mers every canonical k-mer's hash
+    is in the sketch: the table-driven Murmur of every k-mer of a 9000-base
+    genome (each of the 256 + 256 + 1024 table entries used) equals the
+    oracle's."""
+    rng = np.random.default_rng(77)
+    A = np.frombuffer(b"ACGT", dtype=np.uint8)
+    rec = A[rng.integers(0, 4, 9000)]
+    with _lib.Context(0, 21, 12000, 42) as ctx:
+        h, nh, _ = ctx.sketch_records(rec, np.array([0, len(rec)], np.uint64), np.array([0, 1], np.uint64))
+    want = oracle.sketch_records(rec, np.array([0, len(rec)], np.uint64), 21, 12000, 42)
+    assert len(want) > 8900 and nh[0] == len(want) and np.array_equal(h[0, :nh[0]], want)
 
 
 def test_synth_device_matches_oracle_generator(ctx1000):
@@ -233,29 +242,44 @@ def test_allpairs_family_vs_oracle(family, ctx1000):
 
 
 @pytest.mark.parametrize("path", ["table", "band"])
-def test_allpairs_unbuildable_table_falls_back_to_merge(path):
+@pytest.mark.parametrize("partial", [False, True])
+def test_allpairs_unbuildable_table_falls_back_to_merge(path, partial):
     """Three hashes of one row sharing their low 32 bits land in the same two
     slots under every field family, so no cuckoo table exists for that row:
-    the host must discard the table kernel's output and rerun the segment with
-    the literal merge kernel -- counts still exact."""
+    the table kernel merges that row's pairs literally (the band path reruns
+    the segment with the merge kernel) -- counts and denominators still exact,
+    also when some sketches are partial."""
     h, nh = _unbuildable_rows()
+    if partial:                       # partial sketches: denominators below s
+        for i in (1, 7, 12):          # unions below s: denominators < s
+            nh[i] = 300 + i
+            h[i, nh[i]:] = UMAX
     N = len(nh)
-    oc, _ = oracle.allpairs(h, nh, S, threads=4)
+    oc, od = oracle.allpairs(h, nh, S, threads=4)
     good = h.copy()
     for i in (0, 7, 1, 8):
         good[i] = h[i + 2]
-    ogc, _ = oracle.allpairs(good, nh, S, threads=4)
+        good[i, nh[i]:] = UMAX
+    ogc, ogd = oracle.allpairs(good, nh, S, threads=4)
     with _lib.Context(0, 21, S, 42) as ctx:
         if path == "band":
             ctx.set_allpairs_path(ctx.AP_BAND, 256)
-        c, _ = ctx.allpairs(h, nh)
-        # the failure counter is per context and never reset (the table path
-        # compares it with the last value read): a clean call, then a failing
-        # one again, on the same context
-        c2, _ = ctx.allpairs(good, nh)
-        c3, _ = ctx.allpairs(h, nh)
-    assert np.array_equal(c, oc) and np.array_equal(c3, oc)
+        c, d = ctx.allpairs(h, nh)
+        # a clean call, then a failing one again, on the same context
+        c2, d2 = ctx.allpairs(good, nh)
+        c3, d3 = ctx.allpairs(h, nh)
+        # one row range at a time (row segments through the same path)
+        cs = np.zeros_like(c)
+        ds = np.zeros_like(d)
+        for r0, r1 in ((0, 3), (3, 8), (8, N)):
+            a = r0 * N - r0 * (r0 + 1) // 2
+            b = r1 * N - r1 * (r1 + 1) // 2 if r1 < N else len(c)
+            ctx.allpairs_rows(h, nh, r0, r1, cs[a:b], ds[a:b] if partial else None)
+    assert np.array_equal(c, oc) and np.array_equal(c3, oc) and np.array_equal(cs, oc)
     assert np.array_equal(c2, ogc)
+    if partial:
+        assert np.array_equal(d, od) and np.array_equal(d2, ogd) and np.array_equal(ds, od)
+        assert (od < S).any()
     assert c.max() >= 2
 
 
@@ -281,10 +305,11 @@ def _unbuildable_rows():
 
 
 def test_allpairs_device_async_wait():
-    """drephip_allpairs_device_async defers the table-build failure check to
-    drephip_allpairs_wait (or the next all-pairs call): a failing table is
-    still replaced by the merge kernel's exact counts, on either completion,
-    and a clean call between two failing ones is not mistaken for failing."""
+    """drephip_allpairs_device_async returns once the kernels are queued; rows
+    whose table cannot be built are merged literally inside the kernel, so the
+    counts are exact however the call is completed (drephip_allpairs_wait or
+    the next all-pairs call), and a clean call between two failing ones is not
+    affected."""
     import torch
     h, nh = _unbuildable_rows()
     N = len(nh)
@@ -712,9 +737,13 @@ def test_sketch_device_async_wait(ctx1000):
         common = torch.zeros(n * (n - 1) // 2, dtype=torch.int16, device="cuda")
         ctx1000.sketch_device_async(codes.data_ptr(), valid.data_ptr(), off, pad, nk, n,
                                     hashes.data_ptr(), nhash.data_ptr(), st)
-        if sync_after:       # a sketch call before the wait drops the pending check
-            ctx1000.sketch_device(codes.data_ptr(), valid.data_ptr(), off, pad, nk, n,
-                                  hashes.data_ptr(), nhash.data_ptr(), st)
+        if sync_after:       # a sketch call before the wait is refused; the pending check is kept
+            with pytest.raises(_lib.DrepHipError, match="pending"):
+                ctx1000.sketch_device(codes.data_ptr(), valid.data_ptr(), off, pad, nk, n,
+                                      hashes.data_ptr(), nhash.data_ptr(), st)
+            with pytest.raises(_lib.DrepHipError, match="pending"):
+                ctx1000.sketch_device_async(codes.data_ptr(), valid.data_ptr(), off, pad, nk, n,
+                                            hashes.data_ptr(), nhash.data_ptr(), st)
         ctx1000.allpairs_device(hashes.data_ptr(), nhash.data_ptr(), n, 0, n, common.data_ptr(), None, st)
         redone = ctx1000.sketch_wait() if wait else None
         if redone:
@@ -733,6 +762,35 @@ def test_sketch_device_async_wait(ctx1000):
     assert redone is True
     assert np.array_equal(nh, onh) and np.array_equal(h, oh) and np.array_equal(c, oc)
     h, nh, c, redone = run(bad, sync_after=True)
-    assert redone is False
+    assert redone is True
     assert np.array_equal(h, oh) and np.array_equal(c, oc)
     assert ctx1000.sketch_wait() is False          # nothing pending
+
+
+def test_linkage_counts_device_rejects_missing_tables(ctx1000):
+    """drephip_linkage_counts_device refuses a denominator with no distance
+    table and a count above its denominator instead of reading outside the
+    table (device-side check)."""
+    import torch
+    from drep_amd.d_cluster import linkage_tables
+    n = 6
+    c = torch.from_numpy(np.arange(n * (n - 1) // 2, dtype=np.int16) * 10).cuda()
+    d_full = torch.full((n * (n - 1) // 2,), S, dtype=torch.int16, device="cuda")
+    perm = np.arange(n, dtype=np.uint32)
+    lut, off = linkage_tables(np.array([S]), S)
+    st = torch.cuda.current_stream().cuda_stream
+    Z = ctx1000.linkage_counts_device(c.data_ptr(), None, n, perm, lut, off, "average", st)
+    Z2 = ctx1000.linkage_counts_device(c.data_ptr(), d_full.data_ptr(), n, perm, lut, off, "average", st)
+    assert np.array_equal(Z, Z2) and Z.shape == (n - 1, 4)
+    lut7, off7 = linkage_tables(np.array([700]), S)          # no table for s
+    with pytest.raises(_lib.DrepHipError, match="lut_off"):
+        ctx1000.linkage_counts_device(c.data_ptr(), None, n, perm, lut7, off7, "average", st)
+    d_bad = d_full.clone()
+    d_bad[3] = 700                                           # denominator without a table
+    with pytest.raises(_lib.DrepHipError, match="denominator"):
+        ctx1000.linkage_counts_device(c.data_ptr(), d_bad.data_ptr(), n, perm, lut, off, "average", st)
+    d_small = torch.full_like(d_full, 700)
+    c_big = c.clone()
+    c_big[2] = 701                                           # count above its denominator
+    with pytest.raises(_lib.DrepHipError, match="exceeds"):
+        ctx1000.linkage_counts_device(c_big.data_ptr(), d_small.data_ptr(), n, perm, lut7, off7, "average", st)

@@ -12,9 +12,7 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # variant: (mangled-name pattern, k-mers/block)
-KERNELS = {"3": ("k_sketch_hash21_v3", 8), "4": ("k_sketch_hash21_v4", 8),
-           "5": ("k_sketch_hash21_v5ILi128ELi8ENS_13SketchTables5E", 8),
-           "9": ("k_sketch_hash21_v5ILi128ELi8ENS_13SketchTables6E", 8)}
+KERNELS = {"default": ("k_sketch_hash21ILi128ELi4E", 4)}
 
 
 def main():
@@ -48,8 +46,7 @@ def main():
             for k, v in b.items():
                 if k.startswith("v_"):
                     mix[k] += v
-        label = {"5": "k_sketch_hash21_v5<128,8,SketchTables5>",
-                 "9": "k_sketch_hash21_v5<128,8,SketchTables6>"}.get(var, name)
+        label = {"default": "k_sketch_hash21<128,4>"}.get(var, name)
         out["variants"][var] = {
             "kernel": label, "kmers_per_block": per, "blocks": len(hot),
             "valu_per_kmer": sum(valu) / len(hot) / per,

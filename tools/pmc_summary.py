@@ -1,50 +1,79 @@
 """Sum rocprofv3 PMC counter passes per kernel into one JSON (not part of the
-product).  usage: python tools/pmc_summary.py <kernel substring> <csv>... > out.json"""
+product).
+
+usage: python tools/pmc_summary.py <kernel substring> <csv>... [--window-ends N] [--kernel-ms T] > out.json
+
+Derived quantities (MI355X_MICROARCH.md, "s_memtime tick vs SQ PMC units"):
+  * SQ_WAVE_CYCLES, SQ_WAIT_*, SQ_ACTIVE_INST_* count quad-cycles; busy and
+    wait fractions below are ratios of like units;
+  * GRBM_GUI_ACTIVE rides along in every pass and rocprofv3 sums it over the 8
+    XCDs: kernel cycles per dispatch = sum / passes / 8 / dispatches;
+  * valu_busy_frac = SQ_ACTIVE_INST_VALU (quad-cycles) x 4 / (1024 SIMDs x
+    kernel cycles): the share of SIMD cycles holding a VALU instruction.  Above
+    1.0 it says some VALU instructions take fewer than 4 cycles (the
+    fraction is then a lower bound of saturation, not an error);
+  * lds_busy_frac = SQ_LDS_IDX_ACTIVE (LDS-array cycles per CU) / (256 CUs x
+    kernel cycles); lds_bank_conflict_frac = SQ_LDS_BANK_CONFLICT /
+    SQ_LDS_IDX_ACTIVE (the extra cycles conflicts cost);
+  * --window-ends: positions the sketch kernel visits per dispatch, for
+    valu_insts_per_window_end = wave64 VALU instructions x 64 / window ends;
+  * --kernel-ms: average dispatch time (rocprofv3 --stats), for the effective
+    clock = kernel cycles / time.
+"""
+import argparse
 import collections
 import csv
 import json
-import sys
 
 N_CU, N_SIMD = 256, 1024          # MI355X
 
+
 def main():
-    key, files = sys.argv[1], sys.argv[2:]
+    ap = argparse.ArgumentParser()
+    ap.add_argument("key")
+    ap.add_argument("files", nargs="+")
+    ap.add_argument("--window-ends", type=float, default=None)
+    ap.add_argument("--kernel-ms", type=float, default=None)
+    a = ap.parse_args()
     agg = collections.defaultdict(float)
     disp = collections.defaultdict(set)
+    passes_with_grbm = 0
     name = None
-    for f in files:
+    for f in a.files:
+        seen_grbm = False
         for r in csv.DictReader(open(f)):
-            if key in r["Kernel_Name"]:
+            if a.key in r["Kernel_Name"]:
                 name = r["Kernel_Name"]
                 agg[r["Counter_Name"]] += float(r["Counter_Value"])
-                disp[r["Counter_Name"]].add(r["Dispatch_Id"])
+                disp[r["Counter_Name"]].add((f, r["Dispatch_Id"]))
+                seen_grbm |= r["Counter_Name"] == "GRBM_GUI_ACTIVE"
+        passes_with_grbm += seen_grbm
     out = {"kernel": name, "counters": dict(agg), "dispatches": {k: len(v) for k, v in disp.items()}}
     c = agg
+    d = out.setdefault("derived", {})
     if c.get("SQ_WAVE_CYCLES"):
-        out["derived"] = {
-            "wait_any_frac": c.get("SQ_WAIT_ANY", 0) / c["SQ_WAVE_CYCLES"],
-            "wait_inst_any_frac": c.get("SQ_WAIT_INST_ANY", 0) / c["SQ_WAVE_CYCLES"],
-            "active_inst_any_frac": c.get("SQ_ACTIVE_INST_ANY", 0) / c["SQ_WAVE_CYCLES"],
-        }
+        d["wait_any_frac"] = c.get("SQ_WAIT_ANY", 0) / c["SQ_WAVE_CYCLES"]
+        d["wait_inst_any_frac"] = c.get("SQ_WAIT_INST_ANY", 0) / c["SQ_WAVE_CYCLES"]
+        d["active_inst_any_frac"] = c.get("SQ_ACTIVE_INST_ANY", 0) / c["SQ_WAVE_CYCLES"]
     if c.get("SQ_LDS_IDX_ACTIVE"):
-        out.setdefault("derived", {})["lds_bank_conflict_frac"] = c.get("SQ_LDS_BANK_CONFLICT", 0) / c["SQ_LDS_IDX_ACTIVE"]
+        d["lds_bank_conflict_frac"] = c.get("SQ_LDS_BANK_CONFLICT", 0) / c["SQ_LDS_IDX_ACTIVE"]
+    ndisp = max(len(disp.get("SQ_INSTS_VALU", ())), 1)
     if c.get("SQ_WAVES"):
-        out.setdefault("derived", {})["valu_insts_per_wave"] = c.get("SQ_INSTS_VALU", 0) / c["SQ_WAVES"]
-    # GRBM_GUI_ACTIVE rides along in every pass and rocprofv3 sums it over the 8
-    # XCDs: kernel cycles = sum / passes / 8.  A wave64 VALU instruction holds a
-    # SIMD for 4 cycles (SQ_ACTIVE_INST_VALU counts 1 per instruction here);
-    # SQ_LDS_IDX_ACTIVE counts LDS-array cycles per CU.
-    npass = len(disp.get("GRBM_GUI_ACTIVE", ())) or 1
-    npass = max(1, sum(1 for f in files if any(key in r["Kernel_Name"] and r["Counter_Name"] == "GRBM_GUI_ACTIVE"
-                                               for r in csv.DictReader(open(f)))))
+        d["valu_insts_per_wave"] = c.get("SQ_INSTS_VALU", 0) / c["SQ_WAVES"]
+    if c.get("SQ_INSTS_VALU") and a.window_ends:
+        d["valu_insts_per_window_end"] = c["SQ_INSTS_VALU"] / ndisp * 64 / a.window_ends
     if c.get("GRBM_GUI_ACTIVE"):
-        cyc = c["GRBM_GUI_ACTIVE"] / npass / 8
-        d = out.setdefault("derived", {})
-        d["kernel_cycles"] = cyc
+        # every (pass, dispatch) adds one GRBM reading summed over the 8 XCDs
+        cyc = c["GRBM_GUI_ACTIVE"] / 8 / max(len(disp["GRBM_GUI_ACTIVE"]), 1)        # per dispatch
+        d["kernel_cycles_per_dispatch"] = cyc
+        if a.kernel_ms:
+            d["effective_clock_ghz"] = cyc / (a.kernel_ms * 1e-3) / 1e9
+        vd = max(len(disp.get("SQ_ACTIVE_INST_VALU", ())), 1)
         if c.get("SQ_ACTIVE_INST_VALU"):
-            d["valu_busy_frac"] = c["SQ_ACTIVE_INST_VALU"] * 4 / (N_SIMD * cyc)
+            d["valu_busy_frac"] = c["SQ_ACTIVE_INST_VALU"] / vd * 4 / (N_SIMD * cyc)
+        ld = max(len(disp.get("SQ_LDS_IDX_ACTIVE", ())), 1)
         if c.get("SQ_LDS_IDX_ACTIVE"):
-            d["lds_busy_frac"] = c["SQ_LDS_IDX_ACTIVE"] / (N_CU * cyc)
+            d["lds_busy_frac"] = c["SQ_LDS_IDX_ACTIVE"] / ld / (N_CU * cyc)
     print(json.dumps(out, indent=1))
 
 
