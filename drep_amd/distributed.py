@@ -1,0 +1,315 @@
+"""Sharded Mash step + primary clustering across the GPUs of one node
+(BASELINE configs[3]: 10^5 genomes on 8 x MI355X).  One process per GPU
+(torchrun), RCCL over xGMI through torch.distributed ("nccl" backend); gloo
+on CPU in the tests.
+
+The reference does all of this in one process: `mash sketch` per genome on a
+thread pool, `mash paste`, `mash dist -p P` into one TSV, then scipy linkage
+on the pivoted Mdb (drep/d_cluster.py:170-185 -> all_vs_all_MASH 481-596 ->
+cluster_mash_database 598-630 -> store_special('primary_linkage')).  Here:
+
+  1. sketch      rank r sketches its contiguous genome shard (HIP kernels)
+  2. exchange    ONE all-gather of the uint64[N/W][s] sketch shards (+ counts)
+  3. all-pairs   rank r computes the rows [r0, r1) of the triangle balanced by
+                 pair count (parallel.row_partition): one contiguous condensed
+                 segment per rank
+  4. gather      every segment goes to the root GPU, straight into its slice
+                 of one condensed buffer: point-to-point send/recv (the
+                 segments are uneven, so no padded collective), all receives
+                 posted at once so the 7 xGMI links run in parallel
+  5. clustering  on the root GPU: the n x n linkage input built in HBM from
+                 the counts, scipy's linkage algorithm restated (Z
+                 bit-identical, libdrephip drephip_linkage_counts_device),
+                 fcluster -> Cdb; optionally stored in the work-directory
+                 formats of drep_amd.store (condensed counts + the reference's
+                 primary_linkage pickle).
+
+The stage functions are parameters of run_sharded so the plumbing (shards,
+gather order, uneven segments, root assembly) is the same code whether the
+per-rank compute is the HIP library (product) or a CPU stand-in (the gloo
+tests in tests/test_parallel.py).
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+from dataclasses import dataclass
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .parallel import cond_start, gather_sketches, genome_shard, row_partition, segment_size
+
+
+@dataclass
+class ShardPlan:
+    N: int
+    world: int
+    rank: int
+    g0: int          # this rank's genomes [g0, g1), padded shard size nmax
+    g1: int
+    nmax: int
+    r0: int          # this rank's triangle rows [r0, r1)
+    r1: int
+    seg0: int        # condensed index of the segment's first pair
+    seg_len: int
+
+
+def plan(N: int, world: int, rank: int) -> ShardPlan:
+    g0, g1, nmax = genome_shard(N, world, rank)
+    r0, r1 = row_partition(N, world)[rank]
+    return ShardPlan(N, world, rank, g0, g1, nmax, r0, r1, cond_start(r0, N), segment_size(N, r0, r1))
+
+
+def gather_segments(seg, N: int, root: int = 0, out=None):
+    """Condensed segments of every rank -> one condensed vector on the root.
+
+    seg: this rank's segment (1-D tensor; int16 views of the uint16 counts),
+    on the rank's GPU with the nccl backend, on the CPU with gloo.  Returns
+    the full N(N-1)/2 tensor on the root (written into `out` if given), None
+    elsewhere.  Every rank takes part in one batch_isend_irecv: the root posts
+    a receive per other rank into that rank's slice, the others one send."""
+    import torch
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(), dist.get_rank()
+    parts = row_partition(N, world)
+    sizes = [segment_size(N, a, b) for a, b in parts]
+    if seg.numel() < sizes[rank]:
+        raise ValueError("rank %d segment has %d pairs, expected %d" % (rank, seg.numel(), sizes[rank]))
+    # gloo moves host memory only: device segments are staged through the host
+    # (rehearsals of the sharded path on one GPU; RCCL moves device memory)
+    host_p2p = dist.get_backend() == "gloo" and seg.is_cuda
+    ops, landing = [], []
+    full = None
+    if rank == root:
+        npairs = N * (N - 1) // 2
+        full = out if out is not None else torch.empty(npairs, dtype=seg.dtype, device=seg.device)
+        if full.numel() != npairs:
+            raise ValueError("output holds %d pairs, expected %d" % (full.numel(), npairs))
+        for r, (a, b) in enumerate(parts):
+            if not sizes[r]:
+                continue
+            lo = cond_start(a, N)
+            if r == root:
+                full[lo:lo + sizes[r]].copy_(seg[:sizes[r]])
+            elif host_p2p:
+                buf = torch.empty(sizes[r], dtype=seg.dtype)
+                landing.append((full[lo:lo + sizes[r]], buf))
+                ops.append(dist.P2POp(dist.irecv, buf, r))
+            else:
+                ops.append(dist.P2POp(dist.irecv, full[lo:lo + sizes[r]], r))
+    elif sizes[rank]:
+        mine = seg[:sizes[rank]].contiguous()
+        ops.append(dist.P2POp(dist.isend, mine.cpu() if host_p2p else mine, root))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    for dst, buf in landing:
+        dst.copy_(buf)
+    return full
+
+
+SketchFn = Callable[[ShardPlan], Tuple["object", "object"]]            # -> (loc_h [nmax, s], loc_n [nmax])
+AllpairsFn = Callable[["object", "object", ShardPlan], Tuple["object", Optional["object"]]]
+LinkageFn = Callable[["object", Optional["object"], int, str], np.ndarray]
+
+
+def run_sharded(N: int, names: Sequence[str], s: int, sketch_fn: SketchFn, allpairs_fn: AllpairsFn,
+                linkage_fn: LinkageFn, method: str = "average", P_ani: float = 0.9, root: int = 0,
+                sync: Optional[Callable[[], None]] = None) -> Dict:
+    """The sharded pipeline on this rank (torch.distributed initialised).
+
+    Returns, on the root, {'Cdb', 'linkage', 'arguments', 'common', 'denom',
+    'hashes', 'nhash', 'times'}; on the other ranks {'times'}.  `sync` waits
+    for this rank's device work (torch.cuda.synchronize on GPU ranks) so the
+    stage times are real."""
+    import torch
+    import torch.distributed as dist
+    import scipy.cluster.hierarchy as sch
+    from .d_cluster import _gen_cdb_from_fclust
+    world, rank = dist.get_world_size(), dist.get_rank()
+    p = plan(N, world, rank)
+    sync = sync or (lambda: None)
+    times: Dict[str, float] = {}
+
+    def stage(name, fn):
+        sync()
+        dist.barrier()
+        t0 = time.perf_counter()
+        out = fn()
+        sync()
+        dist.barrier()
+        times[name] = time.perf_counter() - t0
+        return out
+
+    loc_h, loc_n = stage("sketch_s", lambda: sketch_fn(p))
+    H, NH = stage("allgather_s", lambda: gather_sketches(loc_h, loc_n))
+    H, NH = H[:N], NH[:N]
+    partial = bool((NH < s).any().item()) if N else False
+    seg_c, seg_d = stage("allpairs_s", lambda: allpairs_fn(H, NH, p))
+    full_c = stage("gather_segments_s", lambda: gather_segments(seg_c, N, root))
+    full_d = None
+    if partial:
+        if seg_d is None:
+            raise ValueError("partial sketches need the denominators")
+        full_d = stage("gather_denominators_s", lambda: gather_segments(seg_d, N, root))
+    res: Dict = {"times": times, "plan": p}
+    if rank == root:
+        t0 = time.perf_counter()
+        Z = linkage_fn(full_c, full_d, N, method)
+        sync()
+        times["linkage_s"] = time.perf_counter() - t0
+        cutoff = 1 - P_ani
+        fcl = sch.fcluster(Z, cutoff, criterion="distance")
+        Cdb = _gen_cdb_from_fclust(fcl, sorted(names)).rename(columns={"cluster": "primary_cluster"})
+        res.update(Cdb=Cdb, linkage=Z, common=full_c, denom=full_d, hashes=H, nhash=NH,
+                   arguments={"linkage_method": method, "linkage_cutoff": cutoff, "comparison_algorithm": "MASH"})
+    return res
+
+
+# ------------------------------------------------------------ HIP stages
+def hip_synth_sketcher(ctx, L: int, family_size: int, seed: int, stream: int, device):
+    """Stage 1 for synthetic genomes (the configs' workload): this rank's shard
+    generated in HBM by the bench generator and sketched, CH genomes at a
+    time (the packed input of 10^4 genomes is ~19 GB)."""
+    import torch
+    from . import _lib
+
+    def fn(p: ShardPlan):
+        s = ctx.s
+        loc_h = torch.full((p.nmax, s), -1, dtype=torch.int64, device=device)
+        loc_n = torch.zeros(p.nmax, dtype=torch.int32, device=device)
+        n = p.g1 - p.g0
+        if n <= 0:
+            return loc_h, loc_n
+        CH = min(n, 10_000)
+        tile = _lib.tile_bases()
+        P = _lib.padded_bases([L])
+        codes = torch.zeros((tile + CH * P) // 16, dtype=torch.int32, device=device)
+        valid = torch.zeros((tile + CH * P) // 32, dtype=torch.int32, device=device)
+        for a in range(0, n, CH):
+            m = min(CH, n - a)
+            ctx.synth_device(seed, p.g0 + a, m, family_size, L, codes.data_ptr(), valid.data_ptr(), stream)
+            ctx.sketch_device(codes.data_ptr(), valid.data_ptr(), np.array([tile + i * P for i in range(m)], np.uint64),
+                              np.full(m, P, np.uint64), np.full(m, L - 20, np.uint64), m,
+                              loc_h[a].data_ptr(), loc_n[a:].data_ptr(), stream)
+        del codes, valid
+        return loc_h, loc_n
+    return fn
+
+
+def hip_file_sketcher(ctx, paths: Sequence[str], threads: int, device):
+    """Stage 1 for FASTA files: this rank's shard of the files read, packed
+    and sketched (drephip_sketch_files), then moved to the rank's GPU."""
+    import torch
+
+    def fn(p: ShardPlan):
+        s = ctx.s
+        loc_h = torch.full((p.nmax, s), -1, dtype=torch.int64, device=device)
+        loc_n = torch.zeros(p.nmax, dtype=torch.int32, device=device)
+        if p.g1 > p.g0:
+            h, nh, _ = ctx.sketch_files(list(paths[p.g0:p.g1]), threads=threads)
+            loc_h[:p.g1 - p.g0] = torch.from_numpy(h.view(np.int64)).to(device)
+            loc_n[:p.g1 - p.g0] = torch.from_numpy(nh.view(np.int32)).to(device)
+        return loc_h, loc_n
+    return fn
+
+
+def hip_allpairs(ctx, stream: int, device):
+    """Stage 3: drephip_allpairs_device over this rank's rows, on its GPU."""
+    import torch
+
+    def fn(H, NH, p: ShardPlan):
+        seg = torch.zeros(max(p.seg_len, 1), dtype=torch.int16, device=device)
+        partial = bool((NH < ctx.s).any().item())
+        segd = torch.zeros(max(p.seg_len, 1), dtype=torch.int16, device=device) if partial else None
+        if p.seg_len:
+            ctx.allpairs_device(H.data_ptr(), NH.data_ptr(), p.N, p.r0, p.r1, seg.data_ptr(),
+                                segd.data_ptr() if segd is not None else None, stream)
+        return seg, segd
+    return fn
+
+
+def hip_linkage(ctx, names: Sequence[str], stream: int):
+    """Stage 5: drephip_linkage_counts_device on the root GPU, rows in
+    sorted-name order (the pivot's order, d_cluster.py:620)."""
+    from .d_cluster import linkage_order, linkage_tables
+
+    def fn(common, denom, N, method):
+        import torch
+        dens = np.array([ctx.s]) if denom is None else torch.unique(denom).cpu().numpy().view(np.uint16)
+        lut, lut_off = linkage_tables(dens, ctx.s)
+        return ctx.linkage_counts_device(common.data_ptr(), None if denom is None else denom.data_ptr(), N,
+                                         linkage_order(names), lut, lut_off, method, stream)
+    return fn
+
+
+def synthetic_names(N: int) -> List[str]:
+    """Genome names of the synthetic workload: sorting them keeps index order."""
+    return ["synthetic_%07d.fna" % i for i in range(N)]
+
+
+def main(argv: Optional[Sequence[str]] = None) -> int:
+    """configs[3] as one job: `python -m torch.distributed.run --nproc-per-node 8
+    --master-addr 127.0.0.1 -m drep_amd.distributed --genomes 100000`.  Prints
+    one JSON line (rank 0); --out stores the condensed counts, the
+    primary_linkage pickle and the primary Cdb in drep_amd.store formats."""
+    import argparse
+    import torch
+    import torch.distributed as dist
+    from . import _lib
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--genomes", type=int, default=100_000)
+    ap.add_argument("--genome-bp", type=int, default=5_000_000)
+    ap.add_argument("--sketch", type=int, default=1000)
+    ap.add_argument("--family-size", type=int, default=100)
+    ap.add_argument("--seed", type=int, default=0xD2E9)
+    ap.add_argument("--method", default="average")
+    ap.add_argument("--P-ani", type=float, default=0.9)
+    ap.add_argument("--out", default=None, help="work-directory data folder to store the results in")
+    a = ap.parse_args(argv)
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0)) % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    backend = os.environ.get("DREPHIP_DIST_BACKEND", "nccl")      # nccl = RCCL over xGMI
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world)
+    N = a.genomes
+    names = synthetic_names(N)
+    ctx = _lib.Context(device=local, k=21, s=a.sketch, seed=42)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    res = run_sharded(N, names, a.sketch, hip_synth_sketcher(ctx, a.genome_bp, a.family_size, a.seed, stream, dev),
+                      hip_allpairs(ctx, stream, dev), hip_linkage(ctx, names, stream), a.method, a.P_ani,
+                      sync=lambda: torch.cuda.synchronize(dev))
+    if rank == 0:
+        out = {"job": "configs[3]-style sharded Mash step + primary clustering", "genomes": N,
+               "genome_bp": a.genome_bp, "sketch": a.sketch, "n_gpus": world, "backend": backend,
+               "method": a.method, "P_ani": a.P_ani, "times": res["times"],
+               "pairs": N * (N - 1) // 2, "primary_clusters": int(res["Cdb"]["primary_cluster"].nunique())}
+        t = res["times"]
+        out["pairs_per_s_job"] = out["pairs"] / sum(v for k, v in t.items())
+        if a.out:
+            from .d_cluster import CondensedMash
+            from .store import store_condensed, store_primary_linkage
+            os.makedirs(a.out, exist_ok=True)
+            cm = CondensedMash(names, names, res["common"].cpu().numpy().view(np.uint16),
+                               None if res["denom"] is None else res["denom"].cpu().numpy().view(np.uint16),
+                               res["nhash"].cpu().numpy().view(np.uint32), np.full(N, a.genome_bp, np.uint64),
+                               a.sketch)
+            store_condensed(a.out, cm)
+            store_primary_linkage(a.out, res["linkage"], None, res["arguments"])
+            res["Cdb"].to_csv(os.path.join(a.out, "primary_Cdb.csv"), index=False)
+            out["stored"] = a.out
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

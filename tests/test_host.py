@@ -323,3 +323,37 @@ def test_device_list_and_balanced_shards(monkeypatch):
         if n_items >= 100:
             tot = [w[s].sum() for s in sh]
             assert max(tot) - min(tot) <= 2 * w.max()
+
+
+@pytest.mark.parametrize("partial", [False, True])
+def test_condensed_store_roundtrip(tmp_path, partial):
+    """drep_amd.store: the condensed Mash result and the reference-format
+    primary_linkage pickle round-trip, and the long-form Mdb rebuilt from the
+    stored counts equals the one built before storing."""
+    from drep_amd.d_cluster import CondensedMash, cluster_mash_condensed, mdb_from_condensed
+    from drep_amd.store import load_condensed, load_primary_linkage, store_condensed, store_primary_linkage
+    rng = np.random.default_rng(1)
+    N, s = 12, 1000
+    c = rng.integers(0, s + 1, N * (N - 1) // 2).astype(np.uint16)
+    d = np.full(len(c), s, np.uint16)
+    nh = np.full(N, s, np.uint32)
+    if partial:
+        d[::3] = 700
+        c = np.minimum(c, d)
+        nh[2] = 650
+    names = ["g%02d.fa" % i for i in rng.permutation(N)]
+    cm = CondensedMash(names, ["/x/" + n for n in names], c, d, nh, np.arange(N, dtype=np.uint64) * 1000, s)
+    store_condensed(str(tmp_path), cm)
+    assert os.path.exists(tmp_path / "MASH_files" / "condensed" / "denom.npy") == partial
+    back = load_condensed(str(tmp_path))
+    assert back.names == cm.names and back.locations == cm.locations and back.s == s
+    for a in ("common", "denom", "nhash", "length"):
+        assert np.array_equal(np.asarray(getattr(back, a)), getattr(cm, a)), a
+    m0 = mdb_from_condensed(cm.names, cm.common, cm.denom, cm.nhash, s)
+    m1 = mdb_from_condensed(back.names, back.common, back.denom, back.nhash, s)
+    assert m0.equals(m1)
+    cdb, (Z, db, args) = cluster_mash_condensed(back, clusterAlg="average", P_ani=0.9)
+    store_primary_linkage(str(tmp_path), Z, db, args)
+    pl = load_primary_linkage(str(tmp_path))
+    assert np.array_equal(pl["linkage"], Z) and pl["db"] is None and pl["arguments"] == args
+    assert set(pl) == {"linkage", "db", "arguments"}          # WorkDirectory.import_clusters keys

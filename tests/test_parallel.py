@@ -82,3 +82,103 @@ def test_gloo_sharded_pipeline_matches_single_process(tmp_path, world):
     assert np.array_equal(full, want)
     for r in range(world):   # every rank saw the full, ordered sketch matrix
         assert np.array_equal(np.load(os.path.join(tmp_path, "H%d.npy" % r)), h)
+
+
+def _worker_pipeline(rank, world, port, N, out_dir, partial):
+    """One rank of drep_amd.distributed.run_sharded with CPU stand-ins for the
+    HIP stages (oracle sketch / merge, scipy linkage): the sharding, the
+    all-gather, the uneven segment gather to the root and the root's
+    clustering are the product code."""
+    import torch
+    import torch.distributed as dist
+    import oracle
+    from drep_amd import distributed as D
+    from drep_amd.d_cluster import CondensedMash, cluster_mash_condensed
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    names = D.synthetic_names(N)
+
+    def sketch_fn(p):
+        loc_h = torch.full((p.nmax, S), -1, dtype=torch.int64)
+        loc_n = torch.zeros(p.nmax, dtype=torch.int32)
+        if p.g1 > p.g0:
+            h, nh = oracle.sketch_synth(p.g0, p.g1 - p.g0, 60_000, seed=4, family_size=5, s=S, threads=1)
+            if partial:                      # genomes 5, 6, 7 keep a partial sketch
+                for g in range(p.g0, p.g1):
+                    if g in (5, 6, 7):
+                        h[g - p.g0, 100 + g:] = np.iinfo(np.uint64).max
+                        nh[g - p.g0] = 100 + g
+            loc_h[:p.g1 - p.g0] = torch.from_numpy(h.view(np.int64))
+            loc_n[:p.g1 - p.g0] = torch.from_numpy(nh.view(np.int32))
+        return loc_h, loc_n
+
+    def allpairs_fn(H, NH, p):
+        Hn = H.numpy().view(np.uint64)
+        Nn = NH.numpy().view(np.uint32)
+        if not p.seg_len:
+            return torch.zeros(1, dtype=torch.int16), torch.zeros(1, dtype=torch.int16)
+        c, d = oracle.allpairs(Hn, Nn, S, r0=p.r0, r1=min(p.r1, N - 1), threads=1)
+        return (torch.from_numpy(c[:p.seg_len].view(np.int16).copy()),
+                torch.from_numpy(d[:p.seg_len].view(np.int16).copy()))
+
+    def linkage_fn(common, denom, n, method):
+        c = common.numpy().view(np.uint16)
+        d = denom.numpy().view(np.uint16) if denom is not None else np.full(len(c), S, np.uint16)
+        cm = CondensedMash(names, names, c, d, np.zeros(n, np.uint32), np.zeros(n, np.uint64), S)
+        _, (Z, _, _) = cluster_mash_condensed(cm, clusterAlg=method)
+        return Z
+
+    res = D.run_sharded(N, names, S, sketch_fn, allpairs_fn, linkage_fn, "average", 0.9)
+    if rank == 0:
+        np.save(os.path.join(out_dir, "Z.npy"), res["linkage"])
+        np.save(os.path.join(out_dir, "common.npy"), res["common"].numpy().view(np.uint16))
+        if res["denom"] is not None:
+            np.save(os.path.join(out_dir, "denom.npy"), res["denom"].numpy().view(np.uint16))
+        res["Cdb"].to_csv(os.path.join(out_dir, "Cdb.csv"), index=False)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,partial", [(2, False), (3, False), (3, True)])
+def test_gloo_sharded_clustering_matches_single_process(tmp_path, world, partial):
+    """configs[3]'s sharded job (drep_amd.distributed.run_sharded) on CPU with
+    gloo: the root's reassembled condensed counts, linkage Z and primary Cdb
+    equal the single-process result (reference chain d_cluster.py:170-185)."""
+    import pandas as pd
+    import torch.multiprocessing as mp
+    import oracle
+    from drep_amd import distributed as D
+    from drep_amd.d_cluster import CondensedMash, cluster_mash_condensed
+    N = 29
+    port = _free_port()
+    mp.start_processes(_worker_pipeline, args=(world, port, N, str(tmp_path), partial), nprocs=world, join=True,
+                       start_method="spawn")
+    h, nh = oracle.sketch_synth(0, N, 60_000, seed=4, family_size=5, s=S, threads=2)
+    if partial:
+        for g in (5, 6, 7):
+            h[g, 100 + g:] = np.iinfo(np.uint64).max
+            nh[g] = 100 + g
+    want_c, want_d = oracle.allpairs(h, nh, S)
+    assert np.array_equal(np.load(os.path.join(tmp_path, "common.npy")), want_c)
+    if partial:
+        assert np.array_equal(np.load(os.path.join(tmp_path, "denom.npy")), want_d)
+        assert (want_d < S).any()
+    names = D.synthetic_names(N)
+    cm = CondensedMash(names, names, want_c, want_d, nh, np.zeros(N, np.uint64), S)
+    cdb, (Z, _, _) = cluster_mash_condensed(cm, clusterAlg="average", P_ani=0.9)
+    assert np.array_equal(np.load(os.path.join(tmp_path, "Z.npy")), Z)
+    got = pd.read_csv(os.path.join(tmp_path, "Cdb.csv"))
+    assert got["genome"].tolist() == cdb["genome"].tolist()
+    assert got["primary_cluster"].tolist() == cdb["primary_cluster"].tolist()
+    assert cdb["primary_cluster"].nunique() > 1
+
+
+def test_shard_plan_covers_everything():
+    from drep_amd import distributed as D
+    for N in (2, 7, 1000, 100_000):
+        for W in (1, 2, 3, 8):
+            ps = [D.plan(N, W, r) for r in range(W)]
+            assert sum(p.seg_len for p in ps) == N * (N - 1) // 2
+            assert sum(p.g1 - p.g0 for p in ps) == N
+            for a, b in zip(ps[:-1], ps[1:]):
+                assert a.seg0 + a.seg_len == b.seg0 or b.seg_len == 0
