@@ -57,6 +57,8 @@ SIGNATURES = {
                                      C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "drephip_sketch": (C.c_int, [vp, u8p, u64p, C.c_uint32, u64p, C.c_uint32, u64p, u32p, u64p]),
     "drephip_sketch_files": (C.c_int, [vp, C.POINTER(C.c_char_p), C.c_uint32, C.c_int, u64p, u32p, u64p]),
+    "drephip_last_ingest_stats": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                            C.POINTER(C.c_double), C.POINTER(C.c_uint32)]),
     "drephip_sketch_device": (C.c_int, [vp, vp, vp, u64p, u64p, u64p, C.c_uint32, vp, vp, vp]),
     "drephip_sketch_device_async": (C.c_int, [vp, vp, vp, u64p, u64p, u64p, C.c_uint32, vp, vp, vp]),
     "drephip_sketch_wait": (C.c_int, [vp, C.POINTER(C.c_int)]),
@@ -258,6 +260,14 @@ class Context:
         check(lib().drephip_sketch_files(self._h, arr, n, int(threads), hashes.reshape(-1), nhash, length),
               "drephip_sketch_files")
         return hashes, nhash, length
+
+    def ingest_stats(self):
+        """{produce_s, gpu_s, wall_s, batches} of the last sketch_files call."""
+        a, b, c = C.c_double(0), C.c_double(0), C.c_double(0)
+        n = C.c_uint32(0)
+        check(lib().drephip_last_ingest_stats(self._h, C.byref(a), C.byref(b), C.byref(c), C.byref(n)),
+              "drephip_last_ingest_stats")
+        return {"produce_s": a.value, "gpu_s": b.value, "wall_s": c.value, "batches": n.value}
 
     def sketch_records(self, seq: np.ndarray, rec_off: np.ndarray, genome_rec_off: np.ndarray):
         seq = np.ascontiguousarray(seq, dtype=np.uint8)

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -330,62 +331,134 @@ DREPHIP_EXPORT int drephip_sketch(drephip_ctx *ctx, const uint8_t *seq, const ui
                               nhash_out);
 }
 
+// One batch of FASTA files read and packed into pinned host memory.
+struct IngestBatch {
+    uint32_t g0 = 0, n = 0;
+    std::vector<uint64_t> off, pad, nk, length;
+    uint64_t bases = 0;                 // padded positions of the batch (codes/valid span)
+    int err = 0;
+    std::string msg;
+    double seconds = 0;
+};
+static uint64_t ingest_batch_bases() {
+    if (const char *e = getenv("DREPHIP_INGEST_BATCH_BASES")) {     // tests: force many batches
+        const uint64_t v = strtoull(e, nullptr, 10);
+        if (v) return v;
+    }
+    return 1ull << 30;                  // ~1 Gbase of sequence per batch
+}
+
+// Read files [g0, ...) until the batch holds >= target bases, then pack them
+// into `slot` (zeroed only where genomes are; every thread packs its own).
+static void produce_batch(const char *const *paths, uint32_t g0, uint32_t n_genomes, int threads, int k,
+                          uint64_t target, PinnedSlot &slot, IngestBatch &B, int device) {
+    const auto t0 = std::chrono::steady_clock::now();
+    (void)hipSetDevice(device);         // the pinned batch belongs with the context's device
+    B = IngestBatch();
+    B.g0 = g0;
+    std::vector<Genome> gs;
+    uint64_t bases = 0;
+    uint32_t g1 = g0;
+    // files are read `threads` at a time, until the batch holds >= target bases
+    const uint32_t per = (uint32_t)std::max(1, std::min(64, threads > 0 ? threads
+                                                               : (int)std::thread::hardware_concurrency()));
+    while (g1 < n_genomes && bases < target) {
+        const uint32_t chunk = std::min<uint32_t>(n_genomes - g1, per);
+        std::vector<Genome> part(chunk);
+        std::vector<int> err(chunk, 0);
+        std::vector<std::string> msg(chunk);
+        parallel_for(chunk, threads, [&](uint32_t i) {
+            err[i] = read_fasta(paths[g1 + i], part[i]);
+            if (err[i]) msg[i] = drephip_last_error();
+        });
+        for (uint32_t i = 0; i < chunk; i++)
+            if (err[i]) { B.err = DREPHIP_ERR_IO; B.msg = msg[i]; return; }
+        for (auto &g : part) { bases += g.length; gs.push_back(std::move(g)); }
+        g1 += chunk;
+    }
+    const uint32_t n = g1 - g0;
+    B.n = n;
+    B.off.resize(n); B.pad.resize(n); B.nk.resize(n); B.length.resize(n);
+    uint64_t cur = kTile;
+    for (uint32_t i = 0; i < n; i++) {
+        B.off[i] = cur;
+        B.pad[i] = padded_span(genome_span(gs[i].rec_len.data(), (uint32_t)gs[i].rec_len.size()));
+        cur += B.pad[i];
+        B.length[i] = gs[i].length;
+    }
+    B.bases = cur;
+    if (slot.reserve(cur / 16 * 4, cur / 32 * 4)) {
+        B.err = DREPHIP_ERR_NOMEM; B.msg = "hipHostMalloc of the pinned ingest batch failed"; return;
+    }
+    uint32_t *codes = slot.codes, *valid = slot.valid;
+    memset(codes, 0, kTile / 16 * 4);
+    memset(valid, 0, kTile / 32 * 4);
+    parallel_for(n, threads, [&](uint32_t i) {
+        memset(codes + B.off[i] / 16, 0, B.pad[i] / 16 * 4);
+        memset(valid + B.off[i] / 32, 0, B.pad[i] / 32 * 4);
+        B.nk[i] = pack_records(gs[i].seq.data(), gs[i].rec_len.data(), (uint32_t)gs[i].rec_len.size(), k,
+                               codes, valid, B.off[i]);
+        std::vector<uint8_t, NoInitAlloc<uint8_t>>().swap(gs[i].seq);   // free as we go
+    });
+    B.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// Ingest pipeline: a producer thread reads + packs batch i+1 (on `threads`
+// workers, into the other of two pinned buffers) while this thread copies
+// batch i to the GPU and sketches it -- the GPU work hides behind the host
+// ingest, which is the slower side by two orders of magnitude.
 DREPHIP_EXPORT int drephip_sketch_files(drephip_ctx *ctx, const char *const *paths, uint32_t n_genomes,
                                         int threads, uint64_t *hashes_out, uint32_t *nhash_out,
                                         uint64_t *length_out) {
     GUARD_CTX(ctx);
+    ctx->ingest = IngestStats();
     if (n_genomes == 0) return DREPHIP_OK;
     if (!paths || !hashes_out || !nhash_out) { set_error("null argument"); return DREPHIP_ERR_ARG; }
-    const uint64_t kBatchBases = 1ull << 31;   // ~2 Gbase of ASCII per batch
-    uint32_t g0 = 0;
-    while (g0 < n_genomes) {
-        // read a batch of files in parallel (bounded by bases read so far)
-        std::vector<Genome> gs;
-        uint64_t bases = 0;
-        uint32_t g1 = g0;
-        while (g1 < n_genomes && bases < kBatchBases) {
-            const uint32_t chunk = std::min<uint32_t>(n_genomes - g1, 64);
-            std::vector<Genome> part(chunk);
-            std::vector<int> err(chunk, 0);
-            std::vector<std::string> msg(chunk);
-            parallel_for(chunk, threads, [&](uint32_t i) {
-                err[i] = read_fasta(paths[g1 + i], part[i]);
-                if (err[i]) msg[i] = drephip_last_error();
+    int rc;
+    if ((rc = refuse_if_pending(ctx))) return rc;
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint64_t target = ingest_batch_bases();
+    PinnedSlot *slots = ctx->ingest_slots;          // kept across calls: pinned allocation is slow
+    IngestBatch B[2];
+    const int k = ctx->k;
+    std::thread producer([&] { produce_batch(paths, 0, n_genomes, threads, k, target, slots[0], B[0], ctx->device); });
+    uint32_t b = 0;
+    rc = DREPHIP_OK;
+    for (;;) {
+        producer.join();
+        IngestBatch &cur = B[b & 1];
+        if (cur.err) { set_error(cur.msg); rc = cur.err; break; }
+        const uint32_t next_g = cur.g0 + cur.n;
+        const bool more = next_g < n_genomes;
+        if (more)
+            producer = std::thread([&, next_g, b] {
+                produce_batch(paths, next_g, n_genomes, threads, k, target, slots[(b + 1) & 1], B[(b + 1) & 1],
+                              ctx->device);
             });
-            for (uint32_t i = 0; i < chunk; i++)
-                if (err[i]) { set_error(msg[i]); return DREPHIP_ERR_IO; }
-            for (auto &g : part) { bases += g.length; gs.push_back(std::move(g)); }
-            g1 += chunk;
+        const auto g0 = std::chrono::steady_clock::now();
+        if (length_out) std::copy(cur.length.begin(), cur.length.end(), length_out + cur.g0);
+        rc = sketch_packed_host(ctx, slots[b & 1].codes, cur.bases / 16, slots[b & 1].valid, cur.bases / 32, cur.off,
+                                cur.pad, cur.nk, hashes_out + (uint64_t)cur.g0 * ctx->s, nhash_out + cur.g0);
+        ctx->ingest.gpu_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - g0).count();
+        ctx->ingest.produce_s += cur.seconds;
+        ctx->ingest.batches++;
+        if (rc || !more) {
+            if (more) producer.join();
+            break;
         }
-        const uint32_t n = g1 - g0;
-        std::vector<uint64_t> off(n), pad(n), nk(n);
-        uint64_t cur = kTile;
-        for (uint32_t i = 0; i < n; i++) {
-            off[i] = cur;
-            pad[i] = padded_span(genome_span(gs[i].rec_len.data(), (uint32_t)gs[i].rec_len.size()));
-            cur += pad[i];
-            if (length_out) length_out[g0 + i] = gs[i].length;
-        }
-        // packed batch in pinned host memory (DMA'd without staging); every
-        // thread zeroes and packs its own genomes' slots
-        uint32_t *codes, *valid;
-        int rc;
-        if ((rc = pinned_host(ctx, "in_codes_h", cur / 16 * 4, (void **)&codes))) return rc;
-        if ((rc = pinned_host(ctx, "in_valid_h", cur / 32 * 4, (void **)&valid))) return rc;
-        memset(codes, 0, kTile / 16 * 4);
-        memset(valid, 0, kTile / 32 * 4);
-        parallel_for(n, threads, [&](uint32_t i) {
-            memset(codes + off[i] / 16, 0, pad[i] / 16 * 4);
-            memset(valid + off[i] / 32, 0, pad[i] / 32 * 4);
-            nk[i] = pack_records(gs[i].seq.data(), gs[i].rec_len.data(), (uint32_t)gs[i].rec_len.size(),
-                                 ctx->k, codes, valid, off[i]);
-        });
-        gs.clear();
-        rc = sketch_packed_host(ctx, codes, cur / 16, valid, cur / 32, off, pad, nk,
-                                hashes_out + (uint64_t)g0 * ctx->s, nhash_out + g0);
-        if (rc) return rc;
-        g0 = g1;
+        b++;
     }
+    ctx->ingest.wall_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+}
+
+DREPHIP_EXPORT int drephip_last_ingest_stats(drephip_ctx *ctx, double *produce_s, double *gpu_s, double *wall_s,
+                                             uint32_t *batches) {
+    if (!ctx) { set_error("null context"); return DREPHIP_ERR_ARG; }
+    if (produce_s) *produce_s = ctx->ingest.produce_s;
+    if (gpu_s) *gpu_s = ctx->ingest.gpu_s;
+    if (wall_s) *wall_s = ctx->ingest.wall_s;
+    if (batches) *batches = ctx->ingest.batches;
     return DREPHIP_OK;
 }
 

@@ -15,6 +15,41 @@ struct DevBuf {
     size_t bytes = 0;
 };
 
+// A pinned host buffer pair of the ingest pipeline (drephip_sketch_files).
+struct PinnedSlot {
+    uint32_t *codes = nullptr, *valid = nullptr;
+    size_t codes_bytes = 0, valid_bytes = 0;
+    PinnedSlot() = default;
+    PinnedSlot(const PinnedSlot &) = delete;
+    PinnedSlot &operator=(const PinnedSlot &) = delete;
+    ~PinnedSlot() {
+        if (codes) (void)hipHostFree(codes);
+        if (valid) (void)hipHostFree(valid);
+    }
+    int reserve(size_t cb, size_t vb) {
+        if (cb > codes_bytes) {
+            if (codes) (void)hipHostFree(codes);
+            codes = nullptr; codes_bytes = 0;
+            if (hipHostMalloc((void **)&codes, cb, hipHostMallocPortable) != hipSuccess) { codes = nullptr; return -1; }
+            codes_bytes = cb;
+        }
+        if (vb > valid_bytes) {
+            if (valid) (void)hipHostFree(valid);
+            valid = nullptr; valid_bytes = 0;
+            if (hipHostMalloc((void **)&valid, vb, hipHostMallocPortable) != hipSuccess) { valid = nullptr; return -1; }
+            valid_bytes = vb;
+        }
+        return 0;
+    }
+};
+
+struct IngestStats {          // last drephip_sketch_files call
+    double produce_s = 0;     // host read + pack, summed over batches (producer thread)
+    double gpu_s = 0;         // H2D + sketch kernels + D2H, summed over batches (calling thread)
+    double wall_s = 0;        // the whole call
+    uint32_t batches = 0;
+};
+
 struct drephip_ctx {
     int device = 0;
     int k = 21;
@@ -75,6 +110,8 @@ struct drephip_ctx {
         bool active = false;
         hipEvent_t ev = nullptr;
     } apend;
+    IngestStats ingest;
+    PinnedSlot ingest_slots[2];   // the two pinned batch buffers, kept across calls
 };
 
 namespace drephip {

@@ -2,11 +2,16 @@
 // reads (drep/d_cluster.py:543-544), turned into the packed layout the sketch
 // kernel streams (2-bit codes + validity bitmap, include/drephip.h).
 //
-// Parsing follows kseq.h as Mash uses it: a record starts at a line beginning
-// with '>' (or '@'); its sequence is every following line, line breaks (and a
-// line-final '\r') dropped, until the next header; a line starting with '+'
-// ends the sequence (FASTQ quality follows).  Bytes are upper-cased a-z; only
-// A/C/G/T are valid bases, anything else breaks k-mers.  Plain or gzip input.
+// Parsing follows kseq.h's kseq_read as Mash loops over it (oracle/
+// mash_oracle.c restates it byte by byte): with no header pending, any bytes
+// up to the next '>' or '@' are skipped; the header is the rest of that line;
+// the sequence is every following line (line breaks and a line-final '\r'
+// dropped) until a line starting with '>', '@' or '+'; after '+' (FASTQ) the
+// rest of that line is skipped and whole quality lines are read until the
+// quality is at least as long as the sequence -- a quality of a different
+// length (or none) ends the file there, that record not kept, as kseq_read's
+// -2 ends Mash's loop.  Bytes are upper-cased a-z; only A/C/G/T are valid
+// bases, anything else breaks k-mers.  Plain or gzip input.
 //
 // Speed: the file is read in 4 MiB blocks, lines are found with memchr and
 // sequence lines appended with memcpy; packing builds each 32-base group
@@ -33,6 +38,12 @@ __attribute__((target("sse2"))) static inline uint64_t newline_mask64(const char
     return m;
 }
 
+// first '>' or '@' in [p, end), or end
+static inline const char *find_header_char(const char *p, const char *end) {
+    while (p < end && *p != '>' && *p != '@') p++;
+    return p;
+}
+
 int read_fasta(const char *path, Genome &g) {
     gzFile f = gzopen(path, "rb");
     if (!f) { set_error(std::string("cannot open ") + path); return -1; }
@@ -56,33 +67,74 @@ int read_fasta(const char *path, Genome &g) {
     auto end_seq_line = [&] {                      // a line-final '\r' is dropped
         if (used && g.seq[used - 1] == '\r' && g.rec_len.back()) { used--; g.rec_len.back()--; }
     };
-    // Line state machine, carried across blocks: START (first byte of a line),
-    // SEQ (inside a sequence line: copied in 64-byte chunks up to the newline),
-    // SKIP (header / '+' / text outside a record: skipped to the newline).
-    enum { START, SEQ, SKIP } st = START;
-    bool in_seq = false;
+    auto drop_last_record = [&] { used -= g.rec_len.back(); g.rec_len.pop_back(); };
+    // Byte state machine, carried across blocks:
+    //   HUNT   no header pending: skip to the next '>' or '@' (anywhere)
+    //   HDR0   just after '>'/'@': the record exists once one more byte does
+    //   HDR    rest of the header line
+    //   START  first byte of a line inside a record
+    //   SEQ    inside a sequence line (copied in 64-byte chunks up to '\n')
+    //   PLUS   rest of a FASTQ '+' line
+    //   QUAL   FASTQ quality lines, counted until >= the sequence length
+    enum { HUNT, HDR0, HDR, START, SEQ, PLUS, QUAL } st = HUNT;
+    uint64_t qlen = 0, qline = 0;                  // quality so far; current quality line's length
+    char qlast = 0;                                // its last byte (a final '\r' is not counted)
+    bool stop = false;
     const size_t kBlock = 4u << 20;
     static thread_local std::vector<char> buf(kBlock + 64);   // reused across files (no 4 MiB memset each)
-    for (;;) {
+    while (!stop) {
         const int got = gzread(f, buf.data(), (unsigned)kBlock);
         if (got < 0) { gzclose(f); set_error(std::string("read error in ") + path); return -1; }
         if (got == 0) break;
         const char *p = buf.data(), *end = p + got;
-        while (p < end) {
-            if (st == START) {
-                const char c = *p;
-                if (c == '\n') { p++; continue; }                                     // empty line
-                if (c == '>' || c == '@') { g.rec_len.push_back(0); in_seq = true; st = SKIP; continue; }
-                if (c == '+') { in_seq = false; st = SKIP; continue; }
-                st = in_seq ? SEQ : SKIP;
+        while (p < end && !stop) {
+            switch (st) {
+            case HUNT:
+                p = find_header_char(p, end);
+                if (p < end) { p++; st = HDR0; }
                 continue;
-            }
-            if (st == SKIP) {
+            case HDR0:
+                g.rec_len.push_back(0);
+                st = HDR;
+                continue;
+            case HDR: {
                 const char *nl = (const char *)memchr(p, '\n', end - p);
-                if (!nl) { p = end; break; }
+                if (!nl) { p = end; continue; }
                 p = nl + 1;
                 st = START;
                 continue;
+            }
+            case PLUS: {
+                const char *nl = (const char *)memchr(p, '\n', end - p);
+                if (!nl) { p = end; continue; }
+                p = nl + 1;
+                st = QUAL; qlen = 0; qline = 0; qlast = 0;
+                continue;
+            }
+            case QUAL: {
+                const char *nl = (const char *)memchr(p, '\n', end - p);
+                const char *le = nl ? nl : end;
+                if (le > p) { qline += (uint64_t)(le - p); qlast = le[-1]; }
+                if (!nl) { p = end; continue; }
+                p = nl + 1;
+                qlen += qline - (qline && qlast == '\r');
+                qline = 0; qlast = 0;
+                if (qlen >= g.rec_len.back()) {
+                    if (qlen != g.rec_len.back()) { drop_last_record(); stop = true; }     // kseq_read: -2
+                    st = HUNT;
+                }
+                continue;
+            }
+            case START: {
+                const char c = *p;
+                if (c == '\n') { p++; continue; }                                     // empty line
+                if (c == '>' || c == '@') { p++; st = HDR0; continue; }
+                if (c == '+') { p++; st = PLUS; continue; }
+                st = SEQ;
+                continue;
+            }
+            case SEQ:
+                break;
             }
             // SEQ: 64-byte chunks; every sequence line inside a chunk is
             // compacted with a fixed 64-byte copy (the output cursor advances by
@@ -133,7 +185,14 @@ int read_fasta(const char *path, Genome &g) {
         next_state:;
         }
     }
+    // end of file
     if (st == SEQ) end_seq_line();
+    else if (st == HDR0) { /* '>' as the last byte: kseq_read returns -1, no record */ }
+    else if (st == PLUS) drop_last_record();                       // no quality string: -2
+    else if (st == QUAL && !stop) {
+        if (qline) qlen += qline - (qlast == '\r');                  // last line, no '\n'
+        if (qlen != g.rec_len.back()) drop_last_record();            // short quality: -2
+    }
     gzclose(f);
     g.seq.resize(used);
     for (uint64_t l : g.rec_len) g.length += l;

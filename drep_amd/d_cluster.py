@@ -9,12 +9,14 @@ directory -- with the external ``mash sketch`` / ``mash paste`` /
 reference (drep/d_cluster.py)    here
 ===============================  ==========================================
 all_vs_all_MASH       481-596    :func:`all_vs_all_MASH`
-cluster_mash_database 598-630    :func:`cluster_mash_database`
-cluster_hierarchical  429-461    :func:`cluster_hierarchical`
-_gen_cdb_from_fclust  463-479    :func:`_gen_cdb_from_fclust`
+cluster_mash_database 598-630    :func:`cluster_mash_database` (its
+  cluster_hierarchical 429-461 /  linkage + fcluster + Cdb steps inline)
+  _gen_cdb_from_fclust 463-479
 _get_genome_name_from_fasta 632  :func:`_get_genome_name_from_fasta`
-load_genomes         1483-1518   :func:`load_genomes`
 ===============================  ==========================================
+
+dRep's own ``load_genomes`` (1483-1518) builds the Bdb these functions take;
+it is not on the hot path and stays dRep's.
 
 Beyond the reference (needed at 10^4-10^5 genomes, where an N^2-row Mdb does
 not fit): :func:`all_vs_all_MASH_condensed` returns the condensed
@@ -48,31 +50,6 @@ MASH_SEED = 42       # Mash default hash seed
 def _get_genome_name_from_fasta(fasta):
     """os.path.basename (reference drep/d_cluster.py:632-642)."""
     return str(os.path.basename(fasta))
-
-
-def load_genomes(genome_list):
-    """List of genome paths (or one text file listing them) -> Bdb
-    [genome, location] (reference drep/d_cluster.py:1483-1518)."""
-    assert type(genome_list) == type(list())
-    if len(genome_list) == 1:
-        logging.info('Loading genomes from a list')
-        try:
-            Table = {'genome': [], 'location': []}
-            with open(genome_list[0], 'r') as o:
-                for line in o.readlines():
-                    genome = line.strip()
-                    assert os.path.isfile(genome), "{0} is not a file".format(genome)
-                    Table['genome'].append(os.path.basename(genome))
-                    Table['location'].append(os.path.abspath(genome))
-            return pd.DataFrame(Table)
-        except Exception:
-            logging.info('Nevermind! Ill try loading as a genome now')
-    Table = {'genome': [], 'location': []}
-    for genome in genome_list:
-        assert os.path.isfile(genome), "{0} is not a file".format(genome)
-        Table['genome'].append(os.path.basename(genome))
-        Table['location'].append(os.path.abspath(genome))
-    return pd.DataFrame(Table)
 
 
 # ----------------------------------------------------------- distances
@@ -403,60 +380,45 @@ def mash_pvalue(common: np.ndarray, len_r: np.ndarray, len_q: np.ndarray, s: int
 def write_mash_table(path: str, cm: CondensedMash) -> None:
     """MASH_table.tsv as `mash dist ALL ALL` prints it (d_cluster.py:570-572):
     reference, query, %g distance, %g p-value, common/denom; outer loop over
-    queries.  N^2 lines -- only sensible for small N."""
+    queries.  N^2 lines (15 GB of text at 10^4 genomes) -- only for callers
+    that read the raw table; one query row at a time, distances by table
+    lookup per denominator, p-values vectorised over the row."""
     N = len(cm.names)
     nh = np.minimum(cm.nhash.astype(np.int64), cm.s)
-    Cm = _square(cm.common, N, nh.astype(np.uint16)).astype(np.int64)
-    Dm = _square(cm.denom, N, nh.astype(np.uint16)).astype(np.int64)
+    Cm = _square(np.asarray(cm.common), N, nh.astype(np.uint16)).astype(np.int64)
+    Dm = _square(np.asarray(cm.denom), N, nh.astype(np.uint16)).astype(np.int64)
+    luts = {int(d): (_lib.distance_lut(int(d), MASH_K) if d else np.zeros(1)) for d in np.unique(Dm)}
+    refs = list(cm.locations)
     with open(path, 'w') as fh:
         for q in range(N):
-            lut = {}
             dist = np.empty(N)
-            for r in range(N):
-                key = (Cm[q, r], Dm[q, r])
-                if key not in lut:
-                    lut[key] = _lib.distance_lut(int(key[1]), MASH_K)[key[0]] if key[1] else 0.0
-                dist[r] = lut[key]
+            for d, lut in luts.items():
+                sel = Dm[q] == d
+                if sel.any():
+                    dist[sel] = lut[Cm[q, sel]]
             p = mash_pvalue(Cm[q], cm.length, np.full(N, cm.length[q]), cm.s)
-            for r in range(N):
-                fh.write("%s\t%s\t%s\t%s\t%d/%d\n" % (cm.locations[r], cm.locations[q], "%g" % dist[r],
-                                                     "%g" % p[r], Cm[q, r], Dm[q, r]))
+            qn = refs[q]
+            fh.write("".join("%s\t%s\t%g\t%g\t%d/%d\n" % (r, qn, x, y, c, d)
+                             for r, x, y, c, d in zip(refs, dist.tolist(), p.tolist(), Cm[q].tolist(),
+                                                      Dm[q].tolist())))
 
 
 # ------------------------------------------------------ primary clustering
-def cluster_hierarchical(db, linkage_method='single', linkage_cutoff=0.10):
-    """Hierarchical clustering of a square distance DataFrame (reference
-    drep/d_cluster.py:429-461)."""
-    names = list(db.columns)
-    arr = np.asarray(db)
-    try:
-        arr = ssd.squareform(arr)
-    except Exception:
-        logging.error("The database passed in is not symmetrical!")
-        logging.error(arr)
-        logging.error(names)
-        raise
-    linkage = scipy.cluster.hierarchy.linkage(arr, method=linkage_method)
-    fclust = scipy.cluster.hierarchy.fcluster(linkage, linkage_cutoff, criterion='distance')
-    Cdb = _gen_cdb_from_fclust(fclust, names)
-    return Cdb, linkage
-
-
-def _gen_cdb_from_fclust(fclust, names):
-    """fcluster labels -> Cdb [cluster, genome] (reference d_cluster.py:463-479)."""
-    Table = {'cluster': [], 'genome': []}
-    for i, c in enumerate(fclust):
-        Table['cluster'].append(c)
-        Table['genome'].append(names[i])
-    return pd.DataFrame(Table)
+def _primary_cdb(labels, names) -> pd.DataFrame:
+    """Cdb [primary_cluster, genome]: fcluster labels in the pivot's genome
+    order (what dRep's _gen_cdb_from_fclust + rename give,
+    d_cluster.py:463-479, 623)."""
+    return pd.DataFrame({'primary_cluster': np.asarray(labels), 'genome': list(names)})
 
 
 def cluster_mash_database(db, **kwargs):
     """
     From a Mash database, cluster and return Cdb (reference
-    drep/d_cluster.py:598-630).  Same in-place update of db['dist'] from
-    db['similarity'] as the reference; ``pivot`` is called with keywords
-    (pandas >= 2 rejects the reference's positional form).
+    drep/d_cluster.py:598-630, with its cluster_hierarchical 429-461).  Same
+    in-place update of db['dist'] from db['similarity'] as the reference, the
+    same pivot (with keywords: pandas >= 2 rejects the positional form) and
+    the same scipy calls on the pivot's squareform, so Cdb and linkage equal
+    the reference's.
 
     Keyword arguments:
         clusterAlg: how to cluster database (default = single)
@@ -466,15 +428,19 @@ def cluster_mash_database(db, **kwargs):
         list: [Cdb, [linkage, linkage_db, arguments]]
     """
     logging.debug('Clustering MASH database')
-    P_Lmethod = kwargs.get('clusterAlg', 'single')
-    P_Lcutoff = 1 - kwargs.get('P_ani', .9)
+    method = kwargs.get('clusterAlg', 'single')
+    cutoff = 1 - kwargs.get('P_ani', .9)
     db['dist'] = 1 - db['similarity']
     linkage_db = db.pivot(index="genome1", columns="genome2", values="dist")
-    Cdb, linkage = cluster_hierarchical(linkage_db, linkage_method=P_Lmethod,
-                                        linkage_cutoff=P_Lcutoff)
-    Cdb = Cdb.rename(columns={'cluster': 'primary_cluster'})
-    arguments = {'linkage_method': P_Lmethod, 'linkage_cutoff': P_Lcutoff,
-                 'comparison_algorithm': 'MASH'}
+    try:
+        y = ssd.squareform(np.asarray(linkage_db))       # raises unless symmetric with a zero diagonal
+    except ValueError:
+        logging.error("The database passed in is not symmetrical!")
+        raise
+    linkage = scipy.cluster.hierarchy.linkage(y, method=method)
+    labels = scipy.cluster.hierarchy.fcluster(linkage, cutoff, criterion='distance')
+    Cdb = _primary_cdb(labels, linkage_db.columns)
+    arguments = {'linkage_method': method, 'linkage_cutoff': cutoff, 'comparison_algorithm': 'MASH'}
     return Cdb, [linkage, linkage_db, arguments]
 
 
@@ -555,7 +521,7 @@ def cluster_mash_condensed(cm: CondensedMash, **kwargs):
         arr = condensed_cluster_distances(cm)
         linkage = scipy.cluster.hierarchy.linkage(arr, method=P_Lmethod)
     fclust = scipy.cluster.hierarchy.fcluster(linkage, P_Lcutoff, criterion='distance')
-    Cdb = _gen_cdb_from_fclust(fclust, names).rename(columns={'cluster': 'primary_cluster'})
+    Cdb = _primary_cdb(fclust, names)
     arguments = {'linkage_method': P_Lmethod, 'linkage_cutoff': P_Lcutoff,
                  'comparison_algorithm': 'MASH'}
     return Cdb, [linkage, None, arguments]

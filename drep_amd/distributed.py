@@ -127,7 +127,7 @@ def run_sharded(N: int, names: Sequence[str], s: int, sketch_fn: SketchFn, allpa
     import torch
     import torch.distributed as dist
     import scipy.cluster.hierarchy as sch
-    from .d_cluster import _gen_cdb_from_fclust
+    from .d_cluster import _primary_cdb
     world, rank = dist.get_world_size(), dist.get_rank()
     p = plan(N, world, rank)
     sync = sync or (lambda: None)
@@ -162,7 +162,7 @@ def run_sharded(N: int, names: Sequence[str], s: int, sketch_fn: SketchFn, allpa
         times["linkage_s"] = time.perf_counter() - t0
         cutoff = 1 - P_ani
         fcl = sch.fcluster(Z, cutoff, criterion="distance")
-        Cdb = _gen_cdb_from_fclust(fcl, sorted(names)).rename(columns={"cluster": "primary_cluster"})
+        Cdb = _primary_cdb(fcl, sorted(names))
         res.update(Cdb=Cdb, linkage=Z, common=full_c, denom=full_d, hashes=H, nhash=NH,
                    arguments={"linkage_method": method, "linkage_cutoff": cutoff, "comparison_algorithm": "MASH"})
     return res

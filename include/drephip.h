@@ -104,11 +104,21 @@ int drephip_sketch(drephip_ctx *ctx, const uint8_t *seq, const uint64_t *rec_off
                    const uint64_t *genome_rec_off, uint32_t n_genomes,
                    uint64_t *hashes_out, uint32_t *nhash_out, uint64_t *length_out);
 
-/* Same, reading FASTA files (host ingest on `threads` CPU threads, 0 = all;
- * batches are streamed through the device). */
+/* Same, reading FASTA files (kseq semantics, plain or gzip) on `threads` CPU
+ * threads (0 = all).  Files are read and packed in batches of ~1 Gbase into
+ * two pinned host buffers by a producer thread while the calling thread copies
+ * the previous batch to the device and sketches it (host ingest and GPU work
+ * overlap).  drephip_last_ingest_stats reports the split. */
 int drephip_sketch_files(drephip_ctx *ctx, const char *const *paths, uint32_t n_genomes,
                          int threads, uint64_t *hashes_out, uint32_t *nhash_out,
                          uint64_t *length_out);
+
+/* Timing of the last drephip_sketch_files call on this context (seconds):
+ * host read + pack summed over batches, device copy + sketch summed over
+ * batches, the whole call's wall time, and the number of batches.  With the
+ * overlap, wall ~ produce + the last batch's device work. */
+int drephip_last_ingest_stats(drephip_ctx *ctx, double *produce_s, double *gpu_s, double *wall_s,
+                              uint32_t *batches);
 
 /* Device-resident sketch: packed genome set already in HBM (see layout).
  * h_base_off/h_padded/h_nkmers are host arrays of n_genomes entries

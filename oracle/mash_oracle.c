@@ -190,45 +190,89 @@ static void scan_record(const uint8_t *seq, uint64_t len, int k, uint32_t seed,
 }
 
 /* ------------------------------------------------------------ FASTA input */
-/* kseq.h semantics as Mash uses it: '>' or '@' starts a record header; the
- * sequence is the concatenation of the following lines (line breaks dropped,
- * a trailing '\r' dropped) until the next line starting with '>' , '+' or '@'.
+/* kseq.h's kseq_read as Mash loops over it (`while ((l = kseq_read(seq)) >=
+ * 0)`), restated character by character (klib kseq.h, public domain):
+ *   - with no header character pending, skip ANY bytes up to the next '>' or
+ *     '@' (text before the first header; the bytes after a FASTQ record);
+ *   - the header line is the rest of that line;
+ *   - sequence: lines whose first byte is not '>', '+' or '@' (empty lines
+ *     skipped), each without its '\n' (and, as Mash's parse of CRLF files
+ *     behaves, without a line-final '\r'); a '>'/'@' line start ends the record
+ *     with the next header's first byte already read;
+ *   - '+' (FASTQ): the rest of that line is skipped, then whole quality lines
+ *     are read until the quality is at least as long as the sequence; a
+ *     quality of a different length, or none (EOF), makes kseq_read return -2:
+ *     that record is not kept and reading stops.
  * Returns a malloc'd buffer of the concatenated, upper-cased record sequences
  * and a malloc'd record-offset array (n_rec + 1 entries). gz or plain. */
+typedef struct { gzFile f; unsigned char buf[1 << 16]; int n, i; } kbuf;
+static int kgetc(kbuf *k) {
+    if (k->i == k->n) { k->n = gzread(k->f, k->buf, sizeof(k->buf)); k->i = 0; if (k->n <= 0) { k->n = 0; return -1; } }
+    return k->buf[k->i++];
+}
+/* one line (after its first byte c0, if c0 >= 0) up to '\n' or EOF: length
+ * without the '\n' and a final '\r'; *end = '\n' or -1 */
+static size_t kline_len(kbuf *k, int c0, int *end) {
+    size_t ll = 0; int c, lastc = -1;
+    if (c0 >= 0) { ll = 1; lastc = c0; }
+    while ((c = kgetc(k)) >= 0 && c != '\n') { ll++; lastc = c; }
+    if (lastc == '\r') ll--;
+    *end = c;
+    return ll;
+}
 int oracle_read_fasta(const char *path, uint8_t **seq_out, uint64_t **off_out,
                       uint32_t *nrec_out, uint64_t *len_out) {
-    gzFile f = gzopen(path, "rb");
-    if (!f) return -1;
+    kbuf *k = (kbuf *)malloc(sizeof(kbuf));
+    k->f = gzopen(path, "rb");
+    if (!k->f) { free(k); return -1; }
+    k->n = k->i = 0;
     size_t cap = 1 << 20, n = 0; uint8_t *seq = (uint8_t *)malloc(cap);
     size_t ocap = 64; uint32_t nrec = 0; uint64_t *off = (uint64_t *)malloc(ocap * 8);
-    char *line = (char *)malloc(1 << 16); size_t lcap = 1 << 16;
-    int in_rec = 0, in_qual = 0;
+    int last = 0, c = 0;
     for (;;) {
-        /* read one line of arbitrary length */
-        size_t ll = 0; int eof = 0;
-        for (;;) {
-            if (!gzgets(f, line + ll, (int)(lcap - ll))) { eof = (ll == 0); break; }
-            ll += strlen(line + ll);
-            if (ll > 0 && line[ll - 1] == '\n') break;
-            if (ll + 1 >= lcap) { lcap *= 2; line = (char *)realloc(line, lcap); }
+        if (!last) {                                   /* hunt for the next header */
+            while ((c = kgetc(k)) >= 0 && c != '>' && c != '@') {}
+            if (c < 0) break;
         }
-        if (eof) break;
-        if (ll > 0 && line[ll - 1] == '\n') line[--ll] = 0;
-        if (ll > 0 && line[ll - 1] == '\r') line[--ll] = 0;
-        if (ll > 0 && (line[0] == '>' || line[0] == '@')) {
-            if (nrec + 2 > ocap) { ocap *= 2; off = (uint64_t *)realloc(off, ocap * 8); }
-            off[nrec++] = n; in_rec = 1; in_qual = 0; continue;
+        last = 0;
+        c = kgetc(k);                                  /* header line */
+        if (c < 0) break;                              /* '>' as the last byte: kseq_read returns -1 */
+        while (c >= 0 && c != '\n') c = kgetc(k);
+        const size_t start = n;
+        if (c >= 0) {
+            while ((c = kgetc(k)) >= 0 && c != '>' && c != '+' && c != '@') {
+                if (c == '\n') continue;
+                const size_t line0 = n;
+                do {
+                    if (n + 1 > cap) { cap *= 2; seq = (uint8_t *)realloc(seq, cap); }
+                    seq[n++] = (uint8_t)((c > 96 && c < 123) ? c - 32 : c);
+                } while ((c = kgetc(k)) >= 0 && c != '\n');
+                if (n > line0 && seq[n - 1] == '\r') n--;
+                if (c < 0) break;
+            }
         }
-        if (ll > 0 && line[0] == '+') { in_qual = 1; continue; }
-        if (!in_rec || in_qual) continue;
-        if (n + ll > cap) { while (n + ll > cap) cap *= 2; seq = (uint8_t *)realloc(seq, cap); }
-        for (size_t i = 0; i < ll; i++) {
-            uint8_t c = (uint8_t)line[i];
-            if (c > 96 && c < 123) c -= 32;
-            seq[n++] = c;
+        if (c == '>' || c == '@') last = c;            /* the next header's first byte is read */
+        if (c == '+') {                                  /* FASTQ: skip the '+' line, then quality lines */
+            int e;
+            (void)kline_len(k, -1, &e);
+            int bad = e < 0;                             /* no quality string */
+            size_t q = 0;
+            if (!bad) {
+                for (;;) {
+                    const int c0 = kgetc(k);
+                    if (c0 < 0) break;                   /* EOF: no further line */
+                    q += c0 == '\n' ? 0 : kline_len(k, c0, &e);
+                    if (q >= n - start || (c0 != '\n' && e < 0)) break;
+                }
+                bad = q != n - start;                    /* quality of a different length */
+            }
+            if (bad) { n = start; break; }               /* kseq_read returns -2: record dropped, reading stops */
         }
+        if (nrec + 2 > ocap) { ocap *= 2; off = (uint64_t *)realloc(off, ocap * 8); }
+        off[nrec++] = start;
+        if (c < 0 && !last) break;
     }
-    gzclose(f); free(line);
+    gzclose(k->f); free(k);
     off[nrec] = n;
     *seq_out = seq; *off_out = off; *nrec_out = nrec; *len_out = n;
     return 0;

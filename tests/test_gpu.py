@@ -35,6 +35,36 @@ def test_sketch_reference_genomes_bitexact(golden, ctx1000):
         assert int(ln[i]) == ref.length
 
 
+def test_sketch_files_many_batches(golden, tmp_path, monkeypatch):
+    """The overlapped ingest pipeline (producer thread + two pinned buffers) with
+    a batch size forced down to ~1 genome: 12 files (the 4 reference genomes,
+    plain and gzip, repeated) in many batches give the reference's sketches in
+    order, and the ingest stats add up."""
+    import gzip
+    fas = sorted(glob.glob(os.path.join(golden, "genomes", "*.gz")))
+    files = []
+    for rep in range(3):
+        for fa in fas:
+            if rep == 1:
+                files.append(fa)                                  # gzip
+            else:
+                p = tmp_path / ("r%d_" % rep + os.path.basename(fa)[:-3])
+                p.write_bytes(gzip.open(fa).read())
+                files.append(str(p))
+    monkeypatch.setenv("DREPHIP_INGEST_BATCH_BASES", "3000000")
+    with _lib.Context(0, 21, S, 42) as ctx:
+        h, nh, ln = ctx.sketch_files(files, threads=3)
+        st = ctx.ingest_stats()
+    assert st["batches"] >= 4          # 3 files (~10 Mbp) per batch
+    assert st["wall_s"] >= max(st["produce_s"], st["gpu_s"]) * 0.5
+    for i, f in enumerate(files):
+        ref = read_msh(os.path.join(golden, "MASH_files", "sketches",
+                                    os.path.basename(f).split("_", 1)[-1].replace(".gz", "") + ".msh")).references[0] \
+            if not f.endswith(".gz") else \
+            read_msh(os.path.join(golden, "MASH_files", "sketches", os.path.basename(f)[:-3] + ".msh")).references[0]
+        assert nh[i] == S and np.array_equal(h[i], ref.hashes) and int(ln[i]) == ref.length, f
+
+
 def _records_case(rng, kind):
     A = np.frombuffer(b"ACGT", dtype=np.uint8)
     if kind == "nruns_lower_multirecord":
@@ -579,6 +609,56 @@ def test_all_vs_all_MASH_dropin_reproduces_reference(golden, tmp_path, gpus):
         link = json.load(open(os.path.join(golden, "ref", "linkage_%s.json" % alg)))
         got = [[float(v).hex() for v in row] for row in ret[0]]
         assert got == link["linkage"]
+
+
+def _dropin_bdb(golden, tmp_path):
+    import gzip
+    fas = sorted(glob.glob(os.path.join(golden, "genomes", "*.gz")))
+    gdir = tmp_path / "genomes"
+    gdir.mkdir(exist_ok=True)
+    locs = []
+    for fa in fas:
+        dst = gdir / os.path.basename(fa)[:-3]
+        dst.write_bytes(gzip.open(fa).read())
+        locs.append(str(dst))
+    locs.append(str(gdir / "Escherichia_coli_Sakai.fna"))     # FASTA absent: its cached sketch is used
+    return pd.DataFrame({"genome": [os.path.basename(x) for x in locs], "location": locs})
+
+
+def test_all_vs_all_MASH_groupsize_and_no_kwargs_call(golden, tmp_path):
+    """The reference's own checks of the boundary (tests/test_suite.py:635-666):
+    25 rows, 0.01 < dist(YI6-1, TX0104) < 0.02, one chunk dir with 6 files by
+    default and, with groupSize=2, 3 chunk dirs with 8 files; plus the
+    no-kwargs call shape of compare_winners (drep/d_evaluate.py:67), which
+    reuses the cached sketches and must return the same Mdb."""
+    from drep_amd import d_cluster
+    Bdb = _dropin_bdb(golden, tmp_path)
+    sakai = os.path.join(golden, "MASH_files", "sketches", "Escherichia_coli_Sakai.fna.msh")
+
+    def check(Mdb):
+        assert len(Mdb) == 25
+        db = Mdb[(Mdb['genome1'] == 'Enterococcus_faecalis_YI6-1.fna') &
+                 (Mdb['genome2'] == 'Enterococcus_faecalis_TX0104.fa')]
+        d = float(db['dist'].tolist()[0])
+        assert 0.01 < d < 0.02
+
+    wd = tmp_path / "wd_groups"
+    (wd / "MASH_files" / "sketches" / "chunk_2").mkdir(parents=True)
+    shutil.copy(sakai, wd / "MASH_files" / "sketches" / "chunk_2" / "Escherichia_coli_Sakai.fna.msh")
+    Mdb2 = d_cluster.all_vs_all_MASH(Bdb, str(wd), groupSize=2)
+    check(Mdb2)
+    assert len(glob.glob(str(wd / "MASH_files" / "sketches" / "*"))) == 3
+    assert len(glob.glob(str(wd / "MASH_files" / "sketches" / "*" / "*"))) == 8
+
+    wd = tmp_path / "wd_default"
+    (wd / "MASH_files" / "sketches" / "chunk_0").mkdir(parents=True)
+    shutil.copy(sakai, wd / "MASH_files" / "sketches" / "chunk_0" / "Escherichia_coli_Sakai.fna.msh")
+    Mdb1 = d_cluster.all_vs_all_MASH(Bdb, str(wd), MASH_sketch="1000", processors=2)     # CLI passes a str
+    check(Mdb1)
+    assert len(glob.glob(str(wd / "MASH_files" / "sketches" / "*"))) == 1
+    assert len(glob.glob(str(wd / "MASH_files" / "sketches" / "*" / "*"))) == 6
+    again = d_cluster.all_vs_all_MASH(Bdb, str(wd))          # compare_winners' call: no kwargs, cached sketches
+    assert again.equals(Mdb1) and Mdb2.equals(Mdb1)
 
 
 def test_errors_are_reported_not_hidden(ctx1000, tmp_path):

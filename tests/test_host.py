@@ -178,19 +178,6 @@ def test_dry_run_parses_existing_table(golden, tmp_path):
     assert list(Mdb["dist"].to_numpy().view(np.uint32)) == meta["dist_bits"]
 
 
-def test_load_genomes(tmp_path):
-    a = tmp_path / "a.fa"
-    b = tmp_path / "b.fna"
-    a.write_text(">x\nACGT\n")
-    b.write_text(">y\nACGT\n")
-    Bdb = d_cluster.load_genomes([str(a), str(b)])
-    assert list(Bdb["genome"]) == ["a.fa", "b.fna"]
-    lst = tmp_path / "list.txt"
-    lst.write_text("%s\n%s\n" % (a, b))
-    Bdb2 = d_cluster.load_genomes([str(lst)])
-    assert list(Bdb2["location"]) == [str(a), str(b)]
-
-
 def _np_pack(recs, tile):
     """numpy restatement of the packed layout (include/drephip.h) for one genome."""
     span = sum(len(r) for r in recs) + max(len(recs) - 1, 0)
@@ -270,8 +257,17 @@ def _messy_fasta(rng, n_rec, big):
             out.append(line + (b"\r\n" if rng.random() < 0.2 else b"\n"))
             if rng.random() < 0.02:
                 out.append(b"\n")
-        if fastq:
-            out.append(b"+\n" + b"I" * len(b"".join(kept)) + b"\n")
+        if fastq:                     # quality lines may start with '@', '>' or '+' (kseq counts them)
+            Q = np.frombuffer(b"@>+!#I5?", dtype=np.uint8)
+            q = Q[rng.integers(0, len(Q), len(b"".join(kept)))].tobytes()
+            out.append(b"+rec%d\n" % r)
+            i = 0
+            while True:
+                w = int(rng.integers(1, 120))
+                out.append(q[i:i + w] + b"\n")
+                i += w
+                if i >= len(q):
+                    break
         recs.append(np.frombuffer(b"".join(kept), dtype=np.uint8))
     return b"".join(out), recs
 
@@ -357,3 +353,61 @@ def test_condensed_store_roundtrip(tmp_path, partial):
     pl = load_primary_linkage(str(tmp_path))
     assert np.array_equal(pl["linkage"], Z) and pl["db"] is None and pl["arguments"] == args
     assert set(pl) == {"linkage", "db", "arguments"}          # WorkDirectory.import_clusters keys
+
+
+KSEQ_CASES = {
+    # text before the first header, a '>' in the middle of it starts a record
+    "hunt_midline": b"junk >hdr one\nACGT\nacgtN\n>two\nGGGG\n",
+    # FASTQ quality lines starting with '@', '>' and '+' are quality, not headers
+    "fastq_quality_lookalikes": b"@r1\nACGTACGT\n+\n@>+!\n@@II\n@r2 x\nTTTT\n+r2\n>>>>\n",
+    # quality longer than the sequence: kseq_read returns -2, the record and the rest are dropped
+    "fastq_long_quality": b"@a\nACGT\n+\nIIII\n@b\nCCCC\n+\nIIIIII\n@c\nGGGG\n+\nIIII\n",
+    # quality cut short by EOF: that record is dropped
+    "fastq_short_quality": b">f\nAAAACCCC\n@q\nACGTACGT\n+\nIII\n",
+    # '+' line and then EOF: no quality, dropped
+    "fastq_plus_eof": b">f\nAAAA\n@q\nACGT\n+",
+    # '>' as the very last byte: no record
+    "gt_last_byte": b">f\nACGT\n>",
+    # header without newline at EOF: an empty record
+    "header_eof": b">f\nACGT\n>g",
+    # empty FASTQ record, nothing after its '+' line
+    "fastq_empty_record": b">f\nACGT\n@e\n+\n",
+    # after a FASTQ record anything up to the next '>'/'@' is skipped, mid-line too
+    "after_fastq_hunt": b"@a\nAC\n+\nII\nnoise x@b\nGGTT\n",
+    # CRLF everywhere, blank lines, a line of only '\r'
+    "crlf": b">a\r\nACG\r\n\r\nTTA\r\n\n@b\r\nAC\r\n+\r\nII\r\n",
+}
+
+
+@pytest.mark.parametrize("case", sorted(KSEQ_CASES))
+def test_fasta_reader_kseq_corner_cases_vs_oracle(tmp_path, case):
+    """The SIMD reader (drephip_fasta_info / _pack) and the oracle's byte-level
+    restatement of kseq_read agree on kseq's corner cases: header hunting
+    anywhere, FASTQ quality lines that look like headers, quality-length
+    errors that end the file, EOF inside headers and quality."""
+    import ctypes as C
+    import gzip
+    tile = _lib.tile_bases()
+    L = _lib.lib()
+    for name, data in (("k.fq", KSEQ_CASES[case]), ("k.fq.gz", gzip.compress(KSEQ_CASES[case]))):
+        path = tmp_path / name
+        path.write_bytes(data)
+        seq, off, ln = oracle.read_fasta(str(path))
+        recs = [seq[off[i]:off[i + 1]] for i in range(len(off) - 1)]
+        info = _lib.fasta_info(str(path))
+        assert info["n_records"] == len(recs), (case, name, info, [bytes(r) for r in recs])
+        assert info["length"] == ln
+        P, want_c, want_v = _np_pack(recs, tile)
+        codes = np.zeros((tile + P) // 16, np.uint32)
+        valid = np.zeros((tile + P) // 32, np.uint32)
+        length = C.c_uint64(0)
+        nk = C.c_uint64(0)
+        assert L.drephip_fasta_pack(str(path).encode(), 21, codes, valid, tile, tile + P, C.byref(length),
+                                    C.byref(nk)) == 0
+        assert np.array_equal(codes[tile // 16:], want_c) and np.array_equal(valid[tile // 32:], want_v), case
+    expect = {"hunt_midline": [b"ACGTACGTN", b"GGGG"], "fastq_quality_lookalikes": [b"ACGTACGT", b"TTTT"],
+              "fastq_long_quality": [b"ACGT"], "fastq_short_quality": [b"AAAACCCC"],
+              "fastq_plus_eof": [b"AAAA"], "gt_last_byte": [b"ACGT"], "header_eof": [b"ACGT", b""],
+              "fastq_empty_record": [b"ACGT", b""], "after_fastq_hunt": [b"AC", b"GGTT"],
+              "crlf": [b"ACGTTA", b"AC"]}[case]
+    assert [bytes(r) for r in recs] == expect

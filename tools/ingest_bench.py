@@ -1,34 +1,61 @@
-"""FASTA ingest + sketch throughput of drephip_sketch_files (host parse/pack
-with `threads` threads, H2D, GPU sketch, D2H) on synthetic 5 Mbp genomes
-written to a temp dir, plain and gzip.  Not part of the product."""
-import gzip, json, os, sys, tempfile, time
-import numpy as np
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from drep_amd import _lib
+"""FASTA ingest + sketch of drephip_sketch_files, and the whole drop-in
+all_vs_all_MASH, on the reference's test genomes replicated into many files
+(plain and gzip).  Reports the host ingest time (read + pack, producer
+thread) next to the device time and the wall time of the overlapped pipeline.
+Not part of the product.
 
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 64
-L = 5_000_000
-threads = int(os.environ.get("INGEST_THREADS", 16))
-rng = np.random.default_rng(0)
-base = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, L)]
-out = {"genomes": n, "genome_bp": L, "threads": threads}
+usage: python tools/ingest_bench.py [copies_per_genome] > profiles/<round>_ingest.json
+"""
+import glob
+import gzip
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+
+import pandas as pd
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from drep_amd import _lib, d_cluster  # noqa: E402
+
+copies = int(sys.argv[1]) if len(sys.argv) > 1 else 125
+threads = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+src = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "genomes", "*.gz")))
+out = {"source": "tests/golden/genomes (4 reference FASTAs) x %d copies each" % copies, "threads": threads}
 with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
     plain, gz = [], []
-    for g in range(n):
-        seq = base.copy()
-        m = rng.random(L) < 0.01
-        seq[m] = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, int(m.sum()))]
-        lines = b"\n".join(seq[i:i + 80].tobytes() for i in range(0, L, 80))
-        txt = b">g%d synthetic\n" % g + lines + b"\n"
-        p = os.path.join(td, "g%04d.fna" % g); open(p, "wb").write(txt); plain.append(p)
-        if g < n // 4:
-            q = p + ".gz"; open(q, "wb").write(gzip.compress(txt, 1)); gz.append(q)
+    for i, f in enumerate(src):
+        txt = gzip.open(f).read()
+        for c in range(copies):
+            p = os.path.join(td, "c%04d_%s" % (c, os.path.basename(f)[:-3]))
+            open(p, "wb").write(txt)
+            plain.append(p)
+        q = os.path.join(td, "z_" + os.path.basename(f))
+        shutil.copy(f, q)
+        gz.extend([q] * max(1, copies // 4))
+    out["files_plain"] = len(plain)
+    out["fasta_bytes"] = sum(os.path.getsize(p) for p in plain)
     with _lib.Context(0, 21, 1000, 42) as ctx:
         ctx.sketch_files(plain[:2], threads=threads)                       # warm-up
         for name, files in (("plain", plain), ("gzip", gz)):
             t0 = time.perf_counter()
             h, nh, ln = ctx.sketch_files(files, threads=threads)
             dt = time.perf_counter() - t0
-            out[name] = {"files": len(files), "s": dt, "Mbp_per_s": len(files) * L / dt / 1e6,
-                         "genomes_per_s": len(files) / dt}
-print(json.dumps(out))
+            st = ctx.ingest_stats()
+            bases = int(ln.sum())
+            out[name] = {"files": len(files), "bases": bases, "wall_s": dt, "Mbp_per_s": bases / dt / 1e6,
+                         "host_read_pack_s": st["produce_s"], "device_s": st["gpu_s"], "batches": st["batches"],
+                         "ingest_only_Mbp_per_s": bases / st["produce_s"] / 1e6,
+                         "overlap_note": "wall ~ host read+pack of every batch + the last batch's device work "
+                                         "(the other batches' device work runs behind the next batch's ingest)"}
+    # the whole drop-in on the plain files: sketch (ingest overlapped) + all-pairs + Mdb
+    Bdb = pd.DataFrame({"genome": [os.path.basename(p) for p in plain], "location": plain})
+    wd = os.path.join(td, "wd")
+    t0 = time.perf_counter()
+    Mdb = d_cluster.all_vs_all_MASH(Bdb, wd, processors=threads)
+    out["dropin_all_vs_all_MASH"] = {"genomes": len(plain), "wall_s": time.perf_counter() - t0, "mdb_rows": len(Mdb),
+                                     "note": "sketch files (+ .msh writing) + HIP all-pairs + float32 Mdb build"}
+print(json.dumps(out, indent=1))
