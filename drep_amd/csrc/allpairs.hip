@@ -42,6 +42,8 @@ constexpr int kApWG = 1024;                     // 16 waves per workgroup
 constexpr uint32_t kApCols = 128;               // columns per work item (fewer when the grid would not fill the chip)
 constexpr uint32_t kApMinCols = 16;             // one column per wave
 constexpr uint32_t kMaxFam = 6;                 // cuckoo field families tried per table
+constexpr uint32_t kFamTwins = 0x40;            // k_build_q32 family byte: the row has two keys with one low word
+constexpr uint32_t kFamFailed = 0xFF;           // ... no family worked (the row's pairs are merged literally)
 constexpr uint32_t kLdsBudget = 156 * 1024;     // dynamic LDS per workgroup
 constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;      // empty slot word
 
@@ -69,9 +71,13 @@ __host__ __device__ __forceinline__ uint32_t rotr32(uint32_t x, uint32_t r) {
     return r ? (x >> r) | (x << (32 - r)) : x;
 }
 __host__ __device__ __forceinline__ QFields qfields(uint32_t fam) {
-    // disjoint fields inside the low word for B <= 12 (o + B <= 32)
-    const uint32_t o1[6] = {0, 16, 2, 18, 4, 20};
-    const uint32_t o2[6] = {16, 0, 18, 2, 20, 4};
+    // disjoint fields inside the low word for B <= 12 (o + B <= 32).  Family 0
+    // (used for nearly every row) takes bits [4, 4+B) and [20, 20+B): with R =
+    // 4 interleaved rows a slot is 16 bytes, so the field AS IT STANDS in the
+    // key is already the slot's byte address (blo & (hm << 4)) -- one VALU op
+    // per choice instead of extract + scale
+    const uint32_t o1[6] = {4, 20, 0, 16, 2, 18};
+    const uint32_t o2[6] = {20, 4, 16, 0, 18, 2};
     return {o1[fam], o2[fam]};
 }
 
@@ -116,7 +122,7 @@ __global__ __launch_bounds__(1024) void k_build_q32(const uint64_t *__restrict__
                                                    uint32_t *__restrict__ blk, uint32_t stride,
                                                    uint8_t *__restrict__ fam_out) {
     extern __shared__ uint32_t Tb[];
-    __shared__ int fail;
+    __shared__ int fail, twins;
     const uint32_t H = 1u << B, hm = H - 1;
     const uint32_t r = blockIdx.x;
     const uint32_t g = row0 + r;
@@ -134,7 +140,7 @@ __global__ __launch_bounds__(1024) void k_build_q32(const uint64_t *__restrict__
     for (uint32_t fam = 0; fam < kMaxFam; fam++) {
         const QFields q = qfields(fam);
         for (uint32_t i = threadIdx.x; i < 2 * H; i += blockDim.x) Tb[i] = kEmpty32;
-        if (threadIdx.x == 0) fail = 0;
+        if (threadIdx.x == 0) { fail = 0; twins = 0; }
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
             if (!cuckoo_insert32(Tb, 1, 0, H, hm, q, (uint32_t)A[i], i)) fail = 1;
@@ -143,13 +149,29 @@ __global__ __launch_bounds__(1024) void k_build_q32(const uint64_t *__restrict__
             if (!cuckoo_has32(Tb, 1, 0, H, hm, q, (uint32_t)A[i], i)) fail = 1;
         __syncthreads();
         if (!fail) {
+            // twins: two keys with one low word occupy both of their shared
+            // slots, so a lookup matches both and must check the second too --
+            // only the generic probe does (kFamTwins keeps this row off FAST).
+            // The empty word can also "match" (a low word whose rotated
+            // quotient is all ones), but never hides a key: a key sits in its
+            // second slot only after an exchange filled its first, and slots
+            // are never emptied, so the fast probe's "first slot if it
+            // matches" is exact on a row without twins.
+            for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+                const uint32_t x = (uint32_t)A[i];
+                const uint32_t e1 = Tb[(x >> q.o1) & hm], e2 = Tb[H + ((x >> q.o2) & hm)];
+                if (e1 != kEmpty32 && e2 != kEmpty32 && (e1 ^ rotr32(x, q.o1)) <= hm &&
+                    (e2 ^ rotr32(x, q.o2)) <= hm)
+                    twins = 1;
+            }
+            __syncthreads();
             for (uint32_t i = threadIdx.x; i < 2 * H; i += blockDim.x) img[i * R + rr] = Tb[i];
-            if (threadIdx.x == 0) fam_out[r] = (uint8_t)fam;
+            if (threadIdx.x == 0) fam_out[r] = (uint8_t)(fam | (twins ? kFamTwins : 0u));
             return;
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) fam_out[r] = 0xFF;          // k_allpairs_q merges this row's pairs literally
+    if (threadIdx.x == 0) fam_out[r] = kFamFailed;    // k_allpairs_q merges this row's pairs literally
 }
 
 // ------------------------------------------------------- literal merge
@@ -183,14 +205,33 @@ __device__ __forceinline__ void merge_pair(const uint64_t *__restrict__ a, uint3
 template <int R>
 struct Slots { uint32_t e1[R], e2[R]; };
 
-template <int R, bool FAST>
+template <int R, bool FAST, int KB, bool ABS = false>
 __device__ __forceinline__ Slots<R> read_slots(uint32_t blo, const uint32_t *T, uint32_t H, uint32_t hm,
                                                const uint32_t (&o1)[R], const uint32_t (&o2)[R]) {
     Slots<R> sl;
     if (FAST) {
-        const uint32_t *p1 = T + (blo & hm) * R;
-        const uint32_t *p2 = T + (H + ((blo >> 16) & hm)) * R;
-        if constexpr (R >= 4) {
+        // family 0: fields at bits 4 and 20; a slot of R rows is 4R bytes, so
+        // its byte offset is the field (x 16) scaled by R/4.  KB = log2 H when
+        // known at compile time puts the second region's start in the
+        // instruction's offset field.
+        const uint32_t f1 = blo & (hm << 4), f2 = (blo >> 16) & (hm << 4);
+        const uint32_t a1 = R >= 4 ? f1 * (R / 4) : f1 / (4 / R);
+        const uint32_t a2 = R >= 4 ? f2 * (R / 4) : f2 / (4 / R);
+        const char *Tb = (const char *)T;
+        const char *T2 = KB ? Tb + (4u << KB) * R : Tb + H * 4 * R;
+        const uint32_t *p1 = (const uint32_t *)(Tb + a1);
+        const uint32_t *p2 = (const uint32_t *)(T2 + a2);
+        if constexpr (ABS && R == 4 && KB > 0) {
+            // the tables start the kernel's LDS (k_allpairs_q declares no
+            // static LDS: T == lds == LDS address 0): address the slots
+            // absolutely, without an add of the (link-time) base per read
+            typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+            typedef __attribute__((address_space(3))) const v4u lds_v4u;
+            const v4u v1 = *(lds_v4u *)(size_t)a1;
+            const v4u v2 = *(lds_v4u *)(size_t)(a2 + (4u << KB) * R);
+            sl.e1[0] = v1[0]; sl.e1[1] = v1[1]; sl.e1[2] = v1[2]; sl.e1[3] = v1[3];
+            sl.e2[0] = v2[0]; sl.e2[1] = v2[1]; sl.e2[2] = v2[2]; sl.e2[3] = v2[3];
+        } else if constexpr (R >= 4) {
 #pragma unroll
             for (int r = 0; r < R; r += 4) {
                 const uint4 v1 = *(const uint4 *)(p1 + r);
@@ -223,31 +264,50 @@ __device__ __forceinline__ Slots<R> read_slots(uint32_t blo, const uint32_t *T, 
 // with scalar popcounts -- counts stay in SGPRs, no per-lane reduction.
 // i = ibase[r] + field, valid below ilim[r].  lanemask drops lanes (band
 // kernel: outside the band).
-template <int R, bool FAST>
+template <int R, bool FAST, bool RETRY = true>
 __device__ __forceinline__ void probe_rows(const Slots<R> &sl, uint64_t b, uint32_t j, const uint32_t *V,
                                            uint32_t vs, uint32_t hm, const uint32_t (&o1)[R],
                                            const uint32_t (&o2)[R], uint32_t actmask, uint64_t lanemask,
                                            const uint32_t (&ibase)[R], const uint32_t (&ilim)[R], uint32_t s,
                                            uint32_t (&mrun)[R], uint32_t (&cnt)[R]) {
     const uint32_t blo = (uint32_t)b, bhi = (uint32_t)(b >> 32);
-    const uint32_t b16 = rotr32(blo, 16);                            // family 0's second field
+    const uint32_t b4 = rotr32(blo, 4), b20 = rotr32(blo, 20);      // family 0's fields, rotated to bit 0
+    uint32_t xs1[R], xs2[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        xs1[r] = sl.e1[r] ^ (FAST ? b4 : rotr32(blo, o1[r]));
+        xs2[r] = sl.e2[r] ^ (FAST ? b20 : rotr32(blo, o2[r]));
+    }
+    {
+        // one test for all rows first (a min3 chain, one compare, one ballot,
+        // one branch): most chunks hit no row.  Inactive rows take part; they
+        // can only send a chunk to the per-row tests, which skip them.
+        uint32_t mn = min(xs1[0], xs2[0]);
+#pragma unroll
+        for (int r = 1; r < R; r++) mn = min(mn, min(xs1[r], xs2[r]));
+        if ((__builtin_amdgcn_ballot_w64(mn <= hm) & lanemask) == 0) return;
+    }
 #pragma unroll
     for (int r = 0; r < R; r++) {
         if (!((actmask >> r) & 1u)) continue;                        // wave-uniform
-        const uint32_t x1 = sl.e1[r] ^ (FAST ? blo : rotr32(blo, o1[r]));
-        const uint32_t x2 = sl.e2[r] ^ (FAST ? b16 : rotr32(blo, o2[r]));
+        const uint32_t x1 = xs1[r], x2 = xs2[r];
         // one compare, one mask: a hit in either slot <=> min(x1, x2) <= hm
         uint64_t m = __builtin_amdgcn_ballot_w64(min(x1, x2) <= hm) & lanemask;
         if (m == 0) continue;                                        // wave-uniform: no hit in this row
-        const bool c1 = x1 <= hm, c2 = x2 <= hm;
+        const bool c1 = x1 <= hm;
         uint32_t f = (c1 ? sl.e1[r] : sl.e2[r]) & hm;
         bool ok = f < ilim[r] && V[r * vs + (f < ilim[r] ? f : 0)] == bhi;
-        const bool retry = c1 && c2 && !ok;                          // two keys share this low word
-        if (__builtin_amdgcn_ballot_w64(retry) != 0) {
-            const uint32_t f2 = sl.e2[r] & hm;
-            const bool ok2 = retry && f2 < ilim[r] && V[r * vs + (f2 < ilim[r] ? f2 : 0)] == bhi;
-            f = ok2 ? f2 : f;
-            ok = ok || ok2;
+        if constexpr (RETRY) {
+            // both slots match when two of the row's keys share this low word
+            // (RETRY = false: k_build_q32 found no such pair in any row), or
+            // when the first is an empty word's false match (see k_build_q32)
+            const bool retry = c1 && x2 <= hm && !ok;
+            if (__builtin_amdgcn_ballot_w64(retry) != 0) {
+                const uint32_t f2 = sl.e2[r] & hm;
+                const bool ok2 = retry && f2 < ilim[r] && V[r * vs + (f2 < ilim[r] ? f2 : 0)] == bhi;
+                f = ok2 ? f2 : f;
+                ok = ok || ok2;
+            }
         }
         m &= __builtin_amdgcn_ballot_w64(ok);
         const uint32_t lim = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
@@ -265,8 +325,27 @@ __device__ __forceinline__ void probe_rows(const Slots<R> &sl, uint64_t b, uint3
 // two workgroups fit a CU.  Slot words are read one chunk ahead of the tests.
 // Counts go straight to the condensed output (lane 0).
 constexpr int kRing = 4;
+// chunks between a slot read and its use: 1 (2 and 3 measured 1-2 % and 8 %
+// slower -- a slot read that far ahead waits on a ring load only 2-1 chunks old)
+constexpr int kSlotAhead = 1;
+static_assert(kSlotAhead >= 1 && kSlotAhead < kRing, "slot prefetch distance");
 
-template <int R, int NCH, bool FAST>
+// Column element loads are raw buffer loads against a per-column resource
+// (base = the column's sketch, num_records = s * 8): the lane's byte offset is
+// a fixed VGPR, the chunk's offset an SGPR, so a ring refill costs no VALU
+// instruction, and lanes past s read 0 without a clamp (they are masked by
+// the tail mask where the chunk is used).
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+constexpr int kBufferRsrcWord3 = 0x00020000;      // gfx9 raw-buffer descriptor dword 3 (CK's value for gfx9)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t column_rsrc(const uint64_t *col, uint32_t s) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)col, (short)0, (int)(s * 8u), kBufferRsrcWord3);
+}
+__device__ __forceinline__ uint64_t ld_chunk(__amdgpu_buffer_rsrc_t rs, uint32_t lane_off, uint32_t chunk) {
+    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, lane_off, rfl(chunk) * 512u, 0);
+    return ((uint64_t)v[1] << 32) | v[0];
+}
+
+template <int R, int NCH, bool FAST, int KB>
 __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ nhash,
                                            const uint32_t *T, const uint32_t *V, uint32_t H, uint32_t hm, uint32_t s,
                                            uint32_t N, uint32_t i0, uint32_t nrows, uint32_t cend, uint32_t c_first,
@@ -275,10 +354,8 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
                                            bool any_partial_row, uint16_t *__restrict__ common,
                                            uint16_t *__restrict__ denom, uint64_t seg0) {
     const uint32_t lane = threadIdx.x & 63;
+    const uint32_t lane_off = lane * 8u;
     const uint32_t nch = (s + 63) / 64;
-    // clamped raw load: no select, so the ring refill never waits on its own
-    // load; lanes past s in the last chunk are masked where the chunk is used
-    auto ld = [&](const uint64_t *Bc, int k) -> uint64_t { return Bc[min(k * 64 + lane, s - 1)]; };
     const uint32_t tail = s - (nch - 1) * 64;                        // valid lanes of the last chunk
     const uint64_t tailmask = tail >= 64 ? ~0ull : (1ull << tail) - 1;
     uint64_t rg[kRing], nx[kRing];
@@ -287,17 +364,19 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
     for (int r = 0; r < R; r++) zero[r] = 0;
     uint32_t c = rfl(c_first);                                       // wave-uniform: scalar column loop
     if (c < cend) {
+        const __amdgpu_buffer_rsrc_t rn = column_rsrc(hashes + (uint64_t)c * s, s);
 #pragma unroll
-        for (int k = 0; k < kRing; k++) nx[k] = ld(hashes + (uint64_t)c * s, k);
+        for (int k = 0; k < kRing; k++) nx[k] = ld_chunk(rn, lane_off, min((uint32_t)k, nch - 1));
     }
     for (; c < cend; c += c_step) {
-        const uint64_t *Bc = hashes + (uint64_t)c * s;
+        const __amdgpu_buffer_rsrc_t rc = column_rsrc(hashes + (uint64_t)c * s, s);
 #pragma unroll
         for (int k = 0; k < kRing; k++) rg[k] = nx[k];
         const uint32_t cn = c + c_step;
         if (cn < cend) {
+            const __amdgpu_buffer_rsrc_t rn = column_rsrc(hashes + (uint64_t)cn * s, s);
 #pragma unroll
-            for (int k = 0; k < kRing; k++) nx[k] = ld(hashes + (uint64_t)cn * s, k);
+            for (int k = 0; k < kRing; k++) nx[k] = ld_chunk(rn, lane_off, min((uint32_t)k, nch - 1));
         }
         uint32_t cnt[R], mrun[R], actmask = 0;
         // elements past every active row's largest hash cannot match: the
@@ -311,10 +390,13 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
             if (act) amax = alast[r] > amax ? alast[r] : amax;
         }
         if (!actmask) continue;                                       // column at or left of the tile's rows
-        // slot words of chunk k live in sb[k & 1] (kRing is even): read one
-        // chunk ahead into the other half, no register copies
-        Slots<R> sb[2];
-        sb[0] = read_slots<R, FAST>((uint32_t)rg[0], T, H, hm, o1, o2);
+        // slot words of chunk k live in sb[k % kRing]: read kSlotAhead chunks
+        // ahead (the LDS reads are bank-conflicted random 16-byte reads, ~3x
+        // their conflict-free cycles; one chunk of work did not cover them)
+        Slots<R> sb[kRing];
+#pragma unroll
+        for (int u = 0; u < kSlotAhead; u++)
+            sb[u] = read_slots<R, FAST, KB, true>((uint32_t)rg[u], T, H, hm, o1, o2);
         // runtime loop over groups of kRing chunks; ring slots are static.  The
         // scan-end test runs once per group, on the group's first chunk (a
         // chunk past every row's largest hash cannot hit, so finishing the
@@ -330,17 +412,26 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
 #pragma unroll
             for (int u = 0; u < kRing; u++) {
                 const uint32_t k = kb + u;
-                if (k >= nch) continue;                                   // wave-uniform
                 const uint64_t b = rg[u];
-                // lanes past s in the last chunk hold clamped copies: masked out
+                // lanes past s in the last chunk read 0 (buffer bounds): masked out
                 const uint64_t lm = k == nch - 1 ? tailmask : ~0ull;
+                // chunk k + kSlotAhead: in rg[(u + kSlotAhead) % kRing] (refilled
+                // earlier in this group when that index is below u)
+                sb[(u + kSlotAhead) % kRing] =
+                    read_slots<R, FAST, KB, true>((uint32_t)rg[(u + kSlotAhead) % kRing], T, H, hm, o1, o2);
+                // a chunk past the last one (the group's tail) only skips the
+                // probe: the ring and slot updates above stay unconditional, or
+                // the compiler merges the ring registers through a copy that
+                // waits for the refill load issued in the same chunk
+                if (k < nch)                                              // wave-uniform
+                    probe_rows<R, FAST, !FAST>(sb[u], b, k * 64 + lane, V, s, hm, o1, o2, actmask, lm, zero, nA, s,
+                                               mrun, cnt);
                 // refill the ring unconditionally (past the end: the last chunk
-                // again): a conditional element update would make the register
-                // tuple a phi whose merge waits on the load
-                rg[u] = ld(Bc, min(k + kRing, nch - 1));
-                sb[(u + 1) & 1] = read_slots<R, FAST>((uint32_t)rg[(u + 1) % kRing], T, H, hm, o1, o2);
-                probe_rows<R, FAST>(sb[u & 1], b, k * 64 + lane, V, s, hm, o1, o2, actmask, lm, zero, nA, s,
-                                    mrun, cnt);
+                // again) and after the chunk's last use, so the load reuses the
+                // chunk's registers: a conditional update, or one while the old
+                // value is live, makes the compiler copy the ring at the loop
+                // back edge behind a wait for the loads just issued
+                rg[u] = ld_chunk(rc, lane_off, min(k + kRing, nch - 1));
             }
         }
         if (lane == 0) {
@@ -410,21 +501,25 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
         const bool ok = (uint32_t)r < nrows;
         nA[r] = ok ? nhash[i0 + r] : s;
         uint32_t f = ok ? fam[i0 - row0 + r] : 0;
-        failmask |= (uint32_t)(f >= kMaxFam) << r;   // no field family worked: merged literally below
-        f = f < kMaxFam ? f : 0;
-        const QFields q = qfields(f);
+        failmask |= (uint32_t)(f == kFamFailed) << r;   // no field family worked: merged literally below
+        f = f == kFamFailed ? 0 : f;
+        fast &= f == 0;                                  // family 0 and no twins (kFamTwins)
+        const QFields q = qfields(f & ~kFamTwins);
         o1[r] = q.o1; o2[r] = q.o2;
-        fast &= f == 0;
         alast[r] = (ok && nA[r] >= s) ? hashes[(uint64_t)(i0 + r) * s + s - 1] : kEmpty;
         any_partial_row |= nA[r] < s;
     }
     __syncthreads();
+    // NCH = 16 means 512 < s <= 1024, i.e. H = 2048 (B = 11) for every such s.
+    // The kernel declares no static LDS (.group_segment_fixed_size 0, checked
+    // by tests/test_host.py), so `lds` is LDS address 0 (read_slots).
+    constexpr int KB = NCH == 16 ? 11 : 0;
     if (fast)
-        ap_columns<R, NCH, true>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend, c0 + wave, WG / 64,
-                                 nA, o1, o2, alast, ~failmask, any_partial_row, common, denom, seg0);
+        ap_columns<R, NCH, true, KB>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend, c0 + wave, WG / 64,
+                                     nA, o1, o2, alast, ~failmask, any_partial_row, common, denom, seg0);
     else
-        ap_columns<R, NCH, false>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend, c0 + wave, WG / 64,
-                                  nA, o1, o2, alast, ~failmask, any_partial_row, common, denom, seg0);
+        ap_columns<R, NCH, false, KB>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend, c0 + wave, WG / 64,
+                                      nA, o1, o2, alast, ~failmask, any_partial_row, common, denom, seg0);
     if (failmask) {
         // a row whose table could not be built (three of its keys share a low
         // word under every field family; never observed on real sketches):
@@ -551,22 +646,27 @@ __device__ __forceinline__ void band_columns(const uint64_t *__restrict__ hashes
         const uint64_t *Bc = hashes + (uint64_t)c * s;
         uint32_t q = q0;
         bool more = true;
-        Slots<R> sb[2];
-        sb[0] = read_slots<R, FAST>((uint32_t)rg[0], T, H, hm, o1, o2);
+        // as ap_columns: ring refill and slot reads unconditional, the refill
+        // after the chunk's last use; a finished column only skips the probe
+        Slots<R> sb[kRing];
+#pragma unroll
+        for (int u = 0; u < kSlotAhead; u++) sb[u] = read_slots<R, FAST, kBandB>((uint32_t)rg[u], T, H, hm, o1, o2);
         for (uint32_t kb = 0; more; kb += kRing) {
 #pragma unroll
             for (int u = 0; u < kRing; u++) {
-                if (!more) continue;                                  // wave-uniform
                 const uint64_t b = rg[u];
                 const uint32_t j0 = q0 + 64 * (kb + u);
+                sb[(u + kSlotAhead) % kRing] =
+                    read_slots<R, FAST, kBandB>((uint32_t)rg[(u + kSlotAhead) % kRing], T, H, hm, o1, o2);
+                if (more) {                                           // wave-uniform
+                    const uint64_t inb = __builtin_amdgcn_ballot_w64(b < hi) & tail_mask(j0, s);
+                    probe_rows<R, FAST>(sb[u], b, q + lane, V, kBandCapMax, hm, o1, o2, actmask, inb, pr, cap_r,
+                                        s, mrun, cnt);
+                    const uint32_t nin = (uint32_t)__popcll(inb);
+                    q += nin;
+                    more = nin == 64;
+                }
                 rg[u] = ld_col(Bc, j0 + 64 * kRing + lane, s);       // refill the ring
-                const uint64_t inb = __builtin_amdgcn_ballot_w64(b < hi) & tail_mask(j0, s);
-                sb[(u + 1) & 1] = read_slots<R, FAST>((uint32_t)rg[(u + 1) % kRing], T, H, hm, o1, o2);
-                probe_rows<R, FAST>(sb[u & 1], b, q + lane, V, kBandCapMax, hm, o1, o2, actmask, inb, pr, cap_r,
-                                    s, mrun, cnt);
-                const uint32_t nin = (uint32_t)__popcll(inb);
-                q += nin;
-                more = nin == 64;
             }
         }
 #pragma unroll

@@ -313,6 +313,36 @@ def test_allpairs_unbuildable_table_falls_back_to_merge(path, partial):
     assert c.max() >= 2
 
 
+@pytest.mark.parametrize("seed", [0, 1])
+def test_allpairs_twin_low_words_vs_oracle(seed):
+    """Rows holding two hashes with one low 32-bit word (twins) fill both of
+    those keys' slots, so a lookup can match a slot whose high word differs and
+    must try the other: such rows leave the fast probe (k_build_q32 flags them).
+    Columns hold the first twin only, the second only, both, or neither.  Keys
+    whose rotated quotient is all ones (they "match" an empty slot word) are
+    spread over rows and columns too."""
+    rng = np.random.default_rng(seed)
+    N = 16
+    pool = rng.choice(2 ** 62, size=400 + N * S, replace=False).astype(np.uint64)
+    shared, fresh = pool[:400], pool[400:].reshape(N, S)  # a common block, so counts are non-trivial
+    lo = np.uint64(0x2468ACE1)
+    tw = np.array([(np.uint64(k) << np.uint64(44)) | lo for k in (5, 9)], dtype=np.uint64)
+    h = np.zeros((N, S), np.uint64)
+    for i in range(N):
+        pick = {0: tw, 1: tw, 2: tw, 3: tw[:1], 4: tw[:1], 5: tw[1:], 6: tw[1:], 7: tw, 8: tw}.get(i, tw[:0])
+        em = np.array([(np.uint64(k) << np.uint64(44)) | np.uint64(w) for k, w in
+                       ((3, 0xAECFFFFF), (4, 0xFFFFABCF), (6, 0x8F0FFFFF))], dtype=np.uint64)[i % 4:]
+        base = np.concatenate([pick, em, shared[: 200 + 10 * i]])
+        h[i] = np.sort(np.concatenate([base, fresh[i][: S - len(base)]]))
+    assert all(len(np.unique(r)) == S for r in h)
+    nh = np.full(N, S, np.uint32)
+    oc, od = oracle.allpairs(h, nh, S, threads=4)
+    with _lib.Context(0, 21, S, 42) as ctx:
+        c, d = ctx.allpairs(h, nh)
+    assert np.array_equal(c, oc) and np.array_equal(d, od)
+    assert oc.max() >= 150
+
+
 def _unbuildable_rows():
     """Rows 0 and 7 hold three hashes with one low word (no cuckoo table can
     hold them); rows 1 and 8 share two of them."""

@@ -30,6 +30,25 @@ def test_library_exports_every_header_symbol():
     assert L.drephip_version() >= 100
 
 
+def test_allpairs_kernel_declares_no_static_lds(tmp_path):
+    """k_allpairs_q addresses its slot tables at absolute LDS address 0
+    (allpairs.hip read_slots, ABS): valid only while the kernel declares no
+    static LDS, so its group segment starts with the dynamic region."""
+    import shutil
+    import subprocess
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    src = os.path.join(ROOT, "drep_amd", "csrc", "allpairs.hip")
+    out = tmp_path / "allpairs.s"
+    subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-S", "-I",
+                    os.path.dirname(src), "-o", str(out), src], check=True, capture_output=True, cwd=tmp_path)
+    fixed = dict(re.findall(r"\.amdhsa_kernel (\S+)\s.*?\.amdhsa_group_segment_fixed_size (\d+)",
+                            out.read_text(), flags=re.S))
+    q = {k: int(v) for k, v in fixed.items() if "k_allpairs_q" in k}
+    assert q and all(v == 0 for v in q.values()), q
+
+
 def test_no_cpu_fallback(monkeypatch):
     """The product path fails loudly when the HIP library is missing."""
     import importlib
