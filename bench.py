@@ -51,7 +51,7 @@ def pmc_block(path):
         d = json.load(open(path))
     except Exception:
         return None
-    keep = ("valu_busy_frac", "lds_busy_frac", "lds_bank_conflict_frac", "wait_any_frac",
+    keep = ("valu_issue_frac_2cyc", "valu_active_quad_frac", "lds_busy_frac", "lds_bank_conflict_frac", "wait_any_frac",
             "wait_inst_any_frac", "active_inst_any_frac", "valu_insts_per_window_end", "effective_clock_ghz")
     out = {k: d["derived"][k] for k in keep if k in d.get("derived", {})}
     out["source"] = os.path.relpath(path, ROOT)

@@ -130,13 +130,13 @@ __global__ __launch_bounds__(1024) void k_build_q32(const uint64_t *__restrict__
     const uint32_t rr = r % R;
     if (g >= row1) {
         for (uint32_t i = threadIdx.x; i < 2 * H; i += blockDim.x) img[i * R + rr] = kEmpty32;
-        for (uint32_t i = threadIdx.x; i < s; i += blockDim.x) img[2 * H * R + rr * s + i] = 0;
+        for (uint32_t i = threadIdx.x; i < s; i += blockDim.x) img[2 * H * R + i * R + rr] = 0;
         if (threadIdx.x == 0) fam_out[r] = 0;
         return;
     }
     const uint32_t n = nhash[g];
     const uint64_t *A = hashes + (uint64_t)g * s;
-    for (uint32_t i = threadIdx.x; i < s; i += blockDim.x) img[2 * H * R + rr * s + i] = (uint32_t)(A[i] >> 32);
+    for (uint32_t i = threadIdx.x; i < s; i += blockDim.x) img[2 * H * R + i * R + rr] = (uint32_t)(A[i] >> 32);
     for (uint32_t fam = 0; fam < kMaxFam; fam++) {
         const QFields q = qfields(fam);
         for (uint32_t i = threadIdx.x; i < 2 * H; i += blockDim.x) Tb[i] = kEmpty32;
@@ -259,12 +259,13 @@ __device__ __forceinline__ Slots<R> read_slots(uint32_t blo, const uint32_t *T, 
 // R row tables, with wave-level lane masks kept in SGPRs: per row the two
 // slot words are compared and their ballots OR-ed; only a row with a hit in
 // the chunk (uniform branch) selects i, confirms the high word against
-// V[r * vs + i] and applies the union-rank rule
+// V[r * vs + i] (VIL: the whole-row image's row-interleaved V[i * R + r], one
+// base for every row) and applies the union-rank rule
 //     i + j < s + mrun + (matches in lower lanes)
 // with scalar popcounts -- counts stay in SGPRs, no per-lane reduction.
 // i = ibase[r] + field, valid below ilim[r].  lanemask drops lanes (band
 // kernel: outside the band).
-template <int R, bool FAST, bool RETRY = true>
+template <int R, bool FAST, bool RETRY = true, bool VIL = false>
 __device__ __forceinline__ void probe_rows(const Slots<R> &sl, uint64_t b, uint32_t j, const uint32_t *V,
                                            uint32_t vs, uint32_t hm, const uint32_t (&o1)[R],
                                            const uint32_t (&o2)[R], uint32_t actmask, uint64_t lanemask,
@@ -296,20 +297,31 @@ __device__ __forceinline__ void probe_rows(const Slots<R> &sl, uint64_t b, uint3
         if (m == 0) continue;                                        // wave-uniform: no hit in this row
         const bool c1 = x1 <= hm;
         uint32_t f = (c1 ? sl.e1[r] : sl.e2[r]) & hm;
-        bool ok = f < ilim[r] && V[r * vs + (f < ilim[r] ? f : 0)] == bhi;
-        if constexpr (RETRY) {
+        // the high-word read runs on every lane (index clamped) and both tests
+        // become lane masks: no exec branch, no bool-to-mask conversions.
+        // f >= ilim only for the empty word's false match (f = hm)
+        const uint32_t vlast = (VIL ? s : vs) - 1;                   // a valid index of the row's V
+        const uint32_t fc = min(f, vlast);
+        const uint32_t vhi = VIL ? V[fc * R + r] : V[r * vs + fc];
+        if constexpr (!RETRY) {
+            // masks straight from the compares (a ballot of a combined bool
+            // costs a select and a compare to rebuild the mask)
+            m &= __builtin_amdgcn_ballot_w64(vhi == bhi) & __builtin_amdgcn_ballot_w64(f < ilim[r]);
+        } else {
+            bool ok = vhi == bhi && f < ilim[r];
             // both slots match when two of the row's keys share this low word
             // (RETRY = false: k_build_q32 found no such pair in any row), or
             // when the first is an empty word's false match (see k_build_q32)
             const bool retry = c1 && x2 <= hm && !ok;
             if (__builtin_amdgcn_ballot_w64(retry) != 0) {
                 const uint32_t f2 = sl.e2[r] & hm;
-                const bool ok2 = retry && f2 < ilim[r] && V[r * vs + (f2 < ilim[r] ? f2 : 0)] == bhi;
+                const uint32_t f2c = min(f2, vlast);
+                const bool ok2 = retry && f2 < ilim[r] && (VIL ? V[f2c * R + r] : V[r * vs + f2c]) == bhi;
                 f = ok2 ? f2 : f;
                 ok = ok || ok2;
             }
+            m &= __builtin_amdgcn_ballot_w64(ok);
         }
-        m &= __builtin_amdgcn_ballot_w64(ok);
         const uint32_t lim = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, s + mrun[r]));
         cnt[r] += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(ibase[r] + f + j < lim) & m);
@@ -424,7 +436,7 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
                 // the compiler merges the ring registers through a copy that
                 // waits for the refill load issued in the same chunk
                 if (k < nch)                                              // wave-uniform
-                    probe_rows<R, FAST, !FAST>(sb[u], b, k * 64 + lane, V, s, hm, o1, o2, actmask, lm, zero, nA, s,
+                    probe_rows<R, FAST, !FAST, true>(sb[u], b, k * 64 + lane, V, s, hm, o1, o2, actmask, lm, zero, nA, s,
                                                mrun, cnt);
                 // refill the ring unconditionally (past the end: the last chunk
                 // again) and after the chunk's last use, so the load reuses the
@@ -474,7 +486,7 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
     extern __shared__ __align__(16) uint32_t lds[];    // 16-B aligned: slot words are read with ds_read_b128
     const uint32_t H = 1u << B, hm = H - 1, TS = 2 * H;
     uint32_t *T = lds;                                  // [TS][R] interleaved slot words
-    uint32_t *V = T + R * TS;                           // [R][s] high words by position
+    uint32_t *V = T + R * TS;                           // [s][R] high words by position (row-interleaved)
     const uint32_t i0 = items[blockIdx.x].x;
     const uint32_t c0 = items[blockIdx.x].y;
     if (i0 == 0xFFFFFFFFu) return;                      // idle padding item (make_items)

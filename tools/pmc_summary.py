@@ -8,10 +8,14 @@ Derived quantities (MI355X_MICROARCH.md, "s_memtime tick vs SQ PMC units"):
     wait fractions below are ratios of like units;
   * GRBM_GUI_ACTIVE rides along in every pass and rocprofv3 sums it over the 8
     XCDs: kernel cycles per dispatch = sum / passes / 8 / dispatches;
-  * valu_busy_frac = SQ_ACTIVE_INST_VALU (quad-cycles) x 4 / (1024 SIMDs x
-    kernel cycles): the share of SIMD cycles holding a VALU instruction.  Above
-    1.0 it says some VALU instructions take fewer than 4 cycles (the
-    fraction is then a lower bound of saturation, not an error);
+  * valu_issue_frac_2cyc = SQ_INSTS_VALU x 2 / (1024 SIMDs x kernel cycles):
+    VALU issue against the guide's peak of one wave64 instruction per 2 cycles
+    per SIMD (SIMD-32).  Integer 3-operand and 64-bit instructions measure
+    ~2.6 cycles and the simple ones ~1.45 (profiles/r01_valu_microbench.json),
+    so a mix-priced bound sits between this and 1.3x it;
+  * valu_active_quad_frac = SQ_ACTIVE_INST_VALU (quad-cycles) x 4 / (1024 SIMDs
+    x kernel cycles): the counter's own unit (it equals SQ_INSTS_VALU, one
+    quad-cycle per instruction), i.e. the share at a 4-cycle issue;
   * lds_busy_frac = SQ_LDS_IDX_ACTIVE (LDS-array cycles per CU) / (256 CUs x
     kernel cycles); lds_bank_conflict_frac = SQ_LDS_BANK_CONFLICT /
     SQ_LDS_IDX_ACTIVE (the extra cycles conflicts cost);
@@ -68,9 +72,11 @@ def main():
         d["kernel_cycles_per_dispatch"] = cyc
         if a.kernel_ms:
             d["effective_clock_ghz"] = cyc / (a.kernel_ms * 1e-3) / 1e9
+        if c.get("SQ_INSTS_VALU"):
+            d["valu_issue_frac_2cyc"] = c["SQ_INSTS_VALU"] / ndisp * 2 / (N_SIMD * cyc)
         vd = max(len(disp.get("SQ_ACTIVE_INST_VALU", ())), 1)
         if c.get("SQ_ACTIVE_INST_VALU"):
-            d["valu_busy_frac"] = c["SQ_ACTIVE_INST_VALU"] / vd * 4 / (N_SIMD * cyc)
+            d["valu_active_quad_frac"] = c["SQ_ACTIVE_INST_VALU"] / vd * 4 / (N_SIMD * cyc)
         ld = max(len(disp.get("SQ_LDS_IDX_ACTIVE", ())), 1)
         if c.get("SQ_LDS_IDX_ACTIVE"):
             d["lds_busy_frac"] = c["SQ_LDS_IDX_ACTIVE"] / ld / (N_CU * cyc)
