@@ -45,7 +45,6 @@ constexpr uint32_t kMaxFam = 6;                 // cuckoo field families tried p
 constexpr uint32_t kFamTwins = 0x40;            // k_build_q32 family byte: the row has two keys with one low word
 constexpr uint32_t kFamFailed = 0xFF;           // ... no family worked (the row's pairs are merged literally)
 constexpr uint32_t kLdsBudget = 156 * 1024;     // dynamic LDS per workgroup
-constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;      // empty slot word
 
 __host__ __device__ __forceinline__ uint64_t cond_index(uint64_t i, uint64_t j, uint64_t N) {
     return i * N - i * (i + 1) / 2 + (j - i - 1);
@@ -56,16 +55,20 @@ __device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin
 // Quotiented two-choice cuckoo table over the keys' low words x = lo32(key):
 // choice 1 sits at T[f1(x)], choice 2 at T[H + f2(x)], where f1/f2 are
 // disjoint B-bit fields of x at offsets o1/o2 (family f picks them).  Because
-// a slot's position fixes those B bits, the stored word replaces them with
-// the key's position i, and is kept rotated right by the field offset:
-//     e = rotr32((x & ~F) | (i << o), o)       (field at bits [0, B))
-// so one 4-byte read answers "does this slot hold low word x" --
-// (e ^ rotr32(x, o)) < 2^B -- and gives i = e & (2^B - 1).  The key's high
-// word is then compared with V[i] = hi32(A[i]).  The all-ones empty word
-// decodes to i = 2^B - 1, past every real position (H >= 2s), and no stored
-// word is all ones (i <= s - 1 < 2^B - 1).  Two keys of one row with equal low
-// words occupy the two slots they share; a hit whose high word does not match
-// retries the other choice.  Exact for every key.
+// a slot's position p fixes those B bits, the stored word replaces them with
+// the key's position i xor p, and is kept rotated right by the field offset:
+//     e = rotr32((x & ~F) | ((i ^ p) << o), o)       (field at bits [0, B))
+// A probe of slot p = f(b) computes d = e ^ rotr32(b, o): its quotient bits are
+// zero iff the slot holds low word lo32(b), and then its field bits are
+// (i ^ p) ^ f(b) = i, so d <= 2^B - 1 is the test AND d is the position -- for
+// two choices, min(d1, d2) is both.  The key's high word is then compared with
+// V[i] = hi32(A[i]).  An empty slot p holds empty_word(p): all-ones quotient,
+// field hm ^ p, so a probe that "matches" it (a low word whose quotient is all
+// ones) decodes to i = hm, past every real position (H >= 2s), and loses
+// every min against a real hit.  Two keys of one row with equal low words
+// (twins) occupy the two slots they share; the generic probe retries the
+// other choice when the high word does not match, and k_build_q32 keeps rows
+// with twins off the fast probe.  Exact for every key.
 struct QFields { uint32_t o1, o2; };
 __host__ __device__ __forceinline__ uint32_t rotr32(uint32_t x, uint32_t r) {
     return r ? (x >> r) | (x << (32 - r)) : x;
@@ -81,6 +84,11 @@ __host__ __device__ __forceinline__ QFields qfields(uint32_t fam) {
     return {o1[fam], o2[fam]};
 }
 
+// The empty word of slot `slot` (either region): all-ones quotient, field
+// hm ^ p, so that a probe decodes it to position hm
+__host__ __device__ __forceinline__ uint32_t empty_word(uint32_t slot, uint32_t hm) {
+    return ~hm | ((slot & hm) ^ hm);
+}
 // Insert (x, ix) into an LDS table whose slot p lives at T[p * stride + col]
 // (stride R, col r: the interleaved band tables; stride 1: one row).
 __device__ __forceinline__ bool cuckoo_insert32(uint32_t *T, uint32_t stride, uint32_t col, uint32_t H,
@@ -90,11 +98,11 @@ __device__ __forceinline__ bool cuckoo_insert32(uint32_t *T, uint32_t stride, ui
     for (int kick = 0; kick < 96; kick++) {
         const bool second = pos >= H;
         const uint32_t o = second ? q.o2 : q.o1, F = second ? F2 : F1;
-        const uint32_t old_r = atomicExch(&T[pos * stride + col], rotr32((x & ~F) | (ix << o), o));
-        if (old_r == kEmpty32) return true;
+        const uint32_t lp = pos & hm;                            // position within the region
+        const uint32_t old_r = atomicExch(&T[pos * stride + col], rotr32((x & ~F) | ((ix ^ lp) << o), o));
+        if (old_r == empty_word(pos, hm)) return true;
         const uint32_t old = rotr32(old_r, (32 - o) & 31);      // decode the evicted entry
-        const uint32_t lp = second ? pos - H : pos;
-        ix = (old >> o) & hm;
+        ix = ((old >> o) & hm) ^ lp;
         x = (old & ~F) | (lp << o);
         pos = second ? ((x >> q.o1) & hm) : (H + ((x >> q.o2) & hm));
     }
@@ -105,9 +113,15 @@ __device__ __forceinline__ bool cuckoo_has32(const uint32_t *T, uint32_t stride,
                                              uint32_t hm, QFields q, uint32_t x, uint32_t ix) {
     const uint32_t e1 = T[((x >> q.o1) & hm) * stride + col];
     const uint32_t e2 = T[(H + ((x >> q.o2) & hm)) * stride + col];
-    const bool ok1 = (e1 ^ rotr32(x, q.o1)) <= hm && (e1 & hm) == ix;
-    const bool ok2 = (e2 ^ rotr32(x, q.o2)) <= hm && (e2 & hm) == ix;
-    return ok1 || ok2;
+    return (e1 ^ rotr32(x, q.o1)) == ix || (e2 ^ rotr32(x, q.o2)) == ix;
+}
+// Both of x's slots hold a key with x's low word (x and a twin; an empty
+// word's false match decodes to hm and does not count)
+__device__ __forceinline__ bool cuckoo_twin32(const uint32_t *T, uint32_t stride, uint32_t col, uint32_t H,
+                                              uint32_t hm, QFields q, uint32_t x) {
+    const uint32_t e1 = T[((x >> q.o1) & hm) * stride + col];
+    const uint32_t e2 = T[(H + ((x >> q.o2) & hm)) * stride + col];
+    return (e1 ^ rotr32(x, q.o1)) < hm && (e2 ^ rotr32(x, q.o2)) < hm;
 }
 
 // One table per row g = row0 + blockIdx.x, written straight into the LDS
@@ -129,7 +143,7 @@ __global__ __launch_bounds__(1024) void k_build_q32(const uint64_t *__restrict__
     uint32_t *img = blk + (uint64_t)(r / R) * stride;
     const uint32_t rr = r % R;
     if (g >= row1) {
-        for (uint32_t i = threadIdx.x; i < 2 * H; i += blockDim.x) img[i * R + rr] = kEmpty32;
+        for (uint32_t i = threadIdx.x; i < 2 * H; i += blockDim.x) img[i * R + rr] = empty_word(i, hm);
         for (uint32_t i = threadIdx.x; i < s; i += blockDim.x) img[2 * H * R + i * R + rr] = 0;
         if (threadIdx.x == 0) fam_out[r] = 0;
         return;
@@ -139,7 +153,7 @@ __global__ __launch_bounds__(1024) void k_build_q32(const uint64_t *__restrict__
     for (uint32_t i = threadIdx.x; i < s; i += blockDim.x) img[2 * H * R + i * R + rr] = (uint32_t)(A[i] >> 32);
     for (uint32_t fam = 0; fam < kMaxFam; fam++) {
         const QFields q = qfields(fam);
-        for (uint32_t i = threadIdx.x; i < 2 * H; i += blockDim.x) Tb[i] = kEmpty32;
+        for (uint32_t i = threadIdx.x; i < 2 * H; i += blockDim.x) Tb[i] = empty_word(i, hm);
         if (threadIdx.x == 0) { fail = 0; twins = 0; }
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
@@ -150,20 +164,12 @@ __global__ __launch_bounds__(1024) void k_build_q32(const uint64_t *__restrict__
         __syncthreads();
         if (!fail) {
             // twins: two keys with one low word occupy both of their shared
-            // slots, so a lookup matches both and must check the second too --
-            // only the generic probe does (kFamTwins keeps this row off FAST).
-            // The empty word can also "match" (a low word whose rotated
-            // quotient is all ones), but never hides a key: a key sits in its
-            // second slot only after an exchange filled its first, and slots
-            // are never emptied, so the fast probe's "first slot if it
-            // matches" is exact on a row without twins.
-            for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-                const uint32_t x = (uint32_t)A[i];
-                const uint32_t e1 = Tb[(x >> q.o1) & hm], e2 = Tb[H + ((x >> q.o2) & hm)];
-                if (e1 != kEmpty32 && e2 != kEmpty32 && (e1 ^ rotr32(x, q.o1)) <= hm &&
-                    (e2 ^ rotr32(x, q.o2)) <= hm)
-                    twins = 1;
-            }
+            // slots, so a lookup matches both (two real positions < hm) and
+            // min(d1, d2) may name the wrong one -- only the generic probe
+            // retries (kFamTwins keeps this row off FAST).  An empty word's
+            // false match decodes to hm and never wins the min.
+            for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+                if (cuckoo_twin32(Tb, 1, 0, H, hm, q, (uint32_t)A[i])) twins = 1;
             __syncthreads();
             for (uint32_t i = threadIdx.x; i < 2 * H; i += blockDim.x) img[i * R + rr] = Tb[i];
             if (threadIdx.x == 0) fam_out[r] = (uint8_t)(fam | (twins ? kFamTwins : 0u));
@@ -295,8 +301,9 @@ __device__ __forceinline__ void probe_rows(const Slots<R> &sl, uint64_t b, uint3
         // one compare, one mask: a hit in either slot <=> min(x1, x2) <= hm
         uint64_t m = __builtin_amdgcn_ballot_w64(min(x1, x2) <= hm) & lanemask;
         if (m == 0) continue;                                        // wave-uniform: no hit in this row
-        const bool c1 = x1 <= hm;
-        uint32_t f = (c1 ? sl.e1[r] : sl.e2[r]) & hm;
+        // the probe value of a hit is its position (row tables above): the
+        // smaller of the two is the hit, an empty word's false match (hm) loses
+        uint32_t f = min(x1, x2);
         // the high-word read runs on every lane (index clamped) and both tests
         // become lane masks: no exec branch, no bool-to-mask conversions.
         // f >= ilim only for the empty word's false match (f = hm)
@@ -312,9 +319,9 @@ __device__ __forceinline__ void probe_rows(const Slots<R> &sl, uint64_t b, uint3
             // both slots match when two of the row's keys share this low word
             // (RETRY = false: k_build_q32 found no such pair in any row), or
             // when the first is an empty word's false match (see k_build_q32)
-            const bool retry = c1 && x2 <= hm && !ok;
+            const bool retry = max(x1, x2) <= hm && !ok;
             if (__builtin_amdgcn_ballot_w64(retry) != 0) {
-                const uint32_t f2 = sl.e2[r] & hm;
+                const uint32_t f2 = max(x1, x2);
                 const uint32_t f2c = min(f2, vlast);
                 const bool ok2 = retry && f2 < ilim[r] && (VIL ? V[f2c * R + r] : V[r * vs + f2c]) == bhi;
                 f = ok2 ? f2 : f;
@@ -608,8 +615,12 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 // are kEmpty in the sketch matrix and fail every band test (b < hi <= the
 // rows' largest element + 1); lanes past s hold clamped copies and are masked
 // by tail_mask.
-__device__ __forceinline__ uint64_t ld_col(const uint64_t *__restrict__ Bc, uint32_t j, uint32_t s) {
-    return Bc[min(j, s - 1)];
+// 64 column elements from position `first` (wave-uniform) on, one per lane,
+// through the column's buffer resource: lanes past s read 0 (buffer bounds)
+// and are dropped by tail_mask where the chunk is used
+__device__ __forceinline__ uint64_t ld_elems(__amdgpu_buffer_rsrc_t rs, uint32_t lane_off, uint32_t first) {
+    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, lane_off, rfl(first) * 8u, 0);
+    return ((uint64_t)v[1] << 32) | v[0];
 }
 __device__ __forceinline__ uint64_t tail_mask(uint32_t j0, uint32_t s) {     // lanes with j0 + lane < s
     return j0 + 64 <= s ? ~0ull : j0 >= s ? 0ull : (1ull << (s - j0)) - 1;
@@ -618,23 +629,24 @@ __device__ __forceinline__ uint64_t tail_mask(uint32_t j0, uint32_t s) {     // 
 // The column phase of one band: wave w takes columns w, w+NW, ... of the
 // item.  A column's band segment streams through a ring of kRing chunks in
 // registers, loaded kRing chunks ahead (the next column's first kRing chunks
-// when a column starts); slot words are read one chunk ahead of the tests
-// into the other half of a two-entry buffer.
-template <int R, uint32_t NW, bool FAST>
+// when a column starts) by raw buffer loads; slot words are read one chunk
+// ahead of the tests.
+template <int R, uint32_t NW, bool FAST, bool RETRY>
 __device__ __forceinline__ void band_columns(const uint64_t *__restrict__ hashes, uint32_t s, const uint32_t *T,
                                              const uint32_t *V, uint32_t *cur, uint16_t *pcnt, uint16_t *pm,
                                              uint32_t c0, uint32_t ncols, uint32_t i0, uint32_t nrows, uint32_t wave,
                                              uint64_t hi, uint32_t fam, const uint32_t (&pr)[R]) {
     constexpr uint32_t H = 1u << kBandB, hm = H - 1;
     const uint32_t lane = threadIdx.x & 63;
+    const uint32_t lane_off = lane * 8u;
     uint32_t ci = wave;
     uint64_t nx[kRing];
     uint32_t nq = 0;
     auto load_first = [&](uint32_t cc) {
         nq = rfl(cur[cc]);
-        const uint64_t *Bn = hashes + (uint64_t)(c0 + cc) * s;
+        const __amdgpu_buffer_rsrc_t rn = column_rsrc(hashes + (uint64_t)(c0 + cc) * s, s);
 #pragma unroll
-        for (int k = 0; k < kRing; k++) nx[k] = ld_col(Bn, nq + 64 * k + lane, s);
+        for (int k = 0; k < kRing; k++) nx[k] = ld_elems(rn, lane_off, nq + 64 * k);
     };
     if (ci < ncols) load_first(ci);
     uint32_t o1[R], o2[R], cap_r[R];
@@ -655,7 +667,7 @@ __device__ __forceinline__ void band_columns(const uint64_t *__restrict__ hashes
         uint32_t mrun[R], cnt[R];
 #pragma unroll
         for (int r = 0; r < R; r++) { mrun[r] = rfl(pm[r * kBandCols + ci]); cnt[r] = 0; }   // scalar counters
-        const uint64_t *Bc = hashes + (uint64_t)c * s;
+        const __amdgpu_buffer_rsrc_t rc = column_rsrc(hashes + (uint64_t)c * s, s);
         uint32_t q = q0;
         bool more = true;
         // as ap_columns: ring refill and slot reads unconditional, the refill
@@ -672,13 +684,13 @@ __device__ __forceinline__ void band_columns(const uint64_t *__restrict__ hashes
                     read_slots<R, FAST, kBandB>((uint32_t)rg[(u + kSlotAhead) % kRing], T, H, hm, o1, o2);
                 if (more) {                                           // wave-uniform
                     const uint64_t inb = __builtin_amdgcn_ballot_w64(b < hi) & tail_mask(j0, s);
-                    probe_rows<R, FAST>(sb[u], b, q + lane, V, kBandCapMax, hm, o1, o2, actmask, inb, pr, cap_r,
+                    probe_rows<R, FAST, RETRY>(sb[u], b, q + lane, V, kBandCapMax, hm, o1, o2, actmask, inb, pr, cap_r,
                                         s, mrun, cnt);
                     const uint32_t nin = (uint32_t)__popcll(inb);
                     q += nin;
                     more = nin == 64;
                 }
-                rg[u] = ld_col(Bc, j0 + 64 * kRing + lane, s);       // refill the ring
+                rg[u] = ld_elems(rc, lane_off, j0 + 64 * kRing);    // refill the ring
             }
         }
 #pragma unroll
@@ -708,7 +720,7 @@ __global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
     uint16_t *pm = pcnt + R * kBandCols;                             // [R][kBandCols] shared so far (<= s)
     __shared__ uint32_t s_p[R], s_q[R];
     __shared__ uint64_t s_hi;
-    __shared__ int s_done, s_fail, s_abort;
+    __shared__ int s_done, s_fail, s_abort, s_twin;
 
     const uint32_t i0 = items[blockIdx.x].x;
     const uint32_t c0 = items[blockIdx.x].y;
@@ -771,8 +783,8 @@ __global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
         uint32_t fam = 0;
         for (; fam < kMaxFam; fam++) {
             const QFields qf = qfields(fam);
-            for (uint32_t k = tid; k < R * TS; k += WG) T[k] = kEmpty32;
-            if (tid == 0) s_fail = 0;
+            for (uint32_t k = tid; k < R * TS; k += WG) T[k] = empty_word(k / R, hm);
+            if (tid == 0) { s_fail = 0; s_twin = 0; }
             __syncthreads();
             for (uint32_t idx = tid; idx < R * cap; idx += WG) {
                 const uint32_t r = idx / cap, t = idx - r * cap;
@@ -796,6 +808,7 @@ __global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
                 const uint64_t x = hashes[(uint64_t)(i0 + r) * s + p + t];
                 if (x >= hi) continue;
                 if (!cuckoo_has32(T, R, r, H, hm, qf, (uint32_t)x, t)) s_fail = 1;
+                if (cuckoo_twin32(T, R, r, H, hm, qf, (uint32_t)x)) s_twin = 1;
                 if (fam == 0) atomicAdd(&s_q[r], 1u);
             }
             __syncthreads();
@@ -808,10 +821,13 @@ __global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
 
         uint64_t t_c0 = prof ? wall_clock64() : 0;
         // ---- columns: wave w takes columns w, w+NW, ...
-        if (fam == 0)
-            band_columns<R, NW, true>(hashes, s, T, V, cur, pcnt, pm, c0, ncols, i0, nrows, wave, hi, fam, pr);
+        // the fast probe without the second-slot retry unless a band table has twins
+        if (fam == 0 && !s_twin)
+            band_columns<R, NW, true, false>(hashes, s, T, V, cur, pcnt, pm, c0, ncols, i0, nrows, wave, hi, fam, pr);
+        else if (fam == 0)
+            band_columns<R, NW, true, true>(hashes, s, T, V, cur, pcnt, pm, c0, ncols, i0, nrows, wave, hi, fam, pr);
         else
-            band_columns<R, NW, false>(hashes, s, T, V, cur, pcnt, pm, c0, ncols, i0, nrows, wave, hi, fam, pr);
+            band_columns<R, NW, false, true>(hashes, s, T, V, cur, pcnt, pm, c0, ncols, i0, nrows, wave, hi, fam, pr);
         __syncthreads();
         if (tid < (uint32_t)R) s_p[tid] += s_q[tid];
         if (prof && tid == 0) {

@@ -313,8 +313,9 @@ def test_allpairs_unbuildable_table_falls_back_to_merge(path, partial):
     assert c.max() >= 2
 
 
+@pytest.mark.parametrize("path", ["table", "band"])
 @pytest.mark.parametrize("seed", [0, 1])
-def test_allpairs_twin_low_words_vs_oracle(seed):
+def test_allpairs_twin_low_words_vs_oracle(seed, path):
     """Rows holding two hashes with one low 32-bit word (twins) fill both of
     those keys' slots, so a lookup can match a slot whose high word differs and
     must try the other: such rows leave the fast probe (k_build_q32 flags them).
@@ -338,6 +339,8 @@ def test_allpairs_twin_low_words_vs_oracle(seed):
     nh = np.full(N, S, np.uint32)
     oc, od = oracle.allpairs(h, nh, S, threads=4)
     with _lib.Context(0, 21, S, 42) as ctx:
+        if path == "band":                    # band tables of 256 elements: twins in the first band
+            ctx.set_allpairs_path(ctx.AP_BAND, 256)
         c, d = ctx.allpairs(h, nh)
     assert np.array_equal(c, oc) and np.array_equal(d, od)
     assert oc.max() >= 150
