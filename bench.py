@@ -26,12 +26,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
-# VALU issue model: SQ_ACTIVE_INST_VALU counts quad-cycles (MI355X_MICROARCH.md,
-# "s_memtime tick vs SQ PMC units") and equals SQ_INSTS_VALU for the sketch
-# kernel, i.e. each of its wave64 VALU instructions holds a SIMD for 4 cycles:
-# peak = 1024 SIMDs x 2.4 GHz / 4 wave-instructions per second.
+# VALU issue model: MI355X_MICROARCH.md gives one wave64 VALU instruction per
+# 2 cycles per SIMD (SIMD-32) as the issue peak: 1024 SIMDs x 2.4 GHz / 2.
+# The measured throughput of the sketch loop's own instruction mix
+# (profiles/r01_valu_microbench.json: simple VOP2 ops ~1.45 cycles, 3-operand,
+# 64-bit and multiply ops 2.6-2.9) gives a second, mix-priced peak.
 N_SIMD = 256 * 4
-VALU_PEAK_WAVE_INST = N_SIMD * 2.4e9 / 4
+VALU_PEAK_WAVE_INST = N_SIMD * 2.4e9 / 2
+VALU_COSTS = os.path.join(ROOT, "profiles", "r01_valu_microbench.json")
 SKETCH_ISA = os.path.join(ROOT, "profiles", "r02_sketch_isa.json")
 # committed PMC summaries (tools/pmc_summary.py): VALU / LDS utilisation of the
 # two kernels, reported next to the live timings
@@ -41,6 +43,23 @@ SKETCH_TRAFFIC = os.path.join(ROOT, "profiles", "r02_sketch_traffic.json")
 PROFILE_STEPS = 3              # untimed steps that time finalize / all-pairs / table build
 VERIFY_GENOMES = 16            # timed-step sketches re-derived by the C oracle (sampled, every run)
 VERIFY_PAIRS = 100_000         # timed-step counts re-derived by the C oracle (random pairs + one row)
+
+
+def mix_priced_cycles(isa):
+    """SIMD-cycles one wave spends issuing the hot loop's instructions for 64
+    k-mers, each mnemonic priced at its measured throughput (VALU_COSTS);
+    mnemonics not measured take their class price (VOP2 e32 1.45, else 2.6)."""
+    if not os.path.exists(VALU_COSTS) or "valu_mix_per_kmer" not in isa:
+        return None
+    cost = {r["inst"]: r["cycles_per_wave_inst_per_simd"] for r in json.load(open(VALU_COSTS))["results"]}
+    total = 0.0
+    for op, n in isa["valu_mix_per_kmer"].items():
+        base = op.replace("_e32", "").replace("_e64", "").replace("_sdwa", "")
+        c = cost.get(op, cost.get(base))
+        if c is None or op.startswith("v_cndmask"):      # the microbench's cndmask chain waits on vcc
+            c = 1.45 if op.endswith("_e32") else 2.6
+        total += n * c
+    return total
 
 
 def pmc_block(path):
@@ -456,9 +475,16 @@ def main():
         valu.update({"bound": "valu_issue", "achieved": ach, "peak": VALU_PEAK_WAVE_INST,
                      "unit": "wave64 VALU instructions/s", "frac": ach / VALU_PEAK_WAVE_INST,
                      "valu_insts_per_kmer_measured": pmc_sk["valu_insts_per_window_end"],
-                     "note": "each VALU instruction of this kernel holds its SIMD one quad-cycle "
-                             "(SQ_ACTIVE_INST_VALU = SQ_INSTS_VALU); time follows the VALU count "
-                             "(profiles/r02_sketch_ab.json)"})
+                     "note": "peak = the guide's 2-cycle wave64 issue on every SIMD; time follows "
+                             "the VALU count (profiles/r02_sketch_ab.json)"})
+        priced = mix_priced_cycles(isa) if isa else None
+        if priced:
+            # SIMD-cycles per 64 window ends of the hot loop at the microbench's
+            # measured per-instruction throughput -> window ends per second
+            peak_we = N_SIMD * 2.4e9 * 64 / priced
+            valu.update({"mix_priced_cycles_per_64_kmers": priced,
+                         "mix_priced_frac": (window_ends / avg_launch_s) / peak_we if avg_launch_s > 0 else 0.0,
+                         "mix_costs_source": os.path.relpath(VALU_COSTS, ROOT)})
 
     # ---- output segment D2H (PCIe-inclusive leg; not part of `value`)
     torch.cuda.synchronize()
