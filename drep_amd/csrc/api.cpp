@@ -9,6 +9,8 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <mutex>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -403,10 +405,12 @@ static void produce_batch(const char *const *paths, uint32_t g0, uint32_t n_geno
     B.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
-// Ingest pipeline: a producer thread reads + packs batch i+1 (on `threads`
+// Ingest pipeline: one producer thread reads + packs batch i+1 (on `threads`
 // workers, into the other of two pinned buffers) while this thread copies
 // batch i to the GPU and sketches it -- the GPU work hides behind the host
-// ingest, which is the slower side by two orders of magnitude.
+// ingest, which is the slower side by an order of magnitude.  The producer
+// lives for the whole call (a thread per batch paid the HIP runtime's
+// per-thread setup and teardown, ~30 ms, on every batch).
 DREPHIP_EXPORT int drephip_sketch_files(drephip_ctx *ctx, const char *const *paths, uint32_t n_genomes,
                                         int threads, uint64_t *hashes_out, uint32_t *nhash_out,
                                         uint64_t *length_out) {
@@ -421,20 +425,38 @@ DREPHIP_EXPORT int drephip_sketch_files(drephip_ctx *ctx, const char *const *pat
     PinnedSlot *slots = ctx->ingest_slots;          // kept across calls: pinned allocation is slow
     IngestBatch B[2];
     const int k = ctx->k;
-    std::thread producer([&] { produce_batch(paths, 0, n_genomes, threads, k, target, slots[0], B[0], ctx->device); });
-    uint32_t b = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    uint32_t produced = 0, consumed = 0;            // batches handed over / released
+    bool stop = false;
+    std::thread producer([&] {
+        uint32_t g = 0;
+        for (uint32_t i = 0; g < n_genomes; i++) {
+            {   // slot i & 1 is free once batch i - 2 has been consumed
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return stop || consumed + 2 > i; });
+                if (stop) return;
+            }
+            produce_batch(paths, g, n_genomes, threads, k, target, slots[i & 1], B[i & 1], ctx->device);
+            const bool last = B[i & 1].err || g + B[i & 1].n >= n_genomes;
+            g += B[i & 1].n;
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                produced = i + 1;
+            }
+            cv.notify_all();
+            if (last) return;
+        }
+    });
     rc = DREPHIP_OK;
-    for (;;) {
-        producer.join();
+    for (uint32_t b = 0;; b++) {
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return produced > b; });
+        }
         IngestBatch &cur = B[b & 1];
         if (cur.err) { set_error(cur.msg); rc = cur.err; break; }
-        const uint32_t next_g = cur.g0 + cur.n;
-        const bool more = next_g < n_genomes;
-        if (more)
-            producer = std::thread([&, next_g, b] {
-                produce_batch(paths, next_g, n_genomes, threads, k, target, slots[(b + 1) & 1], B[(b + 1) & 1],
-                              ctx->device);
-            });
+        const bool more = cur.g0 + cur.n < n_genomes;
         const auto g0 = std::chrono::steady_clock::now();
         if (length_out) std::copy(cur.length.begin(), cur.length.end(), length_out + cur.g0);
         rc = sketch_packed_host(ctx, slots[b & 1].codes, cur.bases / 16, slots[b & 1].valid, cur.bases / 32, cur.off,
@@ -442,12 +464,19 @@ DREPHIP_EXPORT int drephip_sketch_files(drephip_ctx *ctx, const char *const *pat
         ctx->ingest.gpu_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - g0).count();
         ctx->ingest.produce_s += cur.seconds;
         ctx->ingest.batches++;
-        if (rc || !more) {
-            if (more) producer.join();
-            break;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            consumed = b + 1;
         }
-        b++;
+        cv.notify_all();
+        if (rc || !more) break;
     }
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        stop = true;                                // a producer waiting for a slot ends
+    }
+    cv.notify_all();
+    producer.join();
     ctx->ingest.wall_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return rc;
 }
