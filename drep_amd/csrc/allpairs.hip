@@ -40,7 +40,11 @@ namespace drephip {
 
 constexpr int kApWG = 1024;                     // 16 waves per workgroup
 constexpr uint32_t kApCols = 128;               // columns per work item (fewer when the grid would not fill the chip)
-constexpr uint32_t kApMinCols = 16;             // one column per wave
+constexpr uint32_t kApSlots = 2 * 256;          // workgroup slots of the chip (two per CU)
+#ifndef DREPHIP_AP_BAL_ROUNDS
+#define DREPHIP_AP_BAL_ROUNDS 2
+#endif
+constexpr uint32_t kApBalancedRounds = DREPHIP_AP_BAL_ROUNDS;   // balanced items per slot (small problems)
 constexpr uint32_t kMaxFam = 6;                 // cuckoo field families tried per table
 constexpr uint32_t kFamTwins = 0x40;            // k_build_q32 family byte: the row has two keys with one low word
 constexpr uint32_t kFamFailed = 0xFF;           // ... no family worked (the row's pairs are merged literally)
@@ -487,7 +491,7 @@ template <int R, int NCH, int MINW>
 __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
     const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ nhash,
     const uint32_t *__restrict__ blk, uint32_t stride, const uint8_t *__restrict__ fam, uint32_t s, uint32_t N,
-    uint32_t row0, uint32_t row1, uint32_t B, const uint2 *__restrict__ items, uint32_t ncol_item,
+    uint32_t row0, uint32_t row1, uint32_t B, const uint4 *__restrict__ items,
     uint16_t *__restrict__ common, uint16_t *__restrict__ denom, uint64_t seg0) {
     constexpr int WG = kApWG;
     extern __shared__ __align__(16) uint32_t lds[];    // 16-B aligned: slot words are read with ds_read_b128
@@ -498,7 +502,7 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
     const uint32_t c0 = items[blockIdx.x].y;
     if (i0 == 0xFFFFFFFFu) return;                      // idle padding item (make_items)
     const uint32_t nrows = min((uint32_t)R, row1 - i0);
-    const uint32_t cend = min(c0 + ncol_item, N);
+    const uint32_t cend = min(items[blockIdx.x].z, N);
     const uint32_t tid = threadIdx.x, wave = tid >> 6;
     {   // the row group's LDS image (k_build_q32): 16-byte loads, four in flight per lane
         const uint4 *src = (const uint4 *)(blk + (uint64_t)((i0 - row0) / R) * stride);
@@ -907,6 +911,48 @@ static std::vector<uint2> make_items(uint32_t row0, uint32_t row1, uint32_t N, u
     return items;
 }
 
+// Whole-row-table items for a problem too small to give every workgroup slot
+// several fixed-width tiles (N ~ 10^3, or one rank's rows of a sharded job):
+// each row group's columns (i0, N) are cut into pieces of about total / target
+// pairs, so the chip gets `target` items of equal work in one or two rounds --
+// one 80 KiB row image per item instead of one per 64- or 32-column tile, and
+// no tail of the triangle's short rows.  Items are sorted by column and dealt
+// to the XCDs in contiguous column slices (workgroup b runs on XCD b % 8).
+static std::vector<uint4> make_items_balanced(uint32_t row0, uint32_t row1, uint32_t N, uint32_t R,
+                                              uint32_t target) {
+    auto pairs_of = [&](uint32_t i0) {
+        uint64_t p = 0;
+        for (uint32_t r = i0; r < std::min(i0 + R, row1); r++) p += N - 1 - r;
+        return p;
+    };
+    uint64_t total = 0;
+    for (uint32_t i0 = row0; i0 < row1; i0 += R) total += pairs_of(i0);
+    const double per = std::max(1.0, (double)total / std::max(1u, target));
+    std::vector<uint4> raw;
+    for (uint32_t i0 = row0; i0 < row1; i0 += R) {
+        const uint32_t c_lo = i0 + 1, cols = N - c_lo;
+        if (!cols) continue;
+        uint32_t m = (uint32_t)std::max<int64_t>(1, std::llround((double)pairs_of(i0) / per));
+        m = std::min(m, cols);
+        for (uint32_t j = 0; j < m; j++)
+            raw.push_back(make_uint4(i0, c_lo + (uint32_t)((uint64_t)cols * j / m),
+                                     c_lo + (uint32_t)((uint64_t)cols * (j + 1) / m), 0));
+    }
+    std::stable_sort(raw.begin(), raw.end(), [](const uint4 &a, const uint4 &b) { return a.y < b.y; });
+    const size_t len = (raw.size() + kXcds - 1) / kXcds;
+    std::vector<uint4> items(len * kXcds, make_uint4(kIdleItem, 0, 0, 0));
+    for (size_t i = 0; i < raw.size(); i++) items[(i % len) * kXcds + i / len] = raw[i];
+    return items;
+}
+
+// Fixed-width tiles (make_items) as whole-row-table items {i0, c0, c0 + C}
+static std::vector<uint4> make_items_tiles(uint32_t row0, uint32_t row1, uint32_t N, uint32_t R, uint32_t C) {
+    const std::vector<uint2> t = make_items(row0, row1, N, R, C);
+    std::vector<uint4> items(t.size());
+    for (size_t i = 0; i < t.size(); i++) items[i] = make_uint4(t[i].x, t[i].y, t[i].y + C, 0);
+    return items;
+}
+
 static int launch_merge(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N,
                         uint64_t seg0, uint64_t npairs, uint16_t *d_common, uint16_t *d_denom,
                         hipStream_t st) {
@@ -969,14 +1015,14 @@ static int launch_band(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_
 template <int R, int NCH, int MINW>
 static int launch_q(drephip_ctx *ctx, uint32_t nitems, size_t lds, hipStream_t st, const uint64_t *h,
                     const uint32_t *nh, const uint32_t *blk, uint32_t stride, const uint8_t *fam, uint32_t N, uint32_t row0,
-                    uint32_t row1, uint32_t B, const uint2 *items, uint32_t C, uint16_t *cm, uint16_t *dn,
+                    uint32_t row1, uint32_t B, const uint4 *items, uint16_t *cm, uint16_t *dn,
                     uint64_t seg0) {
     HIPC(hipFuncSetAttribute((const void *)k_allpairs_q<R, NCH, MINW>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)lds));
     timing_mark(ctx, 2, st, true);
     for (uint32_t i0 = 0; i0 < nitems; i0 += (uint32_t)max_blocks(kApWG))
         hipLaunchKernelGGL((k_allpairs_q<R, NCH, MINW>), dim3(std::min<uint32_t>(nitems - i0, (uint32_t)max_blocks(kApWG))),
-                           dim3(kApWG), lds, st, h, nh, blk, stride, fam, ctx->s, N, row0, row1, B, items + i0, C, cm, dn,
+                           dim3(kApWG), lds, st, h, nh, blk, stride, fam, ctx->s, N, row0, row1, B, items + i0, cm, dn,
                            seg0);
     timing_mark(ctx, 2, st, false);
     HIPC(hipGetLastError());
@@ -1027,7 +1073,7 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
     const uint32_t stride = (uint32_t)((q_lds_bytes(R, TS, s) / 4 + 3) & ~3ull);   // words, 16-B multiple
     uint32_t *d_blk;
     uint8_t *d_fam;
-    uint2 *d_items;
+    uint4 *d_items;
     int rc;
     if ((rc = scratch(ctx, "ap_blk", (uint64_t)ngroups * stride * 4, (void **)&d_blk))) return rc;
     if ((rc = scratch(ctx, "ap_fam", (uint64_t)ngroups * R, (void **)&d_fam))) return rc;
@@ -1038,31 +1084,30 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
                        d_blk, stride, d_fam);
     timing_mark(ctx, 3, st, false);
     HIPC(hipGetLastError());
-    // column tile: the widest (<= kApCols) whose item count still gives every
-    // workgroup slot of the chip (256 CUs x 2) about four items; small
-    // problems (a rank's shard on 8 GPUs, N ~ 10^3) get narrower items
-    uint32_t C = kApCols;
-    auto nitems_for = [&](uint32_t c) {
-        uint64_t n = 0;
-        const uint32_t nct = (N + c - 1) / c;
-        for (uint32_t i0 = row0; i0 < row1; i0 += R) n += nct - (i0 + 1) / c;
-        return n;
-    };
-    while (C > kApMinCols && nitems_for(C) < 4ull * 2 * 256) C /= 2;
-    // the item list depends only on (N, rows, R, C): reused while the shape and
-    // the scratch allocation are unchanged (repeated calls: bench steps, shards).
-    // Its host copy lives in the context until the next list replaces it (the
-    // queued H2D copy may still be reading it when a deferred call returns).
-    const uint64_t key[5] = {N, row0, row1, R, C};
+    // items: 128-column tiles when that gives every workgroup slot of the chip
+    // (256 CUs x 2) at least four of them; smaller problems (N ~ 10^3, a rank's
+    // shard on 8 GPUs) get balanced variable-width items, kApBalancedRounds
+    // per slot
+    const uint32_t nct = (N + kApCols - 1) / kApCols;
+    uint64_t ntiles = 0;
+    for (uint32_t i0 = row0; i0 < row1; i0 += R) ntiles += nct - (i0 + 1) / kApCols;
+    const bool balanced = ntiles < 4ull * kApSlots;
+    // the item list depends only on (N, rows, R, mode): reused while the shape
+    // and the scratch allocation are unchanged (repeated calls: bench steps,
+    // shards).  Its host copy lives in the context until the next list replaces
+    // it (the queued H2D copy may still be reading it when a deferred call
+    // returns).
+    const uint64_t key[5] = {N, row0, row1, R, balanced ? 0u : kApCols};
     const bool reuse = ctx->ap_items_gen == ctx->alloc_gen && !memcmp(ctx->ap_items_key, key, sizeof(key));
     if (!reuse) {
-        ctx->ap_items_host = make_items(row0, row1, N, R, C);
+        ctx->ap_items_host = balanced ? make_items_balanced(row0, row1, N, R, kApBalancedRounds * kApSlots)
+                                      : make_items_tiles(row0, row1, N, R, kApCols);
         ctx->ap_items_gen = 0;
     }
     const uint32_t ni = (uint32_t)ctx->ap_items_host.size();
-    if ((rc = scratch(ctx, "ap_items", (uint64_t)ni * sizeof(uint2), (void **)&d_items))) return rc;
+    if ((rc = scratch(ctx, "ap_items", (uint64_t)ni * sizeof(uint4), (void **)&d_items))) return rc;
     if (!reuse) {
-        HIPC(hipMemcpyAsync(d_items, ctx->ap_items_host.data(), (uint64_t)ni * sizeof(uint2), hipMemcpyHostToDevice, st));
+        HIPC(hipMemcpyAsync(d_items, ctx->ap_items_host.data(), (uint64_t)ni * sizeof(uint4), hipMemcpyHostToDevice, st));
         memcpy(ctx->ap_items_key, key, sizeof(key));
         ctx->ap_items_gen = ctx->alloc_gen;
     }
@@ -1072,8 +1117,8 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
     const uint32_t nch = (s + 63) / 64;
     // two workgroups per CU when the LDS allows
     const bool two = lds <= 80 * 1024;
-#define DREPHIP_Q(RR, NC) (two ? launch_q<RR, NC, 8>(ctx, ni, lds, st, d_hashes, d_nhash, d_blk, stride, d_fam, N, row0, row1, B, d_items, C, d_common, d_denom, seg0) \
-                               : launch_q<RR, NC, 4>(ctx, ni, lds, st, d_hashes, d_nhash, d_blk, stride, d_fam, N, row0, row1, B, d_items, C, d_common, d_denom, seg0))
+#define DREPHIP_Q(RR, NC) (two ? launch_q<RR, NC, 8>(ctx, ni, lds, st, d_hashes, d_nhash, d_blk, stride, d_fam, N, row0, row1, B, d_items, d_common, d_denom, seg0) \
+                               : launch_q<RR, NC, 4>(ctx, ni, lds, st, d_hashes, d_nhash, d_blk, stride, d_fam, N, row0, row1, B, d_items, d_common, d_denom, seg0))
     if (nch <= 8) {
         switch (R) {
             case 8: rc = DREPHIP_Q(8, 8); break;

@@ -86,7 +86,7 @@ struct drephip_ctx {
     // (host copy kept: a deferred call's H2D copy of it may still be queued)
     uint64_t ap_items_key[5] = {0, 0, 0, 0, 0};
     uint64_t ap_items_gen = 0;
-    std::vector<uint2> ap_items_host;
+    std::vector<uint4> ap_items_host;
     // deferred sketch (drephip_sketch_device_async): the first round is queued
     // without reading its status back; drephip_sketch_wait checks it (and
     // reruns the call synchronously if a genome needs another threshold round).
