@@ -40,11 +40,8 @@ namespace drephip {
 
 constexpr int kApWG = 1024;                     // 16 waves per workgroup
 constexpr uint32_t kApCols = 128;               // columns per work item (fewer when the grid would not fill the chip)
+constexpr uint32_t kApMinCols = 16;             // one column per wave
 constexpr uint32_t kApSlots = 2 * 256;          // workgroup slots of the chip (two per CU)
-#ifndef DREPHIP_AP_BAL_ROUNDS
-#define DREPHIP_AP_BAL_ROUNDS 2
-#endif
-constexpr uint32_t kApBalancedRounds = DREPHIP_AP_BAL_ROUNDS;   // balanced items per slot (small problems)
 constexpr uint32_t kMaxFam = 6;                 // cuckoo field families tried per table
 constexpr uint32_t kFamTwins = 0x40;            // k_build_q32 family byte: the row has two keys with one low word
 constexpr uint32_t kFamFailed = 0xFF;           // ... no family worked (the row's pairs are merged literally)
@@ -911,40 +908,6 @@ static std::vector<uint2> make_items(uint32_t row0, uint32_t row1, uint32_t N, u
     return items;
 }
 
-// Whole-row-table items for a problem too small to give every workgroup slot
-// several fixed-width tiles (N ~ 10^3, or one rank's rows of a sharded job):
-// each row group's columns (i0, N) are cut into pieces of about total / target
-// pairs, so the chip gets `target` items of equal work in one or two rounds --
-// one 80 KiB row image per item instead of one per 64- or 32-column tile, and
-// no tail of the triangle's short rows.  Items are sorted by column and dealt
-// to the XCDs in contiguous column slices (workgroup b runs on XCD b % 8).
-static std::vector<uint4> make_items_balanced(uint32_t row0, uint32_t row1, uint32_t N, uint32_t R,
-                                              uint32_t target) {
-    auto pairs_of = [&](uint32_t i0) {
-        uint64_t p = 0;
-        for (uint32_t r = i0; r < std::min(i0 + R, row1); r++) p += N - 1 - r;
-        return p;
-    };
-    uint64_t total = 0;
-    for (uint32_t i0 = row0; i0 < row1; i0 += R) total += pairs_of(i0);
-    const double per = std::max(1.0, (double)total / std::max(1u, target));
-    std::vector<uint4> raw;
-    for (uint32_t i0 = row0; i0 < row1; i0 += R) {
-        const uint32_t c_lo = i0 + 1, cols = N - c_lo;
-        if (!cols) continue;
-        uint32_t m = (uint32_t)std::max<int64_t>(1, std::llround((double)pairs_of(i0) / per));
-        m = std::min(m, cols);
-        for (uint32_t j = 0; j < m; j++)
-            raw.push_back(make_uint4(i0, c_lo + (uint32_t)((uint64_t)cols * j / m),
-                                     c_lo + (uint32_t)((uint64_t)cols * (j + 1) / m), 0));
-    }
-    std::stable_sort(raw.begin(), raw.end(), [](const uint4 &a, const uint4 &b) { return a.y < b.y; });
-    const size_t len = (raw.size() + kXcds - 1) / kXcds;
-    std::vector<uint4> items(len * kXcds, make_uint4(kIdleItem, 0, 0, 0));
-    for (size_t i = 0; i < raw.size(); i++) items[(i % len) * kXcds + i / len] = raw[i];
-    return items;
-}
-
 // Fixed-width tiles (make_items) as whole-row-table items {i0, c0, c0 + C}
 static std::vector<uint4> make_items_tiles(uint32_t row0, uint32_t row1, uint32_t N, uint32_t R, uint32_t C) {
     const std::vector<uint2> t = make_items(row0, row1, N, R, C);
@@ -1084,24 +1047,27 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
                        d_blk, stride, d_fam);
     timing_mark(ctx, 3, st, false);
     HIPC(hipGetLastError());
-    // items: 128-column tiles when that gives every workgroup slot of the chip
-    // (256 CUs x 2) at least four of them; smaller problems (N ~ 10^3, a rank's
-    // shard on 8 GPUs) get balanced variable-width items, kApBalancedRounds
-    // per slot
-    const uint32_t nct = (N + kApCols - 1) / kApCols;
-    uint64_t ntiles = 0;
-    for (uint32_t i0 = row0; i0 < row1; i0 += R) ntiles += nct - (i0 + 1) / kApCols;
-    const bool balanced = ntiles < 4ull * kApSlots;
-    // the item list depends only on (N, rows, R, mode): reused while the shape
-    // and the scratch allocation are unchanged (repeated calls: bench steps,
-    // shards).  Its host copy lives in the context until the next list replaces
-    // it (the queued H2D copy may still be reading it when a deferred call
-    // returns).
-    const uint64_t key[5] = {N, row0, row1, R, balanced ? 0u : kApCols};
+    // column tile: the widest (<= kApCols) whose item count still gives every
+    // workgroup slot of the chip (256 CUs x 2) about four items; small
+    // problems (a rank's shard on 8 GPUs, N ~ 10^3) get narrower items.  (Items
+    // of equal pair count cut from each row group's whole column range -- one
+    // row image per workgroup slot -- measured 5-25 % slower at N = 1000.)
+    uint32_t C = kApCols;
+    auto nitems_for = [&](uint32_t c) {
+        uint64_t n = 0;
+        const uint32_t nct = (N + c - 1) / c;
+        for (uint32_t i0 = row0; i0 < row1; i0 += R) n += nct - (i0 + 1) / c;
+        return n;
+    };
+    while (C > kApMinCols && nitems_for(C) < 4ull * kApSlots) C /= 2;
+    // the item list depends only on (N, rows, R, C): reused while the shape and
+    // the scratch allocation are unchanged (repeated calls: bench steps, shards).
+    // Its host copy lives in the context until the next list replaces it (the
+    // queued H2D copy may still be reading it when a deferred call returns).
+    const uint64_t key[5] = {N, row0, row1, R, C};
     const bool reuse = ctx->ap_items_gen == ctx->alloc_gen && !memcmp(ctx->ap_items_key, key, sizeof(key));
     if (!reuse) {
-        ctx->ap_items_host = balanced ? make_items_balanced(row0, row1, N, R, kApBalancedRounds * kApSlots)
-                                      : make_items_tiles(row0, row1, N, R, kApCols);
+        ctx->ap_items_host = make_items_tiles(row0, row1, N, R, C);
         ctx->ap_items_gen = 0;
     }
     const uint32_t ni = (uint32_t)ctx->ap_items_host.size();
