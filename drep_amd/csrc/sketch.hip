@@ -71,11 +71,21 @@ __device__ __forceinline__ uint64_t add64(uint64_t a, uint64_t b) {   // one v_l
     asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(y) : "v"(a), "v"(b));
     return y;
 }
-// fmix64 without its last `k ^= k >> 33`, which only changes the low word
-__device__ __forceinline__ uint64_t fmix64_pre(uint64_t k) {
+// fmix64 up to its last multiply: q = ((k ^ k >> 33) C1) ^ (... >> 33); the
+// state before fmix64's final xorshift is then q C2 (fmix_mul)
+constexpr uint64_t kFmixC2 = 0xc4ceb9fe1a85ec53ULL;
+__device__ __forceinline__ uint64_t fmix64_q(uint64_t k) {
     k ^= k >> 33; k *= 0xff51afd7ed558ccdULL;
-    k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ULL;
+    k ^= k >> 33;
     return k;
+}
+__device__ __forceinline__ uint64_t fmix_mul(uint64_t q) { return q * kFmixC2; }
+// hi(q1 C2) + hi(q2 C2) + 1 (mod 2^32) with the multiplies shared:
+// hi(q C2) = hi(lo q lo C2) + lo q hi C2 + hi q lo C2
+__device__ __forceinline__ uint32_t prefilter_hi(uint64_t q1, uint64_t q2) {
+    const uint32_t a1 = (uint32_t)q1, b1 = (uint32_t)(q1 >> 32), a2 = (uint32_t)q2, b2 = (uint32_t)(q2 >> 32);
+    return __umulhi(a1, (uint32_t)kFmixC2) + __umulhi(a2, (uint32_t)kFmixC2) + (a1 + a2) * (uint32_t)(kFmixC2 >> 32) +
+           (b1 + b2) * (uint32_t)kFmixC2 + 1u;
 }
 // Candidates are staged in an LDS buffer (wave-aggregated LDS atomic) and only
 // flushed to the per-genome set after the tile, so the hot loop issues no
@@ -147,9 +157,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // one LDS vector 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 struct SketchTablesQ {
     u32x4 e1[256];        // {lo(TT1), hi(TT1) + (hi(A03 c1) << 31), hi(A03 c1), 0}  by bases 0-3
-    u32x4 e2[256];        // {lo(TT2), hi(TT2), hi(A03 c2), 0}                       by bases 8-11
+    u32x4 e2[256];        // {lo(TT2), hi(TT2), hi(A03 c2), hi(A03 c2) hi(2 c1)}     by bases 8-11
     u32x2 b1[256];        // {A47 lo(c1), A47 lo(c1) << 31}                         by bases 4-7
-    uint32_t b2[256];     // A47 lo(c2)                                              by bases 12-15
+    u32x2 b2[256];        // {A47 lo(c2), A47 lo(c2) hi(2 c1)}                      by bases 12-15
     uint64_t t3[1024];    // tail, by bases 16-20
 };
 
@@ -168,10 +178,12 @@ __device__ void build_tables(SketchTablesQ &tb, uint32_t tid, uint32_t nthreads)
         const uint64_t t1 = ((uint64_t)x1 << 31) * c2 + ((uint64_t)(ta1 << 31) << 32);
         const uint64_t t2 = ((uint64_t)(x2 & 0x7fffffffu) << 33) * c1 + (uint64_t)(x2 >> 31) * c1;
         tb.e1[x] = u32x4{(uint32_t)t1, (uint32_t)(t1 >> 32), ta1, 0u};
-        tb.e2[x] = u32x4{(uint32_t)t2, (uint32_t)(t2 >> 32), ta2, 0u};
+        constexpr uint32_t d1hi = (uint32_t)((c1 * 2) >> 32);
+        tb.e2[x] = u32x4{(uint32_t)t2, (uint32_t)(t2 >> 32), ta2, ta2 * d1hi};
         const uint32_t m1 = a * (uint32_t)c1;
         tb.b1[x] = u32x2{m1, m1 << 31};
-        tb.b2[x] = a * (uint32_t)c2;
+        const uint32_t m2 = a * (uint32_t)c2;
+        tb.b2[x] = u32x2{m2, m2 * d1hi};
     }
     for (uint32_t y = tid; y < 1024; y += nthreads) {
         // bases 16..19 = bits 9..2, base 20 = bits 1..0
@@ -205,23 +217,25 @@ __device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) { 
 }
 
 // Murmur h1 of the canonical k-mer (top-aligned codes hi:lo), returned as the
-// two fmix64 states before their final xorshift: h1 = fin(p1) + fin(p2) with
-// fin(k) = k ^ (k >> 33).  fin leaves the high word unchanged, so
+// two fmix64 states q1, q2 before their last multiply: with p = q C2,
+// h1 = fin(p1) + fin(p2), fin(k) = k ^ (k >> 33).  fin leaves the high word
+// unchanged, so
 //     h1 <= T  implies  hi(p1) + hi(p2) + 1  <=  hi(T) + 1   (mod 2^32)
 // (the low-word sum carries at most 1 into the high word; both sides are
-// taken one past so a wrapping 0xFFFFFFFF + carry = 0 is kept): a one-add,
-// one-compare prefilter; the exact test runs in the rare admit branch.
+// taken one past so a wrapping 0xFFFFFFFF + carry = 0 is kept): the prefilter
+// (prefilter_hi, the two high words with shared multiplies, and a compare);
+// the exact test runs in the rare admit branch.
 __device__ __forceinline__ void murmur21_q(const SketchTablesQ &tb, uint32_t hi, uint32_t lo, uint32_t seed,
-                                           uint64_t &p1, uint64_t &p2) {
+                                           uint64_t &q1, uint64_t &q2) {
     constexpr uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
     constexpr uint64_t d1 = c1 * 2;                                  // 2 c1 mod 2^64
     const u32x4 e1 = tb.e1[hi >> 24];
     const u32x2 f1 = tb.b1[(hi >> 16) & 0xffu];
     const u32x4 e2 = tb.e2[(hi >> 8) & 0xffu];
-    const uint32_t f2 = tb.b2[hi & 0xffu];
+    const u32x2 f2 = tb.b2[hi & 0xffu];
     const uint64_t k3 = tb.t3[lo >> 22];
     const uint32_t X1 = e1.z + f1.x;                                 // hi(k1 * c1)
-    const uint32_t X2 = e2.z + f2;                                   // hi(k2 * c2)
+    const uint32_t X2 = e2.z + f2.x;                                 // hi(k2 * c2)
     const uint64_t tt1 = ((uint64_t)e1.y << 32) | e1.x;
     const uint64_t tt2 = ((uint64_t)e2.y << 32) | e2.x;
     // rotl(k1 c1, 31) c2 ^ seed  (its (X1 << 31) term: in e1.y and f1.y)
@@ -232,17 +246,20 @@ __device__ __forceinline__ void murmur21_q(const SketchTablesQ &tb, uint32_t hi,
     h1 = x5_plus(rotl64_ab(h1, 27), 5ull * seed + 0x52dce729);   // (rotl + seed) * 5 + c
     // rotl(k2 c2, 33) c1 ^ seed
     const uint64_t P2 = mad64(X2, (uint32_t)d1, tt2);
-    const uint32_t g2hi = (uint32_t)(P2 >> 32) + X2 * (uint32_t)(d1 >> 32);
+    // X2 hi(d1) = e2.z hi(d1) + f2.x hi(d1) (mod 2^32): both products are table
+    // entries, one add instead of a move and a multiply
+    const uint32_t g2hi = (uint32_t)(P2 >> 32) + e2.w + f2.y;
     uint64_t h2 = ((uint64_t)g2hi << 32) | ((uint32_t)P2 ^ seed);
     h2 = x5_plus(add64(rotl64_ab(h2, 31), h1), 0x38495ab5);
     h1 ^= k3;
     h2 ^= 21u;
     h1 = add64(h1, h2);
     h2 = add64(h2, h1);
-    p1 = fmix64_pre(h1);
-    p2 = fmix64_pre(h2);
+    q1 = fmix64_q(h1);
+    q2 = fmix64_q(h2);
 }
-__device__ __forceinline__ uint64_t murmur_fin(uint64_t p1, uint64_t p2) {
+__device__ __forceinline__ uint64_t murmur_fin(uint64_t q1, uint64_t q2) {
+    const uint64_t p1 = fmix_mul(q1), p2 = fmix_mul(q2);
     return add64(p1 ^ (p1 >> 33), p2 ^ (p2 >> 33));
 }
 
@@ -331,7 +348,7 @@ __global__ __launch_bounds__(kTile / LANE, DREPHIP_SK_MINW) void k_sketch_hash21
                 const uint64_t rc = ((uint64_t)chi << 32) | clo;
                 const uint64_t cc = fw <= rc ? fw : rc;
                 murmur21_q(tb, (uint32_t)(cc >> 32), (uint32_t)cc, seed, p1[b], p2[b]);
-                hit |= (uint32_t)(p1[b] >> 32) + (uint32_t)(p2[b] >> 32) + 1u <= Tp;
+                hit |= prefilter_hi(p1[b], p2[b]) <= Tp;
             }
             if (__builtin_expect(hit, 0)) {
                 const uint64_t ok = run21(vhist);
