@@ -301,10 +301,17 @@ __global__ __launch_bounds__(kTile / LANE, DREPHIP_SK_MINW) void k_sketch_hash21
         for (uint32_t i = threadIdx.x; i < kTabVec; i += WG) dst[i] = src[i];
     }
 
-    const uint64_t m0 = start / 16;                  // code word of the lane's first window end
-    auto ld = [&](int j) -> uint32_t {               // clamp: the cut after the last word is junk
-        const uint64_t w = m0 + j;
-        return codes[w < wlast ? w : wlast];
+    // code words through a per-workgroup buffer resource based two words before
+    // the tile: the lane's word offset is a fixed VGPR, the word index an
+    // immediate or SGPR, and words past wlast read 0 (buffer bounds) -- junk
+    // either way, every k-mer touching them is invalid
+    const uint64_t w0 = tile_base[t] / 16 - 2;       // >= 0: genomes start at tile 1
+    const uint64_t nrec = (wlast + 1 - w0) * 4;
+    const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(codes + w0), (short)0, (int)(nrec < 0xFFFFFFF0ull ? nrec : 0xFFFFFFF0ull), 0x00020000);
+    const uint32_t lane_off = threadIdx.x * (LANE / 16) * 4;
+    auto ld = [&](int j) -> uint32_t {               // word m0 + j, m0 = the lane's first window end / 16
+        return __builtin_amdgcn_raw_buffer_load_b32(crs, lane_off, (uint32_t)__builtin_amdgcn_readfirstlane(j + 2) * 4u, 0);
     };
     // registers: F words m-2..m (complemented), R words m-2..m+1
     uint32_t nf0 = ~ld(-2), nf1 = ~ld(-1), nf2 = ~ld(0);
@@ -317,7 +324,13 @@ __global__ __launch_bounds__(kTile / LANE, DREPHIP_SK_MINW) void k_sketch_hash21
     uint32_t vcur = vw[1];
     __syncthreads();
 
-#pragma unroll 1
+    // fully unrolled (NCH = 4 chunks of 16 window ends): the code-word
+    // registers rotate by renaming and every load is issued up front.  Rolled,
+    // the compiler copied the rotating words at the back edge behind a wait
+    // for the chunk's own load (7.84 vs 8.00 ms).  The count is explicit: a
+    // bare `#pragma unroll` produced different, slower code (8.09 ms)
+    static_assert(NCH == 4, "unroll count");
+#pragma unroll 4
     for (int wi = 0; wi < NCH; wi++) {
         const uint32_t vbits = (vcur >> ((wi & 1) * 16)) & 0xffffu;
         if (wi + 1 < NCH && (wi & 1)) vcur = vw[2 + (wi >> 1)];
@@ -351,11 +364,14 @@ __global__ __launch_bounds__(kTile / LANE, DREPHIP_SK_MINW) void k_sketch_hash21
                 hit |= prefilter_hi(p1[b], p2[b]) <= Tp;
             }
             if (__builtin_expect(hit, 0)) {
-                const uint64_t ok = run21(vhist);
 #pragma unroll
                 for (int b = 0; b < BATCH; b++) {
                     const uint64_t h = murmur_fin(p1[b], p2[b]);
-                    if (h <= T && ((ok >> (48 + b0 + b)) & 1)) {
+                    // the 21 bases ending at history bit 48 + r are all valid
+                    // (per k-mer, here: a shared run mask over the whole chunk
+                    // was hoisted out of this rare branch into every chunk)
+                    const bool ok = (~(uint32_t)(vhist >> (28 + b0 + b)) & 0x1FFFFFu) == 0;
+                    if (h <= T && ok) {
                         const uint32_t slot = atomicAdd(&nstage, 1u);
                         if (slot < kStage) stage[slot] = h;
                         else set_insert(S, mask, C, limit, h);
