@@ -96,15 +96,6 @@ __device__ __forceinline__ uint32_t prefilter_hi(uint64_t q1, uint64_t q2) {
 #endif
 constexpr uint32_t kStage = DREPHIP_SK_STAGE;
 
-// bit i of the result: the 21 bases ending at history bit i are all valid
-__device__ __forceinline__ uint64_t run21(uint64_t v) {
-    const uint64_t r2 = v & (v << 1);
-    const uint64_t r4 = r2 & (r2 << 2);
-    const uint64_t r8 = r4 & (r4 << 4);
-    const uint64_t r16 = r8 & (r8 << 8);
-    return r16 & (r4 << 16) & (v << 20);
-}
-
 // ------------------------------------------------------------- hash kernel
 // One workgroup of kTile / LANE lanes per 32768-base tile; lane l owns the
 // LANE window ends [tile + LANE l, tile + LANE (l + 1)).  No per-base rolling state: the

@@ -17,7 +17,7 @@ ST = torch.cuda.current_stream().cuda_stream
 tile = _lib.tile_bases(); P = _lib.padded_bases([L]); tot = tile + N * P
 codes = torch.zeros(tot // 16, dtype=torch.int32, device="cuda")
 valid = torch.zeros(tot // 32, dtype=torch.int32, device="cuda")
-ctx.synth_device(7, 0, N, 100, L, codes.data_ptr(), valid.data_ptr(), ST)
+ctx.synth_device(7, 0, N, int(os.environ.get("AP_FAM", 100)), L, codes.data_ptr(), valid.data_ptr(), ST)
 h = torch.full((N, s), -1, dtype=torch.int64, device="cuda"); n = torch.zeros(N, dtype=torch.int32, device="cuda")
 off = np.array([tile + i * P for i in range(N)], np.uint64)
 ctx.sketch_device(codes.data_ptr(), valid.data_ptr(), off, np.full(N, P, np.uint64), np.full(N, L - 20, np.uint64), N, h.data_ptr(), n.data_ptr(), ST)
