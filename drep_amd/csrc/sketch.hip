@@ -255,7 +255,7 @@ __device__ __forceinline__ uint64_t murmur_fin(uint64_t q1, uint64_t q2) {
 }
 
 #ifndef DREPHIP_SK_BATCH
-#define DREPHIP_SK_BATCH 4          // k-mers per admit test: 50 VGPRs, 8 waves per SIMD (8: 70 VGPRs, 7 waves; 0.2-0.3 % slower)
+#define DREPHIP_SK_BATCH 2          // k-mers per admit test: 52 VGPRs (4: 58, 0.8 % slower; 8: 73, 7 waves, 2 % slower)
 #endif
 #ifndef DREPHIP_SK_MINW
 #define DREPHIP_SK_MINW 1

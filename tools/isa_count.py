@@ -12,7 +12,7 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # variant: (mangled-name pattern, k-mers/block)
-KERNELS = {"default": ("k_sketch_hash21ILi64ELi4E", 4)}
+KERNELS = {"default": ("k_sketch_hash21ILi64ELi2E", 2)}
 
 
 def main():
@@ -46,7 +46,7 @@ def main():
             for k, v in b.items():
                 if k.startswith("v_"):
                     mix[k] += v
-        label = {"default": "k_sketch_hash21<64,4>"}.get(var, name)
+        label = {"default": "k_sketch_hash21<64,2>"}.get(var, name)
         out["variants"][var] = {
             "kernel": label, "kmers_per_block": per, "blocks": len(hot),
             "valu_per_kmer": sum(valu) / len(hot) / per,
