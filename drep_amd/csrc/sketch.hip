@@ -216,15 +216,19 @@ __device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) { 
 // taken one past so a wrapping 0xFFFFFFFF + carry = 0 is kept): the prefilter
 // (prefilter_hi, the two high words with shared multiplies, and a compare);
 // the exact test runs in the rare admit branch.
-__device__ __forceinline__ void murmur21_q(const SketchTablesQ &tb, uint32_t hi, uint32_t lo, uint32_t seed,
-                                           uint64_t &q1, uint64_t &q2) {
+// the five table entries of one k-mer
+struct MEnt { u32x4 e1; u32x2 f1; u32x4 e2; u32x2 f2; uint64_t k3; };
+__device__ __forceinline__ MEnt fetch_ent(const SketchTablesQ &tb, uint32_t hi, uint32_t lo) {
+    return MEnt{tb.e1[hi >> 24], tb.b1[(hi >> 16) & 0xffu], tb.e2[(hi >> 8) & 0xffu], tb.b2[hi & 0xffu], tb.t3[lo >> 22]};
+}
+__device__ __forceinline__ void murmur21_ent(const MEnt &E, uint32_t seed, uint64_t &q1, uint64_t &q2) {
     constexpr uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
     constexpr uint64_t d1 = c1 * 2;                                  // 2 c1 mod 2^64
-    const u32x4 e1 = tb.e1[hi >> 24];
-    const u32x2 f1 = tb.b1[(hi >> 16) & 0xffu];
-    const u32x4 e2 = tb.e2[(hi >> 8) & 0xffu];
-    const u32x2 f2 = tb.b2[hi & 0xffu];
-    const uint64_t k3 = tb.t3[lo >> 22];
+    const u32x4 e1 = E.e1;
+    const u32x2 f1 = E.f1;
+    const u32x4 e2 = E.e2;
+    const u32x2 f2 = E.f2;
+    const uint64_t k3 = E.k3;
     const uint32_t X1 = e1.z + f1.x;                                 // hi(k1 * c1)
     const uint32_t X2 = e2.z + f2.x;                                 // hi(k2 * c2)
     const uint64_t tt1 = ((uint64_t)e1.y << 32) | e1.x;
@@ -248,6 +252,10 @@ __device__ __forceinline__ void murmur21_q(const SketchTablesQ &tb, uint32_t hi,
     h2 = add64(h2, h1);
     q1 = fmix64_q(h1);
     q2 = fmix64_q(h2);
+}
+__device__ __forceinline__ void murmur21_q(const SketchTablesQ &tb, uint32_t hi, uint32_t lo, uint32_t seed,
+                                           uint64_t &q1, uint64_t &q2) {
+    murmur21_ent(fetch_ent(tb, hi, lo), seed, q1, q2);
 }
 __device__ __forceinline__ uint64_t murmur_fin(uint64_t q1, uint64_t q2) {
     const uint64_t p1 = fmix_mul(q1), p2 = fmix_mul(q2);
@@ -326,31 +334,34 @@ __global__ __launch_bounds__(kTile / LANE, DREPHIP_SK_MINW) void k_sketch_hash21
         const uint32_t vbits = (vcur >> ((wi & 1) * 16)) & 0xffffu;
         if (wi + 1 < NCH && (wi & 1)) vcur = vw[2 + (wi >> 1)];
         vhist = (vhist >> 16) | ((uint64_t)vbits << 48);
+        // canonical k-mer (top-aligned codes) of window end q = 16m + r
+        auto canon = [&](int r) -> uint64_t {
+            uint32_t chi, clo, fhi, flo;
+            if (r == 15) { chi = nf2; clo = nf1; }
+            else {
+                chi = __builtin_amdgcn_alignbit(nf2, nf1, 2 * (r + 1));
+                clo = __builtin_amdgcn_alignbit(nf1, nf0, 2 * (r + 1));
+            }
+            if (r < 4) {                             // k-mer starts in word m-2 at field r+12
+                fhi = __builtin_amdgcn_alignbit(r0, r1, 32 - 2 * (r + 12));
+                flo = __builtin_amdgcn_alignbit(r1, r2, 32 - 2 * (r + 12));
+            } else if (r == 4) {
+                fhi = r1; flo = r2;
+            } else {                                 // starts in word m-1 at field r-4
+                fhi = __builtin_amdgcn_alignbit(r1, r2, 32 - 2 * (r - 4));
+                flo = __builtin_amdgcn_alignbit(r2, r3, 32 - 2 * (r - 4));
+            }
+            const uint64_t fw = ((uint64_t)fhi << 32) | flo;
+            const uint64_t rc = ((uint64_t)chi << 32) | clo;
+            return fw <= rc ? fw : rc;
+        };
 #pragma unroll
         for (int b0 = 0; b0 < 16; b0 += BATCH) {
             uint64_t p1[BATCH], p2[BATCH];
             bool hit = false;
 #pragma unroll
             for (int b = 0; b < BATCH; b++) {
-                const int r = b0 + b;                // window end q = 16m + r
-                uint32_t chi, clo, fhi, flo;
-                if (r == 15) { chi = nf2; clo = nf1; }
-                else {
-                    chi = __builtin_amdgcn_alignbit(nf2, nf1, 2 * (r + 1));
-                    clo = __builtin_amdgcn_alignbit(nf1, nf0, 2 * (r + 1));
-                }
-                if (r < 4) {                         // k-mer starts in word m-2 at field r+12
-                    fhi = __builtin_amdgcn_alignbit(r0, r1, 32 - 2 * (r + 12));
-                    flo = __builtin_amdgcn_alignbit(r1, r2, 32 - 2 * (r + 12));
-                } else if (r == 4) {
-                    fhi = r1; flo = r2;
-                } else {                             // starts in word m-1 at field r-4
-                    fhi = __builtin_amdgcn_alignbit(r1, r2, 32 - 2 * (r - 4));
-                    flo = __builtin_amdgcn_alignbit(r2, r3, 32 - 2 * (r - 4));
-                }
-                const uint64_t fw = ((uint64_t)fhi << 32) | flo;
-                const uint64_t rc = ((uint64_t)chi << 32) | clo;
-                const uint64_t cc = fw <= rc ? fw : rc;
+                const uint64_t cc = canon(b0 + b);
                 murmur21_q(tb, (uint32_t)(cc >> 32), (uint32_t)cc, seed, p1[b], p2[b]);
                 hit |= prefilter_hi(p1[b], p2[b]) <= Tp;
             }
