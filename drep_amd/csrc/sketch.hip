@@ -27,6 +27,7 @@
 #include "../../include/drephip.h"
 
 #include <algorithm>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -188,6 +189,7 @@ __device__ void build_tables(SketchTablesQ &tb, uint32_t tid, uint32_t nthreads)
 // copies into LDS with 16-byte loads (~5 per lane, L2-resident) instead of
 // recomputing ~1,300 entries (the build cost ~1.2 VALU instructions per k-mer).
 constexpr uint32_t kTabVec = sizeof(SketchTablesQ) / 16;
+constexpr uint32_t kSketchTabShifts = 4u | (3u << 8);     // log2 of the 16- and 8-byte entry sizes (fetch_ent)
 static_assert(sizeof(SketchTablesQ) % 16 == 0, "table image is copied in 16-byte pieces");
 __global__ __launch_bounds__(256) void k_sketch_tables(SketchTablesQ *__restrict__ img) {
     __shared__ SketchTablesQ tb;
@@ -218,8 +220,18 @@ __device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) { 
 // the exact test runs in the rare admit branch.
 // the five table entries of one k-mer
 struct MEnt { u32x4 e1; u32x2 f1; u32x4 e2; u32x2 f2; uint64_t k3; };
-__device__ __forceinline__ MEnt fetch_ent(const SketchTablesQ &tb, uint32_t hi, uint32_t lo) {
-    return MEnt{tb.e1[hi >> 24], tb.b1[(hi >> 16) & 0xffu], tb.e2[(hi >> 8) & 0xffu], tb.b2[hi & 0xffu], tb.t3[lo >> 22]};
+// Table addresses are byte index << entry size.  The shift amounts come in
+// as kernel arguments (sh = 4 | 3 << 8, held in SGPRs): with literal shifts the
+// compiler rematerialised 4 and 3 into VGPRs for the byte-select shifts of
+// every k-mer (two v_mov_b32 each)
+__device__ __forceinline__ MEnt fetch_ent(const SketchTablesQ &tb, uint32_t hi, uint32_t lo, uint32_t sh) {
+    const char *base = (const char *)&tb;
+    const uint32_t s16 = sh & 0xffu, s8 = sh >> 8;
+    return MEnt{*(const u32x4 *)(base + ((hi >> 24) << s16)),
+                *(const u32x2 *)(base + offsetof(SketchTablesQ, b1) + (((hi >> 16) & 0xffu) << s8)),
+                *(const u32x4 *)(base + offsetof(SketchTablesQ, e2) + (((hi >> 8) & 0xffu) << s16)),
+                *(const u32x2 *)(base + offsetof(SketchTablesQ, b2) + ((hi & 0xffu) << s8)),
+                tb.t3[lo >> 22]};
 }
 __device__ __forceinline__ void murmur21_ent(const MEnt &E, uint32_t seed, uint64_t &q1, uint64_t &q2) {
     constexpr uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
@@ -254,8 +266,8 @@ __device__ __forceinline__ void murmur21_ent(const MEnt &E, uint32_t seed, uint6
     q2 = fmix64_q(h2);
 }
 __device__ __forceinline__ void murmur21_q(const SketchTablesQ &tb, uint32_t hi, uint32_t lo, uint32_t seed,
-                                           uint64_t &q1, uint64_t &q2) {
-    murmur21_ent(fetch_ent(tb, hi, lo), seed, q1, q2);
+                                           uint32_t sh, uint64_t &q1, uint64_t &q2) {
+    murmur21_ent(fetch_ent(tb, hi, lo, sh), seed, q1, q2);
 }
 __device__ __forceinline__ uint64_t murmur_fin(uint64_t q1, uint64_t q2) {
     const uint64_t p1 = fmix_mul(q1), p2 = fmix_mul(q2);
@@ -278,7 +290,7 @@ __global__ __launch_bounds__(kTile / LANE, DREPHIP_SK_MINW) void k_sketch_hash21
     const SketchTablesQ *__restrict__ img, const uint32_t *__restrict__ codes, const uint32_t *__restrict__ valid,
     const uint64_t *__restrict__ tile_base, const uint32_t *__restrict__ tile_genome,
     const uint64_t *__restrict__ thr, unsigned long long *__restrict__ sets,
-    uint32_t *__restrict__ cnt, uint32_t set_log2, uint32_t limit, uint32_t seed, uint64_t wlast) {
+    uint32_t *__restrict__ cnt, uint32_t set_log2, uint32_t limit, uint32_t seed, uint64_t wlast, uint32_t sh) {
     constexpr uint32_t WG = kTile / LANE;
     constexpr int NCH = LANE / 16;
     __shared__ SketchTablesQ tb;
@@ -362,7 +374,7 @@ __global__ __launch_bounds__(kTile / LANE, DREPHIP_SK_MINW) void k_sketch_hash21
 #pragma unroll
             for (int b = 0; b < BATCH; b++) {
                 const uint64_t cc = canon(b0 + b);
-                murmur21_q(tb, (uint32_t)(cc >> 32), (uint32_t)cc, seed, p1[b], p2[b]);
+                murmur21_q(tb, (uint32_t)(cc >> 32), (uint32_t)cc, seed, sh, p1[b], p2[b]);
                 hit |= prefilter_hi(p1[b], p2[b]) <= Tp;
             }
             if (__builtin_expect(hit, 0)) {
@@ -685,7 +697,7 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
                 const uint32_t *tbg = tb_tiles_g + t0;
                 hipLaunchKernelGGL((k_sketch_hash21<kHashLane, DREPHIP_SK_BATCH>), dim3(ntc), dim3(kTile / kHashLane), 0, st,
                                    d_img, d_codes, d_valid, tbb, tbg, thr_p, d_sets, d_cnt, plan.set_log2, limit,
-                                   ctx->seed, wlast);
+                                   ctx->seed, wlast, kSketchTabShifts);
             }
             timing_mark(ctx, 0, st, false);
         }

@@ -3,7 +3,7 @@
 # bench: sketch hash kernel time and step time, interleaved runs.
 cd ${GRAFT_REPO_ROOT:-.}
 mkdir -p gpurun_out/ab
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
   for v in ${AB_LIBS}; do
     DREPHIP_LIB=$PWD/drep_amd/lib_ab/$v/libdrephip.so timeout -k 10 120 python bench.py --steps 20 --warmup 3 --cpu-baseline 0 ${BENCH_ARGS} \
         > gpurun_out/ab/$v.$rep.json 2> gpurun_out/ab/$v.$rep.err || { echo "$v failed"; tail -5 gpurun_out/ab/$v.$rep.err; exit 1; }
