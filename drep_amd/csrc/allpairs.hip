@@ -501,33 +501,50 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
     const uint32_t nrows = min((uint32_t)R, row1 - i0);
     const uint32_t cend = min(items[blockIdx.x].z, N);
     const uint32_t tid = threadIdx.x, wave = tid >> 6;
-    {   // the row group's LDS image (k_build_q32): 16-byte loads, four in flight per lane
+    {   // the row group's LDS image (k_build_q32) by LDS-DMA: wave w copies the
+        // 1 KiB pieces w, w + 16, ... (global_load_lds_dwordx4 writes a piece
+        // lane-linearly); every load is in flight at once, no VGPR round trip,
+        // and the per-row loads below overlap it.  Drained by the barrier.
         const uint4 *src = (const uint4 *)(blk + (uint64_t)((i0 - row0) / R) * stride);
-        uint4 *dst = (uint4 *)lds;
-        const uint32_t n16 = stride / 4;
-        uint32_t i = tid;
-        for (; i + 3 * WG < n16; i += 4 * WG) {
-            const uint4 a = src[i], b = src[i + WG], c = src[i + 2 * WG], d = src[i + 3 * WG];
-            dst[i] = a; dst[i + WG] = b; dst[i + 2 * WG] = c; dst[i + 3 * WG] = d;
+        const uint32_t n16 = stride / 4, lane = tid & 63;
+        for (uint32_t p = wave * 64; p < n16; p += WG) {
+            if (p + lane < n16)
+                __builtin_amdgcn_global_load_lds((const void *)(src + p + lane),
+                                                 (__attribute__((address_space(3))) void *)(
+                                                     (__attribute__((address_space(3))) uint4 *)lds + p),
+                                                 16, 0, 0);
         }
-        for (; i < n16; i += WG) dst[i] = src[i];
     }
     uint32_t nA[R], o1[R], o2[R];
     uint64_t alast[R];
     uint32_t failmask = 0;
     bool any_partial_row = false, fast = true;
+    {   // per-row scalars: uniform loads with clamped rows, no branches, so none
+        // of them waits on the image's DMA above (the family bytes as one
+        // aligned 8-byte word; the fam buffer is padded to 8 bytes)
+        const uint32_t fi = i0 - row0;
+        const uint64_t fw = *(const uint64_t *)(fam + (fi & ~7u));
+        uint32_t nraw[R];
+        uint64_t lraw[R];
 #pragma unroll
-    for (int r = 0; r < R; r++) {
-        const bool ok = (uint32_t)r < nrows;
-        nA[r] = ok ? nhash[i0 + r] : s;
-        uint32_t f = ok ? fam[i0 - row0 + r] : 0;
-        failmask |= (uint32_t)(f == kFamFailed) << r;   // no field family worked: merged literally below
-        f = f == kFamFailed ? 0 : f;
-        fast &= f == 0;                                  // family 0 and no twins (kFamTwins)
-        const QFields q = qfields(f & ~kFamTwins);
-        o1[r] = q.o1; o2[r] = q.o2;
-        alast[r] = (ok && nA[r] >= s) ? hashes[(uint64_t)(i0 + r) * s + s - 1] : kEmpty;
-        any_partial_row |= nA[r] < s;
+        for (int r = 0; r < R; r++) {
+            const uint32_t i = min(i0 + (uint32_t)r, row1 - 1);
+            nraw[r] = nhash[i];
+            lraw[r] = hashes[(uint64_t)i * s + s - 1];
+        }
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const bool ok = (uint32_t)r < nrows;
+            nA[r] = ok ? nraw[r] : s;
+            uint32_t f = ok ? (uint32_t)(fw >> (((fi & 7u) + (uint32_t)r) * 8)) & 0xFFu : 0;
+            failmask |= (uint32_t)(f == kFamFailed) << r;   // no field family worked: merged literally below
+            f = f == kFamFailed ? 0 : f;
+            fast &= f == 0;                                  // family 0 and no twins (kFamTwins)
+            const QFields q = qfields(f & ~kFamTwins);
+            o1[r] = q.o1; o2[r] = q.o2;
+            alast[r] = (ok && nA[r] >= s) ? lraw[r] : kEmpty;
+            any_partial_row |= nA[r] < s;
+        }
     }
     __syncthreads();
     // NCH = 16 means 512 < s <= 1024, i.e. H = 2048 (B = 11) for every such s.
@@ -1039,7 +1056,7 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
     uint4 *d_items;
     int rc;
     if ((rc = scratch(ctx, "ap_blk", (uint64_t)ngroups * stride * 4, (void **)&d_blk))) return rc;
-    if ((rc = scratch(ctx, "ap_fam", (uint64_t)ngroups * R, (void **)&d_fam))) return rc;
+    if ((rc = scratch(ctx, "ap_fam", ((uint64_t)ngroups * R + 7) & ~7ull, (void **)&d_fam))) return rc;
     const size_t blds = (size_t)TS * 4;
     HIPC(hipFuncSetAttribute((const void *)k_build_q32, hipFuncAttributeMaxDynamicSharedMemorySize, (int)blds));
     timing_mark(ctx, 3, st, true);
