@@ -17,6 +17,8 @@ __global__ __launch_bounds__(256) void mb(uint32_t *out, int iters, uint32_t c, 
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0) :: "memory");
     uint32_t a[CHAINS];
     uint64_t b[CHAINS];
+    uint32_t tmp;
+    const uint64_t smask = 0x5555555555555555ull ^ c;
     for (int j = 0; j < CHAINS; j++) { a[j] = threadIdx.x * 7 + j; b[j] = ((uint64_t)a[j] << 32) | (a[j] * 3); }
     for (int i = 0; i < iters; i++) {
 #pragma unroll
@@ -45,6 +47,22 @@ __global__ __launch_bounds__(256) void mb(uint32_t *out, int iters, uint32_t c, 
             if constexpr (OP == 20) asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(a[j]) : "v"(c));
             if constexpr (OP == 21) asm volatile("v_add_f32_e32 %0, %1, %0" : "+v"(a[j]) : "v"(c));
             if constexpr (OP == 22) asm volatile("v_pk_fma_f32 %0, %0, %1, %1" : "+v"(b[j]) : "v"(b[(j + 1) % CHAINS]));
+            // the mask in an SGPR pair instead of VCC
+            if constexpr (OP == 23) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a[j]) : "v"(c), "s"(smask));
+            // the canonical-k-mer select as the sketch kernel emits it: a 64-bit
+            // compare into VCC and two selects reading it (3 instructions)
+            if constexpr (OP == 24)
+                asm volatile("v_cmp_lt_u64_e32 vcc, %0, %1\n\tv_cndmask_b32_e32 %2, %3, %2, vcc\n\tv_cndmask_b32_e32 %4, %5, %4, vcc"
+                             : "+v"(b[j]), "+v"(b[(j + 1) % CHAINS]), "+v"(a[j]), "+v"(a[(j + 1) % CHAINS]),
+                               "+v"(a[(j + 2) % CHAINS]), "+v"(a[(j + 3) % CHAINS]) :: "vcc");
+            // the same select through the borrow of a 64-bit subtract and two
+            // bitop3 (5 instructions, the mask in a VGPR)
+            if constexpr (OP == 25)
+                asm volatile("v_sub_co_u32 %4, vcc, %0, %1\n\tv_subb_co_u32 %4, vcc, %2, %3, vcc\n\t"
+                             "v_subbrev_co_u32 %4, vcc, 0, 0, vcc\n\t"
+                             "v_bitop3_b32 %0, %1, %0, %4 bitop3:0xca\n\tv_bitop3_b32 %2, %3, %2, %4 bitop3:0xca"
+                             : "+v"(a[j]), "+v"(a[(j + 1) % CHAINS]), "+v"(a[(j + 2) % CHAINS]), "+v"(a[(j + 3) % CHAINS]),
+                               "=&v"(tmp) :: "vcc");
         }
     }
     uint32_t s = 0;
@@ -59,7 +77,8 @@ static const char *names[] = {"v_xor_b32", "v_mul_lo_u32", "v_mul_hi_u32", "v_ma
                               "v_lshl_add_u64", "v_alignbit_b32", "v_add3_u32", "v_cndmask_b32", "v_lshrrev_b64",
                               "v_cmp_gt_u64", "v_mov_b32", "v_perm_b32", "v_mul_u32_u24", "v_mad_u32_u24",
                               "v_bitop3_b32", "v_xor_b32_e64", "v_add_u32_e32", "v_add_u32_e64", "xor_e32+xor_e64 (2 instr)",
-                              "v_fma_f32", "v_add_f32", "v_pk_fma_f32"};
+                              "v_fma_f32", "v_add_f32", "v_pk_fma_f32", "v_cndmask_b32_e64 (sgpr mask)",
+                              "v_cmp_lt_u64 + 2 v_cndmask (3 instr)", "sub/subb/subbrev + 2 bitop3 (5 instr)"};
 
 static unsigned long long *g_cyc;
 static double g_med_cycles;
@@ -92,21 +111,21 @@ int main() {
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
-    float ms[23];
-    double cy[23];
+    float ms[26];
+    double cy[26];
 #define RUN(i) ms[i] = run<i>(d, blocks, iters, e0, e1); cy[i] = g_med_cycles;
     RUN(0) RUN(1) RUN(2) RUN(3) RUN(4) RUN(5) RUN(6) RUN(7)
     RUN(8) RUN(9) RUN(10) RUN(11) RUN(12) RUN(13) RUN(14) RUN(15)
-    RUN(16) RUN(17) RUN(18) RUN(19) RUN(20) RUN(21) RUN(22)
+    RUN(16) RUN(17) RUN(18) RUN(19) RUN(20) RUN(21) RUN(22) RUN(23) RUN(24) RUN(25)
     // wave-instructions per SIMD = waves per SIMD (8) * iters * CHAINS
     const double winst = 8.0 * iters * CHAINS * REPS;
     printf("{\"cus\": %d, \"clock_mhz\": %d, \"results\": [\n", cus, p.clockRate / 1000);
-    for (int i = 0; i < 23; i++) {
+    for (int i = 0; i < 26; i++) {
         const double ns_per = ms[i] * 1e6 / winst;
         // a block's 4 waves sit on 4 SIMDs; 8 blocks per CU -> 8 waves per SIMD run together
         const double cyc_per = cy[i] / (8.0 * iters * CHAINS * REPS);
         printf("  {\"inst\": \"%s\", \"ms\": %.3f, \"ns_per_wave_inst_per_simd\": %.4f, \"cycles_per_wave_inst_per_simd\": %.3f, \"rel_to_xor\": %.2f}%s\n",
-               names[i], ms[i], ns_per, cyc_per, ms[i] / ms[0], i < 22 ? "," : "");
+               names[i], ms[i], ns_per, cyc_per, ms[i] / ms[0], i < 25 ? "," : "");
     }
     printf("]}\n");
     return 0;
