@@ -332,8 +332,14 @@ def all_vs_all_MASH(Bdb, data_folder, **kwargs):
         write_mash_table(MASH_folder + 'MASH_table.tsv', cm)
     Mdb = mdb_from_condensed(cm.names, cm.common, cm.denom, cm.nhash, cm.s)
 
-    # Filter out those genomes that are not in Bdb (reference 586-594)
+    # Filter out those genomes that are not in Bdb (reference 586-594).  When
+    # every sketched genome is in Bdb (the drop-in sketches Bdb's own genomes)
+    # the block is the identity: no row is dropped and the categories already
+    # are the sorted names, ordered (mdb_from_condensed) -- skip its 10^6-row
+    # isin passes
     genomes = Bdb['genome'].unique()
+    if set(cm.names).issubset(set(genomes)):
+        return Mdb
     Mdb = Mdb[Mdb['genome1'].isin(genomes)]
     Mdb = Mdb[Mdb['genome2'].isin(genomes)]
     for g in ['genome1', 'genome2']:

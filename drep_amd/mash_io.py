@@ -178,61 +178,56 @@ def _list_ptr(off: int, esz: int, cnt: int) -> int:
     return 1 | ((off & 0x3FFFFFFF) << 2) | (esz << 32) | (cnt << 35)
 
 
+def _text_words(text: str) -> np.ndarray:
+    """A Cap'n Proto Text blob: UTF-8 bytes + NUL, zero-padded to whole words."""
+    raw = text.encode("utf-8") + b"\x00"
+    nw = (len(raw) + 7) // 8
+    return np.frombuffer(raw + b"\x00" * (8 * nw - len(raw)), dtype="<u8"), len(raw)
+
+
 def write_msh(path: str, refs: Sequence[MashReference], kmer: int = 21,
               sketch_size: int = 1000, seed: int = 42) -> None:
     """Write ``refs`` as a single-segment Cap'n Proto ``.msh`` message with the
-    structure :func:`read_msh` reads (the layout of the reference fixtures)."""
-    words: List[int] = []
-
-    def alloc(n: int) -> int:
-        s = len(words)
-        words.extend([0] * n)
-        return s
-
-    root_ptr = alloc(1)
-    root = alloc(3 + 2)
-    words[root_ptr] = _struct_ptr(root - root_ptr - 1, 3, 2)
-    words[root + 0] = kmer & 0xFFFFFFFF
-    words[root + 1] = (sketch_size & 0xFFFFFFFF) | (1 << 32)   # concatenated = true
-    words[root + 2] = ((seed ^ 42) & 0xFFFFFFFF) << 32
-    # reference list holder
-    holder = alloc(1)
-    words[root + 3] = _struct_ptr(holder - (root + 3) - 1, 0, 1)
-    locus = alloc(1)
-    words[root + 4] = _struct_ptr(locus - (root + 4) - 1, 0, 1)
-    # locus list: empty list of structs (tag-only composite list)
-    ltag = alloc(1)
-    words[locus] = _list_ptr(ltag - locus - 1, 7, 0)
-    words[ltag] = 0
-    # references composite list
+    structure :func:`read_msh` reads (the layout of the reference fixtures).
+    The message is sized up front and filled in one uint64 array (hash lists
+    are slice copies), in this word order: root pointer, root struct, the
+    reference-list holder, the locus holder and its empty list tag, the
+    references' composite list, then per reference its name, comment and hash
+    list."""
     n = len(refs)
     edw, epc = 2, 6
-    tag = alloc(1 + n * (edw + epc))
-    words[holder] = _list_ptr(tag - holder - 1, 7, n * (edw + epc))
-    words[tag] = (n << 2) | (edw << 32) | (epc << 48)
-    blobs = []
-    for i, r in enumerate(refs):
+    texts = [(_text_words(r.name), _text_words(r.comment)) for r in refs]
+    hashes = [np.asarray(r.hashes, dtype=np.uint64) for r in refs]
+    tag = 9
+    total = tag + 1 + n * (edw + epc) + sum(len(a[0]) + len(b[0]) + len(h) for (a, b), h in zip(texts, hashes))
+    w = np.zeros(total, dtype="<u8")
+    root_ptr, root, holder, locus, ltag = 0, 1, 6, 7, 8
+    w[root_ptr] = _struct_ptr(root - root_ptr - 1, 3, 2)
+    w[root + 0] = kmer & 0xFFFFFFFF
+    w[root + 1] = (sketch_size & 0xFFFFFFFF) | (1 << 32)   # concatenated = true
+    w[root + 2] = ((seed ^ 42) & 0xFFFFFFFF) << 32
+    w[root + 3] = _struct_ptr(holder - (root + 3) - 1, 0, 1)
+    w[root + 4] = _struct_ptr(locus - (root + 4) - 1, 0, 1)
+    # locus list: empty list of structs (tag-only composite list)
+    w[locus] = _list_ptr(ltag - locus - 1, 7, 0)
+    # references composite list
+    w[holder] = _list_ptr(tag - holder - 1, 7, n * (edw + epc))
+    w[tag] = (n << 2) | (edw << 32) | (epc << 48)
+    at = tag + 1 + n * (edw + epc)
+    for i, (r, (name, comment), h) in enumerate(zip(refs, texts, hashes)):
         base = tag + 1 + i * (edw + epc)
-        words[base + 1] = int(r.length) & 0xFFFFFFFFFFFFFFFF
-        blobs.append((base + edw, r))
-    for pbase, r in blobs:
-        for slot, text in ((2, r.name), (3, r.comment)):
-            raw = text.encode("utf-8") + b"\x00"
-            nw = (len(raw) + 7) // 8
-            at = alloc(nw)
-            padded = raw + b"\x00" * (8 * nw - len(raw))
-            for k in range(nw):
-                words[at + k] = int.from_bytes(padded[8 * k:8 * k + 8], "little")
-            words[pbase + slot] = _list_ptr(at - (pbase + slot) - 1, 2, len(raw))
-        h = np.asarray(r.hashes, dtype=np.uint64)
-        at = alloc(len(h))
-        words[pbase + 5] = _list_ptr(at - (pbase + 5) - 1, 5, len(h))
-        blobs_at = at
-        words[blobs_at:blobs_at + len(h)] = [int(x) for x in h]
-    body = np.array(words, dtype="<u8").tobytes()
-    header = struct.pack("<II", 0, len(words))
+        w[base + 1] = int(r.length) & 0xFFFFFFFFFFFFFFFF
+        pbase = base + edw
+        for slot, (tw, nbytes) in ((2, name), (3, comment)):
+            w[at:at + len(tw)] = tw
+            w[pbase + slot] = _list_ptr(at - (pbase + slot) - 1, 2, nbytes)
+            at += len(tw)
+        w[pbase + 5] = _list_ptr(at - (pbase + 5) - 1, 5, len(h))
+        w[at:at + len(h)] = h
+        at += len(h)
+    header = struct.pack("<II", 0, total)
     tmp = path + ".tmp%d" % os.getpid()
     with open(tmp, "wb") as fh:
         fh.write(header)
-        fh.write(body)
+        fh.write(w.tobytes())
     os.replace(tmp, path)
