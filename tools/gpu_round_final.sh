@@ -10,6 +10,6 @@ tail -1 gpurun_out/smoke.log
 SHARD_TIMING=0 timeout -k 10 120 python tools/shard_step.py 1000 8 0 30 > gpurun_out/shard.json 2>/dev/null || { echo "shard failed"; exit 1; }
 SHARD_TIMING=1 timeout -k 10 120 python tools/shard_step.py 1000 8 0 30 >> gpurun_out/shard.json 2>/dev/null || { echo "shard failed"; exit 1; }
 cat gpurun_out/shard.json
-ROUND=r01 bash tools/profile_round.sh || { echo "profile failed"; exit 1; }
+bash tools/profile_round.sh || { echo "profile failed"; exit 1; }
 timeout -k 10 300 python bench.py > gpurun_out/bench.log 2> gpurun_out/bench.err || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.log
