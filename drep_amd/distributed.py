@@ -80,6 +80,10 @@ def gather_segments(seg, N: int, root: int = 0, out=None):
     # gloo moves host memory only: device segments are staged through the host
     # (rehearsals of the sharded path on one GPU; RCCL moves device memory)
     host_p2p = dist.get_backend() == "gloo" and seg.is_cuda
+    # the transfers move bytes (int8 views): NCCL/RCCL has no 16-bit integer
+    # type, and torch's nccl process group rejects int16 tensors
+    def as_bytes(t):
+        return t.view(torch.int8)
     ops, landing = [], []
     full = None
     if rank == root:
@@ -96,12 +100,12 @@ def gather_segments(seg, N: int, root: int = 0, out=None):
             elif host_p2p:
                 buf = torch.empty(sizes[r], dtype=seg.dtype)
                 landing.append((full[lo:lo + sizes[r]], buf))
-                ops.append(dist.P2POp(dist.irecv, buf, r))
+                ops.append(dist.P2POp(dist.irecv, as_bytes(buf), r))
             else:
-                ops.append(dist.P2POp(dist.irecv, full[lo:lo + sizes[r]], r))
+                ops.append(dist.P2POp(dist.irecv, as_bytes(full[lo:lo + sizes[r]]), r))
     elif sizes[rank]:
         mine = seg[:sizes[rank]].contiguous()
-        ops.append(dist.P2POp(dist.isend, mine.cpu() if host_p2p else mine, root))
+        ops.append(dist.P2POp(dist.isend, as_bytes(mine.cpu() if host_p2p else mine), root))
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
