@@ -142,6 +142,18 @@ __device__ void chain_merge(int32_t x, int32_t y, double cur, int32_t len, uint3
 // uses it as its search value -- no cross-workgroup dependence.  After a chain
 // restart t may be y itself: then the search value of i is the freshly
 // computed D[y][i].  The last workgroup makes scipy's chain decision.
+//
+// A step is a chain of dependent memory round trips, so the loads are issued
+// together: each pass takes kLkPer entries per lane (grid-stride) and loads
+// their sizes and D[t][i] (plus D[x][i], D[y][i] after a merge) before any of
+// them is used or any store is made (written as one loop, the compiler kept
+// each entry's loads behind the previous entry's stores: D aliases itself).
+// D[t][i] may be loaded before the update's stores because the update writes
+// D[t][i] only for i = y, whose search value is the freshly computed entry.
+// Likewise the chain decision's D[t][chain[len-2]] is loaded at the start by
+// every workgroup's thread 0: the chain's elements below the top are never x
+// or y, so no update of this step touches it.
+constexpr int kLkPer = 4;
 __global__ __launch_bounds__(kLkWG) void k_nn_step(double *__restrict__ D, uint32_t n, int method,
                                                   int32_t *__restrict__ size, int32_t *__restrict__ chain,
                                                   LinkState *__restrict__ st, MinIdx *__restrict__ parts,
@@ -149,30 +161,51 @@ __global__ __launch_bounds__(kLkWG) void k_nn_step(double *__restrict__ D, uint3
     if (st->k >= (int32_t)n - 1) return;                       // all merged: the rest of the batch idles
     const bool pend = st->pend != 0;
     const int32_t x = st->px, y = st->py, nx = st->pnx, ny = st->pny;
-    const int32_t t = chain[st->chain_len - 1];
+    const int32_t len = st->chain_len;
+    const int32_t t = chain[len - 1];
     const double *Dt = D + (uint64_t)t * n;
     const double *Dx = D + (uint64_t)x * n;
     double *Dy = D + (uint64_t)y * n;
+    int32_t yp = -1;
+    double dp = 0.0;
+    if (threadIdx.x == 0 && len > 1) { yp = chain[len - 2]; dp = Dt[yp]; }
+    // the old D[x][t], D[y][t] for the lane of i = y (loaded before any store)
+    const double dxt = pend ? Dx[t] : 0.0, dyt = pend ? Dy[t] : 0.0;
     double bv = INFINITY;
     int32_t bi = 0x7fffffff;
-    for (uint32_t i = blockIdx.x * kLkWG + threadIdx.x; i < n; i += gridDim.x * kLkWG) {
-        if (size[i] == 0) continue;
-        double v;
-        if (pend && (int32_t)i != y && (int32_t)i != t) {
-            const double u = lw_update(method, Dx[i], Dy[i], nx, ny);
-            Dy[i] = u;
-            D[(uint64_t)i * n + y] = u;
-            v = t == y ? u : Dt[i];
-        } else if (pend && (int32_t)i == y && t != y) {
-            const double u = lw_update(method, Dx[t], Dy[t], nx, ny);   // entry (y, t): old values, unshared
-            Dy[t] = u;
-            D[(uint64_t)t * n + y] = u;
-            v = u;
-        } else {
-            if ((int32_t)i == t) continue;
-            v = Dt[i];
+    const uint32_t stride = gridDim.x * kLkWG;
+    for (uint32_t i0 = blockIdx.x * kLkWG + threadIdx.x; i0 < n; i0 += kLkPer * stride) {
+        int32_t sz[kLkPer];
+        double dt[kLkPer], dx[kLkPer], dy[kLkPer];
+#pragma unroll
+        for (int k = 0; k < kLkPer; k++) {
+            const uint32_t i = i0 + k * stride;
+            const uint32_t ic = i < n ? i : n - 1;              // in bounds; i >= n is skipped below
+            sz[k] = size[ic];
+            dt[k] = Dt[ic];
+            if (pend) { dx[k] = Dx[ic]; dy[k] = Dy[ic]; }
         }
-        if (v < bv) { bv = v; bi = (int32_t)i; }                // ascending i per thread: first minimum kept
+#pragma unroll
+        for (int k = 0; k < kLkPer; k++) {
+            const uint32_t i = i0 + k * stride;
+            if (i >= n || sz[k] == 0) continue;
+            double v;
+            if (pend && (int32_t)i != y && (int32_t)i != t) {
+                const double u = lw_update(method, dx[k], dy[k], nx, ny);
+                Dy[i] = u;
+                D[(uint64_t)i * n + y] = u;
+                v = t == y ? u : dt[k];
+            } else if (pend && (int32_t)i == y && t != y) {
+                const double u = lw_update(method, dxt, dyt, nx, ny);      // entry (y, t): old values, unshared
+                Dy[t] = u;
+                D[(uint64_t)t * n + y] = u;
+                v = u;
+            } else {
+                if ((int32_t)i == t) continue;
+                v = dt[k];
+            }
+            if (v < bv) { bv = v; bi = (int32_t)i; }            // ascending i per thread: first minimum kept
+        }
     }
     const MinIdx part = block_argmin(bv, bi);
     MinIdx g;
@@ -180,15 +213,10 @@ __global__ __launch_bounds__(kLkWG) void k_nn_step(double *__restrict__ D, uint3
     if (threadIdx.x != 0) return;
     // chain decision (scipy nn_chain): the previous chain element wins ties
     st->pend = 0;
-    const int32_t len = st->chain_len;
     int32_t yy = g.i;
     double cur = g.v;
     bool merge = false;
-    if (len > 1) {
-        const int32_t yp = chain[len - 2];
-        const double dp = Dt[yp];
-        if (!(g.v < dp)) { yy = yp; cur = dp; merge = true; }
-    }
+    if (len > 1 && !(g.v < dp)) { yy = yp; cur = dp; merge = true; }
     if (!merge) {
         chain[len] = yy;
         st->chain_len = len + 1;
@@ -207,12 +235,26 @@ __global__ __launch_bounds__(kLkWG) void k_mst_step(const double *__restrict__ D
     const double *Dx = D + (uint64_t)x * n;
     double bv = INFINITY;
     int32_t bi = 0x7fffffff;
-    for (uint32_t i = blockIdx.x * kLkWG + threadIdx.x; i < n; i += gridDim.x * kLkWG) {
-        if (merged[i]) continue;
-        const double d = Dx[i];
-        double m = Dmin[i];
-        if (m > d) { m = d; Dmin[i] = d; }
-        if (m < bv) { bv = m; bi = (int32_t)i; }
+    const uint32_t stride = gridDim.x * kLkWG;
+    for (uint32_t i0 = blockIdx.x * kLkWG + threadIdx.x; i0 < n; i0 += kLkPer * stride) {
+        int32_t mg[kLkPer];
+        double dx[kLkPer], dm[kLkPer];
+#pragma unroll
+        for (int k = 0; k < kLkPer; k++) {                      // loads first (as k_nn_step)
+            const uint32_t i = i0 + k * stride;
+            const uint32_t ic = i < n ? i : n - 1;
+            mg[k] = merged[ic];
+            dx[k] = Dx[ic];
+            dm[k] = Dmin[ic];
+        }
+#pragma unroll
+        for (int k = 0; k < kLkPer; k++) {
+            const uint32_t i = i0 + k * stride;
+            if (i >= n || mg[k]) continue;
+            double m = dm[k];
+            if (m > dx[k]) { m = dx[k]; Dmin[i] = m; }
+            if (m < bv) { bv = m; bi = (int32_t)i; }
+        }
     }
     const MinIdx part = block_argmin(bv, bi);
     MinIdx g;
@@ -305,7 +347,8 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
         set_error("linkage method must be single, complete, average or weighted");
         return DREPHIP_ERR_UNSUPPORTED;
     }
-    // entries per lane of a step (DREPHIP_LINK_PER_LANE, A/B; default 4)
+    // entries per lane of a step, i.e. the grid density (default kLkPer: one pass;
+    // DREPHIP_LINK_PER_LANE exists for the tests, which cover 1, 4 and 16)
     const char *pl = getenv("DREPHIP_LINK_PER_LANE");
     const uint32_t per = pl ? std::max(1, std::min(64, atoi(pl))) : 4;
     const uint32_t grid = std::max(1u, std::min(1024u, (n + kLkWG * per - 1) / (kLkWG * per)));

@@ -795,7 +795,7 @@ def test_gpu_linkage_matches_scipy(method, n, kind):
     else:
         y = np.full(m, 0.5)
     Zs = sch.linkage(y, method=method)
-    for per_lane in ("4", "1"):                      # grid densities of the chain-step kernel
+    for per_lane in ("4", "1", "16"):                # grid densities of the chain-step kernel (16: 4 passes)
         os.environ["DREPHIP_LINK_PER_LANE"] = per_lane
         try:
             with _lib.Context(0, 21, S, 42) as ctx:
