@@ -44,6 +44,7 @@ struct LinkState {
     double pd;
     uint32_t ticket;         // last-workgroup detection of the search kernel
     int32_t x;               // MST: current vertex
+    int32_t bad;             // a step found no valid partial (the host reports an internal error)
 };
 
 struct MinIdx { double v; int32_t i; };
@@ -83,21 +84,28 @@ __device__ MinIdx block_argmin(double v, int32_t i) {
 }
 
 // Last workgroup of a grid: every workgroup publishes its partial, then one
-// agent-scope acq_rel ticket; the workgroup that draws the last ticket reads
-// all partials (agent-scope loads, spread over its threads) and reduces them.
+// agent-scope ticket; the workgroup that draws the last ticket reads all
+// partials (agent-scope loads, spread over its threads) and reduces them.
 // Every thread of the block must call it; the result is valid in thread 0.
+// The partial is an agent-scope atomic store (sc1), complete at the agent's
+// coherence point once vmcnt drains, so a RELAXED ticket after
+// s_waitcnt vmcnt(0) orders it: no release/acquire fence, whose gfx950 form
+// (buffer_wbl2 sc1 before the ticket, buffer_inv sc1 after) wrote back every
+// XCD's dirty L2 lines -- the step's row and column updates, which no other
+// workgroup of this launch reads (the next launch sees them at the kernel
+// boundary) -- once per workgroup per step.
 __device__ bool last_block(MinIdx part, MinIdx *parts, LinkState *st, MinIdx &out) {
     __shared__ int is_last;
     if (threadIdx.x == 0) {
         __hip_atomic_store(&parts[blockIdx.x].v, part.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&parts[blockIdx.x].i, part.i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t t = __hip_atomic_fetch_add(&st->ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t t = __hip_atomic_fetch_add(&st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         is_last = t == gridDim.x - 1;
         if (is_last) st->ticket = 0;
     }
     __syncthreads();
     if (!is_last) return false;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // every published partial is visible
     double bv = INFINITY;
     int32_t bi = 0x7fffffff;
     for (uint32_t b = threadIdx.x; b < gridDim.x; b += blockDim.x) {
@@ -211,6 +219,11 @@ __global__ __launch_bounds__(kLkWG) void k_nn_step(double *__restrict__ D, uint3
     MinIdx g;
     if (!last_block(part, parts, st, g)) return;
     if (threadIdx.x != 0) return;
+    if ((uint32_t)g.i >= n) {                    // no valid partial: stop every later step, the host reports it
+        st->bad = 1;
+        st->k = (int32_t)n - 1;
+        return;
+    }
     // chain decision (scipy nn_chain): the previous chain element wins ties
     st->pend = 0;
     int32_t yy = g.i;
@@ -218,6 +231,11 @@ __global__ __launch_bounds__(kLkWG) void k_nn_step(double *__restrict__ D, uint3
     bool merge = false;
     if (len > 1 && !(g.v < dp)) { yy = yp; cur = dp; merge = true; }
     if (!merge) {
+        if (len >= (int32_t)n) {                 // cannot happen on a consistent matrix: stop, no out-of-range store
+            st->bad = 1;
+            st->k = (int32_t)n - 1;
+            return;
+        }
         chain[len] = yy;
         st->chain_len = len + 1;
         return;
@@ -260,6 +278,11 @@ __global__ __launch_bounds__(kLkWG) void k_mst_step(const double *__restrict__ D
     MinIdx g;
     if (!last_block(part, parts, st, g)) return;
     if (threadIdx.x != 0) return;
+    if ((uint32_t)g.i >= n) {
+        st->bad = 1;
+        st->k = (int32_t)n - 1;
+        return;
+    }
     const int32_t k = st->k;
     Z[4 * k + 0] = x; Z[4 * k + 1] = g.i; Z[4 * k + 2] = g.v; Z[4 * k + 3] = 0;
     merged[g.i] = 1;
@@ -418,6 +441,9 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     HIPC(hipMemcpyAsync(&done, &d_st->k, 4, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));
     if (done != (int32_t)n - 1) { set_error("linkage did not finish"); return DREPHIP_ERR_INTERNAL; }
+    int32_t bad = 0;
+    HIPC(hipMemcpy(&bad, &d_st->bad, 4, hipMemcpyDeviceToHost));
+    if (bad) { set_error("linkage: a chain step found no valid partial"); return DREPHIP_ERR_INTERNAL; }
     std::vector<double> Z(4ull * (n - 1));
     HIPC(hipMemcpy(Z.data(), d_Z, Z.size() * 8, hipMemcpyDeviceToHost));
     sort_and_label(Z, n);
