@@ -3,7 +3,7 @@ synthetic 5 Mbp genomes, s = 1000 -- sketch, all-pairs over the whole triangle
 (5x10^7 / 5x10^9 pairs; 10 GB of condensed counts in HBM at 10^5) and
 average-linkage primary clustering on the GPU (the n x n float64 matrix, 80 GB
 at 10^5, built in HBM from the counts).  Both sizes run by default; the
-GPU time is seconds (sketch 0.9 s, all-pairs 1.3 s, linkage 2.9 s at 10^5).
+GPU time is seconds (sketch 0.9 s, all-pairs 1.1 s, linkage 2.3 s at 10^5).
 DREPHIP_SCALE_N=<n> adds one more size.
 
 Parity at full size, through what the oracle can afford:
