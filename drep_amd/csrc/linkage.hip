@@ -118,15 +118,13 @@ __device__ bool last_block(MinIdx part, MinIdx *parts, LinkState *st, MinIdx &ou
 }
 
 // ---------------------------------------------------------------- nn_chain
-// Merge chain top x with y at distance cur (scipy: the smaller index is
-// dropped, the larger becomes the new cluster), pop both, restart an empty
-// chain at the first active cluster.
-__device__ void chain_merge(int32_t x, int32_t y, double cur, int32_t len, uint32_t n, int32_t *size,
-                            int32_t *chain, LinkState *st, double *Z) {
-    int32_t a = x, b = y;
-    if (a > b) { const int32_t t = a; a = b; b = t; }
-    const int32_t na = size[a], nb = size[b];
-    const int32_t k = st->k;
+// Merge chain top x (size sx) with y (size sy) at distance cur (scipy: the
+// smaller index is dropped, the larger becomes the new cluster), pop both,
+// restart an empty chain at the first active cluster.  k: merges so far.
+__device__ void chain_merge(int32_t x, int32_t y, int32_t sx, int32_t sy, double cur, int32_t len, int32_t k,
+                            uint32_t n, int32_t *size, int32_t *chain, LinkState *st, double *Z) {
+    int32_t a = x, b = y, na = sx, nb = sy;
+    if (a > b) { a = y; b = x; na = sy; nb = sx; }
     Z[4 * k + 0] = a; Z[4 * k + 1] = b; Z[4 * k + 2] = cur; Z[4 * k + 3] = na + nb;
     size[a] = 0;
     size[b] = na + nb;
@@ -158,15 +156,16 @@ __device__ void chain_merge(int32_t x, int32_t y, double cur, int32_t len, uint3
 // each entry's loads behind the previous entry's stores: D aliases itself).
 // D[t][i] may be loaded before the update's stores because the update writes
 // D[t][i] only for i = y, whose search value is the freshly computed entry.
-// Likewise the chain decision's D[t][chain[len-2]] is loaded at the start by
-// every workgroup's thread 0: the chain's elements below the top are never x
-// or y, so no update of this step touches it.
+// Likewise the chain decision's D[t][chain[len-2]] and the two sizes are
+// loaded at the start by every workgroup's thread 0: the chain's elements
+// below the top are never x or y, so no update of this step touches them.
 constexpr int kLkPer = 4;
 __global__ __launch_bounds__(kLkWG) void k_nn_step(double *__restrict__ D, uint32_t n, int method,
                                                   int32_t *__restrict__ size, int32_t *__restrict__ chain,
                                                   LinkState *__restrict__ st, MinIdx *__restrict__ parts,
                                                   double *__restrict__ Z) {
-    if (st->k >= (int32_t)n - 1) return;                       // all merged: the rest of the batch idles
+    const int32_t k0 = st->k;
+    if (k0 >= (int32_t)n - 1) return;                          // all merged: the rest of the batch idles
     const bool pend = st->pend != 0;
     const int32_t x = st->px, y = st->py, nx = st->pnx, ny = st->pny;
     const int32_t len = st->chain_len;
@@ -174,9 +173,12 @@ __global__ __launch_bounds__(kLkWG) void k_nn_step(double *__restrict__ D, uint3
     const double *Dt = D + (uint64_t)t * n;
     const double *Dx = D + (uint64_t)x * n;
     double *Dy = D + (uint64_t)y * n;
-    int32_t yp = -1;
+    // a merge is always of t with yp = chain[len-2]: thread 0 loads the
+    // decision's operands (D[t][yp] and both sizes) now, off the last
+    // workgroup's critical path
+    int32_t yp = -1, szt = 0, szyp = 0;
     double dp = 0.0;
-    if (threadIdx.x == 0 && len > 1) { yp = chain[len - 2]; dp = Dt[yp]; }
+    if (threadIdx.x == 0 && len > 1) { yp = chain[len - 2]; dp = Dt[yp]; szt = size[t]; szyp = size[yp]; }
     // the old D[x][t], D[y][t] for the lane of i = y (loaded before any store)
     const double dxt = pend ? Dx[t] : 0.0, dyt = pend ? Dy[t] : 0.0;
     double bv = INFINITY;
@@ -240,7 +242,7 @@ __global__ __launch_bounds__(kLkWG) void k_nn_step(double *__restrict__ D, uint3
         st->chain_len = len + 1;
         return;
     }
-    chain_merge(t, yy, cur, len, n, size, chain, st, Z);
+    chain_merge(t, yy, szt, szyp, cur, len, k0, n, size, chain, st, Z);
 }
 
 // ------------------------------------------------------------ MST (single)
