@@ -130,20 +130,35 @@ def cpu_model():
 
 
 def cpu_baseline(args, threads):
-    """Bounded sample of the same whole job on the host with the C oracle
-    (Mash-equivalent restatement, OpenMP): sketch a sample of the genomes
-    (about 4 s of wall time) and `mash dist` as many random pairs as the job
-    has; extrapolate the sketch part to all N genomes."""
+    """The same whole job on the host with the C oracle (Mash-equivalent
+    restatement, OpenMP): sketch every genome and `mash dist` every pair when
+    that fits CPU_BUDGET_S of wall time (configs[1]: ~19 s on the GPU box's 16
+    threads), else a bounded sample extrapolated to the job: a probe of
+    16 x threads genomes sketched first decides which."""
     import oracle
     N, L, s = args.genomes, args.genome_bp, args.sketch
+    budget = float(os.environ.get("CPU_BUDGET_S", 30))
     ns = min(N, max(2, 16 * threads))
     t0 = time.perf_counter()
     h, nh = oracle.sketch_synth(0, ns, L, seed=args.seed, family_size=args.family_size, s=s, threads=threads)
     t_sk = time.perf_counter() - t0
-    rng = np.random.default_rng(1)
-    npairs = max(2, min(N * (N - 1) // 2, 5_000_000))
-    pi = rng.integers(0, ns, npairs).astype(np.uint32)
-    pj = ((pi + 1 + rng.integers(0, ns - 1, npairs)) % ns).astype(np.uint32)
+    if ns < N and t_sk / ns * N <= budget:                       # the whole sketch fits: measure it
+        t0 = time.perf_counter()
+        h2, nh2 = oracle.sketch_synth(ns, N - ns, L, seed=args.seed, family_size=args.family_size, s=s,
+                                      threads=threads)
+        t_sk += time.perf_counter() - t0
+        h, nh = np.concatenate([h, h2]), np.concatenate([nh, nh2])
+        ns = N
+    full = ns == N and N * (N - 1) // 2 <= 5_000_000
+    if full:                                                     # every pair of the job
+        iu = np.triu_indices(N, 1)
+        pi, pj = iu[0].astype(np.uint32), iu[1].astype(np.uint32)
+    else:                                                        # random pairs of the sampled genomes
+        rng = np.random.default_rng(1)
+        npairs = max(2, min(N * (N - 1) // 2, 5_000_000))
+        pi = rng.integers(0, ns, npairs).astype(np.uint32)
+        pj = ((pi + 1 + rng.integers(0, ns - 1, npairs)) % ns).astype(np.uint32)
+    npairs = len(pi)
     t0 = time.perf_counter()
     oracle.dist_pairs_list(h, nh, s, pi, pj, threads=threads)
     t_d = time.perf_counter() - t0
@@ -151,6 +166,13 @@ def cpu_baseline(args, threads):
     per_pair = t_d / npairs
     job = N * per_genome + (N * (N - 1) / 2) * per_pair
     visible = os.cpu_count() or threads
+    if ns == N and full:
+        how = ("the whole job measured: sketch of all %d synthetic %d bp genomes in %.2f s + all %d pairs of "
+               "mash dist in %.2f s" % (N, L, t_sk, npairs, t_d))
+    else:
+        how = ("sketch of %d of the %d synthetic %d bp genomes in %.2f s + %d pairs of mash dist in %.2f s; job = "
+               "%d x per-genome sketch + N(N-1)/2 x per-pair dist = %.1f s + %.2f s"
+               % (ns, N, L, t_sk, npairs, t_d, N, N * per_genome, N * (N - 1) / 2 * per_pair))
     return {
         "value": (N * (N - 1) / 2) / job,
         "unit": "genome pairs/s",
@@ -158,14 +180,12 @@ def cpu_baseline(args, threads):
         "kind": "port",
         "cpu_model": cpu_model(),
         "host_cpus_visible": visible,
-        "sample": ("C oracle (Mash-equivalent restatement; Mash itself is absent), OpenMP %d threads = this job's "
-                   "host CPU share: sketch of %d of the %d synthetic %d bp genomes in %.2f s + %d random pairs of "
-                   "mash dist (the job's pair count, capped at 5e6) in %.2f s; job = %d x per-genome sketch + "
-                   "N(N-1)/2 x per-pair dist = %.1f s + %.2f s"
-                   % (threads, ns, N, L, t_sk, npairs, t_d, N, N * per_genome, N * (N - 1) / 2 * per_pair)),
+        "sample": "C oracle (Mash-equivalent restatement; Mash itself is absent), OpenMP %d threads = this job's "
+                  "host CPU share; %s" % (threads, how),
+        "measured_whole_job": bool(ns == N and full),
         "sketch_Mbp_per_s": ns * L / t_sk / 1e6,
         "dist_pairs_per_s": npairs / t_d,
-        # mash dist -p <all host cores>: the sample's per-thread rate times the
+        # mash dist -p <all host cores>: the measured per-thread rate times the
         # host's visible CPUs (linear scaling assumed; both legs are embarrassingly
         # parallel), stated next to the measured share
         "value_all_host_cpus_extrapolated": (N * (N - 1) / 2) / job * visible / threads,
