@@ -99,10 +99,12 @@ def mdb_from_condensed(names: Sequence[str], common: np.ndarray, denom: np.ndarr
     (ordered categoricals sorted by name; float32) and values
     (d_cluster.py:575-596)."""
     N = len(names)
-    nh = np.minimum(np.asarray(nhash, dtype=np.int64), s)
-    Cm = _square(np.asarray(common, dtype=np.uint16), N, nh.astype(np.uint16))
-    Dm = _square(np.asarray(denom, dtype=np.uint16), N, nh.astype(np.uint16))
-    dist = mash_distance_float32(Cm.reshape(-1), Dm.reshape(-1), k)   # row q, col r: symmetric
+    # distances of the N(N-1)/2 pairs, then the symmetric square (row q, col r);
+    # a genome against itself has common = denom = its hash count (or 0 for an
+    # empty sketch), distance 0 either way, so the diagonal is 0
+    from scipy.spatial.distance import squareform
+    dist = squareform(mash_distance_float32(np.asarray(common, dtype=np.uint16),
+                                            np.asarray(denom, dtype=np.uint16), k), checks=False).reshape(-1)
     cats = sorted(set(names))
     pos = {n: i for i, n in enumerate(cats)}
     codes = np.array([pos[n] for n in names], dtype=np.int32)
@@ -467,8 +469,7 @@ def condensed_cluster_distances(cm: CondensedMash) -> np.ndarray:
     order = np.argsort(np.array(cm.names, dtype=object), kind='stable')
     if np.all(order == np.arange(N)):
         return after
-    M = _square(after, N, np.zeros(N, dtype=np.float64))
-    M = M[np.ix_(order, order)]
+    M = ssd.squareform(after, checks=False)[np.ix_(order, order)]
     return ssd.squareform(M, checks=False).astype(np.float64)
 
 
