@@ -102,8 +102,7 @@ def mdb_from_condensed(names: Sequence[str], common: np.ndarray, denom: np.ndarr
     # distances of the N(N-1)/2 pairs, then the symmetric square (row q, col r);
     # a genome against itself has common = denom = its hash count (or 0 for an
     # empty sketch), distance 0 either way, so the diagonal is 0
-    from scipy.spatial.distance import squareform
-    dist = squareform(mash_distance_float32(np.asarray(common, dtype=np.uint16),
+    dist = ssd.squareform(mash_distance_float32(np.asarray(common, dtype=np.uint16),
                                             np.asarray(denom, dtype=np.uint16), k), checks=False).reshape(-1)
     cats = sorted(set(names))
     pos = {n: i for i, n in enumerate(cats)}
