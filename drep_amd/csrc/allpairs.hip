@@ -370,7 +370,8 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
                                            const uint32_t *T, const uint32_t *V, uint32_t H, uint32_t hm, uint32_t s,
                                            uint32_t N, uint32_t i0, uint32_t nrows, uint32_t cend, uint32_t c_first,
                                            uint32_t c_step, const uint32_t (&nA)[R], const uint32_t (&o1)[R],
-                                           const uint32_t (&o2)[R], const uint64_t (&alast)[R], uint32_t okmask,
+                                           const uint32_t (&o2)[R], const uint64_t (&alast)[R],
+                                           const uint64_t (&thr1)[R], const uint64_t (&thr2)[R], uint32_t okmask,
                                            bool any_partial_row, uint16_t *__restrict__ common,
                                            uint16_t *__restrict__ denom, uint64_t seg0) {
     const uint32_t lane = threadIdx.x & 63;
@@ -420,11 +421,19 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
         // runtime loop over groups of kRing chunks; ring slots are static.  The
         // scan-end test runs once per group, on the group's first chunk (a
         // chunk past every row's largest hash cannot hit, so finishing the
-        // group is only wasted work, never a wrong count).  (A union-rank end
-        // -- stop once j0 + #{A < b0} - mrun >= s for every row, as the band
-        // kernel does per band -- measured slower here: one sampled high-word
-        // read per row at two groups per column cost more than the skipped
-        // chunks of these short columns saved, 3.92 vs 3.57 ms at N = 6000.)
+        // group is only wasted work, never a wrong count), and the union-rank
+        // end: b0 at column position j0 has rank u(b0) = j0 + #{A < b0} -
+        // #{matches below b0} in A u B and every later column element ranks
+        // higher, so once u(b0) >= s for every active row no later element is
+        // among the s smallest of A_r u B -- the rank rule (probe_rows) counts
+        // nothing more, and |A u B| > s makes a partial pair's denominator s
+        // whatever mrun the rest would add.  Tested at the two groups past half
+        // the column (j0 = 4 g1 x 64 and the next), where unrelated sketches
+        // get there, for rows with no match so far: b0 > A_r[s - j0 - 1]
+        // (thr1/thr2, scalar, loaded with the row's largest hash) gives
+        // #{A_r < b0} >= s - j0.  Scalar compares only (a sampled high-word
+        // read per row measured slower than the chunks it skipped).
+        const uint32_t kb1 = 4u * ((s / 2 + 255) / 256);
         for (uint32_t kb = 0; kb < nch; kb += kRing) {
             {
                 const uint64_t b = rg[0];
@@ -432,6 +441,14 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
                 // int: through uint32_t so the low word is not sign-extended)
                 const uint64_t b0 = ((uint64_t)rfl((uint32_t)(b >> 32)) << 32) | rfl((uint32_t)b);
                 if (b0 == kEmpty || b0 > amax) break;
+                if (kb == kb1 || kb == kb1 + kRing) {                     // wave-uniform
+                    bool all_past = true;
+#pragma unroll
+                    for (int r = 0; r < R; r++)
+                        if (((actmask >> r) & 1u) && (mrun[r] != 0 || !(b0 > (kb == kb1 ? thr1[r] : thr2[r]))))
+                            all_past = false;
+                    if (all_past) break;
+                }
             }
 #pragma unroll
             for (int u = 0; u < kRing; u++) {
@@ -520,7 +537,7 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
         }
     }
     uint32_t nA[R], o1[R], o2[R];
-    uint64_t alast[R];
+    uint64_t alast[R], thr1[R], thr2[R];
     uint32_t failmask = 0;
     bool any_partial_row = false, fast = true;
     {   // per-row scalars: uniform loads with clamped rows, no branches, so none
@@ -529,12 +546,19 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
         const uint32_t fi = i0 - row0;
         const uint64_t fw = *(const uint64_t *)(fam + (fi & ~7u));
         uint32_t nraw[R];
-        uint64_t lraw[R];
+        uint64_t lraw[R], t1raw[R], t2raw[R];
+        // union-rank thresholds (ap_columns): A_r[s - j0 - 1] for the two test
+        // groups, j0 = 64 kb1 and 64 (kb1 + 4); positions below 0 clamp to 0
+        // (never used then: such a group does not exist or the test is moot)
+        const uint32_t kb1 = 4u * ((s / 2 + 255) / 256);
+        const uint32_t p1 = s > 64 * kb1 ? s - 64 * kb1 - 1 : 0, p2 = s > 64 * (kb1 + 4) ? s - 64 * (kb1 + 4) - 1 : 0;
 #pragma unroll
         for (int r = 0; r < R; r++) {
             const uint32_t i = min(i0 + (uint32_t)r, row1 - 1);
             nraw[r] = nhash[i];
             lraw[r] = hashes[(uint64_t)i * s + s - 1];
+            t1raw[r] = hashes[(uint64_t)i * s + p1];
+            t2raw[r] = hashes[(uint64_t)i * s + p2];
         }
 #pragma unroll
         for (int r = 0; r < R; r++) {
@@ -547,6 +571,10 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
             const QFields q = qfields(f & ~kFamTwins);
             o1[r] = q.o1; o2[r] = q.o2;
             alast[r] = (ok && nA[r] >= s) ? lraw[r] : kEmpty;
+            // a threshold past the row's last element (partial row) or of a
+            // group with j0 >= s never ends the scan (kEmpty: b0 > it is false)
+            thr1[r] = (ok && s > 64 * kb1 && p1 < nA[r]) ? t1raw[r] : kEmpty;
+            thr2[r] = (ok && s > 64 * (kb1 + 4) && p2 < nA[r]) ? t2raw[r] : kEmpty;
             any_partial_row |= nA[r] < s;
         }
     }
@@ -557,10 +585,10 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
     constexpr int KB = NCH == 16 ? 11 : 0;
     if (fast)
         ap_columns<R, NCH, true, KB>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend, c0 + wave, WG / 64,
-                                     nA, o1, o2, alast, ~failmask, any_partial_row, common, denom, seg0);
+                                     nA, o1, o2, alast, thr1, thr2, ~failmask, any_partial_row, common, denom, seg0);
     else
         ap_columns<R, NCH, false, KB>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend, c0 + wave, WG / 64,
-                                      nA, o1, o2, alast, ~failmask, any_partial_row, common, denom, seg0);
+                                      nA, o1, o2, alast, thr1, thr2, ~failmask, any_partial_row, common, denom, seg0);
     if (failmask) {
         // a row whose table could not be built (three of its keys share a low
         // word under every field family; never observed on real sketches):
