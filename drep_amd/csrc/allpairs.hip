@@ -685,7 +685,7 @@ template <int R, uint32_t NW, bool FAST, bool RETRY>
 __device__ __forceinline__ void band_columns(const uint64_t *__restrict__ hashes, uint32_t s, const uint32_t *T,
                                              const uint32_t *V, uint32_t *cur, uint16_t *pcnt, uint16_t *pm,
                                              uint32_t c0, uint32_t ncols, uint32_t i0, uint32_t nrows, uint32_t wave,
-                                             uint64_t hi, uint32_t fam, const uint32_t (&pr)[R]) {
+                                             uint64_t hi, uint32_t fam, const uint32_t (&pr)[R], int *live) {
     constexpr uint32_t H = 1u << kBandB, hm = H - 1;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t lane_off = lane * 8u;
@@ -731,6 +731,7 @@ __device__ __forceinline__ void band_columns(const uint64_t *__restrict__ hashes
         for (int r = 0; r < R; r++)
             if (((actmask >> r) & 1u) && q0 + pr[r] < s + mrun[r]) all_past = false;
         if (all_past) continue;
+        *live = 1;                                                    // benign race: every writer stores 1
         const __amdgpu_buffer_rsrc_t rc = column_rsrc(hashes + (uint64_t)c * s, s);
         uint32_t q = q0;
         bool more = true;
@@ -784,7 +785,7 @@ __global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
     uint16_t *pm = pcnt + R * kBandCols;                             // [R][kBandCols] shared so far (<= s)
     __shared__ uint32_t s_p[R], s_q[R];
     __shared__ uint64_t s_hi;
-    __shared__ int s_done, s_fail, s_abort, s_twin;
+    __shared__ int s_done, s_fail, s_abort, s_twin, s_live;
 
     const uint32_t i0 = items[blockIdx.x].x;
     const uint32_t c0 = items[blockIdx.x].y;
@@ -832,6 +833,7 @@ __global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
                 s_hi = v < maxlast + 1 ? v : maxlast + 1;
                 s_done = !any_left;
                 s_fail = 0;
+                s_live = 0;
             }
             if (lane < (uint32_t)R) s_q[lane] = 0;
         }
@@ -887,12 +889,16 @@ __global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
         // ---- columns: wave w takes columns w, w+NW, ...
         // the fast probe without the second-slot retry unless a band table has twins
         if (fam == 0 && !s_twin)
-            band_columns<R, NW, true, false>(hashes, s, T, V, cur, pcnt, pm, c0, ncols, i0, nrows, wave, hi, fam, pr);
+            band_columns<R, NW, true, false>(hashes, s, T, V, cur, pcnt, pm, c0, ncols, i0, nrows, wave, hi, fam, pr, &s_live);
         else if (fam == 0)
-            band_columns<R, NW, true, true>(hashes, s, T, V, cur, pcnt, pm, c0, ncols, i0, nrows, wave, hi, fam, pr);
+            band_columns<R, NW, true, true>(hashes, s, T, V, cur, pcnt, pm, c0, ncols, i0, nrows, wave, hi, fam, pr, &s_live);
         else
-            band_columns<R, NW, false, true>(hashes, s, T, V, cur, pcnt, pm, c0, ncols, i0, nrows, wave, hi, fam, pr);
+            band_columns<R, NW, false, true>(hashes, s, T, V, cur, pcnt, pm, c0, ncols, i0, nrows, wave, hi, fam, pr, &s_live);
         __syncthreads();
+        // every column past its union-rank end for every row (band_columns):
+        // the same holds in every later band (pr only grows), so no further
+        // band table is built
+        if (!s_live) break;
         if (tid < (uint32_t)R) s_p[tid] += s_q[tid];
         if (prof && tid == 0) {
             const uint64_t t_e = wall_clock64();
