@@ -219,8 +219,10 @@ def check_against_oracle(args, loc_h, loc_n, d_common, g0, nloc, N, r0, r1, worl
             res["mismatches"] += int(not good)
         res["genomes"] = len(starts)
     seg = segment_size(N, r0, r1)
+    # the gather is a collective: every rank joins it, also one whose segment
+    # is empty (row_partition may give the last rank no pairs at small N)
+    hh, nn = (gather_sketches(loc_h, loc_n) if world > 1 else (loc_h, loc_n))
     if seg:
-        hh, nn = (gather_sketches(loc_h, loc_n) if world > 1 else (loc_h, loc_n))
         HA = hh[:N].cpu().numpy().view(np.uint64)
         NA = nn[:N].cpu().numpy().view(np.uint32)
         C = d_common[:seg].cpu().numpy().view(np.uint16)
@@ -489,7 +491,7 @@ def main():
     if pmc_sk and pmc_sk.get("valu_insts_per_window_end"):
         # wave64 VALU instructions per launch (PMC count per window end, the
         # table copy and every loop overhead included) / launch time, against
-        # 1024 SIMDs x 2.4 GHz / 4 cycles per wave instruction
+        # 1024 SIMDs x 2.4 GHz / 2 cycles per wave instruction (VALU_PEAK_WAVE_INST)
         wi = pmc_sk["valu_insts_per_window_end"] * window_ends / 64
         ach = wi / avg_launch_s if avg_launch_s > 0 else 0.0
         valu.update({"bound": "valu_issue", "achieved": ach, "peak": VALU_PEAK_WAVE_INST,

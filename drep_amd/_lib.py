@@ -76,6 +76,8 @@ SIGNATURES = {
     "drephip_linkage_counts_device": (C.c_int, [vp, vp, vp, C.c_uint32, u32p, f64p, C.c_uint32,
                                                 np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS"),
                                                 C.c_int, f64p, vp]),
+    "drephip_linkage_reserve": (C.c_int, [vp, C.c_uint32]),
+    "drephip_last_linkage_stats": (C.c_int, [vp] + [C.POINTER(C.c_double)] * 5),
     "drephip_set_timing": (C.c_int, [vp, C.c_int]),
     "drephip_last_kernel_ms": (C.c_int, [vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
 }
@@ -235,6 +237,16 @@ class Context:
                 np.ascontiguousarray(lut_off, dtype=np.int32), self.LINK_METHODS[method], Z.reshape(-1), stream),
                 "drephip_linkage_counts_device")
         return Z
+
+    def linkage_reserve(self, n: int) -> None:
+        """Allocate the n x n linkage matrix now (drephip_linkage_reserve)."""
+        check(lib().drephip_linkage_reserve(self._h, int(n)), "drephip_linkage_reserve")
+
+    def linkage_stats(self):
+        """{alloc_s, matrix_s, chain_s, finish_s, wall_s} of the last linkage call."""
+        v = [C.c_double(0) for _ in range(5)]
+        check(lib().drephip_last_linkage_stats(self._h, *[C.byref(x) for x in v]), "drephip_last_linkage_stats")
+        return dict(zip(("alloc_s", "matrix_s", "chain_s", "finish_s", "wall_s"), (x.value for x in v)))
 
     def set_timing(self, on: bool = True, kernels=None) -> None:
         """HIP-event timing of kernel launches: all kernels, or only the

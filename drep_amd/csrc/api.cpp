@@ -705,12 +705,15 @@ DREPHIP_EXPORT int drephip_linkage(drephip_ctx *ctx, const double *y, uint32_t n
     if (!y || !Z) { set_error("null argument"); return DREPHIP_ERR_ARG; }
     if (n > 200000) { set_error("linkage supports n <= 200000 (n x n f64 matrix in HBM)"); return DREPHIP_ERR_UNSUPPORTED; }
     timing_begin(ctx);
+    ctx->link = LinkStats{};
+    const auto t0 = std::chrono::steady_clock::now();
     double *d_D;
     int rc = dist_from_condensed_impl(ctx, y, n, &d_D, ctx->stream);
     if (rc) return rc;
     rc = linkage_device_impl(ctx, d_D, n, method, Z, ctx->stream);
     if (rc) return rc;
     timing_collect(ctx);
+    ctx->link.wall_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return DREPHIP_OK;
 }
 
@@ -739,11 +742,34 @@ DREPHIP_EXPORT int drephip_linkage_counts_device(drephip_ctx *ctx, const uint16_
     if (rc) return rc;
     HIPC(hipStreamSynchronize(pick_stream(ctx, stream)));
     timing_begin(ctx);
+    ctx->link = LinkStats{};
+    const auto t0 = std::chrono::steady_clock::now();
     double *d_D;
     rc = dist_matrix_impl(ctx, d_common, d_denom, n, perm, lut, lut_len, lut_off, &d_D, ctx->stream);
     if (rc) return rc;
     rc = linkage_device_impl(ctx, d_D, n, method, Z, ctx->stream);
     if (rc) return rc;
     timing_collect(ctx);
+    ctx->link.wall_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return DREPHIP_OK;
+}
+
+DREPHIP_EXPORT int drephip_linkage_reserve(drephip_ctx *ctx, uint32_t n) {
+    GUARD_CTX(ctx);
+    if (n > 200000) { set_error("linkage supports n <= 200000 (n x n f64 matrix in HBM)"); return DREPHIP_ERR_UNSUPPORTED; }
+    if (n < 2) return DREPHIP_OK;
+    void *p;
+    return scratch(ctx, "lk_D", (uint64_t)n * n * 8, &p);
+}
+
+DREPHIP_EXPORT int drephip_last_linkage_stats(drephip_ctx *ctx, double *alloc_s, double *matrix_s, double *chain_s,
+                                              double *finish_s, double *wall_s) {
+    if (!ctx) { set_error("null context"); return DREPHIP_ERR_ARG; }
+    if (!alloc_s || !matrix_s || !chain_s || !finish_s || !wall_s) { set_error("null argument"); return DREPHIP_ERR_ARG; }
+    *alloc_s = ctx->link.alloc_s;
+    *matrix_s = ctx->link.matrix_s;
+    *chain_s = ctx->link.chain_s;
+    *finish_s = ctx->link.finish_s;
+    *wall_s = ctx->link.wall_s;
     return DREPHIP_OK;
 }

@@ -50,6 +50,14 @@ struct IngestStats {          // last drephip_sketch_files call
     uint32_t batches = 0;
 };
 
+struct LinkStats {            // last drephip_linkage* call, host wall clock (seconds)
+    double alloc_s = 0;       // device scratch for the n x n matrix (hipMalloc; 0 when reused)
+    double matrix_s = 0;      // matrix build from the counts / condensed input (incl. its H2D copies)
+    double chain_s = 0;       // nn-chain / MST steps (graph replays)
+    double finish_s = 0;      // Z readback + stable sort + relabel on the host
+    double wall_s = 0;        // the whole call
+};
+
 struct drephip_ctx {
     int device = 0;
     int k = 21;
@@ -111,6 +119,7 @@ struct drephip_ctx {
         hipEvent_t ev = nullptr;
     } apend;
     IngestStats ingest;
+    LinkStats link;
     PinnedSlot ingest_slots[2];   // the two pinned batch buffers, kept across calls
 };
 

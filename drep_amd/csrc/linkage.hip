@@ -25,6 +25,7 @@
 #include "../../include/drephip.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -34,6 +35,10 @@
 namespace drephip {
 
 constexpr int kLkWG = 256;
+
+static double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 struct LinkState {
     int32_t chain_len;
@@ -89,11 +94,19 @@ __device__ MinIdx block_argmin(double v, int32_t i) {
 // Every thread of the block must call it; the result is valid in thread 0.
 // The partial is an agent-scope atomic store (sc1), complete at the agent's
 // coherence point once vmcnt drains, so a RELAXED ticket after
-// s_waitcnt vmcnt(0) orders it: no release/acquire fence, whose gfx950 form
-// (buffer_wbl2 sc1 before the ticket, buffer_inv sc1 after) wrote back every
-// XCD's dirty L2 lines -- the step's row and column updates, which no other
-// workgroup of this launch reads (the next launch sees them at the kernel
-// boundary) -- once per workgroup per step.
+// s_waitcnt vmcnt(0) orders it: no release fence, whose gfx950 form
+// (buffer_wbl2 sc1 before the ticket) wrote back every XCD's dirty L2 lines --
+// the step's row and column updates, which no other workgroup of this launch
+// reads (the next launch sees them at the kernel boundary) -- once per
+// workgroup per step.  That ordering argument is about this ISA's sc1 store
+// path (gfx942/gfx950), not the HIP/LLVM memory model, so the file refuses
+// other targets.  The workgroup that draws the last ticket still runs an
+// agent-scope ACQUIRE fence before it reads the partials (one buffer_inv sc1
+// per step, in one workgroup): its reads cannot be served from lines cached
+// before the other workgroups' stores landed.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__) && !defined(__gfx942__)
+#error "linkage.hip's relaxed-ticket reduction relies on gfx942/gfx950 sc1 store completion at vmcnt(0)"
+#endif
 __device__ bool last_block(MinIdx part, MinIdx *parts, LinkState *st, MinIdx &out) {
     __shared__ int is_last;
     if (threadIdx.x == 0) {
@@ -106,6 +119,7 @@ __device__ bool last_block(MinIdx part, MinIdx *parts, LinkState *st, MinIdx &ou
     }
     __syncthreads();
     if (!is_last) return false;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     double bv = INFINITY;
     int32_t bi = 0x7fffffff;
     for (uint32_t b = threadIdx.x; b < gridDim.x; b += blockDim.x) {
@@ -417,6 +431,7 @@ static void sort_and_label(std::vector<double> &Z, uint32_t n) {
 
 int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, double *Z_out, hipStream_t st) {
     if (n < 2) return DREPHIP_OK;
+    const double t_chain = now_s();           // chain_s: scratch, graph capture and the steps
     if (method != DREPHIP_LINK_SINGLE && method != DREPHIP_LINK_COMPLETE && method != DREPHIP_LINK_AVERAGE &&
         method != DREPHIP_LINK_WEIGHTED) {
         set_error("linkage method must be single, complete, average or weighted");
@@ -496,10 +511,13 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     int32_t bad = 0;
     HIPC(hipMemcpy(&bad, &d_st->bad, 4, hipMemcpyDeviceToHost));
     if (bad) { set_error("linkage: a chain step found no valid partial"); return DREPHIP_ERR_INTERNAL; }
+    const double t_fin = now_s();
+    ctx->link.chain_s = t_fin - t_chain;
     std::vector<double> Z(4ull * (n - 1));
     HIPC(hipMemcpy(Z.data(), d_Z, Z.size() * 8, hipMemcpyDeviceToHost));
     sort_and_label(Z, n);
     std::copy(Z.begin(), Z.end(), Z_out);
+    ctx->link.finish_s = now_s() - t_fin;
     return DREPHIP_OK;
 }
 
@@ -511,7 +529,10 @@ int dist_matrix_impl(drephip_ctx *ctx, const uint16_t *d_common, const uint16_t 
     uint32_t *d_perm, *d_bad, *h_bad;
     int32_t *d_off;
     int rc;
+    const double t0 = now_s();
     if ((rc = scratch(ctx, "lk_D", (uint64_t)n * n * 8, (void **)&d_D))) return rc;
+    const double t1 = now_s();
+    ctx->link.alloc_s = t1 - t0;
     if ((rc = scratch(ctx, "lk_perm", n * 4ull, (void **)&d_perm))) return rc;
     if ((rc = scratch(ctx, "lk_bad", 4, (void **)&d_bad))) return rc;
     if ((rc = pinned_host(ctx, "lk_bad", 4, (void **)&h_bad))) return rc;
@@ -531,6 +552,7 @@ int dist_matrix_impl(drephip_ctx *ctx, const uint16_t *d_common, const uint16_t 
         set_error("a pair's denominator has no distance table (lut_off < 0) or its count exceeds it");
         return DREPHIP_ERR_ARG;
     }
+    ctx->link.matrix_s = now_s() - t1;
     *d_D_out = d_D;
     return DREPHIP_OK;
 }
@@ -539,13 +561,18 @@ int dist_from_condensed_impl(drephip_ctx *ctx, const double *y, uint32_t n, doub
     double *d_D, *d_y;
     int rc;
     const uint64_t np = (uint64_t)n * (n - 1) / 2;
+    const double t0 = now_s();
     if ((rc = scratch(ctx, "lk_D", (uint64_t)n * n * 8, (void **)&d_D))) return rc;
+    const double t1 = now_s();
+    ctx->link.alloc_s = t1 - t0;
     if ((rc = scratch(ctx, "lk_y", np * 8, (void **)&d_y))) return rc;
     HIPC(hipMemcpyAsync(d_y, y, np * 8, hipMemcpyHostToDevice, st));
     timing_mark(ctx, 3, st, true);
     launch_dist_tiles_condensed(DmFromCondensed{d_y}, n, d_D, st);
     timing_mark(ctx, 3, st, false);
     HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(st));
+    ctx->link.matrix_s = now_s() - t1;
     *d_D_out = d_D;
     return DREPHIP_OK;
 }

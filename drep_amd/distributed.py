@@ -203,21 +203,81 @@ def hip_synth_sketcher(ctx, L: int, family_size: int, seed: int, stream: int, de
     return fn
 
 
-def hip_file_sketcher(ctx, paths: Sequence[str], threads: int, device):
-    """Stage 1 for FASTA files: this rank's shard of the files read, packed
-    and sketched (drephip_sketch_files), then moved to the rank's GPU."""
+def hip_file_sketcher(ctx, paths: Sequence[str], threads: int, device, cached: Optional[Dict[int, object]] = None,
+                      lengths: Optional[np.ndarray] = None):
+    """Stage 1 for FASTA files (the files dRep passes, d_cluster.py:527-549):
+    this rank's shard of the files read, packed and sketched
+    (drephip_sketch_files), then moved to the rank's GPU.  `cached` maps a
+    genome index to the MashReference of its existing .msh sketch (dRep's
+    file-existence cache, d_cluster.py:541-542): those are not read at all.
+    Genome lengths (the .msh length field) go to `lengths` when given."""
     import torch
+    cached = cached or {}
 
     def fn(p: ShardPlan):
         s = ctx.s
         loc_h = torch.full((p.nmax, s), -1, dtype=torch.int64, device=device)
         loc_n = torch.zeros(p.nmax, dtype=torch.int32, device=device)
-        if p.g1 > p.g0:
-            h, nh, _ = ctx.sketch_files(list(paths[p.g0:p.g1]), threads=threads)
-            loc_h[:p.g1 - p.g0] = torch.from_numpy(h.view(np.int64)).to(device)
-            loc_n[:p.g1 - p.g0] = torch.from_numpy(nh.view(np.int32)).to(device)
+        n = p.g1 - p.g0
+        if n <= 0:
+            return loc_h, loc_n
+        h = np.full((n, s), np.iinfo(np.uint64).max, dtype=np.uint64)
+        nh = np.zeros(n, dtype=np.uint32)
+        ln = np.zeros(n, dtype=np.uint64)
+        todo = [i for i in range(n) if p.g0 + i not in cached]
+        for i in range(n):
+            ref = cached.get(p.g0 + i)
+            if ref is not None:
+                m = min(len(ref.hashes), s)
+                h[i, :m] = ref.hashes[:m]
+                nh[i] = m
+                ln[i] = ref.length
+        if todo:
+            th, tnh, tln = ctx.sketch_files([paths[p.g0 + i] for i in todo], threads=threads)
+            h[todo], nh[todo], ln[todo] = th, tnh, tln
+        if lengths is not None:
+            lengths[p.g0:p.g1] = ln
+        loc_h[:n] = torch.from_numpy(h.view(np.int64)).to(device)
+        loc_n[:n] = torch.from_numpy(nh.view(np.int32)).to(device)
         return loc_h, loc_n
     return fn
+
+
+def read_genome_list(bdb: Optional[str] = None, files: Optional[str] = None) -> Tuple[List[str], List[str]]:
+    """(names, locations) of the genomes to compare: a dRep Bdb table (CSV with
+    `genome` and `location` columns, data_tables/Bdb.csv) or a text file of
+    FASTA paths, one per line (names = basenames, as dRep's load_genomes /
+    _get_genome_name_from_fasta give them).  Locations keep Bdb's order,
+    duplicates dropped (d_cluster.py:527)."""
+    from .d_cluster import _get_genome_name_from_fasta
+    if bdb:
+        import pandas as pd
+        B = pd.read_csv(bdb)
+        l2g = B.set_index('location')['genome'].to_dict()
+        locs = list(B['location'].unique())
+        return [l2g[x] for x in locs], locs
+    locs: List[str] = []
+    for line in open(files):
+        line = line.strip()
+        if line and line not in locs:
+            locs.append(line)
+    return [_get_genome_name_from_fasta(x) for x in locs], locs
+
+
+def cached_sketches(data_folder: str, names: Sequence[str], s: int, group_size: int = 1000) -> Dict[int, object]:
+    """Existing sketches of the drop-in's work directory layout
+    (MASH_files/sketches/chunk_<i>/<genome>.msh, groupSize genomes per chunk;
+    d_cluster.py:531-542) that match (k, s, seed)."""
+    from .d_cluster import _load_cached
+    out: Dict[int, object] = {}
+    folder = os.path.join(data_folder, "MASH_files", "sketches")
+    for idx, name in enumerate(names):
+        f = os.path.join(folder, "chunk_%d" % (idx // group_size), name + ".msh")
+        if os.path.isfile(f):
+            ref = _load_cached(f, s)
+            if ref is not None:
+                out[idx] = ref
+    return out
 
 
 def hip_allpairs(ctx, stream: int, device):
@@ -242,7 +302,17 @@ def hip_linkage(ctx, names: Sequence[str], stream: int):
 
     def fn(common, denom, N, method):
         import torch
-        dens = np.array([ctx.s]) if denom is None else torch.unique(denom).cpu().numpy().view(np.uint16)
+        if denom is None:
+            dens = np.array([ctx.s])
+        else:
+            # denominators that occur, by a presence mask over 0..s filled in
+            # chunks (a torch.unique of the whole vector would sort 5x10^9
+            # entries and hold several GB of extra HBM at 10^5 genomes)
+            seen = torch.zeros(ctx.s + 1, dtype=torch.bool, device=denom.device)
+            step = 1 << 27
+            for a in range(0, denom.numel(), step):
+                seen[denom[a:a + step].to(torch.int64) & 0xFFFF] = True
+            dens = np.nonzero(seen.cpu().numpy())[0]
         lut, lut_off = linkage_tables(dens, ctx.s)
         return ctx.linkage_counts_device(common.data_ptr(), None if denom is None else denom.data_ptr(), N,
                                          linkage_order(names), lut, lut_off, method, stream)
@@ -256,9 +326,11 @@ def synthetic_names(N: int) -> List[str]:
 
 def main(argv: Optional[Sequence[str]] = None) -> int:
     """configs[3] as one job: `python -m torch.distributed.run --nproc-per-node 8
-    --master-addr 127.0.0.1 -m drep_amd.distributed --genomes 100000`.  Prints
-    one JSON line (rank 0); --out stores the condensed counts, the
-    primary_linkage pickle and the primary Cdb in drep_amd.store formats."""
+    --master-addr 127.0.0.1 -m drep_amd.distributed --genomes 100000`
+    (synthetic genomes), or over real FASTA files with --bdb Bdb.csv / --files
+    list.txt (and --data-folder for dRep's cached .msh sketches).  Prints one
+    JSON line (rank 0); --out stores the condensed counts, the primary_linkage
+    pickle and the primary Cdb in drep_amd.store formats."""
     import argparse
     import torch
     import torch.distributed as dist
@@ -272,6 +344,13 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
     ap.add_argument("--method", default="average")
     ap.add_argument("--P-ani", type=float, default=0.9)
     ap.add_argument("--out", default=None, help="work-directory data folder to store the results in")
+    ap.add_argument("--bdb", default=None, help="genomes from a dRep Bdb table (CSV: genome, location)")
+    ap.add_argument("--files", default=None, help="genomes from a text file of FASTA paths, one per line")
+    ap.add_argument("--data-folder", default=None,
+                    help="reuse cached sketches under <data-folder>/MASH_files/sketches/chunk_<i>/ (dRep layout)")
+    ap.add_argument("--group-size", type=int, default=1000, help="genomes per sketch chunk folder (dRep groupSize)")
+    ap.add_argument("--processors", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0),
+                    help="host threads for FASTA ingest per rank (0 = all)")
     a = ap.parse_args(argv)
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -283,17 +362,32 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
     else:
         dist.init_process_group(backend, rank=rank, world_size=world)
-    N = a.genomes
-    names = synthetic_names(N)
     ctx = _lib.Context(device=local, k=21, s=a.sketch, seed=42)
     stream = torch.cuda.current_stream(dev).cuda_stream
-    res = run_sharded(N, names, a.sketch, hip_synth_sketcher(ctx, a.genome_bp, a.family_size, a.seed, stream, dev),
-                      hip_allpairs(ctx, stream, dev), hip_linkage(ctx, names, stream), a.method, a.P_ani,
-                      sync=lambda: torch.cuda.synchronize(dev))
+    from_files = bool(a.bdb or a.files)
+    if from_files:
+        names, locations = read_genome_list(a.bdb, a.files)
+        N = len(names)
+        lengths = np.zeros(N, dtype=np.uint64)
+        cached = cached_sketches(a.data_folder, names, a.sketch, a.group_size) if a.data_folder else {}
+        sketch_fn = hip_file_sketcher(ctx, locations, a.processors, dev, cached, lengths)
+    else:
+        N = a.genomes
+        names = locations = synthetic_names(N)
+        lengths = np.full(N, a.genome_bp, np.uint64)
+        sketch_fn = hip_synth_sketcher(ctx, a.genome_bp, a.family_size, a.seed, stream, dev)
+    res = run_sharded(N, names, a.sketch, sketch_fn, hip_allpairs(ctx, stream, dev), hip_linkage(ctx, names, stream),
+                      a.method, a.P_ani, sync=lambda: torch.cuda.synchronize(dev))
+    if from_files and world > 1:
+        # every rank filled its shard's lengths: the root takes the element-wise max
+        allv = [None] * world
+        dist.all_gather_object(allv, lengths)
+        lengths = np.maximum.reduce(allv)
     if rank == 0:
         out = {"job": "configs[3]-style sharded Mash step + primary clustering", "genomes": N,
-               "genome_bp": a.genome_bp, "sketch": a.sketch, "n_gpus": world, "backend": backend,
-               "method": a.method, "P_ani": a.P_ani, "times": res["times"],
+               "input": ("files (%d cached sketches)" % len(cached)) if from_files else "synthetic",
+               "genome_bp": None if from_files else a.genome_bp, "sketch": a.sketch, "n_gpus": world,
+               "backend": backend, "method": a.method, "P_ani": a.P_ani, "times": res["times"],
                "pairs": N * (N - 1) // 2, "primary_clusters": int(res["Cdb"]["primary_cluster"].nunique())}
         t = res["times"]
         out["pairs_per_s_job"] = out["pairs"] / sum(v for k, v in t.items())
@@ -301,10 +395,9 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
             from .d_cluster import CondensedMash
             from .store import store_condensed, store_primary_linkage
             os.makedirs(a.out, exist_ok=True)
-            cm = CondensedMash(names, names, res["common"].cpu().numpy().view(np.uint16),
+            cm = CondensedMash(list(names), list(locations), res["common"].cpu().numpy().view(np.uint16),
                                None if res["denom"] is None else res["denom"].cpu().numpy().view(np.uint16),
-                               res["nhash"].cpu().numpy().view(np.uint32), np.full(N, a.genome_bp, np.uint64),
-                               a.sketch)
+                               res["nhash"].cpu().numpy().view(np.uint32), lengths, a.sketch)
             store_condensed(a.out, cm)
             store_primary_linkage(a.out, res["linkage"], None, res["arguments"])
             res["Cdb"].to_csv(os.path.join(a.out, "primary_Cdb.csv"), index=False)

@@ -88,7 +88,9 @@ def load_condensed(data_folder: str, mmap: bool = True) -> CondensedMash:
     if meta.get("denom_stored"):
         denom = np.load(os.path.join(d, "denom.npy"), mmap_mode=mode, allow_pickle=False)
     else:
-        denom = np.full(len(common), meta["s"], dtype=np.uint16)
+        # every sketch full: denominator s for every pair, as a zero-stride
+        # read-only view (np.full would be a 10 GB host array at N = 10^5)
+        denom = np.broadcast_to(np.uint16(meta["s"]), common.shape)
     names = open(os.path.join(d, "names.txt")).read().split("\n")[:meta["N"]]
     locs = open(os.path.join(d, "locations.txt")).read().split("\n")[:meta["N"]]
     return CondensedMash(names, locs, common, denom,

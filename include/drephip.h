@@ -252,6 +252,19 @@ int drephip_linkage_counts_device(drephip_ctx *ctx, const uint16_t *d_common, co
                                   uint32_t n, const uint32_t *perm, const double *lut, uint32_t lut_len,
                                   const int32_t *lut_off, int method, double *Z /* (n-1)*4 */, void *stream);
 
+/* Allocates (grow-only, kept in the context) the n x n f64 device matrix the
+ * next linkage call of size <= n uses, so that a caller can pay the
+ * allocation (80 GB at n = 10^5) outside the clustering step, e.g. before the
+ * sketch/all-pairs stages.  Same limits as drephip_linkage. */
+int drephip_linkage_reserve(drephip_ctx *ctx, uint32_t n);
+
+/* Host wall-clock split of the last drephip_linkage* call on this context
+ * (seconds): the matrix allocation (0 when reserved/reused), the matrix build,
+ * the chain (or MST) steps including their setup, the Z readback + scipy's
+ * stable sort and relabel, and the whole call. */
+int drephip_last_linkage_stats(drephip_ctx *ctx, double *alloc_s, double *matrix_s, double *chain_s,
+                               double *finish_s, double *wall_s);
+
 /* HIP-event timing of kernel launches: `kernels` is a bitmask of the kernels
  * to bracket with events (bit w = `which` w of drephip_last_kernel_ms; -1 =
  * all, 0 = none).  Each event pair adds a few microseconds of idle time

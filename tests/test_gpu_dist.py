@@ -52,3 +52,66 @@ def test_sharded_job_matches_single_rank(tmp_path):
         assert np.array_equal(cm.common, cm1.common)
         assert np.array_equal(pl["linkage"], pl1["linkage"])
         assert cdb.equals(cdb1)
+
+
+def _file_set(tmp_path, copies=6):
+    """The 4 reference FASTAs, each copied under `copies` distinct names, plus
+    Sakai as a location whose FASTA is absent and whose sketch is cached in the
+    work directory (as in the reference's own test work directory)."""
+    import shutil
+    golden = os.path.join(ROOT, "tests", "golden")
+    gdir = tmp_path / "genomes"
+    gdir.mkdir()
+    locs = []
+    for k in range(copies):
+        for fa in sorted(os.listdir(os.path.join(golden, "genomes"))):
+            dst = gdir / ("c%d_%s" % (k, fa))
+            shutil.copy(os.path.join(golden, "genomes", fa), dst)
+            locs.append(str(dst))
+    locs.append(str(gdir / "Escherichia_coli_Sakai.fna"))
+    sakai = os.path.join(golden, "MASH_files", "sketches", "Escherichia_coli_Sakai.fna.msh")
+
+    def data_folder(name):
+        d = tmp_path / name
+        chunk = d / "MASH_files" / "sketches" / "chunk_0"
+        chunk.mkdir(parents=True)
+        shutil.copy(sakai, chunk / "Escherichia_coli_Sakai.fna.msh")
+        return str(d)
+    return locs, data_folder
+
+
+@pytest.mark.timeout(600)
+def test_sharded_job_on_files_matches_drop_in(tmp_path):
+    """`drep_amd.distributed --files` (2 ranks sharing the GPU over gloo) on
+    real FASTA files plus a cached sketch: stored counts, Z and Cdb equal the
+    single-process drop-in's all_vs_all_MASH_condensed + cluster_mash_condensed
+    (reference path: d_cluster.py:527-549 sketch stage, 170-185 clustering)."""
+    import pandas as pd
+    from drep_amd.d_cluster import all_vs_all_MASH_condensed, cluster_mash_condensed
+    locs, data_folder = _file_set(tmp_path)
+    lst = tmp_path / "genomes.txt"
+    lst.write_text("\n".join(locs) + "\n")
+    Bdb = pd.DataFrame({"genome": [os.path.basename(x) for x in locs], "location": locs})
+    cm = all_vs_all_MASH_condensed(Bdb, data_folder("wd_single"), processors=4)
+    Cdb, (Z, _, _) = cluster_mash_condensed(cm, clusterAlg="average", P_ani=0.9)
+    assert int(cm.nhash[-1]) == 1000 and len(set(Cdb["primary_cluster"])) > 1
+    for world, port in ((2, 29641), (1, 29651)):
+        out = str(tmp_path / ("out%d" % world))
+        env = dict(os.environ, DREPHIP_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+               "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "drep_amd.distributed",
+               "--files", str(lst), "--data-folder", data_folder("wd_dist%d" % world), "--processors", "4",
+               "--out", out]
+        p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0, p.stderr[-3000:]
+        res = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+        assert res["input"] == "files (1 cached sketches)" and res["genomes"] == len(locs)
+        cmd_ = load_condensed(out, mmap=False)
+        pl = load_primary_linkage(out)
+        cdb = pd.read_csv(os.path.join(out, "primary_Cdb.csv"))
+        assert cmd_.names == cm.names and cmd_.locations == cm.locations
+        assert np.array_equal(cmd_.common, cm.common) and np.array_equal(cmd_.nhash, cm.nhash)
+        assert np.array_equal(cmd_.length, cm.length)
+        assert np.array_equal(pl["linkage"], Z)
+        assert np.array_equal(cdb["primary_cluster"].to_numpy(), Cdb["primary_cluster"].to_numpy())
+        assert list(cdb["genome"]) == list(Cdb["genome"])

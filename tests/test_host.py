@@ -430,3 +430,30 @@ def test_fasta_reader_kseq_corner_cases_vs_oracle(tmp_path, case):
               "fastq_empty_record": [b"ACGT", b""], "after_fastq_hunt": [b"AC", b"GGTT"],
               "crlf": [b"ACGTTA", b"AC"]}[case]
     assert [bytes(r) for r in recs] == expect
+
+
+def test_sharded_job_genome_list_and_cache(tmp_path):
+    """drep_amd.distributed's file inputs: a FASTA path list or a dRep Bdb
+    table give (names, locations) in Bdb order with basename names
+    (d_cluster.py:527, 632); the work directory's cached sketches are found in
+    the chunk folders of the drop-in's layout (d_cluster.py:531-542)."""
+    import shutil
+    import pandas as pd
+    from drep_amd.distributed import cached_sketches, read_genome_list
+    locs = ["/x/a.fna", "/y/b.fasta", "/x/a.fna", "/z/Escherichia_coli_Sakai.fna"]
+    lst = tmp_path / "l.txt"
+    lst.write_text("\n".join(locs) + "\n\n")
+    names, got = read_genome_list(files=str(lst))
+    assert got == ["/x/a.fna", "/y/b.fasta", "/z/Escherichia_coli_Sakai.fna"]
+    assert names == ["a.fna", "b.fasta", "Escherichia_coli_Sakai.fna"]
+    pd.DataFrame({"genome": ["A", "B", "A", "S"], "location": locs}).to_csv(tmp_path / "Bdb.csv", index=False)
+    n2, l2 = read_genome_list(bdb=str(tmp_path / "Bdb.csv"))
+    assert n2 == ["A", "B", "S"] and l2 == got
+    chunk = tmp_path / "wd" / "MASH_files" / "sketches" / "chunk_1"
+    chunk.mkdir(parents=True)
+    golden = os.path.join(os.path.dirname(__file__), "golden", "MASH_files", "sketches")
+    shutil.copy(os.path.join(golden, "Escherichia_coli_Sakai.fna.msh"), chunk / "Escherichia_coli_Sakai.fna.msh")
+    c = cached_sketches(str(tmp_path / "wd"), names, 1000, group_size=2)
+    assert list(c) == [2] and len(c[2].hashes) == 1000
+    assert cached_sketches(str(tmp_path / "wd"), names, 1000, group_size=1000) == {}
+    assert cached_sketches(str(tmp_path / "wd"), names, 500, group_size=2) == {}     # other s: not reused

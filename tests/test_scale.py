@@ -1,23 +1,28 @@
-"""BASELINE configs[2] and configs[3] in their one-GPU form: 10^4 and 10^5
-synthetic 5 Mbp genomes, s = 1000 -- sketch, all-pairs over the whole triangle
-(5x10^7 / 5x10^9 pairs; 10 GB of condensed counts in HBM at 10^5) and
-average-linkage primary clustering on the GPU (the n x n float64 matrix, 80 GB
-at 10^5, built in HBM from the counts).  Both sizes run by default; the
-GPU time is seconds (sketch 0.9 s, all-pairs 1.1 s, linkage 2.3 s at 10^5).
-DREPHIP_SCALE_N=<n> adds one more size.
+"""BASELINE configs[2], [3] and [4] in their one-GPU form: 10^4 and 10^5
+synthetic 5 Mbp genomes at s = 1000, and 10^4 genomes at s = 10^4 -- sketch,
+all-pairs over the whole triangle (5x10^7 / 5x10^9 pairs; 10 GB of condensed
+counts in HBM at 10^5) and average-linkage primary clustering on the GPU (the
+n x n float64 matrix, 80 GB at 10^5, built in HBM from the counts).  All three
+run by default.  DREPHIP_SCALE_N=<n> adds one more size (s = 1000).
 
-Parity at full size, through what the oracle can afford:
+Parity at full size:
+  * the WHOLE triangle against an independent implementation: every pair's
+    count is recomputed on the device by k_allpairs_merge (Mash's literal merge
+    loop, one lane per pair; oracle-pinned in tests/test_gpu.py) and compared
+    with the production kernel's (k_allpairs_q for s <= 2048, k_allpairs_band
+    above) -- full_triangle_mismatches must be 0 over all N(N-1)/2 pairs;
   * sketches of a seeded sample of genomes, regenerated and sketched on the
     host by the C oracle, bit-exact;
-  * shared-hash counts of 10^6 random pairs plus three whole rows (first,
-    last, random), recomputed by the oracle's Mash merge from the GPU sketches,
+  * shared-hash counts of random pairs plus three whole rows (first, last,
+    random), recomputed by the host oracle's Mash merge from the GPU sketches,
     bit-exact;
-  * a second all-pairs pass over the same sketches: identical triangle;
   * linkage Z: n-1 merges, monotone heights, consistent sizes; at 10^4 also
     bit-identical to scipy's linkage on the host (reference call:
     drep/d_cluster.py:453; ~1 s of host time).  At 10^5 the scipy comparison
     (121 s of host time) runs only with DREPHIP_SCALE_SCIPY=1.
-Timings go to DREPHIP_SCALE_OUT (default gpurun_out/scale_<N>.json)."""
+Timings go to DREPHIP_SCALE_OUT (default gpurun_out/scale_<N>[_s<s>].json).
+Reference knobs: MASH_sketch (drep/d_cluster.py:499; CLI -ms,
+drep/argumentParser.py:103); Mdb built at drep/d_cluster.py:575-596."""
 import json
 import os
 import subprocess
@@ -34,9 +39,15 @@ from drep_amd.d_cluster import linkage_tables
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SIZES = [10_000, 100_000]
+# (genomes, sketch size, BASELINE.json config)
+CASES = [pytest.param(10_000, 1000, "BASELINE.json configs[2] (1 GPU)", id="10000"),
+         pytest.param(100_000, 1000, "BASELINE.json configs[3] (1 GPU)", id="100000"),
+         pytest.param(10_000, 10_000, "BASELINE.json configs[4] (1 GPU)", id="10000-s10000")]
 if os.environ.get("DREPHIP_SCALE_N"):
-    SIZES.append(int(os.environ["DREPHIP_SCALE_N"]))
+    _n = int(os.environ["DREPHIP_SCALE_N"])
+    CASES.append(pytest.param(_n, int(os.environ.get("DREPHIP_SCALE_S", 1000)), "custom", id="custom%d" % _n))
+if os.environ.get("DREPHIP_SCALE_ONLY"):
+    CASES = [c for c in CASES if c.id in os.environ["DREPHIP_SCALE_ONLY"].split(",")]
 SCIPY_UP_TO = 10_000 if os.environ.get("DREPHIP_SCALE_SCIPY") != "1" else 10 ** 9
 
 
@@ -46,16 +57,48 @@ def _cond_index(i, j, N):
     return i * N - i * (i + 1) // 2 + (j - i - 1)
 
 
-@pytest.mark.parametrize("N", SIZES)
-@pytest.mark.timeout(600)
-def test_scale_sketch_allpairs_linkage_single_gpu(N):
+def full_triangle_check(ctx, hh, nn, N, d_common, note, parts=16):
+    """Every pair of the triangle recomputed by k_allpairs_merge (Mash's
+    literal loop) and compared on the device; row ranges of ~equal pair count,
+    so progress is reported while the (slower) literal kernel runs.  Returns
+    (mismatches, seconds, examples)."""
+    import torch
+    from drep_amd.parallel import cond_start, row_partition, segment_size
+    dev = d_common.device
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    bad, ex = 0, []
+    t0 = time.perf_counter()
+    for r0, r1 in row_partition(N, parts):
+        n = segment_size(N, r0, r1)
+        if n == 0:
+            continue
+        a = cond_start(r0, N)
+        b = a + n
+        seg = torch.empty(n, dtype=torch.int16, device=dev)
+        ctx.allpairs_device(hh.data_ptr(), nn.data_ptr(), N, r0, r1, seg.data_ptr(), None, stream, merge=True)
+        ne = d_common[a:b] != seg
+        nb = int(ne.sum().item())
+        if nb and len(ex) < 20:
+            w = torch.nonzero(ne)[:20 - len(ex), 0].cpu().numpy() + a
+            ex += [[int(t), int(d_common[t].item()), int(seg[t - a].item())] for t in w]
+        bad += nb
+        del seg, ne
+        note("full triangle: rows [%d, %d) checked, %d mismatches so far (%.1f s)"
+             % (r0, r1, bad, time.perf_counter() - t0))
+    torch.cuda.synchronize()
+    return bad, time.perf_counter() - t0, ex
+
+
+@pytest.mark.parametrize("N,s,config", CASES)
+@pytest.mark.timeout(900)
+def test_scale(N, s, config):
     import torch
     L = int(os.environ.get("DREPHIP_SCALE_L", 5_000_000))
-    s = 1000
     fam = 100
     seed = 0xD2E9
     CH = min(N, int(os.environ.get("DREPHIP_SCALE_CHUNK", 10000)))
-    out_path = os.environ.get("DREPHIP_SCALE_OUT", os.path.join(ROOT, "gpurun_out", "scale_%d.json" % N))
+    out_path = os.environ.get("DREPHIP_SCALE_OUT", os.path.join(
+        ROOT, "gpurun_out", "scale_%d%s.json" % (N, "" if s == 1000 else "_s%d" % s)))
     os.makedirs(os.path.dirname(out_path), exist_ok=True)
     log = open(os.path.splitext(out_path)[0] + ".progress", "a")
 
@@ -66,8 +109,7 @@ def test_scale_sketch_allpairs_linkage_single_gpu(N):
         log.flush()
 
     res = {"genomes": N, "genome_bp": L, "sketch": s, "family_size": fam, "pairs": N * (N - 1) // 2,
-           "config": {10_000: "BASELINE.json configs[2] (1 GPU)", 100_000: "BASELINE.json configs[3] (1 GPU)"}
-           .get(N, "custom")}
+           "config": config}
     dev = torch.device("cuda", 0)
     ctx = _lib.Context(device=0, k=21, s=s, seed=42)
     stream = torch.cuda.current_stream(dev).cuda_stream
@@ -107,16 +149,18 @@ def test_scale_sketch_allpairs_linkage_single_gpu(N):
     res["allpairs_s"] = time.perf_counter() - t0
     res["allpairs_pairs_per_s"] = npairs / res["allpairs_s"]
     note("allpairs %.3f s (%.3g pairs/s)" % (res["allpairs_s"], res["allpairs_pairs_per_s"]))
-    # idempotence: a second pass over the same sketches gives the same triangle
-    d_again = torch.zeros(npairs, dtype=torch.int16, device=dev)
-    ctx.allpairs_device(hh.data_ptr(), nn.data_ptr(), N, 0, N, d_again.data_ptr(), None, stream)
-    torch.cuda.synchronize()
-    ndiff = int((d_again != d_common).sum().item())
-    res["second_pass_differences"] = ndiff
-    del d_again
+
+    # ---- parity: the whole triangle against the literal-merge kernel
+    nbad, t_full, ex = full_triangle_check(ctx, hh, nn, N, d_common, note)
+    res["full_triangle_pairs"] = npairs
+    res["full_triangle_mismatches"] = nbad
+    res["full_triangle_check_s"] = t_full
+    res["full_triangle_checker"] = "k_allpairs_merge (Mash's literal merge loop, one lane per pair)"
+    if nbad:
+        res["full_triangle_mismatch_examples"] = ex
+        json.dump(res, open(out_path, "w"), indent=1)
     torch.cuda.empty_cache()
-    note("second pass differences: %d" % ndiff)
-    assert ndiff == 0
+    assert nbad == 0
 
     # ---- parity: sketches of sampled genomes (host oracle regenerates the genome)
     H = hh.cpu().numpy().view(np.uint64)
@@ -134,7 +178,7 @@ def test_scale_sketch_allpairs_linkage_single_gpu(N):
     note("sketch parity ok")
 
     # ---- parity: counts of random pairs and of whole rows, recomputed by the oracle
-    M = 1_000_000
+    M = 1_000_000 if s <= 2048 else 100_000      # host merge cost grows with s
     pi = rng.integers(0, N - 1, M)
     pj = pi + 1 + (rng.random(M) * (N - 1 - pi)).astype(np.int64)
     for r in (0, N - 2, int(rng.integers(1, N - 2))):
@@ -164,7 +208,19 @@ def test_scale_sketch_allpairs_linkage_single_gpu(N):
     res["linkage_s"] = time.perf_counter() - t0
     res["linkage_matrix_build_ms"] = ctx.kernel_ms(3)[0]
     res["linkage_chain_ms"] = ctx.kernel_ms(2)[0]
-    note("gpu linkage %.2f s" % res["linkage_s"])
+    res["linkage_phases_s"] = ctx.linkage_stats()
+    note("gpu linkage %.2f s %s" % (res["linkage_s"], json.dumps(res["linkage_phases_s"])))
+    # the same call again with the matrix already allocated (drephip_linkage_reserve
+    # semantics: the 80 GB allocation outside the clustering step)
+    t0 = time.perf_counter()
+    Z2 = ctx.linkage_counts_device(d_common.data_ptr(), None, N, perm, lut, lut_off, "average")
+    res["linkage_reserved_s"] = time.perf_counter() - t0
+    res["linkage_reserved_phases_s"] = ctx.linkage_stats()
+    res["linkage_reserved_chain_ms"] = ctx.kernel_ms(2)[0]
+    note("gpu linkage (matrix reserved) %.2f s %s" % (res["linkage_reserved_s"],
+                                                      json.dumps(res["linkage_reserved_phases_s"])))
+    assert np.array_equal(Z, Z2)
+    del Z2
     assert Z.shape == (N - 1, 4)
     assert np.all(np.diff(Z[:, 2]) >= 0)           # average linkage is monotone
     assert Z[-1, 3] == N
