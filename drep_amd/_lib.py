@@ -71,6 +71,8 @@ SIGNATURES = {
     "drephip_allpairs_wait": (C.c_int, [vp]),
     "drephip_allpairs_merge_device": (C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp]),
     "drephip_distance_lut": (C.c_int, [C.c_int, C.c_uint32, f64p]),
+    "drephip_write_mash_table": (C.c_int, [C.c_char_p, C.POINTER(C.c_char_p), C.c_uint32, vp, vp, C.c_uint32,
+                                           vp, vp, u16p, f64p, C.c_int]),
     "drephip_set_allpairs_path": (C.c_int, [vp, C.c_int, C.c_uint32]),
     "drephip_linkage": (C.c_int, [vp, f64p, C.c_uint32, C.c_int, f64p]),
     "drephip_linkage_counts_device": (C.c_int, [vp, vp, vp, C.c_uint32, u32p, f64p, C.c_uint32,
@@ -157,6 +159,27 @@ def distance_lut(denom: int, k: int = 21) -> np.ndarray:
     out = np.zeros(denom + 1, dtype=np.float64)
     check(lib().drephip_distance_lut(k, denom, out), "drephip_distance_lut")
     return out
+
+
+def write_mash_table(path: str, names: Sequence[str], common: np.ndarray, denom: Optional[np.ndarray], s: int,
+                     dist: np.ndarray, pval: np.ndarray, self_count: np.ndarray, self_pval: np.ndarray,
+                     threads: int = 0) -> None:
+    """drephip_write_mash_table: condensed arrays (i < j), names of the N genomes."""
+    N = len(names)
+    npairs = N * (N - 1) // 2
+    common = np.ascontiguousarray(common, dtype=np.uint16)
+    dist = np.ascontiguousarray(dist, dtype=np.float64)
+    pval = np.ascontiguousarray(pval, dtype=np.float64)
+    for a in (common, dist, pval) + ((denom,) if denom is not None else ()):
+        if len(a) != npairs:
+            raise ValueError("condensed arrays must hold N(N-1)/2 = %d entries" % npairs)
+    den = None if denom is None else np.ascontiguousarray(denom, dtype=np.uint16)
+    arr = (C.c_char_p * max(N, 1))(*[os.fsencode(n) for n in names])
+    check(lib().drephip_write_mash_table(os.fsencode(path), arr, N, common.ctypes.data,
+                                         None if den is None else den.ctypes.data, int(s), dist.ctypes.data,
+                                         pval.ctypes.data, np.ascontiguousarray(self_count, dtype=np.uint16),
+                                         np.ascontiguousarray(self_pval, dtype=np.float64), int(threads)),
+          "drephip_write_mash_table(%s)" % path)
 
 
 def fasta_info(path: str, k: int = 21):

@@ -384,30 +384,46 @@ def mash_pvalue(common: np.ndarray, len_r: np.ndarray, len_q: np.ndarray, s: int
     return np.where(c == 0, 1.0, p)
 
 
-def write_mash_table(path: str, cm: CondensedMash) -> None:
+def write_mash_table(path: str, cm: CondensedMash, threads: int = 0) -> None:
     """MASH_table.tsv as `mash dist ALL ALL` prints it (d_cluster.py:570-572):
     reference, query, %g distance, %g p-value, common/denom; outer loop over
-    queries.  N^2 lines (15 GB of text at 10^4 genomes) -- only for callers
-    that read the raw table; one query row at a time, distances by table
-    lookup per denominator, p-values vectorised over the row."""
+    queries.  N^2 lines (10^8 at 10^4 genomes).  Distances (per-denominator
+    tables) and p-values are computed once per unordered pair -- both are
+    symmetric in (reference, query) -- and only for pairs sharing a hash (the
+    p-value of c = 0 is 1); libdrephip formats the text on `threads` host
+    threads (drephip_write_mash_table)."""
     N = len(cm.names)
-    nh = np.minimum(cm.nhash.astype(np.int64), cm.s)
-    Cm = _square(np.asarray(cm.common), N, nh.astype(np.uint16)).astype(np.int64)
-    Dm = _square(np.asarray(cm.denom), N, nh.astype(np.uint16)).astype(np.int64)
-    luts = {int(d): (_lib.distance_lut(int(d), MASH_K) if d else np.zeros(1)) for d in np.unique(Dm)}
-    refs = list(cm.locations)
-    with open(path, 'w') as fh:
-        for q in range(N):
-            dist = np.empty(N)
-            for d, lut in luts.items():
-                sel = Dm[q] == d
-                if sel.any():
-                    dist[sel] = lut[Cm[q, sel]]
-            p = mash_pvalue(Cm[q], cm.length, np.full(N, cm.length[q]), cm.s)
-            qn = refs[q]
-            fh.write("".join("%s\t%s\t%g\t%g\t%d/%d\n" % (r, qn, x, y, c, d)
-                             for r, x, y, c, d in zip(refs, dist.tolist(), p.tolist(), Cm[q].tolist(),
-                                                      Dm[q].tolist())))
+    common = np.asarray(cm.common, dtype=np.uint16)
+    denom = np.asarray(cm.denom, dtype=np.uint16)
+    length = np.asarray(cm.length, dtype=np.float64)
+    dist = np.empty(len(common), dtype=np.float64)
+    for d in np.unique(denom):
+        sel = denom == d
+        lut = _lib.distance_lut(int(d), MASH_K) if d else np.zeros(1)
+        dist[sel] = lut[common[sel]]
+    pval = np.ones(len(common), dtype=np.float64)
+    nz = np.nonzero(common)[0]
+    if len(nz):
+        iu, ju = _condensed_ij(nz, N)
+        pval[nz] = mash_pvalue(common[nz], length[iu], length[ju], cm.s)
+    self_count = np.minimum(np.asarray(cm.nhash, dtype=np.int64), cm.s).astype(np.uint16)
+    self_pval = mash_pvalue(self_count, length, length, cm.s)
+    full = bool((denom == cm.s).all())
+    _lib.write_mash_table(path, list(cm.locations), common, None if full else denom, cm.s, dist, pval,
+                          self_count, self_pval, threads)
+
+
+def _condensed_ij(t: np.ndarray, N: int):
+    """(i, j), i < j, of condensed indices t (scipy squareform order)."""
+    t = np.asarray(t, dtype=np.int64)
+    Mf = 2.0 * N - 1.0
+    i = np.floor((Mf - np.sqrt(np.maximum(Mf * Mf - 8.0 * t, 0.0))) / 2.0).astype(np.int64)
+    i = np.clip(i, 0, max(N - 2, 0))
+    for _ in range(2):
+        i = np.where(i * N - i * (i + 1) // 2 > t, i - 1, i)
+        i = np.where((i + 1) * N - (i + 1) * (i + 2) // 2 <= t, i + 1, i)
+    j = t - (i * N - i * (i + 1) // 2) + i + 1
+    return i, j
 
 
 # ------------------------------------------------------ primary clustering

@@ -212,6 +212,20 @@ int drephip_allpairs_merge_device(drephip_ctx *ctx, const uint64_t *d_hashes, co
  * Reference: the "dist" column of MASH_table.tsv parsed at d_cluster.py:581. */
 int drephip_distance_lut(int k, uint32_t denom, double *lut /* denom+1 */);
 
+/* MASH_table.tsv as `mash dist -p P ALL.msh ALL.msh > MASH_table.tsv` prints
+ * it (drep/d_cluster.py:569-573): for every query q (outer loop) and reference
+ * r, "names[r]\tnames[q]\t%g dist\t%g p-value\tcommon/denom\n".  Pairs come
+ * from the condensed result (index(i, j), i < j; denom NULL = s for every
+ * pair) with their distances and p-values (caller-computed: Mash's formula,
+ * drephip_distance_lut; p-values with the binomial tail); a genome against
+ * itself prints distance 0, self_pval[q] and self_count[q]/self_count[q].
+ * Host only; rows are formatted on `threads` threads (0 = all) and written in
+ * order. */
+int drephip_write_mash_table(const char *path, const char *const *names, uint32_t N,
+                             const uint16_t *common, const uint16_t *denom /* nullable */, uint32_t s,
+                             const double *dist, const double *pval, const uint16_t *self_count,
+                             const double *self_pval, int threads);
+
 /* All-pairs kernel selection (no CPU path exists; every choice is a HIP kernel
  * with the same bit-exact result):
  *   DREPHIP_AP_AUTO  whole-row LDS tables for s <= 2048, value bands above;

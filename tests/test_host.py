@@ -457,3 +457,30 @@ def test_sharded_job_genome_list_and_cache(tmp_path):
     assert list(c) == [2] and len(c[2].hashes) == 1000
     assert cached_sketches(str(tmp_path / "wd"), names, 1000, group_size=1000) == {}
     assert cached_sketches(str(tmp_path / "wd"), names, 500, group_size=2) == {}     # other s: not reused
+
+
+def test_write_mash_table_vs_line_by_line(tmp_path):
+    """The threaded C writer against a line-by-line restatement of `mash dist`'s
+    output (query outer, reference inner, %g, common/denom) on a family set
+    with partial sketches (denominators < s) and distinct genome lengths."""
+    n = 37
+    h, nh = oracle.sketch_synth(0, n, 60_000, seed=5, family_size=6, threads=4)
+    for g in (3, 17):                                    # partial sketches
+        h[g, 400:] = np.iinfo(np.uint64).max
+        nh[g] = 400
+    c, d = oracle.allpairs(h, nh, S)
+    names = ["/data/g%02d.fa" % i for i in range(n)]
+    length = np.arange(n, dtype=np.uint64) * 1000 + 60_000
+    cm = d_cluster.CondensedMash(names, names, c, d, nh, length, S)
+    out = tmp_path / "t.tsv"
+    d_cluster.write_mash_table(str(out), cm, threads=3)
+    Cm = d_cluster._square(c, n, np.minimum(nh, S).astype(np.uint16)).astype(np.int64)
+    Dm = d_cluster._square(d, n, np.minimum(nh, S).astype(np.uint16)).astype(np.int64)
+    lines = []
+    for q in range(n):
+        for r in range(n):
+            lut = _lib.distance_lut(int(Dm[q, r])) if Dm[q, r] else np.zeros(1)
+            p = d_cluster.mash_pvalue(np.array([Cm[q, r]]), np.array([float(length[r])]),
+                                      np.array([float(length[q])]), S)[0]
+            lines.append("%s\t%s\t%g\t%g\t%d/%d\n" % (names[r], names[q], lut[Cm[q, r]], p, Cm[q, r], Dm[q, r]))
+    assert out.read_text() == "".join(lines)
