@@ -290,9 +290,18 @@ __device__ __forceinline__ void probe_rows(const Slots<R> &sl, uint64_t b, uint3
         // one test for all rows first (a min3 chain, one compare, one ballot,
         // one branch): most chunks hit no row.  Inactive rows take part; they
         // can only send a chunk to the per-row tests, which skip them.
-        uint32_t mn = min(xs1[0], xs2[0]);
+        // (R = 4: a v_min3 tree over the eight words, 4 VALU; the per-row
+        // minima are formed only on the rare hit path)
+        uint32_t mn;
+        if constexpr (R == 4) {
+            const uint32_t m1 = min(min(xs1[0], xs1[1]), xs1[2]);
+            const uint32_t m2 = min(min(xs1[3], xs2[0]), xs2[1]);
+            mn = min(min(m1, m2), min(xs2[2], xs2[3]));
+        } else {
+            mn = min(xs1[0], xs2[0]);
 #pragma unroll
-        for (int r = 1; r < R; r++) mn = min(mn, min(xs1[r], xs2[r]));
+            for (int r = 1; r < R; r++) mn = min(mn, min(xs1[r], xs2[r]));
+        }
         if ((__builtin_amdgcn_ballot_w64(mn <= hm) & lanemask) == 0) return;
     }
 #pragma unroll
@@ -364,8 +373,23 @@ __device__ __forceinline__ uint64_t ld_chunk(__amdgpu_buffer_rsrc_t rs, uint32_t
     const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, lane_off, rfl(chunk) * 512u, 0);
     return ((uint64_t)v[1] << 32) | v[0];
 }
+// the same with the chunk's byte offset split into a per-group SGPR (soff) and
+// a constant (CB, the instruction's immediate offset field)
+template <uint32_t CB>
+__device__ __forceinline__ uint64_t ld_chunk_at(__amdgpu_buffer_rsrc_t rs, uint32_t lane_off, uint32_t soff) {
+    static_assert(CB < 4096, "MUBUF immediate offset");
+    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, lane_off + CB, soff, 0);
+    return ((uint64_t)v[1] << 32) | v[0];
+}
 
-template <int R, int NCH, bool FAST, int KB>
+// MASKED = false (the common case): no per-chunk tail work at all.  Lanes and
+// chunks past s read 0 through the buffer bounds, and an element 0 can only
+// hit a row holding the key 0 itself (the probe needs the low word 0 in a slot
+// and V == 0), so when no active row's smallest key is 0 the chunks are
+// probed unmasked and unclamped: no tail mask, no chunk-in-range test, no
+// refill clamp -- only the group loop and the early-end tests are scalar
+// work.  MASKED = true keeps them (rows holding the key 0, the generic probe).
+template <int R, int NCH, bool FAST, int KB, bool MASKED>
 __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ nhash,
                                            const uint32_t *T, const uint32_t *V, uint32_t H, uint32_t hm, uint32_t s,
                                            uint32_t N, uint32_t i0, uint32_t nrows, uint32_t cend, uint32_t c_first,
@@ -384,21 +408,25 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
 #pragma unroll
     for (int r = 0; r < R; r++) zero[r] = 0;
     uint32_t c = rfl(c_first);                                       // wave-uniform: scalar column loop
-    if (c < cend) {
-        const __amdgpu_buffer_rsrc_t rn = column_rsrc(hashes + (uint64_t)c * s, s);
+    auto first_chunks = [&](__amdgpu_buffer_rsrc_t rn) {
+        if constexpr (MASKED) {
 #pragma unroll
-        for (int k = 0; k < kRing; k++) nx[k] = ld_chunk(rn, lane_off, min((uint32_t)k, nch - 1));
-    }
+            for (int k = 0; k < kRing; k++) nx[k] = ld_chunk(rn, lane_off, min((uint32_t)k, nch - 1));
+        } else {
+            nx[0] = ld_chunk_at<0>(rn, lane_off, 0);
+            nx[1] = ld_chunk_at<512>(rn, lane_off, 0);
+            nx[2] = ld_chunk_at<1024>(rn, lane_off, 0);
+            nx[3] = ld_chunk_at<1536>(rn, lane_off, 0);
+        }
+    };
+    static_assert(kRing == 4, "first_chunks / refill offsets");
+    if (c < cend) first_chunks(column_rsrc(hashes + (uint64_t)c * s, s));
     for (; c < cend; c += c_step) {
         const __amdgpu_buffer_rsrc_t rc = column_rsrc(hashes + (uint64_t)c * s, s);
 #pragma unroll
         for (int k = 0; k < kRing; k++) rg[k] = nx[k];
         const uint32_t cn = c + c_step;
-        if (cn < cend) {
-            const __amdgpu_buffer_rsrc_t rn = column_rsrc(hashes + (uint64_t)cn * s, s);
-#pragma unroll
-            for (int k = 0; k < kRing; k++) nx[k] = ld_chunk(rn, lane_off, min((uint32_t)k, nch - 1));
-        }
+        if (cn < cend) first_chunks(column_rsrc(hashes + (uint64_t)cn * s, s));
         uint32_t cnt[R], mrun[R], actmask = 0;
         // elements past every active row's largest hash cannot match: the
         // scan ends at the first chunk whose smallest element is past them
@@ -450,12 +478,14 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
                     if (all_past) break;
                 }
             }
+            const uint32_t gofs = rfl(kb) * 512u;                        // the group's byte offset (SGPR)
 #pragma unroll
             for (int u = 0; u < kRing; u++) {
                 const uint32_t k = kb + u;
                 const uint64_t b = rg[u];
-                // lanes past s in the last chunk read 0 (buffer bounds): masked out
-                const uint64_t lm = k == nch - 1 ? tailmask : ~0ull;
+                // lanes past s in the last chunk read 0 (buffer bounds): masked
+                // out (MASKED), or harmless (see above)
+                const uint64_t lm = MASKED ? (k == nch - 1 ? tailmask : ~0ull) : ~0ull;
                 // chunk k + kSlotAhead: in rg[(u + kSlotAhead) % kRing] (refilled
                 // earlier in this group when that index is below u)
                 sb[(u + kSlotAhead) % kRing] =
@@ -464,15 +494,23 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
                 // probe: the ring and slot updates above stay unconditional, or
                 // the compiler merges the ring registers through a copy that
                 // waits for the refill load issued in the same chunk
-                if (k < nch)                                              // wave-uniform
+                if (!MASKED || k < nch)                                   // wave-uniform
                     probe_rows<R, FAST, !FAST, true>(sb[u], b, k * 64 + lane, V, s, hm, o1, o2, actmask, lm, zero, nA, s,
                                                mrun, cnt);
-                // refill the ring unconditionally (past the end: the last chunk
-                // again) and after the chunk's last use, so the load reuses the
-                // chunk's registers: a conditional update, or one while the old
-                // value is live, makes the compiler copy the ring at the loop
-                // back edge behind a wait for the loads just issued
-                rg[u] = ld_chunk(rc, lane_off, min(k + kRing, nch - 1));
+                // refill the ring unconditionally and after the chunk's last use,
+                // so the load reuses the chunk's registers: a conditional update,
+                // or one while the old value is live, makes the compiler copy the
+                // ring at the loop back edge behind a wait for the loads just
+                // issued.  MASKED: past the end, the last chunk again; else the
+                // chunk itself (zeros past s), its offset in the immediate field
+                if constexpr (MASKED) {
+                    rg[u] = ld_chunk(rc, lane_off, min(k + kRing, nch - 1));
+                } else {
+                    if (u == 0) rg[u] = ld_chunk_at<(0 + kRing) * 512>(rc, lane_off, gofs);
+                    if (u == 1) rg[u] = ld_chunk_at<(1 + kRing) * 512>(rc, lane_off, gofs);
+                    if (u == 2) rg[u] = ld_chunk_at<(2 + kRing) * 512>(rc, lane_off, gofs);
+                    if (u == 3) rg[u] = ld_chunk_at<(3 + kRing) * 512>(rc, lane_off, gofs);
+                }
             }
         }
         if (lane == 0) {
@@ -539,14 +577,14 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
     uint32_t nA[R], o1[R], o2[R];
     uint64_t alast[R], thr1[R], thr2[R];
     uint32_t failmask = 0;
-    bool any_partial_row = false, fast = true;
+    bool any_partial_row = false, fast = true, zero_key = false;
     {   // per-row scalars: uniform loads with clamped rows, no branches, so none
         // of them waits on the image's DMA above (the family bytes as one
         // aligned 8-byte word; the fam buffer is padded to 8 bytes)
         const uint32_t fi = i0 - row0;
         const uint64_t fw = *(const uint64_t *)(fam + (fi & ~7u));
         uint32_t nraw[R];
-        uint64_t lraw[R], t1raw[R], t2raw[R];
+        uint64_t lraw[R], t1raw[R], t2raw[R], fraw[R];
         // union-rank thresholds (ap_columns): A_r[s - j0 - 1] for the two test
         // groups, j0 = 64 kb1 and 64 (kb1 + 4); positions below 0 clamp to 0
         // (never used then: such a group does not exist or the test is moot)
@@ -559,6 +597,7 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
             lraw[r] = hashes[(uint64_t)i * s + s - 1];
             t1raw[r] = hashes[(uint64_t)i * s + p1];
             t2raw[r] = hashes[(uint64_t)i * s + p2];
+            fraw[r] = hashes[(uint64_t)i * s];
         }
 #pragma unroll
         for (int r = 0; r < R; r++) {
@@ -576,6 +615,7 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
             thr1[r] = (ok && s > 64 * kb1 && p1 < nA[r]) ? t1raw[r] : kEmpty;
             thr2[r] = (ok && s > 64 * (kb1 + 4) && p2 < nA[r]) ? t2raw[r] : kEmpty;
             any_partial_row |= nA[r] < s;
+            zero_key |= ok && fraw[r] == 0;                  // the row holds the hash value 0 (MASKED probe)
         }
     }
     __syncthreads();
@@ -583,12 +623,18 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
     // The kernel declares no static LDS (.group_segment_fixed_size 0, checked
     // by tests/test_host.py), so `lds` is LDS address 0 (read_slots).
     constexpr int KB = NCH == 16 ? 11 : 0;
-    if (fast)
-        ap_columns<R, NCH, true, KB>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend, c0 + wave, WG / 64,
-                                     nA, o1, o2, alast, thr1, thr2, ~failmask, any_partial_row, common, denom, seg0);
+    if (fast && !zero_key)
+        ap_columns<R, NCH, true, KB, false>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend, c0 + wave, WG / 64,
+                                            nA, o1, o2, alast, thr1, thr2, ~failmask, any_partial_row, common, denom,
+                                            seg0);
+    else if (fast)
+        ap_columns<R, NCH, true, KB, true>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend, c0 + wave, WG / 64,
+                                           nA, o1, o2, alast, thr1, thr2, ~failmask, any_partial_row, common, denom,
+                                           seg0);
     else
-        ap_columns<R, NCH, false, KB>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend, c0 + wave, WG / 64,
-                                      nA, o1, o2, alast, thr1, thr2, ~failmask, any_partial_row, common, denom, seg0);
+        ap_columns<R, NCH, false, KB, true>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend, c0 + wave, WG / 64,
+                                            nA, o1, o2, alast, thr1, thr2, ~failmask, any_partial_row, common, denom,
+                                            seg0);
     if (failmask) {
         // a row whose table could not be built (three of its keys share a low
         // word under every field family; never observed on real sketches):
