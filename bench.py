@@ -38,7 +38,9 @@ SKETCH_ISA = os.path.join(ROOT, "profiles", "r02_sketch_isa.json")
 # committed PMC summaries (tools/pmc_summary.py): VALU / LDS utilisation of the
 # two kernels, reported next to the live timings
 SKETCH_PMC = os.path.join(ROOT, "profiles", "r02_sketch_pmc_sq.json")
-DIST_PMC = os.path.join(ROOT, "profiles", "r02_allpairs_pmc_sq_N6000.json")
+# all-pairs profiles of tools/profile_allpairs.sh, one per (N, s) case: the
+# bench line quotes the one of its own workload (never another N's)
+DIST_PROFILE = os.path.join(ROOT, "profiles", "r03_allpairs_N%d%s.json")
 SKETCH_TRAFFIC = os.path.join(ROOT, "profiles", "r02_sketch_traffic.json")
 PROFILE_STEPS = 3              # untimed steps that time finalize / all-pairs / table build
 VERIFY_GENOMES = 16            # timed-step sketches re-derived by the C oracle (sampled, every run)
@@ -60,6 +62,34 @@ def mix_priced_cycles(isa):
             c = 1.45 if op.endswith("_e32") else 2.6
         total += n * c
     return total
+
+
+def dist_roofline(N, s, pairs_per_launch, launch_ms):
+    """Roofline block of the all-pairs kernel from the committed profile of
+    this exact workload (tools/profile_allpairs.sh): VALU issue against the
+    2-cycle wave64 peak (the PMC's VALU instructions per pair x this launch's
+    pairs / this launch's live HIP-event time), LDS busy, HBM traffic and L2
+    hit rate of the profiled dispatches."""
+    path = DIST_PROFILE % (N, "" if s == 1000 else "_s%d" % s)
+    if not os.path.exists(path):
+        return {"note": "no all-pairs profile committed for N=%d s=%d (%s)" % (N, s, os.path.relpath(path, ROOT))}
+    d = json.load(open(path))
+    dv = d.get("derived", {})
+    out = {"kernel": (d.get("kernel") or "")[:60], "source": os.path.relpath(path, ROOT),
+           "profiled_avg_dispatch_ms": d.get("avg_dispatch_ms")}
+    if dv.get("valu_wave_insts_per_pair") and launch_ms:
+        ach = dv["valu_wave_insts_per_pair"] * pairs_per_launch / (launch_ms * 1e-3)
+        out.update({"bound": "valu+lds", "achieved": ach, "peak": VALU_PEAK_WAVE_INST,
+                    "unit": "wave64 VALU instructions/s", "frac": ach / VALU_PEAK_WAVE_INST,
+                    "valu_wave_insts_per_pair": dv["valu_wave_insts_per_pair"],
+                    "salu_over_valu": dv.get("salu_over_valu")})
+    for k in ("lds_busy_frac", "lds_bank_conflict_frac", "valu_issue_frac_2cyc", "wait_inst_any_frac",
+              "wait_any_frac", "l2_hit_rate", "hbm_bytes_x2", "hbm_GBps_x2", "hbm_frac_of_8TBps_x2",
+              "algorithmic_bytes", "effective_clock_ghz"):
+        if k in dv:
+            out[k] = dv[k]
+    out["traffic"] = dv.get("hbm_bytes_x2")
+    return out
 
 
 def pmc_block(path):
@@ -618,7 +648,8 @@ def main():
                 "pairs_per_launch": segment_size(N, r0, r1),
                 "pairs_per_s_per_gpu": (segment_size(N, r0, r1) / (kms[2][0] / max(kms[2][1], 1) / 1e3)
                                         if kms[2][0] else None),
-                "pmc": pmc_block(DIST_PMC),
+                "roofline": dist_roofline(N, args.sketch, segment_size(N, r0, r1),
+                                          kms[2][0] / max(kms[2][1], 1)),
             },
             "cpu_baseline": cpu,
         }

@@ -376,7 +376,26 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
         names = locations = synthetic_names(N)
         lengths = np.full(N, a.genome_bp, np.uint64)
         sketch_fn = hip_synth_sketcher(ctx, a.genome_bp, a.family_size, a.seed, stream, dev)
-    res = run_sharded(N, names, a.sketch, sketch_fn, hip_allpairs(ctx, stream, dev), hip_linkage(ctx, names, stream),
+    # the root's n x n linkage matrix (80 GB at 10^5: ~2 s of hipMalloc) is
+    # allocated by a separate context on a helper thread while the sketch and
+    # all-pairs stages run, so the serial clustering tail does not pay for it
+    link_ctx, reserve = ctx, None
+    if rank == 0 and N >= 2:
+        import threading
+        link_ctx = _lib.Context(device=local, k=21, s=a.sketch, seed=42)
+        reserve = threading.Thread(target=link_ctx.linkage_reserve, args=(N,), daemon=True)
+        reserve.start()
+    linkage_fn = hip_linkage(link_ctx, names, stream)
+    if reserve is not None:
+        inner = linkage_fn
+
+        def linkage_fn(*args):
+            t0 = time.perf_counter()
+            reserve.join()
+            res_wait["reserve_wait_s"] = time.perf_counter() - t0
+            return inner(*args)
+    res_wait = {}
+    res = run_sharded(N, names, a.sketch, sketch_fn, hip_allpairs(ctx, stream, dev), linkage_fn,
                       a.method, a.P_ani, sync=lambda: torch.cuda.synchronize(dev))
     if from_files and world > 1:
         # every rank filled its shard's lengths: the root takes the element-wise max
@@ -389,6 +408,8 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
                "genome_bp": None if from_files else a.genome_bp, "sketch": a.sketch, "n_gpus": world,
                "backend": backend, "method": a.method, "P_ani": a.P_ani, "times": res["times"],
                "pairs": N * (N - 1) // 2, "primary_clusters": int(res["Cdb"]["primary_cluster"].nunique())}
+        out.update(res_wait)
+        out["linkage_phases_s"] = link_ctx.linkage_stats()
         t = res["times"]
         out["pairs_per_s_job"] = out["pairs"] / sum(v for k, v in t.items())
         if a.out:
@@ -403,6 +424,8 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
             res["Cdb"].to_csv(os.path.join(a.out, "primary_Cdb.csv"), index=False)
             out["stored"] = a.out
         print(json.dumps(out), flush=True)
+    if link_ctx is not ctx:
+        link_ctx.close()
     ctx.close()
     dist.destroy_process_group()
     return 0

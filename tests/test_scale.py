@@ -113,6 +113,19 @@ def test_scale(N, s, config):
     dev = torch.device("cuda", 0)
     ctx = _lib.Context(device=0, k=21, s=s, seed=42)
     stream = torch.cuda.current_stream(dev).cuda_stream
+    # the n x n linkage matrix (80 GB at 10^5, ~2 s of hipMalloc) is allocated
+    # by the clustering context on a helper thread while the sketch and
+    # all-pairs stages run (as drep_amd.distributed does on its root rank)
+    import threading
+    link_ctx = _lib.Context(device=0, k=21, s=s, seed=42)
+    reserve_t = {}
+
+    def reserve():
+        t0 = time.perf_counter()
+        link_ctx.linkage_reserve(N)
+        reserve_t["s"] = time.perf_counter() - t0
+    reserver = threading.Thread(target=reserve, daemon=True)
+    reserver.start()
 
     # ---- sketch, CH genomes at a time (inputs generated on device, untimed)
     tile = _lib.tile_bases()
@@ -202,25 +215,20 @@ def test_scale(N, s, config):
     # ---- primary clustering: average linkage on the GPU from the device counts
     lut, lut_off = linkage_tables(np.array([s]), s)
     perm = np.arange(N, dtype=np.uint32)          # names g000000.. sort in index order
-    ctx.set_timing(True)
     t0 = time.perf_counter()
-    Z = ctx.linkage_counts_device(d_common.data_ptr(), None, N, perm, lut, lut_off, "average")
+    reserver.join()
+    res["linkage_reserve_s"] = reserve_t.get("s")              # on the helper thread, beside the stages above
+    res["linkage_reserve_wait_s"] = time.perf_counter() - t0
+    link_ctx.set_timing(True)
+    t0 = time.perf_counter()
+    Z = link_ctx.linkage_counts_device(d_common.data_ptr(), None, N, perm, lut, lut_off, "average", stream)
     res["linkage_s"] = time.perf_counter() - t0
-    res["linkage_matrix_build_ms"] = ctx.kernel_ms(3)[0]
-    res["linkage_chain_ms"] = ctx.kernel_ms(2)[0]
-    res["linkage_phases_s"] = ctx.linkage_stats()
-    note("gpu linkage %.2f s %s" % (res["linkage_s"], json.dumps(res["linkage_phases_s"])))
-    # the same call again with the matrix already allocated (drephip_linkage_reserve
-    # semantics: the 80 GB allocation outside the clustering step)
-    t0 = time.perf_counter()
-    Z2 = ctx.linkage_counts_device(d_common.data_ptr(), None, N, perm, lut, lut_off, "average")
-    res["linkage_reserved_s"] = time.perf_counter() - t0
-    res["linkage_reserved_phases_s"] = ctx.linkage_stats()
-    res["linkage_reserved_chain_ms"] = ctx.kernel_ms(2)[0]
-    note("gpu linkage (matrix reserved) %.2f s %s" % (res["linkage_reserved_s"],
-                                                      json.dumps(res["linkage_reserved_phases_s"])))
-    assert np.array_equal(Z, Z2)
-    del Z2
+    res["linkage_matrix_build_ms"] = link_ctx.kernel_ms(3)[0]
+    res["linkage_chain_ms"] = link_ctx.kernel_ms(2)[0]
+    res["linkage_phases_s"] = link_ctx.linkage_stats()
+    note("gpu linkage %.2f s %s (matrix reserved in %.2f s beside sketch/all-pairs, waited %.3f s)"
+         % (res["linkage_s"], json.dumps(res["linkage_phases_s"]), res["linkage_reserve_s"] or -1,
+            res["linkage_reserve_wait_s"]))
     assert Z.shape == (N - 1, 4)
     assert np.all(np.diff(Z[:, 2]) >= 0)           # average linkage is monotone
     assert Z[-1, 3] == N
@@ -252,6 +260,7 @@ def test_scale(N, s, config):
         res["linkage_identical_to_scipy"] = bool(np.array_equal(Z, Zs))
         note("scipy linkage %.1f s identical=%s" % (res["scipy_linkage_s"], res["linkage_identical_to_scipy"]))
         assert res["linkage_identical_to_scipy"]
+    link_ctx.close()
     ctx.close()
     json.dump(res, open(out_path, "w"), indent=1)
     note(json.dumps(res))

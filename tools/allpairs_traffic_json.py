@@ -77,7 +77,8 @@ def main():
         dv["active_inst_any_frac"] = c.get("SQ_ACTIVE_INST_ANY", 0) / c["SQ_WAVE_CYCLES"]
     if c.get("SQ_INSTS_VALU"):
         dv["salu_over_valu"] = c.get("SQ_INSTS_SALU", 0) / c["SQ_INSTS_VALU"]
-        dv["valu_per_pair"] = c["SQ_INSTS_VALU"] * 64 / max(N * (N - 1) // 2, 1)
+        dv["valu_wave_insts_per_pair"] = c["SQ_INSTS_VALU"] / max(N * (N - 1) // 2, 1)
+        dv["salu_insts_per_pair"] = c.get("SQ_INSTS_SALU", 0) / max(N * (N - 1) // 2, 1)
         if cyc:
             dv["valu_issue_frac_2cyc"] = c["SQ_INSTS_VALU"] * 2 / (N_SIMD * cyc)
     if c.get("SQ_LDS_IDX_ACTIVE") and cyc:

@@ -1,17 +1,17 @@
 #!/bin/bash
-# Linkage A/B: parity tests on the default library, then the configs[3]-size
-# scale test (N = 10^5, -k 100000) once per library in AB_LIBS ("lib" = the
-# default drep_amd/lib, other names = drep_amd/lib_ab/<name>), linkage time printed.
+# Linkage A/B: tools/link_ab.py (synthetic configs workload, average linkage
+# from the device counts, two calls) once per library in AB_LIBS (names under
+# drep_amd/lib_ab/, "lib" = drep_amd/lib) and N in LINK_NS, interleaved.
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-.}
-mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu.py -m gpu -x -q -k "linkage or cluster_mash" --timeout 120 --timeout-method thread \
-    > gpurun_out/gpu_link.log 2>&1 || { tail -40 gpurun_out/gpu_link.log; exit 1; }
-tail -1 gpurun_out/gpu_link.log
-for v in ${AB_LIBS:-lib}; do
-  if [ "$v" = lib ]; then L=$PWD/drep_amd/lib/libdrephip.so; else L=$PWD/drep_amd/lib_ab/$v/libdrephip.so; fi
-  DREPHIP_LIB=$L DREPHIP_SCALE_OUT=gpurun_out/scale_link_$v.json timeout -k 10 600 \
-     python -u -m pytest tests/test_scale.py -m gpu -x -q -s -k 100000 --timeout 580 --timeout-method thread > gpurun_out/scale_link_$v.log 2>&1 \
-     || { tail -20 gpurun_out/scale_link_$v.log; exit 1; }
-  python3 -c "import json; d=json.load(open('gpurun_out/scale_link_$v.json')); print('$v', 'linkage_s %.3f' % d['linkage_s'])"
+mkdir -p gpurun_out/linkab
+for N in ${LINK_NS:-10000 100000}; do
+  for rep in 1 2; do
+    for v in ${AB_LIBS:-lib}; do
+      if [ "$v" = lib ]; then L=$PWD/drep_amd/lib/libdrephip.so; else L=$PWD/drep_amd/lib_ab/$v/libdrephip.so; fi
+      DREPHIP_LIB=$L timeout -k 10 300 python tools/link_ab.py $N > gpurun_out/linkab/$v.$N.$rep.json 2> gpurun_out/linkab/$v.$N.$rep.err \
+          || { echo "$v $N failed"; tail -5 gpurun_out/linkab/$v.$N.$rep.err; exit 1; }
+      python3 -c "import json; d=json.load(open('gpurun_out/linkab/$v.$N.$rep.json')); print('$v', $N, $rep, 'chain %.1f ms / %.1f ms' % (d['chain_kernel_ms_0'], d['chain_kernel_ms_1']), 'wall %.3f / %.3f s' % (d['wall_s_0'], d['wall_s_1']), 'alloc %.3f s' % d['phases_0']['alloc_s'], 'Z', d['Z_sha1'])"
+    done
+  done
 done
