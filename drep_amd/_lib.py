@@ -80,6 +80,7 @@ SIGNATURES = {
                                                 C.c_int, f64p, vp]),
     "drephip_linkage_reserve": (C.c_int, [vp, C.c_uint32]),
     "drephip_last_linkage_stats": (C.c_int, [vp] + [C.POINTER(C.c_double)] * 5),
+    "drephip_last_linkage_path": (C.c_int, [vp] + [C.POINTER(C.c_int)] * 3),
     "drephip_set_timing": (C.c_int, [vp, C.c_int]),
     "drephip_last_kernel_ms": (C.c_int, [vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
 }
@@ -269,7 +270,12 @@ class Context:
         """{alloc_s, matrix_s, chain_s, finish_s, wall_s} of the last linkage call."""
         v = [C.c_double(0) for _ in range(5)]
         check(lib().drephip_last_linkage_stats(self._h, *[C.byref(x) for x in v]), "drephip_last_linkage_stats")
-        return dict(zip(("alloc_s", "matrix_s", "chain_s", "finish_s", "wall_s"), (x.value for x in v)))
+        out = dict(zip(("alloc_s", "matrix_s", "chain_s", "finish_s", "wall_s"), (x.value for x in v)))
+        w = [C.c_int(0) for _ in range(3)]
+        check(lib().drephip_last_linkage_path(self._h, *[C.byref(x) for x in w]), "drephip_last_linkage_path")
+        out.update(path=("graph", "persistent")[w[0].value], persist_steps=w[1].value,
+                   persist_participants=w[2].value)
+        return out
 
     def set_timing(self, on: bool = True, kernels=None) -> None:
         """HIP-event timing of kernel launches: all kernels, or only the

@@ -350,58 +350,123 @@ static uint64_t ingest_batch_bases() {
     return 1ull << 30;                  // ~1 Gbase of sequence per batch
 }
 
-// Read files [g0, ...) until the batch holds >= target bases, then pack them
-// into `slot` (zeroed only where genomes are; every thread packs its own).
+// Upper bound on a file's bases (every base is one byte of the uncompressed
+// text): the size of a plain file; for a gzip file its trailer's ISIZE (the
+// uncompressed size mod 2^32 of the LAST member -- exact for the usual
+// single-member file; a multi-member (bgzf) file shows an ISIZE below its
+// compressed size and gets the generic guess of 4x).  A wrong guess costs an
+// overflow repack, never a wrong result.
+static uint64_t estimate_bases(const char *path) {
+    FILE *fp = fopen(path, "rb");
+    if (!fp) return 0;
+    uint8_t magic[2] = {0, 0};
+    const size_t got = fread(magic, 1, 2, fp);
+    fseek(fp, 0, SEEK_END);
+    const long sz = ftell(fp);
+    uint64_t est = sz > 0 ? (uint64_t)sz : 0;
+    if (got == 2 && magic[0] == 0x1f && magic[1] == 0x8b && sz >= 18) {
+        uint8_t t[4];
+        fseek(fp, -4, SEEK_END);
+        if (fread(t, 1, 4, fp) == 4) {
+            const uint64_t isize = (uint64_t)t[0] | (uint64_t)t[1] << 8 | (uint64_t)t[2] << 16 | (uint64_t)t[3] << 24;
+            est = isize >= (uint64_t)sz ? isize : 4 * (uint64_t)sz;
+        }
+    }
+    fclose(fp);
+    return est;
+}
+
+// Grow a pinned slot keeping its first `keep_c` / `keep_v` words.
+static int grow_pinned(PinnedSlot &slot, size_t cb, size_t vb, size_t keep_c, size_t keep_v) {
+    PinnedSlot n;
+    if (n.reserve(cb, vb)) return -1;
+    memcpy(n.codes, slot.codes, keep_c * 4);
+    memcpy(n.valid, slot.valid, keep_v * 4);
+    std::swap(slot.codes, n.codes); std::swap(slot.codes_bytes, n.codes_bytes);
+    std::swap(slot.valid, n.valid); std::swap(slot.valid_bytes, n.valid_bytes);
+    return 0;                          // n frees the old buffers
+}
+
+// One batch: files [g0, ...) chosen by their estimated bases until the batch
+// holds >= target, each given a tile-aligned region of its estimated padded
+// span; then ONE pass over the batch's files on `threads` workers (dynamic
+// scheduling): a worker reads + parses a file into its own reused buffer and
+// packs it straight into the pinned batch while the sequence is cache-hot (a
+// genome whose real span outgrew its estimate is kept and packed after the
+// pass, at the end of the batch).  Regions are zeroed by their worker; the
+// slack between a genome's padded span and its region stays zero and no tile
+// covers it.
 static void produce_batch(const char *const *paths, uint32_t g0, uint32_t n_genomes, int threads, int k,
                           uint64_t target, PinnedSlot &slot, IngestBatch &B, int device) {
     const auto t0 = std::chrono::steady_clock::now();
     (void)hipSetDevice(device);         // the pinned batch belongs with the context's device
     B = IngestBatch();
     B.g0 = g0;
-    std::vector<Genome> gs;
-    uint64_t bases = 0;
+    std::vector<uint64_t> reserved;
+    uint64_t est_total = 0;
     uint32_t g1 = g0;
-    // files are read `threads` at a time, until the batch holds >= target bases
-    const uint32_t per = (uint32_t)std::max(1, std::min(64, threads > 0 ? threads
-                                                               : (int)std::thread::hardware_concurrency()));
-    while (g1 < n_genomes && bases < target) {
-        const uint32_t chunk = std::min<uint32_t>(n_genomes - g1, per);
-        std::vector<Genome> part(chunk);
-        std::vector<int> err(chunk, 0);
-        std::vector<std::string> msg(chunk);
-        parallel_for(chunk, threads, [&](uint32_t i) {
-            err[i] = read_fasta(paths[g1 + i], part[i]);
-            if (err[i]) msg[i] = drephip_last_error();
-        });
-        for (uint32_t i = 0; i < chunk; i++)
-            if (err[i]) { B.err = DREPHIP_ERR_IO; B.msg = msg[i]; return; }
-        for (auto &g : part) { bases += g.length; gs.push_back(std::move(g)); }
-        g1 += chunk;
+    while (g1 < n_genomes && (g1 == g0 || est_total < target)) {
+        const uint64_t e = estimate_bases(paths[g1]);
+        reserved.push_back(padded_span(e));
+        est_total += e;
+        g1++;
     }
     const uint32_t n = g1 - g0;
     B.n = n;
     B.off.resize(n); B.pad.resize(n); B.nk.resize(n); B.length.resize(n);
     uint64_t cur = kTile;
-    for (uint32_t i = 0; i < n; i++) {
-        B.off[i] = cur;
-        B.pad[i] = padded_span(genome_span(gs[i].rec_len.data(), (uint32_t)gs[i].rec_len.size()));
-        cur += B.pad[i];
-        B.length[i] = gs[i].length;
-    }
-    B.bases = cur;
+    for (uint32_t i = 0; i < n; i++) { B.off[i] = cur; cur += reserved[i]; }
     if (slot.reserve(cur / 16 * 4, cur / 32 * 4)) {
         B.err = DREPHIP_ERR_NOMEM; B.msg = "hipHostMalloc of the pinned ingest batch failed"; return;
     }
-    uint32_t *codes = slot.codes, *valid = slot.valid;
-    memset(codes, 0, kTile / 16 * 4);
-    memset(valid, 0, kTile / 32 * 4);
-    parallel_for(n, threads, [&](uint32_t i) {
-        memset(codes + B.off[i] / 16, 0, B.pad[i] / 16 * 4);
-        memset(valid + B.off[i] / 32, 0, B.pad[i] / 32 * 4);
-        B.nk[i] = pack_records(gs[i].seq.data(), gs[i].rec_len.data(), (uint32_t)gs[i].rec_len.size(), k,
-                               codes, valid, B.off[i]);
-        std::vector<uint8_t, NoInitAlloc<uint8_t>>().swap(gs[i].seq);   // free as we go
-    });
+    memset(slot.codes, 0, kTile / 16 * 4);
+    memset(slot.valid, 0, kTile / 32 * 4);
+    std::vector<int> err(n, 0);
+    std::vector<std::string> msg(n);
+    std::vector<Genome> overflow(n);                 // genomes whose span outgrew the estimate (rare)
+    std::vector<char> over(n, 0);
+    std::vector<Genome> work(std::max(1, threads > 0 ? threads : (int)std::thread::hardware_concurrency()));
+    std::atomic<uint32_t> next(0);
+    auto worker = [&](uint32_t w) {
+        Genome &g = work[w];                         // reused: no fresh pages per file
+        for (uint32_t i = next++; i < n; i = next++) {
+            if (read_fasta(paths[g0 + i], g)) { err[i] = DREPHIP_ERR_IO; msg[i] = drephip_last_error(); continue; }
+            const uint64_t P = padded_span(genome_span(g.rec_len.data(), (uint32_t)g.rec_len.size()));
+            B.length[i] = g.length;
+            B.pad[i] = P;
+            if (P > reserved[i]) { std::swap(overflow[i], g); over[i] = 1; continue; }
+            memset(slot.codes + B.off[i] / 16, 0, reserved[i] / 16 * 4);
+            memset(slot.valid + B.off[i] / 32, 0, reserved[i] / 32 * 4);
+            B.nk[i] = pack_records(g.seq.data(), g.rec_len.data(), (uint32_t)g.rec_len.size(), k, slot.codes,
+                                   slot.valid, B.off[i]);
+        }
+    };
+    const uint32_t nt = (uint32_t)std::min<size_t>(work.size(), n);
+    std::vector<std::thread> pool;
+    for (uint32_t w = 1; w < nt; w++) pool.emplace_back(worker, w);
+    worker(0);
+    for (auto &th : pool) th.join();
+    for (uint32_t i = 0; i < n; i++)
+        if (err[i]) { B.err = err[i]; B.msg = msg[i]; return; }
+    uint64_t end = cur;
+    for (uint32_t i = 0; i < n; i++) if (over[i]) end += B.pad[i];
+    if (end > cur) {
+        if (grow_pinned(slot, end / 16 * 4, end / 32 * 4, cur / 16, cur / 32)) {
+            B.err = DREPHIP_ERR_NOMEM; B.msg = "hipHostMalloc of the pinned ingest batch failed"; return;
+        }
+        uint64_t at = cur;
+        for (uint32_t i = 0; i < n; i++) {
+            if (!over[i]) continue;
+            const Genome &g = overflow[i];
+            B.off[i] = at;
+            memset(slot.codes + at / 16, 0, B.pad[i] / 16 * 4);
+            memset(slot.valid + at / 32, 0, B.pad[i] / 32 * 4);
+            B.nk[i] = pack_records(g.seq.data(), g.rec_len.data(), (uint32_t)g.rec_len.size(), k, slot.codes,
+                                   slot.valid, at);
+            at += B.pad[i];
+        }
+    }
+    B.bases = end;
     B.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
@@ -710,7 +775,8 @@ DREPHIP_EXPORT int drephip_linkage(drephip_ctx *ctx, const double *y, uint32_t n
     double *d_D;
     int rc = dist_from_condensed_impl(ctx, y, n, &d_D, ctx->stream);
     if (rc) return rc;
-    rc = linkage_device_impl(ctx, d_D, n, method, Z, ctx->stream);
+    rc = linkage_device_impl(ctx, d_D, n, method, Z, ctx->stream,
+                             [&] { double *d2; return dist_from_condensed_impl(ctx, y, n, &d2, ctx->stream); });
     if (rc) return rc;
     timing_collect(ctx);
     ctx->link.wall_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -747,7 +813,10 @@ DREPHIP_EXPORT int drephip_linkage_counts_device(drephip_ctx *ctx, const uint16_
     double *d_D;
     rc = dist_matrix_impl(ctx, d_common, d_denom, n, perm, lut, lut_len, lut_off, &d_D, ctx->stream);
     if (rc) return rc;
-    rc = linkage_device_impl(ctx, d_D, n, method, Z, ctx->stream);
+    rc = linkage_device_impl(ctx, d_D, n, method, Z, ctx->stream, [&] {
+        double *d2;
+        return dist_matrix_impl(ctx, d_common, d_denom, n, perm, lut, lut_len, lut_off, &d2, ctx->stream);
+    });
     if (rc) return rc;
     timing_collect(ctx);
     ctx->link.wall_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -760,6 +829,14 @@ DREPHIP_EXPORT int drephip_linkage_reserve(drephip_ctx *ctx, uint32_t n) {
     if (n < 2) return DREPHIP_OK;
     void *p;
     return scratch(ctx, "lk_D", (uint64_t)n * n * 8, &p);
+}
+
+DREPHIP_EXPORT int drephip_last_linkage_path(drephip_ctx *ctx, int *path, int *steps, int *participants) {
+    if (!ctx) { set_error("null context"); return DREPHIP_ERR_ARG; }
+    if (path) *path = ctx->link.path;
+    if (steps) *steps = ctx->link.persist_steps;
+    if (participants) *participants = ctx->link.persist_participants;
+    return DREPHIP_OK;
 }
 
 DREPHIP_EXPORT int drephip_last_linkage_stats(drephip_ctx *ctx, double *alloc_s, double *matrix_s, double *chain_s,

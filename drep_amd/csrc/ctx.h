@@ -4,6 +4,7 @@
 #include "common.h"
 
 #include <hip/hip_runtime.h>
+#include <functional>
 #include <map>
 #include <memory>
 #include <utility>
@@ -56,6 +57,9 @@ struct LinkStats {            // last drephip_linkage* call, host wall clock (se
     double chain_s = 0;       // nn-chain / MST steps (graph replays)
     double finish_s = 0;      // Z readback + stable sort + relabel on the host
     double wall_s = 0;        // the whole call
+    int path = 0;             // 0: per-step graph, 1: persistent kernel
+    int persist_steps = 0;    // steps the persistent kernel ran (0 when not used)
+    int persist_participants = 0;
 };
 
 struct drephip_ctx {
@@ -159,7 +163,8 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
 int allpairs_wait_impl(drephip_ctx *ctx);
 
 // Primary clustering (linkage.hip).
-int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, double *Z_out, hipStream_t st);
+int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, double *Z_out, hipStream_t st,
+                        const std::function<int()> &rebuild);
 int dist_matrix_impl(drephip_ctx *ctx, const uint16_t *d_common, const uint16_t *d_denom, uint32_t n,
                      const uint32_t *perm, const double *lut, uint32_t lut_len, const int32_t *lut_off,
                      double **d_D_out, hipStream_t st);

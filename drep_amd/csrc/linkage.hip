@@ -29,6 +29,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <numeric>
 #include <vector>
 
@@ -329,6 +330,331 @@ __global__ __launch_bounds__(kLkWG) void k_mst_step(const double *__restrict__ D
     st->k = k + 1;
 }
 
+// --------------------------------------------------- persistent chain / MST
+// The whole chain (or Prim's MST) in ONE launch: P participant workgroups of
+// kPW threads (one per CU; P <= 64 << 256 CUs, so all are resident), each
+// owning a contiguous slice of the n columns with its clusters' sizes (and,
+// for MST, the merged flags and running minima) in LDS.  A step is the
+// k_nn_step / k_mst_step work on the participant's slice, then an exchange:
+// every participant publishes its slice's candidate (value, index, that
+// cluster's size, and the slice's first active cluster other than the one a
+// merge of this step would retire, with its size) and a step tag; every
+// participant reads all P candidates and makes the SAME scipy decision from
+// them (replicated, deterministic), so no state is shared between
+// participants except the matrix itself and the published candidates.  The
+// chain (indices + sizes) lives in each participant's LDS.
+//
+// Visibility (MI355X_MICROARCH.md, Valid forms, first row of the sc1 table):
+// every load and store of the matrix and of the candidates is an agent-scope
+// (sc1) access; every wave drains its stores (s_waitcnt vmcnt(0)) before the
+// workgroup barrier behind which ONE lane stores the step tag (sc1); the
+// consumer lanes poll the tags with sc1 loads and read the candidates after
+// their tag matched; the other waves read after the workgroup barrier.  The
+// only matrix entries one participant reads after another wrote them are the
+// Lance-Williams column entries D[i][y], read as D[t][y] in a later step --
+// always after the writer's tag of the step that wrote them.
+//
+// Every spin is bounded (2 s of s_memrealtime per step): a participant that
+// never arrives makes the others stop with an error flag instead of hanging,
+// and the host then runs the per-step graph path.  Every index taken from a
+// candidate is range-checked before use.
+constexpr bool kLinkPersistDefault = false; // auto: the per-step graph path until the persistent one is the default
+constexpr int kPW = 1024;                 // threads per participant
+constexpr uint32_t kPMaxSlice = 4096;     // columns per participant (LDS: sizes 16 KB, MST minima 32 KB)
+constexpr uint32_t kPMaxP = 64;           // participants (one wave polls them)
+constexpr uint32_t kPChainCap = 4096;     // chain entries in LDS (longer: error flag, graph path)
+constexpr uint64_t kPTimeout = 200000000; // s_memrealtime ticks (100 MHz): 2 s per step
+
+struct PCand { double v; int32_t i, sz, fa, szfa; int32_t pad[2]; };   // 32 B per participant
+struct PStat { int32_t err; int32_t steps; int32_t pad[14]; };
+
+__device__ __forceinline__ double ld1(const double *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void st1(double *p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ int32_t ld1i(const int32_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void st1i(int32_t *p, int32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// (v, i) lexicographic minimum of a workgroup plus a second minimum (f, with
+// its payload fs); results in thread 0.  Payload sz rides with (v, i).
+struct PRed { double v; int32_t i, sz, f, fs; };
+__device__ PRed block_reduce_p(PRed r) {
+    __shared__ PRed sr[kPW / 64];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        PRed q;
+        q.v = __shfl_xor(r.v, o, 64); q.i = __shfl_xor(r.i, o, 64); q.sz = __shfl_xor(r.sz, o, 64);
+        q.f = __shfl_xor(r.f, o, 64); q.fs = __shfl_xor(r.fs, o, 64);
+        if (better(q.v, q.i, r.v, r.i)) { r.v = q.v; r.i = q.i; r.sz = q.sz; }
+        if (q.f < r.f) { r.f = q.f; r.fs = q.fs; }
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) sr[w] = r;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        for (int k = 1; k < kPW / 64; k++) {
+            const PRed q = sr[k];
+            if (better(q.v, q.i, r.v, r.i)) { r.v = q.v; r.i = q.i; r.sz = q.sz; }
+            if (q.f < r.f) { r.f = q.f; r.fs = q.fs; }
+        }
+    return r;
+}
+
+// Publish this participant's candidate for step `step` and collect everyone's:
+// returns the global reduction in thread 0; false (all threads) on a timeout.
+__device__ bool p_exchange(PRed mine, uint32_t step, uint32_t P, PCand *cand, int32_t *tags, PRed &out,
+                           PStat *stat) {
+    __shared__ int s_ok;
+    PCand *slot = cand + (uint64_t)(step & 1) * kPMaxP;
+    // every wave's matrix stores are complete before the tag (condition 3)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        PCand *c = slot + blockIdx.x;
+        st1(&c->v, mine.v);
+        st1i(&c->i, mine.i); st1i(&c->sz, mine.sz); st1i(&c->fa, mine.f); st1i(&c->szfa, mine.fs);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        st1i(&tags[blockIdx.x * 16], (int32_t)step);
+    }
+    if (threadIdx.x < 64) {
+        const uint32_t lane = threadIdx.x;
+        PRed r{INFINITY, 0x7fffffff, 0, 0x7fffffff, 0};
+        bool ok = true;
+        if (lane < P) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (ld1i(&tags[lane * 16]) != (int32_t)step) {
+                __builtin_amdgcn_s_sleep(1);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kPTimeout) { ok = false; break; }
+            }
+            if (ok) {
+                const PCand *c = slot + lane;
+                r.v = ld1(&c->v); r.i = ld1i(&c->i); r.sz = ld1i(&c->sz); r.f = ld1i(&c->fa); r.fs = ld1i(&c->szfa);
+            }
+        }
+        const bool all_ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            PRed q;
+            q.v = __shfl_xor(r.v, o, 64); q.i = __shfl_xor(r.i, o, 64); q.sz = __shfl_xor(r.sz, o, 64);
+            q.f = __shfl_xor(r.f, o, 64); q.fs = __shfl_xor(r.fs, o, 64);
+            if (better(q.v, q.i, r.v, r.i)) { r.v = q.v; r.i = q.i; r.sz = q.sz; }
+            if (q.f < r.f) { r.f = q.f; r.fs = q.fs; }
+        }
+        if (lane == 0) {
+            out = r;
+            s_ok = all_ok;
+            if (!all_ok) st1i(&stat->err, 1);
+        }
+    }
+    __syncthreads();
+    return s_ok != 0;
+}
+
+// Replicated nn-chain state (identical in every participant; thread 0 writes
+// it, everyone reads it after a barrier)
+struct PChain {
+    int32_t k, len, top, below, pend, x, y, nx, ny, stop;
+};
+
+template <int PER>
+__global__ __launch_bounds__(kPW) void k_chain_persist(double *__restrict__ D, uint32_t n, int method, uint32_t S,
+                                                       PCand *__restrict__ cand, int32_t *__restrict__ tags,
+                                                       PStat *__restrict__ stat, double *__restrict__ Z) {
+    __shared__ int32_t size_s[kPMaxSlice];
+    __shared__ int32_t ch_i[kPChainCap], ch_s[kPChainCap];
+    __shared__ PChain cs;
+    __shared__ double s_dp;
+    const uint32_t P = gridDim.x, p = blockIdx.x;
+    const uint32_t lo = p * S, hi = min(n, lo + S);
+    for (uint32_t j = threadIdx.x; j < S; j += kPW) size_s[j] = lo + j < hi ? 1 : 0;
+    if (threadIdx.x == 0) {
+        cs = PChain{0, 1, 0, -1, 0, 0, 0, 0, 0, 0};
+        ch_i[0] = 0; ch_s[0] = 1;
+    }
+    __syncthreads();
+    for (uint32_t step = 0;; step++) {
+        const PChain c = cs;
+        if (c.k >= (int32_t)n - 1 || c.stop) break;
+        const int32_t t = c.top;
+        const bool pend = c.pend != 0;
+        const int32_t x = c.x, y = c.y;
+        const int32_t a_m = c.len > 1 ? min(t, c.below) : -1;          // retired if this step merges
+        const double *Dt = D + (uint64_t)t * n;
+        const double *Dx = D + (uint64_t)x * n;
+        double *Dy = D + (uint64_t)y * n;
+        if (threadIdx.x == 0 && c.len > 1) s_dp = ld1(Dt + c.below);
+        const bool own_y = pend && (uint32_t)y >= lo && (uint32_t)y < hi;
+        const double dxt = own_y ? ld1(Dx + t) : 0.0, dyt = own_y ? ld1(Dy + t) : 0.0;
+        PRed r{INFINITY, 0x7fffffff, 0, 0x7fffffff, 0};
+        for (uint32_t j0 = threadIdx.x; j0 < hi - lo; j0 += PER * kPW) {
+            int32_t sz[PER];
+            double dt[PER], dx[PER], dy[PER];
+#pragma unroll
+            for (int q = 0; q < PER; q++) {
+                const uint32_t j = j0 + q * kPW;
+                const uint32_t jc = j < hi - lo ? j : hi - lo - 1;
+                const uint32_t i = lo + jc;
+                sz[q] = size_s[jc];
+                dt[q] = ld1(Dt + i);
+                if (pend) { dx[q] = ld1(Dx + i); dy[q] = ld1(Dy + i); }
+            }
+#pragma unroll
+            for (int q = 0; q < PER; q++) {
+                const uint32_t j = j0 + q * kPW;
+                if (j >= hi - lo || sz[q] == 0) continue;
+                const int32_t i = (int32_t)(lo + j);
+                if (i != a_m && i < r.f) { r.f = i; r.fs = sz[q]; }
+                double v;
+                if (pend && i != y && i != t) {
+                    const double u = lw_update(method, dx[q], dy[q], c.nx, c.ny);
+                    st1(Dy + i, u);
+                    st1(D + (uint64_t)i * n + y, u);
+                    v = t == y ? u : dt[q];
+                } else if (pend && i == y && t != y) {
+                    const double u = lw_update(method, dxt, dyt, c.nx, c.ny);
+                    st1(Dy + t, u);
+                    st1(D + (uint64_t)t * n + y, u);
+                    v = u;
+                } else {
+                    if (i == t) continue;
+                    v = dt[q];
+                }
+                if (v < r.v) { r.v = v; r.i = i; r.sz = sz[q]; }
+            }
+        }
+        r = block_reduce_p(r);
+        PRed g;
+        if (!p_exchange(r, step, P, cand, tags, g, stat)) return;
+        if (threadIdx.x == 0) {
+            PChain d = c;
+            d.pend = 0;
+            if ((uint32_t)g.i >= n) { st1i(&stat->err, 2); d.stop = 1; }
+            else {
+                const double dp = s_dp;
+                const bool merge = c.len > 1 && !(g.v < dp);
+                if (!merge) {
+                    if (c.len >= (int32_t)kPChainCap || c.len >= (int32_t)n) { st1i(&stat->err, 3); d.stop = 1; }
+                    else {
+                        ch_i[c.len] = g.i; ch_s[c.len] = g.sz;
+                        d.len = c.len + 1; d.below = t; d.top = g.i;
+                    }
+                } else {
+                    const int32_t yb = c.below;
+                    const int32_t st_ = ch_s[c.len - 1], sb = ch_s[c.len - 2];
+                    int32_t a = t, b = yb, na = st_, nb = sb;
+                    if (a > b) { a = yb; b = t; na = sb; nb = st_; }
+                    if (p == 0) {
+                        double *z = Z + 4ull * c.k;
+                        z[0] = a; z[1] = b; z[2] = dp; z[3] = na + nb;
+                    }
+                    if ((uint32_t)a >= lo && (uint32_t)a < hi) size_s[a - lo] = 0;
+                    if ((uint32_t)b >= lo && (uint32_t)b < hi) size_s[b - lo] = na + nb;
+                    d.pend = 1; d.x = a; d.y = b; d.nx = na; d.ny = nb;
+                    d.k = c.k + 1;
+                    d.len = c.len - 2;
+                    d.top = d.len > 0 ? ch_i[d.len - 1] : -1;
+                    d.below = d.len > 1 ? ch_i[d.len - 2] : -1;
+                    if (d.len == 0 && d.k < (int32_t)n - 1) {
+                        if ((uint32_t)g.f >= n) { st1i(&stat->err, 4); d.stop = 1; }
+                        else { ch_i[0] = g.f; ch_s[0] = g.fs; d.len = 1; d.top = g.f; d.below = -1; }
+                    }
+                }
+            }
+            cs = d;
+            if (p == 0) stat->steps = (int32_t)step + 1;
+        }
+        __syncthreads();
+    }
+}
+
+template <int PER>
+__global__ __launch_bounds__(kPW) void k_mst_persist(const double *__restrict__ D, uint32_t n, uint32_t S,
+                                                     PCand *__restrict__ cand, int32_t *__restrict__ tags,
+                                                     PStat *__restrict__ stat, double *__restrict__ Z) {
+    __shared__ double dmin_s[kPMaxSlice];
+    __shared__ uint8_t merged_s[kPMaxSlice];
+    __shared__ int32_t s_x, s_k, s_stop;
+    const uint32_t P = gridDim.x, p = blockIdx.x;
+    const uint32_t lo = p * S, hi = min(n, lo + S);
+    for (uint32_t j = threadIdx.x; j < S; j += kPW) { dmin_s[j] = INFINITY; merged_s[j] = lo + j >= hi || lo + j == 0; }
+    if (threadIdx.x == 0) { s_x = 0; s_k = 0; s_stop = 0; }           // scipy: x = 0, merged[0] = 1
+    __syncthreads();
+    for (uint32_t step = 0;; step++) {
+        const int32_t x = s_x, k = s_k;
+        if (k >= (int32_t)n - 1 || s_stop) break;
+        const double *Dx = D + (uint64_t)x * n;
+        PRed r{INFINITY, 0x7fffffff, 0, 0x7fffffff, 0};
+        for (uint32_t j0 = threadIdx.x; j0 < hi - lo; j0 += PER * kPW) {
+            double dx[PER];
+#pragma unroll
+            for (int q = 0; q < PER; q++) {
+                const uint32_t j = j0 + q * kPW;
+                dx[q] = ld1(Dx + lo + (j < hi - lo ? j : hi - lo - 1));
+            }
+#pragma unroll
+            for (int q = 0; q < PER; q++) {
+                const uint32_t j = j0 + q * kPW;
+                if (j >= hi - lo || merged_s[j]) continue;
+                double m = dmin_s[j];
+                if (m > dx[q]) { m = dx[q]; dmin_s[j] = m; }
+                if (m < r.v) { r.v = m; r.i = (int32_t)(lo + j); }
+            }
+        }
+        r = block_reduce_p(r);
+        PRed g;
+        if (!p_exchange(r, step, P, cand, tags, g, stat)) return;
+        if (threadIdx.x == 0) {
+            if ((uint32_t)g.i >= n) { st1i(&stat->err, 2); s_stop = 1; }
+            else {
+                if (p == 0) {
+                    double *z = Z + 4ull * k;
+                    z[0] = x; z[1] = g.i; z[2] = g.v; z[3] = 0;
+                }
+                if ((uint32_t)g.i >= lo && (uint32_t)g.i < hi) merged_s[g.i - lo] = 1;
+                s_x = g.i;
+                s_k = k + 1;
+            }
+            if (p == 0) stat->steps = (int32_t)step + 1;
+        }
+        __syncthreads();
+    }
+}
+
+// Persistent path: returns DREPHIP_OK with d_Z filled, or DREPHIP_ERR_INTERNAL
+// (with the reason in the error text) when a participant timed out or the
+// chain outgrew its LDS -- the caller then runs the per-step graph path.
+static int linkage_persist(drephip_ctx *ctx, double *d_D, uint32_t n, int method, double *d_Z, hipStream_t st) {
+    uint32_t P = std::max(1u, std::min(kPMaxP, (n + 2047) / 2048));
+    uint32_t S = (n + P - 1) / P;
+    if (S > kPMaxSlice) { set_error("persistent linkage: n too large"); return DREPHIP_ERR_UNSUPPORTED; }
+    PCand *d_cand;
+    int32_t *d_tags;
+    PStat *d_stat, *h_stat;
+    int rc;
+    if ((rc = scratch(ctx, "lkp_cand", 2 * kPMaxP * sizeof(PCand), (void **)&d_cand))) return rc;
+    if ((rc = scratch(ctx, "lkp_tags", kPMaxP * 16 * 4, (void **)&d_tags))) return rc;
+    if ((rc = scratch(ctx, "lkp_stat", sizeof(PStat), (void **)&d_stat))) return rc;
+    if ((rc = pinned_host(ctx, "lkp_stat", sizeof(PStat), (void **)&h_stat))) return rc;
+    HIPC(hipMemsetAsync(d_tags, 0xFF, kPMaxP * 16 * 4, st));         // tag -1: no step published
+    HIPC(hipMemsetAsync(d_stat, 0, sizeof(PStat), st));
+    timing_mark(ctx, 2, st, true);
+    if (method == DREPHIP_LINK_SINGLE)
+        hipLaunchKernelGGL(k_mst_persist<4>, dim3(P), dim3(kPW), 0, st, d_D, n, S, d_cand, d_tags, d_stat, d_Z);
+    else
+        hipLaunchKernelGGL(k_chain_persist<4>, dim3(P), dim3(kPW), 0, st, d_D, n, method, S, d_cand, d_tags, d_stat, d_Z);
+    timing_mark(ctx, 2, st, false);
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(h_stat, d_stat, sizeof(PStat), hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    ctx->link.persist_steps = h_stat->steps;
+    ctx->link.persist_participants = P;
+    if (h_stat->err) {
+        static const char *why[] = {"", "a participant timed out", "no valid candidate", "chain longer than its LDS",
+                                    "no cluster to restart the chain"};
+        set_error(std::string("persistent linkage stopped: ") + why[std::min(h_stat->err, 4)]);
+        return DREPHIP_ERR_INTERNAL;
+    }
+    return DREPHIP_OK;
+}
+
 // ------------------------------------------------------------ matrix build
 // D (n x n f64, rows in perm order) from the condensed upper triangle, by
 // 64 x 64 tiles of (row block bi <= column block bj): a wave reads one row's
@@ -452,13 +778,46 @@ static void sort_and_label(std::vector<double> &Z, uint32_t n) {
     Z.swap(S);
 }
 
-int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, double *Z_out, hipStream_t st) {
+// Which chain implementation runs: DREPHIP_LINK_PATH=persist (one persistent
+// launch), graph (per-step kernels replayed from a hipGraph), or auto.
+static bool use_persistent(uint32_t n) {
+    const char *e = getenv("DREPHIP_LINK_PATH");
+    if (e && !strcmp(e, "graph")) return false;
+    if (e && !strcmp(e, "persist")) return true;
+    return kLinkPersistDefault && n <= kPMaxP * kPMaxSlice;
+}
+
+int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, double *Z_out, hipStream_t st,
+                        const std::function<int()> &rebuild) {
     if (n < 2) return DREPHIP_OK;
     const double t_chain = now_s();           // chain_s: scratch, graph capture and the steps
     if (method != DREPHIP_LINK_SINGLE && method != DREPHIP_LINK_COMPLETE && method != DREPHIP_LINK_AVERAGE &&
         method != DREPHIP_LINK_WEIGHTED) {
         set_error("linkage method must be single, complete, average or weighted");
         return DREPHIP_ERR_UNSUPPORTED;
+    }
+    ctx->link.path = 0;
+    if (use_persistent(n) && n <= kPMaxP * kPMaxSlice) {
+        double *d_Zp;
+        int rc;
+        if ((rc = scratch(ctx, "lk_Z", (n - 1) * 32ull, (void **)&d_Zp))) return rc;
+        rc = linkage_persist(ctx, d_D, n, method, d_Zp, st);
+        if (rc == DREPHIP_OK) {
+            ctx->link.path = 1;
+            const double t_fin = now_s();
+            ctx->link.chain_s = t_fin - t_chain;
+            std::vector<double> Z(4ull * (n - 1));
+            HIPC(hipMemcpy(Z.data(), d_Zp, Z.size() * 8, hipMemcpyDeviceToHost));
+            sort_and_label(Z, n);
+            std::copy(Z.begin(), Z.end(), Z_out);
+            ctx->link.finish_s = now_s() - t_fin;
+            return DREPHIP_OK;
+        }
+        if (rc != DREPHIP_ERR_INTERNAL) return rc;
+        // a participant timed out or the chain outgrew its LDS: the matrix may
+        // hold partial Lance-Williams updates -- rebuilt, then the graph path
+        fprintf(stderr, "[drephip] %s; running the per-step linkage path\n", drephip_last_error());
+        if ((rc = rebuild())) return rc;
     }
     // entries per lane of a step, i.e. the grid density (default kLkPer: one pass;
     // DREPHIP_LINK_PER_LANE exists for the tests, which cover 1, 4 and 16)

@@ -279,6 +279,12 @@ int drephip_linkage_reserve(drephip_ctx *ctx, uint32_t n);
 int drephip_last_linkage_stats(drephip_ctx *ctx, double *alloc_s, double *matrix_s, double *chain_s,
                                double *finish_s, double *wall_s);
 
+/* Which chain implementation the last drephip_linkage* call ran: *path = 0
+ * for the per-step kernels replayed from a hipGraph, 1 for the persistent
+ * kernel (steps it ran, participant workgroups).  DREPHIP_LINK_PATH=graph /
+ * persist / auto selects it. */
+int drephip_last_linkage_path(drephip_ctx *ctx, int *path, int *steps, int *participants);
+
 /* HIP-event timing of kernel launches: `kernels` is a bitmask of the kernels
  * to bracket with events (bit w = `which` w of drephip_last_kernel_ms; -1 =
  * all, 0 = none).  Each event pair adds a few microseconds of idle time

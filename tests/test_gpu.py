@@ -65,6 +65,39 @@ def test_sketch_files_many_batches(golden, tmp_path, monkeypatch):
         assert nh[i] == S and np.array_equal(h[i], ref.hashes) and int(ln[i]) == ref.length, f
 
 
+def test_sketch_files_estimate_overflow(golden, tmp_path, monkeypatch):
+    """The ingest places each genome in a region sized from its file (plain
+    size, or a gzip trailer's ISIZE -- the LAST member's size).  A two-member
+    gzip file whose last member is large enough to pass for the whole file
+    underestimates its bases: that genome is repacked at the end of the batch.
+    Sketches equal the oracle's, in order, with neighbours in the same batch."""
+    import gzip
+    import zlib
+    fas = sorted(glob.glob(os.path.join(golden, "genomes", "*.gz")))
+    txt = [gzip.open(fa).read() for fa in fas]
+    multi = tmp_path / "two_members.fa.gz"
+    half = len(txt[0]) // 2
+    cut = txt[0].index(b"\n", half) + 1                     # split at a line end
+    with open(multi, "wb") as fh:
+        for part in (txt[0][:cut], txt[0][cut:]):
+            co = zlib.compressobj(6, zlib.DEFLATED, 31)       # one gzip member each
+            fh.write(co.compress(part) + co.flush())
+    assert len(gzip.open(multi).read()) == len(txt[0])
+    plain = tmp_path / "plain.fa"
+    plain.write_bytes(txt[1])
+    files = [str(plain), str(multi), fas[2], str(multi), fas[3]]
+    want = [fas[1], fas[0], fas[2], fas[0], fas[3]]
+    for bb in (None, "4000000"):
+        if bb:
+            monkeypatch.setenv("DREPHIP_INGEST_BATCH_BASES", bb)
+        with _lib.Context(0, 21, S, 42) as ctx:
+            h, nh, ln = ctx.sketch_files(files, threads=3)
+        for i, fa in enumerate(want):
+            ref = read_msh(os.path.join(golden, "MASH_files", "sketches",
+                                        os.path.basename(fa)[:-3] + ".msh")).references[0]
+            assert nh[i] == S and np.array_equal(h[i], ref.hashes) and int(ln[i]) == ref.length, (bb, i)
+
+
 def _records_case(rng, kind):
     A = np.frombuffer(b"ACGT", dtype=np.uint8)
     if kind == "nruns_lower_multirecord":
@@ -769,13 +802,16 @@ def test_sketch_layout_cache_follows_layout_changes(ctx1000):
 # ------------------------------------------------------ primary clustering
 @pytest.mark.parametrize("method", ["single", "complete", "average", "weighted"])
 @pytest.mark.parametrize("n,kind", [(2, "ties"), (3, "ties"), (17, "ties"), (257, "ties"), (300, "cont"),
-                                    (64, "equal"), (400, "fewvals"), (1500, "mash")])
+                                    (64, "equal"), (400, "fewvals"), (1500, "mash"), (4500, "mash"),
+                                    (2100, "ties")])
 def test_gpu_linkage_matches_scipy(method, n, kind):
     """drephip_linkage == scipy.cluster.hierarchy.linkage bit for bit, with
     Mash-like ties (a few distinct distances, many 1.0), continuous values,
     all-equal distances, a few values whose Lance-Williams averages round
-    (fewvals), and family structure with 1.0 between families (mash), at two
-    grid densities of the chain-step kernel."""
+    (fewvals), and family structure with 1.0 between families (mash): the
+    per-step graph path at three grid densities of the chain-step kernel, and
+    the persistent kernel (one participant per 2048 columns: n = 2100 and 4500
+    have 2 and 3 participants exchanging candidates)."""
     import scipy.cluster.hierarchy as sch
     rng = np.random.default_rng(n * 31 + len(method))
     m = n * (n - 1) // 2
@@ -795,15 +831,24 @@ def test_gpu_linkage_matches_scipy(method, n, kind):
     else:
         y = np.full(m, 0.5)
     Zs = sch.linkage(y, method=method)
-    for per_lane in ("4", "1", "16"):                # grid densities of the chain-step kernel (16: 4 passes)
-        os.environ["DREPHIP_LINK_PER_LANE"] = per_lane
+    runs = [("graph", "4"), ("graph", "1"), ("graph", "16"), ("persist", None)]
+    if n > 2000:
+        runs = [("graph", "4"), ("persist", None)]
+    for path, per_lane in runs:                      # grid densities of the chain-step kernel (16: 4 passes)
+        os.environ["DREPHIP_LINK_PATH"] = path
+        if per_lane:
+            os.environ["DREPHIP_LINK_PER_LANE"] = per_lane
         try:
             with _lib.Context(0, 21, S, 42) as ctx:
                 Z = ctx.linkage(y, method)
+                st = ctx.linkage_stats()
         finally:
             os.environ.pop("DREPHIP_LINK_PER_LANE", None)
+            os.environ.pop("DREPHIP_LINK_PATH", None)
         assert Z.shape == Zs.shape
-        assert np.array_equal(Z, Zs), (per_lane, np.argwhere(Z != Zs)[:5])
+        assert np.array_equal(Z, Zs), (path, per_lane, np.argwhere(Z != Zs)[:5])
+        if n >= 2:
+            assert st["path"] == ("persistent" if path == "persist" else "graph"), st
 
 
 @pytest.mark.parametrize("method", ["average", "single"])

@@ -6,7 +6,13 @@ HBM -- so both the raw and the doubled read figure are given: the column loads
 here are 8 B per lane, an uncalibrated width), the L2 hit rate, and the SQ
 issue/stall fractions (tools/pmc_summary.py's definitions).
 
-usage: python tools/allpairs_traffic_json.py <kernel substring> <dir> <case> N s
+usage: python tools/allpairs_traffic_json.py <kernel substring> <dir> <case> N s calls
+
+`calls` = all-pairs calls the profiled command made (bench.py --steps 1
+--warmup 0: 4, its three timing steps included; tools/ap_bench.py with
+AP_ITERS=1: 1).  A call over a large triangle is several dispatches (grid
+limit), so every figure is per CALL = the whole N(N-1)/2 triangle: the sum
+over dispatches divided by `calls`.
 """
 import collections
 import csv
@@ -34,18 +40,24 @@ def per_dispatch(files, key):
 
 def main():
     key, d, case, N, s = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5])
+    ncalls = int(sys.argv[6])
     stats = glob.glob(os.path.join(d, case + "_trace", "**", "*kernel_stats.csv"), recursive=True)
-    avg_ms, calls = None, None
+    avg_ms, ndisp = None, None
     for r in csv.DictReader(open(stats[0])):
         if key in r["Name"]:
-            avg_ms, calls = float(r["AverageNs"]) / 1e6, int(r["Calls"])
+            ndisp = int(r["Calls"])
+            avg_ms = float(r["AverageNs"]) / 1e6 * ndisp / ncalls        # per call (whole triangle)
     files = sorted(glob.glob(os.path.join(d, case + "_p*", "**", "pmc_counter_collection.csv"), recursive=True))
-    c, nd, name = per_dispatch(files, key)
-    # GRBM_GUI_ACTIVE rides in every pass: average over passes, summed over 8 XCDs
+    cd, nd, name = per_dispatch(files, key)
+    # per call: the per-dispatch average times the dispatches of one pass over calls
+    passes = len({f for f in files})
+    c = {k: v * nd[k] / max(1, passes if k == "GRBM_GUI_ACTIVE" else 1) / ncalls for k, v in cd.items()}
+    # GRBM_GUI_ACTIVE rides in every pass (summed over 8 XCDs): its dispatch
+    # count above spans all passes, hence the division by the pass count
     cyc = c.get("GRBM_GUI_ACTIVE", 0.0) / 8
     out = {"case": case, "kernel": name, "genomes": N, "sketch": s, "pairs": N * (N - 1) // 2,
-           "avg_dispatch_ms": avg_ms, "dispatches_traced": calls, "counters_per_dispatch": c,
-           "dispatches_per_counter": nd}
+           "calls": ncalls, "dispatches_per_call": (ndisp or 0) / ncalls, "avg_call_ms": avg_ms,
+           "counters_per_call": c, "dispatches_per_counter": nd}
     dv = out["derived"] = {}
     if cyc and avg_ms:
         dv["kernel_cycles"] = cyc
@@ -59,6 +71,7 @@ def main():
     alg_read = N * s * 8                                 # every sketch read once
     alg_write = N * (N - 1) // 2 * 2                     # uint16 common per pair
     dv["algorithmic_bytes"] = alg_read + alg_write
+    dv["column_stream_bytes_logical"] = (N * (N - 1) // 2) * s * 8 / 4   # every pair's column once per 4-row tile
     if "hbm_read_bytes_raw" in dv and "hbm_write_bytes" in dv and avg_ms:
         for tag in ("raw", "x2"):
             tot = dv["hbm_read_bytes_" + tag] + dv["hbm_write_bytes"]

@@ -5,7 +5,7 @@
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-.}
 mkdir -p gpurun_out
-timeout -k 10 ${TESTS_LIMIT:-1100} python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread "$@" \
+timeout -k 10 ${TESTS_LIMIT:-1100} python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 900 --timeout-method thread "$@" \
     > gpurun_out/gputest.log 2>&1
 rc=$?
 tail -5 gpurun_out/gputest.log
