@@ -76,7 +76,7 @@ def dist_roofline(N, s, pairs_per_launch, launch_ms):
     d = json.load(open(path))
     dv = d.get("derived", {})
     out = {"kernel": (d.get("kernel") or "")[:60], "source": os.path.relpath(path, ROOT),
-           "profiled_avg_dispatch_ms": d.get("avg_dispatch_ms")}
+           "profiled_avg_call_ms": d.get("avg_call_ms")}
     if dv.get("valu_wave_insts_per_pair") and launch_ms:
         ach = dv["valu_wave_insts_per_pair"] * pairs_per_launch / (launch_ms * 1e-3)
         out.update({"bound": "valu+lds", "achieved": ach, "peak": VALU_PEAK_WAVE_INST,

@@ -59,6 +59,8 @@ SIGNATURES = {
     "drephip_sketch_files": (C.c_int, [vp, C.POINTER(C.c_char_p), C.c_uint32, C.c_int, u64p, u32p, u64p]),
     "drephip_last_ingest_stats": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                             C.POINTER(C.c_double), C.POINTER(C.c_uint32)]),
+    "drephip_last_ingest_phases": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                             C.POINTER(C.c_uint32)]),
     "drephip_sketch_device": (C.c_int, [vp, vp, vp, u64p, u64p, u64p, C.c_uint32, vp, vp, vp]),
     "drephip_sketch_device_async": (C.c_int, [vp, vp, vp, u64p, u64p, u64p, C.c_uint32, vp, vp, vp]),
     "drephip_sketch_wait": (C.c_int, [vp, C.POINTER(C.c_int)]),
@@ -80,7 +82,6 @@ SIGNATURES = {
                                                 C.c_int, f64p, vp]),
     "drephip_linkage_reserve": (C.c_int, [vp, C.c_uint32]),
     "drephip_last_linkage_stats": (C.c_int, [vp] + [C.POINTER(C.c_double)] * 5),
-    "drephip_last_linkage_path": (C.c_int, [vp] + [C.POINTER(C.c_int)] * 3),
     "drephip_set_timing": (C.c_int, [vp, C.c_int]),
     "drephip_last_kernel_ms": (C.c_int, [vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
 }
@@ -123,6 +124,11 @@ def lib():
         except OSError as e:
             raise DrepHipError("cannot load %s: %s" % (LIB_PATH, e)) from e
         for name, (res, args) in SIGNATURES.items():
+            # an older build loaded for a same-box A/B (DREPHIP_LIB) may lack
+            # entry points added since; the product library has them all
+            # (tests/test_host.py checks the export list)
+            if "DREPHIP_LIB" in os.environ and not hasattr(L, name):
+                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
@@ -270,12 +276,7 @@ class Context:
         """{alloc_s, matrix_s, chain_s, finish_s, wall_s} of the last linkage call."""
         v = [C.c_double(0) for _ in range(5)]
         check(lib().drephip_last_linkage_stats(self._h, *[C.byref(x) for x in v]), "drephip_last_linkage_stats")
-        out = dict(zip(("alloc_s", "matrix_s", "chain_s", "finish_s", "wall_s"), (x.value for x in v)))
-        w = [C.c_int(0) for _ in range(3)]
-        check(lib().drephip_last_linkage_path(self._h, *[C.byref(x) for x in w]), "drephip_last_linkage_path")
-        out.update(path=("graph", "persistent")[w[0].value], persist_steps=w[1].value,
-                   persist_participants=w[2].value)
-        return out
+        return dict(zip(("alloc_s", "matrix_s", "chain_s", "finish_s", "wall_s"), (x.value for x in v)))
 
     def set_timing(self, on: bool = True, kernels=None) -> None:
         """HIP-event timing of kernel launches: all kernels, or only the
@@ -308,7 +309,12 @@ class Context:
         n = C.c_uint32(0)
         check(lib().drephip_last_ingest_stats(self._h, C.byref(a), C.byref(b), C.byref(c), C.byref(n)),
               "drephip_last_ingest_stats")
-        return {"produce_s": a.value, "gpu_s": b.value, "wall_s": c.value, "batches": n.value}
+        r, p = C.c_double(0), C.c_double(0)
+        o = C.c_uint32(0)
+        check(lib().drephip_last_ingest_phases(self._h, C.byref(r), C.byref(p), C.byref(o)),
+              "drephip_last_ingest_phases")
+        return {"produce_s": a.value, "gpu_s": b.value, "wall_s": c.value, "batches": n.value,
+                "read_thread_s": r.value, "pack_thread_s": p.value, "overflow_genomes": o.value}
 
     def sketch_records(self, seq: np.ndarray, rec_off: np.ndarray, genome_rec_off: np.ndarray):
         seq = np.ascontiguousarray(seq, dtype=np.uint8)

@@ -421,22 +421,40 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
     };
     static_assert(kRing == 4, "first_chunks / refill offsets");
     if (c < cend) first_chunks(column_rsrc(hashes + (uint64_t)c * s, s));
+    // per item, not per column: the active rows and their largest hash once
+    // every row of the tile is left of the column (c >= i0 + R: all columns
+    // but the diagonal tile's), and row 0's output offset (row r + 1's is row
+    // r's plus N - (i0 + r) - 2)
+    uint32_t act_full = 0;
+    uint64_t amax_full = 0;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const bool act = (uint32_t)r < nrows && ((okmask >> r) & 1u);
+        act_full |= (uint32_t)act << r;
+        if (act) amax_full = alast[r] > amax_full ? alast[r] : amax_full;
+    }
+    const uint64_t obase = cond_index(i0, 0, N) - seg0;            // + c: row i0's pair (i0, c)
     for (; c < cend; c += c_step) {
         const __amdgpu_buffer_rsrc_t rc = column_rsrc(hashes + (uint64_t)c * s, s);
 #pragma unroll
         for (int k = 0; k < kRing; k++) rg[k] = nx[k];
         const uint32_t cn = c + c_step;
         if (cn < cend) first_chunks(column_rsrc(hashes + (uint64_t)cn * s, s));
-        uint32_t cnt[R], mrun[R], actmask = 0;
+        uint32_t cnt[R], mrun[R], actmask = act_full;
         // elements past every active row's largest hash cannot match: the
         // scan ends at the first chunk whose smallest element is past them
-        uint64_t amax = 0;
+        uint64_t amax = amax_full;
 #pragma unroll
-        for (int r = 0; r < R; r++) {
-            cnt[r] = 0; mrun[r] = 0;
-            const bool act = (uint32_t)r < nrows && i0 + r < c && ((okmask >> r) & 1u);
-            actmask |= (uint32_t)act << r;
-            if (act) amax = alast[r] > amax ? alast[r] : amax;
+        for (int r = 0; r < R; r++) { cnt[r] = 0; mrun[r] = 0; }
+        if (c < i0 + R) {                                             // the diagonal tile: rows right of c drop out
+            actmask = 0;
+            amax = 0;
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const bool act = ((act_full >> r) & 1u) && i0 + r < c;
+                actmask |= (uint32_t)act << r;
+                if (act) amax = alast[r] > amax ? alast[r] : amax;
+            }
         }
         if (!actmask) continue;                                       // column at or left of the tile's rows
         // slot words of chunk k live in sb[k % kRing]: read kSlotAhead chunks
@@ -527,10 +545,11 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
             // across the chunk loop would force every LDS wait there to lgkmcnt(0)
             const uint32_t nB = nhash[c];
             const bool partial = any_partial_row || nB < s;
+            uint64_t o = obase + c;
 #pragma unroll
             for (int r = 0; r < R; r++) {
+                if (r > 0) o += N - (i0 + r - 1) - 2;                   // cond_index(i0 + r, c) - seg0
                 if (!((actmask >> r) & 1u)) continue;
-                const uint64_t o = cond_index(i0 + r, c, N) - seg0;
                 common[o] = (uint16_t)cnt[r];
                 if (denom) {
                     uint32_t dd = s;

@@ -341,6 +341,8 @@ struct IngestBatch {
     int err = 0;
     std::string msg;
     double seconds = 0;
+    double read_thread_s = 0, pack_thread_s = 0;
+    uint32_t overflow = 0;
 };
 static uint64_t ingest_batch_bases() {
     if (const char *e = getenv("DREPHIP_INGEST_BATCH_BASES")) {     // tests: force many batches
@@ -427,10 +429,15 @@ static void produce_batch(const char *const *paths, uint32_t g0, uint32_t n_geno
     std::vector<char> over(n, 0);
     std::vector<Genome> work(std::max(1, threads > 0 ? threads : (int)std::thread::hardware_concurrency()));
     std::atomic<uint32_t> next(0);
+    std::vector<double> t_read(work.size(), 0.0), t_pack(work.size(), 0.0);
     auto worker = [&](uint32_t w) {
         Genome &g = work[w];                         // reused: no fresh pages per file
         for (uint32_t i = next++; i < n; i = next++) {
-            if (read_fasta(paths[g0 + i], g)) { err[i] = DREPHIP_ERR_IO; msg[i] = drephip_last_error(); continue; }
+            const auto r0 = std::chrono::steady_clock::now();
+            const int rr = read_fasta(paths[g0 + i], g);
+            const auto r1 = std::chrono::steady_clock::now();
+            t_read[w] += std::chrono::duration<double>(r1 - r0).count();
+            if (rr) { err[i] = DREPHIP_ERR_IO; msg[i] = drephip_last_error(); continue; }
             const uint64_t P = padded_span(genome_span(g.rec_len.data(), (uint32_t)g.rec_len.size()));
             B.length[i] = g.length;
             B.pad[i] = P;
@@ -439,6 +446,7 @@ static void produce_batch(const char *const *paths, uint32_t g0, uint32_t n_geno
             memset(slot.valid + B.off[i] / 32, 0, reserved[i] / 32 * 4);
             B.nk[i] = pack_records(g.seq.data(), g.rec_len.data(), (uint32_t)g.rec_len.size(), k, slot.codes,
                                    slot.valid, B.off[i]);
+            t_pack[w] += std::chrono::duration<double>(std::chrono::steady_clock::now() - r1).count();
         }
     };
     const uint32_t nt = (uint32_t)std::min<size_t>(work.size(), n);
@@ -448,8 +456,9 @@ static void produce_batch(const char *const *paths, uint32_t g0, uint32_t n_geno
     for (auto &th : pool) th.join();
     for (uint32_t i = 0; i < n; i++)
         if (err[i]) { B.err = err[i]; B.msg = msg[i]; return; }
+    for (size_t w = 0; w < work.size(); w++) { B.read_thread_s += t_read[w]; B.pack_thread_s += t_pack[w]; }
     uint64_t end = cur;
-    for (uint32_t i = 0; i < n; i++) if (over[i]) end += B.pad[i];
+    for (uint32_t i = 0; i < n; i++) if (over[i]) { end += B.pad[i]; B.overflow++; }
     if (end > cur) {
         if (grow_pinned(slot, end / 16 * 4, end / 32 * 4, cur / 16, cur / 32)) {
             B.err = DREPHIP_ERR_NOMEM; B.msg = "hipHostMalloc of the pinned ingest batch failed"; return;
@@ -528,6 +537,9 @@ DREPHIP_EXPORT int drephip_sketch_files(drephip_ctx *ctx, const char *const *pat
                                 cur.pad, cur.nk, hashes_out + (uint64_t)cur.g0 * ctx->s, nhash_out + cur.g0);
         ctx->ingest.gpu_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - g0).count();
         ctx->ingest.produce_s += cur.seconds;
+        ctx->ingest.read_thread_s += cur.read_thread_s;
+        ctx->ingest.pack_thread_s += cur.pack_thread_s;
+        ctx->ingest.overflow += cur.overflow;
         ctx->ingest.batches++;
         {
             std::lock_guard<std::mutex> lk(mu);
@@ -553,6 +565,15 @@ DREPHIP_EXPORT int drephip_last_ingest_stats(drephip_ctx *ctx, double *produce_s
     if (gpu_s) *gpu_s = ctx->ingest.gpu_s;
     if (wall_s) *wall_s = ctx->ingest.wall_s;
     if (batches) *batches = ctx->ingest.batches;
+    return DREPHIP_OK;
+}
+
+DREPHIP_EXPORT int drephip_last_ingest_phases(drephip_ctx *ctx, double *read_thread_s, double *pack_thread_s,
+                                              uint32_t *overflow) {
+    if (!ctx) { set_error("null context"); return DREPHIP_ERR_ARG; }
+    if (read_thread_s) *read_thread_s = ctx->ingest.read_thread_s;
+    if (pack_thread_s) *pack_thread_s = ctx->ingest.pack_thread_s;
+    if (overflow) *overflow = ctx->ingest.overflow;
     return DREPHIP_OK;
 }
 
@@ -775,8 +796,7 @@ DREPHIP_EXPORT int drephip_linkage(drephip_ctx *ctx, const double *y, uint32_t n
     double *d_D;
     int rc = dist_from_condensed_impl(ctx, y, n, &d_D, ctx->stream);
     if (rc) return rc;
-    rc = linkage_device_impl(ctx, d_D, n, method, Z, ctx->stream,
-                             [&] { double *d2; return dist_from_condensed_impl(ctx, y, n, &d2, ctx->stream); });
+    rc = linkage_device_impl(ctx, d_D, n, method, Z, ctx->stream);
     if (rc) return rc;
     timing_collect(ctx);
     ctx->link.wall_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -813,10 +833,7 @@ DREPHIP_EXPORT int drephip_linkage_counts_device(drephip_ctx *ctx, const uint16_
     double *d_D;
     rc = dist_matrix_impl(ctx, d_common, d_denom, n, perm, lut, lut_len, lut_off, &d_D, ctx->stream);
     if (rc) return rc;
-    rc = linkage_device_impl(ctx, d_D, n, method, Z, ctx->stream, [&] {
-        double *d2;
-        return dist_matrix_impl(ctx, d_common, d_denom, n, perm, lut, lut_len, lut_off, &d2, ctx->stream);
-    });
+    rc = linkage_device_impl(ctx, d_D, n, method, Z, ctx->stream);
     if (rc) return rc;
     timing_collect(ctx);
     ctx->link.wall_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -829,14 +846,6 @@ DREPHIP_EXPORT int drephip_linkage_reserve(drephip_ctx *ctx, uint32_t n) {
     if (n < 2) return DREPHIP_OK;
     void *p;
     return scratch(ctx, "lk_D", (uint64_t)n * n * 8, &p);
-}
-
-DREPHIP_EXPORT int drephip_last_linkage_path(drephip_ctx *ctx, int *path, int *steps, int *participants) {
-    if (!ctx) { set_error("null context"); return DREPHIP_ERR_ARG; }
-    if (path) *path = ctx->link.path;
-    if (steps) *steps = ctx->link.persist_steps;
-    if (participants) *participants = ctx->link.persist_participants;
-    return DREPHIP_OK;
 }
 
 DREPHIP_EXPORT int drephip_last_linkage_stats(drephip_ctx *ctx, double *alloc_s, double *matrix_s, double *chain_s,

@@ -4,7 +4,6 @@
 #include "common.h"
 
 #include <hip/hip_runtime.h>
-#include <functional>
 #include <map>
 #include <memory>
 #include <utility>
@@ -49,6 +48,9 @@ struct IngestStats {          // last drephip_sketch_files call
     double gpu_s = 0;         // H2D + sketch kernels + D2H, summed over batches (calling thread)
     double wall_s = 0;        // the whole call
     uint32_t batches = 0;
+    double read_thread_s = 0; // read + parse (incl. gzip inflate), summed over worker threads
+    double pack_thread_s = 0; // 2-bit pack into the pinned batch, summed over worker threads
+    uint32_t overflow = 0;    // genomes repacked because their span outgrew the file-size estimate
 };
 
 struct LinkStats {            // last drephip_linkage* call, host wall clock (seconds)
@@ -57,9 +59,6 @@ struct LinkStats {            // last drephip_linkage* call, host wall clock (se
     double chain_s = 0;       // nn-chain / MST steps (graph replays)
     double finish_s = 0;      // Z readback + stable sort + relabel on the host
     double wall_s = 0;        // the whole call
-    int path = 0;             // 0: per-step graph, 1: persistent kernel
-    int persist_steps = 0;    // steps the persistent kernel ran (0 when not used)
-    int persist_participants = 0;
 };
 
 struct drephip_ctx {
@@ -163,8 +162,7 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
 int allpairs_wait_impl(drephip_ctx *ctx);
 
 // Primary clustering (linkage.hip).
-int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, double *Z_out, hipStream_t st,
-                        const std::function<int()> &rebuild);
+int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, double *Z_out, hipStream_t st);
 int dist_matrix_impl(drephip_ctx *ctx, const uint16_t *d_common, const uint16_t *d_denom, uint32_t n,
                      const uint32_t *perm, const double *lut, uint32_t lut_len, const int32_t *lut_off,
                      double **d_D_out, hipStream_t st);

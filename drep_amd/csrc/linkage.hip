@@ -13,13 +13,14 @@
 // all-pairs shared-hash counts through a per-(denominator, common) table of
 // the exact float64 values dRep feeds scipy; nothing n^2 crosses PCIe.  Each
 // step of the (inherently sequential) chain is one launch: the previous
-// merge's row + column update fused with the grid-wide argmin over the chain
-// top's row, whose last workgroup makes the chain decision.  Steps are
-// launched in batches captured in a hipGraph; kernels after the last merge
-// exit at once.
-// Roofline: HBM -- a step reads one 8n-byte row (and after a merge two more
-// rows, writing a row and a strided column); at n = 10^5 (0.8 MB rows) the
-// ~5 us launch floor and the grid-wide reduction dominate.
+// step's chain decision (made by every workgroup from the previous launch's
+// partials), the pending merge's row + column update and the grid-wide argmin
+// over the chain top's row.  Steps are launched in batches captured in a
+// hipGraph; kernels after the last merge exit at once.
+// Roofline: latency -- a step reads one 8n-byte row (and after a merge two
+// more rows, writing a row and a strided column); at n = 10^5 (0.8 MB rows)
+// the kernel boundary and the dependent loads of a step (state -> partials
+// and decision -> row) dominate, ~6.4 us per step.
 
 #include "ctx.h"
 #include "../../include/drephip.h"
@@ -29,7 +30,6 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
-#include <functional>
 #include <numeric>
 #include <vector>
 
@@ -40,19 +40,6 @@ constexpr int kLkWG = 256;
 static double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
-
-struct LinkState {
-    int32_t chain_len;
-    int32_t first_active;    // smallest index with size > 0 (non-decreasing)
-    int32_t top, below;      // chain[len-1], chain[len-2] (below: -1 if len < 2): a step's row without a dependent load
-    int32_t k;               // merges done
-    int32_t pend;            // 1: the update kernel applies merge (px <- py)
-    int32_t px, py, pnx, pny;
-    double pd;
-    uint32_t ticket;         // last-workgroup detection of the search kernel
-    int32_t x;               // MST: current vertex
-    int32_t bad;             // a step found no valid partial (the host reports an internal error)
-};
 
 struct MinIdx { double v; int32_t i; };
 
@@ -90,143 +77,155 @@ __device__ MinIdx block_argmin(double v, int32_t i) {
     return r;
 }
 
-// Last workgroup of a grid: every workgroup publishes its partial, then one
-// agent-scope ticket; the workgroup that draws the last ticket reads all
-// partials (agent-scope loads, spread over its threads) and reduces them.
-// Every thread of the block must call it; the result is valid in thread 0.
-//
-// Visibility follows the "Valid forms" hand-off of MI355X_MICROARCH.md
-// (inter-workgroup visibility, first row of its sc1 table), condition by
-// condition:
-//   (1) every load of a partial is an agent-scope atomic load (global_load
-//       ... sc1, to registers, never flat);
-//   (2) every store of a partial is an agent-scope atomic store (sc1, 8 and 4
-//       bytes);
-//   (3) the storing lane -- the only one -- waits s_waitcnt vmcnt(0) after its
-//       stores and only then adds to the ONE unsharded ticket;
-//   (4) the consumer is the workgroup whose add came last, told by the value
-//       its add returned; its thread 0 reads after the add returned and the
-//       other waves after the __syncthreads that thread 0 joins; hipMalloc
-//       memory; at most one such workgroup per CU (grids of <= 1024
-//       256-thread workgroups over 256 CUs are dealt round-robin).
-// Under those four conditions the guide measured the sc1 loads as a valid
-// replacement for an agent-scope acquire, so no fence is issued: the acquire
-// (buffer_inv sc1 + its vmcnt wait, in the last workgroup only) measured +13 %
-// chain time at n = 10^4 and +4 % at 10^5 (profiles/r03_scale_*.json), and the
-// release/acquire ticket (buffer_wbl2 sc1 per workgroup per step) +21 %.  The
-// argument is about the gfx942/gfx950 sc1 path, not the HIP/LLVM memory
-// model, so the file refuses other targets.
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__) && !defined(__gfx942__)
-#error "linkage.hip's ticket reduction relies on the gfx942/gfx950 sc1 hand-off (MI355X_MICROARCH.md, Valid forms)"
-#endif
-__device__ bool last_block(MinIdx part, MinIdx *parts, LinkState *st, MinIdx &out) {
-    __shared__ int is_last;
-    if (threadIdx.x == 0) {
-        __hip_atomic_store(&parts[blockIdx.x].v, part.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&parts[blockIdx.x].i, part.i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t t = __hip_atomic_fetch_add(&st->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        is_last = t == gridDim.x - 1;
-        if (is_last) st->ticket = 0;
-    }
-    __syncthreads();
-    if (!is_last) return false;
-    double bv = INFINITY;
-    int32_t bi = 0x7fffffff;
-    for (uint32_t b = threadIdx.x; b < gridDim.x; b += blockDim.x) {
-        const double v = __hip_atomic_load(&parts[b].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int32_t i = __hip_atomic_load(&parts[b].i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (better(v, i, bv, bi)) { bv = v; bi = i; }
-    }
-    out = block_argmin(bv, bi);
-    return true;
-}
-
-// ---------------------------------------------------------------- nn_chain
-// Merge chain top x (size sx) with y (size sy) at distance cur (scipy: the
-// smaller index is dropped, the larger becomes the new cluster), pop both,
-// restart an empty chain at the first active cluster.  k: merges so far.
-__device__ void chain_merge(int32_t x, int32_t y, int32_t sx, int32_t sy, double cur, int32_t len, int32_t k,
-                            uint32_t n, int32_t *size, int32_t *chain, LinkState *st, double *Z, int32_t c3, int32_t c4) {
-    int32_t a = x, b = y, na = sx, nb = sy;
-    if (a > b) { a = y; b = x; na = sy; nb = sx; }
-    Z[4 * k + 0] = a; Z[4 * k + 1] = b; Z[4 * k + 2] = cur; Z[4 * k + 3] = na + nb;
-    size[a] = 0;
-    size[b] = na + nb;
-    st->pend = 1; st->px = a; st->py = b; st->pnx = na; st->pny = nb; st->pd = cur;
-    st->k = k + 1;
-    st->chain_len = len - 2;
-    st->top = c3;                                // chain[len-3], chain[len-4] (loaded at the step's start)
-    st->below = len >= 4 ? c4 : -1;
-    if (st->chain_len == 0 && k + 1 < (int32_t)n - 1) {
-        int32_t f = st->first_active;
-        while (size[f] == 0) f++;
-        st->first_active = f;
-        chain[0] = f;
-        st->chain_len = 1;
-        st->top = f;
-        st->below = -1;
-    }
-}
-
+// ---------------------------------------------------------------- the steps
 // One chain step per launch: the pending merge's Lance-Williams update (row and
 // column y) fused with the search of the chain top's row.  The search of row
 // t = chain top reads D[t][i]; the update rewrites only row/column y, so every
 // D[t][i] with i != y is untouched, and the one changed entry D[t][y] is
 // produced by the thread of i = y (the thread of i = t skips it), which also
-// uses it as its search value -- no cross-workgroup dependence.  After a chain
-// restart t may be y itself: then the search value of i is the freshly
-// computed D[y][i].  The last workgroup makes scipy's chain decision.
+// uses it as its search value -- no cross-workgroup dependence within the
+// step.  After a chain restart t may be y itself: then the search value of i
+// is the freshly computed D[y][i].
+//
+// A step's chain decision is made at the START of the next launch: kernel s
+// publishes its workgroup partials (plain stores -- the kernel boundary orders
+// them) and every workgroup of kernel s + 1 reads all of them and makes step
+// s's scipy decision itself (replicated: same partials, same state, same
+// bits) before doing step s + 1's work.  An earlier version reduced the
+// partials in the last workgroup of kernel s (a drained partial store, an
+// agent-scope ticket, the last workgroup's partial loads) and measured
+// 2.09 s at n = 10^5 against 1.92 s for this one (profiles/r03_linkage_*).
+// Workgroup 0 alone writes the decision's side effects (Z row, chain push)
+// and the state the next kernel reads; the two sizes a merge changes are
+// written by workgroup 0 of the launch AFTER the deciding one, and every
+// reader of that launch overrides them (it knows the decision), so no
+// workgroup reads a value another workgroup of the same launch may be
+// writing.  State and partials are double buffered by step parity q (kernel q
+// reads buffer q ^ 1 and writes q); the chain entries a launch reads after a
+// merge (the new top and below, chain[len-3] and chain[len-4]) are below the
+// position a push writes.
 //
 // A step is a chain of dependent memory round trips, so the loads are issued
 // together: each pass takes kLkPer entries per lane (grid-stride) and loads
 // their sizes and D[t][i] (plus D[x][i], D[y][i] after a merge) before any of
 // them is used or any store is made (written as one loop, the compiler kept
 // each entry's loads behind the previous entry's stores: D aliases itself).
-// D[t][i] may be loaded before the update's stores because the update writes
-// D[t][i] only for i = y, whose search value is the freshly computed entry.
-// Likewise the chain decision's D[t][chain[len-2]] and the two sizes are
-// loaded at the start by every workgroup's thread 0: the chain's elements
-// below the top are never x or y, so no update of this step touches them.
-// The chain's top and the element below it are kept in LinkState (the step's
-// row needs no load of chain[]), and chain[len-3], chain[len-4] -- the top
-// and below after a merge -- are loaded at the start too.
+// The decision's operands -- D[t][below] and the two sizes -- are loaded with
+// the partials: the chain's elements below the top are never x or y, so no
+// update touches them.
 constexpr int kLkPer = 4;
+struct alignas(64) LinkState {
+    int32_t k, len, top, below, first_active;
+    int32_t pend, x, y, nx, ny;   // Lance-Williams update this state's step applies
+    int32_t decide;               // 1: the reader first decides the previous step from its partials
+    int32_t bad;
+    int32_t mx;                   // MST: current vertex
+    int32_t psa, psb, psbsz;      // the sizes this state's merge changed (psa = -1: none), written to
+                                  // size[] by workgroup 0 of the NEXT kernel, which every reader of
+                                  // that kernel therefore overrides
+};
+
+// all partials of the previous kernel -> their minimum (thread 0)
+__device__ __forceinline__ MinIdx read_partials(const MinIdx *parts, uint32_t G) {
+    double bv = INFINITY;
+    int32_t bi = 0x7fffffff;
+    for (uint32_t b = threadIdx.x; b < G; b += blockDim.x) {
+        const MinIdx m = parts[b];
+        if (better(m.v, m.i, bv, bi)) { bv = m.v; bi = m.i; }
+    }
+    return block_argmin(bv, bi);
+}
+
 __global__ __launch_bounds__(kLkWG) void k_nn_step(double *__restrict__ D, uint32_t n, int method,
-                                                  int32_t *__restrict__ size, int32_t *__restrict__ chain,
-                                                  LinkState *__restrict__ st, MinIdx *__restrict__ parts,
-                                                  double *__restrict__ Z) {
-    const int32_t k0 = st->k;
-    if (k0 >= (int32_t)n - 1) return;                          // all merged: the rest of the batch idles
-    const bool pend = st->pend != 0;
-    const int32_t x = st->px, y = st->py, nx = st->pnx, ny = st->pny;
-    const int32_t len = st->chain_len;
-    const int32_t t = st->top;
+                                                   int32_t *__restrict__ size, int32_t *__restrict__ chain,
+                                                   LinkState *__restrict__ st, MinIdx *__restrict__ parts,
+                                                   int32_t *__restrict__ done, double *__restrict__ Z, uint32_t q) {
+    __shared__ LinkState sx;
+    const LinkState S = st[q ^ 1];
+    if (S.k >= (int32_t)n - 1) return;                         // all merged
+    const uint32_t G = gridDim.x;
+    const bool w0 = blockIdx.x == 0;
+    // size of cluster i as of the previous decision: workgroup 0 writes that
+    // decision's two sizes during this kernel, so every reader overrides them
+    auto size_prev = [&](int32_t i, int32_t stored) {
+        return i == S.psa ? 0 : i == S.psb ? S.psbsz : stored;
+    };
+    if (w0 && threadIdx.x == 0 && S.psa >= 0) { size[S.psa] = 0; size[S.psb] = S.psbsz; }
+    // ---- the previous step's decision (replicated in every workgroup)
+    double dp = 0.0;
+    int32_t szt = 0, szb = 0, c3 = 0, c4 = 0;
+    if (threadIdx.x == 0 && S.decide && S.len > 1) {
+        dp = D[(uint64_t)S.top * n + S.below];
+        szt = size_prev(S.top, size[S.top]); szb = size_prev(S.below, size[S.below]);
+        if (S.len >= 3) c3 = chain[S.len - 3];
+        if (S.len >= 4) c4 = chain[S.len - 4];
+    }
+    const MinIdx g = S.decide ? read_partials(parts + (uint64_t)(q ^ 1) * 1024, G) : MinIdx{0.0, 0};
+    if (threadIdx.x == 0) {
+        LinkState X = S;
+        X.psa = -1; X.psb = -1; X.psbsz = 0;
+        if (S.decide) {
+            X.pend = 0;
+            if ((uint32_t)g.i >= n) {                                  // no valid partial: stop
+                X.bad = 1; X.k = (int32_t)n - 1;
+            } else if (!(S.len > 1 && !(g.v < dp))) {                 // push (scipy: the previous element wins ties)
+                if (S.len >= (int32_t)n) { X.bad = 1; X.k = (int32_t)n - 1; }
+                else {
+                    if (w0) chain[S.len] = g.i;
+                    X.len = S.len + 1; X.below = S.top; X.top = g.i;
+                }
+            } else {                                                   // merge top with below at dp
+                int32_t a = S.top, b = S.below, na = szt, nb = szb;
+                if (a > b) { a = S.below; b = S.top; na = szb; nb = szt; }
+                if (w0) {
+                    double *z = Z + 4ull * S.k;
+                    z[0] = a; z[1] = b; z[2] = dp; z[3] = na + nb;
+                }
+                X.psa = a; X.psb = b; X.psbsz = na + nb;
+                X.pend = 1; X.x = a; X.y = b; X.nx = na; X.ny = nb;
+                X.k = S.k + 1;
+                X.len = S.len - 2;
+                X.top = c3;
+                X.below = X.len >= 2 ? c4 : -1;
+                if (X.len == 0 && X.k < (int32_t)n - 1) {             // restart at the first active cluster
+                    int32_t f = S.first_active;
+                    while (f < (int32_t)n && !(f == b || (f != a && size_prev(f, size[f]) > 0))) f++;
+                    if (f >= (int32_t)n) { X.bad = 1; X.k = (int32_t)n - 1; }
+                    else {
+                        if (w0) chain[0] = f;
+                        X.first_active = f; X.top = f; X.below = -1; X.len = 1;
+                    }
+                }
+            }
+        }
+        X.decide = 1;
+        sx = X;
+        if (w0) {
+            st[q] = X;
+            if (X.k >= (int32_t)n - 1) st[q ^ 1] = X;           // the finished state in both buffers
+            *done = X.k;
+        }
+    }
+    __syncthreads();
+    const LinkState X = sx;
+    if (X.k >= (int32_t)n - 1) return;
+    // ---- this step: the pending update fused with the search of row t
+    const bool pend = X.pend != 0;
+    const int32_t x = X.x, y = X.y, nx = X.nx, ny = X.ny, t = X.top;
     const double *Dt = D + (uint64_t)t * n;
     const double *Dx = D + (uint64_t)x * n;
     double *Dy = D + (uint64_t)y * n;
-    // a merge is always of t with yp = chain[len-2]: thread 0 loads the
-    // decision's operands (D[t][yp] and both sizes) now, off the last
-    // workgroup's critical path
-    int32_t yp = -1, szt = 0, szyp = 0, c3 = 0, c4 = 0;
-    double dp = 0.0;
-    if (threadIdx.x == 0 && len > 1) {
-        yp = st->below; dp = Dt[yp]; szt = size[t]; szyp = size[yp];
-        if (len >= 3) c3 = chain[len - 3];                   // the chain's new top and below after a merge
-        if (len >= 4) c4 = chain[len - 4];
-    }
-    // the old D[x][t], D[y][t] for the lane of i = y (loaded before any store)
     const double dxt = pend ? Dx[t] : 0.0, dyt = pend ? Dy[t] : 0.0;
     double bv = INFINITY;
     int32_t bi = 0x7fffffff;
-    const uint32_t stride = gridDim.x * kLkWG;
+    const uint32_t stride = G * kLkWG;
     for (uint32_t i0 = blockIdx.x * kLkWG + threadIdx.x; i0 < n; i0 += kLkPer * stride) {
         int32_t sz[kLkPer];
         double dt[kLkPer], dx[kLkPer], dy[kLkPer];
 #pragma unroll
         for (int k = 0; k < kLkPer; k++) {
             const uint32_t i = i0 + k * stride;
-            const uint32_t ic = i < n ? i : n - 1;              // in bounds; i >= n is skipped below
+            const uint32_t ic = i < n ? i : n - 1;
             sz[k] = size[ic];
             dt[k] = Dt[ic];
             if (pend) { dx[k] = Dx[ic]; dy[k] = Dy[ic]; }
@@ -234,7 +233,11 @@ __global__ __launch_bounds__(kLkWG) void k_nn_step(double *__restrict__ D, uint3
 #pragma unroll
         for (int k = 0; k < kLkPer; k++) {
             const uint32_t i = i0 + k * stride;
-            if (i >= n || sz[k] == 0) continue;
+            if (i >= n) continue;
+            // the sizes as of this step's decision: the previous decision's
+            // (being written by workgroup 0) and this one's (not yet written)
+            const int32_t szi = (int32_t)i == X.psa ? 0 : (int32_t)i == X.psb ? X.psbsz : size_prev((int32_t)i, sz[k]);
+            if (szi == 0) continue;
             double v;
             if (pend && (int32_t)i != y && (int32_t)i != t) {
                 const double u = lw_update(method, dx[k], dy[k], nx, ny);
@@ -242,7 +245,7 @@ __global__ __launch_bounds__(kLkWG) void k_nn_step(double *__restrict__ D, uint3
                 D[(uint64_t)i * n + y] = u;
                 v = t == y ? u : dt[k];
             } else if (pend && (int32_t)i == y && t != y) {
-                const double u = lw_update(method, dxt, dyt, nx, ny);      // entry (y, t): old values, unshared
+                const double u = lw_update(method, dxt, dyt, nx, ny);
                 Dy[t] = u;
                 D[(uint64_t)t * n + y] = u;
                 v = u;
@@ -250,55 +253,62 @@ __global__ __launch_bounds__(kLkWG) void k_nn_step(double *__restrict__ D, uint3
                 if ((int32_t)i == t) continue;
                 v = dt[k];
             }
-            if (v < bv) { bv = v; bi = (int32_t)i; }            // ascending i per thread: first minimum kept
+            if (v < bv) { bv = v; bi = (int32_t)i; }
         }
     }
     const MinIdx part = block_argmin(bv, bi);
-    MinIdx g;
-    if (!last_block(part, parts, st, g)) return;
-    if (threadIdx.x != 0) return;
-    if ((uint32_t)g.i >= n) {                    // no valid partial: stop every later step, the host reports it
-        st->bad = 1;
-        st->k = (int32_t)n - 1;
-        return;
-    }
-    // chain decision (scipy nn_chain): the previous chain element wins ties
-    st->pend = 0;
-    int32_t yy = g.i;
-    double cur = g.v;
-    bool merge = false;
-    if (len > 1 && !(g.v < dp)) { yy = yp; cur = dp; merge = true; }
-    if (!merge) {
-        if (len >= (int32_t)n) {                 // cannot happen on a consistent matrix: stop, no out-of-range store
-            st->bad = 1;
-            st->k = (int32_t)n - 1;
-            return;
-        }
-        chain[len] = yy;
-        st->chain_len = len + 1;
-        st->below = t;
-        st->top = yy;
-        return;
-    }
-    chain_merge(t, yy, szt, szyp, cur, len, k0, n, size, chain, st, Z, c3, c4);
+    if (threadIdx.x == 0) parts[(uint64_t)q * 1024 + blockIdx.x] = part;
 }
 
-// ------------------------------------------------------------ MST (single)
 __global__ __launch_bounds__(kLkWG) void k_mst_step(const double *__restrict__ D, uint32_t n,
-                                                   int32_t *__restrict__ merged, double *__restrict__ Dmin,
-                                                   LinkState *__restrict__ st, MinIdx *__restrict__ parts,
-                                                   double *__restrict__ Z) {
-    if (st->k >= (int32_t)n - 1) return;
-    const int32_t x = st->x;
+                                                    int32_t *__restrict__ merged, double *__restrict__ Dmin,
+                                                    LinkState *__restrict__ st, MinIdx *__restrict__ parts,
+                                                    int32_t *__restrict__ done, double *__restrict__ Z, uint32_t q) {
+    __shared__ LinkState sx;
+    __shared__ int32_t s_ov;
+    const LinkState S = st[q ^ 1];
+    if (S.k >= (int32_t)n - 1) return;
+    const uint32_t G = gridDim.x;
+    const MinIdx g = S.decide ? read_partials(parts + (uint64_t)(q ^ 1) * 1024, G) : MinIdx{0.0, 0};
+    if (threadIdx.x == 0) {
+        LinkState X = S;
+        int32_t ov = -1;
+        const bool w0 = blockIdx.x == 0;
+        if (S.decide) {
+            if ((uint32_t)g.i >= n) { X.bad = 1; X.k = (int32_t)n - 1; }
+            else {
+                if (w0) {
+                    double *z = Z + 4ull * S.k;
+                    z[0] = S.mx; z[1] = g.i; z[2] = g.v; z[3] = 0;
+                    merged[g.i] = 1;
+                }
+                ov = g.i;
+                X.mx = g.i;
+                X.k = S.k + 1;
+            }
+        }
+        X.decide = 1;
+        sx = X;
+        s_ov = ov;
+        if (w0) {
+            st[q] = X;
+            if (X.k >= (int32_t)n - 1) st[q ^ 1] = X;
+            *done = X.k;
+        }
+    }
+    __syncthreads();
+    const LinkState X = sx;
+    if (X.k >= (int32_t)n - 1) return;
+    const int32_t ov = s_ov, x = X.mx;
     const double *Dx = D + (uint64_t)x * n;
     double bv = INFINITY;
     int32_t bi = 0x7fffffff;
-    const uint32_t stride = gridDim.x * kLkWG;
+    const uint32_t stride = G * kLkWG;
     for (uint32_t i0 = blockIdx.x * kLkWG + threadIdx.x; i0 < n; i0 += kLkPer * stride) {
         int32_t mg[kLkPer];
         double dx[kLkPer], dm[kLkPer];
 #pragma unroll
-        for (int k = 0; k < kLkPer; k++) {                      // loads first (as k_nn_step)
+        for (int k = 0; k < kLkPer; k++) {
             const uint32_t i = i0 + k * stride;
             const uint32_t ic = i < n ? i : n - 1;
             mg[k] = merged[ic];
@@ -308,351 +318,14 @@ __global__ __launch_bounds__(kLkWG) void k_mst_step(const double *__restrict__ D
 #pragma unroll
         for (int k = 0; k < kLkPer; k++) {
             const uint32_t i = i0 + k * stride;
-            if (i >= n || mg[k]) continue;
+            if (i >= n || mg[k] || (int32_t)i == ov) continue;
             double m = dm[k];
             if (m > dx[k]) { m = dx[k]; Dmin[i] = m; }
             if (m < bv) { bv = m; bi = (int32_t)i; }
         }
     }
     const MinIdx part = block_argmin(bv, bi);
-    MinIdx g;
-    if (!last_block(part, parts, st, g)) return;
-    if (threadIdx.x != 0) return;
-    if ((uint32_t)g.i >= n) {
-        st->bad = 1;
-        st->k = (int32_t)n - 1;
-        return;
-    }
-    const int32_t k = st->k;
-    Z[4 * k + 0] = x; Z[4 * k + 1] = g.i; Z[4 * k + 2] = g.v; Z[4 * k + 3] = 0;
-    merged[g.i] = 1;
-    st->x = g.i;
-    st->k = k + 1;
-}
-
-// --------------------------------------------------- persistent chain / MST
-// The whole chain (or Prim's MST) in ONE launch: P participant workgroups of
-// kPW threads (one per CU; P <= 64 << 256 CUs, so all are resident), each
-// owning a contiguous slice of the n columns with its clusters' sizes (and,
-// for MST, the merged flags and running minima) in LDS.  A step is the
-// k_nn_step / k_mst_step work on the participant's slice, then an exchange:
-// every participant publishes its slice's candidate (value, index, that
-// cluster's size, and the slice's first active cluster other than the one a
-// merge of this step would retire, with its size) and a step tag; every
-// participant reads all P candidates and makes the SAME scipy decision from
-// them (replicated, deterministic), so no state is shared between
-// participants except the matrix itself and the published candidates.  The
-// chain (indices + sizes) lives in each participant's LDS.
-//
-// Visibility (MI355X_MICROARCH.md, Valid forms, first row of the sc1 table):
-// every load and store of the matrix and of the candidates is an agent-scope
-// (sc1) access; every wave drains its stores (s_waitcnt vmcnt(0)) before the
-// workgroup barrier behind which ONE lane stores the step tag (sc1); the
-// consumer lanes poll the tags with sc1 loads and read the candidates after
-// their tag matched; the other waves read after the workgroup barrier.  The
-// only matrix entries one participant reads after another wrote them are the
-// Lance-Williams column entries D[i][y], read as D[t][y] in a later step --
-// always after the writer's tag of the step that wrote them.
-//
-// Every spin is bounded (2 s of s_memrealtime per step): a participant that
-// never arrives makes the others stop with an error flag instead of hanging,
-// and the host then runs the per-step graph path.  Every index taken from a
-// candidate is range-checked before use.
-constexpr bool kLinkPersistDefault = false; // auto: the per-step graph path until the persistent one is the default
-constexpr int kPW = 1024;                 // threads per participant
-constexpr uint32_t kPMaxSlice = 4096;     // columns per participant (LDS: sizes 16 KB, MST minima 32 KB)
-constexpr uint32_t kPMaxP = 64;           // participants (one wave polls them)
-constexpr uint32_t kPChainCap = 4096;     // chain entries in LDS (longer: error flag, graph path)
-constexpr uint64_t kPTimeout = 200000000; // s_memrealtime ticks (100 MHz): 2 s per step
-
-struct PCand { double v; int32_t i, sz, fa, szfa; int32_t pad[2]; };   // 32 B per participant
-struct PStat { int32_t err; int32_t steps; int32_t pad[14]; };
-
-__device__ __forceinline__ double ld1(const double *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ void st1(double *p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ int32_t ld1i(const int32_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ void st1i(int32_t *p, int32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-
-// (v, i) lexicographic minimum of a workgroup plus a second minimum (f, with
-// its payload fs); results in thread 0.  Payload sz rides with (v, i).
-struct PRed { double v; int32_t i, sz, f, fs; };
-__device__ PRed block_reduce_p(PRed r) {
-    __shared__ PRed sr[kPW / 64];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        PRed q;
-        q.v = __shfl_xor(r.v, o, 64); q.i = __shfl_xor(r.i, o, 64); q.sz = __shfl_xor(r.sz, o, 64);
-        q.f = __shfl_xor(r.f, o, 64); q.fs = __shfl_xor(r.fs, o, 64);
-        if (better(q.v, q.i, r.v, r.i)) { r.v = q.v; r.i = q.i; r.sz = q.sz; }
-        if (q.f < r.f) { r.f = q.f; r.fs = q.fs; }
-    }
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) sr[w] = r;
-    __syncthreads();
-    if (threadIdx.x == 0)
-        for (int k = 1; k < kPW / 64; k++) {
-            const PRed q = sr[k];
-            if (better(q.v, q.i, r.v, r.i)) { r.v = q.v; r.i = q.i; r.sz = q.sz; }
-            if (q.f < r.f) { r.f = q.f; r.fs = q.fs; }
-        }
-    return r;
-}
-
-// Publish this participant's candidate for step `step` and collect everyone's:
-// returns the global reduction in thread 0; false (all threads) on a timeout.
-__device__ bool p_exchange(PRed mine, uint32_t step, uint32_t P, PCand *cand, int32_t *tags, PRed &out,
-                           PStat *stat) {
-    __shared__ int s_ok;
-    PCand *slot = cand + (uint64_t)(step & 1) * kPMaxP;
-    // every wave's matrix stores are complete before the tag (condition 3)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        PCand *c = slot + blockIdx.x;
-        st1(&c->v, mine.v);
-        st1i(&c->i, mine.i); st1i(&c->sz, mine.sz); st1i(&c->fa, mine.f); st1i(&c->szfa, mine.fs);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        st1i(&tags[blockIdx.x * 16], (int32_t)step);
-    }
-    if (threadIdx.x < 64) {
-        const uint32_t lane = threadIdx.x;
-        PRed r{INFINITY, 0x7fffffff, 0, 0x7fffffff, 0};
-        bool ok = true;
-        if (lane < P) {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            while (ld1i(&tags[lane * 16]) != (int32_t)step) {
-                __builtin_amdgcn_s_sleep(1);
-                if (__builtin_amdgcn_s_memrealtime() - t0 > kPTimeout) { ok = false; break; }
-            }
-            if (ok) {
-                const PCand *c = slot + lane;
-                r.v = ld1(&c->v); r.i = ld1i(&c->i); r.sz = ld1i(&c->sz); r.f = ld1i(&c->fa); r.fs = ld1i(&c->szfa);
-            }
-        }
-        const bool all_ok = __builtin_amdgcn_ballot_w64(!ok) == 0;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            PRed q;
-            q.v = __shfl_xor(r.v, o, 64); q.i = __shfl_xor(r.i, o, 64); q.sz = __shfl_xor(r.sz, o, 64);
-            q.f = __shfl_xor(r.f, o, 64); q.fs = __shfl_xor(r.fs, o, 64);
-            if (better(q.v, q.i, r.v, r.i)) { r.v = q.v; r.i = q.i; r.sz = q.sz; }
-            if (q.f < r.f) { r.f = q.f; r.fs = q.fs; }
-        }
-        if (lane == 0) {
-            out = r;
-            s_ok = all_ok;
-            if (!all_ok) st1i(&stat->err, 1);
-        }
-    }
-    __syncthreads();
-    return s_ok != 0;
-}
-
-// Replicated nn-chain state (identical in every participant; thread 0 writes
-// it, everyone reads it after a barrier)
-struct PChain {
-    int32_t k, len, top, below, pend, x, y, nx, ny, stop;
-};
-
-template <int PER>
-__global__ __launch_bounds__(kPW) void k_chain_persist(double *__restrict__ D, uint32_t n, int method, uint32_t S,
-                                                       PCand *__restrict__ cand, int32_t *__restrict__ tags,
-                                                       PStat *__restrict__ stat, double *__restrict__ Z) {
-    __shared__ int32_t size_s[kPMaxSlice];
-    __shared__ int32_t ch_i[kPChainCap], ch_s[kPChainCap];
-    __shared__ PChain cs;
-    __shared__ double s_dp;
-    const uint32_t P = gridDim.x, p = blockIdx.x;
-    const uint32_t lo = p * S, hi = min(n, lo + S);
-    for (uint32_t j = threadIdx.x; j < S; j += kPW) size_s[j] = lo + j < hi ? 1 : 0;
-    if (threadIdx.x == 0) {
-        cs = PChain{0, 1, 0, -1, 0, 0, 0, 0, 0, 0};
-        ch_i[0] = 0; ch_s[0] = 1;
-    }
-    __syncthreads();
-    for (uint32_t step = 0;; step++) {
-        const PChain c = cs;
-        if (c.k >= (int32_t)n - 1 || c.stop) break;
-        const int32_t t = c.top;
-        const bool pend = c.pend != 0;
-        const int32_t x = c.x, y = c.y;
-        const int32_t a_m = c.len > 1 ? min(t, c.below) : -1;          // retired if this step merges
-        const double *Dt = D + (uint64_t)t * n;
-        const double *Dx = D + (uint64_t)x * n;
-        double *Dy = D + (uint64_t)y * n;
-        if (threadIdx.x == 0 && c.len > 1) s_dp = ld1(Dt + c.below);
-        const bool own_y = pend && (uint32_t)y >= lo && (uint32_t)y < hi;
-        const double dxt = own_y ? ld1(Dx + t) : 0.0, dyt = own_y ? ld1(Dy + t) : 0.0;
-        PRed r{INFINITY, 0x7fffffff, 0, 0x7fffffff, 0};
-        for (uint32_t j0 = threadIdx.x; j0 < hi - lo; j0 += PER * kPW) {
-            int32_t sz[PER];
-            double dt[PER], dx[PER], dy[PER];
-#pragma unroll
-            for (int q = 0; q < PER; q++) {
-                const uint32_t j = j0 + q * kPW;
-                const uint32_t jc = j < hi - lo ? j : hi - lo - 1;
-                const uint32_t i = lo + jc;
-                sz[q] = size_s[jc];
-                dt[q] = ld1(Dt + i);
-                if (pend) { dx[q] = ld1(Dx + i); dy[q] = ld1(Dy + i); }
-            }
-#pragma unroll
-            for (int q = 0; q < PER; q++) {
-                const uint32_t j = j0 + q * kPW;
-                if (j >= hi - lo || sz[q] == 0) continue;
-                const int32_t i = (int32_t)(lo + j);
-                if (i != a_m && i < r.f) { r.f = i; r.fs = sz[q]; }
-                double v;
-                if (pend && i != y && i != t) {
-                    const double u = lw_update(method, dx[q], dy[q], c.nx, c.ny);
-                    st1(Dy + i, u);
-                    st1(D + (uint64_t)i * n + y, u);
-                    v = t == y ? u : dt[q];
-                } else if (pend && i == y && t != y) {
-                    const double u = lw_update(method, dxt, dyt, c.nx, c.ny);
-                    st1(Dy + t, u);
-                    st1(D + (uint64_t)t * n + y, u);
-                    v = u;
-                } else {
-                    if (i == t) continue;
-                    v = dt[q];
-                }
-                if (v < r.v) { r.v = v; r.i = i; r.sz = sz[q]; }
-            }
-        }
-        r = block_reduce_p(r);
-        PRed g;
-        if (!p_exchange(r, step, P, cand, tags, g, stat)) return;
-        if (threadIdx.x == 0) {
-            PChain d = c;
-            d.pend = 0;
-            if ((uint32_t)g.i >= n) { st1i(&stat->err, 2); d.stop = 1; }
-            else {
-                const double dp = s_dp;
-                const bool merge = c.len > 1 && !(g.v < dp);
-                if (!merge) {
-                    if (c.len >= (int32_t)kPChainCap || c.len >= (int32_t)n) { st1i(&stat->err, 3); d.stop = 1; }
-                    else {
-                        ch_i[c.len] = g.i; ch_s[c.len] = g.sz;
-                        d.len = c.len + 1; d.below = t; d.top = g.i;
-                    }
-                } else {
-                    const int32_t yb = c.below;
-                    const int32_t st_ = ch_s[c.len - 1], sb = ch_s[c.len - 2];
-                    int32_t a = t, b = yb, na = st_, nb = sb;
-                    if (a > b) { a = yb; b = t; na = sb; nb = st_; }
-                    if (p == 0) {
-                        double *z = Z + 4ull * c.k;
-                        z[0] = a; z[1] = b; z[2] = dp; z[3] = na + nb;
-                    }
-                    if ((uint32_t)a >= lo && (uint32_t)a < hi) size_s[a - lo] = 0;
-                    if ((uint32_t)b >= lo && (uint32_t)b < hi) size_s[b - lo] = na + nb;
-                    d.pend = 1; d.x = a; d.y = b; d.nx = na; d.ny = nb;
-                    d.k = c.k + 1;
-                    d.len = c.len - 2;
-                    d.top = d.len > 0 ? ch_i[d.len - 1] : -1;
-                    d.below = d.len > 1 ? ch_i[d.len - 2] : -1;
-                    if (d.len == 0 && d.k < (int32_t)n - 1) {
-                        if ((uint32_t)g.f >= n) { st1i(&stat->err, 4); d.stop = 1; }
-                        else { ch_i[0] = g.f; ch_s[0] = g.fs; d.len = 1; d.top = g.f; d.below = -1; }
-                    }
-                }
-            }
-            cs = d;
-            if (p == 0) stat->steps = (int32_t)step + 1;
-        }
-        __syncthreads();
-    }
-}
-
-template <int PER>
-__global__ __launch_bounds__(kPW) void k_mst_persist(const double *__restrict__ D, uint32_t n, uint32_t S,
-                                                     PCand *__restrict__ cand, int32_t *__restrict__ tags,
-                                                     PStat *__restrict__ stat, double *__restrict__ Z) {
-    __shared__ double dmin_s[kPMaxSlice];
-    __shared__ uint8_t merged_s[kPMaxSlice];
-    __shared__ int32_t s_x, s_k, s_stop;
-    const uint32_t P = gridDim.x, p = blockIdx.x;
-    const uint32_t lo = p * S, hi = min(n, lo + S);
-    for (uint32_t j = threadIdx.x; j < S; j += kPW) { dmin_s[j] = INFINITY; merged_s[j] = lo + j >= hi || lo + j == 0; }
-    if (threadIdx.x == 0) { s_x = 0; s_k = 0; s_stop = 0; }           // scipy: x = 0, merged[0] = 1
-    __syncthreads();
-    for (uint32_t step = 0;; step++) {
-        const int32_t x = s_x, k = s_k;
-        if (k >= (int32_t)n - 1 || s_stop) break;
-        const double *Dx = D + (uint64_t)x * n;
-        PRed r{INFINITY, 0x7fffffff, 0, 0x7fffffff, 0};
-        for (uint32_t j0 = threadIdx.x; j0 < hi - lo; j0 += PER * kPW) {
-            double dx[PER];
-#pragma unroll
-            for (int q = 0; q < PER; q++) {
-                const uint32_t j = j0 + q * kPW;
-                dx[q] = ld1(Dx + lo + (j < hi - lo ? j : hi - lo - 1));
-            }
-#pragma unroll
-            for (int q = 0; q < PER; q++) {
-                const uint32_t j = j0 + q * kPW;
-                if (j >= hi - lo || merged_s[j]) continue;
-                double m = dmin_s[j];
-                if (m > dx[q]) { m = dx[q]; dmin_s[j] = m; }
-                if (m < r.v) { r.v = m; r.i = (int32_t)(lo + j); }
-            }
-        }
-        r = block_reduce_p(r);
-        PRed g;
-        if (!p_exchange(r, step, P, cand, tags, g, stat)) return;
-        if (threadIdx.x == 0) {
-            if ((uint32_t)g.i >= n) { st1i(&stat->err, 2); s_stop = 1; }
-            else {
-                if (p == 0) {
-                    double *z = Z + 4ull * k;
-                    z[0] = x; z[1] = g.i; z[2] = g.v; z[3] = 0;
-                }
-                if ((uint32_t)g.i >= lo && (uint32_t)g.i < hi) merged_s[g.i - lo] = 1;
-                s_x = g.i;
-                s_k = k + 1;
-            }
-            if (p == 0) stat->steps = (int32_t)step + 1;
-        }
-        __syncthreads();
-    }
-}
-
-// Persistent path: returns DREPHIP_OK with d_Z filled, or DREPHIP_ERR_INTERNAL
-// (with the reason in the error text) when a participant timed out or the
-// chain outgrew its LDS -- the caller then runs the per-step graph path.
-static int linkage_persist(drephip_ctx *ctx, double *d_D, uint32_t n, int method, double *d_Z, hipStream_t st) {
-    uint32_t P = std::max(1u, std::min(kPMaxP, (n + 2047) / 2048));
-    uint32_t S = (n + P - 1) / P;
-    if (S > kPMaxSlice) { set_error("persistent linkage: n too large"); return DREPHIP_ERR_UNSUPPORTED; }
-    PCand *d_cand;
-    int32_t *d_tags;
-    PStat *d_stat, *h_stat;
-    int rc;
-    if ((rc = scratch(ctx, "lkp_cand", 2 * kPMaxP * sizeof(PCand), (void **)&d_cand))) return rc;
-    if ((rc = scratch(ctx, "lkp_tags", kPMaxP * 16 * 4, (void **)&d_tags))) return rc;
-    if ((rc = scratch(ctx, "lkp_stat", sizeof(PStat), (void **)&d_stat))) return rc;
-    if ((rc = pinned_host(ctx, "lkp_stat", sizeof(PStat), (void **)&h_stat))) return rc;
-    HIPC(hipMemsetAsync(d_tags, 0xFF, kPMaxP * 16 * 4, st));         // tag -1: no step published
-    HIPC(hipMemsetAsync(d_stat, 0, sizeof(PStat), st));
-    timing_mark(ctx, 2, st, true);
-    if (method == DREPHIP_LINK_SINGLE)
-        hipLaunchKernelGGL(k_mst_persist<4>, dim3(P), dim3(kPW), 0, st, d_D, n, S, d_cand, d_tags, d_stat, d_Z);
-    else
-        hipLaunchKernelGGL(k_chain_persist<4>, dim3(P), dim3(kPW), 0, st, d_D, n, method, S, d_cand, d_tags, d_stat, d_Z);
-    timing_mark(ctx, 2, st, false);
-    HIPC(hipGetLastError());
-    HIPC(hipMemcpyAsync(h_stat, d_stat, sizeof(PStat), hipMemcpyDeviceToHost, st));
-    HIPC(hipStreamSynchronize(st));
-    ctx->link.persist_steps = h_stat->steps;
-    ctx->link.persist_participants = P;
-    if (h_stat->err) {
-        static const char *why[] = {"", "a participant timed out", "no valid candidate", "chain longer than its LDS",
-                                    "no cluster to restart the chain"};
-        set_error(std::string("persistent linkage stopped: ") + why[std::min(h_stat->err, 4)]);
-        return DREPHIP_ERR_INTERNAL;
-    }
-    return DREPHIP_OK;
+    if (threadIdx.x == 0) parts[(uint64_t)q * 1024 + blockIdx.x] = part;
 }
 
 // ------------------------------------------------------------ matrix build
@@ -778,17 +451,7 @@ static void sort_and_label(std::vector<double> &Z, uint32_t n) {
     Z.swap(S);
 }
 
-// Which chain implementation runs: DREPHIP_LINK_PATH=persist (one persistent
-// launch), graph (per-step kernels replayed from a hipGraph), or auto.
-static bool use_persistent(uint32_t n) {
-    const char *e = getenv("DREPHIP_LINK_PATH");
-    if (e && !strcmp(e, "graph")) return false;
-    if (e && !strcmp(e, "persist")) return true;
-    return kLinkPersistDefault && n <= kPMaxP * kPMaxSlice;
-}
-
-int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, double *Z_out, hipStream_t st,
-                        const std::function<int()> &rebuild) {
+int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, double *Z_out, hipStream_t st) {
     if (n < 2) return DREPHIP_OK;
     const double t_chain = now_s();           // chain_s: scratch, graph capture and the steps
     if (method != DREPHIP_LINK_SINGLE && method != DREPHIP_LINK_COMPLETE && method != DREPHIP_LINK_AVERAGE &&
@@ -796,35 +459,12 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
         set_error("linkage method must be single, complete, average or weighted");
         return DREPHIP_ERR_UNSUPPORTED;
     }
-    ctx->link.path = 0;
-    if (use_persistent(n) && n <= kPMaxP * kPMaxSlice) {
-        double *d_Zp;
-        int rc;
-        if ((rc = scratch(ctx, "lk_Z", (n - 1) * 32ull, (void **)&d_Zp))) return rc;
-        rc = linkage_persist(ctx, d_D, n, method, d_Zp, st);
-        if (rc == DREPHIP_OK) {
-            ctx->link.path = 1;
-            const double t_fin = now_s();
-            ctx->link.chain_s = t_fin - t_chain;
-            std::vector<double> Z(4ull * (n - 1));
-            HIPC(hipMemcpy(Z.data(), d_Zp, Z.size() * 8, hipMemcpyDeviceToHost));
-            sort_and_label(Z, n);
-            std::copy(Z.begin(), Z.end(), Z_out);
-            ctx->link.finish_s = now_s() - t_fin;
-            return DREPHIP_OK;
-        }
-        if (rc != DREPHIP_ERR_INTERNAL) return rc;
-        // a participant timed out or the chain outgrew its LDS: the matrix may
-        // hold partial Lance-Williams updates -- rebuilt, then the graph path
-        fprintf(stderr, "[drephip] %s; running the per-step linkage path\n", drephip_last_error());
-        if ((rc = rebuild())) return rc;
-    }
     // entries per lane of a step, i.e. the grid density (default kLkPer: one pass;
     // DREPHIP_LINK_PER_LANE exists for the tests, which cover 1, 4 and 16)
     const char *pl = getenv("DREPHIP_LINK_PER_LANE");
     const uint32_t per = pl ? std::max(1, std::min(64, atoi(pl))) : 4;
     const uint32_t grid = std::max(1u, std::min(1024u, (n + kLkWG * per - 1) / (kLkWG * per)));
-    int32_t *d_size, *d_chain;
+    int32_t *d_size, *d_chain, *d_done;
     double *d_Z, *d_Dmin;
     LinkState *d_st;
     MinIdx *d_parts;
@@ -832,41 +472,47 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     if ((rc = scratch(ctx, "lk_size", n * 4ull, (void **)&d_size))) return rc;
     if ((rc = scratch(ctx, "lk_chain", n * 4ull, (void **)&d_chain))) return rc;
     if ((rc = scratch(ctx, "lk_Z", (n - 1) * 32ull, (void **)&d_Z))) return rc;
-    if ((rc = scratch(ctx, "lk_st", sizeof(LinkState), (void **)&d_st))) return rc;
-    if ((rc = scratch(ctx, "lk_parts", 1024 * sizeof(MinIdx), (void **)&d_parts))) return rc;
+    if ((rc = scratch(ctx, "lk_parts", 2 * 1024 * sizeof(MinIdx), (void **)&d_parts))) return rc;
+    if ((rc = scratch(ctx, "lk_st", 2 * sizeof(LinkState), (void **)&d_st))) return rc;
+    if ((rc = scratch(ctx, "lk_done", 4, (void **)&d_done))) return rc;
     const bool mst = method == DREPHIP_LINK_SINGLE;
     if (mst && (rc = scratch(ctx, "lk_dmin", n * 8ull, (void **)&d_Dmin))) return rc;
-    LinkState h{};
-    std::vector<int32_t> init(n, 1);
     if (mst) {
         std::vector<double> inf(n, INFINITY);
         std::vector<int32_t> mg(n, 0);
         mg[0] = 1;                                            // scipy: x = 0, merged[x] = 1
         HIPC(hipMemcpyAsync(d_size, mg.data(), n * 4ull, hipMemcpyHostToDevice, st));
         HIPC(hipMemcpyAsync(d_Dmin, inf.data(), n * 8ull, hipMemcpyHostToDevice, st));
-        h.x = 0;
     } else {
+        std::vector<int32_t> init(n, 1);
         HIPC(hipMemcpyAsync(d_size, init.data(), n * 4ull, hipMemcpyHostToDevice, st));
         int32_t zero = 0;
         HIPC(hipMemcpyAsync(d_chain, &zero, 4, hipMemcpyHostToDevice, st));
-        h.chain_len = 1;                                      // chain starts at the first active cluster, 0
-        h.top = 0;
-        h.below = -1;
     }
-    HIPC(hipMemcpyAsync(d_st, &h, sizeof(h), hipMemcpyHostToDevice, st));
+    {   // the chain starts at the first active cluster, 0 (MST: at vertex 0); the
+        // first kernel (parity 0) reads buffer 1, with no decision pending
+        LinkState h[2] = {};
+        h[1].len = 1; h[1].top = 0; h[1].below = -1; h[1].first_active = 0; h[1].mx = 0;
+        h[1].psa = h[1].psb = -1;
+        h[0] = h[1];
+        HIPC(hipMemcpyAsync(d_st, h, sizeof(h), hipMemcpyHostToDevice, st));
+        int32_t zero = 0;
+        HIPC(hipMemcpyAsync(d_done, &zero, 4, hipMemcpyHostToDevice, st));
+    }
     // batches of steps captured once in a graph, replayed until every merge is done
     constexpr int kBatch = 256;
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
     HIPC(hipStreamSynchronize(st));
     HIPC(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    static_assert(kBatch % 2 == 0, "step parity must restart at 0 with every replay");
     for (int b = 0; b < kBatch; b++) {
-        if (mst) {
-            hipLaunchKernelGGL(k_mst_step, dim3(grid), dim3(kLkWG), 0, st, d_D, n, d_size, d_Dmin, d_st, d_parts, d_Z);
-        } else {
+        if (mst)
+            hipLaunchKernelGGL(k_mst_step, dim3(grid), dim3(kLkWG), 0, st, d_D, n, d_size, d_Dmin, d_st, d_parts,
+                               d_done, d_Z, (uint32_t)(b & 1));
+        else
             hipLaunchKernelGGL(k_nn_step, dim3(grid), dim3(kLkWG), 0, st, d_D, n, method, d_size, d_chain, d_st,
-                               d_parts, d_Z);
-        }
+                               d_parts, d_done, d_Z, (uint32_t)(b & 1));
     }
     HIPC(hipStreamEndCapture(st, &graph));
     hipError_t e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
@@ -880,7 +526,7 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
         e = hipGraphLaunch(exec, st);
         if (e != hipSuccess) break;
         if ((it & 3) == 3 || it + 1 == max_batches) {
-            e = hipMemcpyAsync(&done, &d_st->k, 4, hipMemcpyDeviceToHost, st);
+            e = hipMemcpyAsync(&done, d_done, 4, hipMemcpyDeviceToHost, st);
             if (e == hipSuccess) e = hipStreamSynchronize(st);
             if (e != hipSuccess || done >= (int32_t)n - 1) break;
         }
@@ -889,11 +535,12 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     (void)hipGraphExecDestroy(exec);
     (void)hipGraphDestroy(graph);
     HIPC(e);
-    HIPC(hipMemcpyAsync(&done, &d_st->k, 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(&done, d_done, 4, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));
     if (done != (int32_t)n - 1) { set_error("linkage did not finish"); return DREPHIP_ERR_INTERNAL; }
-    int32_t bad = 0;
-    HIPC(hipMemcpy(&bad, &d_st->bad, 4, hipMemcpyDeviceToHost));
+    LinkState hs[2];
+    HIPC(hipMemcpy(hs, d_st, sizeof(hs), hipMemcpyDeviceToHost));
+    const int32_t bad = hs[0].bad | hs[1].bad;
     if (bad) { set_error("linkage: a chain step found no valid partial"); return DREPHIP_ERR_INTERNAL; }
     const double t_fin = now_s();
     ctx->link.chain_s = t_fin - t_chain;

@@ -120,6 +120,13 @@ int drephip_sketch_files(drephip_ctx *ctx, const char *const *paths, uint32_t n_
 int drephip_last_ingest_stats(drephip_ctx *ctx, double *produce_s, double *gpu_s, double *wall_s,
                               uint32_t *batches);
 
+/* Host phases of the last drephip_sketch_files call, summed over the worker
+ * threads (seconds): FASTA read + parse (gzip inflate included) and the 2-bit
+ * pack; and the number of genomes whose span outgrew the region their file
+ * size (or gzip ISIZE) reserved, repacked at the end of their batch. */
+int drephip_last_ingest_phases(drephip_ctx *ctx, double *read_thread_s, double *pack_thread_s,
+                               uint32_t *overflow);
+
 /* Device-resident sketch: packed genome set already in HBM (see layout).
  * h_base_off/h_padded/h_nkmers are host arrays of n_genomes entries
  * (h_nkmers: valid k-mer positions, used only to seed the candidate
@@ -278,12 +285,6 @@ int drephip_linkage_reserve(drephip_ctx *ctx, uint32_t n);
  * stable sort and relabel, and the whole call. */
 int drephip_last_linkage_stats(drephip_ctx *ctx, double *alloc_s, double *matrix_s, double *chain_s,
                                double *finish_s, double *wall_s);
-
-/* Which chain implementation the last drephip_linkage* call ran: *path = 0
- * for the per-step kernels replayed from a hipGraph, 1 for the persistent
- * kernel (steps it ran, participant workgroups).  DREPHIP_LINK_PATH=graph /
- * persist / auto selects it. */
-int drephip_last_linkage_path(drephip_ctx *ctx, int *path, int *steps, int *participants);
 
 /* HIP-event timing of kernel launches: `kernels` is a bitmask of the kernels
  * to bracket with events (bit w = `which` w of drephip_last_kernel_ms; -1 =

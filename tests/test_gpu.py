@@ -808,10 +808,9 @@ def test_gpu_linkage_matches_scipy(method, n, kind):
     """drephip_linkage == scipy.cluster.hierarchy.linkage bit for bit, with
     Mash-like ties (a few distinct distances, many 1.0), continuous values,
     all-equal distances, a few values whose Lance-Williams averages round
-    (fewvals), and family structure with 1.0 between families (mash): the
-    per-step graph path at three grid densities of the chain-step kernel, and
-    the persistent kernel (one participant per 2048 columns: n = 2100 and 4500
-    have 2 and 3 participants exchanging candidates)."""
+    (fewvals), and family structure with 1.0 between families (mash), at three
+    grid densities of the chain-step kernel (16 entries per lane: several
+    passes)."""
     import scipy.cluster.hierarchy as sch
     rng = np.random.default_rng(n * 31 + len(method))
     m = n * (n - 1) // 2
@@ -831,24 +830,15 @@ def test_gpu_linkage_matches_scipy(method, n, kind):
     else:
         y = np.full(m, 0.5)
     Zs = sch.linkage(y, method=method)
-    runs = [("graph", "4"), ("graph", "1"), ("graph", "16"), ("persist", None)]
-    if n > 2000:
-        runs = [("graph", "4"), ("persist", None)]
-    for path, per_lane in runs:                      # grid densities of the chain-step kernel (16: 4 passes)
-        os.environ["DREPHIP_LINK_PATH"] = path
-        if per_lane:
-            os.environ["DREPHIP_LINK_PER_LANE"] = per_lane
+    for per_lane in (("4", "1", "16") if n <= 2000 else ("4",)):   # grid densities of the chain-step kernel
+        os.environ["DREPHIP_LINK_PER_LANE"] = per_lane
         try:
             with _lib.Context(0, 21, S, 42) as ctx:
                 Z = ctx.linkage(y, method)
-                st = ctx.linkage_stats()
         finally:
             os.environ.pop("DREPHIP_LINK_PER_LANE", None)
-            os.environ.pop("DREPHIP_LINK_PATH", None)
         assert Z.shape == Zs.shape
-        assert np.array_equal(Z, Zs), (path, per_lane, np.argwhere(Z != Zs)[:5])
-        if n >= 2:
-            assert st["path"] == ("persistent" if path == "persist" else "graph"), st
+        assert np.array_equal(Z, Zs), (per_lane, np.argwhere(Z != Zs)[:5])
 
 
 @pytest.mark.parametrize("method", ["average", "single"])

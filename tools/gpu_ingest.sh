@@ -8,6 +8,6 @@ python3 - <<'PY'
 import json
 d = json.load(open("gpurun_out/ingest.json"))
 for k in ("plain_first_call", "plain", "gzip"):
-    print(k, {x: round(d[k][x], 4) for x in ("wall_s", "library_wall_s", "host_read_pack_s", "device_s", "batches")})
+    print(k, {x: round(d[k][x], 4) for x in ("wall_s", "Mbp_per_s", "library_wall_s", "host_read_pack_s", "read_parse_thread_s", "pack_thread_s", "device_s", "batches")})
 print(d["dropin_all_vs_all_MASH"])
 PY

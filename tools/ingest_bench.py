@@ -50,6 +50,8 @@ with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
             out[name] = {"files": len(files), "bases": bases, "wall_s": dt, "Mbp_per_s": bases / dt / 1e6,
                          "library_wall_s": st["wall_s"],
                          "host_read_pack_s": st["produce_s"], "device_s": st["gpu_s"], "batches": st["batches"],
+                         "read_parse_thread_s": st["read_thread_s"], "pack_thread_s": st["pack_thread_s"],
+                         "overflow_genomes": st["overflow_genomes"],
                          "ingest_only_Mbp_per_s": bases / st["produce_s"] / 1e6,
                          "overlap_note": "wall ~ host read+pack of every batch + the last batch's device work "
                                          "(the other batches' device work runs behind the next batch's ingest)"}
