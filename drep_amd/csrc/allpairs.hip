@@ -474,16 +474,17 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
         // among the s smallest of A_r u B -- the rank rule (probe_rows) counts
         // nothing more, and |A u B| > s makes a partial pair's denominator s
         // whatever mrun the rest would add.  Tested for rows with no match so
-        // far, where unrelated sketches get there: at chunk kb1 (j0 = 64 kb1,
-        // about half the column; the group's first chunk) and at chunk kb1 + 1
-        // (inside that group: with 4 rows, the first test ends only ~40 % of
-        // unrelated columns -- B[512] > A_r[487] holds for ~79 % of rows at s =
-        // 1000 -- the second nearly all), then at every later group start:
-        // b0 > A_r[s - j0 - 1] (thr1 at kb1, thr2 at kb1 + 1: scalar, loaded
+        // far, at the group starting at chunk kb1 (j0 = 64 kb1, about half the
+        // column, where unrelated sketches get there) and every later group:
+        // b0 > A_r[s - j0 - 1] (thr1 at kb1, thr2 at kb1 + 4: scalar, loaded
         // with the row's largest hash) gives #{A_r < b0} >= s - j0, and thr2
         // stays a sufficient bound at every later j0.  Scalar compares only (a
         // sampled high-word read per row measured slower than the chunks it
-        // skipped).
+        // skipped).  With 4 rows the kb1 test ends only ~40 % of unrelated
+        // columns (B[512] > A_r[487] holds for ~79 % of rows at s = 1000); a
+        // third test inside that group, at chunk kb1 + 1, would end nearly all
+        // of them, but its registers (64 VGPRs) made the kernel 3-4 % slower
+        // than the chunks it saved (profiles/r03_allpairs_ab_*).
         const uint32_t kb1 = 4u * ((s / 2 + 255) / 256);
         auto past = [&](uint64_t bv, const uint64_t (&thr)[R]) {          // wave-uniform
             const uint64_t b0 = ((uint64_t)rfl((uint32_t)(bv >> 32)) << 32) | rfl((uint32_t)bv);
@@ -493,7 +494,6 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
                 if (((actmask >> r) & 1u) && (mrun[r] != 0 || !(b0 > thr[r]))) all_past = false;
             return all_past;
         };
-        bool ended = false;
         for (uint32_t kb = 0; kb < nch; kb += kRing) {
             {
                 const uint64_t b = rg[0];
@@ -508,7 +508,6 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
             for (int u = 0; u < kRing; u++) {
                 const uint32_t k = kb + u;
                 const uint64_t b = rg[u];
-                if (u == 1 && kb == kb1 && past(b, thr2)) { ended = true; break; }   // chunk kb1 + 1
                 // lanes past s in the last chunk read 0 (buffer bounds): masked
                 // out (MASKED), or harmless (see above)
                 const uint64_t lm = MASKED ? (k == nch - 1 ? tailmask : ~0ull) : ~0ull;
@@ -538,7 +537,6 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
                     if (u == 3) rg[u] = ld_chunk_at<(3 + kRing) * 512>(rc, lane_off, gofs);
                 }
             }
-            if (ended) break;
         }
         if (lane == 0) {
             // the column's count is read only here: a scalar load left in flight
@@ -614,10 +612,10 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
         uint32_t nraw[R];
         uint64_t lraw[R], t1raw[R], t2raw[R], fraw[R];
         // union-rank thresholds (ap_columns): A_r[s - j0 - 1] for the two test
-        // chunks, j0 = 64 kb1 and 64 (kb1 + 1); positions below 0 clamp to 0
+        // groups, j0 = 64 kb1 and 64 (kb1 + 4); positions below 0 clamp to 0
         // (never used then: such a group does not exist or the test is moot)
         const uint32_t kb1 = 4u * ((s / 2 + 255) / 256);
-        const uint32_t p1 = s > 64 * kb1 ? s - 64 * kb1 - 1 : 0, p2 = s > 64 * (kb1 + 1) ? s - 64 * (kb1 + 1) - 1 : 0;
+        const uint32_t p1 = s > 64 * kb1 ? s - 64 * kb1 - 1 : 0, p2 = s > 64 * (kb1 + 4) ? s - 64 * (kb1 + 4) - 1 : 0;
 #pragma unroll
         for (int r = 0; r < R; r++) {
             const uint32_t i = min(i0 + (uint32_t)r, row1 - 1);
@@ -641,7 +639,7 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
             // a threshold past the row's last element (partial row) or of a
             // group with j0 >= s never ends the scan (kEmpty: b0 > it is false)
             thr1[r] = (ok && s > 64 * kb1 && p1 < nA[r]) ? t1raw[r] : kEmpty;
-            thr2[r] = (ok && s > 64 * (kb1 + 1) && p2 < nA[r]) ? t2raw[r] : kEmpty;
+            thr2[r] = (ok && s > 64 * (kb1 + 4) && p2 < nA[r]) ? t2raw[r] : kEmpty;
             any_partial_row |= nA[r] < s;
             zero_key |= ok && fraw[r] == 0;                  // the row holds the hash value 0 (MASKED probe)
         }
