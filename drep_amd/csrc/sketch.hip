@@ -275,7 +275,9 @@ __device__ __forceinline__ uint64_t murmur_fin(uint64_t q1, uint64_t q2) {
 }
 
 #ifndef DREPHIP_SK_BATCH
-#define DREPHIP_SK_BATCH 2          // k-mers per admit test: 52 VGPRs (4: 58, 0.8 % slower; 8: 73, 7 waves, 2 % slower)
+#define DREPHIP_SK_BATCH 2          // k-mers per admit test: 52 VGPRs (4: 58, 0.8 % slower; 8: 73, 7 waves, 2 % slower;
+                                    // all 16 of a chunk as one block, keeping only the prefilter bits and recomputing
+                                    // the rare hits: 56 VGPRs, 4 % slower -- profiles/r03_sketch_ab_block16.txt)
 #endif
 #ifndef DREPHIP_SK_MINW
 #define DREPHIP_SK_MINW 1
