@@ -3,13 +3,13 @@
 #   kernel trace + stats of the default bench, HBM traffic PMC passes
 #   (FETCH_SIZE and WRITE_SIZE in separate passes, MI355X_MICROARCH.md HBM),
 #   SQ issue/stall counter passes (<= 8 SQ + 2 GRBM counters per pass) of the
-#   bench (sketch kernel) and of tools/ap_bench.py at N = 6000 and 1000
-#   (all-pairs kernel).  Every profiled command runs the product path only
+#   bench (sketch kernel).  The all-pairs kernel's passes are
+#   tools/profile_allpairs.sh.  Every profiled command runs the product path only
 #   (--check 0 --cpu-baseline 0: no oracle work under the profiler).
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-.}
 export TMPDIR=/tmp
-R=${ROUND:-r02}
+R=${ROUND:-r03}
 OUT=$PWD/gpurun_out/$R
 mkdir -p $OUT
 BARGS="--check 0 --cpu-baseline 0"
@@ -38,21 +38,4 @@ for grp in "${CGROUPS[@]}"; do
 done
 python3 tools/pmc_summary.py k_sketch_hash21 $OUT/sq*/pmc_counter_collection.csv --window-ends $WE --kernel-ms $KMS \
     > $OUT/sketch_pmc_sq.json || exit 1
-for N in 6000 1000; do
-  i=0
-  for grp in "${CGROUPS[@]}"; do
-    i=$((i+1))
-    AP_ITERS=1 AP_SAMPLE=1000 AP_N=$N timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv \
-        -d $OUT/ap${N}_sq$i -o pmc -- python tools/ap_bench.py > $OUT/ap${N}_sq$i.log 2>&1 || exit 1
-  done
-  AP_ITERS=3 AP_N=$N timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ap${N}_trace -o ap \
-      -- python tools/ap_bench.py > $OUT/ap${N}_trace.log 2>&1 || exit 1
-  AKMS=$(python3 -c "
-import csv,glob
-for r in csv.DictReader(open(glob.glob('$OUT/ap${N}_trace/**/*kernel_stats.csv', recursive=True)[0])):
-    if 'k_allpairs_q' in r['Name']: print(float(r['AverageNs'])/1e6)
-") || exit 1
-  python3 tools/pmc_summary.py k_allpairs_q $OUT/ap${N}_sq*/pmc_counter_collection.csv --kernel-ms $AKMS \
-      > $OUT/allpairs_pmc_sq_N$N.json || exit 1
-done
 echo "profiles in $OUT"
