@@ -1015,46 +1015,103 @@ __global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
 // which stay in that XCD's L2 (the mapping is a speed hint only; any
 // placement gives the same result).  Lists are padded with idle items
 // (i0 = kIdleItem).
+//
+// The items of column tile ct are the row tiles i0 = row0, row0 + R, ... up to
+// (ct + 1) C - 2: an arithmetic run.  The host therefore plans only groups --
+// runs of one tile's items, {first i0, c0, offset in its XCD's list, count} --
+// and k_expand_items writes the item array on the device (at N = 10^5 the
+// list holds ~10^7 items: built item by item on the host and copied, it cost
+// ~0.1 s per call shape).
 constexpr uint32_t kXcds = 8;
 constexpr uint32_t kIdleItem = 0xFFFFFFFFu;
 
-static std::vector<uint2> make_items(uint32_t row0, uint32_t row1, uint32_t N, uint32_t R, uint32_t C) {
+using ItemGroup = ApItemGroup;
+struct XcdStarts { uint32_t v[kXcds + 1]; };      // list x = groups [v[x], v[x + 1]), ascending off
+struct ItemPlan {
+    std::vector<ItemGroup> groups;
+    XcdStarts xs{};
+    uint64_t slots = 0;                          // kXcds x the longest list
+};
+
+static ItemPlan plan_items(uint32_t row0, uint32_t row1, uint32_t N, uint32_t R, uint32_t C) {
     const uint32_t nct = (N + C - 1) / C;
-    std::vector<std::vector<uint2>> tiles(nct);
-    size_t total = 0;
-    for (uint32_t i0 = row0; i0 < row1; i0 += R)
-        for (uint32_t ct = (i0 + 1) / C; ct < nct; ct++) { tiles[ct].push_back(make_uint2(i0, ct * C)); total++; }
-    // groups: runs of one column tile's items, at most ~1/16 of an XCD's share,
-    // so that dealing them largest-first balances the XCDs
-    const size_t gmax = std::max<size_t>(1, total / (kXcds * 16));
-    std::vector<std::pair<uint32_t, uint32_t>> groups;              // (tile, first item) -> size via gmax
-    for (uint32_t t = 0; t < nct; t++)
-        for (size_t i = 0; i < tiles[t].size(); i += gmax) groups.push_back({t, (uint32_t)i});
-    auto gsize = [&](const std::pair<uint32_t, uint32_t> &g) {
-        return std::min(gmax, tiles[g.first].size() - g.second);
+    auto count = [&](uint32_t ct) -> uint64_t {   // row tiles i0 in [row0, row1) with (i0 + 1) / C <= ct
+        const uint64_t lim = std::min<uint64_t>(row1 - 1, (uint64_t)(ct + 1) * C - 2);
+        return (uint64_t)row0 + 1 > (uint64_t)(ct + 1) * C - 1 ? 0 : (lim - row0) / R + 1;
     };
-    std::stable_sort(groups.begin(), groups.end(), [&](const auto &a, const auto &b) { return gsize(a) > gsize(b); });
-    std::vector<std::vector<uint2>> lists(kXcds);
-    for (const auto &g : groups) {
-        uint32_t best = 0;
-        for (uint32_t x = 1; x < kXcds; x++) if (lists[x].size() < lists[best].size()) best = x;
-        const auto &tl = tiles[g.first];
-        lists[best].insert(lists[best].end(), tl.begin() + g.second, tl.begin() + g.second + gsize(g));
+    uint64_t total = 0;
+    for (uint32_t ct = 0; ct < nct; ct++) total += count(ct);
+    // groups of at most ~1/16 of an XCD's share, so that dealing them
+    // largest-first balances the XCDs
+    const uint64_t gmax = std::max<uint64_t>(1, total / (kXcds * 16));
+    struct G { uint32_t ct; uint64_t first, size; };
+    std::vector<G> gs;
+    for (uint32_t ct = 0; ct < nct; ct++) {
+        const uint64_t n = count(ct);
+        for (uint64_t i = 0; i < n; i += gmax) gs.push_back({ct, i, std::min(gmax, n - i)});
     }
-    size_t len = 0;
-    for (auto &l : lists) len = std::max(len, l.size());
-    std::vector<uint2> items(len * kXcds, make_uint2(kIdleItem, 0));
-    for (uint32_t x = 0; x < kXcds; x++)
-        for (size_t i = 0; i < lists[x].size(); i++) items[i * kXcds + x] = lists[x][i];
-    return items;
+    std::stable_sort(gs.begin(), gs.end(), [](const G &a, const G &b) { return a.size > b.size; });
+    std::vector<std::vector<ItemGroup>> lists(kXcds);
+    uint64_t len[kXcds] = {};
+    for (const G &g : gs) {
+        uint32_t best = 0;
+        for (uint32_t x = 1; x < kXcds; x++) if (len[x] < len[best]) best = x;
+        lists[best].push_back({(uint32_t)(row0 + g.first * R), g.ct * C, (uint32_t)len[best], (uint32_t)g.size});
+        len[best] += g.size;
+    }
+    ItemPlan p;
+    uint64_t lmax = 0;
+    for (uint32_t x = 0; x < kXcds; x++) {
+        p.xs.v[x] = (uint32_t)p.groups.size();
+        p.groups.insert(p.groups.end(), lists[x].begin(), lists[x].end());
+        lmax = std::max(lmax, len[x]);
+    }
+    p.xs.v[kXcds] = (uint32_t)p.groups.size();
+    p.slots = lmax * kXcds;
+    return p;
 }
 
-// Fixed-width tiles (make_items) as whole-row-table items {i0, c0, c0 + C}
-static std::vector<uint4> make_items_tiles(uint32_t row0, uint32_t row1, uint32_t N, uint32_t R, uint32_t C) {
-    const std::vector<uint2> t = make_items(row0, row1, N, R, C);
-    std::vector<uint4> items(t.size());
-    for (size_t i = 0; i < t.size(); i++) items[i] = make_uint4(t[i].x, t[i].y, t[i].y + C, 0);
-    return items;
+// slot t = the (t / 8)-th item of XCD (t % 8)'s list, or idle past its end;
+// whole-row-table items are {i0, c0, c0 + C, 0}, band items {i0, c0}
+template <bool WIDE>
+__global__ __launch_bounds__(256) void k_expand_items(const ItemGroup *__restrict__ g, XcdStarts xs, uint64_t slots,
+                                                     uint32_t R, uint32_t C, void *__restrict__ out) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= slots) return;
+    const uint32_t x = (uint32_t)(t % kXcds), i = (uint32_t)(t / kXcds);
+    uint32_t lo = xs.v[x], hi = xs.v[x + 1];
+    uint32_t i0 = kIdleItem, c0 = 0;
+    if (lo < hi) {                                   // the last group with off <= i (the first has off 0)
+        while (hi - lo > 1) {
+            const uint32_t m = (lo + hi) / 2;
+            if (g[m].off <= i) lo = m; else hi = m;
+        }
+        const ItemGroup G = g[lo];
+        if (i - G.off < G.size) { i0 = G.i0 + (i - G.off) * R; c0 = G.c0; }
+    }
+    if (WIDE) ((uint4 *)out)[t] = make_uint4(i0, c0, c0 + C, 0);
+    else ((uint2 *)out)[t] = make_uint2(i0, c0);
+}
+
+// Upload a plan's groups (host copy kept in *host until the next plan: the
+// copy is queued) and expand them into the item array *d_items (grow-only
+// scratch `name`).  Returns the item count in *nitems.
+template <bool WIDE>
+static int expand_items(drephip_ctx *ctx, ItemPlan &&plan, std::vector<ItemGroup> &host, const char *name,
+                        uint32_t R, uint32_t C, hipStream_t st, void **d_items, uint64_t *nitems) {
+    int rc;
+    *nitems = plan.slots;
+    host = std::move(plan.groups);
+    if (plan.slots == 0) return DREPHIP_OK;
+    const std::string gname = std::string(name) + "_groups";
+    ItemGroup *d_groups;
+    if ((rc = scratch(ctx, gname.c_str(), host.size() * sizeof(ItemGroup), (void **)&d_groups))) return rc;
+    if ((rc = scratch(ctx, name, plan.slots * (WIDE ? sizeof(uint4) : sizeof(uint2)), d_items))) return rc;
+    HIPC(hipMemcpyAsync(d_groups, host.data(), host.size() * sizeof(ItemGroup), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_expand_items<WIDE>, dim3((uint32_t)((plan.slots + 255) / 256)), dim3(256), 0, st, d_groups,
+                       plan.xs, plan.slots, R, C, *d_items);
+    HIPC(hipGetLastError());
+    return DREPHIP_OK;
 }
 
 static int launch_merge(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N,
@@ -1078,15 +1135,17 @@ static int launch_band(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_
                        uint16_t *d_denom, hipStream_t st) {
     constexpr int R = 4;
     const uint32_t cap = std::min(std::max(ctx->band_cap, 1u), kBandCapMax);
-    const std::vector<uint2> items = make_items(row0, row1, N, R, kBandCols);
-    if (items.empty()) return DREPHIP_OK;
     uint2 *d_items;
+    uint64_t nitems;
     uint32_t *d_nfail;
     int rc;
-    if ((rc = scratch(ctx, "apb_items", items.size() * sizeof(uint2), (void **)&d_items))) return rc;
+    std::vector<ItemGroup> groups;                   // lives until the stream sync below
+    if ((rc = expand_items<false>(ctx, plan_items(row0, row1, N, R, kBandCols), groups, "apb_items", R, kBandCols, st,
+                                  (void **)&d_items, &nitems)))
+        return rc;
+    if (nitems == 0) return DREPHIP_OK;
     if ((rc = scratch(ctx, "ap_nfail_band", 4, (void **)&d_nfail))) return rc;
     HIPC(hipMemsetAsync(d_nfail, 0, 4, st));
-    HIPC(hipMemcpyAsync(d_items, items.data(), items.size() * sizeof(uint2), hipMemcpyHostToDevice, st));
     uint64_t *d_prof = nullptr;                      // DREPHIP_BAND_PROF=1: per-phase wall-clock sums
     const bool prof = getenv("DREPHIP_BAND_PROF") != nullptr;
     if (prof) {
@@ -1096,8 +1155,8 @@ static int launch_band(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_
     const size_t lds = band_lds_bytes(R);         // <= 80 KiB: two workgroups per CU
     HIPC(hipFuncSetAttribute((const void *)k_allpairs_band<R, 1024, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     timing_mark(ctx, 2, st, true);
-    for (size_t i0 = 0; i0 < items.size(); i0 += max_blocks(1024))
-        hipLaunchKernelGGL((k_allpairs_band<R, 1024, 8>), dim3((uint32_t)std::min<size_t>(items.size() - i0, max_blocks(1024))),
+    for (uint64_t i0 = 0; i0 < nitems; i0 += max_blocks(1024))
+        hipLaunchKernelGGL((k_allpairs_band<R, 1024, 8>), dim3((uint32_t)std::min<uint64_t>(nitems - i0, max_blocks(1024))),
                            dim3(1024), lds, st, d_hashes, d_nhash, ctx->s, N, row1, cap, d_items + i0, d_common,
                            d_denom, seg0, d_nfail, d_prof);
     timing_mark(ctx, 2, st, false);
@@ -1109,7 +1168,7 @@ static int launch_band(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_
         uint64_t h[3];
         HIPC(hipMemcpy(h, d_prof, 24, hipMemcpyDeviceToHost));
         fprintf(stderr, "[drephip] band kernel: %llu bands over %zu items; per band: build %.2f us, columns %.2f us (100 MHz wall clock)\n",
-                (unsigned long long)h[2], items.size(), h[2] ? h[0] / 100.0 / h[2] : 0.0, h[2] ? h[1] / 100.0 / h[2] : 0.0);
+                (unsigned long long)h[2], (size_t)nitems, h[2] ? h[0] / 100.0 / h[2] : 0.0, h[2] ? h[1] / 100.0 / h[2] : 0.0);
     }
     if (nfail)   // a band table could not be built with any field pair: exact merge kernel instead
         return launch_merge(ctx, d_hashes, d_nhash, N, seg0, npairs, d_common, d_denom, st);
@@ -1203,21 +1262,22 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
     while (C > kApMinCols && nitems_for(C) < 4ull * kApSlots) C /= 2;
     // the item list depends only on (N, rows, R, C): reused while the shape and
     // the scratch allocation are unchanged (repeated calls: bench steps, shards).
-    // Its host copy lives in the context until the next list replaces it (the
+    // Its group table lives in the context until the next plan replaces it (the
     // queued H2D copy may still be reading it when a deferred call returns).
     const uint64_t key[5] = {N, row0, row1, R, C};
-    const bool reuse = ctx->ap_items_gen == ctx->alloc_gen && !memcmp(ctx->ap_items_key, key, sizeof(key));
-    if (!reuse) {
-        ctx->ap_items_host = make_items_tiles(row0, row1, N, R, C);
+    if (ctx->ap_items_gen == ctx->alloc_gen && !memcmp(ctx->ap_items_key, key, sizeof(key))) {
+        if ((rc = scratch(ctx, "ap_items", ctx->ap_items_n * sizeof(uint4), (void **)&d_items))) return rc;
+    } else {
+        uint64_t n;
         ctx->ap_items_gen = 0;
-    }
-    const uint32_t ni = (uint32_t)ctx->ap_items_host.size();
-    if ((rc = scratch(ctx, "ap_items", (uint64_t)ni * sizeof(uint4), (void **)&d_items))) return rc;
-    if (!reuse) {
-        HIPC(hipMemcpyAsync(d_items, ctx->ap_items_host.data(), (uint64_t)ni * sizeof(uint4), hipMemcpyHostToDevice, st));
+        if ((rc = expand_items<true>(ctx, plan_items(row0, row1, N, R, C), ctx->ap_groups_host, "ap_items", R, C, st,
+                                     (void **)&d_items, &n)))
+            return rc;
+        ctx->ap_items_n = n;
         memcpy(ctx->ap_items_key, key, sizeof(key));
         ctx->ap_items_gen = ctx->alloc_gen;
     }
+    const uint32_t ni = (uint32_t)ctx->ap_items_n;
     // a row whose table cannot be built is merged literally inside the main
     // kernel (k_allpairs_q): no host round trip, nothing to check afterwards
     const size_t lds = (size_t)stride * 4;

@@ -61,6 +61,10 @@ struct LinkStats {            // last drephip_linkage* call, host wall clock (se
     double wall_s = 0;        // the whole call
 };
 
+// A run of all-pairs work items (allpairs.hip, plan_items): `size` row tiles
+// from i0 (step R) against column tile c0, at offset `off` of its XCD's list.
+struct ApItemGroup { uint32_t i0, c0, off, size; };
+
 struct drephip_ctx {
     int device = 0;
     int k = 21;
@@ -93,11 +97,12 @@ struct drephip_ctx {
     uint64_t sk_tab_gen = 0;     // alloc_gen when the Murmur table image was built
     // pinned host staging for the small per-call readbacks (status, failure count)
     std::map<std::string, DevBuf> pinned;
-    // all-pairs work-item list of the last call, reused on the same shape
-    // (host copy kept: a deferred call's H2D copy of it may still be queued)
+    // all-pairs work-item list of the last call, reused on the same shape (its
+    // group table kept on the host: a deferred call's H2D copy may still be queued)
     uint64_t ap_items_key[5] = {0, 0, 0, 0, 0};
     uint64_t ap_items_gen = 0;
-    std::vector<uint4> ap_items_host;
+    uint64_t ap_items_n = 0;
+    std::vector<ApItemGroup> ap_groups_host;
     // deferred sketch (drephip_sketch_device_async): the first round is queued
     // without reading its status back; drephip_sketch_wait checks it (and
     // reruns the call synchronously if a genome needs another threshold round).

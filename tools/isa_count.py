@@ -2,7 +2,7 @@
 product).  Compiles drep_amd/csrc/sketch.hip to gfx950 assembly, finds each
 kernel's unrolled loop blocks (the ones holding the BATCH-wide hash code) and
 reports VALU instructions per window end.  Output feeds bench.py's VALU
-roofline: python tools/isa_count.py > profiles/sketch_isa.json"""
+roofline: python tools/isa_count.py > profiles/r03_sketch_isa.json"""
 import collections
 import json
 import os
