@@ -81,6 +81,10 @@ SIGNATURES = {
                                                 np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS"),
                                                 C.c_int, f64p, vp]),
     "drephip_linkage_reserve": (C.c_int, [vp, C.c_uint32]),
+    "drephip_set_linkage_path": (C.c_int, [vp, C.c_int]),
+    "drephip_linkage_sparse": (C.c_int, [C.c_uint32, C.c_uint64, u32p, u32p, f64p, C.c_int, f64p]),
+    "drephip_last_linkage_info": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_uint64), C.POINTER(C.c_uint32),
+                                            C.POINTER(C.c_uint32)]),
     "drephip_last_linkage_stats": (C.c_int, [vp] + [C.POINTER(C.c_double)] * 5),
     "drephip_set_timing": (C.c_int, [vp, C.c_int]),
     "drephip_last_kernel_ms": (C.c_int, [vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
@@ -199,6 +203,28 @@ def fasta_info(path: str, k: int = 21):
     return {"length": length.value, "padded": padded.value, "n_records": nrec.value, "n_kmers": nk.value}
 
 
+# scipy linkage method codes (include/drephip.h DREPHIP_LINK_*)
+LINK_METHODS = {"single": 0, "complete": 1, "average": 2, "weighted": 6}
+
+
+def linkage_sparse(n: int, i: np.ndarray, j: np.ndarray, v: np.ndarray, method: str) -> np.ndarray:
+    """drephip_linkage_sparse (host only, no GPU): scipy's linkage Z of the n x n
+    distance matrix that holds v[t] at (i[t], j[t]) and 1.0 at every pair not
+    listed (each unordered pair at most once, v in [0, 1))."""
+    i = np.ascontiguousarray(i, dtype=np.uint32)
+    j = np.ascontiguousarray(j, dtype=np.uint32)
+    v = np.ascontiguousarray(v, dtype=np.float64)
+    if not (len(i) == len(j) == len(v)):
+        raise ValueError("i, j and v must have one entry per pair")
+    Z = np.zeros((max(n - 1, 0), 4), dtype=np.float64)
+    if n >= 2:
+        e = np.zeros(1, np.uint32)
+        check(lib().drephip_linkage_sparse(int(n), len(v), i if len(i) else e, j if len(j) else e,
+                                           v if len(v) else np.zeros(1), LINK_METHODS[method], Z.reshape(-1)),
+              "drephip_linkage_sparse")
+    return Z
+
+
 class Context:
     """One libdrephip context: a HIP device plus (k, s, seed)."""
 
@@ -237,8 +263,19 @@ class Context:
     def set_allpairs_path(self, path: int, band_cap: int = 1024) -> None:
         check(lib().drephip_set_allpairs_path(self._h, path, band_cap), "drephip_set_allpairs_path")
 
-    # scipy linkage method codes (include/drephip.h DREPHIP_LINK_*)
-    LINK_METHODS = {"single": 0, "complete": 1, "average": 2, "weighted": 6}
+    LINK_METHODS = LINK_METHODS
+    # linkage path (include/drephip.h DREPHIP_LINK_PATH_*)
+    LINK_AUTO, LINK_DENSE, LINK_SPARSE = 0, 1, 2
+
+    def set_linkage_path(self, path: int) -> None:
+        check(lib().drephip_set_linkage_path(self._h, int(path)), "drephip_set_linkage_path")
+
+    def linkage_info(self):
+        """{sparse, pairs, components, largest} of the last linkage call."""
+        sp, npairs, nc, lg = C.c_int(0), C.c_uint64(0), C.c_uint32(0), C.c_uint32(0)
+        check(lib().drephip_last_linkage_info(self._h, C.byref(sp), C.byref(npairs), C.byref(nc), C.byref(lg)),
+              "drephip_last_linkage_info")
+        return {"sparse": bool(sp.value), "pairs": npairs.value, "components": nc.value, "largest": lg.value}
 
     def linkage(self, y: np.ndarray, method: str) -> np.ndarray:
         """scipy.cluster.hierarchy.linkage(y, method) on the GPU, bit-identical

@@ -169,6 +169,9 @@ DREPHIP_EXPORT int drephip_create(int device, int k, uint32_t s, uint32_t seed, 
     drephip_ctx *c = new (std::nothrow) drephip_ctx();
     if (!c) { set_error("out of host memory"); return DREPHIP_ERR_NOMEM; }
     c->device = device; c->k = k; c->s = s; c->seed = seed;
+    if (const char *lp = std::getenv("DREPHIP_LINK_PATH"))      // default linkage path (tests, A/B runs)
+        c->link_path = !strcmp(lp, "dense") ? DREPHIP_LINK_PATH_DENSE : !strcmp(lp, "sparse") ? DREPHIP_LINK_PATH_SPARSE
+                                                                                                : DREPHIP_LINK_PATH_AUTO;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) { delete c; set_error(hipGetErrorString(e)); return DREPHIP_ERR_HIP; }
     *out = c;
@@ -785,6 +788,65 @@ DREPHIP_EXPORT int drephip_distance_lut(int k, uint32_t denom, double *lut) {
     return DREPHIP_OK;
 }
 
+// Sparse linkage limits: the per-component matrices (sum of m^2 f64 cells) of
+// the automatic choice, and of an explicit drephip_linkage_sparse call.
+constexpr uint64_t kSparseAutoCells = 1ull << 28;     // 2 GB of host memory
+constexpr uint64_t kSparseMaxCells = 1ull << 31;      // 16 GB
+constexpr uint64_t kSparseMaxPairs = 1ull << 26;      // device pair list: 768 MB
+
+static uint64_t sparse_auto_cells() {
+    if (const char *e = std::getenv("DREPHIP_LINK_SPARSE_CELLS")) return std::strtoull(e, nullptr, 10);
+    return kSparseAutoCells;
+}
+
+DREPHIP_EXPORT int drephip_set_linkage_path(drephip_ctx *ctx, int path) {
+    GUARD_CTX(ctx);
+    if (path < DREPHIP_LINK_PATH_AUTO || path > DREPHIP_LINK_PATH_SPARSE) { set_error("bad linkage path"); return DREPHIP_ERR_ARG; }
+    ctx->link_path = path;
+    return DREPHIP_OK;
+}
+
+DREPHIP_EXPORT int drephip_linkage_sparse(uint32_t n, uint64_t npairs, const uint32_t *i, const uint32_t *j,
+                                          const double *v, int method, double *Z) {
+    if (n < 2) return DREPHIP_OK;
+    if (!Z || (npairs && (!i || !j || !v))) { set_error("null argument"); return DREPHIP_ERR_ARG; }
+    return linkage_sparse_impl(n, npairs, i, j, v, method, kSparseMaxCells, Z, nullptr);
+}
+
+// the sparse path from a host condensed vector: the pairs below 1.0 when no
+// value exceeds 1.0; returns 1 when it produced Z, 0 when the dense path must run
+static int linkage_condensed_sparse(drephip_ctx *ctx, const double *y, uint32_t n, int method, double *Z, int *rc) {
+    *rc = DREPHIP_OK;
+    if (ctx->link_path == DREPHIP_LINK_PATH_DENSE) return 0;
+    const double t0 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    std::vector<uint32_t> pi, pj;
+    std::vector<double> pv;
+    uint64_t t = 0;
+    for (uint32_t a = 0; a + 1 < n; a++)
+        for (uint32_t b = a + 1; b < n; b++, t++) {
+            const double d = y[t];
+            if (!(d <= 1.0)) {
+                if (ctx->link_path == DREPHIP_LINK_PATH_SPARSE) { set_error("sparse linkage: a distance above 1.0 or NaN"); *rc = DREPHIP_ERR_ARG; }
+                return 0;
+            }
+            if (d < 1.0) {
+                if (pi.size() >= kSparseMaxPairs && ctx->link_path != DREPHIP_LINK_PATH_SPARSE) return 0;
+                pi.push_back(a); pj.push_back(b); pv.push_back(d);
+            }
+        }
+    const double t1 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    const int r = linkage_sparse_impl(n, pi.size(), pi.data(), pj.data(), pv.data(), method,
+                                      ctx->link_path == DREPHIP_LINK_PATH_SPARSE ? kSparseMaxCells : sparse_auto_cells(),
+                                      Z, &ctx->link.sp);
+    if (r == DREPHIP_ERR_UNSUPPORTED && ctx->link_path != DREPHIP_LINK_PATH_SPARSE) return 0;
+    if (r) { *rc = r; return 0; }
+    ctx->link.sparse = 1;
+    ctx->link.matrix_s = t1 - t0;
+    ctx->link.chain_s = ctx->link.sp.setup_s + ctx->link.sp.chain_s;
+    ctx->link.finish_s = ctx->link.sp.finish_s;
+    return 1;
+}
+
 DREPHIP_EXPORT int drephip_linkage(drephip_ctx *ctx, const double *y, uint32_t n, int method, double *Z) {
     GUARD_CTX(ctx);
     if (n < 2) return DREPHIP_OK;
@@ -793,11 +855,15 @@ DREPHIP_EXPORT int drephip_linkage(drephip_ctx *ctx, const double *y, uint32_t n
     timing_begin(ctx);
     ctx->link = LinkStats{};
     const auto t0 = std::chrono::steady_clock::now();
-    double *d_D;
-    int rc = dist_from_condensed_impl(ctx, y, n, &d_D, ctx->stream);
-    if (rc) return rc;
-    rc = linkage_device_impl(ctx, d_D, n, method, Z, ctx->stream);
-    if (rc) return rc;
+    int rc;
+    if (!linkage_condensed_sparse(ctx, y, n, method, Z, &rc)) {
+        if (rc) return rc;
+        double *d_D;
+        rc = dist_from_condensed_impl(ctx, y, n, &d_D, ctx->stream);
+        if (rc) return rc;
+        rc = linkage_device_impl(ctx, d_D, n, method, Z, ctx->stream);
+        if (rc) return rc;
+    }
     timing_collect(ctx);
     ctx->link.wall_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return DREPHIP_OK;
@@ -830,11 +896,51 @@ DREPHIP_EXPORT int drephip_linkage_counts_device(drephip_ctx *ctx, const uint16_
     timing_begin(ctx);
     ctx->link = LinkStats{};
     const auto t0 = std::chrono::steady_clock::now();
-    double *d_D;
-    rc = dist_matrix_impl(ctx, d_common, d_denom, n, perm, lut, lut_len, lut_off, &d_D, ctx->stream);
-    if (rc) return rc;
-    rc = linkage_device_impl(ctx, d_D, n, method, Z, ctx->stream);
-    if (rc) return rc;
+    bool done = false;
+    if (ctx->link_path != DREPHIP_LINK_PATH_DENSE) {
+        // sparse path: the pairs below 1.0 (nonzero counts) extracted on the GPU,
+        // scipy's algorithm replayed on them on the host (linkage_sparse.cpp)
+        const bool forced = ctx->link_path == DREPHIP_LINK_PATH_SPARSE;
+        const uint64_t cap = std::min<uint64_t>((uint64_t)n * (n - 1) / 2, kSparseMaxPairs);
+        uint32_t *ij = nullptr, *lidx = nullptr, flags = 0;
+        uint64_t np = 0;
+        rc = sparse_pairs_impl(ctx, d_common, d_denom, n, perm, lut, lut_len, lut_off, cap, &ij, &lidx, &np, &flags,
+                               ctx->stream);
+        if (rc) return rc;
+        ctx->link.sp.pairs = np;
+        if (flags & 1) {
+            set_error("a pair's denominator has no distance table (lut_off < 0) or its count exceeds it");
+            return DREPHIP_ERR_ARG;
+        }
+        const double t1 = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (!(flags & 2) && np <= cap) {
+            std::vector<uint32_t> pi(np), pj(np);
+            std::vector<double> pv(np);
+            for (uint64_t t = 0; t < np; t++) { pi[t] = ij[2 * t]; pj[t] = ij[2 * t + 1]; pv[t] = lut[lidx[t]]; }
+            rc = linkage_sparse_impl(n, np, pi.data(), pj.data(), pv.data(), method,
+                                     forced ? kSparseMaxCells : sparse_auto_cells(), Z, &ctx->link.sp);
+            if (rc == DREPHIP_OK) {
+                done = true;
+                ctx->link.sparse = 1;
+                ctx->link.matrix_s = t1;
+                ctx->link.chain_s = ctx->link.sp.setup_s + ctx->link.sp.chain_s;
+                ctx->link.finish_s = ctx->link.sp.finish_s;
+            } else if (rc != DREPHIP_ERR_UNSUPPORTED || forced) {
+                return rc;
+            }
+        } else if (forced) {
+            set_error(flags & 2 ? "sparse linkage: the distance table holds a value above 1.0 (or 0 shared hashes is not 1.0)"
+                                : "sparse linkage: more pairs below 1.0 than the pair list holds");
+            return DREPHIP_ERR_UNSUPPORTED;
+        }
+    }
+    if (!done) {
+        double *d_D;
+        rc = dist_matrix_impl(ctx, d_common, d_denom, n, perm, lut, lut_len, lut_off, &d_D, ctx->stream);
+        if (rc) return rc;
+        rc = linkage_device_impl(ctx, d_D, n, method, Z, ctx->stream);
+        if (rc) return rc;
+    }
     timing_collect(ctx);
     ctx->link.wall_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return DREPHIP_OK;
@@ -846,6 +952,17 @@ DREPHIP_EXPORT int drephip_linkage_reserve(drephip_ctx *ctx, uint32_t n) {
     if (n < 2) return DREPHIP_OK;
     void *p;
     return scratch(ctx, "lk_D", (uint64_t)n * n * 8, &p);
+}
+
+DREPHIP_EXPORT int drephip_last_linkage_info(drephip_ctx *ctx, int *sparse, uint64_t *pairs, uint32_t *components,
+                                             uint32_t *largest) {
+    if (!ctx) { set_error("null context"); return DREPHIP_ERR_ARG; }
+    if (!sparse || !pairs || !components || !largest) { set_error("null argument"); return DREPHIP_ERR_ARG; }
+    *sparse = ctx->link.sparse;
+    *pairs = ctx->link.sp.pairs;
+    *components = ctx->link.sp.components;
+    *largest = ctx->link.sp.largest;
+    return DREPHIP_OK;
 }
 
 DREPHIP_EXPORT int drephip_last_linkage_stats(drephip_ctx *ctx, double *alloc_s, double *matrix_s, double *chain_s,

@@ -53,12 +53,25 @@ struct IngestStats {          // last drephip_sketch_files call
     uint32_t overflow = 0;    // genomes repacked because their span outgrew the file-size estimate
 };
 
+struct SparseLinkInfo {       // the sparse linkage path (linkage_sparse.cpp)
+    uint64_t pairs = 0;       // listed pairs (distance below 1.0)
+    uint32_t components = 0;  // connected components with >= 2 members (0 for single linkage)
+    uint32_t largest = 0;     // members of the largest one
+    uint64_t cells = 0;       // per-component matrix cells (sum of m^2)
+    double setup_s = 0;       // components + matrices
+    double chain_s = 0;       // nn-chain / Prim steps
+    double finish_s = 0;      // stable sort + relabel
+};
+
 struct LinkStats {            // last drephip_linkage* call, host wall clock (seconds)
     double alloc_s = 0;       // device scratch for the n x n matrix (hipMalloc; 0 when reused)
-    double matrix_s = 0;      // matrix build from the counts / condensed input (incl. its H2D copies)
-    double chain_s = 0;       // nn-chain / MST steps (graph replays)
+    double matrix_s = 0;      // matrix build from the counts / condensed input (incl. its H2D copies);
+                              // sparse path: the pair extraction (kernel + readback)
+    double chain_s = 0;       // nn-chain / MST steps (graph replays; sparse path: host setup + steps)
     double finish_s = 0;      // Z readback + stable sort + relabel on the host
     double wall_s = 0;        // the whole call
+    int sparse = 0;           // 1: the sparse path produced Z
+    SparseLinkInfo sp;        // its figures (pairs also when the dense path was chosen)
 };
 
 // A run of all-pairs work items (allpairs.hip, plan_items): `size` row tiles
@@ -73,6 +86,7 @@ struct drephip_ctx {
     hipStream_t stream = nullptr;
     uint32_t timing = 0;      // bitmask of timed kernels (bit w = `which` w of drephip_last_kernel_ms)
     int ap_path = 0;          // DREPHIP_AP_*: 0 auto (table for s <= 2048, else band)
+    int link_path = 0;        // DREPHIP_LINK_PATH_*: 0 auto (sparse when it applies, else dense)
     uint32_t band_cap = 1024; // elements per row per band of the banded all-pairs kernel (clamped to its LDS budget)
     // named grow-only device scratch buffers
     std::map<std::string, DevBuf> bufs;
@@ -172,6 +186,19 @@ int dist_matrix_impl(drephip_ctx *ctx, const uint16_t *d_common, const uint16_t 
                      const uint32_t *perm, const double *lut, uint32_t lut_len, const int32_t *lut_off,
                      double **d_D_out, hipStream_t st);
 int dist_from_condensed_impl(drephip_ctx *ctx, const double *y, uint32_t n, double **d_D_out, hipStream_t st);
+// pairs below 1.0 of the device counts (rows/columns through perm), as (perm i, perm j, lut index) in
+// pinned context buffers (*h_ij, *h_lidx; valid until the next call);
+// *np = their count (> cap: not written); *flags bit 0: a pair's denominator has no table or its count
+// exceeds it, bit 1: the table holds a value above 1.0 or NaN (no sparse form).  Blocking.
+int sparse_pairs_impl(drephip_ctx *ctx, const uint16_t *d_common, const uint16_t *d_denom, uint32_t n,
+                      const uint32_t *perm, const double *lut, uint32_t lut_len, const int32_t *lut_off,
+                      uint64_t cap, uint32_t **h_ij, uint32_t **h_lidx, uint64_t *np, uint32_t *flags,
+                      hipStream_t st);
+// Host (linkage_sparse.cpp): scipy's linkage from the pairs below 1.0 (every other pair at 1.0).
+// DREPHIP_ERR_UNSUPPORTED when the per-component matrices would exceed max_cells.
+int linkage_sparse_impl(uint32_t n, uint64_t np, const uint32_t *pi, const uint32_t *pj, const double *pv,
+                        int method, uint64_t max_cells, double *Z_out, SparseLinkInfo *info);
+void sort_and_label(std::vector<double> &Z, uint32_t n);
 
 // Host ingest (ingest.cpp).
 // std::allocator that leaves new elements uninitialised (resize() without the

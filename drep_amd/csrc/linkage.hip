@@ -419,38 +419,7 @@ static void launch_dist_tiles_condensed(const DmFromCondensed &v, uint32_t n, do
 }
 
 // ------------------------------------------------------------- host driver
-// scipy: Z sorted by distance (np.argsort kind='mergesort': stable), then
-// `label` (union-find over 2n-1 nodes; the smaller root first; sizes).
-static void sort_and_label(std::vector<double> &Z, uint32_t n) {
-    const uint32_t m = n - 1;
-    std::vector<uint32_t> order(m);
-    std::iota(order.begin(), order.end(), 0u);
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return Z[4 * a + 2] < Z[4 * b + 2]; });
-    std::vector<double> S(4ull * m);
-    for (uint32_t r = 0; r < m; r++)
-        for (int c = 0; c < 4; c++) S[4ull * r + c] = Z[4ull * order[r] + c];
-    std::vector<int64_t> parent(2ull * n - 1);
-    std::iota(parent.begin(), parent.end(), 0);
-    std::vector<int64_t> sz(2ull * n - 1, 1);
-    auto find = [&](int64_t x) {
-        int64_t p = x;
-        while (parent[p] != p) p = parent[p];
-        while (parent[x] != p) { const int64_t nx = parent[x]; parent[x] = p; x = nx; }
-        return p;
-    };
-    int64_t next = n;
-    for (uint32_t r = 0; r < m; r++) {
-        const int64_t xr = find((int64_t)S[4ull * r]), yr = find((int64_t)S[4ull * r + 1]);
-        S[4ull * r] = (double)std::min(xr, yr);
-        S[4ull * r + 1] = (double)std::max(xr, yr);
-        parent[xr] = next; parent[yr] = next;
-        sz[next] = sz[xr] + sz[yr];
-        S[4ull * r + 3] = (double)sz[next];
-        next++;
-    }
-    Z.swap(S);
-}
-
+// (sort_and_label: linkage_sparse.cpp, shared with the sparse path)
 int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, double *Z_out, hipStream_t st) {
     if (n < 2) return DREPHIP_OK;
     const double t_chain = now_s();           // chain_s: scratch, graph capture and the steps
@@ -605,6 +574,158 @@ int dist_from_condensed_impl(drephip_ctx *ctx, const double *y, uint32_t n, doub
     HIPC(hipStreamSynchronize(st));
     ctx->link.matrix_s = now_s() - t1;
     *d_D_out = d_D;
+    return DREPHIP_OK;
+}
+
+
+// ------------------------------------------------------- sparse pair list
+// The pairs below 1.0 of the all-pairs counts, for the sparse linkage path
+// (linkage_sparse.cpp): a pair with no shared hash is exactly 1.0, so only a
+// nonzero count can be below it.  The condensed counts are streamed 8 per
+// lane (16-byte loads, plus the denominators when some sketch is partial);
+// a wave's finds are packed with one atomic per wave.  Output: (perm i,
+// perm j) and the table index off[denom] + common, unordered.  HBM-bound: 2 B
+// per pair (4 with denominators) -- 10 GB at n = 10^5.
+constexpr int kSpWG = 256;
+__device__ __forceinline__ void cond_ij(uint64_t t, uint32_t n, uint32_t &i, uint32_t &j) {
+    const double Mf = 2.0 * n - 1.0;
+    int64_t r = (int64_t)((Mf - sqrt(fmax(Mf * Mf - 8.0 * (double)t, 0.0))) * 0.5);
+    if (r < 0) r = 0;
+    if (r > (int64_t)n - 2) r = (int64_t)n - 2;
+    auto S = [&](int64_t a) { return (uint64_t)(a * (int64_t)n - a * (a + 1) / 2); };
+    while (r > 0 && S(r) > t) r--;
+    while (r + 1 <= (int64_t)n - 2 && S(r + 1) <= t) r++;
+    i = (uint32_t)r;
+    j = (uint32_t)(t - S(r) + r + 1);
+}
+
+__global__ __launch_bounds__(kSpWG) void k_sparse_pairs(const uint16_t *__restrict__ common,
+                                                         const uint16_t *__restrict__ denom, uint64_t np,
+                                                         uint32_t n, uint32_t s, const double *__restrict__ lut,
+                                                         const int32_t *__restrict__ off,
+                                                         const uint32_t *__restrict__ perm, uint64_t cap,
+                                                         uint32_t *__restrict__ out_ij, uint32_t *__restrict__ out_l,
+                                                         unsigned long long *__restrict__ count,
+                                                         uint32_t *__restrict__ flags) {
+    const uint64_t nchunk = (np + 7) / 8;
+    const uint64_t stride = (uint64_t)gridDim.x * kSpWG;
+    const int32_t off_s = off[s];
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t bad = 0;
+    for (uint64_t c0 = (uint64_t)blockIdx.x * kSpWG; c0 < nchunk; c0 += stride) {   // wave-uniform trip count
+        const uint64_t c = c0 + threadIdx.x;
+        const uint64_t t0 = c * 8;
+        uint16_t cm[8], dn[8];
+        const bool full = t0 + 8 <= np;
+        if (full) {
+            const uint4 w = *(const uint4 *)(common + t0);
+            const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int e = 0; e < 8; e++) cm[e] = (uint16_t)(ww[e >> 1] >> (16 * (e & 1)));
+            if (denom) {
+                const uint4 d = *(const uint4 *)(denom + t0);
+                const uint32_t dd[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+                for (int e = 0; e < 8; e++) dn[e] = (uint16_t)(dd[e >> 1] >> (16 * (e & 1)));
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                cm[e] = t0 + e < np ? common[t0 + e] : 0;
+                dn[e] = denom && t0 + e < np ? denom[t0 + e] : (uint16_t)s;
+            }
+        }
+        uint32_t hit = 0, lidx[8];
+        if (c < nchunk) {
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                const uint32_t d = denom ? dn[e] : s;
+                if (denom || cm[e]) {
+                    const int32_t o = !denom ? off_s : d <= s ? off[d] : -1;
+                    if (o < 0 || cm[e] > d) { bad = 1; continue; }
+                    lidx[e] = (uint32_t)o + cm[e];
+                    if (cm[e] && lut[lidx[e]] < 1.0) hit |= 1u << e;
+                }
+            }
+        }
+        // pack the wave's finds: one atomic per wave
+        const uint32_t h = __builtin_popcount(hit);
+        if (__ballot(h != 0)) {
+            uint32_t inc = h;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(inc, d, 64);
+                if (lane >= (uint32_t)d) inc += y;
+            }
+            unsigned long long base = 0;
+            if (lane == 63) base = atomicAdd(count, (unsigned long long)inc);
+            base = __shfl(base, 63, 64);
+            uint64_t slot = base + inc - h;
+            for (int e = 0; e < 8; e++) {
+                if (!(hit >> e & 1)) continue;
+                if (slot < cap) {
+                    uint32_t i, j;
+                    cond_ij(t0 + e, n, i, j);
+                    out_ij[2 * slot] = perm[i];
+                    out_ij[2 * slot + 1] = perm[j];
+                    out_l[slot] = lidx[e];
+                }
+                slot++;
+            }
+        }
+    }
+    if (bad) atomicOr(flags, 1u);
+}
+
+int sparse_pairs_impl(drephip_ctx *ctx, const uint16_t *d_common, const uint16_t *d_denom, uint32_t n,
+                      const uint32_t *perm, const double *lut, uint32_t lut_len, const int32_t *lut_off,
+                      uint64_t cap, uint32_t **h_ij, uint32_t **h_lidx, uint64_t *np_out, uint32_t *flags_out,
+                      hipStream_t st) {
+    const uint32_t s = ctx->s;
+    *np_out = 0;
+    *flags_out = 0;
+    // no sparse form unless a count of 0 means exactly 1.0 and nothing exceeds it
+    for (uint32_t k = 0; k < lut_len; k++)
+        if (!(lut[k] <= 1.0)) { *flags_out = 2; return DREPHIP_OK; }
+    for (uint32_t d = 0; d <= s; d++)
+        if (lut_off[d] >= 0 && lut[lut_off[d]] != 1.0) { *flags_out = 2; return DREPHIP_OK; }
+    const uint64_t np = (uint64_t)n * (n - 1) / 2;
+    double *d_lut;
+    int32_t *d_off;
+    uint32_t *d_perm, *d_ij, *d_l, *d_flags;
+    unsigned long long *d_cnt;
+    struct Head { unsigned long long cnt; uint32_t flags, pad; } *h_head;
+    int rc;
+    if ((rc = scratch(ctx, "lk_lut", lut_len * 8ull, (void **)&d_lut))) return rc;
+    if ((rc = scratch(ctx, "lk_off", (s + 1) * 4ull, (void **)&d_off))) return rc;
+    if ((rc = scratch(ctx, "lk_perm", n * 4ull, (void **)&d_perm))) return rc;
+    if ((rc = scratch(ctx, "lk_sp_head", 16, (void **)&d_cnt))) return rc;
+    d_flags = (uint32_t *)(d_cnt + 1);
+    if ((rc = scratch(ctx, "lk_sp_ij", std::max<uint64_t>(cap, 1) * 8, (void **)&d_ij))) return rc;
+    if ((rc = scratch(ctx, "lk_sp_l", std::max<uint64_t>(cap, 1) * 4, (void **)&d_l))) return rc;
+    if ((rc = pinned_host(ctx, "lk_sp_head", sizeof(Head), (void **)&h_head))) return rc;
+    HIPC(hipMemcpyAsync(d_lut, lut, lut_len * 8ull, hipMemcpyHostToDevice, st));
+    HIPC(hipMemcpyAsync(d_off, lut_off, (s + 1) * 4ull, hipMemcpyHostToDevice, st));
+    HIPC(hipMemcpyAsync(d_perm, perm, n * 4ull, hipMemcpyHostToDevice, st));
+    HIPC(hipMemsetAsync(d_cnt, 0, 16, st));
+    const uint64_t nchunk = (np + 7) / 8;
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, (nchunk + kSpWG - 1) / kSpWG));
+    timing_mark(ctx, 3, st, true);
+    hipLaunchKernelGGL(k_sparse_pairs, dim3(grid), dim3(kSpWG), 0, st, d_common, d_denom, np, n, s, d_lut, d_off,
+                       d_perm, cap, d_ij, d_l, d_cnt, d_flags);
+    timing_mark(ctx, 3, st, false);
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(h_head, d_cnt, sizeof(Head), hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    *np_out = h_head->cnt;
+    *flags_out = h_head->flags;
+    if (h_head->flags || h_head->cnt > cap || h_head->cnt == 0) return DREPHIP_OK;
+    // pinned, grow-only: 60 MB at n = 10^5 (configs[3]), kept for the next call
+    if ((rc = pinned_host(ctx, "lk_sp_ij", h_head->cnt * 8, (void **)h_ij))) return rc;
+    if ((rc = pinned_host(ctx, "lk_sp_l", h_head->cnt * 4, (void **)h_lidx))) return rc;
+    HIPC(hipMemcpyAsync(*h_ij, d_ij, h_head->cnt * 8, hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(*h_lidx, d_l, h_head->cnt * 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
     return DREPHIP_OK;
 }
 

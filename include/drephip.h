@@ -259,6 +259,20 @@ int drephip_set_allpairs_path(drephip_ctx *ctx, int path, uint32_t band_cap);
 #define DREPHIP_LINK_COMPLETE 1
 #define DREPHIP_LINK_AVERAGE 2
 #define DREPHIP_LINK_WEIGHTED 6
+/* Two paths, chosen per call (drephip_set_linkage_path):
+ *  - sparse: when no distance exceeds 1.0 -- Mash's distance of two genomes
+ *    sharing no hash is exactly 1.0, the top of its range -- scipy's algorithm
+ *    is replayed on the host over the pairs below 1.0 only (one small dense
+ *    matrix per connected component of those pairs; the counts path extracts
+ *    them on the GPU).  Bit-identical to scipy.  Used automatically when the
+ *    per-component matrices fit 2^28 f64 cells (DREPHIP_LINK_SPARSE_CELLS);
+ *  - dense: the n x n f64 matrix in HBM, one GPU launch per chain step. */
+#define DREPHIP_LINK_PATH_AUTO 0
+#define DREPHIP_LINK_PATH_DENSE 1
+#define DREPHIP_LINK_PATH_SPARSE 2   /* fails (DREPHIP_ERR_UNSUPPORTED) where it does not apply */
+/* (a new context starts at DREPHIP_LINK_PATH_AUTO, or at the path named by the
+ * environment variable DREPHIP_LINK_PATH = auto | dense | sparse) */
+int drephip_set_linkage_path(drephip_ctx *ctx, int path);
 /* From a host condensed distance vector y (n(n-1)/2 doubles, scipy order). */
 int drephip_linkage(drephip_ctx *ctx, const double *y, uint32_t n, int method, double *Z /* (n-1)*4 */);
 /* From the device-resident all-pairs output of drephip_allpairs_device (rows
@@ -272,6 +286,20 @@ int drephip_linkage(drephip_ctx *ctx, const double *y, uint32_t n, int method, d
 int drephip_linkage_counts_device(drephip_ctx *ctx, const uint16_t *d_common, const uint16_t *d_denom,
                                   uint32_t n, const uint32_t *perm, const double *lut, uint32_t lut_len,
                                   const int32_t *lut_off, int method, double *Z /* (n-1)*4 */, void *stream);
+
+/* The sparse path on its own, no context or GPU: the npairs pairs (i[t], j[t])
+ * with distance v[t] in [0, 1), each unordered pair at most once; every pair
+ * not listed is at 1.0.  Z as scipy.cluster.hierarchy.linkage(squareform(D),
+ * method) of that matrix.  DREPHIP_ERR_UNSUPPORTED when the per-component
+ * matrices exceed 2^31 cells. */
+int drephip_linkage_sparse(uint32_t n, uint64_t npairs, const uint32_t *i, const uint32_t *j, const double *v,
+                           int method, double *Z /* (n-1)*4 */);
+
+/* Which path the last drephip_linkage* call on this context took (sparse = 1)
+ * and its pair list: pairs below 1.0, components with >= 2 members and the
+ * largest one's size (0 for single linkage). */
+int drephip_last_linkage_info(drephip_ctx *ctx, int *sparse, uint64_t *pairs, uint32_t *components,
+                              uint32_t *largest);
 
 /* Allocates (grow-only, kept in the context) the n x n f64 device matrix the
  * next linkage call of size <= n uses, so that a caller can pay the

@@ -803,14 +803,15 @@ def test_sketch_layout_cache_follows_layout_changes(ctx1000):
 @pytest.mark.parametrize("method", ["single", "complete", "average", "weighted"])
 @pytest.mark.parametrize("n,kind", [(2, "ties"), (3, "ties"), (17, "ties"), (257, "ties"), (300, "cont"),
                                     (64, "equal"), (400, "fewvals"), (1500, "mash"), (4500, "mash"),
-                                    (2100, "ties")])
+                                    (2100, "ties"), (700, "above1")])
 def test_gpu_linkage_matches_scipy(method, n, kind):
     """drephip_linkage == scipy.cluster.hierarchy.linkage bit for bit, with
     Mash-like ties (a few distinct distances, many 1.0), continuous values,
     all-equal distances, a few values whose Lance-Williams averages round
-    (fewvals), and family structure with 1.0 between families (mash), at three
-    grid densities of the chain-step kernel (16 entries per lane: several
-    passes)."""
+    (fewvals), family structure with 1.0 between families (mash) and values
+    above 1.0 (no sparse form): the dense GPU path at three grid densities of
+    the chain-step kernel (16 entries per lane: several passes), and the
+    automatic choice (the sparse path wherever no value exceeds 1.0)."""
     import scipy.cluster.hierarchy as sch
     rng = np.random.default_rng(n * 31 + len(method))
     m = n * (n - 1) // 2
@@ -827,6 +828,8 @@ def test_gpu_linkage_matches_scipy(method, n, kind):
         same = fam[iu[0]] == fam[iu[1]]
         y = np.ones(m)
         y[same] = np.round(rng.random(int(same.sum())) * 0.2, 3)
+    elif kind == "above1":
+        y = rng.random(m) * 1.5
     else:
         y = np.full(m, 0.5)
     Zs = sch.linkage(y, method=method)
@@ -834,19 +837,33 @@ def test_gpu_linkage_matches_scipy(method, n, kind):
         os.environ["DREPHIP_LINK_PER_LANE"] = per_lane
         try:
             with _lib.Context(0, 21, S, 42) as ctx:
+                ctx.set_linkage_path(ctx.LINK_DENSE)
                 Z = ctx.linkage(y, method)
+                assert not ctx.linkage_info()["sparse"]
         finally:
             os.environ.pop("DREPHIP_LINK_PER_LANE", None)
         assert Z.shape == Zs.shape
         assert np.array_equal(Z, Zs), (per_lane, np.argwhere(Z != Zs)[:5])
+    with _lib.Context(0, 21, S, 42) as ctx:
+        Z = ctx.linkage(y, method)
+        assert ctx.linkage_info()["sparse"] == (kind != "above1")
+        assert np.array_equal(Z, Zs), ("auto", np.argwhere(Z != Zs)[:5])
+        if kind == "above1":
+            ctx.set_linkage_path(ctx.LINK_SPARSE)
+            with pytest.raises(_lib.DrepHipError, match="above 1.0"):
+                ctx.linkage(y, method)
 
 
-@pytest.mark.parametrize("method", ["average", "single"])
-def test_cluster_mash_condensed_gpu_equals_reference_path(family, ctx1000, method):
-    """Primary clustering from device-resident all-pairs counts (GPU linkage)
-    gives the reference path's linkage matrix and Cdb (scipy on the float32
-    Mdb distances), with names in a shuffled order."""
+@pytest.mark.parametrize("path", ["auto", "dense", "sparse"])
+@pytest.mark.parametrize("method", ["average", "single", "complete", "weighted"])
+def test_cluster_mash_condensed_gpu_equals_reference_path(family, ctx1000, method, path, monkeypatch):
+    """Primary clustering from device-resident all-pairs counts (GPU linkage:
+    the pairs below 1.0 extracted on the device and replayed on the host --
+    the automatic choice here -- or the dense n x n chain) gives the reference
+    path's linkage matrix and Cdb (scipy on the float32 Mdb distances), with
+    names in a shuffled order."""
     from drep_amd.d_cluster import CondensedMash, cluster_mash_condensed
+    monkeypatch.setenv("DREPHIP_LINK_PATH", path)
     h, nh = family
     N = len(nh)
     c, d = ctx1000.allpairs(h, nh)
@@ -858,6 +875,55 @@ def test_cluster_mash_condensed_gpu_equals_reference_path(family, ctx1000, metho
     assert np.array_equal(z_gpu, z_cpu)
     assert cdb_gpu.equals(cdb_cpu)
     assert cdb_gpu['primary_cluster'].nunique() > 1
+
+
+@pytest.mark.parametrize("partial", [False, True])
+def test_linkage_counts_device_sparse_vs_dense(ctx1000, partial):
+    """The two linkage paths on device counts agree bit for bit with each other
+    and with scipy: families of 1-60 genomes (pairs below 1.0 only inside a
+    family), count ties, shuffled rows (perm), partial sketches (a denominator
+    per pair), and the pair list reported by drephip_last_linkage_info."""
+    import torch
+    import scipy.cluster.hierarchy as sch
+    from drep_amd.d_cluster import linkage_tables, _linkage_values
+    rng = np.random.default_rng(11 + partial)
+    n = 1500
+    fam = np.repeat(np.arange(200), rng.integers(1, 60, 200))[:n]
+    rng.shuffle(fam)
+    iu = np.triu_indices(n, 1)
+    same = fam[iu[0]] == fam[iu[1]]
+    common = np.zeros(len(same), np.uint16)
+    common[same] = rng.integers(1, 40, int(same.sum())) * 20          # many equal counts
+    denom = np.full(len(same), S, np.uint16)
+    if partial:
+        denom = rng.choice(np.array([600, 800, S], np.uint16), len(same))
+        common = np.minimum(common, denom)
+    perm = rng.permutation(n).astype(np.uint32)
+    lut, off = linkage_tables(np.unique(denom), S)
+    st = torch.cuda.current_stream().cuda_stream
+    d_c = torch.from_numpy(common.view(np.int16)).cuda()
+    d_d = torch.from_numpy(denom.view(np.int16)).cuda() if partial else None
+    # scipy on the same matrix, rows in perm order
+    D = np.zeros((n, n))
+    v = _linkage_values(common, denom)
+    D[perm[iu[0]], perm[iu[1]]] = v
+    D = D + D.T
+    from scipy.spatial.distance import squareform
+    y = squareform(D, checks=False)
+    for method in ("average", "single", "complete"):
+        Zs = sch.linkage(y, method=method)
+        got = {}
+        for path in (ctx1000.LINK_SPARSE, ctx1000.LINK_DENSE):
+            ctx1000.set_linkage_path(path)
+            got[path] = ctx1000.linkage_counts_device(d_c.data_ptr(), None if d_d is None else d_d.data_ptr(), n,
+                                                      perm, lut, off, method, st)
+            info = ctx1000.linkage_info()
+            assert info["sparse"] == (path == ctx1000.LINK_SPARSE)
+            if info["sparse"]:
+                assert info["pairs"] == int((common > 0).sum())
+        ctx1000.set_linkage_path(ctx1000.LINK_AUTO)
+        assert np.array_equal(got[ctx1000.LINK_SPARSE], Zs), method
+        assert np.array_equal(got[ctx1000.LINK_DENSE], Zs), method
 
 
 def test_sketch_device_async_wait(ctx1000):

@@ -484,3 +484,71 @@ def test_write_mash_table_vs_line_by_line(tmp_path):
                                       np.array([float(length[q])]), S)[0]
             lines.append("%s\t%s\t%g\t%g\t%d/%d\n" % (names[r], names[q], lut[Cm[q, r]], p, Cm[q, r], Dm[q, r]))
     assert out.read_text() == "".join(lines)
+
+
+# ------------------------------------------------- sparse linkage (host only)
+def _sparse_instance(rng, n, kind):
+    """n x n distances in [0, 1] with 1.0 between 'families' (Mash's distance of
+    genomes with no shared hash): few distinct values (ties), continuous
+    values, values a hair below 1.0 (weighted averages round to 1.0), or no
+    pair at 1.0 at all (one component)."""
+    fam = rng.integers(0, max(1, n // int(rng.integers(2, 12))), n)
+    iu = np.triu_indices(n, 1)
+    m = len(iu[0])
+    if kind == "ties":
+        v = rng.integers(1, 5, m) / 8.0
+    elif kind == "cont":
+        v = rng.random(m) * 0.9
+    elif kind == "near1":
+        v = 1.0 - rng.integers(1, 4, m) * 2.0 ** -52
+    else:                                   # "dense": every pair below 1.0
+        v = rng.integers(1, 50, m) / 64.0
+    keep = (fam[iu[0]] == fam[iu[1]]) & (rng.random(m) < rng.random()) if kind != "dense" else np.ones(m, bool)
+    y = np.ones(m)
+    y[keep] = v[keep]
+    return y, iu
+
+
+@pytest.mark.parametrize("kind", ["ties", "cont", "near1", "dense"])
+def test_linkage_sparse_matches_scipy(kind):
+    """drephip_linkage_sparse (scipy's nn_chain / Prim replayed on the pairs
+    below 1.0, every other pair at 1.0) == scipy.cluster.hierarchy.linkage of
+    the dense matrix, bit for bit, for every method it serves -- including
+    ties, clusters that lose every edge below 1.0 (complete linkage; weighted
+    averages rounding up to 1.0) and a set with no pair at 1.0."""
+    import scipy.cluster.hierarchy as sch
+    rng = np.random.default_rng(len(kind))
+    for trial in range(60):
+        n = int(rng.integers(2, 120))
+        y, iu = _sparse_instance(rng, n, kind)
+        sel = y < 1.0
+        perm = rng.permutation(int(sel.sum()))           # the list order does not matter
+        pi, pj, pv = iu[0][sel][perm], iu[1][sel][perm], y[sel][perm]
+        if trial % 2:
+            pi, pj = pj, pi                               # nor which end comes first
+        for method in ("single", "complete", "average", "weighted"):
+            Zs = sch.linkage(y, method=method)
+            Z = _lib.linkage_sparse(n, pi, pj, pv, method)
+            assert np.array_equal(Z, Zs), (kind, trial, n, method, np.argwhere(Z != Zs)[:4])
+
+
+def test_linkage_sparse_rejects_bad_lists():
+    """A pair listed twice, a value at or above 1.0 (not a sparse entry), an
+    index out of range or i == j is refused, not silently clustered."""
+    with pytest.raises(_lib.DrepHipError, match="twice"):
+        _lib.linkage_sparse(4, [0, 1], [1, 0], [0.5, 0.5], "average")
+    with pytest.raises(_lib.DrepHipError, match="twice"):
+        _lib.linkage_sparse(4, [0, 0], [1, 1], [0.5, 0.25], "single")
+    with pytest.raises(_lib.DrepHipError, match=r"\[0, 1\)"):
+        _lib.linkage_sparse(4, [0], [1], [1.0], "average")
+    with pytest.raises(_lib.DrepHipError, match=r"\[0, 1\)"):
+        _lib.linkage_sparse(4, [0], [1], [np.nan], "complete")
+    with pytest.raises(_lib.DrepHipError, match="range"):
+        _lib.linkage_sparse(4, [0], [4], [0.5], "average")
+    with pytest.raises(_lib.DrepHipError, match="range"):
+        _lib.linkage_sparse(4, [2], [2], [0.5], "average")
+    with pytest.raises(KeyError):
+        _lib.linkage_sparse(4, [0], [1], [0.5], "ward")
+    assert _lib.linkage_sparse(1, [], [], [], "average").shape == (0, 4)
+    Z = _lib.linkage_sparse(3, [], [], [], "average")          # no pair below 1.0
+    assert Z.tolist() == [[0, 1, 1.0, 2], [2, 3, 1.0, 3]]
