@@ -788,15 +788,36 @@ DREPHIP_EXPORT int drephip_distance_lut(int k, uint32_t denom, double *lut) {
     return DREPHIP_OK;
 }
 
-// Sparse linkage limits: the per-component matrices (sum of m^2 f64 cells) of
-// the automatic choice, and of an explicit drephip_linkage_sparse call.
-constexpr uint64_t kSparseAutoCells = 1ull << 28;     // 2 GB of host memory
+// Sparse linkage limits.  The automatic choice takes the sparse path only
+// where it beats the dense GPU chain: a step there scans one row of the top's
+// component on the host (~1 us per 1000 members) against ~6 us per GPU step,
+// so the largest component may hold 4096 members (DREPHIP_LINK_SPARSE_MAXCOMP)
+// and the matrices 2^28 cells (2 GB; DREPHIP_LINK_SPARSE_CELLS); the pair list
+// is first counted on the device and not read back beyond 32 pairs per genome
+// (+2^20).  Mash data at s = 1000 has a few random shared hashes per 1000
+// unrelated pairs (two 5 Mbp genomes share ~6 random 21-mers), so beyond a few
+// thousand genomes everything is one component and the dense path runs.  An
+// explicit sparse request (drephip_set_linkage_path / drephip_linkage_sparse)
+// allows 2^31 cells and any component size.
 constexpr uint64_t kSparseMaxCells = 1ull << 31;      // 16 GB
 constexpr uint64_t kSparseMaxPairs = 1ull << 26;      // device pair list: 768 MB
 
-static uint64_t sparse_auto_cells() {
-    if (const char *e = std::getenv("DREPHIP_LINK_SPARSE_CELLS")) return std::strtoull(e, nullptr, 10);
-    return kSparseAutoCells;
+static uint64_t env_u64(const char *name, uint64_t dflt) {
+    if (const char *e = std::getenv(name)) return std::strtoull(e, nullptr, 10);
+    return dflt;
+}
+static uint64_t sparse_cells(const drephip_ctx *ctx) {
+    return ctx->link_path == DREPHIP_LINK_PATH_SPARSE ? kSparseMaxCells : env_u64("DREPHIP_LINK_SPARSE_CELLS", 1ull << 28);
+}
+static uint32_t sparse_maxcomp(const drephip_ctx *ctx) {
+    return ctx->link_path == DREPHIP_LINK_PATH_SPARSE ? 0xFFFFFFFFu
+                                                      : (uint32_t)env_u64("DREPHIP_LINK_SPARSE_MAXCOMP", 4096);
+}
+static uint64_t sparse_pair_cap(const drephip_ctx *ctx, uint32_t n) {
+    const uint64_t all = (uint64_t)n * (n - 1) / 2;
+    const uint64_t cap = ctx->link_path == DREPHIP_LINK_PATH_SPARSE ? kSparseMaxPairs
+                                                                    : std::min<uint64_t>(kSparseMaxPairs, 32ull * n + (1ull << 20));
+    return std::min(all, cap);
 }
 
 DREPHIP_EXPORT int drephip_set_linkage_path(drephip_ctx *ctx, int path) {
@@ -810,7 +831,7 @@ DREPHIP_EXPORT int drephip_linkage_sparse(uint32_t n, uint64_t npairs, const uin
                                           const double *v, int method, double *Z) {
     if (n < 2) return DREPHIP_OK;
     if (!Z || (npairs && (!i || !j || !v))) { set_error("null argument"); return DREPHIP_ERR_ARG; }
-    return linkage_sparse_impl(n, npairs, i, j, v, method, kSparseMaxCells, Z, nullptr);
+    return linkage_sparse_impl(n, npairs, i, j, v, method, kSparseMaxCells, 0xFFFFFFFFu, Z, nullptr);
 }
 
 // the sparse path from a host condensed vector: the pairs below 1.0 when no
@@ -830,14 +851,16 @@ static int linkage_condensed_sparse(drephip_ctx *ctx, const double *y, uint32_t 
                 return 0;
             }
             if (d < 1.0) {
-                if (pi.size() >= kSparseMaxPairs && ctx->link_path != DREPHIP_LINK_PATH_SPARSE) return 0;
+                if (pi.size() >= sparse_pair_cap(ctx, n)) {
+                    if (ctx->link_path == DREPHIP_LINK_PATH_SPARSE) { set_error("sparse linkage: more pairs below 1.0 than the pair list holds"); *rc = DREPHIP_ERR_UNSUPPORTED; }
+                    return 0;
+                }
                 pi.push_back(a); pj.push_back(b); pv.push_back(d);
             }
         }
     const double t1 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
-    const int r = linkage_sparse_impl(n, pi.size(), pi.data(), pj.data(), pv.data(), method,
-                                      ctx->link_path == DREPHIP_LINK_PATH_SPARSE ? kSparseMaxCells : sparse_auto_cells(),
-                                      Z, &ctx->link.sp);
+    const int r = linkage_sparse_impl(n, pi.size(), pi.data(), pj.data(), pv.data(), method, sparse_cells(ctx),
+                                      sparse_maxcomp(ctx), Z, &ctx->link.sp);
     if (r == DREPHIP_ERR_UNSUPPORTED && ctx->link_path != DREPHIP_LINK_PATH_SPARSE) return 0;
     if (r) { *rc = r; return 0; }
     ctx->link.sparse = 1;
@@ -901,7 +924,7 @@ DREPHIP_EXPORT int drephip_linkage_counts_device(drephip_ctx *ctx, const uint16_
         // sparse path: the pairs below 1.0 (nonzero counts) extracted on the GPU,
         // scipy's algorithm replayed on them on the host (linkage_sparse.cpp)
         const bool forced = ctx->link_path == DREPHIP_LINK_PATH_SPARSE;
-        const uint64_t cap = std::min<uint64_t>((uint64_t)n * (n - 1) / 2, kSparseMaxPairs);
+        const uint64_t cap = sparse_pair_cap(ctx, n);
         uint32_t *ij = nullptr, *lidx = nullptr, flags = 0;
         uint64_t np = 0;
         rc = sparse_pairs_impl(ctx, d_common, d_denom, n, perm, lut, lut_len, lut_off, cap, &ij, &lidx, &np, &flags,
@@ -917,8 +940,8 @@ DREPHIP_EXPORT int drephip_linkage_counts_device(drephip_ctx *ctx, const uint16_
             std::vector<uint32_t> pi(np), pj(np);
             std::vector<double> pv(np);
             for (uint64_t t = 0; t < np; t++) { pi[t] = ij[2 * t]; pj[t] = ij[2 * t + 1]; pv[t] = lut[lidx[t]]; }
-            rc = linkage_sparse_impl(n, np, pi.data(), pj.data(), pv.data(), method,
-                                     forced ? kSparseMaxCells : sparse_auto_cells(), Z, &ctx->link.sp);
+            rc = linkage_sparse_impl(n, np, pi.data(), pj.data(), pv.data(), method, sparse_cells(ctx),
+                                     sparse_maxcomp(ctx), Z, &ctx->link.sp);
             if (rc == DREPHIP_OK) {
                 done = true;
                 ctx->link.sparse = 1;

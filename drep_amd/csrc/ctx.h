@@ -195,9 +195,10 @@ int sparse_pairs_impl(drephip_ctx *ctx, const uint16_t *d_common, const uint16_t
                       uint64_t cap, uint32_t **h_ij, uint32_t **h_lidx, uint64_t *np, uint32_t *flags,
                       hipStream_t st);
 // Host (linkage_sparse.cpp): scipy's linkage from the pairs below 1.0 (every other pair at 1.0).
-// DREPHIP_ERR_UNSUPPORTED when the per-component matrices would exceed max_cells.
+// DREPHIP_ERR_UNSUPPORTED when the per-component matrices would exceed max_cells or a component
+// max_comp members.
 int linkage_sparse_impl(uint32_t n, uint64_t np, const uint32_t *pi, const uint32_t *pj, const double *pv,
-                        int method, uint64_t max_cells, double *Z_out, SparseLinkInfo *info);
+                        int method, uint64_t max_cells, uint32_t max_comp, double *Z_out, SparseLinkInfo *info);
 void sort_and_label(std::vector<double> &Z, uint32_t n);
 
 // Host ingest (ingest.cpp).

@@ -277,7 +277,7 @@ template <class F> static void for_components(size_t nc, F fn) {
 }
 
 int linkage_sparse_impl(uint32_t n, uint64_t np, const uint32_t *pi, const uint32_t *pj, const double *pv,
-                        int method, uint64_t max_cells, double *Z_out, SparseLinkInfo *info) {
+                        int method, uint64_t max_cells, uint32_t max_comp, double *Z_out, SparseLinkInfo *info) {
     SparseLinkInfo loc_info;
     SparseLinkInfo &I = info ? *info : loc_info;
     I = SparseLinkInfo{};
@@ -331,9 +331,10 @@ int linkage_sparse_impl(uint32_t n, uint64_t np, const uint32_t *pi, const uint3
         }
         I.components = (uint32_t)comps.size();
         I.cells = cells;
-        if (cells > max_cells) {
+        if (cells > max_cells || I.largest > max_comp) {
             set_error("sparse linkage: the components need " + std::to_string(cells) + " matrix cells (limit " +
-                      std::to_string(max_cells) + ")");
+                      std::to_string(max_cells) + "), the largest has " + std::to_string(I.largest) +
+                      " members (limit " + std::to_string(max_comp) + ")");
             return DREPHIP_ERR_UNSUPPORTED;
         }
         // v -> component (kNone: a singleton) and its index among the members

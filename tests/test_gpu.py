@@ -846,12 +846,17 @@ def test_gpu_linkage_matches_scipy(method, n, kind):
         assert np.array_equal(Z, Zs), (per_lane, np.argwhere(Z != Zs)[:5])
     with _lib.Context(0, 21, S, 42) as ctx:
         Z = ctx.linkage(y, method)
-        assert ctx.linkage_info()["sparse"] == (kind != "above1")
+        if kind in ("mash", "above1"):          # small components / no sparse form
+            assert ctx.linkage_info()["sparse"] == (kind == "mash")
         assert np.array_equal(Z, Zs), ("auto", np.argwhere(Z != Zs)[:5])
+        ctx.set_linkage_path(ctx.LINK_SPARSE)
         if kind == "above1":
-            ctx.set_linkage_path(ctx.LINK_SPARSE)
             with pytest.raises(_lib.DrepHipError, match="above 1.0"):
                 ctx.linkage(y, method)
+        else:
+            Z = ctx.linkage(y, method)
+            assert ctx.linkage_info()["sparse"]
+            assert np.array_equal(Z, Zs), ("sparse", np.argwhere(Z != Zs)[:5])
 
 
 @pytest.mark.parametrize("path", ["auto", "dense", "sparse"])

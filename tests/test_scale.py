@@ -1,10 +1,10 @@
 """BASELINE configs[2], [3] and [4] in their one-GPU form: 10^4 and 10^5
 synthetic 5 Mbp genomes at s = 1000, and 10^4 genomes at s = 10^4 -- sketch,
 all-pairs over the whole triangle (5x10^7 / 5x10^9 pairs; 10 GB of condensed
-counts in HBM at 10^5) and average-linkage primary clustering (the automatic
-path -- the pairs below 1.0 extracted on the GPU, scipy's chain replayed on
-them on the host -- and the dense GPU chain on the n x n float64 matrix, 80 GB
-at 10^5, built in HBM from the counts).  All three
+counts in HBM at 10^5) and average-linkage primary clustering (the dense GPU
+chain on the n x n float64 matrix, 80 GB at 10^5, built in HBM from the
+counts; up to 2x10^4 genomes also the sparse path -- the pairs below 1.0
+extracted on the GPU, scipy's chain replayed on them on the host).  All three
 run by default.  DREPHIP_SCALE_N=<n> adds one more size (s = 1000).
 
 Parity at full size:
@@ -18,8 +18,8 @@ Parity at full size:
   * shared-hash counts of random pairs plus three whole rows (first, last,
     random), recomputed by the host oracle's Mash merge from the GPU sketches,
     bit-exact;
-  * linkage Z: the sparse and the dense path bit-identical to each other;
-    n-1 merges, monotone heights, consistent sizes; at 10^4 also
+  * linkage Z: the sparse and the dense path bit-identical to each other (up
+    to 2x10^4 genomes); n-1 merges, monotone heights, consistent sizes; at 10^4 also
     bit-identical to scipy's linkage on the host (reference call:
     drep/d_cluster.py:453; ~1 s of host time).  At 10^5 the scipy comparison
     (121 s of host time) runs only with DREPHIP_SCALE_SCIPY=1.
@@ -223,31 +223,34 @@ def test_scale(N, s, config):
     res["linkage_reserve_s"] = reserve_t.get("s")              # on the helper thread, beside the stages above
     res["linkage_reserve_wait_s"] = time.perf_counter() - t0
     link_ctx.set_timing(True)
-    # the automatic path (sparse here: pairs below 1.0 extracted on the GPU,
-    # scipy's chain replayed on them on the host), then the dense GPU chain on
-    # the n x n matrix: two independent implementations, compared bit for bit
+    # the automatic path (dense here: at s = 1000 random shared hashes join the
+    # families into one component), then -- up to 2x10^4 genomes -- the sparse
+    # path forced (the pairs below 1.0 extracted on the GPU, scipy's chain
+    # replayed on them on the host): two independent implementations,
+    # compared bit for bit
     t0 = time.perf_counter()
     Z = link_ctx.linkage_counts_device(d_common.data_ptr(), None, N, perm, lut, lut_off, "average", stream)
     res["linkage_s"] = time.perf_counter() - t0
     res["linkage_info"] = link_ctx.linkage_info()
-    res["linkage_extract_ms"] = link_ctx.kernel_ms(3)[0]
+    res["linkage_matrix_build_ms"] = link_ctx.kernel_ms(3)[0]
+    res["linkage_chain_ms"] = link_ctx.kernel_ms(2)[0]
     res["linkage_phases_s"] = link_ctx.linkage_stats()
-    note("linkage (%s) %.3f s %s %s" % ("sparse" if res["linkage_info"]["sparse"] else "dense", res["linkage_s"],
-                                         json.dumps(res["linkage_phases_s"]), json.dumps(res["linkage_info"])))
-    link_ctx.set_linkage_path(link_ctx.LINK_DENSE)
-    t0 = time.perf_counter()
-    Zd = link_ctx.linkage_counts_device(d_common.data_ptr(), None, N, perm, lut, lut_off, "average", stream)
-    res["linkage_dense_s"] = time.perf_counter() - t0
-    res["linkage_dense_matrix_build_ms"] = link_ctx.kernel_ms(3)[0]
-    res["linkage_dense_chain_ms"] = link_ctx.kernel_ms(2)[0]
-    res["linkage_dense_phases_s"] = link_ctx.linkage_stats()
-    res["linkage_sparse_equals_dense"] = bool(np.array_equal(Z, Zd))
-    note("dense GPU linkage %.2f s %s (matrix reserved in %.2f s beside sketch/all-pairs, waited %.3f s); "
-         "sparse == dense: %s" % (res["linkage_dense_s"], json.dumps(res["linkage_dense_phases_s"]),
-                                  res["linkage_reserve_s"] or -1, res["linkage_reserve_wait_s"],
-                                  res["linkage_sparse_equals_dense"]))
-    assert res["linkage_info"]["sparse"]
-    assert res["linkage_sparse_equals_dense"]
+    note("linkage (%s) %.3f s %s %s (matrix reserved in %.2f s beside sketch/all-pairs, waited %.3f s)"
+         % ("sparse" if res["linkage_info"]["sparse"] else "dense", res["linkage_s"],
+            json.dumps(res["linkage_phases_s"]), json.dumps(res["linkage_info"]),
+            res["linkage_reserve_s"] or -1, res["linkage_reserve_wait_s"]))
+    if N <= 20_000:
+        link_ctx.set_linkage_path(link_ctx.LINK_DENSE if res["linkage_info"]["sparse"] else link_ctx.LINK_SPARSE)
+        t0 = time.perf_counter()
+        Z2 = link_ctx.linkage_counts_device(d_common.data_ptr(), None, N, perm, lut, lut_off, "average", stream)
+        other = "sparse" if link_ctx.linkage_info()["sparse"] else "dense"
+        res["linkage_%s_s" % other] = time.perf_counter() - t0
+        res["linkage_%s_phases_s" % other] = link_ctx.linkage_stats()
+        res["linkage_sparse_equals_dense"] = bool(np.array_equal(Z, Z2))
+        note("linkage (%s) %.3f s %s; sparse == dense: %s" % (other, res["linkage_%s_s" % other],
+                                                            json.dumps(link_ctx.linkage_stats()),
+                                                            res["linkage_sparse_equals_dense"]))
+        assert res["linkage_sparse_equals_dense"]
     assert Z.shape == (N - 1, 4)
     assert np.all(np.diff(Z[:, 2]) >= 0)           # average linkage is monotone
     assert Z[-1, 3] == N
