@@ -106,14 +106,13 @@ __device__ MinIdx block_argmin(double v, int32_t i) {
 // position a push writes.
 //
 // A step is a chain of dependent memory round trips, so the loads are issued
-// together: each pass takes kLkPer entries per lane (grid-stride) and loads
+// together: each pass takes kLkPer (1, 2 or 4) entries per lane (grid-stride) and loads
 // their sizes and D[t][i] (plus D[x][i], D[y][i] after a merge) before any of
 // them is used or any store is made (written as one loop, the compiler kept
 // each entry's loads behind the previous entry's stores: D aliases itself).
 // The decision's operands -- D[t][below] and the two sizes -- are loaded with
 // the partials: the chain's elements below the top are never x or y, so no
 // update touches them.
-constexpr int kLkPer = 4;
 struct alignas(64) LinkState {
     int32_t k, len, top, below, first_active;
     int32_t pend, x, y, nx, ny;   // Lance-Williams update this state's step applies
@@ -136,6 +135,7 @@ __device__ __forceinline__ MinIdx read_partials(const MinIdx *parts, uint32_t G)
     return block_argmin(bv, bi);
 }
 
+template <int kLkPer>
 __global__ __launch_bounds__(kLkWG) void k_nn_step(double *__restrict__ D, uint32_t n, int method,
                                                    int32_t *__restrict__ size, int32_t *__restrict__ chain,
                                                    LinkState *__restrict__ st, MinIdx *__restrict__ parts,
@@ -260,6 +260,7 @@ __global__ __launch_bounds__(kLkWG) void k_nn_step(double *__restrict__ D, uint3
     if (threadIdx.x == 0) parts[(uint64_t)q * 1024 + blockIdx.x] = part;
 }
 
+template <int kLkPer>
 __global__ __launch_bounds__(kLkWG) void k_mst_step(const double *__restrict__ D, uint32_t n,
                                                     int32_t *__restrict__ merged, double *__restrict__ Dmin,
                                                     LinkState *__restrict__ st, MinIdx *__restrict__ parts,
@@ -428,11 +429,16 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
         set_error("linkage method must be single, complete, average or weighted");
         return DREPHIP_ERR_UNSUPPORTED;
     }
-    // entries per lane of a step, i.e. the grid density (default kLkPer: one pass;
-    // DREPHIP_LINK_PER_LANE exists for the tests, which cover 1, 4 and 16)
+    // entries per lane of a step, i.e. the grid density: ~200 workgroups at
+    // most (n = 10^5: 2 per lane, 1.76 s of chain against 1.91 s at 4 and
+    // 1.89 s at 1; n = 10^4: 1 per lane, 40 workgroups, 158 ms against 176 ms
+    // at 4 -- profiles/r03_linkage_grid_density.txt).  DREPHIP_LINK_PER_LANE
+    // overrides it (the tests cover 1, 4 and 16: several passes)
     const char *pl = getenv("DREPHIP_LINK_PER_LANE");
-    const uint32_t per = pl ? std::max(1, std::min(64, atoi(pl))) : 4;
+    const uint32_t per = pl ? std::max(1, std::min(64, atoi(pl)))
+                            : std::max(1u, (n + kLkWG * 200 - 1) / (kLkWG * 200));
     const uint32_t grid = std::max(1u, std::min(1024u, (n + kLkWG * per - 1) / (kLkWG * per)));
+    const int tpl = per <= 1 ? 1 : per <= 2 ? 2 : 4;          // entries per lane per pass
     int32_t *d_size, *d_chain, *d_done;
     double *d_Z, *d_Dmin;
     LinkState *d_st;
@@ -476,12 +482,16 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     HIPC(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
     static_assert(kBatch % 2 == 0, "step parity must restart at 0 with every replay");
     for (int b = 0; b < kBatch; b++) {
-        if (mst)
-            hipLaunchKernelGGL(k_mst_step, dim3(grid), dim3(kLkWG), 0, st, d_D, n, d_size, d_Dmin, d_st, d_parts,
-                               d_done, d_Z, (uint32_t)(b & 1));
-        else
-            hipLaunchKernelGGL(k_nn_step, dim3(grid), dim3(kLkWG), 0, st, d_D, n, method, d_size, d_chain, d_st,
-                               d_parts, d_done, d_Z, (uint32_t)(b & 1));
+        const uint32_t q = (uint32_t)(b & 1);
+        if (mst) {
+            if (tpl == 1) hipLaunchKernelGGL(k_mst_step<1>, dim3(grid), dim3(kLkWG), 0, st, d_D, n, d_size, d_Dmin, d_st, d_parts, d_done, d_Z, q);
+            else if (tpl == 2) hipLaunchKernelGGL(k_mst_step<2>, dim3(grid), dim3(kLkWG), 0, st, d_D, n, d_size, d_Dmin, d_st, d_parts, d_done, d_Z, q);
+            else hipLaunchKernelGGL(k_mst_step<4>, dim3(grid), dim3(kLkWG), 0, st, d_D, n, d_size, d_Dmin, d_st, d_parts, d_done, d_Z, q);
+        } else {
+            if (tpl == 1) hipLaunchKernelGGL(k_nn_step<1>, dim3(grid), dim3(kLkWG), 0, st, d_D, n, method, d_size, d_chain, d_st, d_parts, d_done, d_Z, q);
+            else if (tpl == 2) hipLaunchKernelGGL(k_nn_step<2>, dim3(grid), dim3(kLkWG), 0, st, d_D, n, method, d_size, d_chain, d_st, d_parts, d_done, d_Z, q);
+            else hipLaunchKernelGGL(k_nn_step<4>, dim3(grid), dim3(kLkWG), 0, st, d_D, n, method, d_size, d_chain, d_st, d_parts, d_done, d_Z, q);
+        }
     }
     HIPC(hipStreamEndCapture(st, &graph));
     hipError_t e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
