@@ -135,15 +135,34 @@ __device__ __forceinline__ MinIdx read_partials(const MinIdx *parts, uint32_t G)
     return block_argmin(bv, bi);
 }
 
+// The decision's operands -- D[top][below], the two sizes and the chain
+// entries a merge exposes -- are loaded by one extra workgroup of the kernel
+// that makes the PREVIOUS decision (it replicates that decision and writes
+// them to fwd[q] while the others run the step), so a step's critical path is
+// two dependent round trips (state + partials, issued together; then the row)
+// instead of three.  They are stable while that kernel runs: D[top][below]
+// after a merge is between chain elements below the merged pair (never x or
+// y), after a push no update is pending; the chain entries are older than the
+// kernel's own push; the sizes go through the same overrides as everywhere.
+struct alignas(64) LinkFwd {
+    double dp;
+    int32_t szt, szb, c3, c4;
+};
+
 template <int kLkPer>
 __global__ __launch_bounds__(kLkWG) void k_nn_step(double *__restrict__ D, uint32_t n, int method,
                                                    int32_t *__restrict__ size, int32_t *__restrict__ chain,
-                                                   LinkState *__restrict__ st, MinIdx *__restrict__ parts,
-                                                   int32_t *__restrict__ done, double *__restrict__ Z, uint32_t q) {
+                                                   LinkState *__restrict__ st, LinkFwd *__restrict__ fwd,
+                                                   MinIdx *__restrict__ parts, int32_t *__restrict__ done,
+                                                   double *__restrict__ Z, uint32_t q) {
     __shared__ LinkState sx;
+    const uint32_t G = gridDim.x - 1;                          // step workgroups; workgroup G forwards operands
     const LinkState S = st[q ^ 1];
+    const LinkFwd F = fwd[q ^ 1];
+    // the partials are read whether or not a decision is pending (valid memory
+    // either way), so their loads are not held behind the state's
+    const MinIdx g = read_partials(parts + (uint64_t)(q ^ 1) * 1024, G);
     if (S.k >= (int32_t)n - 1) return;                         // all merged
-    const uint32_t G = gridDim.x;
     const bool w0 = blockIdx.x == 0;
     // size of cluster i as of the previous decision: workgroup 0 writes that
     // decision's two sizes during this kernel, so every reader overrides them
@@ -152,15 +171,8 @@ __global__ __launch_bounds__(kLkWG) void k_nn_step(double *__restrict__ D, uint3
     };
     if (w0 && threadIdx.x == 0 && S.psa >= 0) { size[S.psa] = 0; size[S.psb] = S.psbsz; }
     // ---- the previous step's decision (replicated in every workgroup)
-    double dp = 0.0;
-    int32_t szt = 0, szb = 0, c3 = 0, c4 = 0;
-    if (threadIdx.x == 0 && S.decide && S.len > 1) {
-        dp = D[(uint64_t)S.top * n + S.below];
-        szt = size_prev(S.top, size[S.top]); szb = size_prev(S.below, size[S.below]);
-        if (S.len >= 3) c3 = chain[S.len - 3];
-        if (S.len >= 4) c4 = chain[S.len - 4];
-    }
-    const MinIdx g = S.decide ? read_partials(parts + (uint64_t)(q ^ 1) * 1024, G) : MinIdx{0.0, 0};
+    const double dp = F.dp;
+    const int32_t szt = F.szt, szb = F.szb, c3 = F.c3, c4 = F.c4;
     if (threadIdx.x == 0) {
         LinkState X = S;
         X.psa = -1; X.psb = -1; X.psbsz = 0;
@@ -205,7 +217,23 @@ __global__ __launch_bounds__(kLkWG) void k_nn_step(double *__restrict__ D, uint3
             if (X.k >= (int32_t)n - 1) st[q ^ 1] = X;           // the finished state in both buffers
             *done = X.k;
         }
+        if (blockIdx.x == G && X.k < (int32_t)n - 1) {
+            // the next decision's operands (sizes as of this decision)
+            auto size_now = [&](int32_t i) {
+                return i == X.psa ? 0 : i == X.psb ? X.psbsz : size_prev(i, size[i]);
+            };
+            LinkFwd f{0.0, 0, 0, 0, 0};
+            if (X.len > 1) {
+                f.dp = D[(uint64_t)X.top * n + X.below];
+                f.szt = size_now(X.top);
+                f.szb = size_now(X.below);
+            }
+            if (X.len >= 3) f.c3 = chain[X.len - 3];
+            if (X.len >= 4) f.c4 = chain[X.len - 4];
+            fwd[q] = f;
+        }
     }
+    if (blockIdx.x == G) return;                               // the forwarding workgroup has no step work
     __syncthreads();
     const LinkState X = sx;
     if (X.k >= (int32_t)n - 1) return;
@@ -268,9 +296,9 @@ __global__ __launch_bounds__(kLkWG) void k_mst_step(const double *__restrict__ D
     __shared__ LinkState sx;
     __shared__ int32_t s_ov;
     const LinkState S = st[q ^ 1];
-    if (S.k >= (int32_t)n - 1) return;
     const uint32_t G = gridDim.x;
-    const MinIdx g = S.decide ? read_partials(parts + (uint64_t)(q ^ 1) * 1024, G) : MinIdx{0.0, 0};
+    const MinIdx g = read_partials(parts + (uint64_t)(q ^ 1) * 1024, G);     // unconditional: not held behind S
+    if (S.k >= (int32_t)n - 1) return;
     if (threadIdx.x == 0) {
         LinkState X = S;
         int32_t ov = -1;
@@ -449,6 +477,9 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     if ((rc = scratch(ctx, "lk_Z", (n - 1) * 32ull, (void **)&d_Z))) return rc;
     if ((rc = scratch(ctx, "lk_parts", 2 * 1024 * sizeof(MinIdx), (void **)&d_parts))) return rc;
     if ((rc = scratch(ctx, "lk_st", 2 * sizeof(LinkState), (void **)&d_st))) return rc;
+    LinkFwd *d_fwd;
+    if ((rc = scratch(ctx, "lk_fwd", 2 * sizeof(LinkFwd), (void **)&d_fwd))) return rc;
+    HIPC(hipMemsetAsync(d_fwd, 0, 2 * sizeof(LinkFwd), st));
     if ((rc = scratch(ctx, "lk_done", 4, (void **)&d_done))) return rc;
     const bool mst = method == DREPHIP_LINK_SINGLE;
     if (mst && (rc = scratch(ctx, "lk_dmin", n * 8ull, (void **)&d_Dmin))) return rc;
@@ -488,9 +519,9 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
             else if (tpl == 2) hipLaunchKernelGGL(k_mst_step<2>, dim3(grid), dim3(kLkWG), 0, st, d_D, n, d_size, d_Dmin, d_st, d_parts, d_done, d_Z, q);
             else hipLaunchKernelGGL(k_mst_step<4>, dim3(grid), dim3(kLkWG), 0, st, d_D, n, d_size, d_Dmin, d_st, d_parts, d_done, d_Z, q);
         } else {
-            if (tpl == 1) hipLaunchKernelGGL(k_nn_step<1>, dim3(grid), dim3(kLkWG), 0, st, d_D, n, method, d_size, d_chain, d_st, d_parts, d_done, d_Z, q);
-            else if (tpl == 2) hipLaunchKernelGGL(k_nn_step<2>, dim3(grid), dim3(kLkWG), 0, st, d_D, n, method, d_size, d_chain, d_st, d_parts, d_done, d_Z, q);
-            else hipLaunchKernelGGL(k_nn_step<4>, dim3(grid), dim3(kLkWG), 0, st, d_D, n, method, d_size, d_chain, d_st, d_parts, d_done, d_Z, q);
+            if (tpl == 1) hipLaunchKernelGGL(k_nn_step<1>, dim3(grid + 1), dim3(kLkWG), 0, st, d_D, n, method, d_size, d_chain, d_st, d_fwd, d_parts, d_done, d_Z, q);
+            else if (tpl == 2) hipLaunchKernelGGL(k_nn_step<2>, dim3(grid + 1), dim3(kLkWG), 0, st, d_D, n, method, d_size, d_chain, d_st, d_fwd, d_parts, d_done, d_Z, q);
+            else hipLaunchKernelGGL(k_nn_step<4>, dim3(grid + 1), dim3(kLkWG), 0, st, d_D, n, method, d_size, d_chain, d_st, d_fwd, d_parts, d_done, d_Z, q);
         }
     }
     HIPC(hipStreamEndCapture(st, &graph));

@@ -277,11 +277,11 @@ __device__ __forceinline__ uint64_t murmur_fin(uint64_t q1, uint64_t q2) {
 #ifndef DREPHIP_SK_BATCH
 #define DREPHIP_SK_BATCH 2          // k-mers per admit test: 52 VGPRs (4: 58, 0.8 % slower; 8: 73, 7 waves, 2 % slower;
                                     // all 16 of a chunk as one block, keeping only the prefilter bits and recomputing
-                                    // the rare hits: 56 VGPRs, 4 % slower -- profiles/r03_sketch_ab_block16.txt)
-#endif
-#ifndef DREPHIP_SK_MODE
-#define DREPHIP_SK_MODE 0           // 0: fetch+hash per k-mer; 1: a batch's table reads issued first; 2: the next batch's
-                                    // reads issued before this batch's hash (within a chunk)
+                                    // the rare hits: 56 VGPRs, 4 % slower -- profiles/r03_sketch_ab_block16.txt).
+                                    // Issuing a batch's table reads before its hash (64 VGPRs), or the next
+                                    // k-mer's reads before this one's (65; capped at 64: 8 B of spill) measured
+                                    // 0.3-0.7 % slower (profiles/r03_sketch_ab_sched.txt): the LDS latency is
+                                    // already covered by the other waves
 #endif
 #ifndef DREPHIP_SK_MINW
 #define DREPHIP_SK_MINW 1
@@ -373,53 +373,16 @@ __global__ __launch_bounds__(kTile / LANE, DREPHIP_SK_MINW) void k_sketch_hash21
             const uint64_t rc = ((uint64_t)chi << 32) | clo;
             return fw <= rc ? fw : rc;
         };
-        auto fetch = [&](int r) -> MEnt {
-            const uint64_t cc = canon(r);
-            return fetch_ent(tb, (uint32_t)(cc >> 32), (uint32_t)cc, sh);
-        };
-#if DREPHIP_SK_MODE == 2
-        MEnt Ecur[BATCH];
-#pragma unroll
-        for (int b = 0; b < BATCH; b++) Ecur[b] = fetch(b);
-#endif
 #pragma unroll
         for (int b0 = 0; b0 < 16; b0 += BATCH) {
             uint64_t p1[BATCH], p2[BATCH];
             bool hit = false;
-#if DREPHIP_SK_MODE == 0
 #pragma unroll
             for (int b = 0; b < BATCH; b++) {
                 const uint64_t cc = canon(b0 + b);
                 murmur21_q(tb, (uint32_t)(cc >> 32), (uint32_t)cc, seed, sh, p1[b], p2[b]);
                 hit |= prefilter_hi(p1[b], p2[b]) <= Tp;
             }
-#elif DREPHIP_SK_MODE == 1
-            MEnt E[BATCH];
-#pragma unroll
-            for (int b = 0; b < BATCH; b++) E[b] = fetch(b0 + b);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int b = 0; b < BATCH; b++) {
-                murmur21_ent(E[b], seed, p1[b], p2[b]);
-                hit |= prefilter_hi(p1[b], p2[b]) <= Tp;
-            }
-#else
-            MEnt Enext[BATCH];
-            if (b0 + BATCH < 16) {
-#pragma unroll
-                for (int b = 0; b < BATCH; b++) Enext[b] = fetch(b0 + BATCH + b);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int b = 0; b < BATCH; b++) {
-                murmur21_ent(Ecur[b], seed, p1[b], p2[b]);
-                hit |= prefilter_hi(p1[b], p2[b]) <= Tp;
-            }
-            if (b0 + BATCH < 16) {
-#pragma unroll
-                for (int b = 0; b < BATCH; b++) Ecur[b] = Enext[b];
-            }
-#endif
             if (__builtin_expect(hit, 0)) {
 #pragma unroll
                 for (int b = 0; b < BATCH; b++) {
