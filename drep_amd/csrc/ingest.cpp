@@ -11,7 +11,8 @@
 // quality is at least as long as the sequence -- a quality of a different
 // length (or none) ends the file there, that record not kept, as kseq_read's
 // -2 ends Mash's loop.  Bytes are upper-cased a-z; only A/C/G/T are valid
-// bases, anything else breaks k-mers.  Plain or gzip input.
+// bases, anything else breaks k-mers.  Plain or gzip input (gzip inflated
+// whole by libdeflate when it is present, else streamed through zlib).
 //
 // Speed: the file is read in 4 MiB blocks, lines are found with memchr and
 // sequence lines appended with memcpy; packing builds each 32-base group
@@ -20,6 +21,7 @@
 #include "ctx.h"
 
 #include <zlib.h>
+#include <dlfcn.h>
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
@@ -44,15 +46,92 @@ static inline const char *find_header_char(const char *p, const char *end) {
     return p;
 }
 
+// libdeflate (Ubuntu's libdeflate0 1.10; its header is not installed, so the
+// four entry points used are declared here and bound at run time): a gzip file
+// is read whole and inflated in one call, 2-3x zlib's streaming inflate.  Any
+// file it does not take (no library, DREPHIP_NO_LIBDEFLATE, not gzip, a
+// member it rejects) goes through zlib's gzread, which defines the semantics
+// (concatenated members, trailing garbage ignored).
+namespace {
+struct Libdeflate {
+    typedef void *(*alloc_t)();
+    typedef int (*gunzip_t)(void *, const void *, size_t, void *, size_t, size_t *, size_t *);
+    typedef void (*free_t)(void *);
+    alloc_t alloc = nullptr;
+    gunzip_t gunzip = nullptr;
+    free_t release = nullptr;
+    Libdeflate() {
+        if (std::getenv("DREPHIP_NO_LIBDEFLATE")) return;
+        void *h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        alloc = (alloc_t)dlsym(h, "libdeflate_alloc_decompressor");
+        gunzip = (gunzip_t)dlsym(h, "libdeflate_gzip_decompress_ex");
+        release = (free_t)dlsym(h, "libdeflate_free_decompressor");
+        if (!alloc || !gunzip || !release) alloc = nullptr;
+    }
+};
+const Libdeflate &libdeflate() {
+    static const Libdeflate d;
+    return d;
+}
+struct Decompressor {                      // one per worker thread
+    void *d = nullptr;
+    ~Decompressor() { if (d) libdeflate().release(d); }
+};
+constexpr int kLdSuccess = 0, kLdInsufficientSpace = 3;
+
+// the whole gzip file at `path` inflated into out[0..*n); false: not taken
+bool gunzip_whole(const char *path, std::vector<char> &in, std::vector<char> &out, size_t *n) {
+    const Libdeflate &L = libdeflate();
+    if (!L.alloc) return false;
+    FILE *fp = fopen(path, "rb");
+    if (!fp) return false;
+    fseek(fp, 0, SEEK_END);
+    const long sz = ftell(fp);
+    fseek(fp, 0, SEEK_SET);
+    if (sz < 18) { fclose(fp); return false; }
+    if (in.size() < (size_t)sz) in.resize((size_t)sz);
+    const size_t got = fread(in.data(), 1, (size_t)sz, fp);
+    fclose(fp);
+    if (got != (size_t)sz || (uint8_t)in[0] != 0x1f || (uint8_t)in[1] != 0x8b) return false;
+    static thread_local Decompressor dec;
+    if (!dec.d && !(dec.d = L.alloc())) return false;
+    // the last member's ISIZE (exact for the usual single-member file)
+    uint32_t isize;
+    memcpy(&isize, in.data() + sz - 4, 4);
+    size_t pos = 0, o = 0;
+    if (out.size() < (size_t)isize + 64) out.resize((size_t)isize + 64);
+    while (pos < (size_t)sz) {
+        if (sz - pos < 18 || (uint8_t)in[pos] != 0x1f || (uint8_t)in[pos + 1] != 0x8b) break;   // trailing bytes
+        size_t used_in = 0, produced = 0;
+        const int r = L.gunzip(dec.d, in.data() + pos, (size_t)sz - pos, out.data() + o, out.size() - o, &used_in, &produced);
+        if (r == kLdInsufficientSpace) { out.resize(2 * out.size() + (1u << 20)); continue; }
+        if (r != kLdSuccess) return false;
+        pos += used_in;
+        o += produced;
+    }
+    *n = o;
+    return true;
+}
+}  // namespace
+
 int read_fasta(const char *path, Genome &g) {
-    gzFile f = gzopen(path, "rb");
-    if (!f) { set_error(std::string("cannot open ") + path); return -1; }
-    gzbuffer(f, 1 << 20);
+    static thread_local std::vector<char> zin, zout;              // libdeflate buffers, reused across files
+    size_t zn = 0;
+    const bool whole = gunzip_whole(path, zin, zout, &zn);
+    gzFile f = nullptr;
+    if (!whole) {
+        f = gzopen(path, "rb");
+        if (!f) { set_error(std::string("cannot open ") + path); return -1; }
+        gzbuffer(f, 1 << 20);
+    }
     g.seq.clear(); g.rec_len.clear(); g.length = 0;
-    // the sequence buffer is sized once (file size; x4 if gzip) and written
-    // through a cursor, then trimmed at the end
+    // the sequence buffer is sized once (file size; x4 if gzip; the inflated
+    // size) and written through a cursor, then trimmed at the end
     size_t used = 0;
-    if (FILE *fp = fopen(path, "rb")) {
+    if (whole) {
+        g.seq.resize(zn);
+    } else if (FILE *fp = fopen(path, "rb")) {
         fseek(fp, 0, SEEK_END);
         const long sz = ftell(fp);
         fclose(fp);
@@ -80,13 +159,8 @@ int read_fasta(const char *path, Genome &g) {
     uint64_t qlen = 0, qline = 0;                  // quality so far; current quality line's length
     char qlast = 0;                                // its last byte (a final '\r' is not counted)
     bool stop = false;
-    const size_t kBlock = 4u << 20;
-    static thread_local std::vector<char> buf(kBlock + 64);   // reused across files (no 4 MiB memset each)
-    while (!stop) {
-        const int got = gzread(f, buf.data(), (unsigned)kBlock);
-        if (got < 0) { gzclose(f); set_error(std::string("read error in ") + path); return -1; }
-        if (got == 0) break;
-        const char *p = buf.data(), *end = p + got;
+    // one block of the file through the state machine
+    auto feed = [&](const char *p, const char *end) {
         while (p < end && !stop) {
             switch (st) {
             case HUNT:
@@ -184,6 +258,19 @@ int read_fasta(const char *path, Genome &g) {
             st = START;
         next_state:;
         }
+    };
+    if (whole) {
+        feed(zout.data(), zout.data() + zn);
+    } else {
+        const size_t kBlock = 4u << 20;
+        static thread_local std::vector<char> buf(kBlock + 64);   // reused across files (no 4 MiB memset each)
+        while (!stop) {
+            const int got = gzread(f, buf.data(), (unsigned)kBlock);
+            if (got < 0) { gzclose(f); set_error(std::string("read error in ") + path); return -1; }
+            if (got == 0) break;
+            feed(buf.data(), buf.data() + got);
+        }
+        gzclose(f);
     }
     // end of file
     if (st == SEQ) end_seq_line();
@@ -193,7 +280,6 @@ int read_fasta(const char *path, Genome &g) {
         if (qline) qlen += qline - (qlast == '\r');                  // last line, no '\n'
         if (qlen != g.rec_len.back()) drop_last_record();            // short quality: -2
     }
-    gzclose(f);
     g.seq.resize(used);
     for (uint64_t l : g.rec_len) g.length += l;
     return 0;
