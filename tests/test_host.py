@@ -552,3 +552,57 @@ def test_linkage_sparse_rejects_bad_lists():
     assert _lib.linkage_sparse(1, [], [], [], "average").shape == (0, 4)
     Z = _lib.linkage_sparse(3, [], [], [], "average")          # no pair below 1.0
     assert Z.tolist() == [[0, 1, 1.0, 2], [2, 3, 1.0, 3]]
+
+
+def test_gzip_reader_libdeflate_equals_zlib(golden, tmp_path):
+    """The whole-file libdeflate inflate and zlib's streaming gzread give the
+    same packed genome (and the same errors) on: the reference's gzipped
+    genomes, a file of several gzip members with trailing junk (zlib's
+    gzread semantics), a gzipped FASTQ and a truncated member."""
+    import glob
+    import gzip
+    import subprocess
+    import sys
+    ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    fas = sorted(glob.glob(os.path.join(golden, "genomes", "*.gz")))
+    raw = gzip.decompress(open(fas[1], "rb").read())
+    third = len(raw) // 3
+    mm = tmp_path / "multi.fa.gz"
+    mm.write_bytes(gzip.compress(raw[:third]) + gzip.compress(raw[third:2 * third]) +
+                   gzip.compress(raw[2 * third:]) + b"trailing junk")
+    fq = tmp_path / "reads.fq.gz"
+    fq.write_bytes(gzip.compress(b"@r1\nACGTACGTACGTACGTACGTACGTAC\n+\nIIIIIIIIIIIIIIIIIIIIIIIIII\n"
+                                 b"@r2\nTTTTGGGGCCCCAAAATTTTGGGGCCCC\n+\nIIIIIIIIIIIIIIIIIIIIIIIIIIII\n"))
+    tr = tmp_path / "truncated.fa.gz"
+    full = gzip.compress(raw)
+    tr.write_bytes(full[:len(full) // 2])
+    files = fas + [str(mm), str(fq), str(tr)]
+    code = r"""
+import ctypes as C, hashlib, json, sys
+import numpy as np
+sys.path.insert(0, %r)
+from drep_amd import _lib
+L = _lib.lib(); tile = _lib.tile_bases(); out = []
+for fa in %r:
+    try:
+        info = _lib.fasta_info(fa)
+    except _lib.DrepHipError as e:
+        out.append("error"); continue
+    P = info["padded"]
+    codes = np.zeros((tile + P) // 16, np.uint32); valid = np.zeros((tile + P) // 32, np.uint32)
+    ln, nk = C.c_uint64(0), C.c_uint64(0)
+    rc = L.drephip_fasta_pack(fa.encode(), 21, codes, valid, tile, tile + P, C.byref(ln), C.byref(nk))
+    out.append([rc, ln.value, nk.value, hashlib.sha1(codes.tobytes() + valid.tobytes()).hexdigest()])
+print(json.dumps(out))
+""" % (ROOT, files)
+    res = []
+    for no_ld in (False, True):
+        env = dict(os.environ)
+        env.pop("DREPHIP_NO_LIBDEFLATE", None)
+        if no_ld:
+            env["DREPHIP_NO_LIBDEFLATE"] = "1"
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True)
+        res.append(json.loads(r.stdout))
+    assert res[0] == res[1]
+    assert res[0][len(fas)] == res[0][1]            # the members concatenated: the original file
+    assert res[0][-1] == "error" or res[0][-1][0] != 0 or res[0][-1][1] < len(raw)
