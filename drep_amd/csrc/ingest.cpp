@@ -86,6 +86,8 @@ bool gunzip_whole(const char *path, std::vector<char> &in, std::vector<char> &ou
     if (!L.alloc) return false;
     FILE *fp = fopen(path, "rb");
     if (!fp) return false;
+    unsigned char magic[2] = {0, 0};
+    if (fread(magic, 1, 2, fp) != 2 || magic[0] != 0x1f || magic[1] != 0x8b) { fclose(fp); return false; }   // plain: zlib path
     fseek(fp, 0, SEEK_END);
     const long sz = ftell(fp);
     fseek(fp, 0, SEEK_SET);
@@ -93,7 +95,7 @@ bool gunzip_whole(const char *path, std::vector<char> &in, std::vector<char> &ou
     if (in.size() < (size_t)sz) in.resize((size_t)sz);
     const size_t got = fread(in.data(), 1, (size_t)sz, fp);
     fclose(fp);
-    if (got != (size_t)sz || (uint8_t)in[0] != 0x1f || (uint8_t)in[1] != 0x8b) return false;
+    if (got != (size_t)sz) return false;
     static thread_local Decompressor dec;
     if (!dec.d && !(dec.d = L.alloc())) return false;
     // the last member's ISIZE (exact for the usual single-member file)
