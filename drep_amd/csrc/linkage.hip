@@ -623,11 +623,16 @@ int dist_from_condensed_impl(drephip_ctx *ctx, const double *y, uint32_t n, doub
 // The pairs below 1.0 of the all-pairs counts, for the sparse linkage path
 // (linkage_sparse.cpp): a pair with no shared hash is exactly 1.0, so only a
 // nonzero count can be below it.  The condensed counts are streamed 8 per
-// lane (16-byte loads, plus the denominators when some sketch is partial);
-// a wave's finds are packed with one atomic per wave.  Output: (perm i,
-// perm j) and the table index off[denom] + common, unordered.  HBM-bound: 2 B
-// per pair (4 with denominators) -- 10 GB at n = 10^5.
+// lane (16-byte loads, plus the denominators when some sketch is partial).
+// Two passes over the same grid-stride ranges: the first counts each
+// workgroup's finds, the host turns the counts into offsets (and stops there
+// when the list would exceed its cap), the second writes (perm i, perm j) and
+// the table index off[denom] + common at the workgroup's offset -- no global
+// atomic (one counter for ~10^7 finds at 10^5 genomes serialised the pass:
+// 28 ms instead of ~3).  HBM-bound: 2 B per pair (4 with denominators), 10 GB
+// at n = 10^5.
 constexpr int kSpWG = 256;
+constexpr uint32_t kSpGrid = 4096;
 __device__ __forceinline__ void cond_ij(uint64_t t, uint32_t n, uint32_t &i, uint32_t &j) {
     const double Mf = 2.0 * n - 1.0;
     int64_t r = (int64_t)((Mf - sqrt(fmax(Mf * Mf - 8.0 * (double)t, 0.0))) * 0.5);
@@ -640,25 +645,30 @@ __device__ __forceinline__ void cond_ij(uint64_t t, uint32_t n, uint32_t &i, uin
     j = (uint32_t)(t - S(r) + r + 1);
 }
 
+template <bool WRITE>
 __global__ __launch_bounds__(kSpWG) void k_sparse_pairs(const uint16_t *__restrict__ common,
                                                          const uint16_t *__restrict__ denom, uint64_t np,
                                                          uint32_t n, uint32_t s, const double *__restrict__ lut,
                                                          const int32_t *__restrict__ off,
-                                                         const uint32_t *__restrict__ perm, uint64_t cap,
+                                                         const uint32_t *__restrict__ perm,
+                                                         uint32_t *__restrict__ wg_count,
+                                                         const uint64_t *__restrict__ wg_off,
                                                          uint32_t *__restrict__ out_ij, uint32_t *__restrict__ out_l,
-                                                         unsigned long long *__restrict__ count,
                                                          uint32_t *__restrict__ flags) {
+    __shared__ uint32_t s_n;
     const uint64_t nchunk = (np + 7) / 8;
     const uint64_t stride = (uint64_t)gridDim.x * kSpWG;
     const int32_t off_s = off[s];
     const uint32_t lane = threadIdx.x & 63;
-    uint32_t bad = 0;
-    for (uint64_t c0 = (uint64_t)blockIdx.x * kSpWG; c0 < nchunk; c0 += stride) {   // wave-uniform trip count
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    const uint64_t base = WRITE ? wg_off[blockIdx.x] : 0;
+    uint32_t bad = 0, mine = 0;
+    for (uint64_t c0 = (uint64_t)blockIdx.x * kSpWG; c0 < nchunk; c0 += stride) {
         const uint64_t c = c0 + threadIdx.x;
         const uint64_t t0 = c * 8;
         uint16_t cm[8], dn[8];
-        const bool full = t0 + 8 <= np;
-        if (full) {
+        if (t0 + 8 <= np) {
             const uint4 w = *(const uint4 *)(common + t0);
             const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
@@ -677,19 +687,20 @@ __global__ __launch_bounds__(kSpWG) void k_sparse_pairs(const uint16_t *__restri
             }
         }
         uint32_t hit = 0, lidx[8];
-        if (c < nchunk) {
 #pragma unroll
-            for (int e = 0; e < 8; e++) {
-                const uint32_t d = denom ? dn[e] : s;
-                if (denom || cm[e]) {
-                    const int32_t o = !denom ? off_s : d <= s ? off[d] : -1;
-                    if (o < 0 || cm[e] > d) { bad = 1; continue; }
-                    lidx[e] = (uint32_t)o + cm[e];
-                    if (cm[e] && lut[lidx[e]] < 1.0) hit |= 1u << e;
-                }
+        for (int e = 0; e < 8; e++) {
+            lidx[e] = 0;
+            if (t0 + e >= np) continue;
+            const uint32_t d = denom ? dn[e] : s;
+            if (denom || cm[e]) {
+                const int32_t o = !denom ? off_s : d <= s ? off[d] : -1;
+                if (o < 0 || cm[e] > d) { bad = 1; continue; }
+                lidx[e] = (uint32_t)o + cm[e];
+                if (cm[e] && lut[lidx[e]] < 1.0) hit |= 1u << e;
             }
         }
-        // pack the wave's finds: one atomic per wave
+        if (!WRITE) { mine += __builtin_popcount(hit); continue; }
+        // the wave's finds: lane offsets by a wave scan, one LDS atomic per wave
         const uint32_t h = __builtin_popcount(hit);
         if (__ballot(h != 0)) {
             uint32_t inc = h;
@@ -698,24 +709,27 @@ __global__ __launch_bounds__(kSpWG) void k_sparse_pairs(const uint16_t *__restri
                 const uint32_t y = __shfl_up(inc, d, 64);
                 if (lane >= (uint32_t)d) inc += y;
             }
-            unsigned long long base = 0;
-            if (lane == 63) base = atomicAdd(count, (unsigned long long)inc);
-            base = __shfl(base, 63, 64);
-            uint64_t slot = base + inc - h;
+            uint32_t wbase = 0;
+            if (lane == 63) wbase = atomicAdd(&s_n, inc);
+            wbase = __shfl(wbase, 63, 64);
+            uint64_t slot = base + wbase + inc - h;
             for (int e = 0; e < 8; e++) {
                 if (!(hit >> e & 1)) continue;
-                if (slot < cap) {
-                    uint32_t i, j;
-                    cond_ij(t0 + e, n, i, j);
-                    out_ij[2 * slot] = perm[i];
-                    out_ij[2 * slot + 1] = perm[j];
-                    out_l[slot] = lidx[e];
-                }
+                uint32_t i, j;
+                cond_ij(t0 + e, n, i, j);
+                out_ij[2 * slot] = perm[i];
+                out_ij[2 * slot + 1] = perm[j];
+                out_l[slot] = lidx[e];
                 slot++;
             }
         }
     }
     if (bad) atomicOr(flags, 1u);
+    if (!WRITE) {
+        atomicAdd(&s_n, mine);
+        __syncthreads();
+        if (threadIdx.x == 0) wg_count[blockIdx.x] = s_n;
+    }
 }
 
 int sparse_pairs_impl(drephip_ctx *ctx, const uint16_t *d_common, const uint16_t *d_denom, uint32_t n,
@@ -733,39 +747,50 @@ int sparse_pairs_impl(drephip_ctx *ctx, const uint16_t *d_common, const uint16_t
     const uint64_t np = (uint64_t)n * (n - 1) / 2;
     double *d_lut;
     int32_t *d_off;
-    uint32_t *d_perm, *d_ij, *d_l, *d_flags;
-    unsigned long long *d_cnt;
-    struct Head { unsigned long long cnt; uint32_t flags, pad; } *h_head;
+    uint32_t *d_perm, *d_ij, *d_l, *d_flags, *d_cnt, *h_cnt, *h_flags;
+    uint64_t *d_wgoff, *h_wgoff;
     int rc;
+    const uint64_t nchunk = (np + 7) / 8;
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kSpGrid, (nchunk + kSpWG - 1) / kSpWG));
     if ((rc = scratch(ctx, "lk_lut", lut_len * 8ull, (void **)&d_lut))) return rc;
     if ((rc = scratch(ctx, "lk_off", (s + 1) * 4ull, (void **)&d_off))) return rc;
     if ((rc = scratch(ctx, "lk_perm", n * 4ull, (void **)&d_perm))) return rc;
-    if ((rc = scratch(ctx, "lk_sp_head", 16, (void **)&d_cnt))) return rc;
-    d_flags = (uint32_t *)(d_cnt + 1);
-    if ((rc = scratch(ctx, "lk_sp_ij", std::max<uint64_t>(cap, 1) * 8, (void **)&d_ij))) return rc;
-    if ((rc = scratch(ctx, "lk_sp_l", std::max<uint64_t>(cap, 1) * 4, (void **)&d_l))) return rc;
-    if ((rc = pinned_host(ctx, "lk_sp_head", sizeof(Head), (void **)&h_head))) return rc;
+    if ((rc = scratch(ctx, "lk_sp_cnt", (kSpGrid + 1) * 4ull, (void **)&d_cnt))) return rc;
+    if ((rc = scratch(ctx, "lk_sp_off", kSpGrid * 8ull, (void **)&d_wgoff))) return rc;
+    if ((rc = pinned_host(ctx, "lk_sp_cnt", (kSpGrid + 1) * 4ull, (void **)&h_cnt))) return rc;
+    if ((rc = pinned_host(ctx, "lk_sp_off", kSpGrid * 8ull, (void **)&h_wgoff))) return rc;
+    d_flags = d_cnt + kSpGrid;
+    h_flags = h_cnt + kSpGrid;
     HIPC(hipMemcpyAsync(d_lut, lut, lut_len * 8ull, hipMemcpyHostToDevice, st));
     HIPC(hipMemcpyAsync(d_off, lut_off, (s + 1) * 4ull, hipMemcpyHostToDevice, st));
     HIPC(hipMemcpyAsync(d_perm, perm, n * 4ull, hipMemcpyHostToDevice, st));
-    HIPC(hipMemsetAsync(d_cnt, 0, 16, st));
-    const uint64_t nchunk = (np + 7) / 8;
-    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, (nchunk + kSpWG - 1) / kSpWG));
+    HIPC(hipMemsetAsync(d_flags, 0, 4, st));
     timing_mark(ctx, 3, st, true);
-    hipLaunchKernelGGL(k_sparse_pairs, dim3(grid), dim3(kSpWG), 0, st, d_common, d_denom, np, n, s, d_lut, d_off,
-                       d_perm, cap, d_ij, d_l, d_cnt, d_flags);
+    hipLaunchKernelGGL(k_sparse_pairs<false>, dim3(grid), dim3(kSpWG), 0, st, d_common, d_denom, np, n, s, d_lut,
+                       d_off, d_perm, d_cnt, (const uint64_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                       d_flags);
     timing_mark(ctx, 3, st, false);
     HIPC(hipGetLastError());
-    HIPC(hipMemcpyAsync(h_head, d_cnt, sizeof(Head), hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(h_cnt, d_cnt, (kSpGrid + 1) * 4ull, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));
-    *np_out = h_head->cnt;
-    *flags_out = h_head->flags;
-    if (h_head->flags || h_head->cnt > cap || h_head->cnt == 0) return DREPHIP_OK;
-    // pinned, grow-only: 60 MB at n = 10^5 (configs[3]), kept for the next call
-    if ((rc = pinned_host(ctx, "lk_sp_ij", h_head->cnt * 8, (void **)h_ij))) return rc;
-    if ((rc = pinned_host(ctx, "lk_sp_l", h_head->cnt * 4, (void **)h_lidx))) return rc;
-    HIPC(hipMemcpyAsync(*h_ij, d_ij, h_head->cnt * 8, hipMemcpyDeviceToHost, st));
-    HIPC(hipMemcpyAsync(*h_lidx, d_l, h_head->cnt * 4, hipMemcpyDeviceToHost, st));
+    uint64_t total = 0;
+    for (uint32_t b = 0; b < grid; b++) { h_wgoff[b] = total; total += h_cnt[b]; }
+    *np_out = total;
+    *flags_out = *h_flags;
+    if (*h_flags || total > cap || total == 0) return DREPHIP_OK;
+    if ((rc = scratch(ctx, "lk_sp_ij", total * 8, (void **)&d_ij))) return rc;
+    if ((rc = scratch(ctx, "lk_sp_l", total * 4, (void **)&d_l))) return rc;
+    HIPC(hipMemcpyAsync(d_wgoff, h_wgoff, grid * 8ull, hipMemcpyHostToDevice, st));
+    timing_mark(ctx, 3, st, true);
+    hipLaunchKernelGGL(k_sparse_pairs<true>, dim3(grid), dim3(kSpWG), 0, st, d_common, d_denom, np, n, s, d_lut,
+                       d_off, d_perm, (uint32_t *)nullptr, d_wgoff, d_ij, d_l, d_flags);
+    timing_mark(ctx, 3, st, false);
+    HIPC(hipGetLastError());
+    // pinned, grow-only: 60 MB at 5x10^6 pairs, kept for the next call
+    if ((rc = pinned_host(ctx, "lk_sp_ij", total * 8, (void **)h_ij))) return rc;
+    if ((rc = pinned_host(ctx, "lk_sp_l", total * 4, (void **)h_lidx))) return rc;
+    HIPC(hipMemcpyAsync(*h_ij, d_ij, total * 8, hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(*h_lidx, d_l, total * 4, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));
     return DREPHIP_OK;
 }
