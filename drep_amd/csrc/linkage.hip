@@ -35,7 +35,10 @@
 
 namespace drephip {
 
-constexpr int kLkWG = 256;
+#ifndef DREPHIP_LK_WG
+#define DREPHIP_LK_WG 256
+#endif
+constexpr int kLkWG = DREPHIP_LK_WG;
 
 static double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -463,8 +466,10 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     // at 4 -- profiles/r03_linkage_grid_density.txt).  DREPHIP_LINK_PER_LANE
     // overrides it (the tests cover 1, 4 and 16: several passes)
     const char *pl = getenv("DREPHIP_LINK_PER_LANE");
+    const char *tg = getenv("DREPHIP_LINK_TARGET_WG");                 // A/B runs only
+    const uint32_t kLkTarget = tg ? std::max(1, atoi(tg)) : 200;
     const uint32_t per = pl ? std::max(1, std::min(64, atoi(pl)))
-                            : std::max(1u, (n + kLkWG * 200 - 1) / (kLkWG * 200));
+                            : std::max(1u, (n + kLkWG * kLkTarget - 1) / (kLkWG * kLkTarget));
     const uint32_t grid = std::max(1u, std::min(1024u, (n + kLkWG * per - 1) / (kLkWG * per)));
     const int tpl = per <= 1 ? 1 : per <= 2 ? 2 : 4;          // entries per lane per pass
     int32_t *d_size, *d_chain, *d_done;
