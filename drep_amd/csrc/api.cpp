@@ -840,24 +840,59 @@ static int linkage_condensed_sparse(drephip_ctx *ctx, const double *y, uint32_t 
     *rc = DREPHIP_OK;
     if (ctx->link_path == DREPHIP_LINK_PATH_DENSE) return 0;
     const double t0 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    // the pairs below 1.0, scanned by host threads over row ranges of equal
+    // pair counts; any value above 1.0 (or NaN) means no sparse form, more
+    // pairs than the cap means the dense path
+    const uint64_t np_all = (uint64_t)n * (n - 1) / 2, cap = sparse_pair_cap(ctx, n);
+    const unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<uint32_t> rb(T + 1, n - 1);
+    rb[0] = 0;
+    for (unsigned k = 1; k < T; k++) {             // first row whose pairs start at or after k/T of all
+        const uint64_t target = np_all * k / T;
+        uint32_t lo = rb[k - 1], hi = n - 1;
+        while (lo < hi) {
+            const uint32_t mid = lo + (hi - lo) / 2;
+            if ((uint64_t)mid * n - (uint64_t)mid * (mid + 1) / 2 < target) lo = mid + 1; else hi = mid;
+        }
+        rb[k] = lo;
+    }
+    std::vector<std::vector<uint32_t>> qi(T), qj(T);
+    std::vector<std::vector<double>> qv(T);
+    std::atomic<int> above(0);
+    std::atomic<uint64_t> found(0);
+    {
+        std::vector<std::thread> pool;
+        for (unsigned k = 0; k < T; k++)
+            pool.emplace_back([&, k] {
+                uint64_t t = (uint64_t)rb[k] * n - (uint64_t)rb[k] * (rb[k] + 1) / 2;
+                for (uint32_t a = rb[k]; a < rb[k + 1] && !above.load(std::memory_order_relaxed); a++) {
+                    uint64_t local = 0;
+                    for (uint32_t b = a + 1; b < n; b++, t++) {
+                        const double d = y[t];
+                        if (!(d <= 1.0)) { above = 1; return; }
+                        if (d < 1.0) { qi[k].push_back(a); qj[k].push_back(b); qv[k].push_back(d); local++; }
+                    }
+                    if (found.fetch_add(local) + local > cap) return;     // dense path; stop early
+                }
+            });
+        for (auto &th : pool) th.join();
+    }
+    if (above) {
+        if (ctx->link_path == DREPHIP_LINK_PATH_SPARSE) { set_error("sparse linkage: a distance above 1.0 or NaN"); *rc = DREPHIP_ERR_ARG; }
+        return 0;
+    }
+    if (found.load() > cap) {
+        if (ctx->link_path == DREPHIP_LINK_PATH_SPARSE) { set_error("sparse linkage: more pairs below 1.0 than the pair list holds"); *rc = DREPHIP_ERR_UNSUPPORTED; }
+        return 0;
+    }
     std::vector<uint32_t> pi, pj;
     std::vector<double> pv;
-    uint64_t t = 0;
-    for (uint32_t a = 0; a + 1 < n; a++)
-        for (uint32_t b = a + 1; b < n; b++, t++) {
-            const double d = y[t];
-            if (!(d <= 1.0)) {
-                if (ctx->link_path == DREPHIP_LINK_PATH_SPARSE) { set_error("sparse linkage: a distance above 1.0 or NaN"); *rc = DREPHIP_ERR_ARG; }
-                return 0;
-            }
-            if (d < 1.0) {
-                if (pi.size() >= sparse_pair_cap(ctx, n)) {
-                    if (ctx->link_path == DREPHIP_LINK_PATH_SPARSE) { set_error("sparse linkage: more pairs below 1.0 than the pair list holds"); *rc = DREPHIP_ERR_UNSUPPORTED; }
-                    return 0;
-                }
-                pi.push_back(a); pj.push_back(b); pv.push_back(d);
-            }
-        }
+    pi.reserve(found.load()); pj.reserve(found.load()); pv.reserve(found.load());
+    for (unsigned k = 0; k < T; k++) {
+        pi.insert(pi.end(), qi[k].begin(), qi[k].end());
+        pj.insert(pj.end(), qj[k].begin(), qj[k].end());
+        pv.insert(pv.end(), qv[k].begin(), qv[k].end());
+    }
     const double t1 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
     const int r = linkage_sparse_impl(n, pi.size(), pi.data(), pj.data(), pv.data(), method, sparse_cells(ctx),
                                       sparse_maxcomp(ctx), Z, &ctx->link.sp);

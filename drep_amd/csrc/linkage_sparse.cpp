@@ -102,10 +102,11 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 struct ActiveList {
     std::vector<uint32_t> nx, pv;
     uint32_t n;
-    explicit ActiveList(uint32_t n_) : nx(n_ + 1), pv(n_ + 1), n(n_) {
-        for (uint32_t i = 0; i <= n; i++) { nx[i] = i == n ? 0 : i + 1; pv[i] = i == 0 ? n : i - 1; }
-        nx[n] = n ? 0 : n; pv[0] = n;
-        if (n) pv[n] = n - 1;
+    explicit ActiveList(uint32_t n_) : nx(n_ + 1), pv(n_ + 1), n(n_) {   // 0 .. n-1 linked, n the sentinel
+        for (uint32_t i = 0; i <= n; i++) {
+            nx[i] = i == n ? 0 : i + 1;
+            pv[i] = i == 0 ? n : i - 1;
+        }
     }
     uint32_t first() const { return nx[n]; }
     uint32_t after(uint32_t i) const { return nx[i]; }
