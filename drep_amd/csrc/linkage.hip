@@ -35,10 +35,11 @@
 
 namespace drephip {
 
-#ifndef DREPHIP_LK_WG
-#define DREPHIP_LK_WG 256
-#endif
-constexpr int kLkWG = DREPHIP_LK_WG;
+// step workgroups: 256 lanes, or 128 for n <= kLkSmallN (more workgroups
+// per row at small n: 136 vs 143 ms of chain at n = 10^4; 256 is faster at
+// 10^5 -- profiles/r03_linkage_wg_ab.txt)
+constexpr int kLkWG = 256;
+constexpr uint32_t kLkSmallN = 30000;
 
 static double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -61,9 +62,10 @@ __device__ __forceinline__ double lw_update(int method, double dxi, double dyi, 
 }
 
 // Block argmin (smallest index among equal minima); result valid in thread 0.
+template <int WG>
 __device__ MinIdx block_argmin(double v, int32_t i) {
-    __shared__ double sv[kLkWG / 64];
-    __shared__ int32_t si[kLkWG / 64];
+    __shared__ double sv[WG / 64];
+    __shared__ int32_t si[WG / 64];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const double ov = __shfl_xor(v, o, 64);
@@ -75,7 +77,7 @@ __device__ MinIdx block_argmin(double v, int32_t i) {
     __syncthreads();
     MinIdx r{INFINITY, 0x7fffffff};
     if (threadIdx.x == 0)
-        for (int k = 0; k < kLkWG / 64; k++)
+        for (int k = 0; k < WG / 64; k++)
             if (better(sv[k], si[k], r.v, r.i)) { r.v = sv[k]; r.i = si[k]; }
     return r;
 }
@@ -128,6 +130,7 @@ struct alignas(64) LinkState {
 };
 
 // all partials of the previous kernel -> their minimum (thread 0)
+template <int WG>
 __device__ __forceinline__ MinIdx read_partials(const MinIdx *parts, uint32_t G) {
     double bv = INFINITY;
     int32_t bi = 0x7fffffff;
@@ -135,7 +138,7 @@ __device__ __forceinline__ MinIdx read_partials(const MinIdx *parts, uint32_t G)
         const MinIdx m = parts[b];
         if (better(m.v, m.i, bv, bi)) { bv = m.v; bi = m.i; }
     }
-    return block_argmin(bv, bi);
+    return block_argmin<WG>(bv, bi);
 }
 
 // The decision's operands -- D[top][below], the two sizes and the chain
@@ -152,8 +155,8 @@ struct alignas(64) LinkFwd {
     int32_t szt, szb, c3, c4;
 };
 
-template <int kLkPer>
-__global__ __launch_bounds__(kLkWG) void k_nn_step(double *__restrict__ D, uint32_t n, int method,
+template <int WG, int kLkPer>
+__global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t n, int method,
                                                    int32_t *__restrict__ size, int32_t *__restrict__ chain,
                                                    LinkState *__restrict__ st, LinkFwd *__restrict__ fwd,
                                                    MinIdx *__restrict__ parts, int32_t *__restrict__ done,
@@ -164,7 +167,7 @@ __global__ __launch_bounds__(kLkWG) void k_nn_step(double *__restrict__ D, uint3
     const LinkFwd F = fwd[q ^ 1];
     // the partials are read whether or not a decision is pending (valid memory
     // either way), so their loads are not held behind the state's
-    const MinIdx g = read_partials(parts + (uint64_t)(q ^ 1) * 1024, G);
+    const MinIdx g = read_partials<WG>(parts + (uint64_t)(q ^ 1) * 1024, G);
     if (S.k >= (int32_t)n - 1) return;                         // all merged
     const bool w0 = blockIdx.x == 0;
     // size of cluster i as of the previous decision: workgroup 0 writes that
@@ -249,8 +252,8 @@ __global__ __launch_bounds__(kLkWG) void k_nn_step(double *__restrict__ D, uint3
     const double dxt = pend ? Dx[t] : 0.0, dyt = pend ? Dy[t] : 0.0;
     double bv = INFINITY;
     int32_t bi = 0x7fffffff;
-    const uint32_t stride = G * kLkWG;
-    for (uint32_t i0 = blockIdx.x * kLkWG + threadIdx.x; i0 < n; i0 += kLkPer * stride) {
+    const uint32_t stride = G * WG;
+    for (uint32_t i0 = blockIdx.x * WG + threadIdx.x; i0 < n; i0 += kLkPer * stride) {
         int32_t sz[kLkPer];
         double dt[kLkPer], dx[kLkPer], dy[kLkPer];
 #pragma unroll
@@ -287,12 +290,12 @@ __global__ __launch_bounds__(kLkWG) void k_nn_step(double *__restrict__ D, uint3
             if (v < bv) { bv = v; bi = (int32_t)i; }
         }
     }
-    const MinIdx part = block_argmin(bv, bi);
+    const MinIdx part = block_argmin<WG>(bv, bi);
     if (threadIdx.x == 0) parts[(uint64_t)q * 1024 + blockIdx.x] = part;
 }
 
-template <int kLkPer>
-__global__ __launch_bounds__(kLkWG) void k_mst_step(const double *__restrict__ D, uint32_t n,
+template <int WG, int kLkPer>
+__global__ __launch_bounds__(WG) void k_mst_step(const double *__restrict__ D, uint32_t n,
                                                     int32_t *__restrict__ merged, double *__restrict__ Dmin,
                                                     LinkState *__restrict__ st, MinIdx *__restrict__ parts,
                                                     int32_t *__restrict__ done, double *__restrict__ Z, uint32_t q) {
@@ -300,7 +303,7 @@ __global__ __launch_bounds__(kLkWG) void k_mst_step(const double *__restrict__ D
     __shared__ int32_t s_ov;
     const LinkState S = st[q ^ 1];
     const uint32_t G = gridDim.x;
-    const MinIdx g = read_partials(parts + (uint64_t)(q ^ 1) * 1024, G);     // unconditional: not held behind S
+    const MinIdx g = read_partials<WG>(parts + (uint64_t)(q ^ 1) * 1024, G);     // unconditional: not held behind S
     if (S.k >= (int32_t)n - 1) return;
     if (threadIdx.x == 0) {
         LinkState X = S;
@@ -335,8 +338,8 @@ __global__ __launch_bounds__(kLkWG) void k_mst_step(const double *__restrict__ D
     const double *Dx = D + (uint64_t)x * n;
     double bv = INFINITY;
     int32_t bi = 0x7fffffff;
-    const uint32_t stride = G * kLkWG;
-    for (uint32_t i0 = blockIdx.x * kLkWG + threadIdx.x; i0 < n; i0 += kLkPer * stride) {
+    const uint32_t stride = G * WG;
+    for (uint32_t i0 = blockIdx.x * WG + threadIdx.x; i0 < n; i0 += kLkPer * stride) {
         int32_t mg[kLkPer];
         double dx[kLkPer], dm[kLkPer];
 #pragma unroll
@@ -356,7 +359,7 @@ __global__ __launch_bounds__(kLkWG) void k_mst_step(const double *__restrict__ D
             if (m < bv) { bv = m; bi = (int32_t)i; }
         }
     }
-    const MinIdx part = block_argmin(bv, bi);
+    const MinIdx part = block_argmin<WG>(bv, bi);
     if (threadIdx.x == 0) parts[(uint64_t)q * 1024 + blockIdx.x] = part;
 }
 
@@ -470,7 +473,8 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     const uint32_t kLkTarget = tg ? std::max(1, atoi(tg)) : 200;
     const uint32_t per = pl ? std::max(1, std::min(64, atoi(pl)))
                             : std::max(1u, (n + kLkWG * kLkTarget - 1) / (kLkWG * kLkTarget));
-    const uint32_t grid = std::max(1u, std::min(1024u, (n + kLkWG * per - 1) / (kLkWG * per)));
+    const uint32_t wg = n <= kLkSmallN && !pl ? 128 : kLkWG;
+    const uint32_t grid = std::max(1u, std::min(1024u, (n + wg * per - 1) / (wg * per)));
     const int tpl = per <= 1 ? 1 : per <= 2 ? 2 : 4;          // entries per lane per pass
     int32_t *d_size, *d_chain, *d_done;
     double *d_Z, *d_Dmin;
@@ -519,15 +523,24 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     static_assert(kBatch % 2 == 0, "step parity must restart at 0 with every replay");
     for (int b = 0; b < kBatch; b++) {
         const uint32_t q = (uint32_t)(b & 1);
-        if (mst) {
-            if (tpl == 1) hipLaunchKernelGGL(k_mst_step<1>, dim3(grid), dim3(kLkWG), 0, st, d_D, n, d_size, d_Dmin, d_st, d_parts, d_done, d_Z, q);
-            else if (tpl == 2) hipLaunchKernelGGL(k_mst_step<2>, dim3(grid), dim3(kLkWG), 0, st, d_D, n, d_size, d_Dmin, d_st, d_parts, d_done, d_Z, q);
-            else hipLaunchKernelGGL(k_mst_step<4>, dim3(grid), dim3(kLkWG), 0, st, d_D, n, d_size, d_Dmin, d_st, d_parts, d_done, d_Z, q);
+        const dim3 gm(grid), gn(grid + 1), blk(wg);
+#define DREPHIP_LK_LAUNCH(W, P)                                                                                      \
+    do {                                                                                                         \
+        if (mst) hipLaunchKernelGGL((k_mst_step<W, P>), gm, blk, 0, st, d_D, n, d_size, d_Dmin, d_st, d_parts, d_done, \
+                                    d_Z, q);                                                                     \
+        else hipLaunchKernelGGL((k_nn_step<W, P>), gn, blk, 0, st, d_D, n, method, d_size, d_chain, d_st, d_fwd,    \
+                                d_parts, d_done, d_Z, q);                                                        \
+    } while (0)
+        if (wg == 128) {
+            if (tpl == 1) DREPHIP_LK_LAUNCH(128, 1);
+            else if (tpl == 2) DREPHIP_LK_LAUNCH(128, 2);
+            else DREPHIP_LK_LAUNCH(128, 4);
         } else {
-            if (tpl == 1) hipLaunchKernelGGL(k_nn_step<1>, dim3(grid + 1), dim3(kLkWG), 0, st, d_D, n, method, d_size, d_chain, d_st, d_fwd, d_parts, d_done, d_Z, q);
-            else if (tpl == 2) hipLaunchKernelGGL(k_nn_step<2>, dim3(grid + 1), dim3(kLkWG), 0, st, d_D, n, method, d_size, d_chain, d_st, d_fwd, d_parts, d_done, d_Z, q);
-            else hipLaunchKernelGGL(k_nn_step<4>, dim3(grid + 1), dim3(kLkWG), 0, st, d_D, n, method, d_size, d_chain, d_st, d_fwd, d_parts, d_done, d_Z, q);
+            if (tpl == 1) DREPHIP_LK_LAUNCH(256, 1);
+            else if (tpl == 2) DREPHIP_LK_LAUNCH(256, 2);
+            else DREPHIP_LK_LAUNCH(256, 4);
         }
+#undef DREPHIP_LK_LAUNCH
     }
     HIPC(hipStreamEndCapture(st, &graph));
     hipError_t e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
