@@ -38,6 +38,9 @@
 
 namespace drephip {
 
+#ifndef DREPHIP_AP_MID
+#define DREPHIP_AP_MID 1          // first union-rank test one chunk into its group (ap_columns); 0: at the group start
+#endif
 constexpr int kApWG = 1024;                     // 16 waves per workgroup
 constexpr uint32_t kApCols = 128;               // columns per work item (fewer when the grid would not fill the chip)
 constexpr uint32_t kApMinCols = 16;             // one column per wave
@@ -474,17 +477,18 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
         // among the s smallest of A_r u B -- the rank rule (probe_rows) counts
         // nothing more, and |A u B| > s makes a partial pair's denominator s
         // whatever mrun the rest would add.  Tested for rows with no match so
-        // far, at the group starting at chunk kb1 (j0 = 64 kb1, about half the
-        // column, where unrelated sketches get there) and every later group:
-        // b0 > A_r[s - j0 - 1] (thr1 at kb1, thr2 at kb1 + 4: scalar, loaded
-        // with the row's largest hash) gives #{A_r < b0} >= s - j0, and thr2
-        // stays a sufficient bound at every later j0.  Scalar compares only (a
-        // sampled high-word read per row measured slower than the chunks it
-        // skipped).  With 4 rows the kb1 test ends only ~40 % of unrelated
-        // columns (B[512] > A_r[487] holds for ~79 % of rows at s = 1000); a
-        // third test inside that group, at chunk kb1 + 1, would end nearly all
-        // of them, but its registers (64 VGPRs) made the kernel 3-4 % slower
-        // than the chunks it saved (profiles/r03_allpairs_ab_*).
+        // far, one chunk into the group starting at chunk kb1 (j0 = 64 (kb1 + 1),
+        // just past half the column, where unrelated sketches get there) and
+        // at every later group start: b0 > A_r[s - j0 - 1] (thr1, thr2:
+        // scalar, loaded with the row's largest hash) gives #{A_r < b0} >=
+        // s - j0, and thr2 stays a sufficient bound at every later j0.  Scalar
+        // compares only (a sampled high-word read per row measured slower than
+        // the chunks it skipped).  At the group start itself (j0 = 64 kb1) the
+        // test ended only ~40 % of unrelated columns with 4 rows (B[512] >
+        // A_r[487] holds for ~79 % of rows at s = 1000); one chunk later it ends
+        // nearly all: N = 6000 2.67 -> 2.54 ms, 20000 29.1 -> 26.5 ms, same
+        // registers (profiles/r03_allpairs_ab_midtest.txt).  A SECOND test there
+        // (keeping the group-start one) cost 64 VGPRs and 3-4 %.
         const uint32_t kb1 = 4u * ((s / 2 + 255) / 256);
         auto past = [&](uint64_t bv, const uint64_t (&thr)[R]) {          // wave-uniform
             const uint64_t b0 = ((uint64_t)rfl((uint32_t)(bv >> 32)) << 32) | rfl((uint32_t)bv);
@@ -501,7 +505,11 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
                 // int: through uint32_t so the low word is not sign-extended)
                 const uint64_t b0 = ((uint64_t)rfl((uint32_t)(b >> 32)) << 32) | rfl((uint32_t)b);
                 if (b0 == kEmpty || b0 > amax) break;
+#if DREPHIP_AP_MID
+                if (kb > kb1 && past(b, thr2)) break;                      // wave-uniform
+#else
                 if (kb >= kb1 && past(b, kb == kb1 ? thr1 : thr2)) break;    // wave-uniform
+#endif
             }
             const uint32_t gofs = rfl(kb) * 512u;                        // the group's byte offset (SGPR)
 #pragma unroll
@@ -536,8 +544,16 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
                     if (u == 2) rg[u] = ld_chunk_at<(2 + kRing) * 512>(rc, lane_off, gofs);
                     if (u == 3) rg[u] = ld_chunk_at<(3 + kRing) * 512>(rc, lane_off, gofs);
                 }
+#if DREPHIP_AP_MID
+                // the first union-rank test one chunk into group kb1: B[64 (kb1 + 1)]
+                // against A_r[s - 64 (kb1 + 1) - 1] (thr1) after chunk kb1's probe
+                if (u == 0 && kb == kb1 && kb1 + 1 < nch && past(rg[1], thr1)) goto column_done;
+#endif
             }
         }
+#if DREPHIP_AP_MID
+    column_done:
+#endif
         if (lane == 0) {
             // the column's count is read only here: a scalar load left in flight
             // across the chunk loop would force every LDS wait there to lgkmcnt(0)
@@ -615,7 +631,8 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
         // groups, j0 = 64 kb1 and 64 (kb1 + 4); positions below 0 clamp to 0
         // (never used then: such a group does not exist or the test is moot)
         const uint32_t kb1 = 4u * ((s / 2 + 255) / 256);
-        const uint32_t p1 = s > 64 * kb1 ? s - 64 * kb1 - 1 : 0, p2 = s > 64 * (kb1 + 4) ? s - 64 * (kb1 + 4) - 1 : 0;
+        const uint32_t j1 = 64 * (kb1 + (DREPHIP_AP_MID ? 1 : 0));         // column position of the first test
+        const uint32_t p1 = s > j1 ? s - j1 - 1 : 0, p2 = s > 64 * (kb1 + 4) ? s - 64 * (kb1 + 4) - 1 : 0;
 #pragma unroll
         for (int r = 0; r < R; r++) {
             const uint32_t i = min(i0 + (uint32_t)r, row1 - 1);
@@ -638,7 +655,7 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
             alast[r] = (ok && nA[r] >= s) ? lraw[r] : kEmpty;
             // a threshold past the row's last element (partial row) or of a
             // group with j0 >= s never ends the scan (kEmpty: b0 > it is false)
-            thr1[r] = (ok && s > 64 * kb1 && p1 < nA[r]) ? t1raw[r] : kEmpty;
+            thr1[r] = (ok && s > j1 && p1 < nA[r]) ? t1raw[r] : kEmpty;
             thr2[r] = (ok && s > 64 * (kb1 + 4) && p2 < nA[r]) ? t2raw[r] : kEmpty;
             any_partial_row |= nA[r] < s;
             zero_key |= ok && fraw[r] == 0;                  // the row holds the hash value 0 (MASKED probe)
