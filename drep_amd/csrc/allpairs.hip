@@ -487,8 +487,9 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
         // test ended only ~40 % of unrelated columns with 4 rows (B[512] >
         // A_r[487] holds for ~79 % of rows at s = 1000); one chunk later it ends
         // nearly all: N = 6000 2.67 -> 2.54 ms, 20000 29.1 -> 26.5 ms, same
-        // registers (profiles/r03_allpairs_ab_midtest.txt).  A SECOND test there
-        // (keeping the group-start one) cost 64 VGPRs and 3-4 %.
+        // registers (profiles/r03_allpairs_ab_midtest.txt).  Keeping the
+        // group-start test as well (same 52 VGPRs) is 5-8 % slower
+        // (profiles/r03_allpairs_ab_twotests.txt).
         const uint32_t kb1 = 4u * ((s / 2 + 255) / 256);
         auto past = [&](uint64_t bv, const uint64_t (&thr)[R]) {          // wave-uniform
             const uint64_t b0 = ((uint64_t)rfl((uint32_t)(bv >> 32)) << 32) | rfl((uint32_t)bv);
