@@ -96,7 +96,8 @@ def gather_segments(seg, N: int, root: int = 0, out=None):
                 continue
             lo = cond_start(a, N)
             if r == root:
-                full[lo:lo + sizes[r]].copy_(seg[:sizes[r]])
+                if seg.data_ptr() != full[lo:lo + sizes[r]].data_ptr():   # not already in place
+                    full[lo:lo + sizes[r]].copy_(seg[:sizes[r]])
             elif host_p2p:
                 buf = torch.empty(sizes[r], dtype=seg.dtype)
                 landing.append((full[lo:lo + sizes[r]], buf))
@@ -115,7 +116,7 @@ def gather_segments(seg, N: int, root: int = 0, out=None):
 
 
 SketchFn = Callable[[ShardPlan], Tuple["object", "object"]]            # -> (loc_h [nmax, s], loc_n [nmax])
-AllpairsFn = Callable[["object", "object", ShardPlan], Tuple["object", Optional["object"]]]
+AllpairsFn = Callable[..., Tuple["object", Optional["object"]]]      # fn(H, NH, plan, out=None)
 LinkageFn = Callable[["object", Optional["object"], int, str], np.ndarray]
 
 
@@ -151,8 +152,17 @@ def run_sharded(N: int, names: Sequence[str], s: int, sketch_fn: SketchFn, allpa
     H, NH = stage("allgather_s", lambda: gather_sketches(loc_h, loc_n))
     H, NH = H[:N], NH[:N]
     partial = bool((NH < s).any().item()) if N else False
-    seg_c, seg_d = stage("allpairs_s", lambda: allpairs_fn(H, NH, p))
-    full_c = stage("gather_segments_s", lambda: gather_segments(seg_c, N, root))
+    # the root's rows are written straight into its slice of the full condensed
+    # vector, so gathering the segments copies nothing on the root (at 10^5
+    # genomes on one GPU that was a 10 GB device copy plus its allocation)
+    full_c = None
+    out = None
+    if rank == root and N >= 2:
+        full_c = torch.empty(N * (N - 1) // 2, dtype=torch.int16, device=H.device)
+        lo = cond_start(p.r0, N)
+        out = full_c[lo:lo + p.seg_len]
+    seg_c, seg_d = stage("allpairs_s", lambda: allpairs_fn(H, NH, p, out=out))
+    full_c = stage("gather_segments_s", lambda: gather_segments(seg_c, N, root, out=full_c))
     full_d = None
     if partial:
         if seg_d is None:
@@ -284,8 +294,9 @@ def hip_allpairs(ctx, stream: int, device):
     """Stage 3: drephip_allpairs_device over this rank's rows, on its GPU."""
     import torch
 
-    def fn(H, NH, p: ShardPlan):
-        seg = torch.zeros(max(p.seg_len, 1), dtype=torch.int16, device=device)
+    def fn(H, NH, p: ShardPlan, out=None):
+        # `out`: where the segment goes (a slice of the root's full vector)
+        seg = out if out is not None and p.seg_len else torch.zeros(max(p.seg_len, 1), dtype=torch.int16, device=device)
         partial = bool((NH < ctx.s).any().item())
         segd = torch.zeros(max(p.seg_len, 1), dtype=torch.int16, device=device) if partial else None
         if p.seg_len:

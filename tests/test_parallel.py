@@ -113,7 +113,7 @@ def _worker_pipeline(rank, world, port, N, out_dir, partial):
             loc_n[:p.g1 - p.g0] = torch.from_numpy(nh.view(np.int32))
         return loc_h, loc_n
 
-    def allpairs_fn(H, NH, p):
+    def allpairs_fn(H, NH, p, out=None):
         Hn = H.numpy().view(np.uint64)
         Nn = NH.numpy().view(np.uint32)
         if not p.seg_len:
