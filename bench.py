@@ -11,8 +11,14 @@ value = N(N-1)/2 genome pairs / step time, whole job (all ranks; max over ranks)
 
 Default workload = BASELINE.json configs[1]: 1,000 synthetic 5 Mbp genomes,
 k=21, s=1000.  The same total workload is used at every GPU count (strong
-scaling).  Launch: `python bench.py` (1 GPU) or
-`python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`.
+scaling).  Launch: `python bench.py` (1 GPU), `python bench.py --gpus N`
+(starts N ranks itself, one per GPU, under torch.distributed.run as a child
+process) or `python -m torch.distributed.run --nproc-per-node N bench.py
+--gpus N`.
+
+Two throughputs: `value` is the whole step (sketch + exchange + all-pairs),
+end to end; `dist_pairs_per_s` is the metric's own quantity per SURVEY.md
+§8(d): pairs / all-pairs stage time with the sketches resident.
 """
 import argparse
 import json
@@ -159,7 +165,7 @@ def cpu_model():
     return None
 
 
-def cpu_baseline(args, threads):
+def cpu_baseline(args, threads, share):
     """The same whole job on the host with the C oracle (Mash-equivalent
     restatement, OpenMP): sketch every genome and `mash dist` every pair when
     that fits CPU_BUDGET_S of wall time (configs[1]: ~19 s on the GPU box's 16
@@ -195,7 +201,7 @@ def cpu_baseline(args, threads):
     per_genome = t_sk / ns
     per_pair = t_d / npairs
     job = N * per_genome + (N * (N - 1) / 2) * per_pair
-    visible = os.cpu_count() or threads
+    visible = share["visible_cpus"] or threads
     if ns == N and full:
         how = ("the whole job measured: sketch of all %d synthetic %d bp genomes in %.2f s + all %d pairs of "
                "mash dist in %.2f s" % (N, L, t_sk, npairs, t_d))
@@ -203,23 +209,27 @@ def cpu_baseline(args, threads):
         how = ("sketch of %d of the %d synthetic %d bp genomes in %.2f s + %d pairs of mash dist in %.2f s; job = "
                "%d x per-genome sketch + N(N-1)/2 x per-pair dist = %.1f s + %.2f s"
                % (ns, N, L, t_sk, npairs, t_d, N, N * per_genome, N * (N - 1) / 2 * per_pair))
-    return {
+    out = {
         "value": (N * (N - 1) / 2) / job,
         "unit": "genome pairs/s",
         "cores": threads,
         "kind": "port",
         "cpu_model": cpu_model(),
         "host_cpus_visible": visible,
-        "sample": "C oracle (Mash-equivalent restatement; Mash itself is absent), OpenMP %d threads = this job's "
-                  "host CPU share; %s" % (threads, how),
+        "sample": "C oracle (Mash-equivalent restatement; Mash itself is absent), OpenMP on all %d host CPUs "
+                  "this job may use (mash dist -p <all host cores>, d_cluster.py:570); %s" % (threads, how),
+        "host_cpu_share": share,
         "measured_whole_job": bool(ns == N and full),
         "sketch_Mbp_per_s": ns * L / t_sk / 1e6,
         "dist_pairs_per_s": npairs / t_d,
-        # mash dist -p <all host cores>: the measured per-thread rate times the
-        # host's visible CPUs (linear scaling assumed; both legs are embarrassingly
-        # parallel), stated next to the measured share
-        "value_all_host_cpus_extrapolated": (N * (N - 1) / 2) / job * visible / threads,
     }
+    if visible > threads:
+        # the machine has more CPUs than this job may use: the measured rate
+        # scaled linearly to all of them, labelled as an extrapolation
+        out["value_all_visible_cpus_extrapolated"] = (N * (N - 1) / 2) / job * visible / threads
+        out["extrapolation_note"] = ("%d of %d visible CPUs are this job's share; linear scaling assumed"
+                                     % (threads, visible))
+    return out
 
 
 def check_against_oracle(args, loc_h, loc_n, d_common, g0, nloc, N, r0, r1, world, gather_sketches):
@@ -275,30 +285,78 @@ def check_against_oracle(args, loc_h, loc_n, d_common, g0, nloc, N, r0, r1, worl
         res["mismatches"] += bad
     if world > 1:
         import torch.distributed as dist
-        flag = torch.tensor([1 if ok else 0, res["genomes"], res["pairs"], res["mismatches"]], dtype=torch.int64,
-                            device=loc_h.device)
-        f2 = flag.clone()
-        dist.all_reduce(flag[:1], op=dist.ReduceOp.MIN)
-        dist.all_reduce(f2[1:], op=dist.ReduceOp.SUM)
-        ok = bool(flag[0].item())
-        res.update(genomes=int(f2[1].item()), pairs=int(f2[2].item()), mismatches=int(f2[3].item()))
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int64, device=loc_h.device)
+        tot = torch.tensor([res["genomes"], res["pairs"], res["mismatches"]], dtype=torch.int64,
+                           device=loc_h.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        ok = bool(flag.item())
+        res.update(genomes=int(tot[0].item()), pairs=int(tot[1].item()), mismatches=int(tot[2].item()))
     res["verified"] = bool(ok)
     return res
 
 
+def launch_ranks(args):
+    """`--gpus N` without torch.distributed.run around us: start N ranks (one
+    per GPU) as a child `python -m torch.distributed.run` on 127.0.0.1 -- a
+    child process, started before this process touches the GPU -- and return
+    its exit code.  Rank 0 prints the JSON line to the inherited stdout."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    print("bench: starting %d ranks: %s" % (args.gpus, " ".join(cmd)), file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1")).returncode
+
+
+def host_cpu_share():
+    """The host CPUs this job may use: the CPU affinity mask, capped by a
+    cgroup v2 CPU quota (cpu.max) and by OMP_NUM_THREADS when either is set
+    (the GPU box gives a one-GPU job 16 of the visible CPUs)."""
+    import math
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None
+    cores = aff
+    if quota:
+        cores = min(cores, max(1, math.floor(quota)))
+    if omp:
+        cores = min(cores, omp)
+    return cores, {"affinity_cpus": aff, "cgroup_cpu_quota": quota, "omp_num_threads": omp,
+                   "visible_cpus": os.cpu_count()}
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args)
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        print("bench: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world), file=sys.stderr)
+        return 2
     import torch
     import torch.distributed as dist
+    backend = os.environ.get("DREPHIP_DIST_BACKEND", "nccl")          # nccl = RCCL over xGMI
+    if world > 1 and backend == "nccl" and world > torch.cuda.device_count():
+        # RCCL needs one GPU per rank (gloo may share one, for rehearsals)
+        print("bench: %d ranks over RCCL but %d GPUs visible" % (world, torch.cuda.device_count()), file=sys.stderr)
+        return 2
     # one rank per GPU; ranks beyond the visible GPUs wrap (only for rehearsing
     # the multi-rank path on a smaller box, with DREPHIP_DIST_BACKEND=gloo)
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        backend = os.environ.get("DREPHIP_DIST_BACKEND", "nccl")          # nccl = RCCL over xGMI
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -578,17 +636,24 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline:
-        # the host CPUs this job may use: OMP_NUM_THREADS (the GPU box sets it to
-        # the job's share, 16 per GPU), else every visible CPU
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-        cpu = cpu_baseline(args, max(1, threads))
+        # `mash dist -p <all host cores>` (d_cluster.py:570): every CPU this
+        # job may use (affinity, cgroup quota, OMP_NUM_THREADS)
+        threads, share = host_cpu_share()
+        cpu = cpu_baseline(args, threads, share)
 
     if rank == 0:
         out = {
             "metric": "genome pairs/sec (mash dist, k=21 s=1000) + sketch GB/s, at 1/2/4/8 GPUs",
             "value": value,
             "unit": "genome pairs/s",
+            "value_kind": "end to end: N(N-1)/2 / whole step (sketch + sketch exchange + all-pairs), inputs in HBM",
+            "dist_pairs_per_s": pairs / (stage["dist"] / K) if stage["dist"] else None,
+            "dist_pairs_per_s_kind": "the metric's quantity (SURVEY.md 8(d)): N(N-1)/2 / all-pairs stage time "
+                                     "per step, sketches resident",
             "n_gpus": world,
+            "ranks_seen": dist.get_world_size() if world > 1 else 1,
+            "backend": (backend if world > 1 else None),
+            "rccl_version": rccl_version(torch) if world > 1 and backend == "nccl" else None,
             "steps": K,
             "warmup": args.warmup,
             "ms_per_step": ms_step,
@@ -665,5 +730,13 @@ def main():
         dist.destroy_process_group()
 
 
+def rccl_version(torch):
+    try:
+        v = torch.cuda.nccl.version()
+        return ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception as e:
+        return "unknown (%s)" % e
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

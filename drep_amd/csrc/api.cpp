@@ -844,7 +844,7 @@ static int linkage_condensed_sparse(drephip_ctx *ctx, const double *y, uint32_t 
     // pair counts; any value above 1.0 (or NaN) means no sparse form, more
     // pairs than the cap means the dense path
     const uint64_t np_all = (uint64_t)n * (n - 1) / 2, cap = sparse_pair_cap(ctx, n);
-    const unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const unsigned T = host_threads();
     std::vector<uint32_t> rb(T + 1, n - 1);
     rb[0] = 0;
     for (unsigned k = 1; k < T; k++) {             // first row whose pairs start at or after k/T of all
@@ -869,7 +869,9 @@ static int linkage_condensed_sparse(drephip_ctx *ctx, const double *y, uint32_t 
                     uint64_t local = 0;
                     for (uint32_t b = a + 1; b < n; b++, t++) {
                         const double d = y[t];
-                        if (!(d <= 1.0)) { above = 1; return; }
+                        // above 1.0, NaN or negative: no sparse form (scipy takes negative
+                        // values; the dense path does too)
+                        if (!(d <= 1.0) || d < 0.0) { above = 1; return; }
                         if (d < 1.0) { qi[k].push_back(a); qj[k].push_back(b); qv[k].push_back(d); local++; }
                     }
                     if (found.fetch_add(local) + local > cap) return;     // dense path; stop early
@@ -878,7 +880,7 @@ static int linkage_condensed_sparse(drephip_ctx *ctx, const double *y, uint32_t 
         for (auto &th : pool) th.join();
     }
     if (above) {
-        if (ctx->link_path == DREPHIP_LINK_PATH_SPARSE) { set_error("sparse linkage: a distance above 1.0 or NaN"); *rc = DREPHIP_ERR_ARG; }
+        if (ctx->link_path == DREPHIP_LINK_PATH_SPARSE) { set_error("sparse linkage: a distance above 1.0, below 0 or NaN"); *rc = DREPHIP_ERR_ARG; }
         return 0;
     }
     if (found.load() > cap) {

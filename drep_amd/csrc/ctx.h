@@ -200,6 +200,9 @@ int sparse_pairs_impl(drephip_ctx *ctx, const uint16_t *d_common, const uint16_t
 int linkage_sparse_impl(uint32_t n, uint64_t np, const uint32_t *pi, const uint32_t *pj, const double *pv,
                         int method, uint64_t max_cells, uint32_t max_comp, double *Z_out, SparseLinkInfo *info);
 void sort_and_label(std::vector<double> &Z, uint32_t n);
+// host worker threads of the linkage paths: OMP_NUM_THREADS if set, else the
+// hardware threads, at most 16
+unsigned host_threads();
 
 // Host ingest (ingest.cpp).
 // std::allocator that leaves new elements uninitialised (resize() without the

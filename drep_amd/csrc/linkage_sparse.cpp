@@ -260,7 +260,7 @@ void prim_component(const Comp &C, const uint32_t *members, const double *mat, d
 
 }  // namespace
 
-static unsigned host_threads() {
+unsigned host_threads() {
     unsigned t = std::thread::hardware_concurrency();
     if (const char *e = std::getenv("OMP_NUM_THREADS")) t = (unsigned)std::max(1, atoi(e));
     return std::max(1u, std::min(t, 16u));

@@ -115,6 +115,8 @@ def gather_segments(seg, N: int, root: int = 0, out=None):
     return full
 
 
+POISON = 0x7FFF        # an impossible shared-hash count (s <= 12000)
+
 SketchFn = Callable[[ShardPlan], Tuple["object", "object"]]            # -> (loc_h [nmax, s], loc_n [nmax])
 AllpairsFn = Callable[..., Tuple["object", Optional["object"]]]      # fn(H, NH, plan, out=None)
 LinkageFn = Callable[["object", Optional["object"], int, str], np.ndarray]
@@ -157,12 +159,22 @@ def run_sharded(N: int, names: Sequence[str], s: int, sketch_fn: SketchFn, allpa
     # genomes on one GPU that was a 10 GB device copy plus its allocation)
     full_c = None
     out = None
+    # DREPHIP_SEGMENT_POISON=1 (tests): the root's vector starts as POISON, a
+    # value no count takes (s <= 12000), and no pair may still hold it after the
+    # gather -- every kernel path must write every pair of its rows
+    poison = os.environ.get("DREPHIP_SEGMENT_POISON") == "1"
     if rank == root and N >= 2:
-        full_c = torch.empty(N * (N - 1) // 2, dtype=torch.int16, device=H.device)
+        npairs = N * (N - 1) // 2
+        full_c = (torch.full((npairs,), POISON, dtype=torch.int16, device=H.device) if poison
+                  else torch.empty(npairs, dtype=torch.int16, device=H.device))
         lo = cond_start(p.r0, N)
         out = full_c[lo:lo + p.seg_len]
     seg_c, seg_d = stage("allpairs_s", lambda: allpairs_fn(H, NH, p, out=out))
     full_c = stage("gather_segments_s", lambda: gather_segments(seg_c, N, root, out=full_c))
+    if poison and full_c is not None:
+        left = int((full_c == POISON).sum().item())
+        if left:
+            raise RuntimeError("%d pairs of the condensed vector were never written" % left)
     full_d = None
     if partial:
         if seg_d is None:
@@ -330,6 +342,37 @@ def hip_linkage(ctx, names: Sequence[str], stream: int):
     return fn
 
 
+def start_linkage_reserve(link_ctx, N: int, s: int, device, record: Dict):
+    """Reserve the root's n x n f64 linkage matrix on a helper thread (80 GB at
+    10^5 genomes: ~2 s of hipMalloc once the process has cached memory, 0.5 ms
+    at its start), beside the sketch and all-pairs stages.  Skipped when it
+    would not leave the stages their HBM: the full sketch matrix, the condensed
+    counts (2 B per pair, twice with partial sketches) and a 4 GiB margin.  An
+    exception in the thread is recorded in `record['reserve_error']` (the job's
+    JSON line), not lost; the linkage then allocates the matrix itself.
+    Returns the started thread, or None when skipped."""
+    import threading
+    import torch
+    need = N * N * 8
+    stages = N * s * 8 + 4 * (N * (N - 1) // 2) + (4 << 30)
+    free, _ = torch.cuda.mem_get_info(device)
+    if need + stages > free:
+        record["reserve_skipped"] = ("matrix %.1f GB + stages %.1f GB > free HBM %.1f GB"
+                                     % (need / 1e9, stages / 1e9, free / 1e9))
+        return None
+
+    def run():
+        t0 = time.perf_counter()
+        try:
+            link_ctx.linkage_reserve(N)
+            record["reserve_s"] = time.perf_counter() - t0
+        except Exception as e:          # recorded; the linkage allocates on its own
+            record["reserve_error"] = "%s: %s" % (type(e).__name__, e)
+    t = threading.Thread(target=run, daemon=True)
+    t.start()
+    return t
+
+
 def synthetic_names(N: int) -> List[str]:
     """Genome names of the synthetic workload: sorting them keeps index order."""
     return ["synthetic_%07d.fna" % i for i in range(N)]
@@ -391,11 +434,10 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
     # allocated by a separate context on a helper thread while the sketch and
     # all-pairs stages run, so the serial clustering tail does not pay for it
     link_ctx, reserve = ctx, None
+    res_wait: Dict = {}
     if rank == 0 and N >= 2:
-        import threading
         link_ctx = _lib.Context(device=local, k=21, s=a.sketch, seed=42)
-        reserve = threading.Thread(target=link_ctx.linkage_reserve, args=(N,), daemon=True)
-        reserve.start()
+        reserve = start_linkage_reserve(link_ctx, N, a.sketch, dev, res_wait)
     linkage_fn = hip_linkage(link_ctx, names, stream)
     if reserve is not None:
         inner = linkage_fn
@@ -405,7 +447,6 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
             reserve.join()
             res_wait["reserve_wait_s"] = time.perf_counter() - t0
             return inner(*args)
-    res_wait = {}
     res = run_sharded(N, names, a.sketch, sketch_fn, hip_allpairs(ctx, stream, dev), linkage_fn,
                       a.method, a.P_ani, sync=lambda: torch.cuda.synchronize(dev))
     if from_files and world > 1:

@@ -803,13 +803,13 @@ def test_sketch_layout_cache_follows_layout_changes(ctx1000):
 @pytest.mark.parametrize("method", ["single", "complete", "average", "weighted"])
 @pytest.mark.parametrize("n,kind", [(2, "ties"), (3, "ties"), (17, "ties"), (257, "ties"), (300, "cont"),
                                     (64, "equal"), (400, "fewvals"), (1500, "mash"), (4500, "mash"),
-                                    (2100, "ties"), (700, "above1")])
+                                    (2100, "ties"), (700, "above1"), (300, "negative")])
 def test_gpu_linkage_matches_scipy(method, n, kind):
     """drephip_linkage == scipy.cluster.hierarchy.linkage bit for bit, with
     Mash-like ties (a few distinct distances, many 1.0), continuous values,
     all-equal distances, a few values whose Lance-Williams averages round
-    (fewvals), family structure with 1.0 between families (mash) and values
-    above 1.0 (no sparse form): the dense GPU path at three grid densities of
+    (fewvals), family structure with 1.0 between families (mash), values
+    above 1.0 and negative values (no sparse form; scipy accepts both): the dense GPU path at three grid densities of
     the chain-step kernel (16 entries per lane: several passes), and the
     automatic choice (the sparse path wherever no value exceeds 1.0)."""
     import scipy.cluster.hierarchy as sch
@@ -830,6 +830,8 @@ def test_gpu_linkage_matches_scipy(method, n, kind):
         y[same] = np.round(rng.random(int(same.sum())) * 0.2, 3)
     elif kind == "above1":
         y = rng.random(m) * 1.5
+    elif kind == "negative":
+        y = rng.random(m) - 0.3
     else:
         y = np.full(m, 0.5)
     Zs = sch.linkage(y, method=method)
@@ -846,12 +848,12 @@ def test_gpu_linkage_matches_scipy(method, n, kind):
         assert np.array_equal(Z, Zs), (per_lane, np.argwhere(Z != Zs)[:5])
     with _lib.Context(0, 21, S, 42) as ctx:
         Z = ctx.linkage(y, method)
-        if kind in ("mash", "above1"):          # small components / no sparse form
+        if kind in ("mash", "above1", "negative"):      # small components / no sparse form
             assert ctx.linkage_info()["sparse"] == (kind == "mash")
         assert np.array_equal(Z, Zs), ("auto", np.argwhere(Z != Zs)[:5])
         ctx.set_linkage_path(ctx.LINK_SPARSE)
-        if kind == "above1":
-            with pytest.raises(_lib.DrepHipError, match="above 1.0"):
+        if kind in ("above1", "negative"):
+            with pytest.raises(_lib.DrepHipError, match="above 1.0, below 0"):
                 ctx.linkage(y, method)
         else:
             Z = ctx.linkage(y, method)

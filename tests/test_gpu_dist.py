@@ -20,11 +20,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 N, L = 240, 300_000
 
 
-def _run(world, out, port):
-    env = dict(os.environ, DREPHIP_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+def _run(world, out, port, n=N, sketch=1000):
+    # the root's condensed vector starts poisoned: every pair must be written
+    env = dict(os.environ, DREPHIP_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1", DREPHIP_SEGMENT_POISON="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "drep_amd.distributed",
-           "--genomes", str(N), "--genome-bp", str(L), "--family-size", "20", "--out", out]
+           "--genomes", str(n), "--genome-bp", str(L), "--family-size", "20", "--sketch", str(sketch),
+           "--out", out]
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-3000:]
     return json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
@@ -52,6 +54,32 @@ def test_sharded_job_matches_single_rank(tmp_path):
         assert np.array_equal(cm.common, cm1.common)
         assert np.array_equal(pl["linkage"], pl1["linkage"])
         assert cdb.equals(cdb1)
+
+
+@pytest.mark.timeout(600)
+def test_sharded_job_band_path_matches_single_rank(tmp_path):
+    """s = 4096 (> 2048: the value-band kernel, configs[4]'s path): the root's
+    segment written in place into its slice of the full vector (out=), the
+    other rank's received into its slice; the vector starts poisoned and no
+    pair may keep the poison.  1 and 2 ranks give the same counts, Z and Cdb,
+    and rows of the counts equal the oracle's merge."""
+    n, s = 96, 4096
+    one = _run(1, str(tmp_path / "b1"), 29661, n=n, sketch=s)
+    two = _run(2, str(tmp_path / "b2"), 29671, n=n, sketch=s)
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+    cm1 = load_condensed(str(tmp_path / "b1"), mmap=False)
+    cm2 = load_condensed(str(tmp_path / "b2"), mmap=False)
+    assert np.array_equal(cm1.common, cm2.common)
+    assert np.array_equal(load_primary_linkage(str(tmp_path / "b1"))["linkage"],
+                          load_primary_linkage(str(tmp_path / "b2"))["linkage"])
+    assert pd.read_csv(tmp_path / "b1" / "primary_Cdb.csv").equals(pd.read_csv(tmp_path / "b2" / "primary_Cdb.csv"))
+    h, nh = oracle.sketch_synth(0, n, L, seed=0xD2E9, family_size=20, s=s, threads=8)
+    assert np.array_equal(cm1.nhash, nh)
+    # the first rows (rank 0's in-place segment) and the last rows (rank 1's)
+    for r0, r1 in ((0, 4), (n - 6, n - 1)):
+        want, _ = oracle.allpairs(h, nh, s, r0=r0, r1=r1, threads=8)
+        a = r0 * n - r0 * (r0 + 1) // 2
+        assert np.array_equal(cm2.common[a:a + len(want)], want), (r0, r1)
 
 
 def _file_set(tmp_path, copies=6):

@@ -19,10 +19,13 @@ Parity at full size:
     random), recomputed by the host oracle's Mash merge from the GPU sketches,
     bit-exact;
   * linkage Z: the sparse and the dense path bit-identical to each other (up
-    to 2x10^4 genomes); n-1 merges, monotone heights, consistent sizes; at 10^4 also
-    bit-identical to scipy's linkage on the host (reference call:
-    drep/d_cluster.py:453; ~1 s of host time).  At 10^5 the scipy comparison
-    (121 s of host time) runs only with DREPHIP_SCALE_SCIPY=1.
+    to 2x10^4 genomes); n-1 merges, monotone heights, consistent sizes; at
+    EVERY size bit-identical to scipy's linkage on the host (reference call:
+    drep/d_cluster.py:447-457: linkage, then fcluster at 1 - P_ani), and the
+    fcluster labels equal.  At 10^5 scipy takes ~2 min and ~80 GB of host
+    memory (the 40 GB condensed f64 vector and nn_chain's copy of it).  Z's
+    sha1 must also equal the digest committed for the workload in
+    tests/golden/scale_linkage_sha1.json (scipy's Z of the same counts).
 Timings go to DREPHIP_SCALE_OUT (default gpurun_out/scale_<N>[_s<s>].json).
 Reference knobs: MASH_sketch (drep/d_cluster.py:499; CLI -ms,
 drep/argumentParser.py:103); Mdb built at drep/d_cluster.py:575-596."""
@@ -43,7 +46,8 @@ pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # (genomes, sketch size, BASELINE.json config)
-CASES = [pytest.param(10_000, 1000, "BASELINE.json configs[2] (1 GPU)", id="10000"),
+CASES = [pytest.param(1_000, 1000, "BASELINE.json configs[1] (the bench workload)", id="1000"),
+         pytest.param(10_000, 1000, "BASELINE.json configs[2] (1 GPU)", id="10000"),
          pytest.param(100_000, 1000, "BASELINE.json configs[3] (1 GPU)", id="100000"),
          pytest.param(10_000, 10_000, "BASELINE.json configs[4] (1 GPU)", id="10000-s10000")]
 if os.environ.get("DREPHIP_SCALE_N"):
@@ -51,7 +55,14 @@ if os.environ.get("DREPHIP_SCALE_N"):
     CASES.append(pytest.param(_n, int(os.environ.get("DREPHIP_SCALE_S", 1000)), "custom", id="custom%d" % _n))
 if os.environ.get("DREPHIP_SCALE_ONLY"):
     CASES = [c for c in CASES if c.id in os.environ["DREPHIP_SCALE_ONLY"].split(",")]
-SCIPY_UP_TO = 10_000 if os.environ.get("DREPHIP_SCALE_SCIPY") != "1" else 10 ** 9
+# scipy's Z digest per workload (test id), committed after a run in which Z
+# equalled scipy's (the result JSON records it as linkage_sha1)
+DIGESTS = os.path.join(ROOT, "tests", "golden", "scale_linkage_sha1.json")
+
+
+def z_digest(Z):
+    import hashlib
+    return hashlib.sha1(np.ascontiguousarray(Z, dtype="<f8").tobytes()).hexdigest()
 
 
 def _cond_index(i, j, N):
@@ -258,30 +269,44 @@ def test_scale(N, s, config):
     import scipy.cluster.hierarchy as sch
     fcl = sch.fcluster(Z, 0.1, criterion="distance")
     res["primary_clusters_at_P_ani_0.9"] = int(fcl.max())
+    res["linkage_sha1"] = z_digest(Z)
+    case = "%d" % N if s == 1000 else "%d-s%d" % (N, s)
+    golden = json.load(open(DIGESTS)).get(case) if os.path.exists(DIGESTS) else None
+    res["linkage_sha1_golden"] = golden
+    note("Z sha1 %s (golden %s)" % (res["linkage_sha1"], golden))
+    json.dump(res, open(out_path, "w"), indent=1)
 
-    if N <= SCIPY_UP_TO:
-        common = d_common.cpu().numpy().view(np.uint16)
-        del d_common
-        torch.cuda.empty_cache()
-        y = np.empty(npairs, dtype=np.float64)
-        step = 1 << 27
-        for a in range(0, npairs, step):
-            y[a:a + step] = lut[common[a:a + step]]
-        del common
-        hb = subprocess.Popen([sys.executable, "-c",
-                               "import time,sys\nwhile True:\n print(time.time(), 'scipy linkage running', "
-                               "file=open(sys.argv[1], 'a'), flush=True); time.sleep(20)",
-                               os.path.splitext(out_path)[0] + ".progress"])
-        try:
-            t0 = time.perf_counter()
-            Zs = sch.linkage(y, method="average")
-            res["scipy_linkage_s"] = time.perf_counter() - t0
-        finally:
-            hb.kill()
-            hb.wait()
-        res["linkage_identical_to_scipy"] = bool(np.array_equal(Z, Zs))
-        note("scipy linkage %.1f s identical=%s" % (res["scipy_linkage_s"], res["linkage_identical_to_scipy"]))
-        assert res["linkage_identical_to_scipy"]
+    common = d_common.cpu().numpy().view(np.uint16)
+    del d_common
+    torch.cuda.empty_cache()
+    y = np.empty(npairs, dtype=np.float64)
+    step = 1 << 27
+    for a in range(0, npairs, step):
+        y[a:a + step] = lut[common[a:a + step]]
+    del common
+    hb = subprocess.Popen([sys.executable, "-c",
+                           "import time,sys\nwhile True:\n print(time.time(), 'scipy linkage running', "
+                           "file=open(sys.argv[1], 'a'), flush=True); time.sleep(20)",
+                           os.path.splitext(out_path)[0] + ".progress"])
+    try:
+        t0 = time.perf_counter()
+        Zs = sch.linkage(y, method="average")
+        res["scipy_linkage_s"] = time.perf_counter() - t0
+    finally:
+        hb.kill()
+        hb.wait()
+    res["linkage_identical_to_scipy"] = bool(np.array_equal(Z, Zs))
+    res["scipy_linkage_sha1"] = z_digest(Zs)
+    fcl_s = sch.fcluster(Zs, 0.1, criterion="distance")
+    res["fcluster_labels_identical_to_scipy"] = bool(np.array_equal(fcl, fcl_s))
+    del y, Zs
+    note("scipy linkage %.1f s identical=%s, fcluster labels identical=%s"
+         % (res["scipy_linkage_s"], res["linkage_identical_to_scipy"], res["fcluster_labels_identical_to_scipy"]))
+    json.dump(res, open(out_path, "w"), indent=1)
+    assert res["linkage_identical_to_scipy"]
+    assert res["fcluster_labels_identical_to_scipy"]
+    if golden is not None:
+        assert res["linkage_sha1"] == golden
     link_ctx.close()
     ctx.close()
     json.dump(res, open(out_path, "w"), indent=1)
