@@ -3,7 +3,9 @@ N synthetic 5 Mbp genomes sketched and all-pairs'ed on the GPU (as
 tests/test_scale.py, no checks), then average linkage from the device counts
 twice -- the first call allocates the n x n matrix, the second reuses it --
 with the phase split (drephip_last_linkage_stats) and a digest of Z so runs of
-different libraries (DREPHIP_LIB) can be compared.
+different libraries (DREPHIP_LIB) can be compared.  For average linkage at a
+size whose scipy digest is committed (tests/golden/scale_linkage_sha1.json:
+scipy's own Z of the same counts) any other digest fails the run (exit 1).
 usage: python tools/link_ab.py N [method]"""
 import hashlib, json, os, sys, time
 import numpy as np
@@ -43,5 +45,10 @@ for rep in range(2):
     out["wall_s_%d" % rep] = time.perf_counter() - t0
     out["phases_%d" % rep] = ctx.linkage_stats()
     out["chain_kernel_ms_%d" % rep] = ctx.kernel_ms(2)[0]
-out["Z_sha1"] = hashlib.sha1(Z.tobytes()).hexdigest()[:16]
+out["Z_sha1"] = hashlib.sha1(np.ascontiguousarray(Z, dtype="<f8").tobytes()).hexdigest()
+golden = json.load(open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
+                                     "scale_linkage_sha1.json"))).get(str(N)) if method == "average" else None
+out["Z_equals_scipy_digest"] = None if golden is None else out["Z_sha1"] == golden
 print(json.dumps(out))
+if golden is not None and out["Z_sha1"] != golden:
+    sys.exit("Z digest %s != scipy's %s" % (out["Z_sha1"], golden))
