@@ -719,7 +719,7 @@ __global__ __launch_bounds__(256) void k_allpairs_merge(const uint64_t *__restri
 }
 
 // ------------------------------------------------------- banded all-pairs
-// Large sketches (s > 2048, up to kMaxSketch): a whole-row table no longer fits
+// Large sketches (s > 2048, up to kMaxSketch = 32767): a whole-row table no longer fits
 // LDS, so the hash range is cut into value bands per row tile.  Band k of a
 // tile of R rows is [lo_k, hi_k) with hi_k = min over rows of A_r[p_r + cap]
 // (p_r = the row's first element >= lo_k), so every row has <= cap elements in
@@ -738,9 +738,14 @@ __global__ __launch_bounds__(256) void k_allpairs_merge(const uint64_t *__restri
 // literal merge); a band's build is amortised over kBandCols columns.
 // Roofline: as k_allpairs_q (LDS random reads + VALU); column chunks are read
 // once per band per tile, i.e. s * 8 / R bytes per pair from L2.
+//
+// Geometry (template): R rows per tile, 2^BB slots per choice, CAP elements
+// per row per band (launch_band: R = 4, 2^11, 768).
+// Round 4: the columns a band visits come from a live list built by the band
+// before it -- a column whose union-rank end has passed for every row is
+// dropped once instead of being re-tested (and its first chunks re-loaded)
+// in every later band.
 constexpr uint32_t kBandCols = 128;
-constexpr uint32_t kBandB = 11;                       // H = 2048 slots per choice
-constexpr uint32_t kBandCapMax = 768;                 // elements per row per band (<= H/2): LDS for 2 workgroups/CU
 
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 #pragma unroll
@@ -750,14 +755,11 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
     }
     return v;
 }
-// Column element j: an unconditional load clamped to the row, no select (a
-// select would wait on the load right where it is issued).  Elements past nB
-// are kEmpty in the sketch matrix and fail every band test (b < hi <= the
-// rows' largest element + 1); lanes past s hold clamped copies and are masked
-// by tail_mask.
 // 64 column elements from position `first` (wave-uniform) on, one per lane,
 // through the column's buffer resource: lanes past s read 0 (buffer bounds)
-// and are dropped by tail_mask where the chunk is used
+// and are dropped by tail_mask where the chunk is used.  Elements past nB are
+// kEmpty in the sketch matrix and fail every band test (b < hi <= the rows'
+// largest element + 1).
 __device__ __forceinline__ uint64_t ld_elems(__amdgpu_buffer_rsrc_t rs, uint32_t lane_off, uint32_t first) {
     const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, lane_off, rfl(first) * 8u, 0);
     return ((uint64_t)v[1] << 32) | v[0];
@@ -766,20 +768,23 @@ __device__ __forceinline__ uint64_t tail_mask(uint32_t j0, uint32_t s) {     // 
     return j0 + 64 <= s ? ~0ull : j0 >= s ? 0ull : (1ull << (s - j0)) - 1;
 }
 
-// The column phase of one band: wave w takes columns w, w+NW, ... of the
-// item.  A column's band segment streams through a ring of kRing chunks in
-// registers, loaded kRing chunks ahead (the next column's first kRing chunks
-// when a column starts) by raw buffer loads; slot words are read one chunk
-// ahead of the tests.
-template <int R, uint32_t NW, bool FAST, bool RETRY>
+// The column phase of one band: wave w takes the live columns w, w+NW, ... of
+// the band's list (live[0..nlive)).  A column's band segment streams through a
+// ring of kRing chunks in registers, loaded kRing chunks ahead (the next
+// column's first kRing chunks when a column starts) by raw buffer loads; slot
+// words are read one chunk ahead of the tests.  After the band a column goes
+// on the next band's list (next, *nnext) unless its union-rank end has passed
+// for every row with the next band's row positions pn.
+template <int R, uint32_t NW, int BB, int CAP, bool FAST, bool RETRY>
 __device__ __forceinline__ void band_columns(const uint64_t *__restrict__ hashes, uint32_t s, const uint32_t *T,
                                              const uint32_t *V, uint32_t *cur, uint16_t *pcnt, uint16_t *pm,
-                                             uint32_t c0, uint32_t ncols, uint32_t i0, uint32_t nrows, uint32_t wave,
-                                             uint64_t hi, uint32_t fam, const uint32_t (&pr)[R], int *live) {
-    constexpr uint32_t H = 1u << kBandB, hm = H - 1;
+                                             const uint8_t *live, uint32_t nlive, uint8_t *next, uint32_t *nnext,
+                                             uint32_t c0, uint32_t i0, uint32_t nrows, uint32_t wave, uint64_t hi,
+                                             uint32_t fam, const uint32_t (&pr)[R], const uint32_t (&pn)[R]) {
+    constexpr uint32_t H = 1u << BB, hm = H - 1;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t lane_off = lane * 8u;
-    uint32_t ci = wave;
+    uint32_t li = wave;
     uint64_t nx[kRing];
     uint32_t nq = 0;
     auto load_first = [&](uint32_t cc) {
@@ -788,40 +793,26 @@ __device__ __forceinline__ void band_columns(const uint64_t *__restrict__ hashes
 #pragma unroll
         for (int k = 0; k < kRing; k++) nx[k] = ld_elems(rn, lane_off, nq + 64 * k);
     };
-    if (ci < ncols) load_first(ci);
+    uint32_t cnx = li < nlive ? rfl(live[li]) : 0;
+    if (li < nlive) load_first(cnx);
     uint32_t o1[R], o2[R], cap_r[R];
     const QFields qf = qfields(fam);
 #pragma unroll
-    for (int r = 0; r < R; r++) { o1[r] = qf.o1; o2[r] = qf.o2; cap_r[r] = kBandCapMax; }
-    for (; ci < ncols; ci += NW) {
+    for (int r = 0; r < R; r++) { o1[r] = qf.o1; o2[r] = qf.o2; cap_r[r] = CAP; }
+    for (; li < nlive; li += NW) {
+        const uint32_t ci = cnx;
         const uint32_t c = c0 + ci;
         const uint32_t q0 = nq;
         uint64_t rg[kRing];
 #pragma unroll
         for (int k = 0; k < kRing; k++) rg[k] = nx[k];
-        if (ci + NW < ncols) load_first(ci + NW);
+        if (li + NW < nlive) { cnx = rfl(live[li + NW]); load_first(cnx); }
         uint32_t actmask = 0;
 #pragma unroll
         for (int r = 0; r < R; r++) actmask |= (uint32_t)((uint32_t)r < nrows && i0 + r < c) << r;
-        if (!actmask) continue;
         uint32_t mrun[R], cnt[R];
 #pragma unroll
         for (int r = 0; r < R; r++) { mrun[r] = rfl(pm[r * kBandCols + ci]); cnt[r] = 0; }   // scalar counters
-        // union-rank end: the column's next element b (position q0, at or above
-        // the band's low bound, below which A_r has pr[r] elements) has rank
-        // u(b) = q0 + #{A_r < b} - #{matches below b} >= q0 + pr[r] - mrun in
-        // A_r u B, and every later column element ranks higher.  Once that is
-        // >= s for every active row, the rank rule counts nothing more in this
-        // or any later band (cursor, counts and shared-so-far stay; |A u B| > s
-        // then makes a partial pair's denominator s whatever mrun misses).
-        // Mash's merge stops at the s-th union element the same way; unrelated
-        // sketches get there about half way down the column.
-        bool all_past = true;
-#pragma unroll
-        for (int r = 0; r < R; r++)
-            if (((actmask >> r) & 1u) && q0 + pr[r] < s + mrun[r]) all_past = false;
-        if (all_past) continue;
-        *live = 1;                                                    // benign race: every writer stores 1
         const __amdgpu_buffer_rsrc_t rc = column_rsrc(hashes + (uint64_t)c * s, s);
         uint32_t q = q0;
         bool more = true;
@@ -829,18 +820,18 @@ __device__ __forceinline__ void band_columns(const uint64_t *__restrict__ hashes
         // after the chunk's last use; a finished column only skips the probe
         Slots<R> sb[kRing];
 #pragma unroll
-        for (int u = 0; u < kSlotAhead; u++) sb[u] = read_slots<R, FAST, kBandB>((uint32_t)rg[u], T, H, hm, o1, o2);
+        for (int u = 0; u < kSlotAhead; u++) sb[u] = read_slots<R, FAST, BB>((uint32_t)rg[u], T, H, hm, o1, o2);
         for (uint32_t kb = 0; more; kb += kRing) {
 #pragma unroll
             for (int u = 0; u < kRing; u++) {
                 const uint64_t b = rg[u];
                 const uint32_t j0 = q0 + 64 * (kb + u);
                 sb[(u + kSlotAhead) % kRing] =
-                    read_slots<R, FAST, kBandB>((uint32_t)rg[(u + kSlotAhead) % kRing], T, H, hm, o1, o2);
+                    read_slots<R, FAST, BB>((uint32_t)rg[(u + kSlotAhead) % kRing], T, H, hm, o1, o2);
                 if (more) {                                           // wave-uniform
                     const uint64_t inb = __builtin_amdgcn_ballot_w64(b < hi) & tail_mask(j0, s);
-                    probe_rows<R, FAST, RETRY>(sb[u], b, q + lane, V, kBandCapMax, hm, o1, o2, actmask, inb, pr, cap_r,
-                                        s, mrun, cnt);
+                    probe_rows<R, FAST, RETRY>(sb[u], b, q + lane, V, CAP, hm, o1, o2, actmask, inb, pr, cap_r,
+                                               s, mrun, cnt);
                     const uint32_t nin = (uint32_t)__popcll(inb);
                     q += nin;
                     more = nin == 64;
@@ -848,34 +839,56 @@ __device__ __forceinline__ void band_columns(const uint64_t *__restrict__ hashes
                 rg[u] = ld_elems(rc, lane_off, j0 + 64 * kRing);    // refill the ring
             }
         }
+        // union-rank end for the next band: the column's next element b
+        // (position q, at or above the next band's low bound, below which A_r
+        // has pn[r] elements) has rank u(b) = q + #{A_r < b} - #{matches below
+        // b} >= q + pn[r] - mrun in A_r u B, and every later column element
+        // ranks higher.  Once that is >= s for every active row, the rank rule
+        // counts nothing more in any later band (cursor, counts and
+        // shared-so-far stay; |A u B| > s then makes a partial pair's
+        // denominator s whatever mrun misses).  Mash's merge stops at the s-th
+        // union element the same way; unrelated sketches get there about half
+        // way down the column.
+        bool all_past = true;
 #pragma unroll
         for (int r = 0; r < R; r++)
-            if (lane == 0) { pcnt[r * kBandCols + ci] += cnt[r]; pm[r * kBandCols + ci] = mrun[r]; }
-        if (lane == 0) cur[ci] = q;
+            if (((actmask >> r) & 1u) && q + pn[r] < s + mrun[r]) all_past = false;
+        if (lane == 0) {
+#pragma unroll
+            for (int r = 0; r < R; r++) { pcnt[r * kBandCols + ci] += cnt[r]; pm[r * kBandCols + ci] = mrun[r]; }
+            cur[ci] = q;
+            if (!all_past) next[atomicAdd(nnext, 1u)] = (uint8_t)ci;
+        }
     }
 }
 
-__host__ __device__ constexpr size_t band_lds_bytes(uint32_t R) {
-    return (size_t)R * (2u << kBandB) * 4 + (size_t)R * kBandCapMax * 4 + kBandCols * 4 + 2ull * R * kBandCols * 2;
+template <int R, int BB, int CAP>
+__host__ __device__ constexpr size_t band_lds_bytes() {
+    // slot words, high words, cursors, counts + shared-so-far, two live lists
+    return (size_t)R * (2u << BB) * 4 + (size_t)R * CAP * 4 + kBandCols * 4 + 2ull * R * kBandCols * 2 +
+           2ull * kBandCols;
 }
-static_assert(band_lds_bytes(4) <= 80 * 1024, "band kernel LDS must allow two workgroups per CU");
+static_assert(kBandCols <= 256, "live lists hold column indices in bytes");
+static_assert(band_lds_bytes<4, 11, 768>() <= 80 * 1024 - 128, "R = 4: two workgroups per CU");
 
-template <int R, int WG, int MINW>
+template <int R, int BB, int CAP, int WG, int MINW>
 __global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
     const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ nhash, uint32_t s, uint32_t N,
     uint32_t row1, uint32_t cap, const uint2 *__restrict__ items, uint16_t *__restrict__ common,
     uint16_t *__restrict__ denom, uint64_t seg0, uint32_t *__restrict__ nfail, uint64_t *__restrict__ prof) {
-    constexpr uint32_t H = 1u << kBandB, hm = H - 1, TS = 2 * H;
+    constexpr uint32_t H = 1u << BB, hm = H - 1, TS = 2 * H;
     constexpr uint32_t NW = WG / 64;
+    static_assert(CAP < H, "band positions stay below the empty word's position hm");
     extern __shared__ __align__(16) uint32_t lds[];    // 16-B aligned: slot words are read with ds_read_b128
     uint32_t *T = lds;                                               // [TS][R] interleaved slot words
-    uint32_t *V = T + R * TS;                                        // [R][kBandCapMax] high words
-    uint32_t *cur = V + R * kBandCapMax;                             // [kBandCols] column cursors
+    uint32_t *V = T + R * TS;                                        // [R][CAP] high words
+    uint32_t *cur = V + R * CAP;                                     // [kBandCols] column cursors
     uint16_t *pcnt = (uint16_t *)(cur + kBandCols);                  // [R][kBandCols] counts (<= s)
     uint16_t *pm = pcnt + R * kBandCols;                             // [R][kBandCols] shared so far (<= s)
-    __shared__ uint32_t s_p[R], s_q[R];
+    uint8_t *lists = (uint8_t *)(pm + R * kBandCols);                // [2][kBandCols] live columns per band
+    __shared__ uint32_t s_p[R], s_q[R], s_nlive[2];
     __shared__ uint64_t s_hi;
-    __shared__ int s_done, s_fail, s_abort, s_twin, s_live;
+    __shared__ int s_done, s_fail, s_abort, s_twin;
 
     const uint32_t i0 = items[blockIdx.x].x;
     const uint32_t c0 = items[blockIdx.x].y;
@@ -901,9 +914,15 @@ __global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
     for (uint32_t k = tid; k < kBandCols; k += WG) cur[k] = 0;
     for (uint32_t k = tid; k < R * kBandCols; k += WG) { pcnt[k] = 0; pm[k] = 0; }
     if (tid < (uint32_t)R) s_p[tid] = 0;
-    if (tid == 0) s_abort = 0;
+    if (tid == 0) { s_abort = 0; s_nlive[0] = 0; s_nlive[1] = 0; }
+    __syncthreads();
+    // the first band's list: every column right of the tile's first row
+    // (columns left of every row have no pair in the item)
+    for (uint32_t k = tid; k < ncols; k += WG)
+        if (i0 < c0 + k) lists[atomicAdd(&s_nlive[0], 1u)] = (uint8_t)k;
 
-    for (;;) {
+    for (uint32_t band = 0;; band++) {
+        const uint32_t lb = band & 1u;                   // this band's list; the next band's is lb ^ 1
         __syncthreads();
         if (wave == 0) {
             // band bound: the (cap+1)-th remaining element of the tightest row
@@ -921,9 +940,9 @@ __global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
             const bool any_left = __ballot(left) != 0;
             if (lane == 0) {
                 s_hi = v < maxlast + 1 ? v : maxlast + 1;
-                s_done = !any_left;
+                s_done = !any_left || s_nlive[lb] == 0;
                 s_fail = 0;
-                s_live = 0;
+                s_nlive[lb ^ 1u] = 0;
             }
             if (lane < (uint32_t)R) s_q[lane] = 0;
         }
@@ -950,7 +969,7 @@ __global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
                 if (p + t >= nl) continue;
                 const uint64_t x = hashes[(uint64_t)(i0 + r) * s + p + t];
                 if (x >= hi) continue;
-                if (fam == 0) V[r * kBandCapMax + t] = (uint32_t)(x >> 32);
+                if (fam == 0) V[r * CAP + t] = (uint32_t)(x >> 32);
                 if (!cuckoo_insert32(T, R, r, H, hm, qf, (uint32_t)x, t)) s_fail = 1;
             }
             __syncthreads();
@@ -974,21 +993,27 @@ __global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
             if (tid == 0) { s_abort = 1; atomicAdd(nfail, 1u); }
             break;
         }
+        // the next band's row positions (s_q is final after the build)
+        uint32_t pn[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) pn[r] = pr[r] + s_q[r];
 
         uint64_t t_c0 = prof ? wall_clock64() : 0;
-        // ---- columns: wave w takes columns w, w+NW, ...
+        // ---- columns: wave w takes the live columns w, w+NW, ...
         // the fast probe without the second-slot retry unless a band table has twins
+        const uint8_t *live = lists + lb * kBandCols;
+        uint8_t *next = lists + (lb ^ 1u) * kBandCols;
+        const uint32_t nlive = s_nlive[lb];
         if (fam == 0 && !s_twin)
-            band_columns<R, NW, true, false>(hashes, s, T, V, cur, pcnt, pm, c0, ncols, i0, nrows, wave, hi, fam, pr, &s_live);
+            band_columns<R, NW, BB, CAP, true, false>(hashes, s, T, V, cur, pcnt, pm, live, nlive, next, &s_nlive[lb ^ 1u],
+                                                      c0, i0, nrows, wave, hi, fam, pr, pn);
         else if (fam == 0)
-            band_columns<R, NW, true, true>(hashes, s, T, V, cur, pcnt, pm, c0, ncols, i0, nrows, wave, hi, fam, pr, &s_live);
+            band_columns<R, NW, BB, CAP, true, true>(hashes, s, T, V, cur, pcnt, pm, live, nlive, next, &s_nlive[lb ^ 1u],
+                                                     c0, i0, nrows, wave, hi, fam, pr, pn);
         else
-            band_columns<R, NW, false, true>(hashes, s, T, V, cur, pcnt, pm, c0, ncols, i0, nrows, wave, hi, fam, pr, &s_live);
+            band_columns<R, NW, BB, CAP, false, true>(hashes, s, T, V, cur, pcnt, pm, live, nlive, next, &s_nlive[lb ^ 1u],
+                                                      c0, i0, nrows, wave, hi, fam, pr, pn);
         __syncthreads();
-        // every column past its union-rank end for every row (band_columns):
-        // the same holds in every later band (pr only grows), so no further
-        // band table is built
-        if (!s_live) break;
         if (tid < (uint32_t)R) s_p[tid] += s_q[tid];
         if (prof && tid == 0) {
             const uint64_t t_e = wall_clock64();
@@ -1148,11 +1173,13 @@ static int launch_merge(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32
     return DREPHIP_OK;
 }
 
-static int launch_band(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N,
-                       uint32_t row0, uint32_t row1, uint64_t seg0, uint64_t npairs, uint16_t *d_common,
-                       uint16_t *d_denom, hipStream_t st) {
-    constexpr int R = 4;
-    const uint32_t cap = std::min(std::max(ctx->band_cap, 1u), kBandCapMax);
+// One band-kernel geometry: R rows per tile, 2^BB slots per choice, CAP
+// elements per row per band, MINW = 8 (two workgroups per CU) or 4 (one).
+template <int R, int BB, int CAP, int MINW>
+static int launch_band_cfg(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N,
+                           uint32_t row0, uint32_t row1, uint64_t seg0, uint64_t npairs, uint16_t *d_common,
+                           uint16_t *d_denom, hipStream_t st) {
+    const uint32_t cap = std::min(std::max(ctx->band_cap, 1u), (uint32_t)CAP);
     uint2 *d_items;
     uint64_t nitems;
     uint32_t *d_nfail;
@@ -1170,13 +1197,14 @@ static int launch_band(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_
         if ((rc = scratch(ctx, "apb_prof", 64, (void **)&d_prof))) return rc;
         HIPC(hipMemsetAsync(d_prof, 0, 64, st));
     }
-    const size_t lds = band_lds_bytes(R);         // <= 80 KiB: two workgroups per CU
-    HIPC(hipFuncSetAttribute((const void *)k_allpairs_band<R, 1024, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    constexpr size_t lds = band_lds_bytes<R, BB, CAP>();
+    auto kern = k_allpairs_band<R, BB, CAP, 1024, MINW>;
+    HIPC(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     timing_mark(ctx, 2, st, true);
     for (uint64_t i0 = 0; i0 < nitems; i0 += max_blocks(1024))
-        hipLaunchKernelGGL((k_allpairs_band<R, 1024, 8>), dim3((uint32_t)std::min<uint64_t>(nitems - i0, max_blocks(1024))),
-                           dim3(1024), lds, st, d_hashes, d_nhash, ctx->s, N, row1, cap, d_items + i0, d_common,
-                           d_denom, seg0, d_nfail, d_prof);
+        hipLaunchKernelGGL(kern, dim3((uint32_t)std::min<uint64_t>(nitems - i0, max_blocks(1024))), dim3(1024), lds, st,
+                           d_hashes, d_nhash, ctx->s, N, row1, cap, d_items + i0, d_common, d_denom, seg0, d_nfail,
+                           d_prof);
     timing_mark(ctx, 2, st, false);
     HIPC(hipGetLastError());
     uint32_t nfail = 0;
@@ -1185,12 +1213,26 @@ static int launch_band(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_
     if (prof) {
         uint64_t h[3];
         HIPC(hipMemcpy(h, d_prof, 24, hipMemcpyDeviceToHost));
-        fprintf(stderr, "[drephip] band kernel: %llu bands over %zu items; per band: build %.2f us, columns %.2f us (100 MHz wall clock)\n",
-                (unsigned long long)h[2], (size_t)nitems, h[2] ? h[0] / 100.0 / h[2] : 0.0, h[2] ? h[1] / 100.0 / h[2] : 0.0);
+        fprintf(stderr, "[drephip] band kernel R=%d 2^%d slots cap %u: %llu bands over %zu items; per band: build %.2f us, columns %.2f us (100 MHz wall clock)\n",
+                R, BB, cap, (unsigned long long)h[2], (size_t)nitems, h[2] ? h[0] / 100.0 / h[2] : 0.0,
+                h[2] ? h[1] / 100.0 / h[2] : 0.0);
     }
     if (nfail)   // a band table could not be built with any field pair: exact merge kernel instead
         return launch_merge(ctx, d_hashes, d_nhash, N, seg0, npairs, d_common, d_denom, st);
     return DREPHIP_OK;
+}
+
+// Band geometry: R = 4 rows, 2^11 slots per choice, cap 768, two workgroups
+// per CU.  Round 4 measured R = 8 (configs[4], N = 10^4, s = 10^4, whole
+// triangle exact): 113 ms with 2^11 slots / cap 768 / one workgroup per CU and
+// 147 ms with 2^10 slots / cap 352 / two per CU, against 84 ms here
+// (profiles/r04_band_geometry_ab.json): the band bound is the tightest of R
+// rows, so more rows mean narrower bands, more table builds and more
+// per-column band overhead, which outweighs the halved column stream.
+static int launch_band(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N,
+                       uint32_t row0, uint32_t row1, uint64_t seg0, uint64_t npairs, uint16_t *d_common,
+                       uint16_t *d_denom, hipStream_t st) {
+    return launch_band_cfg<4, 11, 768, 8>(ctx, d_hashes, d_nhash, N, row0, row1, seg0, npairs, d_common, d_denom, st);
 }
 
 template <int R, int NCH, int MINW>
@@ -1247,6 +1289,12 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
     static const uint32_t kR[] = {8, 4, 2, 1};
     uint32_t R = 1;
     for (uint32_t r : kR) if (q_lds_bytes(r, TS, s) + 16 <= kLdsBudget) { R = r; break; }
+    if (const char *e = getenv("DREPHIP_AP_R")) {
+        // A/B override: R rows per workgroup if their tables fit the whole
+        // 160 KiB of a CU (one workgroup per CU above 80 KiB)
+        const uint32_t r = (uint32_t)atoi(e);
+        if ((r == 1 || r == 2 || r == 4 || r == 8) && q_lds_bytes(r, TS, s) <= 160 * 1024) R = r;
+    }
 
     // row-group LDS images (tables + high words), built once per call
     const uint32_t nrows = row1 - row0;

@@ -21,7 +21,9 @@ constexpr uint64_t kTile = (uint64_t)kLaneBases * kSketchWG;   // 32768 bases
 constexpr uint32_t kWarm = 32;                // bases rolled before the first window end
 constexpr uint64_t kEmpty = ~0ull;            // empty slot / "no hash" sentinel
 constexpr uint64_t kMaxThr = ~0ull - 1;       // inclusive threshold that admits every hash but kEmpty
-constexpr uint32_t kMaxSketch = 12000;        // finalize sorts <= 16384 candidates in LDS
+constexpr uint32_t kLdsSortSketch = 12000;    // up to here finalize sorts <= 16384 candidates in LDS
+constexpr uint32_t kMaxSketch = 32767;        // above: a global sort buffer; counts are uint16 (<= s), and
+                                              // 0xFFFF stays an impossible count
 
 inline uint64_t round_up(uint64_t x, uint64_t m) { return (x + m - 1) / m * m; }
 

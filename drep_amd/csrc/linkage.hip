@@ -39,6 +39,9 @@ namespace drephip {
 // per row at small n: 136 vs 143 ms of chain at n = 10^4; 256 is faster at
 // 10^5 -- profiles/r03_linkage_wg_ab.txt)
 constexpr int kLkWG = 256;
+#ifndef DREPHIP_LK_COLSTORE
+#define DREPHIP_LK_COLSTORE 1     // column-y stores of a merge step: 1 plain, 2 nontemporal, 0 none (A/B timing only)
+#endif
 constexpr uint32_t kLkSmallN = 30000;
 
 static double now_s() {
@@ -276,7 +279,13 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             if (pend && (int32_t)i != y && (int32_t)i != t) {
                 const double u = lw_update(method, dx[k], dy[k], nx, ny);
                 Dy[i] = u;
+#if DREPHIP_LK_COLSTORE == 0
+                // timing-only A/B build: no column-y stores (Z is wrong)
+#elif DREPHIP_LK_COLSTORE == 2
+                __builtin_nontemporal_store(u, &D[(uint64_t)i * n + y]);
+#else
                 D[(uint64_t)i * n + y] = u;
+#endif
                 v = t == y ? u : dt[k];
             } else if (pend && (int32_t)i == y && t != y) {
                 const double u = lw_update(method, dxt, dyt, nx, ny);

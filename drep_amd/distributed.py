@@ -115,7 +115,7 @@ def gather_segments(seg, N: int, root: int = 0, out=None):
     return full
 
 
-POISON = 0x7FFF        # an impossible shared-hash count (s <= 12000)
+POISON = -1            # int16 view of 0xFFFF: an impossible shared-hash count (s <= 32767)
 
 SketchFn = Callable[[ShardPlan], Tuple["object", "object"]]            # -> (loc_h [nmax, s], loc_n [nmax])
 AllpairsFn = Callable[..., Tuple["object", Optional["object"]]]      # fn(H, NH, plan, out=None)
@@ -160,7 +160,7 @@ def run_sharded(N: int, names: Sequence[str], s: int, sketch_fn: SketchFn, allpa
     full_c = None
     out = None
     # DREPHIP_SEGMENT_POISON=1 (tests): the root's vector starts as POISON, a
-    # value no count takes (s <= 12000), and no pair may still hold it after the
+    # value no count takes (s <= 32767), and no pair may still hold it after the
     # gather -- every kernel path must write every pair of its rows
     poison = os.environ.get("DREPHIP_SEGMENT_POISON") == "1"
     if rank == root and N >= 2:

@@ -157,8 +157,11 @@ def test_sketch_edge_cases_vs_oracle(ctx1000):
         assert int(ln[gi]) == int(off[-1]), kind
 
 
-@pytest.mark.parametrize("s", [1, 64, 4096, 12000])
+@pytest.mark.parametrize("s", [1, 64, 4096, 12000, 12001, 20000, 32767])
 def test_sketch_sizes_vs_oracle(s):
+    """Sketch sizes up to kMaxSketch = 32767 (dRep's -ms is unbounded,
+    drep/argumentParser.py:103): above 12000 the finalize sorts its
+    candidates in a global buffer instead of LDS."""
     rng = np.random.default_rng(s)
     A = np.frombuffer(b"ACGT", dtype=np.uint8)
     recs = [A[rng.integers(0, 4, 250_000)], A[rng.integers(0, 4, 3000)], A[rng.integers(0, 4, 900_000)]]
@@ -195,11 +198,12 @@ def test_sketch_mixed_case_nruns_vs_oracle(seed):
     assert nh[1] < S
 
 
-@pytest.mark.parametrize("s", [1, 1000, 12000])
+@pytest.mark.parametrize("s", [1, 1000, 12000, 24000])
 def test_sketch_finalize_vs_oracle(s):
     """The bucket-sort finalize gives the oracle's sketches: full and partial
-    sketches, its 4096- and 16384-candidate instantiations, and a
-    low-complexity genome whose candidates crowd few buckets."""
+    sketches, its 4096- and 16384-candidate LDS instantiations and the
+    global-buffer one (s > 12000), and a low-complexity genome whose
+    candidates crowd few buckets."""
     rng = np.random.default_rng(100 + s)
     A = np.frombuffer(b"ACGT", dtype=np.uint8)
     motif = A[rng.integers(0, 4, 40)]
@@ -467,7 +471,7 @@ def test_allpairs_partial_sketches_vs_oracle(ctx1000):
     assert np.array_equal(c, oc) and np.array_equal(d, od)
 
 
-@pytest.mark.parametrize("s", [1, 16, 100, 513, 1024, 1025, 2048, 2049, 4096, 10000, 12000])
+@pytest.mark.parametrize("s", [1, 16, 100, 513, 1024, 1025, 2048, 2049, 4096, 10000, 12000, 20000, 32767])
 def test_allpairs_sketch_sizes(s):
     h, nh = oracle.sketch_synth(0, 48, 120_000, seed=s, family_size=12, s=s, threads=8)
     with _lib.Context(0, 21, s, 42) as ctx:
@@ -477,7 +481,7 @@ def test_allpairs_sketch_sizes(s):
 
 
 @pytest.mark.parametrize("s,cap", [(1, 1), (100, 7), (1000, 64), (1000, 1024), (4096, 300),
-                                   (10000, 1024), (12000, 1000)])
+                                   (10000, 1024), (12000, 1000), (20000, 768)])
 def test_allpairs_band_kernel_vs_oracle(s, cap):
     """Value-banded kernel (production path for s > 2048): many bands per row
     tile at small caps, bit-exact counts and denominators."""
@@ -739,7 +743,8 @@ def test_errors_are_reported_not_hidden(ctx1000, tmp_path):
         ctx1000.sketch_files([str(bad)])
     with pytest.raises(_lib.DrepHipError):
         _lib.Context(device=0, k=21, s=0, seed=42)
-    with pytest.raises(_lib.DrepHipError):
+    assert _lib.max_sketch() == 32767          # uint16 counts; 0xFFFF stays an impossible count
+    with pytest.raises(_lib.DrepHipError, match=r"sketch size must be in 1\.\.32767"):
         _lib.Context(device=0, k=21, s=_lib.max_sketch() + 1, seed=42)
     with pytest.raises(_lib.DrepHipError):
         _lib.Context(device=1 << 20, k=21, s=1000, seed=42)

@@ -28,6 +28,9 @@ def test_library_exports_every_header_symbol():
     for name in declared:
         assert getattr(L, name) is not None
     assert L.drephip_version() >= 100
+    # sketch sizes up to 32767 (dRep's -ms/--MASH_sketch is unbounded,
+    # drep/argumentParser.py:103; counts and denominators are uint16)
+    assert _lib.max_sketch() == 32767
 
 
 def test_allpairs_kernel_declares_no_static_lds(tmp_path):
