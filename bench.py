@@ -401,7 +401,7 @@ def main():
     d_common = torch.zeros(max(seg, 1), dtype=torch.int16, device=dev)
 
     stage = {"sketch": 0.0, "gather": 0.0, "dist": 0.0}
-    kms = {0: [0.0, 0], 1: [0.0, 0], 2: [0.0, 0], 3: [0.0, 0]}
+    kms = {0: [0.0, 0], 1: [0.0, 0], 2: [0.0, 0], 3: [0.0, 0], 4: [0.0, 0]}
 
     ev = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
 
@@ -434,7 +434,7 @@ def main():
         if seg:
             ctx.allpairs_device(hh.data_ptr(), nn.data_ptr(), N, r0, r1, d_common.data_ptr(), None, stream)
         if record and seg:
-            read_kms((2, 3))
+            read_kms((2, 3, 4))
         if nloc and ctx.sketch_wait():
             # a genome needed another threshold round: the sketches were redone.
             # One rank alone cannot redo the gather (the other ranks would hang
@@ -537,13 +537,14 @@ def main():
     # bracketed by events (not part of the timed region)
     keep = (list(kms[0]), dict(stage))
     ctx.set_timing(True)
-    for w in (1, 2, 3):
+    for w in (1, 2, 3, 4):
         kms[w] = [0.0, 0]
     for _ in range(PROFILE_STEPS):
         step(True)
     torch.cuda.synchronize()
     kms[0], stage = keep
     ctx.set_timing(True, kernels=(0,))
+    screen = ctx.screen_stats()
 
     K = args.steps
     # stage split per step from the kernels' HIP events (the host cannot see
@@ -695,8 +696,9 @@ def main():
                 "sketch_finalize_ms_avg": kms[1][0] / max(kms[1][1], 1),
                 "allpairs_ms_avg": kms[2][0] / max(kms[2][1], 1),
                 "cuckoo_build_ms_avg": kms[3][0] / max(kms[3][1], 1),
+                "screen_ms_avg": kms[4][0] / max(kms[4][1], 1),
                 "launches": {"sketch_hash": sk_n, "finalize": kms[1][1], "allpairs": kms[2][1],
-                             "build": kms[3][1]},
+                             "build": kms[3][1], "screen": kms[4][1]},
             },
             "roofline": {
                 "kernel": valu.get("kernel", "k_sketch_hash21"),
@@ -714,6 +716,8 @@ def main():
             },
             "dist_kernel": {
                 "kernel": "k_allpairs_q (s <= 2048) / k_allpairs_band",
+                "screen": dict(screen, note="shared-hash screen (screen.hip): the kernel runs only on the (row "
+                               "tile, column) cells whose genomes share a hash; auto from 4096 genomes"),
                 "bound": "VALU + LDS (random slot reads); integer set intersection, no MFMA",
                 "ms_per_launch": kms[2][0] / max(kms[2][1], 1),
                 "pairs_per_launch": segment_size(N, r0, r1),

@@ -88,6 +88,9 @@ SIGNATURES = {
     "drephip_last_linkage_stats": (C.c_int, [vp] + [C.POINTER(C.c_double)] * 5),
     "drephip_set_timing": (C.c_int, [vp, C.c_int]),
     "drephip_last_kernel_ms": (C.c_int, [vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
+    "drephip_set_allpairs_screen": (C.c_int, [vp, C.c_int]),
+    "drephip_last_screen_stats": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                             C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
 }
 
 
@@ -259,6 +262,20 @@ class Context:
 
     # all-pairs kernel selection (include/drephip.h DREPHIP_AP_*)
     AP_AUTO, AP_TABLE, AP_BAND, AP_MERGE = 0, 1, 2, 3
+
+    SCREEN_AUTO, SCREEN_ON, SCREEN_OFF = 0, 1, 2
+
+    def set_allpairs_screen(self, mode: int) -> None:
+        """The shared-hash screen in front of the all-pairs kernels
+        (include/drephip.h: auto / on / off)."""
+        check(lib().drephip_set_allpairs_screen(self._h, mode), "drephip_set_allpairs_screen")
+
+    def screen_stats(self) -> dict:
+        u = C.c_int(0)
+        e, r, c, m = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
+        check(lib().drephip_last_screen_stats(self._h, C.byref(u), C.byref(e), C.byref(r), C.byref(c), C.byref(m)),
+              "drephip_last_screen_stats")
+        return {"used": bool(u.value), "entries": e.value, "runs": r.value, "checks": c.value, "marked": m.value}
 
     def set_allpairs_path(self, path: int, band_cap: int = 1024) -> None:
         check(lib().drephip_set_allpairs_path(self._h, path, band_cap), "drephip_set_allpairs_path")

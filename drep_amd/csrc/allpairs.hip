@@ -49,6 +49,7 @@ constexpr uint32_t kMaxFam = 6;                 // cuckoo field families tried p
 constexpr uint32_t kFamTwins = 0x40;            // k_build_q32 family byte: the row has two keys with one low word
 constexpr uint32_t kFamFailed = 0xFF;           // ... no family worked (the row's pairs are merged literally)
 constexpr uint32_t kLdsBudget = 156 * 1024;     // dynamic LDS per workgroup
+constexpr uint32_t kScreenMinN = 4096;          // genomes from which the shared-hash screen runs (auto)
 
 __host__ __device__ __forceinline__ uint64_t cond_index(uint64_t i, uint64_t j, uint64_t N) {
     return i * N - i * (i + 1) / 2 + (j - i - 1);
@@ -392,11 +393,16 @@ __device__ __forceinline__ uint64_t ld_chunk_at(__amdgpu_buffer_rsrc_t rs, uint3
 // probed unmasked and unclamped: no tail mask, no chunk-in-range test, no
 // refill clamp -- only the group loop and the early-end tests are scalar
 // work.  MASKED = true keeps them (rows holding the key 0, the generic probe).
-template <int R, int NCH, bool FAST, int KB, bool MASKED>
+//
+// LIST (the screened path, screen.hip): the item's columns are clist[0..cend)
+// -- ascending, each sharing a hash with a row of the tile -- and c_first /
+// c_step walk that list instead of the column range.
+template <int R, int NCH, bool FAST, int KB, bool MASKED, bool LIST = false>
 __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ nhash,
                                            const uint32_t *T, const uint32_t *V, uint32_t H, uint32_t hm, uint32_t s,
                                            uint32_t N, uint32_t i0, uint32_t nrows, uint32_t cend, uint32_t c_first,
-                                           uint32_t c_step, const uint32_t (&nA)[R], const uint32_t (&o1)[R],
+                                           uint32_t c_step, const uint32_t *__restrict__ clist,
+                                           const uint32_t (&nA)[R], const uint32_t (&o1)[R],
                                            const uint32_t (&o2)[R], const uint64_t (&alast)[R],
                                            const uint64_t (&thr1)[R], const uint64_t (&thr2)[R], uint32_t okmask,
                                            bool any_partial_row, uint16_t *__restrict__ common,
@@ -410,7 +416,9 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
     uint32_t zero[R];
 #pragma unroll
     for (int r = 0; r < R; r++) zero[r] = 0;
-    uint32_t c = rfl(c_first);                                       // wave-uniform: scalar column loop
+    uint32_t kc = rfl(c_first);                                      // wave-uniform: scalar column loop
+    auto column_of = [&](uint32_t k) -> uint32_t { return LIST ? rfl(clist[k]) : k; };
+    uint32_t c = kc < cend ? column_of(kc) : 0;
     auto first_chunks = [&](__amdgpu_buffer_rsrc_t rn) {
         if constexpr (MASKED) {
 #pragma unroll
@@ -423,7 +431,7 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
         }
     };
     static_assert(kRing == 4, "first_chunks / refill offsets");
-    if (c < cend) first_chunks(column_rsrc(hashes + (uint64_t)c * s, s));
+    if (kc < cend) first_chunks(column_rsrc(hashes + (uint64_t)c * s, s));
     // per item, not per column: the active rows and their largest hash once
     // every row of the tile is left of the column (c >= i0 + R: all columns
     // but the diagonal tile's), and row 0's output offset (row r + 1's is row
@@ -437,12 +445,13 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
         if (act) amax_full = alast[r] > amax_full ? alast[r] : amax_full;
     }
     const uint64_t obase = cond_index(i0, 0, N) - seg0;            // + c: row i0's pair (i0, c)
-    for (; c < cend; c += c_step) {
+    for (uint32_t cnext = 0; kc < cend; kc += c_step, c = cnext) {
         const __amdgpu_buffer_rsrc_t rc = column_rsrc(hashes + (uint64_t)c * s, s);
 #pragma unroll
         for (int k = 0; k < kRing; k++) rg[k] = nx[k];
-        const uint32_t cn = c + c_step;
-        if (cn < cend) first_chunks(column_rsrc(hashes + (uint64_t)cn * s, s));
+        const uint32_t kn = kc + c_step;
+        cnext = kn < cend ? column_of(kn) : 0;
+        if (kn < cend) first_chunks(column_rsrc(hashes + (uint64_t)cnext * s, s));
         uint32_t cnt[R], mrun[R], actmask = act_full;
         // elements past every active row's largest hash cannot match: the
         // scan ends at the first chunk whose smallest element is past them
@@ -586,12 +595,14 @@ __host__ __device__ constexpr size_t q_lds_bytes(uint32_t R, uint32_t TS, uint32
 // R rows (tables in LDS) x kApCols columns per workgroup of kApWG lanes; each
 // wave walks every 16th column of the item.  MINW = 8: two workgroups per CU
 // (LDS <= 80 KiB, <= 64 VGPRs).
-template <int R, int NCH, int MINW>
+// LIST: items are {i0, list offset, count, 0} over the screened column list
+// (screen.hip); otherwise {i0, c0, cend, 0} over the column range.
+template <int R, int NCH, int MINW, bool LIST = false>
 __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
     const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ nhash,
     const uint32_t *__restrict__ blk, uint32_t stride, const uint8_t *__restrict__ fam, uint32_t s, uint32_t N,
     uint32_t row0, uint32_t row1, uint32_t B, const uint4 *__restrict__ items,
-    uint16_t *__restrict__ common, uint16_t *__restrict__ denom, uint64_t seg0) {
+    uint16_t *__restrict__ common, uint16_t *__restrict__ denom, uint64_t seg0, const uint32_t *__restrict__ clist) {
     constexpr int WG = kApWG;
     extern __shared__ __align__(16) uint32_t lds[];    // 16-B aligned: slot words are read with ds_read_b128
     const uint32_t H = 1u << B, hm = H - 1, TS = 2 * H;
@@ -601,7 +612,10 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
     const uint32_t c0 = items[blockIdx.x].y;
     if (i0 == 0xFFFFFFFFu) return;                      // idle padding item (make_items)
     const uint32_t nrows = min((uint32_t)R, row1 - i0);
-    const uint32_t cend = min(items[blockIdx.x].z, N);
+    // LIST: c0 = the item's list offset, cend = its column count
+    const uint32_t cend = LIST ? items[blockIdx.x].z : min(items[blockIdx.x].z, N);
+    const uint32_t *ilist = LIST ? clist + c0 : nullptr;
+    const uint32_t cfirst = LIST ? 0 : c0;
     const uint32_t tid = threadIdx.x, wave = tid >> 6;
     {   // the row group's LDS image (k_build_q32) by LDS-DMA: wave w copies the
         // 1 KiB pieces w, w + 16, ... (global_load_lds_dwordx4 writes a piece
@@ -668,24 +682,24 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
     // by tests/test_host.py), so `lds` is LDS address 0 (read_slots).
     constexpr int KB = NCH == 16 ? 11 : 0;
     if (fast && !zero_key)
-        ap_columns<R, NCH, true, KB, false>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend, c0 + wave, WG / 64,
+        ap_columns<R, NCH, true, KB, false, LIST>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend, cfirst + wave, WG / 64, ilist,
                                             nA, o1, o2, alast, thr1, thr2, ~failmask, any_partial_row, common, denom,
                                             seg0);
     else if (fast)
-        ap_columns<R, NCH, true, KB, true>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend, c0 + wave, WG / 64,
+        ap_columns<R, NCH, true, KB, true, LIST>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend, cfirst + wave, WG / 64, ilist,
                                            nA, o1, o2, alast, thr1, thr2, ~failmask, any_partial_row, common, denom,
                                            seg0);
     else
-        ap_columns<R, NCH, false, KB, true>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend, c0 + wave, WG / 64,
+        ap_columns<R, NCH, false, KB, true, LIST>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend, cfirst + wave, WG / 64, ilist,
                                             nA, o1, o2, alast, thr1, thr2, ~failmask, any_partial_row, common, denom,
                                             seg0);
     if (failmask) {
         // a row whose table could not be built (three of its keys share a low
         // word under every field family; never observed on real sketches):
         // its pairs of this item by Mash's literal merge, one lane per pair
-        const uint32_t ncol = cend - c0;
+        const uint32_t ncol = cend - cfirst;
         for (uint32_t t = tid; t < (uint32_t)R * ncol; t += WG) {
-            const uint32_t r = t / ncol, c = c0 + t % ncol, i = i0 + r;
+            const uint32_t r = t / ncol, c = LIST ? ilist[t % ncol] : c0 + t % ncol, i = i0 + r;
             if (!((failmask >> r) & 1u) || c <= i) continue;
             uint32_t cm, dd;
             merge_pair(hashes + (uint64_t)i * s, nhash[i], hashes + (uint64_t)c * s, nhash[c], s, cm, dd);
@@ -775,12 +789,15 @@ __device__ __forceinline__ uint64_t tail_mask(uint32_t j0, uint32_t s) {     // 
 // words are read one chunk ahead of the tests.  After the band a column goes
 // on the next band's list (next, *nnext) unless its union-rank end has passed
 // for every row with the next band's row positions pn.
-template <int R, uint32_t NW, int BB, int CAP, bool FAST, bool RETRY>
+template <int R, uint32_t NW, int BB, int CAP, bool FAST, bool RETRY, bool LIST>
 __device__ __forceinline__ void band_columns(const uint64_t *__restrict__ hashes, uint32_t s, const uint32_t *T,
                                              const uint32_t *V, uint32_t *cur, uint16_t *pcnt, uint16_t *pm,
                                              const uint8_t *live, uint32_t nlive, uint8_t *next, uint32_t *nnext,
-                                             uint32_t c0, uint32_t i0, uint32_t nrows, uint32_t wave, uint64_t hi,
-                                             uint32_t fam, const uint32_t (&pr)[R], const uint32_t (&pn)[R]) {
+                                             uint32_t c0, const uint32_t *__restrict__ cl, uint32_t i0, uint32_t nrows,
+                                             uint32_t wave, uint64_t hi, uint32_t fam, const uint32_t (&pr)[R],
+                                             const uint32_t (&pn)[R]) {
+    // column of item column ci: c0 + ci, or (LIST) the screened list's entry
+    auto col = [&](uint32_t ci) -> uint32_t { return LIST ? rfl(cl[ci]) : c0 + ci; };
     constexpr uint32_t H = 1u << BB, hm = H - 1;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t lane_off = lane * 8u;
@@ -789,7 +806,7 @@ __device__ __forceinline__ void band_columns(const uint64_t *__restrict__ hashes
     uint32_t nq = 0;
     auto load_first = [&](uint32_t cc) {
         nq = rfl(cur[cc]);
-        const __amdgpu_buffer_rsrc_t rn = column_rsrc(hashes + (uint64_t)(c0 + cc) * s, s);
+        const __amdgpu_buffer_rsrc_t rn = column_rsrc(hashes + (uint64_t)col(cc) * s, s);
 #pragma unroll
         for (int k = 0; k < kRing; k++) nx[k] = ld_elems(rn, lane_off, nq + 64 * k);
     };
@@ -801,7 +818,7 @@ __device__ __forceinline__ void band_columns(const uint64_t *__restrict__ hashes
     for (int r = 0; r < R; r++) { o1[r] = qf.o1; o2[r] = qf.o2; cap_r[r] = CAP; }
     for (; li < nlive; li += NW) {
         const uint32_t ci = cnx;
-        const uint32_t c = c0 + ci;
+        const uint32_t c = col(ci);
         const uint32_t q0 = nq;
         uint64_t rg[kRing];
 #pragma unroll
@@ -871,11 +888,15 @@ __host__ __device__ constexpr size_t band_lds_bytes() {
 static_assert(kBandCols <= 256, "live lists hold column indices in bytes");
 static_assert(band_lds_bytes<4, 11, 768>() <= 80 * 1024 - 128, "R = 4: two workgroups per CU");
 
-template <int R, int BB, int CAP, int WG, int MINW>
+// LIST (the screened path, screen.hip): items are {i0, list offset, count, 0}
+// (litems) over the column list clist; otherwise {i0, c0} over kBandCols
+// consecutive columns.
+template <int R, int BB, int CAP, int WG, int MINW, bool LIST = false>
 __global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
     const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ nhash, uint32_t s, uint32_t N,
     uint32_t row1, uint32_t cap, const uint2 *__restrict__ items, uint16_t *__restrict__ common,
-    uint16_t *__restrict__ denom, uint64_t seg0, uint32_t *__restrict__ nfail, uint64_t *__restrict__ prof) {
+    uint16_t *__restrict__ denom, uint64_t seg0, uint32_t *__restrict__ nfail, uint64_t *__restrict__ prof,
+    const uint4 *__restrict__ litems, const uint32_t *__restrict__ clist) {
     constexpr uint32_t H = 1u << BB, hm = H - 1, TS = 2 * H;
     constexpr uint32_t NW = WG / 64;
     static_assert(CAP < H, "band positions stay below the empty word's position hm");
@@ -890,12 +911,12 @@ __global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
     __shared__ uint64_t s_hi;
     __shared__ int s_done, s_fail, s_abort, s_twin;
 
-    const uint32_t i0 = items[blockIdx.x].x;
-    const uint32_t c0 = items[blockIdx.x].y;
+    const uint32_t i0 = LIST ? litems[blockIdx.x].x : items[blockIdx.x].x;
+    const uint32_t c0 = LIST ? 0 : items[blockIdx.x].y;
     if (i0 == 0xFFFFFFFFu) return;                      // idle padding item (make_items)
     const uint32_t nrows = min((uint32_t)R, row1 - i0);
-    const uint32_t cend = min(c0 + kBandCols, N);
-    const uint32_t ncols = cend - c0;
+    const uint32_t *cl = LIST ? clist + litems[blockIdx.x].y : nullptr;
+    const uint32_t ncols = LIST ? litems[blockIdx.x].z : min(c0 + kBandCols, N) - c0;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t wave = rfl(tid >> 6);          // wave-uniform for the compiler: scalar column loop
 
@@ -919,7 +940,7 @@ __global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
     // the first band's list: every column right of the tile's first row
     // (columns left of every row have no pair in the item)
     for (uint32_t k = tid; k < ncols; k += WG)
-        if (i0 < c0 + k) lists[atomicAdd(&s_nlive[0], 1u)] = (uint8_t)k;
+        if (i0 < (LIST ? cl[k] : c0 + k)) lists[atomicAdd(&s_nlive[0], 1u)] = (uint8_t)k;
 
     for (uint32_t band = 0;; band++) {
         const uint32_t lb = band & 1u;                   // this band's list; the next band's is lb ^ 1
@@ -1005,14 +1026,14 @@ __global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
         uint8_t *next = lists + (lb ^ 1u) * kBandCols;
         const uint32_t nlive = s_nlive[lb];
         if (fam == 0 && !s_twin)
-            band_columns<R, NW, BB, CAP, true, false>(hashes, s, T, V, cur, pcnt, pm, live, nlive, next, &s_nlive[lb ^ 1u],
-                                                      c0, i0, nrows, wave, hi, fam, pr, pn);
+            band_columns<R, NW, BB, CAP, true, false, LIST>(hashes, s, T, V, cur, pcnt, pm, live, nlive, next, &s_nlive[lb ^ 1u],
+                                                      c0, cl, i0, nrows, wave, hi, fam, pr, pn);
         else if (fam == 0)
-            band_columns<R, NW, BB, CAP, true, true>(hashes, s, T, V, cur, pcnt, pm, live, nlive, next, &s_nlive[lb ^ 1u],
-                                                     c0, i0, nrows, wave, hi, fam, pr, pn);
+            band_columns<R, NW, BB, CAP, true, true, LIST>(hashes, s, T, V, cur, pcnt, pm, live, nlive, next, &s_nlive[lb ^ 1u],
+                                                     c0, cl, i0, nrows, wave, hi, fam, pr, pn);
         else
-            band_columns<R, NW, BB, CAP, false, true>(hashes, s, T, V, cur, pcnt, pm, live, nlive, next, &s_nlive[lb ^ 1u],
-                                                      c0, i0, nrows, wave, hi, fam, pr, pn);
+            band_columns<R, NW, BB, CAP, false, true, LIST>(hashes, s, T, V, cur, pcnt, pm, live, nlive, next, &s_nlive[lb ^ 1u],
+                                                      c0, cl, i0, nrows, wave, hi, fam, pr, pn);
         __syncthreads();
         if (tid < (uint32_t)R) s_p[tid] += s_q[tid];
         if (prof && tid == 0) {
@@ -1024,6 +1045,29 @@ __global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
     }
     __syncthreads();
     if (s_abort) return;
+    if (LIST) {
+        // the screened columns: one pair per (row, list entry) right of the row
+        for (uint32_t t = tid; t < nrows * ncols; t += WG) {
+            const uint32_t r = t / ncols, ci = t - r * ncols, i = i0 + r, c = cl[ci];
+            if (c <= i) continue;
+            uint32_t nl = 0;
+#pragma unroll
+            for (int rr = 0; rr < R; rr++) if ((uint32_t)rr == r) nl = nA[rr];
+            const uint64_t o = cond_index(i, c, N) - seg0;
+            common[o] = (uint16_t)pcnt[r * kBandCols + ci];
+            if (denom) {
+                const uint32_t nB = nhash[c];
+                uint32_t dd = s;
+                if (any_partial_row || nB < s) {
+                    const uint32_t u = nl + nB - pm[r * kBandCols + ci];
+                    dd = u < s ? u : s;
+                }
+                denom[o] = (uint16_t)dd;
+            }
+        }
+        return;
+    }
+    const uint32_t cend = c0 + ncols;
     for (uint32_t r = 0; r < nrows; r++) {
         const uint32_t i = i0 + r;
         const uint32_t cs = max(c0, i + 1);
@@ -1175,19 +1219,29 @@ static int launch_merge(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32
 
 // One band-kernel geometry: R rows per tile, 2^BB slots per choice, CAP
 // elements per row per band, MINW = 8 (two workgroups per CU) or 4 (one).
+// scr: the screened lists (LIST kernel over them, every other pair filled as
+// no-shared-hash), or null for the dense item plan.
 template <int R, int BB, int CAP, int MINW>
 static int launch_band_cfg(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N,
                            uint32_t row0, uint32_t row1, uint64_t seg0, uint64_t npairs, uint16_t *d_common,
-                           uint16_t *d_denom, hipStream_t st) {
+                           uint16_t *d_denom, hipStream_t st, const ScreenResult *scr) {
     const uint32_t cap = std::min(std::max(ctx->band_cap, 1u), (uint32_t)CAP);
-    uint2 *d_items;
+    uint2 *d_items = nullptr;
     uint64_t nitems;
     uint32_t *d_nfail;
     int rc;
     std::vector<ItemGroup> groups;                   // lives until the stream sync below
-    if ((rc = expand_items<false>(ctx, plan_items(row0, row1, N, R, kBandCols), groups, "apb_items", R, kBandCols, st,
-                                  (void **)&d_items, &nitems)))
+    if (scr) {
+        nitems = scr->nitems;
+    } else if ((rc = expand_items<false>(ctx, plan_items(row0, row1, N, R, kBandCols), groups, "apb_items", R,
+                                         kBandCols, st, (void **)&d_items, &nitems))) {
         return rc;
+    }
+    if (scr) {
+        timing_mark(ctx, 2, st, true);
+        if ((rc = screen_fill_impl(ctx, d_nhash, N, row0, row1, seg0, npairs, d_common, d_denom, st))) return rc;
+        if (nitems == 0) { timing_mark(ctx, 2, st, false); HIPC(hipStreamSynchronize(st)); return DREPHIP_OK; }
+    }
     if (nitems == 0) return DREPHIP_OK;
     if ((rc = scratch(ctx, "ap_nfail_band", 4, (void **)&d_nfail))) return rc;
     HIPC(hipMemsetAsync(d_nfail, 0, 4, st));
@@ -1198,13 +1252,13 @@ static int launch_band_cfg(drephip_ctx *ctx, const uint64_t *d_hashes, const uin
         HIPC(hipMemsetAsync(d_prof, 0, 64, st));
     }
     constexpr size_t lds = band_lds_bytes<R, BB, CAP>();
-    auto kern = k_allpairs_band<R, BB, CAP, 1024, MINW>;
+    auto kern = scr ? k_allpairs_band<R, BB, CAP, 1024, MINW, true> : k_allpairs_band<R, BB, CAP, 1024, MINW, false>;
     HIPC(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    timing_mark(ctx, 2, st, true);
+    if (!scr) timing_mark(ctx, 2, st, true);
     for (uint64_t i0 = 0; i0 < nitems; i0 += max_blocks(1024))
         hipLaunchKernelGGL(kern, dim3((uint32_t)std::min<uint64_t>(nitems - i0, max_blocks(1024))), dim3(1024), lds, st,
-                           d_hashes, d_nhash, ctx->s, N, row1, cap, d_items + i0, d_common, d_denom, seg0, d_nfail,
-                           d_prof);
+                           d_hashes, d_nhash, ctx->s, N, row1, cap, scr ? nullptr : d_items + i0, d_common, d_denom, seg0,
+                           d_nfail, d_prof, scr ? scr->items + i0 : nullptr, scr ? scr->clist : nullptr);
     timing_mark(ctx, 2, st, false);
     HIPC(hipGetLastError());
     uint32_t nfail = 0;
@@ -1229,24 +1283,28 @@ static int launch_band_cfg(drephip_ctx *ctx, const uint64_t *d_hashes, const uin
 // (profiles/r04_band_geometry_ab.json): the band bound is the tightest of R
 // rows, so more rows mean narrower bands, more table builds and more
 // per-column band overhead, which outweighs the halved column stream.
+constexpr uint32_t kBandR = 4;
 static int launch_band(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N,
                        uint32_t row0, uint32_t row1, uint64_t seg0, uint64_t npairs, uint16_t *d_common,
-                       uint16_t *d_denom, hipStream_t st) {
-    return launch_band_cfg<4, 11, 768, 8>(ctx, d_hashes, d_nhash, N, row0, row1, seg0, npairs, d_common, d_denom, st);
+                       uint16_t *d_denom, hipStream_t st, const ScreenResult *scr) {
+    return launch_band_cfg<kBandR, 11, 768, 8>(ctx, d_hashes, d_nhash, N, row0, row1, seg0, npairs, d_common, d_denom,
+                                               st, scr);
 }
 
-template <int R, int NCH, int MINW>
+// LIST: the screened items / column list (clist); the caller opened the
+// timing span (it covers the no-shared-hash fill as well)
+template <int R, int NCH, int MINW, bool LIST>
 static int launch_q(drephip_ctx *ctx, uint32_t nitems, size_t lds, hipStream_t st, const uint64_t *h,
                     const uint32_t *nh, const uint32_t *blk, uint32_t stride, const uint8_t *fam, uint32_t N, uint32_t row0,
                     uint32_t row1, uint32_t B, const uint4 *items, uint16_t *cm, uint16_t *dn,
-                    uint64_t seg0) {
-    HIPC(hipFuncSetAttribute((const void *)k_allpairs_q<R, NCH, MINW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                    uint64_t seg0, const uint32_t *clist) {
+    HIPC(hipFuncSetAttribute((const void *)k_allpairs_q<R, NCH, MINW, LIST>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)lds));
-    timing_mark(ctx, 2, st, true);
+    if (!LIST) timing_mark(ctx, 2, st, true);
     for (uint32_t i0 = 0; i0 < nitems; i0 += (uint32_t)max_blocks(kApWG))
-        hipLaunchKernelGGL((k_allpairs_q<R, NCH, MINW>), dim3(std::min<uint32_t>(nitems - i0, (uint32_t)max_blocks(kApWG))),
-                           dim3(kApWG), lds, st, h, nh, blk, stride, fam, ctx->s, N, row0, row1, B, items + i0, cm, dn,
-                           seg0);
+        hipLaunchKernelGGL((k_allpairs_q<R, NCH, MINW, LIST>),
+                           dim3(std::min<uint32_t>(nitems - i0, (uint32_t)max_blocks(kApWG))), dim3(kApWG), lds, st, h,
+                           nh, blk, stride, fam, ctx->s, N, row0, row1, B, items + i0, cm, dn, seg0, clist);
     timing_mark(ctx, 2, st, false);
     HIPC(hipGetLastError());
     return DREPHIP_OK;
@@ -1280,10 +1338,9 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
         set_error("whole-row table all-pairs kernel needs s <= 2048");
         return DREPHIP_ERR_UNSUPPORTED;
     }
+    ctx->last_screen = ScreenResult{};
     if (path == DREPHIP_AP_MERGE)
         return launch_merge(ctx, d_hashes, d_nhash, N, seg0, npairs, d_common, d_denom, st);
-    if (path == DREPHIP_AP_BAND)
-        return launch_band(ctx, d_hashes, d_nhash, N, row0, row1, seg0, npairs, d_common, d_denom, st);
 
     // rows per workgroup: the most (8, 4, 2, 1) whose tables + high words fit
     static const uint32_t kR[] = {8, 4, 2, 1};
@@ -1295,6 +1352,23 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
         const uint32_t r = (uint32_t)atoi(e);
         if ((r == 1 || r == 2 || r == 4 || r == 8) && q_lds_bytes(r, TS, s) <= 160 * 1024) R = r;
     }
+    if (path == DREPHIP_AP_BAND) R = kBandR;
+
+    // the shared-hash screen (screen.hip): auto from kScreenMinN genomes on
+    int smode = ctx->screen;
+    if (const char *e = getenv("DREPHIP_AP_SCREEN")) smode = atoi(e);
+    const char *mn = getenv("DREPHIP_SCREEN_MIN_N");
+    const uint32_t min_n = mn ? (uint32_t)atoi(mn) : kScreenMinN;
+    ScreenResult scr;
+    if (smode == DREPHIP_SCREEN_ON || (smode == DREPHIP_SCREEN_AUTO && N >= min_n)) {
+        int rc = screen_impl(ctx, d_hashes, d_nhash, N, row0, row1, R, path == DREPHIP_AP_BAND ? kBandCols : kApCols,
+                             npairs, smode == DREPHIP_SCREEN_ON, st, &scr);
+        if (rc) return rc;
+        ctx->last_screen = scr;
+    }
+    if (path == DREPHIP_AP_BAND)
+        return launch_band(ctx, d_hashes, d_nhash, N, row0, row1, seg0, npairs, d_common, d_denom, st,
+                           scr.use ? &scr : nullptr);
 
     // row-group LDS images (tables + high words), built once per call
     const uint32_t nrows = row1 - row0;
@@ -1325,13 +1399,18 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
         for (uint32_t i0 = row0; i0 < row1; i0 += R) n += nct - (i0 + 1) / c;
         return n;
     };
-    while (C > kApMinCols && nitems_for(C) < 4ull * kApSlots) C /= 2;
+    if (!scr.use) while (C > kApMinCols && nitems_for(C) < 4ull * kApSlots) C /= 2;
     // the item list depends only on (N, rows, R, C): reused while the shape and
     // the scratch allocation are unchanged (repeated calls: bench steps, shards).
     // Its group table lives in the context until the next plan replaces it (the
     // queued H2D copy may still be reading it when a deferred call returns).
     const uint64_t key[5] = {N, row0, row1, R, C};
-    if (ctx->ap_items_gen == ctx->alloc_gen && !memcmp(ctx->ap_items_key, key, sizeof(key))) {
+    if (scr.use) {
+        // the screened items; every other pair gets the no-shared-hash fill
+        d_items = (uint4 *)scr.items;
+        timing_mark(ctx, 2, st, true);
+        if ((rc = screen_fill_impl(ctx, d_nhash, N, row0, row1, seg0, npairs, d_common, d_denom, st))) return rc;
+    } else if (ctx->ap_items_gen == ctx->alloc_gen && !memcmp(ctx->ap_items_key, key, sizeof(key))) {
         if ((rc = scratch(ctx, "ap_items", ctx->ap_items_n * sizeof(uint4), (void **)&d_items))) return rc;
     } else {
         uint64_t n;
@@ -1343,15 +1422,18 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
         memcpy(ctx->ap_items_key, key, sizeof(key));
         ctx->ap_items_gen = ctx->alloc_gen;
     }
-    const uint32_t ni = (uint32_t)ctx->ap_items_n;
+    const uint32_t ni = scr.use ? scr.nitems : (uint32_t)ctx->ap_items_n;
+    const bool lst = scr.use;
     // a row whose table cannot be built is merged literally inside the main
     // kernel (k_allpairs_q): no host round trip, nothing to check afterwards
     const size_t lds = (size_t)stride * 4;
     const uint32_t nch = (s + 63) / 64;
     // two workgroups per CU when the LDS allows
     const bool two = lds <= 80 * 1024;
-#define DREPHIP_Q(RR, NC) (two ? launch_q<RR, NC, 8>(ctx, ni, lds, st, d_hashes, d_nhash, d_blk, stride, d_fam, N, row0, row1, B, d_items, d_common, d_denom, seg0) \
-                               : launch_q<RR, NC, 4>(ctx, ni, lds, st, d_hashes, d_nhash, d_blk, stride, d_fam, N, row0, row1, B, d_items, d_common, d_denom, seg0))
+#define DREPHIP_Q1(RR, NC, MW, LS) launch_q<RR, NC, MW, LS>(ctx, ni, lds, st, d_hashes, d_nhash, d_blk, stride, d_fam, N, row0, row1, B, \
+                                                          d_items, d_common, d_denom, seg0, scr.clist)
+#define DREPHIP_Q(RR, NC) (two ? (lst ? DREPHIP_Q1(RR, NC, 8, true) : DREPHIP_Q1(RR, NC, 8, false)) \
+                               : (lst ? DREPHIP_Q1(RR, NC, 4, true) : DREPHIP_Q1(RR, NC, 4, false)))
     if (nch <= 8) {
         switch (R) {
             case 8: rc = DREPHIP_Q(8, 8); break;
@@ -1374,6 +1456,7 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
         }
     }
 #undef DREPHIP_Q
+#undef DREPHIP_Q1
     if (rc) return rc;
     if (defer) {
         // drephip_allpairs_wait (or the next all-pairs call) waits for this event

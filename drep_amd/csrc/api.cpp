@@ -72,7 +72,7 @@ int pinned_host(drephip_ctx *ctx, const char *name, size_t bytes, void **out) {
 }
 
 void timing_begin(drephip_ctx *ctx) {
-    for (int i = 0; i < 4; i++) { ctx->kms[i] = 0; ctx->kn[i] = 0; }
+    for (int i = 0; i < 5; i++) { ctx->kms[i] = 0; ctx->kn[i] = 0; }
     ctx->spans.clear();
     ctx->ev_used = 0;
 }
@@ -198,7 +198,7 @@ DREPHIP_EXPORT int drephip_destroy(drephip_ctx *ctx) {
 
 DREPHIP_EXPORT int drephip_set_timing(drephip_ctx *ctx, int kernels) {
     if (!ctx) { set_error("null context"); return DREPHIP_ERR_ARG; }
-    ctx->timing = (uint32_t)kernels & 0xFu;
+    ctx->timing = (uint32_t)kernels & 0x1Fu;
     return DREPHIP_OK;
 }
 
@@ -211,8 +211,27 @@ DREPHIP_EXPORT int drephip_set_allpairs_path(drephip_ctx *ctx, int path, uint32_
     return DREPHIP_OK;
 }
 
+DREPHIP_EXPORT int drephip_set_allpairs_screen(drephip_ctx *ctx, int mode) {
+    if (!ctx) { set_error("null context"); return DREPHIP_ERR_ARG; }
+    if (mode < DREPHIP_SCREEN_AUTO || mode > DREPHIP_SCREEN_OFF) { set_error("unknown screen mode"); return DREPHIP_ERR_ARG; }
+    ctx->screen = mode;
+    return DREPHIP_OK;
+}
+
+DREPHIP_EXPORT int drephip_last_screen_stats(drephip_ctx *ctx, int *used, uint64_t *entries, uint64_t *runs,
+                                             uint64_t *checks, uint64_t *marked) {
+    if (!ctx) { set_error("null context"); return DREPHIP_ERR_ARG; }
+    const ScreenResult &r = ctx->last_screen;
+    if (used) *used = r.use ? 1 : 0;
+    if (entries) *entries = r.entries;
+    if (runs) *runs = r.runs;
+    if (checks) *checks = r.checks;
+    if (marked) *marked = r.marked;
+    return DREPHIP_OK;
+}
+
 DREPHIP_EXPORT int drephip_last_kernel_ms(drephip_ctx *ctx, int which, double *ms, int *launches) {
-    if (!ctx || which < 0 || which > 3 || !ms) { set_error("bad argument"); return DREPHIP_ERR_ARG; }
+    if (!ctx || which < 0 || which > 4 || !ms) { set_error("bad argument"); return DREPHIP_ERR_ARG; }
     *ms = ctx->kms[which];
     if (launches) *launches = ctx->kn[which];
     return DREPHIP_OK;

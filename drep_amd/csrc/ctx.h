@@ -74,6 +74,18 @@ struct LinkStats {            // last drephip_linkage* call, host wall clock (se
     SparseLinkInfo sp;        // its figures (pairs also when the dense path was chosen)
 };
 
+// The shared-hash screen of the last all-pairs call (screen.hip).
+struct ScreenResult {
+    bool use = false;             // the screened lists below replace the dense item plan
+    const uint32_t *clist = nullptr;   // marked columns, per row tile, ascending (device)
+    const uint4 *items = nullptr;      // {i0, list offset, count, 0} (device)
+    uint32_t nitems = 0;
+    uint64_t entries = 0;         // sketch entries sorted
+    uint64_t runs = 0;            // runs of >= 2 equal 32-bit keys
+    uint64_t checks = 0;          // pair checks of the marking (sum of m(m-1)/2)
+    uint64_t marked = 0;          // marked (row tile, column) cells
+};
+
 // A run of all-pairs work items (allpairs.hip, plan_items): `size` row tiles
 // from i0 (step R) against column tile c0, at offset `off` of its XCD's list.
 struct ApItemGroup { uint32_t i0, c0, off, size; };
@@ -86,13 +98,15 @@ struct drephip_ctx {
     hipStream_t stream = nullptr;
     uint32_t timing = 0;      // bitmask of timed kernels (bit w = `which` w of drephip_last_kernel_ms)
     int ap_path = 0;          // DREPHIP_AP_*: 0 auto (table for s <= 2048, else band)
+    int screen = 0;           // DREPHIP_SCREEN_*: 0 auto, 1 on, 2 off
+    ScreenResult last_screen; // the last all-pairs call's screen (stats; pointers into scratch)
     int link_path = 0;        // DREPHIP_LINK_PATH_*: 0 auto (sparse when it applies, else dense)
     uint32_t band_cap = 1024; // elements per row per band of the banded all-pairs kernel (clamped to its LDS budget)
     // named grow-only device scratch buffers
     std::map<std::string, DevBuf> bufs;
     // per-kernel timing of the last call: {sum ms, launches}
-    double kms[4] = {0, 0, 0, 0};
-    int kn[4] = {0, 0, 0, 0};
+    double kms[5] = {0, 0, 0, 0, 0};
+    int kn[5] = {0, 0, 0, 0, 0};
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
     struct Span { int which; hipEvent_t a, b; };
@@ -179,6 +193,17 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
                          uint32_t N, uint32_t row0, uint32_t row1, uint16_t *d_common,
                          uint16_t *d_denom, hipStream_t st, bool force_merge, bool defer = false);
 int allpairs_wait_impl(drephip_ctx *ctx);
+// The shared-hash screen (screen.hip): the (row tile of R rows, column) cells
+// of rows [row0, row1) whose row and column share a hash, as per-tile column
+// lists and LIST work items of at most C columns.  res->use = false when the
+// set is too dense for it to pay (unless force) or too large for its 32-bit
+// indices; the dense path runs then.  Synchronises the stream.
+int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N, uint32_t row0,
+                uint32_t row1, uint32_t R, uint32_t C, uint64_t npairs, bool force, hipStream_t st, ScreenResult *res);
+// Every pair of the segment as an unscreened one: common 0, denominator
+// min(s, |A| + |B|); the LIST kernels then overwrite the screened pairs.
+int screen_fill_impl(drephip_ctx *ctx, const uint32_t *d_nhash, uint32_t N, uint32_t row0, uint32_t row1,
+                     uint64_t seg0, uint64_t npairs, uint16_t *d_common, uint16_t *d_denom, hipStream_t st);
 
 // Primary clustering (linkage.hip).
 int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, double *Z_out, hipStream_t st);

@@ -248,6 +248,28 @@ int drephip_write_mash_table(const char *path, const char *const *names, uint32_
 #define DREPHIP_AP_MERGE 3
 int drephip_set_allpairs_path(drephip_ctx *ctx, int path, uint32_t band_cap);
 
+/* The shared-hash screen in front of the table / band kernels (an exact
+ * shortcut inside `mash dist`, drep/d_cluster.py:569-573): Mash's merge of two
+ * sketches that share no hash is common 0, denominator min(s, |A| + |B|), so
+ * the sketch entries are grouped by value (radix sort on the device), the
+ * (row tile, column) cells whose genomes share a hash are listed, the kernels
+ * run on those only and every other pair is written as no-shared-hash.
+ *   DREPHIP_SCREEN_AUTO  on when N >= 4096 and the pair checks the grouping
+ *                        implies stay below (pairs x s) / 16 (else the dense
+ *                        item plan runs);
+ *   DREPHIP_SCREEN_ON    always (unless N x s >= 2^32);
+ *   DREPHIP_SCREEN_OFF   never.
+ * The environment variable DREPHIP_AP_SCREEN (0/1/2) overrides the mode. */
+#define DREPHIP_SCREEN_AUTO 0
+#define DREPHIP_SCREEN_ON 1
+#define DREPHIP_SCREEN_OFF 2
+int drephip_set_allpairs_screen(drephip_ctx *ctx, int mode);
+/* The last all-pairs call's screen: whether it replaced the dense plan, the
+ * sketch entries grouped, the runs of equal keys, the pair checks and the
+ * marked (row tile, column) cells. */
+int drephip_last_screen_stats(drephip_ctx *ctx, int *used, uint64_t *entries, uint64_t *runs, uint64_t *checks,
+                              uint64_t *marked);
+
 /* ---------------------------------------------------------- primary clustering
  * Replaces: scipy.cluster.hierarchy.linkage(squareform(dist), method) in
  * cluster_hierarchical (drep/d_cluster.py:447-453), called from
@@ -322,7 +344,8 @@ int drephip_set_timing(drephip_ctx *ctx, int kernels);
 
 /* Per-launch timing of the last sketch/allpairs call on this context
  * (milliseconds, from HIP events on the launch stream): which = 0 sketch hash
- * kernel, 1 sketch finalize kernel, 2 allpairs kernel, 3 table build kernel.
+ * kernel, 1 sketch finalize kernel, 2 allpairs kernel, 3 table build kernel,
+ * 4 the shared-hash screen (grouping + lists, including its host round trips).
  * Returns the count of launches summed into *ms. */
 int drephip_last_kernel_ms(drephip_ctx *ctx, int which, double *ms, int *launches);
 

@@ -1,0 +1,142 @@
+"""The shared-hash screen in front of the all-pairs kernels (screen.hip):
+every pair that shares no hash is written as Mash's merge gives it (common 0,
+denominator min(s, |A| + |B|)), the others by the LIST kernels.  Checked bit
+for bit against the C oracle's Mash merge (reference: `mash dist`,
+drep/d_cluster.py:569-573) and against the unscreened (dense) path, on
+sketches built to stress it: families sharing values at every rank position,
+partial sketches, hashes that agree in their low 32 bits only (the sort key),
+values shared by many genomes, genomes sharing nothing, and row segments
+(the sharded path's slices)."""
+import numpy as np
+import pytest
+
+import oracle
+from drep_amd import _lib
+
+pytestmark = pytest.mark.gpu
+UMAX = np.iinfo(np.uint64).max
+
+
+def planted_sketches(N, s, seed, fam=6, partial_every=7, lo_twins=40, hub=True):
+    """N sorted sketches: families of `fam` genomes draw from a shared pool
+    (so family members share hashes anywhere in the rank order), every
+    partial_every-th genome is partial, `lo_twins` hashes are copied to
+    another genome with only their high word changed (equal sort keys, no
+    shared hash), and one hub value sits in a third of all genomes."""
+    rng = np.random.default_rng(seed)
+    H = np.full((N, s), UMAX, dtype=np.uint64)
+    NH = np.zeros(N, dtype=np.uint32)
+    hubv = np.uint64(rng.integers(1, 1 << 40))
+    pools = {}
+    for g in range(N):
+        f = g // fam
+        if f not in pools:
+            pools[f] = rng.integers(1, 1 << 62, size=3 * s, dtype=np.uint64)
+        own = rng.integers(1, 1 << 62, size=s, dtype=np.uint64)
+        take = rng.random(3 * s) < 0.3
+        vals = np.unique(np.concatenate([pools[f][take], own] + ([np.array([hubv])] if hub and g % 3 == 0 else [])))
+        n = s if g % partial_every else int(rng.integers(1, s))
+        vals = vals[:n]
+        H[g, :len(vals)] = vals
+        NH[g] = len(vals)
+    for _ in range(lo_twins):
+        a, b = rng.integers(0, N, 2)
+        if a == b or NH[a] == 0 or NH[b] == 0:
+            continue
+        v = H[a, rng.integers(0, NH[a])]
+        twin = (v & np.uint64(0xFFFFFFFF)) | (np.uint64(rng.integers(1, 1 << 30)) << np.uint64(32))
+        if twin in H[b, :NH[b]] or twin in H[a, :NH[a]]:
+            continue
+        row = np.sort(np.concatenate([H[b, :NH[b]], [twin]]))[:s]
+        H[b, :] = UMAX
+        H[b, :len(row)] = row
+        NH[b] = len(row)
+    return H, NH
+
+
+def run(ctx, H, NH, mode, want_denom=True):
+    ctx.set_allpairs_screen(mode)
+    c, d = ctx.allpairs(H, NH, want_denom=want_denom)
+    return c, d, ctx.screen_stats()
+
+
+@pytest.mark.parametrize("s,N", [(64, 300), (1000, 200), (2048, 96), (4096, 80)])
+def test_screen_matches_oracle_and_dense(s, N):
+    H, NH = planted_sketches(N, s, seed=s + N)
+    oc, od = oracle.allpairs(H, NH, s, threads=8)
+    with _lib.Context(0, 21, s, 42) as ctx:
+        c, d, st = run(ctx, H, NH, ctx.SCREEN_ON)
+        assert st["used"] and st["marked"] > 0 and st["entries"] == int(NH.sum())
+        assert np.array_equal(c, oc) and np.array_equal(d, od)
+        c2, d2, st2 = run(ctx, H, NH, ctx.SCREEN_OFF)
+        assert not st2["used"]
+        assert np.array_equal(c2, c) and np.array_equal(d2, d)
+    assert (oc > 0).sum() > N          # families and the hub: many pairs share hashes
+    assert (oc == 0).sum() > N         # and many share none
+
+
+def test_screen_nothing_shared_and_all_shared():
+    s, N = 200, 150
+    rng = np.random.default_rng(11)
+    H = np.sort(rng.permutation(np.arange(1, N * s + 1, dtype=np.uint64) * np.uint64(7919)).reshape(N, s), axis=1)
+    NH = np.full(N, s, dtype=np.uint32)
+    NH[::5] = 37
+    H[::5, 37:] = UMAX
+    with _lib.Context(0, 21, s, 42) as ctx:
+        c, d, st = run(ctx, H, NH, ctx.SCREEN_ON)
+        assert st["used"] and st["marked"] == 0
+        oc, od = oracle.allpairs(H, NH, s, threads=8)
+        assert np.array_equal(c, oc) and np.array_equal(d, od) and c.max() == 0
+        # every genome identical: every cell marked
+        same = np.tile(np.sort(rng.integers(1, 1 << 60, size=s, dtype=np.uint64)), (N, 1))
+        c, d, st = run(ctx, same, np.full(N, s, np.uint32), ctx.SCREEN_ON)
+        assert (c == s).all() and (d == s).all()
+        # auto mode refuses the all-shared set (the dense path is cheaper)
+        ctx.set_allpairs_screen(ctx.SCREEN_AUTO)
+        import os
+        os.environ["DREPHIP_SCREEN_MIN_N"] = "2"
+        try:
+            c, d = ctx.allpairs(same, np.full(N, s, np.uint32), want_denom=True)
+            assert not ctx.screen_stats()["used"] and (c == s).all()
+        finally:
+            os.environ.pop("DREPHIP_SCREEN_MIN_N")
+
+
+@pytest.mark.parametrize("s", [1000, 4096])
+def test_screen_row_segments(s):
+    """Row ranges (a rank's slice of the triangle): the screen marks only
+    pairs whose smaller genome is a row of the call."""
+    N = 120
+    H, NH = planted_sketches(N, s, seed=5 * s)
+    oc, od = oracle.allpairs(H, NH, s, threads=8)
+
+    def start(i):
+        return i * N - i * (i + 1) // 2
+    with _lib.Context(0, 21, s, 42) as ctx:
+        ctx.set_allpairs_screen(ctx.SCREEN_ON)
+        for r0, r1 in ((0, 17), (17, 64), (64, 119), (118, 119)):
+            n = start(r1) - start(r0)
+            co = np.zeros(n, np.uint16)
+            do = np.zeros(n, np.uint16)
+            ctx.allpairs_rows(H, NH, r0, r1, co, do)
+            assert ctx.screen_stats()["used"]
+            assert np.array_equal(co, oc[start(r0):start(r1)]), (r0, r1)
+            assert np.array_equal(do, od[start(r0):start(r1)]), (r0, r1)
+
+
+def test_screen_auto_on_family_sets():
+    """Auto mode on sketches of synthetic genome families (the bench's
+    generator; many unrelated pairs): the screen is taken and gives the
+    oracle's counts."""
+    import os
+    h, nh = oracle.sketch_synth(0, 200, 300_000, seed=9, family_size=20, s=1000, threads=8)
+    os.environ["DREPHIP_SCREEN_MIN_N"] = "2"
+    try:
+        with _lib.Context(0, 21, 1000, 42) as ctx:
+            c, d = ctx.allpairs(h, nh, want_denom=True)
+            st = ctx.screen_stats()
+    finally:
+        os.environ.pop("DREPHIP_SCREEN_MIN_N")
+    oc, od = oracle.allpairs(h, nh, 1000, threads=8)
+    assert np.array_equal(c, oc) and np.array_equal(d, od)
+    assert st["used"] and st["entries"] == int(nh.sum())

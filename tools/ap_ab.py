@@ -40,7 +40,7 @@ ctx.allpairs_device(hh.data_ptr(), nn.data_ptr(), N, 0, N, ref.data_ptr(), None,
 torch.cuda.synchronize()
 out = {"N": N, "s": s, "pairs": npairs, "merge_s": time.perf_counter() - t0, "cfg": {}}
 print("reference (literal merge) done in %.2f s" % out["merge_s"], file=sys.stderr, flush=True)
-ctx.set_timing(True, kernels=[2])
+ctx.set_timing(True, kernels=[2, 4])
 got = torch.empty(npairs, dtype=torch.int16, device=dev)
 for rd in range(rounds):
     for c in (cfgs or [-1]):
@@ -48,9 +48,15 @@ for rd in range(rounds):
             os.environ[VAR] = str(c)
         got.fill_(0x7FFF)
         ctx.allpairs_device(hh.data_ptr(), nn.data_ptr(), N, 0, N, got.data_ptr(), None, st)
-        ms = ctx.kernel_ms(2)[0]
+        # the all-pairs kernel (with the no-shared-hash fill when screened) plus the screen itself
+        ms = ctx.kernel_ms(2)[0] + (ctx.kernel_ms(4)[0] if hasattr(_lib.lib(), "drephip_last_screen_stats") else 0.0)
         bad = int((got != ref).sum().item())
         r = out["cfg"].setdefault(str(c), {"ms": [], "mismatches": 0})
+        if hasattr(_lib.lib(), "drephip_last_screen_stats"):       # libraries from before round 4 have no screen
+            r["screen"] = ctx.screen_stats()
+            r["screen_ms"] = ctx.kernel_ms(4)[0]
+            print("  stats %s=%d: %s, screen %.3f ms" % (VAR, c, r["screen"], r["screen_ms"]), file=sys.stderr,
+                  flush=True)
         r["ms"].append(ms); r["mismatches"] += bad
         print("round %d %s=%d: %.3f ms, %d mismatches" % (rd, VAR, c, ms, bad), file=sys.stderr, flush=True)
 for c, r in out["cfg"].items():
