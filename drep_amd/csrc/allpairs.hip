@@ -50,6 +50,7 @@ constexpr uint32_t kFamTwins = 0x40;            // k_build_q32 family byte: the 
 constexpr uint32_t kFamFailed = 0xFF;           // ... no family worked (the row's pairs are merged literally)
 constexpr uint32_t kLdsBudget = 156 * 1024;     // dynamic LDS per workgroup
 constexpr uint32_t kScreenMinN = 4096;          // genomes from which the shared-hash screen runs (auto)
+constexpr uint32_t kListCols = 512;             // screened columns per whole-row LIST item
 
 __host__ __device__ __forceinline__ uint64_t cond_index(uint64_t i, uint64_t j, uint64_t N) {
     return i * N - i * (i + 1) / 2 + (j - i - 1);
@@ -1361,7 +1362,10 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
     const uint32_t min_n = mn ? (uint32_t)atoi(mn) : kScreenMinN;
     ScreenResult scr;
     if (smode == DREPHIP_SCREEN_ON || (smode == DREPHIP_SCREEN_AUTO && N >= min_n)) {
-        int rc = screen_impl(ctx, d_hashes, d_nhash, N, row0, row1, R, path == DREPHIP_AP_BAND ? kBandCols : kApCols,
+        // LIST items: the band kernel's per-column LDS state holds kBandCols
+        // columns; the whole-row kernel takes up to kListCols per item, so a
+        // row tile's image is loaded once for most tiles
+        int rc = screen_impl(ctx, d_hashes, d_nhash, N, row0, row1, R, path == DREPHIP_AP_BAND ? kBandCols : kListCols,
                              npairs, smode == DREPHIP_SCREEN_ON, st, &scr);
         if (rc) return rc;
         ctx->last_screen = scr;

@@ -39,8 +39,10 @@
 #include <hipcub/device/device_scan.hpp>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 namespace drephip {
 
@@ -65,92 +67,217 @@ __global__ void k_screen_total(const uint32_t *__restrict__ nh, uint64_t *__rest
     if (threadIdx.x == 0) eoff[N] = eoff[N - 1] + nh[N - 1];
 }
 
-// runs of >= 2 equal keys in the sorted keys: (start, length) appended to
-// runs (wave-aggregated atomics), the sum of length (length - 1) / 2 to *E
-__global__ __launch_bounds__(kScWG) void k_screen_runs(const uint32_t *__restrict__ keys, uint32_t M,
-                                                       uint2 *__restrict__ runs, uint32_t *__restrict__ nruns,
-                                                       unsigned long long *__restrict__ E) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t stride = gridDim.x * kScWG;
-    // every lane of a wave runs the same number of iterations (ballots below)
-    for (uint32_t i0 = blockIdx.x * kScWG; i0 < M; i0 += stride) {
-        const uint32_t i = i0 + threadIdx.x;
-        bool emit = false;
-        uint32_t m = 0;
-        if (i < M) {
-            const uint32_t k = keys[i];
-            const bool head = i == 0 || keys[i - 1] != k;
-            if (head && i + 1 < M && keys[i + 1] == k) {
-                uint32_t j = i + 2;
-                while (j < M && keys[j] == k) j++;
-                m = j - i;
-                emit = true;
-            }
-        }
-        const uint64_t mask = __ballot(emit);
-        if (mask == 0) continue;
-        uint32_t base = 0;
-        unsigned long long e = emit ? (unsigned long long)m * (m - 1) / 2 : 0;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) e += __shfl_xor(e, o, 64);
-        const uint32_t first = (uint32_t)__ffsll((long long)mask) - 1;
-        if (lane == first) {
-            base = atomicAdd(nruns, (uint32_t)__popcll(mask));
-            atomicAdd(E, e);
-        }
-        base = __shfl(base, first, 64);
-        if (emit) {
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
-            runs[base + rank] = make_uint2(i, m);
-        }
+// Runs of equal keys in the sorted keys, without a serial walk: head flags
+// (k_run_flags), their inclusive scan = run id + 1 per position, the heads and
+// tails writing each run's bounds (k_run_bounds), then the runs of >= 2
+// entries appended with their first genome (k_run_collect).  (A head thread
+// walking its run measured 35.6 ms at 10^8 entries, the walks' dependent
+// loads holding every wave with a head.)
+__global__ __launch_bounds__(kScWG) void k_run_flags(const uint32_t *__restrict__ keys, uint32_t M,
+                                                     uint32_t *__restrict__ flag) {
+    for (uint32_t i = blockIdx.x * kScWG + threadIdx.x; i < M; i += gridDim.x * kScWG)
+        flag[i] = (i == 0 || keys[i - 1] != keys[i]) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(kScWG) void k_run_bounds(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ rid,
+                                                      uint32_t M, uint32_t *__restrict__ rstart,
+                                                      uint32_t *__restrict__ rend) {
+    for (uint32_t i = blockIdx.x * kScWG + threadIdx.x; i < M; i += gridDim.x * kScWG) {
+        const uint32_t k = keys[i];
+        const uint32_t r = rid[i] - 1;
+        if (i == 0 || keys[i - 1] != k) rstart[r] = i;
+        if (i + 1 == M || keys[i + 1] != k) rend[r] = i + 1;
     }
 }
 
-// One wave per run: the run's entries in 64-entry tiles (x tile <= y tile);
-// lane l holds y entry yb + l, the x tile's entries are broadcast by readlane.
-// Pairs with equal 64-bit hashes mark (tile of min g, max g) when the smaller
-// genome is a row of this call.
-__global__ __launch_bounds__(kScWG) void k_screen_mark(const uint32_t *__restrict__ vals, const uint64_t *__restrict__ H,
+// runs of >= 2 entries: (start, length) and their first (smallest) genome --
+// a run lists its entries in ascending genome order (the radix sort is
+// stable and the keys were written genome by genome).  Two passes over the
+// same contiguous blocks of runs, no contended atomics: k_run_count counts
+// each block's runs of >= 2 (cnt[b]) and their pair checks (chk[b]); after a
+// scan of the counts k_run_write writes each block's runs at its offset, in
+// order.  (One atomic counter for all ~5x10^6 runs serialised the pass:
+// 16 ms at 10^8 entries.)
+constexpr uint32_t kRunBlocks = 4096;
+__device__ __forceinline__ uint32_t block_exclusive_count(bool f, uint32_t *wsum, uint32_t *total) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t mask = __ballot(f);
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+    if (lane == 0) wsum[wave] = (uint32_t)__popcll(mask);
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+    for (uint32_t w = 0; w < kScWG / 64; w++) {
+        if (w < wave) base += wsum[w];
+        tot += wsum[w];
+    }
+    __syncthreads();
+    *total = tot;
+    return base + below;
+}
+
+__global__ __launch_bounds__(kScWG) void k_run_count(const uint32_t *__restrict__ rstart,
+                                                     const uint32_t *__restrict__ rend, uint32_t nr, uint32_t per,
+                                                     uint32_t *__restrict__ cnt2, uint32_t *__restrict__ cnt3,
+                                                     unsigned long long *__restrict__ chk) {
+    __shared__ uint32_t wsum[2][kScWG / 64];
+    __shared__ unsigned long long esum[kScWG / 64];
+    const uint32_t r0 = blockIdx.x * per, r1 = min(r0 + per, nr);
+    uint32_t c2 = 0, c3 = 0;
+    unsigned long long e = 0;
+    for (uint32_t r = r0 + threadIdx.x; r < r1; r += kScWG) {
+        const uint32_t m = rend[r] - rstart[r];
+        c2 += m == 2;
+        c3 += m >= 3;
+        if (m >= 2) e += (unsigned long long)m * (m - 1) / 2;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        c2 += __shfl_xor(c2, o, 64);
+        c3 += __shfl_xor(c3, o, 64);
+        e += __shfl_xor(e, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        wsum[0][threadIdx.x >> 6] = c2;
+        wsum[1][threadIdx.x >> 6] = c3;
+        esum[threadIdx.x >> 6] = e;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t2 = 0, t3 = 0;
+        unsigned long long te = 0;
+        for (int w = 0; w < kScWG / 64; w++) { t2 += wsum[0][w]; t3 += wsum[1][w]; te += esum[w]; }
+        cnt2[blockIdx.x] = t2;
+        cnt3[blockIdx.x] = t3;
+        chk[blockIdx.x] = te;
+    }
+}
+
+// the runs of two entries (chance sharing, mostly) as their start positions
+// (pairs), the longer ones with their first genome (runs, rfirst, ridx)
+__global__ __launch_bounds__(kScWG) void k_run_write(const uint32_t *__restrict__ rstart,
+                                                     const uint32_t *__restrict__ rend, uint32_t nr, uint32_t per,
+                                                     const uint32_t *__restrict__ off2, const uint32_t *__restrict__ off3,
+                                                     const uint32_t *__restrict__ vals, uint32_t s,
+                                                     uint32_t *__restrict__ pairs, uint2 *__restrict__ runs,
+                                                     uint32_t *__restrict__ rfirst, uint32_t *__restrict__ ridx) {
+    __shared__ uint32_t wsum[kScWG / 64];
+    const uint32_t r0 = blockIdx.x * per, r1 = min(r0 + per, nr);
+    uint32_t b2 = off2[blockIdx.x], b3 = off3[blockIdx.x];
+    for (uint32_t rb = r0; rb < r1; rb += kScWG) {                  // uniform trip count
+        const uint32_t r = rb + threadIdx.x;
+        uint32_t st = 0, m = 0;
+        if (r < r1) { st = rstart[r]; m = rend[r] - st; }
+        uint32_t t2, t3;
+        const uint32_t q2 = b2 + block_exclusive_count(m == 2, wsum, &t2);
+        const uint32_t q3 = b3 + block_exclusive_count(m >= 3, wsum, &t3);
+        if (m == 2) pairs[q2] = st;
+        if (m >= 3) {
+            runs[q3] = make_uint2(st, m);
+            rfirst[q3] = vals[st] / s;
+            ridx[q3] = q3;
+        }
+        b2 += t2;
+        b3 += t3;
+    }
+}
+
+// runs of two entries: one lane each; equal 64-bit hashes of two genomes
+// mark (row tile of the smaller, larger) straight in the bitmap
+__global__ __launch_bounds__(kScWG) void k_screen_mark2(const uint32_t *__restrict__ vals, const uint64_t *__restrict__ H,
+                                                        uint32_t s, const uint32_t *__restrict__ pairs, uint32_t n2,
+                                                        uint32_t row0, uint32_t row1, uint32_t rshift, uint32_t NW,
+                                                        uint32_t *__restrict__ bm) {
+    for (uint32_t q = blockIdx.x * kScWG + threadIdx.x; q < n2; q += gridDim.x * kScWG) {
+        const uint32_t st = pairs[q];
+        const uint32_t ix = vals[st], iy = vals[st + 1];
+        const uint32_t gx = ix / s, gy = iy / s;          // gx <= gy (a run is in genome order)
+        if (gx == gy || gx < row0 || gx >= row1 || H[ix] != H[iy]) continue;
+        atomicOr(bm + (uint64_t)((gx - row0) >> rshift) * NW + (gy >> 5), 1u << (gy & 31));
+    }
+}
+
+// Marking, one workgroup per chunk of kMarkChunk runs taken in order of their
+// first genome (runs sorted by it): a family's runs -- each of its ~10^3
+// shared hashes is one -- land in the same few chunks, so their pairs are
+// OR-ed into an LDS window of the bitmap (kMarkTiles row tiles from the
+// chunk's first genome x kMarkCols columns; rows padded to 65 words so the
+// tiles of one column sit in different banks) and each window word reaches
+// HBM once, by one atomicOr.  Pairs outside the window (chance sharing across
+// families) go to the bitmap directly.  Inside a run a wave compares every
+// entry pair: lane = x entry, the y entries broadcast by readlane; a pair of
+// equal 64-bit hashes of two genomes marks (row tile of gx, gy), gx < gy.
+// The x entries are in ascending genome order, so lanes of one row tile are
+// adjacent: only the first ok lane of each tile marks (one LDS atomic per
+// tile and y, none on a shared word).
+constexpr uint32_t kMarkWG = 1024;
+constexpr uint32_t kMarkChunk = 256;
+constexpr uint32_t kMarkTiles = 128;
+constexpr uint32_t kMarkCols = 2048;
+constexpr uint32_t kMarkWords = kMarkCols / 32;
+constexpr uint32_t kMarkStride = kMarkWords + 1;
+__global__ __launch_bounds__(kMarkWG) void k_screen_mark(const uint32_t *__restrict__ vals, const uint64_t *__restrict__ H,
                                                        uint32_t s, const uint2 *__restrict__ runs,
-                                                       const uint32_t *__restrict__ nruns_p, uint32_t row0,
-                                                       uint32_t row1, uint32_t rshift, uint32_t NW,
+                                                       const uint32_t *__restrict__ order,
+                                                       const uint32_t *__restrict__ rfirst_sorted, uint32_t nruns,
+                                                       uint32_t row0, uint32_t row1, uint32_t rshift, uint32_t NW,
                                                        uint32_t *__restrict__ bm) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t nruns = *nruns_p;
-    const uint32_t nwaves = gridDim.x * (kScWG / 64);
-    for (uint32_t r = __builtin_amdgcn_readfirstlane(blockIdx.x * (kScWG / 64) + (threadIdx.x >> 6)); r < nruns;
-         r += nwaves) {
-        const uint2 run = runs[r];
+    __shared__ uint32_t win[kMarkTiles * kMarkStride];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t q0 = blockIdx.x * kMarkChunk;
+    const uint32_t q1 = min(q0 + kMarkChunk, nruns);
+    for (uint32_t i = threadIdx.x; i < kMarkTiles * kMarkStride; i += kMarkWG) win[i] = 0;
+    // window: row tiles [t_lo, t_lo + kMarkTiles), columns [c_lo, c_lo + kMarkCols)
+    const uint32_t g_lo = rfirst_sorted[q0];
+    const uint32_t t_lo = g_lo > row0 ? (g_lo - row0) >> rshift : 0;
+    const uint32_t c_lo = g_lo & ~31u;
+    __syncthreads();
+    for (uint32_t q = q0 + wave; q < q1; q += kMarkWG / 64) {
+        const uint2 run = runs[order[q]];
         const uint32_t start = run.x, m = run.y;
-        for (uint32_t yb = 0; yb < m; yb += 64) {
-            const uint32_t y = yb + lane;
-            const bool vy_ok = y < m;
-            const uint32_t iy = vals[start + (vy_ok ? y : m - 1)];
-            const uint32_t gy = iy / s;
-            const uint64_t vy = H[iy];
-            for (uint32_t xb = 0; xb <= yb; xb += 64) {
-                const uint32_t xl = xb + lane;
-                const uint32_t ix = vals[start + (xl < m ? xl : m - 1)];
-                const uint32_t gxl = ix / s;
-                const uint64_t vxl = H[ix];
-                const uint32_t nx = min(64u, m - xb);
-                for (uint32_t xi = 0; xi < nx; xi++) {
-                    const uint32_t vlo = __builtin_amdgcn_readlane((uint32_t)vxl, xi);
-                    const uint32_t vhi = __builtin_amdgcn_readlane((uint32_t)(vxl >> 32), xi);
-                    const uint32_t gx = __builtin_amdgcn_readlane(gxl, xi);
-                    const bool ok = vy_ok && xb + xi < y && (uint32_t)vy == vlo && (uint32_t)(vy >> 32) == vhi;
-                    if (__ballot(ok) == 0) continue;
-                    if (ok) {
-                        const uint32_t a = min(gx, gy), b = max(gx, gy);
-                        if (a >= row0 && a < row1) {
-                            uint32_t *w = bm + (uint64_t)((a - row0) >> rshift) * NW + (b >> 5);
-                            const uint32_t bit = 1u << (b & 31);
-                            if (!(*w & bit)) atomicOr(w, bit);
-                        }
-                    }
+        for (uint32_t xb = 0; xb + 1 < m; xb += 64) {
+            const uint32_t x = xb + lane;
+            const uint32_t ix = vals[start + (x < m ? x : m - 1)];
+            const uint32_t gx = ix / s;
+            const uint64_t vx = H[ix];
+            const bool x_ok = x < m && gx >= row0 && gx < row1;
+            const uint32_t tx = x_ok ? (gx - row0) >> rshift : 0xFFFFFFFFu;
+            // first lane of its row tile among the x tile (lanes are in genome order)
+            const uint32_t tprev = __shfl_up(tx, 1, 64);
+            const bool tile_head = lane == 0 || tprev != tx;
+            for (uint32_t yb = xb; yb < m; yb += 64) {
+                const uint32_t yl = yb + lane;
+                const uint32_t iyl = vals[start + (yl < m ? yl : m - 1)];
+                const uint32_t gyl = iyl / s;
+                const uint64_t vyl = H[iyl];
+                const uint32_t ny = min(64u, m - yb);
+                for (uint32_t yi = 0; yi < ny; yi++) {
+                    const uint32_t vlo = __builtin_amdgcn_readlane((uint32_t)vyl, yi);
+                    const uint32_t vhi = __builtin_amdgcn_readlane((uint32_t)(vyl >> 32), yi);
+                    const uint32_t gy = __builtin_amdgcn_readlane(gyl, yi);
+                    // x before y in the run: gx <= gy (gx == gy: two hashes of one
+                    // genome with equal low words, never equal hashes)
+                    const bool ok = x_ok && x < yb + yi && (uint32_t)vx == vlo && (uint32_t)(vx >> 32) == vhi && gx != gy;
+                    const uint64_t okm = __ballot(ok);
+                    if (okm == 0) continue;
+                    // the first ok lane of each row tile marks (lane - 1 not ok, or another tile)
+                    const bool prev_ok = lane > 0 && ((okm >> (lane - 1)) & 1ull);
+                    if (!ok || (prev_ok && !tile_head)) continue;
+                    const uint32_t bit = 1u << (gy & 31);
+                    if (tx - t_lo < kMarkTiles && gy - c_lo < kMarkCols)
+                        atomicOr(&win[(tx - t_lo) * kMarkStride + ((gy - c_lo) >> 5)], bit);
+                    else
+                        atomicOr(bm + (uint64_t)tx * NW + (gy >> 5), bit);
                 }
             }
         }
+    }
+    __syncthreads();
+    const uint32_t tmax = ((row1 - row0) + (1u << rshift) - 1) >> rshift;
+    for (uint32_t i = threadIdx.x; i < kMarkTiles * kMarkStride; i += kMarkWG) {
+        const uint32_t v = win[i];
+        if (!v) continue;
+        const uint32_t t = t_lo + i / kMarkStride, w = (c_lo >> 5) + i % kMarkStride;
+        if (t < tmax && w < NW) atomicOr(bm + (uint64_t)t * NW + w, v);
     }
 }
 
@@ -226,6 +353,31 @@ __global__ __launch_bounds__(kScWG) void k_screen_denoms(const uint32_t *__restr
     }
 }
 
+// DREPHIP_SCREEN_PROF=1: HIP events between the phases, printed to stderr
+struct ScreenProf {
+    bool on = getenv("DREPHIP_SCREEN_PROF") != nullptr;
+    std::vector<std::pair<const char *, hipEvent_t>> ev;
+    void mark(const char *name, hipStream_t st) {
+        if (!on) return;
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return;
+        (void)hipEventRecord(e, st);
+        ev.push_back({name, e});
+    }
+    ~ScreenProf() {
+        if (!on || ev.empty()) return;
+        (void)hipEventSynchronize(ev.back().second);
+        fprintf(stderr, "[drephip] screen phases (ms):");
+        for (size_t i = 1; i < ev.size(); i++) {
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, ev[i - 1].second, ev[i].second);
+            fprintf(stderr, " %s %.3f", ev[i].first, ms);
+        }
+        fprintf(stderr, "\n");
+        for (auto &p : ev) (void)hipEventDestroy(p.second);
+    }
+};
+
 template <class T>
 static int hip_scan(drephip_ctx *ctx, const char *name, const uint32_t *in, T *out, uint32_t n, hipStream_t st) {
     size_t tb = 0;
@@ -247,23 +399,31 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
     if ((rc = scratch(ctx, "sc_eoff", (N + 1) * 8ull, (void **)&d_eoff))) return rc;
     if ((rc = pinned_host(ctx, "sc_tot", 32, (void **)&h_tot))) return rc;
     timing_mark(ctx, 4, st, true);
+    ScreenProf prof;
+    prof.mark("start", st);
     if ((rc = hip_scan(ctx, "sc_scan_tmp0", d_nhash, d_eoff, N, st))) return rc;
     hipLaunchKernelGGL(k_screen_total, dim3(1), dim3(64), 0, st, d_nhash, d_eoff, N);
     HIPC(hipMemcpyAsync(h_tot, d_eoff + N, 8, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));
     const uint32_t M = (uint32_t)h_tot[0];
-    uint32_t *k_in, *k_out, *v_in, *v_out, *d_nruns;
+    if (M < 2) {
+        // fewer than two sketch entries: no pair shares a hash; every pair
+        // gets the no-shared-hash fill, no LIST work
+        timing_mark(ctx, 4, st, false);
+        res->entries = M;
+        res->use = true;
+        return DREPHIP_OK;
+    }
+    uint32_t *k_in, *k_out, *v_in, *v_out;
     uint2 *d_runs;
-    unsigned long long *d_E;
     if ((rc = scratch(ctx, "sc_kin", M * 4ull + 16, (void **)&k_in))) return rc;
     if ((rc = scratch(ctx, "sc_kout", M * 4ull + 16, (void **)&k_out))) return rc;
     if ((rc = scratch(ctx, "sc_vin", M * 4ull + 16, (void **)&v_in))) return rc;
     if ((rc = scratch(ctx, "sc_vout", M * 4ull + 16, (void **)&v_out))) return rc;
     if ((rc = scratch(ctx, "sc_runs", (M / 2 + 1) * 8ull, (void **)&d_runs))) return rc;
-    if ((rc = scratch(ctx, "sc_cnt", 16, (void **)&d_nruns))) return rc;
-    d_E = (unsigned long long *)(d_nruns + 2);
-    HIPC(hipMemsetAsync(d_nruns, 0, 16, st));
+    prof.mark("offsets+alloc", st);
     hipLaunchKernelGGL(k_screen_keys, dim3(N), dim3(kScWG), 0, st, d_hashes, d_nhash, d_eoff, s, k_in, v_in);
+    prof.mark("keys", st);
     {
         size_t tb = 0;
         HIPC(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k_in, k_out, v_in, v_out, M, 0, 32, st));
@@ -271,15 +431,60 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
         if ((rc = scratch(ctx, "sc_sort_tmp", std::max<size_t>(tb, 16), &tmp))) return rc;
         HIPC(hipcub::DeviceRadixSort::SortPairs(tmp, tb, k_in, k_out, v_in, v_out, M, 0, 32, st));
     }
+    prof.mark("sort", st);
     const uint32_t rgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, (M + kScWG - 1) / kScWG));
-    hipLaunchKernelGGL(k_screen_runs, dim3(rgrid), dim3(kScWG), 0, st, k_out, M, d_runs, d_nruns, d_E);
-    HIPC(hipGetLastError());
-    HIPC(hipMemcpyAsync(h_tot, d_nruns, 16, hipMemcpyDeviceToHost, st));
+    // runs: flags -> run ids (scan) -> bounds -> runs of >= 2 with their first genome
+    uint32_t *flag = k_in, *rid = v_in, *rstart, *rend, *rfirst, *ridx, *rfirst_s, *ridx_s;
+    if ((rc = scratch(ctx, "sc_rstart", M * 4ull + 16, (void **)&rstart))) return rc;
+    if ((rc = scratch(ctx, "sc_rend", M * 4ull + 16, (void **)&rend))) return rc;
+    hipLaunchKernelGGL(k_run_flags, dim3(rgrid), dim3(kScWG), 0, st, k_out, M, flag);
+    {
+        size_t tb = 0;
+        HIPC(hipcub::DeviceScan::InclusiveSum(nullptr, tb, flag, rid, M, st));
+        void *tmp;
+        if ((rc = scratch(ctx, "sc_scan_tmp3", std::max<size_t>(tb, 16), &tmp))) return rc;
+        HIPC(hipcub::DeviceScan::InclusiveSum(tmp, tb, flag, rid, M, st));
+    }
+    hipLaunchKernelGGL(k_run_bounds, dim3(rgrid), dim3(kScWG), 0, st, k_out, rid, M, rstart, rend);
+    HIPC(hipMemcpyAsync(h_tot, rid + (M - 1), 4, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));
-    const uint32_t nruns = ((const uint32_t *)h_tot)[0];
-    const uint64_t E = ((const unsigned long long *)h_tot)[1];
+    const uint32_t nr = ((const uint32_t *)h_tot)[0];             // distinct keys
+    // the run lists (at most M / 2 runs of >= 2); rfirst / ridx reuse the key
+    // and value inputs of the sort, which are free now
+    rfirst = flag;
+    ridx = rid;
+    if ((rc = scratch(ctx, "sc_rfirst_s", (M / 2 + 1) * 4ull, (void **)&rfirst_s))) return rc;
+    if ((rc = scratch(ctx, "sc_ridx_s", (M / 2 + 1) * 4ull, (void **)&ridx_s))) return rc;
+    const uint32_t per = (nr + kRunBlocks - 1) / kRunBlocks;
+    uint32_t *bcnt2, *bcnt3, *boff2, *boff3, *d_pairs;
+    unsigned long long *bchk;
+    if ((rc = scratch(ctx, "sc_bcnt2", (kRunBlocks + 1) * 4ull, (void **)&bcnt2))) return rc;
+    if ((rc = scratch(ctx, "sc_bcnt3", (kRunBlocks + 1) * 4ull, (void **)&bcnt3))) return rc;
+    if ((rc = scratch(ctx, "sc_boff2", (kRunBlocks + 1) * 4ull, (void **)&boff2))) return rc;
+    if ((rc = scratch(ctx, "sc_boff3", (kRunBlocks + 1) * 4ull, (void **)&boff3))) return rc;
+    if ((rc = scratch(ctx, "sc_bchk", kRunBlocks * 8ull, (void **)&bchk))) return rc;
+    if ((rc = scratch(ctx, "sc_pairs", (M / 2 + 1) * 4ull, (void **)&d_pairs))) return rc;
+    HIPC(hipMemsetAsync(bcnt2 + kRunBlocks, 0, 4, st));
+    HIPC(hipMemsetAsync(bcnt3 + kRunBlocks, 0, 4, st));
+    hipLaunchKernelGGL(k_run_count, dim3(kRunBlocks), dim3(kScWG), 0, st, rstart, rend, nr, per, bcnt2, bcnt3, bchk);
+    if ((rc = hip_scan(ctx, "sc_scan_tmp4", bcnt2, boff2, kRunBlocks + 1, st))) return rc;
+    if ((rc = hip_scan(ctx, "sc_scan_tmp5", bcnt3, boff3, kRunBlocks + 1, st))) return rc;
+    hipLaunchKernelGGL(k_run_write, dim3(kRunBlocks), dim3(kScWG), 0, st, rstart, rend, nr, per, boff2, boff3, v_out, s,
+                       d_pairs, d_runs, rfirst, ridx);
+    HIPC(hipGetLastError());
+    unsigned long long *h_chk;
+    if ((rc = pinned_host(ctx, "sc_chk", kRunBlocks * 8ull, (void **)&h_chk))) return rc;
+    HIPC(hipMemcpyAsync(h_chk, bchk, kRunBlocks * 8ull, hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(h_tot, boff2 + kRunBlocks, 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync((uint32_t *)h_tot + 1, boff3 + kRunBlocks, 4, hipMemcpyDeviceToHost, st));
+    prof.mark("runs", st);
+    HIPC(hipStreamSynchronize(st));
+    const uint32_t n2 = ((const uint32_t *)h_tot)[0];           // runs of two entries
+    const uint32_t nruns = ((const uint32_t *)h_tot)[1];        // runs of three or more
+    uint64_t E = 0;
+    for (uint32_t b = 0; b < kRunBlocks; b++) E += h_chk[b];
     res->entries = M;
-    res->runs = nruns;
+    res->runs = (uint64_t)n2 + nruns;
     res->checks = E;
     // dense set: a pair check costs about as much as a few probes of the
     // dense kernels, which make ~s/2 probes per pair (DREPHIP_SCREEN_RATIO
@@ -300,18 +505,33 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
     if ((rc = scratch(ctx, "sc_titc", (ntiles + 1) * 4ull, (void **)&d_itc))) return rc;
     if ((rc = scratch(ctx, "sc_coff", (ntiles + 1) * 8ull, (void **)&d_coff))) return rc;
     if ((rc = scratch(ctx, "sc_ioff", (ntiles + 1) * 8ull, (void **)&d_ioff))) return rc;
+    prof.mark("readback+alloc", st);
     HIPC(hipMemsetAsync(d_bm, 0, (uint64_t)ntiles * NW * 4, st));
+    prof.mark("bitmap-clear", st);
     if (nruns) {
-        const uint32_t mgrid = std::max(1u, std::min(8192u, (nruns + 3) / 4));
-        hipLaunchKernelGGL(k_screen_mark, dim3(mgrid), dim3(kScWG), 0, st, v_out, d_hashes, s, d_runs, d_nruns, row0,
-                           row1, rshift, NW, d_bm);
+        // runs in order of their first genome (a family's runs together)
+        size_t tb = 0;
+        HIPC(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, rfirst, rfirst_s, ridx, ridx_s, nruns, 0, 32, st));
+        void *tmp;
+        if ((rc = scratch(ctx, "sc_sort_tmp2", std::max<size_t>(tb, 16), &tmp))) return rc;
+        HIPC(hipcub::DeviceRadixSort::SortPairs(tmp, tb, rfirst, rfirst_s, ridx, ridx_s, nruns, 0, 32, st));
+        prof.mark("run-sort", st);
+        hipLaunchKernelGGL(k_screen_mark, dim3((nruns + kMarkChunk - 1) / kMarkChunk), dim3(kMarkWG), 0, st, v_out,
+                           d_hashes, s, d_runs, ridx_s, rfirst_s, nruns, row0, row1, rshift, NW, d_bm);
     }
+    if (n2) {
+        const uint32_t g2 = std::max(1u, std::min(8192u, (n2 + kScWG - 1) / kScWG));
+        hipLaunchKernelGGL(k_screen_mark2, dim3(g2), dim3(kScWG), 0, st, v_out, d_hashes, s, d_pairs, n2, row0, row1,
+                           rshift, NW, d_bm);
+    }
+    prof.mark("mark", st);
     hipLaunchKernelGGL(k_screen_count, dim3(ntiles), dim3(kScWG), 0, st, d_bm, NW, C, d_cnt, d_itc);
     // the last entry of each scan holds the totals: count entries ntiles + 1, the last one zero
     HIPC(hipMemsetAsync(d_cnt + ntiles, 0, 4, st));
     HIPC(hipMemsetAsync(d_itc + ntiles, 0, 4, st));
     if ((rc = hip_scan(ctx, "sc_scan_tmp1", d_cnt, d_coff, ntiles + 1, st))) return rc;
     if ((rc = hip_scan(ctx, "sc_scan_tmp2", d_itc, d_ioff, ntiles + 1, st))) return rc;
+    prof.mark("count+scans", st);
     HIPC(hipMemcpyAsync(h_tot, d_coff + ntiles, 8, hipMemcpyDeviceToHost, st));
     HIPC(hipMemcpyAsync(h_tot + 1, d_ioff + ntiles, 8, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));
@@ -322,8 +542,10 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
     uint4 *d_items;
     if ((rc = scratch(ctx, "sc_list", std::max<uint64_t>(marked, 1) * 4, (void **)&d_list))) return rc;
     if ((rc = scratch(ctx, "sc_items", std::max<uint64_t>(nitems, 1) * 16, (void **)&d_items))) return rc;
+    prof.mark("readback+alloc", st);
     hipLaunchKernelGGL(k_screen_lists, dim3(ntiles), dim3(kScWG), 0, st, d_bm, NW, C, row0, R, d_cnt, d_coff, d_ioff,
                        d_list, d_items);
+    prof.mark("lists", st);
     timing_mark(ctx, 4, st, false);
     HIPC(hipGetLastError());
     res->use = true;
