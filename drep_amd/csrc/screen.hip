@@ -231,9 +231,25 @@ __global__ __launch_bounds__(kMarkWG) void k_screen_mark(const uint32_t *__restr
     const uint32_t t_lo = g_lo > row0 ? (g_lo - row0) >> rshift : 0;
     const uint32_t c_lo = g_lo & ~31u;
     __syncthreads();
+    // one cell mark: the LDS window when (tile, column) falls in it, else the bitmap
+    auto mark = [&](uint32_t t, uint32_t col, uint32_t bits) {
+        if (t - t_lo < kMarkTiles && col - c_lo < kMarkCols)
+            atomicOr(&win[(t - t_lo) * kMarkStride + ((col - c_lo) >> 5)], bits);
+        else
+            atomicOr(bm + (uint64_t)t * NW + (col >> 5), bits);
+    };
     for (uint32_t q = q0 + wave; q < q1; q += kMarkWG / 64) {
         const uint2 run = runs[order[q]];
         const uint32_t start = run.x, m = run.y;
+        // a run whose entries all hold one 64-bit hash (a hash shared by m
+        // genomes; only a low-word collision breaks this) takes the fast path
+        const uint64_t v0 = H[vals[start]];
+        bool same = true;
+        for (uint32_t b = 0; b < m && same; b += 64) {
+            const uint32_t x = b + lane;
+            const uint64_t v = x < m ? H[vals[start + x]] : v0;
+            same = __ballot(v != v0) == 0;
+        }
         for (uint32_t xb = 0; xb + 1 < m; xb += 64) {
             const uint32_t x = xb + lane;
             const uint32_t ix = vals[start + (x < m ? x : m - 1)];
@@ -246,8 +262,36 @@ __global__ __launch_bounds__(kMarkWG) void k_screen_mark(const uint32_t *__restr
             const bool tile_head = lane == 0 || tprev != tx;
             for (uint32_t yb = xb; yb < m; yb += 64) {
                 const uint32_t yl = yb + lane;
-                const uint32_t iyl = vals[start + (yl < m ? yl : m - 1)];
+                const bool y_ok = yl < m;
+                const uint32_t iyl = vals[start + (y_ok ? yl : m - 1)];
                 const uint32_t gyl = iyl / s;
+                if (same) {
+                    // every x before y pairs with y: for each row tile T among the
+                    // x entries (its first position p), every y after p marks
+                    // (T, gy).  The y lanes' columns, in genome order, form runs
+                    // of one bitmap word; each lane holds the OR of its own and the
+                    // later bits of its word (a segmented suffix scan), so a tile
+                    // costs one atomic per word: the word's first lane after p.
+                    const uint32_t word = gyl >> 5;
+                    uint32_t suf = y_ok ? 1u << (gyl & 31) : 0u;
+#pragma unroll
+                    for (int d = 1; d < 64; d <<= 1) {
+                        const uint32_t o = __shfl_down(suf, d, 64);
+                        const uint32_t ow = __shfl_down(word, d, 64);
+                        if (lane + d < 64 && ow == word) suf |= o;
+                    }
+                    const uint32_t wprev = __shfl_up(word, 1, 64);
+                    const bool seg_head = lane == 0 || wprev != word;
+                    uint64_t heads = __ballot(x_ok && tile_head);
+                    while (heads) {
+                        const uint32_t p = (uint32_t)__ffsll((long long)heads) - 1;
+                        heads &= heads - 1;
+                        const uint32_t T = __builtin_amdgcn_readlane(tx, p);
+                        const int32_t qd = (int32_t)(xb + p) - (int32_t)yb;      // y lanes after the tile's first x
+                        if (y_ok && (int32_t)lane > qd && (seg_head || (int32_t)lane == qd + 1)) mark(T, gyl, suf);
+                    }
+                    continue;
+                }
                 const uint64_t vyl = H[iyl];
                 const uint32_t ny = min(64u, m - yb);
                 for (uint32_t yi = 0; yi < ny; yi++) {
@@ -262,11 +306,7 @@ __global__ __launch_bounds__(kMarkWG) void k_screen_mark(const uint32_t *__restr
                     // the first ok lane of each row tile marks (lane - 1 not ok, or another tile)
                     const bool prev_ok = lane > 0 && ((okm >> (lane - 1)) & 1ull);
                     if (!ok || (prev_ok && !tile_head)) continue;
-                    const uint32_t bit = 1u << (gy & 31);
-                    if (tx - t_lo < kMarkTiles && gy - c_lo < kMarkCols)
-                        atomicOr(&win[(tx - t_lo) * kMarkStride + ((gy - c_lo) >> 5)], bit);
-                    else
-                        atomicOr(bm + (uint64_t)tx * NW + (gy >> 5), bit);
+                    mark(tx, gy, 1u << (gy & 31));
                 }
             }
         }
