@@ -570,12 +570,15 @@ def test_allpairs_row_segments_and_merge_kernel(family, ctx1000):
     assert np.array_equal(out.cpu().numpy().view(np.uint16), oc)
 
 
+@pytest.mark.parametrize("screen", ["2", "1"])
 @pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0, 0, 0]])
-def test_condensed_allpairs_multi_device(family, devices):
+def test_condensed_allpairs_multi_device(family, devices, screen, monkeypatch):
     """In-process multi-device all-pairs (drephip_allpairs_rows per device on
     balanced row ranges, threads) assembles the same triangle, with partial
-    sketches (denominators) too."""
+    sketches (denominators) too -- with the shared-hash screen off and forced
+    on (each device screens its own row range)."""
     from drep_amd.d_cluster import condensed_allpairs
+    monkeypatch.setenv("DREPHIP_AP_SCREEN", screen)
     h, nh = family
     oc, od = oracle.allpairs(h, nh, S, threads=8)
     c, d = condensed_allpairs(h, nh, S, devices)

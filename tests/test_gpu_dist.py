@@ -20,9 +20,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 N, L = 240, 300_000
 
 
-def _run(world, out, port, n=N, sketch=1000):
+def _run(world, out, port, n=N, sketch=1000, screen=None):
     # the root's condensed vector starts poisoned: every pair must be written
     env = dict(os.environ, DREPHIP_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1", DREPHIP_SEGMENT_POISON="1")
+    if screen is not None:          # the shared-hash screen forced on (1) / off (2) in every rank
+        env["DREPHIP_AP_SCREEN"] = str(screen)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "drep_amd.distributed",
            "--genomes", str(n), "--genome-bp", str(L), "--family-size", "20", "--sketch", str(sketch),
@@ -64,8 +66,8 @@ def test_sharded_job_band_path_matches_single_rank(tmp_path):
     pair may keep the poison.  1 and 2 ranks give the same counts, Z and Cdb,
     and rows of the counts equal the oracle's merge."""
     n, s = 96, 4096
-    one = _run(1, str(tmp_path / "b1"), 29661, n=n, sketch=s)
-    two = _run(2, str(tmp_path / "b2"), 29671, n=n, sketch=s)
+    one = _run(1, str(tmp_path / "b1"), 29661, n=n, sketch=s, screen=2)
+    two = _run(2, str(tmp_path / "b2"), 29671, n=n, sketch=s, screen=2)
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2
     cm1 = load_condensed(str(tmp_path / "b1"), mmap=False)
     cm2 = load_condensed(str(tmp_path / "b2"), mmap=False)
@@ -80,6 +82,30 @@ def test_sharded_job_band_path_matches_single_rank(tmp_path):
         want, _ = oracle.allpairs(h, nh, s, r0=r0, r1=r1, threads=8)
         a = r0 * n - r0 * (r0 + 1) // 2
         assert np.array_equal(cm2.common[a:a + len(want)], want), (r0, r1)
+    # the same with the shared-hash screen forced on in both ranks: the
+    # no-shared-hash fill plus the LIST band kernel write every pair
+    three = _run(2, str(tmp_path / "b3"), 29681, n=n, sketch=s, screen=1)
+    assert three["n_gpus"] == 2
+    cm3 = load_condensed(str(tmp_path / "b3"), mmap=False)
+    assert np.array_equal(cm3.common, cm1.common)
+    assert np.array_equal(load_primary_linkage(str(tmp_path / "b3"))["linkage"],
+                          load_primary_linkage(str(tmp_path / "b1"))["linkage"])
+
+
+@pytest.mark.timeout(600)
+def test_sharded_job_screened_matches_unscreened(tmp_path):
+    """s = 1000 (whole-row kernel): 3 ranks with the shared-hash screen forced
+    on equal 1 rank with it off (stored counts, Z, Cdb), the root's vector
+    starting poisoned."""
+    off = _run(1, str(tmp_path / "off"), 29691, screen=2)
+    on = _run(3, str(tmp_path / "on"), 29701, screen=1)
+    assert off["n_gpus"] == 1 and on["n_gpus"] == 3
+    a = load_condensed(str(tmp_path / "off"), mmap=False)
+    b = load_condensed(str(tmp_path / "on"), mmap=False)
+    assert np.array_equal(a.common, b.common)
+    assert np.array_equal(load_primary_linkage(str(tmp_path / "off"))["linkage"],
+                          load_primary_linkage(str(tmp_path / "on"))["linkage"])
+    assert pd.read_csv(tmp_path / "off" / "primary_Cdb.csv").equals(pd.read_csv(tmp_path / "on" / "primary_Cdb.csv"))
 
 
 def _file_set(tmp_path, copies=6):
