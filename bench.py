@@ -723,8 +723,14 @@ def main():
                 "pairs_per_launch": segment_size(N, r0, r1),
                 "pairs_per_s_per_gpu": (segment_size(N, r0, r1) / (kms[2][0] / max(kms[2][1], 1) / 1e3)
                                         if kms[2][0] else None),
-                "roofline": dist_roofline(N, args.sketch, segment_size(N, r0, r1),
-                                          kms[2][0] / max(kms[2][1], 1)),
+                "roofline": (dist_roofline(N, args.sketch, segment_size(N, r0, r1), kms[2][0] / max(kms[2][1], 1))
+                             if not screen.get("used") else
+                             {"note": "screened path (DESIGN.md 4.6): the sort/mark/list passes, the no-shared-hash fill "
+                                      "and the LIST kernel on the marked (row tile, column) cells; the dense kernel's "
+                                      "per-pair profile does not apply",
+                              "screen_ms_avg": kms[4][0] / max(kms[4][1], 1),
+                              "sort_bytes_per_launch_est": 4 * 16 * screen.get("entries", 0),
+                              "marked_cells": screen.get("marked"), "pair_checks": screen.get("checks")}),
             },
             "cpu_baseline": cpu,
         }
