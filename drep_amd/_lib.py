@@ -90,7 +90,7 @@ SIGNATURES = {
     "drephip_last_kernel_ms": (C.c_int, [vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
     "drephip_set_allpairs_screen": (C.c_int, [vp, C.c_int]),
     "drephip_last_screen_stats": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
-                                             C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+                                             C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
 }
 
 
@@ -272,10 +272,11 @@ class Context:
 
     def screen_stats(self) -> dict:
         u = C.c_int(0)
-        e, r, c, m = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
-        check(lib().drephip_last_screen_stats(self._h, C.byref(u), C.byref(e), C.byref(r), C.byref(c), C.byref(m)),
-              "drephip_last_screen_stats")
-        return {"used": bool(u.value), "entries": e.value, "runs": r.value, "checks": c.value, "marked": m.value}
+        e, r, c, m, sp = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
+        check(lib().drephip_last_screen_stats(self._h, C.byref(u), C.byref(e), C.byref(r), C.byref(c), C.byref(m),
+                                              C.byref(sp)), "drephip_last_screen_stats")
+        return {"used": bool(u.value), "entries": e.value, "runs": r.value, "checks": c.value, "marked": m.value,
+                "simple": sp.value}
 
     def set_allpairs_path(self, path: int, band_cap: int = 1024) -> None:
         check(lib().drephip_set_allpairs_path(self._h, path, band_cap), "drephip_set_allpairs_path")

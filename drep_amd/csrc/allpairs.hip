@@ -1238,12 +1238,10 @@ static int launch_band_cfg(drephip_ctx *ctx, const uint64_t *d_hashes, const uin
                                          kBandCols, st, (void **)&d_items, &nitems))) {
         return rc;
     }
-    if (scr) {
-        timing_mark(ctx, 2, st, true);
-        if ((rc = screen_fill_impl(ctx, d_nhash, N, row0, row1, seg0, npairs, d_common, d_denom, st))) return rc;
-        if (nitems == 0) { timing_mark(ctx, 2, st, false); HIPC(hipStreamSynchronize(st)); return DREPHIP_OK; }
+    if (nitems == 0) {                              // (screened: the screen wrote the whole segment)
+        if (scr) HIPC(hipStreamSynchronize(st));
+        return DREPHIP_OK;
     }
-    if (nitems == 0) return DREPHIP_OK;
     if ((rc = scratch(ctx, "ap_nfail_band", 4, (void **)&d_nfail))) return rc;
     HIPC(hipMemsetAsync(d_nfail, 0, 4, st));
     uint64_t *d_prof = nullptr;                      // DREPHIP_BAND_PROF=1: per-phase wall-clock sums
@@ -1255,7 +1253,7 @@ static int launch_band_cfg(drephip_ctx *ctx, const uint64_t *d_hashes, const uin
     constexpr size_t lds = band_lds_bytes<R, BB, CAP>();
     auto kern = scr ? k_allpairs_band<R, BB, CAP, 1024, MINW, true> : k_allpairs_band<R, BB, CAP, 1024, MINW, false>;
     HIPC(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    if (!scr) timing_mark(ctx, 2, st, true);
+    timing_mark(ctx, 2, st, true);
     for (uint64_t i0 = 0; i0 < nitems; i0 += max_blocks(1024))
         hipLaunchKernelGGL(kern, dim3((uint32_t)std::min<uint64_t>(nitems - i0, max_blocks(1024))), dim3(1024), lds, st,
                            d_hashes, d_nhash, ctx->s, N, row1, cap, scr ? nullptr : d_items + i0, d_common, d_denom, seg0,
@@ -1292,8 +1290,7 @@ static int launch_band(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_
                                                st, scr);
 }
 
-// LIST: the screened items / column list (clist); the caller opened the
-// timing span (it covers the no-shared-hash fill as well)
+// LIST: the screened items / column list (clist)
 template <int R, int NCH, int MINW, bool LIST>
 static int launch_q(drephip_ctx *ctx, uint32_t nitems, size_t lds, hipStream_t st, const uint64_t *h,
                     const uint32_t *nh, const uint32_t *blk, uint32_t stride, const uint8_t *fam, uint32_t N, uint32_t row0,
@@ -1301,7 +1298,7 @@ static int launch_q(drephip_ctx *ctx, uint32_t nitems, size_t lds, hipStream_t s
                     uint64_t seg0, const uint32_t *clist) {
     HIPC(hipFuncSetAttribute((const void *)k_allpairs_q<R, NCH, MINW, LIST>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)lds));
-    if (!LIST) timing_mark(ctx, 2, st, true);
+    timing_mark(ctx, 2, st, true);
     for (uint32_t i0 = 0; i0 < nitems; i0 += (uint32_t)max_blocks(kApWG))
         hipLaunchKernelGGL((k_allpairs_q<R, NCH, MINW, LIST>),
                            dim3(std::min<uint32_t>(nitems - i0, (uint32_t)max_blocks(kApWG))), dim3(kApWG), lds, st, h,
@@ -1366,7 +1363,7 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
         // columns; the whole-row kernel takes up to kListCols per item, so a
         // row tile's image is loaded once for most tiles
         int rc = screen_impl(ctx, d_hashes, d_nhash, N, row0, row1, R, path == DREPHIP_AP_BAND ? kBandCols : kListCols,
-                             npairs, smode == DREPHIP_SCREEN_ON, st, &scr);
+                             seg0, npairs, d_common, d_denom, smode == DREPHIP_SCREEN_ON, st, &scr);
         if (rc) return rc;
         ctx->last_screen = scr;
     }
@@ -1410,10 +1407,8 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
     // queued H2D copy may still be reading it when a deferred call returns).
     const uint64_t key[5] = {N, row0, row1, R, C};
     if (scr.use) {
-        // the screened items; every other pair gets the no-shared-hash fill
+        // the screened items (the screen has written every other pair)
         d_items = (uint4 *)scr.items;
-        timing_mark(ctx, 2, st, true);
-        if ((rc = screen_fill_impl(ctx, d_nhash, N, row0, row1, seg0, npairs, d_common, d_denom, st))) return rc;
     } else if (ctx->ap_items_gen == ctx->alloc_gen && !memcmp(ctx->ap_items_key, key, sizeof(key))) {
         if ((rc = scratch(ctx, "ap_items", ctx->ap_items_n * sizeof(uint4), (void **)&d_items))) return rc;
     } else {

@@ -219,7 +219,7 @@ DREPHIP_EXPORT int drephip_set_allpairs_screen(drephip_ctx *ctx, int mode) {
 }
 
 DREPHIP_EXPORT int drephip_last_screen_stats(drephip_ctx *ctx, int *used, uint64_t *entries, uint64_t *runs,
-                                             uint64_t *checks, uint64_t *marked) {
+                                             uint64_t *checks, uint64_t *marked, uint64_t *simple) {
     if (!ctx) { set_error("null context"); return DREPHIP_ERR_ARG; }
     const ScreenResult &r = ctx->last_screen;
     if (used) *used = r.use ? 1 : 0;
@@ -227,6 +227,7 @@ DREPHIP_EXPORT int drephip_last_screen_stats(drephip_ctx *ctx, int *used, uint64
     if (runs) *runs = r.runs;
     if (checks) *checks = r.checks;
     if (marked) *marked = r.marked;
+    if (simple) *simple = r.simple;
     return DREPHIP_OK;
 }
 

@@ -84,6 +84,7 @@ struct ScreenResult {
     uint64_t runs = 0;            // runs of >= 2 equal 32-bit keys
     uint64_t checks = 0;          // pair checks of the marking (sum of m(m-1)/2)
     uint64_t marked = 0;          // marked (row tile, column) cells
+    uint64_t simple = 0;          // pairs sharing exactly one hash, written by the screen itself
 };
 
 // A run of all-pairs work items (allpairs.hip, plan_items): `size` row tiles
@@ -195,11 +196,15 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
 int allpairs_wait_impl(drephip_ctx *ctx);
 // The shared-hash screen (screen.hip): the (row tile of R rows, column) cells
 // of rows [row0, row1) whose row and column share a hash, as per-tile column
-// lists and LIST work items of at most C columns.  res->use = false when the
-// set is too dense for it to pay (unless force) or too large for its 32-bit
-// indices; the dense path runs then.  Synchronises the stream.
+// lists and LIST work items of at most C columns.  When it applies it also
+// writes the segment: every pair as no-shared-hash, then the pairs that share
+// exactly one hash (outside the listed cells); the LIST kernels complete it.
+// res->use = false when the set is too dense for it to pay (unless force) or
+// too large for its 32-bit indices; the dense path runs then (and rewrites
+// every pair).  Synchronises the stream.
 int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N, uint32_t row0,
-                uint32_t row1, uint32_t R, uint32_t C, uint64_t npairs, bool force, hipStream_t st, ScreenResult *res);
+                uint32_t row1, uint32_t R, uint32_t C, uint64_t seg0, uint64_t npairs, uint16_t *d_common,
+                uint16_t *d_denom, bool force, hipStream_t st, ScreenResult *res);
 // Every pair of the segment as an unscreened one: common 0, denominator
 // min(s, |A| + |B|); the LIST kernels then overwrite the screened pairs.
 int screen_fill_impl(drephip_ctx *ctx, const uint32_t *d_nhash, uint32_t N, uint32_t row0, uint32_t row1,

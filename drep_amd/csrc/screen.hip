@@ -181,19 +181,70 @@ __global__ __launch_bounds__(kScWG) void k_run_write(const uint32_t *__restrict_
     }
 }
 
-// runs of two entries: one lane each; equal 64-bit hashes of two genomes
-// mark (row tile of the smaller, larger) straight in the bitmap
+// Runs of two entries (chance sharing, mostly): one lane each.  Two genomes
+// holding one 64-bit hash go into a pair map (key (a, b), a < b; how many
+// such runs hold the pair; the hash's positions i in a and j in b) instead of
+// the bitmap: a pair that shares exactly one hash has count (i + j < s) --
+// the hash's rank in A u B is i + j -- and needs no kernel (k_screen_simple).
+constexpr uint64_t kPairEmpty = ~0ull;
+__device__ __forceinline__ uint32_t pair_slot(uint64_t key, uint32_t mask) {
+    uint64_t h = key * 0x9E3779B97F4A7C15ull;
+    return (uint32_t)(h >> 32) & mask;
+}
 __global__ __launch_bounds__(kScWG) void k_screen_mark2(const uint32_t *__restrict__ vals, const uint64_t *__restrict__ H,
                                                         uint32_t s, const uint32_t *__restrict__ pairs, uint32_t n2,
-                                                        uint32_t row0, uint32_t row1, uint32_t rshift, uint32_t NW,
-                                                        uint32_t *__restrict__ bm) {
+                                                        uint32_t row0, uint32_t row1,
+                                                        unsigned long long *__restrict__ pkey, uint32_t *__restrict__ pcnt,
+                                                        uint32_t *__restrict__ ppos, uint32_t pmask) {
     for (uint32_t q = blockIdx.x * kScWG + threadIdx.x; q < n2; q += gridDim.x * kScWG) {
         const uint32_t st = pairs[q];
         const uint32_t ix = vals[st], iy = vals[st + 1];
         const uint32_t gx = ix / s, gy = iy / s;          // gx <= gy (a run is in genome order)
         if (gx == gy || gx < row0 || gx >= row1 || H[ix] != H[iy]) continue;
-        atomicOr(bm + (uint64_t)((gx - row0) >> rshift) * NW + (gy >> 5), 1u << (gy & 31));
+        const unsigned long long key = ((unsigned long long)gx << 32) | gy;
+        for (uint32_t slot = pair_slot(key, pmask);; slot = (slot + 1) & pmask) {
+            const unsigned long long k = atomicCAS(&pkey[slot], kPairEmpty, key);
+            if (k == kPairEmpty) {                        // first run of this pair: its positions
+                ppos[slot] = ((ix - gx * s) << 16) | (iy - gy * s);
+                atomicAdd(&pcnt[slot], 1u);
+                break;
+            }
+            if (k == key) { atomicAdd(&pcnt[slot], 1u); break; }
+        }
     }
+}
+
+// The pair map: a pair held by one run of two with both sketches full shares
+// exactly one hash unless a longer run holds it too -- and then that run has
+// marked its cell -- so when its cell is unmarked its count is written here,
+// (i + j < s), over the no-shared-hash fill (the denominator, s, is already
+// right).  Pairs held by several runs, or with a partial sketch (whose
+// denominator depends on the merge), mark their cell for the LIST kernel,
+// which runs after this and rewrites every pair of a marked cell exactly.
+__global__ __launch_bounds__(kScWG) void k_screen_simple(const unsigned long long *__restrict__ pkey,
+                                                         const uint32_t *__restrict__ pcnt,
+                                                         const uint32_t *__restrict__ ppos, uint32_t pcap,
+                                                         const uint32_t *__restrict__ nh, uint32_t s, uint32_t N,
+                                                         uint32_t row0, uint32_t rshift, uint32_t NW,
+                                                         uint64_t seg0, uint32_t *__restrict__ bm,
+                                                         uint16_t *__restrict__ common, unsigned long long *__restrict__ nsimple) {
+    uint32_t mine = 0;
+    for (uint32_t q = blockIdx.x * kScWG + threadIdx.x; q < pcap; q += gridDim.x * kScWG) {
+        const unsigned long long key = pkey[q];
+        if (key == kPairEmpty) continue;
+        const uint32_t a = (uint32_t)(key >> 32), b = (uint32_t)key;
+        uint32_t *w = bm + (uint64_t)((a - row0) >> rshift) * NW + (b >> 5);
+        const uint32_t bit = 1u << (b & 31);
+        if (pcnt[q] >= 2 || nh[a] != s || nh[b] != s) { atomicOr(w, bit); continue; }
+        if (*w & bit) continue;                                       // a longer run holds the pair too
+        const uint32_t pos = ppos[q];
+        const uint64_t o = (uint64_t)a * N - (uint64_t)a * (a + 1) / 2 + (b - a - 1) - seg0;
+        common[o] = (uint16_t)(((pos >> 16) + (pos & 0xFFFFu)) < s ? 1 : 0);
+        mine++;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
+    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(nsimple, (unsigned long long)mine);
 }
 
 // Marking, one workgroup per chunk of kMarkChunk runs taken in order of their
@@ -430,14 +481,15 @@ static int hip_scan(drephip_ctx *ctx, const char *name, const uint32_t *in, T *o
 }
 
 int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N, uint32_t row0,
-                uint32_t row1, uint32_t R, uint32_t C, uint64_t npairs, bool force, hipStream_t st, ScreenResult *res) {
+                uint32_t row1, uint32_t R, uint32_t C, uint64_t seg0, uint64_t npairs, uint16_t *d_common,
+                uint16_t *d_denom, bool force, hipStream_t st, ScreenResult *res) {
     *res = ScreenResult{};
     const uint32_t s = ctx->s;
     if ((uint64_t)N * s >= (1ull << 32)) return DREPHIP_OK;          // entry values g * s + k are 32-bit
     int rc;
     uint64_t *d_eoff, *h_tot;
     if ((rc = scratch(ctx, "sc_eoff", (N + 1) * 8ull, (void **)&d_eoff))) return rc;
-    if ((rc = pinned_host(ctx, "sc_tot", 32, (void **)&h_tot))) return rc;
+    if ((rc = pinned_host(ctx, "sc_tot", 64, (void **)&h_tot))) return rc;
     timing_mark(ctx, 4, st, true);
     ScreenProf prof;
     prof.mark("start", st);
@@ -449,6 +501,7 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
     if (M < 2) {
         // fewer than two sketch entries: no pair shares a hash; every pair
         // gets the no-shared-hash fill, no LIST work
+        if ((rc = screen_fill_impl(ctx, d_nhash, N, row0, row1, seg0, npairs, d_common, d_denom, st))) return rc;
         timing_mark(ctx, 4, st, false);
         res->entries = M;
         res->use = true;
@@ -545,8 +598,24 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
     if ((rc = scratch(ctx, "sc_titc", (ntiles + 1) * 4ull, (void **)&d_itc))) return rc;
     if ((rc = scratch(ctx, "sc_coff", (ntiles + 1) * 8ull, (void **)&d_coff))) return rc;
     if ((rc = scratch(ctx, "sc_ioff", (ntiles + 1) * 8ull, (void **)&d_ioff))) return rc;
+    // the pair map of the runs of two (k_screen_mark2), twice their count
+    uint32_t pcap = 1024;
+    while (pcap < 2ull * n2) pcap <<= 1;
+    unsigned long long *pkey, *d_nsimple;
+    uint32_t *pcnt, *ppos;
+    if ((rc = scratch(ctx, "sc_pkey", pcap * 8ull, (void **)&pkey))) return rc;
+    if ((rc = scratch(ctx, "sc_pcnt", pcap * 4ull, (void **)&pcnt))) return rc;
+    if ((rc = scratch(ctx, "sc_ppos", pcap * 4ull, (void **)&ppos))) return rc;
+    if ((rc = scratch(ctx, "sc_nsimple", 8, (void **)&d_nsimple))) return rc;
     prof.mark("readback+alloc", st);
+    // every pair as no-shared-hash first: the simple pairs are written over it
+    // below, the LIST kernel over both
+    if ((rc = screen_fill_impl(ctx, d_nhash, N, row0, row1, seg0, npairs, d_common, d_denom, st))) return rc;
+    prof.mark("fill", st);
     HIPC(hipMemsetAsync(d_bm, 0, (uint64_t)ntiles * NW * 4, st));
+    HIPC(hipMemsetAsync(pkey, 0xFF, pcap * 8ull, st));
+    HIPC(hipMemsetAsync(pcnt, 0, pcap * 4ull, st));
+    HIPC(hipMemsetAsync(d_nsimple, 0, 8, st));
     prof.mark("bitmap-clear", st);
     if (nruns) {
         // runs in order of their first genome (a family's runs together)
@@ -562,7 +631,10 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
     if (n2) {
         const uint32_t g2 = std::max(1u, std::min(8192u, (n2 + kScWG - 1) / kScWG));
         hipLaunchKernelGGL(k_screen_mark2, dim3(g2), dim3(kScWG), 0, st, v_out, d_hashes, s, d_pairs, n2, row0, row1,
-                           rshift, NW, d_bm);
+                           pkey, pcnt, ppos, pcap - 1);
+        const uint32_t gs = std::max(1u, std::min(8192u, (pcap + kScWG - 1) / kScWG));
+        hipLaunchKernelGGL(k_screen_simple, dim3(gs), dim3(kScWG), 0, st, pkey, pcnt, ppos, pcap, d_nhash, s, N, row0,
+                           rshift, NW, seg0, d_bm, d_common, d_nsimple);
     }
     prof.mark("mark", st);
     hipLaunchKernelGGL(k_screen_count, dim3(ntiles), dim3(kScWG), 0, st, d_bm, NW, C, d_cnt, d_itc);
@@ -574,9 +646,11 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
     prof.mark("count+scans", st);
     HIPC(hipMemcpyAsync(h_tot, d_coff + ntiles, 8, hipMemcpyDeviceToHost, st));
     HIPC(hipMemcpyAsync(h_tot + 1, d_ioff + ntiles, 8, hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(h_tot + 2, d_nsimple, 8, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));
     const uint64_t marked = h_tot[0], nitems = h_tot[1];
     res->marked = marked;
+    res->simple = h_tot[2];
     if (marked >= (1ull << 32) || nitems >= (1ull << 31)) { timing_mark(ctx, 4, st, false); return DREPHIP_OK; }
     uint32_t *d_list;
     uint4 *d_items;

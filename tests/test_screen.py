@@ -140,3 +140,37 @@ def test_screen_auto_on_family_sets():
     oc, od = oracle.allpairs(h, nh, 1000, threads=8)
     assert np.array_equal(c, oc) and np.array_equal(d, od)
     assert st["used"] and st["entries"] == int(nh.sum())
+
+
+def test_screen_single_shared_hash_pairs():
+    """Pairs of otherwise unrelated genomes that share exactly one hash are
+    written by the screen itself (count = 1 iff the hash's rank in A u B,
+    i + j, is below s); pairs sharing two such hashes, or with a partial
+    sketch, go to the kernel.  Planted at positions on both sides of
+    i + j = s, checked against the oracle."""
+    s, N = 256, 400
+    rng = np.random.default_rng(21)
+    H = np.sort(rng.integers(1, 1 << 62, size=(N, s), dtype=np.uint64), axis=1)     # random: no value shared by chance
+    NH = np.full(N, s, dtype=np.uint32)
+    for g in range(0, N, 9):                       # partial sketches
+        NH[g] = rng.integers(s // 3, s)
+        H[g, NH[g]:] = UMAX
+    planted = 0
+    for _ in range(600):
+        a, b = sorted(rng.choice(N, 2, replace=False))
+        for _k in range(1 if rng.random() < 0.8 else 2):           # one shared hash, sometimes two
+            i, j = int(rng.integers(0, NH[a])), int(rng.integers(0, NH[b]))
+            v = H[a, i]
+            if v in H[b, :NH[b]]:
+                continue
+            row = np.sort(np.concatenate([np.delete(H[b, :NH[b]], j), [v]]))
+            H[b, :NH[b]] = row
+            planted += 1
+    oc, od = oracle.allpairs(H, NH, s, threads=8)
+    with _lib.Context(0, 21, s, 42) as ctx:
+        c, d, st = run(ctx, H, NH, ctx.SCREEN_ON)
+        assert st["used"] and st["simple"] > 100, st
+        assert np.array_equal(c, oc) and np.array_equal(d, od)
+        c2, d2, _ = run(ctx, H, NH, ctx.SCREEN_OFF)
+        assert np.array_equal(c2, oc) and np.array_equal(d2, od)
+    assert planted > 500 and (oc == 1).sum() > 100 and ((oc == 0) & (od == s)).sum() > 1000
