@@ -174,3 +174,13 @@ def test_screen_single_shared_hash_pairs():
         c2, d2, _ = run(ctx, H, NH, ctx.SCREEN_OFF)
         assert np.array_equal(c2, oc) and np.array_equal(d2, od)
     assert planted > 500 and (oc == 1).sum() > 100 and ((oc == 0) & (od == s)).sum() > 1000
+
+
+def test_screen_mode_argument_checked():
+    with _lib.Context(0, 21, 1000, 42) as ctx:
+        with pytest.raises(_lib.DrepHipError, match="unknown screen mode"):
+            ctx.set_allpairs_screen(3)
+        ctx.set_allpairs_screen(ctx.SCREEN_AUTO)
+        h = np.sort(np.random.default_rng(1).integers(1, 1 << 62, size=(3, 1000), dtype=np.uint64), axis=1)
+        ctx.allpairs(h, np.full(3, 1000, np.uint32))
+        assert not ctx.screen_stats()["used"]            # auto: N < 4096
