@@ -58,6 +58,8 @@ struct SparseLinkInfo {       // the sparse linkage path (linkage_sparse.cpp)
     uint32_t components = 0;  // connected components with >= 2 members (0 for single linkage)
     uint32_t largest = 0;     // members of the largest one
     uint64_t cells = 0;       // per-component matrix cells (sum of m^2)
+    int rows = 0;             // 1: the sparse-row chain ran (no per-component matrices)
+    uint64_t scanned = 0;     // sparse-row chain: row entries read by the searches and merges
     double setup_s = 0;       // components + matrices
     double chain_s = 0;       // nn-chain / Prim steps
     double finish_s = 0;      // stable sort + relabel
@@ -228,7 +230,10 @@ int sparse_pairs_impl(drephip_ctx *ctx, const uint16_t *d_common, const uint16_t
 // DREPHIP_ERR_UNSUPPORTED when the per-component matrices would exceed max_cells or a component
 // max_comp members.
 int linkage_sparse_impl(uint32_t n, uint64_t np, const uint32_t *pi, const uint32_t *pj, const double *pv,
-                        int method, uint64_t max_cells, uint32_t max_comp, double *Z_out, SparseLinkInfo *info);
+                        int method, uint64_t max_cells, uint32_t max_comp, double *Z_out, SparseLinkInfo *info,
+                        int rows = 0);
+// rows: 0 never the sparse-row chain, 1 where the components exceed the
+// matrix limits, 2 always (DREPHIP_LINK_ROWS overrides: 0 / 1 / 2)
 void sort_and_label(std::vector<double> &Z, uint32_t n);
 // host worker threads of the linkage paths: OMP_NUM_THREADS if set, else the
 // hardware threads, at most 16

@@ -372,6 +372,520 @@ __global__ __launch_bounds__(WG) void k_mst_step(const double *__restrict__ D, u
     if (threadIdx.x == 0) parts[(uint64_t)q * 1024 + blockIdx.x] = part;
 }
 
+// ------------------------------------------------ the cache-driven chain
+// Round 5 of the step design: fewer launches.  Three of every ~5 chain steps
+// at Mash scale are pushes, and a push's only work is the row search of the
+// pushed cluster -- a whole launch (~5.5 us at n = 10^5, latency-bound).  Each
+// active cluster j keeps a row cache: up to two entries of its row, the
+// smallest ones ((value, index) order), and a bound (bv, bi): every entry of
+// the row not in the cache is >= (bv, bi).  The cache's first entry is then
+// the row's minimum with scipy's tie rule (lowest index among equal values),
+// so a push can be decided from the cache without reading the row.
+//
+// A launch's decision loop (replicated in every workgroup, as before) starts
+// from the previous launch's search of the chain top, then follows pushes
+// through the caches of the pushed clusters until a merge (the launch applies
+// it and searches the new top, fused as before) or a cache without an entry
+// (the launch searches that top).  The merged row y's entries are all new:
+// the merge launch also reduces them to per-workgroup two smallest (P2
+// partials), from which the NEXT launch takes y's minimum (if y is pushed)
+// and its forwarding workgroup writes y's cache.  A merge launch keeps every
+// other cache exact: entries for x and y leave, (D'[j][y], y) enters if it is
+// below the bound (the third entry becomes the bound).
+//
+// Races: within a launch the loops read the caches of the clusters they push
+// (P, the same list in every workgroup) and nothing else, so no cache in P is
+// written during the launch: the merge's maintenance skips them, and they --
+// with the new top after a merge, whose maintenance would need the value
+// another workgroup computes -- are invalidated by workgroup 0 of the next
+// launch (they are chain members: their caches are not needed unless a
+// cluster is pushed twice).  The row y whose cache the forwarding workgroup
+// writes is excluded from both; if the same launch merges (x', y') the
+// forwarding workgroup applies that merge to y's cache itself: D[y][x'] is
+// stable during the launch, D[y][y'] is not (being rewritten), so it uses y'
+// 's cached value when y' is in the cache, else a lower bound on the new
+// entry -- Lance-Williams of (m, m) with m <= both operands, rounding being
+// monotone -- and lowers the cache bound to it.
+constexpr int kCPush = 16;          // pushes one decision loop may make through caches
+constexpr int kCInval = kCPush + 1;
+
+struct alignas(64) CLinkState {
+    int32_t k, len, top, below, first_active;
+    int32_t pend, x, y, nx, ny;     // the merge this state's launch applies
+    int32_t decide;                 // 1: the launch that wrote this state searched `top` (P1 partials)
+    int32_t mrow;                   // the row that launch's merge formed (P2 partials), -1: none
+    int32_t bad;
+    int32_t psa, psb, psbsz;        // sizes changed by this state's merge (as in LinkState)
+    int32_t ninval;                 // rows whose caches the next launch invalidates (list: cinval[parity])
+};
+
+struct alignas(64) CLinkFwd {
+    double dp;
+    int32_t szt, szb, c3, c4;
+};
+
+__device__ __forceinline__ bool lex_lt(double v, int32_t i, double w, int32_t j) { return v < w || (v == w && i < j); }
+
+// wave-wide minimum of (v, i) by butterfly (every lane gets it)
+__device__ __forceinline__ void wave_min(double &v, int32_t &i) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double ov = __shfl_xor(v, o, 64);
+        const int32_t oi = __shfl_xor(i, o, 64);
+        if (better(ov, oi, v, i)) { v = ov; i = oi; }
+    }
+}
+
+// The two smallest (v, i) of the workgroup from each lane's sorted pair
+// (a0 <= a1); result in thread 0 (r[0] <= r[1]).
+template <int WG>
+__device__ void block_min2(double a0v, int32_t a0i, double a1v, int32_t a1i, MinIdx r[2]) {
+    __shared__ MinIdx sw[WG / 64][2];
+    double v = a0v;
+    int32_t i = a0i;
+    wave_min(v, i);
+    const double w1v = v;
+    const int32_t w1i = i;
+    if (a0i == w1i && a0v == w1v) { a0v = a1v; a0i = a1i; }       // the winner's lane pops its head
+    v = a0v; i = a0i;
+    wave_min(v, i);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { sw[w][0] = MinIdx{w1v, w1i}; sw[w][1] = MinIdx{v, i}; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        MinIdx b0{INFINITY, 0x7fffffff}, b1{INFINITY, 0x7fffffff};
+        for (int k = 0; k < WG / 64; k++)
+            for (int e = 0; e < 2; e++) {
+                const MinIdx c = sw[k][e];
+                if (better(c.v, c.i, b0.v, b0.i)) { b1 = b0; b0 = c; }
+                else if (better(c.v, c.i, b1.v, b1.i)) b1 = c;
+            }
+        r[0] = b0; r[1] = b1;
+    }
+}
+
+// a sorted list of up to three entries in named slots (no private arrays:
+// dynamic indexing would put them in scratch memory); empty slots are
+// (inf, INT_MAX)
+struct L3 {
+    MinIdx a, b, c;
+    int cnt;
+};
+__device__ __forceinline__ L3 l3_empty() {
+    const MinIdx E{INFINITY, 0x7fffffff};
+    return L3{E, E, E, 0};
+}
+// (written as selects: conditional assignments through the slots made the
+// compiler address them in scratch memory)
+__device__ __forceinline__ MinIdx sel(bool p, MinIdx a, MinIdx b) { return MinIdx{p ? a.v : b.v, p ? a.i : b.i}; }
+__device__ __forceinline__ void l3_push_back(L3 &l, MinIdx e) {       // e >= every entry
+    l.a = sel(l.cnt == 0, e, l.a);
+    l.b = sel(l.cnt == 1, e, l.b);
+    l.c = sel(l.cnt == 2, e, l.c);
+    l.cnt++;
+}
+__device__ __forceinline__ void l3_insert(L3 &l, MinIdx u) {          // l.cnt <= 2
+    const bool la = better(u.v, u.i, l.a.v, l.a.i), lb = better(u.v, u.i, l.b.v, l.b.i);
+    l.c = sel(lb, l.b, u);
+    l.b = sel(la, l.a, sel(lb, u, l.b));
+    l.a = sel(la, u, l.a);
+    l.cnt++;
+}
+__device__ __forceinline__ MinIdx l3_last(const L3 &l) { return sel(l.cnt == 1, l.a, sel(l.cnt == 2, l.b, l.c)); }
+__device__ __forceinline__ void l3_pop_back(L3 &l) {
+    const MinIdx E{INFINITY, 0x7fffffff};
+    l.c = sel(l.cnt == 3, E, l.c);
+    l.b = sel(l.cnt == 2, E, l.b);
+    l.a = sel(l.cnt == 1, E, l.a);
+    l.cnt--;
+}
+
+// lane-local insertion into a sorted pair
+__device__ __forceinline__ void ins2(double v, int32_t i, double &a0v, int32_t &a0i, double &a1v, int32_t &a1i) {
+    const bool l0 = better(v, i, a0v, a0i), l1 = better(v, i, a1v, a1i);
+    a1v = l0 ? a0v : l1 ? v : a1v;
+    a1i = l0 ? a0i : l1 ? i : a1i;
+    a0v = l0 ? v : a0v;
+    a0i = l0 ? i : a0i;
+}
+
+// Initial caches: per row the three smallest entries (i != row): two cached,
+// the third the bound.  One workgroup per row; O(n^2) reads once per linkage.
+template <int WG>
+__global__ __launch_bounds__(WG) void k_cache_init(const double *__restrict__ D, uint32_t n, int2 *__restrict__ ci,
+                                                   double2 *__restrict__ cv, double *__restrict__ cb,
+                                                   int32_t *__restrict__ cbi) {
+    __shared__ MinIdx sw[WG / 64][3];
+    const uint32_t r = blockIdx.x;
+    const double *Dr = D + (uint64_t)r * n;
+    double a0v = INFINITY, a1v = INFINITY, a2v = INFINITY;
+    int32_t a0i = 0x7fffffff, a1i = 0x7fffffff, a2i = 0x7fffffff;
+    for (uint32_t i = threadIdx.x; i < n; i += WG) {
+        if (i == r) continue;
+        const double v = Dr[i];
+        const int32_t ii = (int32_t)i;
+        if (!better(v, ii, a2v, a2i)) continue;
+        if (better(v, ii, a0v, a0i)) { a2v = a1v; a2i = a1i; a1v = a0v; a1i = a0i; a0v = v; a0i = ii; }
+        else if (better(v, ii, a1v, a1i)) { a2v = a1v; a2i = a1i; a1v = v; a1i = ii; }
+        else { a2v = v; a2i = ii; }
+    }
+    MinIdx win[3];
+#pragma unroll
+    for (int round = 0; round < 3; round++) {
+        double v = a0v;
+        int32_t i = a0i;
+        wave_min(v, i);
+        win[round] = MinIdx{v, i};
+        if (a0i == i && a0v == v) { a0v = a1v; a0i = a1i; a1v = a2v; a1i = a2i; a2v = INFINITY; a2i = 0x7fffffff; }
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { sw[w][0] = win[0]; sw[w][1] = win[1]; sw[w][2] = win[2]; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        MinIdx b[3] = {{INFINITY, 0x7fffffff}, {INFINITY, 0x7fffffff}, {INFINITY, 0x7fffffff}};
+        for (int k = 0; k < WG / 64; k++)
+            for (int e = 0; e < 3; e++) {
+                const MinIdx c = sw[k][e];
+                if (better(c.v, c.i, b[0].v, b[0].i)) { b[2] = b[1]; b[1] = b[0]; b[0] = c; }
+                else if (better(c.v, c.i, b[1].v, b[1].i)) { b[2] = b[1]; b[1] = c; }
+                else if (better(c.v, c.i, b[2].v, b[2].i)) b[2] = c;
+            }
+        const bool h0 = b[0].i != 0x7fffffff, h1 = b[1].i != 0x7fffffff;
+        ci[r] = make_int2(h0 ? b[0].i : -1, h1 ? b[1].i : -1);
+        cv[r] = make_double2(b[0].v, b[1].v);
+        cb[r] = b[2].v;
+        cbi[r] = b[2].i;
+    }
+}
+
+// Cache of row r from the P2 partials of the launch that formed r (each
+// workgroup's two smallest entries): entries outside every pair are >= the
+// smallest second entry U, so the cache takes the candidates below U (at most
+// two) and the next candidate as its bound.  Then, if this launch merges
+// (mx, my), that merge's effect (see the header above).  Block-wide; the
+// result is written by thread 0.
+template <int WG>
+__device__ void cache_refresh(const MinIdx *__restrict__ p2, uint32_t G, int32_t r, const double *__restrict__ D,
+                              uint32_t n, int method, bool merge, int32_t mx, int32_t my, int32_t mnx, int32_t mny,
+                              int2 *__restrict__ ci, double2 *__restrict__ cv, double *__restrict__ cb,
+                              int32_t *__restrict__ cbi) {
+    __shared__ MinIdx s_best;
+    // U: the smallest second entry over the workgroups (a workgroup whose slice
+    // had fewer than two entries reports +inf there: it has nothing unreported)
+    double uv = INFINITY;
+    int32_t ui = 0x7fffffff;
+    double a0v = INFINITY, a1v = INFINITY, a2v = INFINITY;
+    int32_t a0i = 0x7fffffff, a1i = 0x7fffffff, a2i = 0x7fffffff;
+    for (uint32_t b = threadIdx.x; b < G; b += blockDim.x) {
+        const MinIdx e0 = p2[2 * b], e1 = p2[2 * b + 1];
+        if (better(e1.v, e1.i, uv, ui)) { uv = e1.v; ui = e1.i; }
+        for (int e = 0; e < 2; e++) {
+            const MinIdx c = e ? e1 : e0;
+            if (!better(c.v, c.i, a2v, a2i)) continue;
+            if (better(c.v, c.i, a0v, a0i)) { a2v = a1v; a2i = a1i; a1v = a0v; a1i = a0i; a0v = c.v; a0i = c.i; }
+            else if (better(c.v, c.i, a1v, a1i)) { a2v = a1v; a2i = a1i; a1v = c.v; a1i = c.i; }
+            else { a2v = c.v; a2i = c.i; }
+        }
+    }
+    MinIdx c[3];
+#pragma unroll
+    for (int round = 0; round < 3; round++) {
+        const MinIdx m = block_argmin<WG>(a0v, a0i);
+        if (threadIdx.x == 0) s_best = m;
+        __syncthreads();
+        c[round] = s_best;
+        if (a0i == c[round].i && a0v == c[round].v) { a0v = a1v; a0i = a1i; a1v = a2v; a1i = a2i; a2v = INFINITY; a2i = 0x7fffffff; }
+        __syncthreads();
+    }
+    const MinIdx U = block_argmin<WG>(uv, ui);
+    if (threadIdx.x != 0) return;
+    // list: the candidates below U (c[0] always is: every U is some workgroup's
+    // second entry, above that workgroup's first); bound: the next candidate
+    L3 l = l3_empty();
+    MinIdx B;
+    const bool in0 = c[0].i != 0x7fffffff && better(c[0].v, c[0].i, U.v, U.i);
+    const bool in1 = in0 && c[1].i != 0x7fffffff && better(c[1].v, c[1].i, U.v, U.i);
+    if (in0) l3_push_back(l, c[0]);
+    if (in1) l3_push_back(l, c[1]);
+    B = in1 ? c[2] : in0 ? c[1] : c[0];
+    if (!better(B.v, B.i, U.v, U.i)) B = U;
+    if (merge && r != mx && r != my) {
+        const double a = D[(uint64_t)r * n + mx];              // stable: row/column mx are not rewritten
+        double b = 0.0;
+        bool bk = false;
+        L3 k = l3_empty();
+        if (l.cnt > 0) { if (l.a.i == my) { b = l.a.v; bk = true; } else if (l.a.i != mx) l3_push_back(k, l.a); }
+        if (l.cnt > 1) { if (l.b.i == my) { b = l.b.v; bk = true; } else if (l.b.i != mx) l3_push_back(k, l.b); }
+        l = k;
+        if (bk) {
+            const double u = lw_update(method, a, b, mnx, mny);
+            if (better(u, my, B.v, B.i)) {
+                l3_insert(l, MinIdx{u, my});
+                if (l.cnt > 2) { B = l.c; l3_pop_back(l); }
+            }
+        } else {
+            // D[r][my] >= B.v, so the new entry is >= lw(m, m) with m = min(a, B.v)
+            const double m = a < B.v ? a : B.v;
+            const double lo = lw_update(method, m, m, mnx, mny);
+            if (better(lo, -1, B.v, B.i)) B = MinIdx{lo, -1};
+            while (l.cnt > 0 && !better(l3_last(l).v, l3_last(l).i, B.v, B.i)) l3_pop_back(l);
+        }
+    }
+    ci[r] = make_int2(l.cnt > 0 ? l.a.i : -1, l.cnt > 1 ? l.b.i : -1);
+    cv[r] = make_double2(l.a.v, l.b.v);
+    cb[r] = B.v;
+    cbi[r] = B.i;
+}
+
+template <int WG, int kLkPer>
+__global__ __launch_bounds__(WG) void k_nn_cstep(double *__restrict__ D, uint32_t n, int method,
+                                                    int32_t *__restrict__ size, int32_t *__restrict__ chain,
+                                                    CLinkState *__restrict__ st, CLinkFwd *__restrict__ fwd,
+                                                    MinIdx *__restrict__ parts1, MinIdx *__restrict__ parts2,
+                                                    int32_t *__restrict__ cinval,
+                                                    int2 *__restrict__ ci, double2 *__restrict__ cv,
+                                                    double *__restrict__ cb, int32_t *__restrict__ cbi,
+                                                    int32_t *__restrict__ done, double *__restrict__ Z, uint32_t q) {
+    __shared__ CLinkState sx;
+    __shared__ int32_t s_pushed[kCPush];
+    __shared__ int32_t s_skip[2 * kCInval + 2], s_nskip;
+    const uint32_t G = gridDim.x - 1;                          // step workgroups; workgroup G forwards
+    const CLinkState S = st[q ^ 1];
+    const CLinkFwd F = fwd[q ^ 1];
+    const MinIdx g1 = read_partials<WG>(parts1 + (uint64_t)(q ^ 1) * 1024, G);
+    // P2 minimum: the first entries of the pairs (stride 2)
+    double b2v = INFINITY;
+    int32_t b2i = 0x7fffffff;
+    for (uint32_t b = threadIdx.x; b < G; b += blockDim.x) {
+        const MinIdx m = parts2[((uint64_t)(q ^ 1) * 1024 + b) * 2];
+        if (better(m.v, m.i, b2v, b2i)) { b2v = m.v; b2i = m.i; }
+    }
+    __syncthreads();
+    const MinIdx g2 = block_argmin<WG>(b2v, b2i);
+    if (S.k >= (int32_t)n - 1) return;
+    const bool w0 = blockIdx.x == 0;
+    auto size_prev = [&](int32_t i, int32_t stored) {
+        return i == S.psa ? 0 : i == S.psb ? S.psbsz : stored;
+    };
+    if (w0 && threadIdx.x == 0 && S.psa >= 0) { size[S.psa] = 0; size[S.psb] = S.psbsz; }
+    __shared__ int32_t s_sinval[kCInval];
+    const int sninval = S.ninval;
+    if ((int)threadIdx.x < sninval) s_sinval[threadIdx.x] = cinval[(q ^ 1) * kCInval + threadIdx.x];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        // ---- the decision loop (replicated in every workgroup)
+        CLinkState X = S;
+        X.psa = -1; X.psb = -1; X.psbsz = 0;
+        X.pend = 0;
+        int32_t top = S.top, below = S.below, c3 = F.c3, c4 = F.c4, len = S.len;
+        double dp = F.dp;
+        int32_t szt = F.szt, szb = F.szb;
+        int np = 0;
+        bool have = S.decide != 0, merged = false;
+        MinIdx res = g1;
+        int2 nhi = make_int2(-1, -1);                                // the pushed row's cache head (loaded with its size)
+        double nhv = INFINITY;
+        for (;;) {
+            if (!have) {
+                if (top == S.mrow && S.mrow >= 0) res = g2;
+                else {
+                    bool inv = false;
+                    for (int e = 0; e < sninval && !inv; e++) inv = s_sinval[e] == top;
+                    if (inv || nhi.x < 0) break;
+                    res = MinIdx{nhv, nhi.x};
+                }
+            }
+            have = false;
+            if ((uint32_t)res.i >= n) { X.bad = 1; X.k = (int32_t)n - 1; break; }
+            if (len > 1 && !(res.v < dp)) {                       // merge top with below at dp
+                int32_t a = top, b = below, na = szt, nb = szb;
+                if (a > b) { a = below; b = top; na = szb; nb = szt; }
+                if (w0) {
+                    double *z = Z + 4ull * X.k;
+                    z[0] = a; z[1] = b; z[2] = dp; z[3] = na + nb;
+                }
+                X.psa = a; X.psb = b; X.psbsz = na + nb;
+                X.pend = 1; X.x = a; X.y = b; X.nx = na; X.ny = nb;
+                X.k = X.k + 1;
+                len -= 2;
+                top = c3;
+                below = len >= 2 ? c4 : -1;
+                if (len == 0 && X.k < (int32_t)n - 1) {             // restart at the first active cluster
+                    int32_t f = S.first_active;
+                    while (f < (int32_t)n && !(f == b || (f != a && size_prev(f, size[f]) > 0))) f++;
+                    if (f >= (int32_t)n) { X.bad = 1; X.k = (int32_t)n - 1; }
+                    else {
+                        if (w0) chain[0] = f;
+                        X.first_active = f; top = f; below = -1; len = 1;
+                    }
+                }
+                merged = true;
+                break;
+            }
+            if (len >= (int32_t)n) { X.bad = 1; X.k = (int32_t)n - 1; break; }
+            if (np >= kCPush) break;                                  // this launch searches the top again
+            const int32_t a = res.i;                                 // push
+            if (w0) chain[len] = a;
+            s_pushed[np++] = a;
+            c4 = c3; c3 = below; below = top; top = a;
+            dp = res.v;
+            // a's size and cache head, loaded together (the head is ignored
+            // when a's cache is being written this launch: see the header)
+            const int32_t sza = size[a];
+            nhi = ci[a];
+            nhv = cv[a].x;
+            szb = szt; szt = size_prev(a, sza);
+            len++;
+        }
+        X.len = len; X.top = top; X.below = below;
+        X.decide = 1;
+        X.mrow = merged ? X.y : -1;
+        // caches to invalidate next launch: the pushed rows, and after a merge
+        // the new top; rows no maintenance of this launch may write: those,
+        // the rows workgroup 0 invalidates now (the previous list) and the
+        // refreshed row
+        int ns = 0;
+        for (int e = 0; e < np; e++) s_skip[ns++] = s_pushed[e];
+        if (merged) s_skip[ns++] = top;
+        X.ninval = ns;
+        for (int e = 0; e < sninval; e++) s_skip[ns++] = s_sinval[e];
+        if (S.mrow >= 0) s_skip[ns++] = S.mrow;
+        s_nskip = ns;
+        sx = X;
+        if (w0) {
+            st[q] = X;
+            for (int e = 0; e < X.ninval; e++) cinval[q * kCInval + e] = s_skip[e];
+            if (X.k >= (int32_t)n - 1) st[q ^ 1] = X;
+            *done = X.k;
+            for (int e = 0; e < sninval; e++)
+                if (s_sinval[e] != S.mrow) ci[s_sinval[e]] = make_int2(-1, -1);
+        }
+        if (blockIdx.x == G && X.k < (int32_t)n - 1) {
+            auto size_now = [&](int32_t i) { return i == X.psa ? 0 : i == X.psb ? X.psbsz : size_prev(i, size[i]); };
+            // chain entries: this launch's pushes from the loop's record (workgroup 0 is writing them)
+            auto chain_at = [&](int32_t p) { return p >= S.len ? s_pushed[p - S.len] : chain[p]; };
+            CLinkFwd f{0.0, 0, 0, 0, 0};
+            f.szt = size_now(X.top);
+            if (X.len > 1) {
+                f.dp = D[(uint64_t)X.top * n + X.below];
+                f.szb = size_now(X.below);
+            }
+            if (X.len >= 3) f.c3 = chain_at(X.len - 3);
+            if (X.len >= 4) f.c4 = chain_at(X.len - 4);
+            fwd[q] = f;
+        }
+    }
+    __syncthreads();
+    const CLinkState X = sx;
+    if (blockIdx.x == G) {
+        // the forwarding workgroup: the cache of the row the previous launch formed
+        const int32_t r = S.mrow;
+        if (r >= 0 && X.k < (int32_t)n - 1 && !(X.pend && (r == X.x || r == X.y))) {
+            const int32_t szr = r == X.psa ? 0 : r == X.psb ? X.psbsz : size_prev(r, size[r]);
+            if (szr > 0)
+                cache_refresh<WG>(parts2 + (uint64_t)(q ^ 1) * 2048, G, r, D, n, method, X.pend != 0, X.x, X.y, X.nx,
+                                  X.ny, ci, cv, cb, cbi);
+        }
+        return;
+    }
+    if (X.k >= (int32_t)n - 1) return;                        // all merged (the last merge needs no update)
+    // ---- this step: the pending update fused with the search of row t, the
+    // merged row's two smallest per workgroup, and the caches' maintenance
+    const bool pend = X.pend != 0;
+    const int32_t x = X.x, y = X.y, nx = X.nx, ny = X.ny, t = X.top;
+    const double *Dt = D + (uint64_t)t * n;
+    const double *Dx = D + (uint64_t)x * n;
+    double *Dy = D + (uint64_t)y * n;
+    const double dxt = pend ? Dx[t] : 0.0, dyt = pend ? Dy[t] : 0.0;
+    const int nskip = s_nskip;
+    double bv = INFINITY;
+    int32_t bi = 0x7fffffff;
+    double m0v = INFINITY, m1v = INFINITY;                       // this lane's two smallest of the new row y
+    int32_t m0i = 0x7fffffff, m1i = 0x7fffffff;
+    const uint32_t stride = G * WG;
+    for (uint32_t i0 = blockIdx.x * WG + threadIdx.x; i0 < n; i0 += kLkPer * stride) {
+        int32_t sz[kLkPer];
+        double dt[kLkPer], dx[kLkPer], dy[kLkPer];
+        int2 hi[kLkPer];
+        double2 hv[kLkPer];
+        double hb[kLkPer];
+        int32_t hbi[kLkPer];
+#pragma unroll
+        for (int k = 0; k < kLkPer; k++) {
+            const uint32_t i = i0 + k * stride;
+            const uint32_t ic = i < n ? i : n - 1;
+            sz[k] = size[ic];
+            dt[k] = Dt[ic];
+            if (pend) {
+                dx[k] = Dx[ic]; dy[k] = Dy[ic];
+                hi[k] = ci[ic]; hv[k] = cv[ic]; hb[k] = cb[ic]; hbi[k] = cbi[ic];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kLkPer; k++) {
+            const uint32_t i = i0 + k * stride;
+            if (i >= n) continue;
+            const int32_t szi = (int32_t)i == X.psa ? 0 : (int32_t)i == X.psb ? X.psbsz : size_prev((int32_t)i, sz[k]);
+            if (szi == 0) continue;
+            double v;
+            if (pend && (int32_t)i != y && (int32_t)i != t) {
+                const double u = lw_update(method, dx[k], dy[k], nx, ny);
+                Dy[i] = u;
+                D[(uint64_t)i * n + y] = u;
+                ins2(u, (int32_t)i, m0v, m0i, m1v, m1i);
+                v = t == y ? u : dt[k];
+                // cache maintenance of row i: x and y leave, (u, y) enters below the bound
+                bool skip = hi[k].x < 0;
+                for (int e = 0; e < nskip && !skip; e++) skip = s_skip[e] == (int32_t)i;
+                if (!skip) {
+                    L3 l = l3_empty();
+                    bool changed = false;
+                    if (hi[k].x == x || hi[k].x == y) changed = true; else l3_push_back(l, MinIdx{hv[k].x, hi[k].x});
+                    if (hi[k].y >= 0) {
+                        if (hi[k].y == x || hi[k].y == y) changed = true; else l3_push_back(l, MinIdx{hv[k].y, hi[k].y});
+                    }
+                    double nbv = hb[k];
+                    int32_t nbi = hbi[k];
+                    if (better(u, y, nbv, nbi)) {
+                        l3_insert(l, MinIdx{u, y});
+                        if (l.cnt > 2) { nbv = l.c.v; nbi = l.c.i; l3_pop_back(l); }
+                        changed = true;
+                    }
+                    if (changed) {
+                        ci[i] = make_int2(l.cnt > 0 ? l.a.i : -1, l.cnt > 1 ? l.b.i : -1);
+                        cv[i] = make_double2(l.a.v, l.b.v);
+                        cb[i] = nbv;
+                        cbi[i] = nbi;
+                    }
+                }
+            } else if (pend && (int32_t)i == y && t != y) {
+                const double u = lw_update(method, dxt, dyt, nx, ny);
+                Dy[t] = u;
+                D[(uint64_t)t * n + y] = u;
+                ins2(u, t, m0v, m0i, m1v, m1i);
+                ci[y] = make_int2(-1, -1);                       // y's row is new: its cache comes from P2
+                v = u;
+            } else {
+                if (pend && (int32_t)i == y) ci[y] = make_int2(-1, -1);
+                if ((int32_t)i == t) continue;
+                v = dt[k];
+            }
+            if (v < bv) { bv = v; bi = (int32_t)i; }
+        }
+    }
+    const MinIdx part = block_argmin<WG>(bv, bi);
+    if (threadIdx.x == 0) parts1[(uint64_t)q * 1024 + blockIdx.x] = part;
+    if (pend) {
+        __syncthreads();
+        MinIdx r2[2];
+        block_min2<WG>(m0v, m0i, m1v, m1i, r2);
+        if (threadIdx.x == 0) {
+            parts2[((uint64_t)q * 1024 + blockIdx.x) * 2] = r2[0];
+            parts2[((uint64_t)q * 1024 + blockIdx.x) * 2 + 1] = r2[1];
+        }
+    }
+}
+
 // ------------------------------------------------------------ matrix build
 // D (n x n f64, rows in perm order) from the condensed upper triangle, by
 // 64 x 64 tiles of (row block bi <= column block bj): a wave reads one row's
@@ -501,6 +1015,36 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     if ((rc = scratch(ctx, "lk_done", 4, (void **)&d_done))) return rc;
     const bool mst = method == DREPHIP_LINK_SINGLE;
     if (mst && (rc = scratch(ctx, "lk_dmin", n * 8ull, (void **)&d_Dmin))) return rc;
+    // the cache-driven chain (complete / average / weighted): DREPHIP_LINK_CACHE=1 (A/B, not yet the default)
+    const char *lc = getenv("DREPHIP_LINK_CACHE");
+    const bool cached = !mst && lc && atoi(lc) != 0;
+    int2 *d_ci = nullptr;
+    double2 *d_cv = nullptr;
+    double *d_cb = nullptr;
+    int32_t *d_cbi = nullptr;
+    MinIdx *d_parts2 = nullptr;
+    int32_t *d_cinval = nullptr;
+    CLinkState *d_cst = nullptr;
+    CLinkFwd *d_cfwd = nullptr;
+    if (cached) {
+        if ((rc = scratch(ctx, "lk_ci", n * 8ull, (void **)&d_ci))) return rc;
+        if ((rc = scratch(ctx, "lk_cv", n * 16ull, (void **)&d_cv))) return rc;
+        if ((rc = scratch(ctx, "lk_cb", n * 8ull, (void **)&d_cb))) return rc;
+        if ((rc = scratch(ctx, "lk_cbi", n * 4ull, (void **)&d_cbi))) return rc;
+        if ((rc = scratch(ctx, "lk_parts2", 2 * 1024 * 2 * sizeof(MinIdx), (void **)&d_parts2))) return rc;
+        if ((rc = scratch(ctx, "lk_cst", 2 * sizeof(CLinkState), (void **)&d_cst))) return rc;
+        if ((rc = scratch(ctx, "lk_cinval", 2 * kCInval * 4ull, (void **)&d_cinval))) return rc;
+        if ((rc = scratch(ctx, "lk_cfwd", 2 * sizeof(CLinkFwd), (void **)&d_cfwd))) return rc;
+        HIPC(hipMemsetAsync(d_parts2, 0, 2 * 1024 * 2 * sizeof(MinIdx), st));
+        HIPC(hipMemsetAsync(d_cfwd, 0, 2 * sizeof(CLinkFwd), st));
+        CLinkState h[2] = {};
+        h[1].len = 1; h[1].top = 0; h[1].below = -1; h[1].first_active = 0;
+        h[1].psa = h[1].psb = -1; h[1].decide = 0; h[1].mrow = -1; h[1].ninval = 0;
+        h[0] = h[1];
+        HIPC(hipMemcpyAsync(d_cst, h, sizeof(h), hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_cache_init<256>, dim3(n), dim3(256), 0, st, (const double *)d_D, n, d_ci, d_cv, d_cb, d_cbi);
+        HIPC(hipGetLastError());
+    }
     if (mst) {
         std::vector<double> inf(n, INFINITY);
         std::vector<int32_t> mg(n, 0);
@@ -537,6 +1081,10 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     do {                                                                                                         \
         if (mst) hipLaunchKernelGGL((k_mst_step<W, P>), gm, blk, 0, st, d_D, n, d_size, d_Dmin, d_st, d_parts, d_done, \
                                     d_Z, q);                                                                     \
+        else if (cached) hipLaunchKernelGGL((k_nn_cstep<W, P>), gn, blk, 0, st, d_D, n, method, d_size, d_chain,   \
+                                            d_cst, d_cfwd, d_parts, d_parts2, d_cinval, d_ci, d_cv, d_cb, d_cbi, \
+                                            d_done,                                                              \
+                                            d_Z, q);                                                             \
         else hipLaunchKernelGGL((k_nn_step<W, P>), gn, blk, 0, st, d_D, n, method, d_size, d_chain, d_st, d_fwd,    \
                                 d_parts, d_done, d_Z, q);                                                        \
     } while (0)
@@ -575,9 +1123,16 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     HIPC(hipMemcpyAsync(&done, d_done, 4, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));
     if (done != (int32_t)n - 1) { set_error("linkage did not finish"); return DREPHIP_ERR_INTERNAL; }
-    LinkState hs[2];
-    HIPC(hipMemcpy(hs, d_st, sizeof(hs), hipMemcpyDeviceToHost));
-    const int32_t bad = hs[0].bad | hs[1].bad;
+    int32_t bad;
+    if (cached) {
+        CLinkState hs[2];
+        HIPC(hipMemcpy(hs, d_cst, sizeof(hs), hipMemcpyDeviceToHost));
+        bad = hs[0].bad | hs[1].bad;
+    } else {
+        LinkState hs[2];
+        HIPC(hipMemcpy(hs, d_st, sizeof(hs), hipMemcpyDeviceToHost));
+        bad = hs[0].bad | hs[1].bad;
+    }
     if (bad) { set_error("linkage: a chain step found no valid partial"); return DREPHIP_ERR_INTERNAL; }
     const double t_fin = now_s();
     ctx->link.chain_s = t_fin - t_chain;

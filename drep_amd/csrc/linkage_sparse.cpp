@@ -45,6 +45,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <numeric>
+#include <queue>
 #include <thread>
 #include <vector>
 #include <sys/mman.h>
@@ -258,6 +259,251 @@ void prim_component(const Comp &C, const uint32_t *members, const double *mat, d
     }
 }
 
+// ---------------------------------------------------------------------------
+// The sparse-row chain: scipy's nn_chain without any matrix, for a set whose
+// pairs below 1.0 join (almost) everything into one component -- Mash data at
+// scale, where chance shared hashes link unrelated genomes.  Every cluster
+// keeps the entries of its row below 1.0; an entry not stored is 1.0.
+//
+// Rows are never searched or edited in place.  Cluster c's row has two parts:
+//   own[c]   the row written when c was formed (stamp[c]; the input pairs for
+//            a genome, stamp 0): its entry for j is current while j has not
+//            been re-formed since (stamp[j] <= stamp[c]), and
+//   newer[c] entries (j, t, v) appended when a merge formed j at time t with
+//            an entry for c: current while stamp[j] == t.
+// Clusters merged away (size 0) are skipped everywhere.  So a merge of x into
+// y writes y's new row once (Lance-Williams over the union of the two rows,
+// 1.0 where a row has no entry) and appends one entry to each neighbour's
+// newer list -- no lookups in other rows.  A search of row x reads x's two
+// lists only (and drops the stale entries it meets); the ties follow scipy's
+// scan as in chain_sparse: the previous chain element when nothing is
+// strictly smaller, else the lowest index of the row minimum; with nothing
+// below 1.0 and no previous element, the lowest active index.
+struct REnt {
+    uint32_t j, t;
+    double v;
+};
+
+struct RList {                 // malloc'd entry list; cap == 0: a slice of the input arrays (not owned)
+    REnt *p = nullptr;
+    uint32_t len = 0, cap = 0;
+    void release() {
+        if (cap) free(p);
+        p = nullptr; len = cap = 0;
+    }
+};
+
+struct RowsChain {
+    uint32_t n;
+    int method;
+    std::vector<uint64_t> meta;    // size (low 32 bits, 0 = merged away) | stamp << 32
+    std::vector<RList> own, nw;
+    std::vector<REnt> base;        // the input pairs, both directions, grouped by row
+    std::vector<uint32_t> ep;      // merge scratch, per cluster
+    std::vector<double> vx, vy;
+    std::vector<uint32_t> touched;
+    std::vector<REnt> row;
+    uint64_t scanned = 0, appended = 0, scans = 0;
+    double t_scan = 0, t_gather = 0, t_row = 0, t_append = 0;
+    bool oom = false;
+
+    static uint32_t size_of(uint64_t m) { return (uint32_t)m; }
+    static uint32_t stamp_of(uint64_t m) { return (uint32_t)(m >> 32); }
+
+    RowsChain(uint32_t n_, uint64_t np, const uint32_t *pi, const uint32_t *pj, const double *pv, int method_)
+        : n(n_), method(method_), meta(n_, 1), own(n_), nw(n_), ep(n_, 0), vx(n_), vy(n_) {
+        std::vector<uint64_t> off(n + 1, 0);
+        for (uint64_t t = 0; t < np; t++) { off[pi[t] + 1]++; off[pj[t] + 1]++; }
+        for (uint32_t v = 0; v < n; v++) off[v + 1] += off[v];
+        base.resize(2 * np);
+        std::vector<uint64_t> w(off.begin(), off.end() - 1);
+        for (uint64_t t = 0; t < np; t++) {
+            base[w[pi[t]]++] = REnt{pj[t], 0, pv[t]};
+            base[w[pj[t]]++] = REnt{pi[t], 0, pv[t]};
+        }
+        for (uint32_t v = 0; v < n; v++) { own[v].p = base.data() + off[v]; own[v].len = (uint32_t)(off[v + 1] - off[v]); }
+    }
+    ~RowsChain() {
+        for (auto &l : own) l.release();
+        for (auto &l : nw) l.release();
+    }
+
+    bool append(RList &l, const REnt &e) {
+        if (l.len == l.cap) {
+            // first drop the stale entries; grow only if at least half remain
+            uint32_t w = 0;
+            for (uint32_t a = 0; a < l.len; a++) {
+                const uint64_t m = meta[l.p[a].j];
+                if (size_of(m) && stamp_of(m) == l.p[a].t) l.p[w++] = l.p[a];
+            }
+            l.len = w;
+            if (w + 1 > l.cap / 2) {
+                const uint32_t nc = std::max<uint32_t>(16, l.cap * 2);
+                REnt *q = (REnt *)realloc(l.p, (size_t)nc * sizeof(REnt));
+                if (!q) { oom = true; return false; }
+                l.p = q; l.cap = nc;
+            }
+        }
+        l.p[l.len++] = e;
+        return true;
+    }
+
+    // calls f(j, v) for every current entry of x's row, compacting both lists
+    template <class F> void visit(uint32_t x, F f) {
+        const uint32_t sx = stamp_of(meta[x]);
+        RList &o = own[x];
+        uint32_t w = 0;
+        for (uint32_t a = 0; a < o.len; a++) {
+            const REnt e = o.p[a];
+            const uint64_t m = meta[e.j];
+            if (!size_of(m) || stamp_of(m) > sx) continue;
+            o.p[w++] = e;
+            f(e.j, e.v);
+        }
+        scanned += o.len;
+        o.len = w;
+        RList &q = nw[x];
+        w = 0;
+        for (uint32_t a = 0; a < q.len; a++) {
+            const REnt e = q.p[a];
+            const uint64_t m = meta[e.j];
+            if (!size_of(m) || stamp_of(m) != e.t) continue;
+            q.p[w++] = e;
+            f(e.j, e.v);
+        }
+        scanned += q.len;
+        q.len = w;
+    }
+
+    int run(std::vector<double> &Z) {
+        ActiveList act(n);
+        std::vector<uint32_t> chain(n);
+        uint32_t len = 0, clock = 0, epoch = 0;
+        for (uint32_t k = 0; k + 1 < n; k++) {
+            if (len == 0) { chain[0] = act.first(); len = 1; }
+            uint32_t x, y;
+            double cur;
+            double ta = host_now_s();
+            for (;;) {
+                x = chain[len - 1];
+                scans++;
+                const uint32_t pvx = len > 1 ? chain[len - 2] : kNone;
+                double best = INFINITY, dp = 1.0;
+                uint32_t by = kNone;
+                visit(x, [&](uint32_t j, double v) {
+                    if (v < best || (v == best && j < by)) { best = v; by = j; }
+                    if (j == pvx) dp = v;
+                });
+                if (len > 1) {
+                    if (best < dp) { y = by; cur = best; }
+                    else { y = pvx; cur = dp; break; }
+                } else if (best < 1.0) {
+                    y = by; cur = best;
+                } else {                                          // every entry is 1.0
+                    y = act.first() == x ? act.after(x) : act.first();
+                    cur = 1.0;
+                }
+                if (len >= n) return DREPHIP_ERR_INTERNAL;
+                chain[len++] = y;
+            }
+            len -= 2;
+            double tb = host_now_s();
+            t_scan += tb - ta;
+            if (x > y) std::swap(x, y);
+            const uint32_t nx = size_of(meta[x]), ny = size_of(meta[y]);
+            Z[4ull * k] = x; Z[4ull * k + 1] = y; Z[4ull * k + 2] = cur; Z[4ull * k + 3] = nx + ny;
+            // y's new row: Lance-Williams over the union of the two rows
+            epoch++;
+            touched.clear();
+            visit(x, [&](uint32_t j, double v) {
+                if (j == y) return;
+                ep[j] = epoch; vx[j] = v; vy[j] = 1.0;
+                touched.push_back(j);
+            });
+            visit(y, [&](uint32_t j, double v) {
+                if (j == x) return;
+                if (ep[j] == epoch) { vy[j] = v; return; }
+                ep[j] = epoch; vx[j] = 1.0; vy[j] = v;
+                touched.push_back(j);
+            });
+            const uint32_t T = ++clock;
+            double tc = host_now_s();
+            t_gather += tc - tb;
+            row.clear();
+            for (uint32_t j : touched) {
+                const double u = lw_host(method, vx[j], vy[j], (int32_t)nx, (int32_t)ny);
+                if (u < 1.0) row.push_back(REnt{j, T, u});
+            }
+            scanned += touched.size();
+            meta[x] = 0;
+            meta[y] = (uint64_t)(nx + ny) | (uint64_t)T << 32;
+            act.remove(x);
+            own[x].release(); nw[x].release(); own[y].release(); nw[y].len = 0;
+            double td = host_now_s();
+            t_row += td - tc;
+            appended += row.size();
+            if (!row.empty()) {
+                RList &o = own[y];
+                o.p = (REnt *)malloc(row.size() * sizeof(REnt));
+                if (!o.p) return DREPHIP_ERR_NOMEM;
+                o.cap = o.len = (uint32_t)row.size();
+                std::copy(row.begin(), row.end(), o.p);
+                for (const REnt &e : row)
+                    if (!append(nw[e.j], REnt{y, T, e.v})) return DREPHIP_ERR_NOMEM;
+            }
+            t_append += host_now_s() - td;
+        }
+        if (std::getenv("DREPHIP_DEBUG"))
+            fprintf(stderr, "[drephip] rows chain: scans %llu appended %llu; scan %.3f gather %.3f row %.3f append %.3f s\n",
+                    (unsigned long long)scans, (unsigned long long)appended, t_scan, t_gather, t_row, t_append);
+        return oom ? DREPHIP_ERR_NOMEM : DREPHIP_OK;
+    }
+};
+
+// scipy's Prim (mst_single_linkage) over the sparse rows: keys below 1.0 in a
+// heap ordered by (key, index) (stale heap entries skipped), the lowest
+// unmerged index for a minimum at 1.0 -- after the first step every unmerged
+// key is <= 1.0, and scipy's scan keeps the first index of a minimum.
+int prim_rows(uint32_t n, uint64_t np, const uint32_t *pi, const uint32_t *pj, const double *pv,
+              std::vector<double> &Z, uint64_t *scanned) {
+    std::vector<uint64_t> off(n + 1, 0);
+    for (uint64_t t = 0; t < np; t++) { off[pi[t] + 1]++; off[pj[t] + 1]++; }
+    for (uint32_t v = 0; v < n; v++) off[v + 1] += off[v];
+    std::vector<uint32_t> adj(2 * np);
+    std::vector<double> av(2 * np);
+    {
+        std::vector<uint64_t> w(off.begin(), off.end() - 1);
+        for (uint64_t t = 0; t < np; t++) {
+            adj[w[pi[t]]] = pj[t]; av[w[pi[t]]++] = pv[t];
+            adj[w[pj[t]]] = pi[t]; av[w[pj[t]]++] = pv[t];
+        }
+    }
+    std::vector<double> key(n, 1.0);
+    std::vector<uint8_t> merged(n, 0);
+    ActiveList act(n);
+    using HE = std::pair<double, uint32_t>;
+    std::priority_queue<HE, std::vector<HE>, std::greater<HE>> heap;
+    uint32_t x = 0;
+    for (uint32_t k = 0; k + 1 < n; k++) {
+        merged[x] = 1;
+        act.remove(x);
+        for (uint64_t e = off[x]; e < off[x + 1]; e++) {
+            const uint32_t i = adj[e];
+            if (!merged[i] && av[e] < key[i]) { key[i] = av[e]; heap.push(HE(av[e], i)); }
+        }
+        *scanned += off[x + 1] - off[x];
+        while (!heap.empty() && (merged[heap.top().second] || heap.top().first != key[heap.top().second])) heap.pop();
+        uint32_t y;
+        double cur;
+        if (!heap.empty()) { y = heap.top().second; cur = heap.top().first; heap.pop(); }
+        else { y = act.first(); cur = 1.0; }
+        if (y >= n) return DREPHIP_ERR_INTERNAL;
+        Z[4ull * k] = x; Z[4ull * k + 1] = y; Z[4ull * k + 2] = cur; Z[4ull * k + 3] = 0;
+        x = y;
+    }
+    return DREPHIP_OK;
+}
+
 }  // namespace
 
 unsigned host_threads() {
@@ -278,7 +524,8 @@ template <class F> static void for_components(size_t nc, F fn) {
 }
 
 int linkage_sparse_impl(uint32_t n, uint64_t np, const uint32_t *pi, const uint32_t *pj, const double *pv,
-                        int method, uint64_t max_cells, uint32_t max_comp, double *Z_out, SparseLinkInfo *info) {
+                        int method, uint64_t max_cells, uint32_t max_comp, double *Z_out, SparseLinkInfo *info,
+                        int rows) {
     SparseLinkInfo loc_info;
     SparseLinkInfo &I = info ? *info : loc_info;
     I = SparseLinkInfo{};
@@ -332,6 +579,35 @@ int linkage_sparse_impl(uint32_t n, uint64_t np, const uint32_t *pi, const uint3
         }
         I.components = (uint32_t)comps.size();
         I.cells = cells;
+        if (const char *e = std::getenv("DREPHIP_LINK_ROWS")) rows = atoi(e);
+        if (rows == 2 || (rows == 1 && (cells > max_cells || I.largest > max_comp))) {
+            I.rows = 1;
+            I.setup_s = host_now_s() - t0;
+            std::vector<double> Z(4ull * (n - 1));
+            int rc;
+            if (method == DREPHIP_LINK_SINGLE) {
+                rc = prim_rows(n, np, pi, pj, pv, Z, &I.scanned);
+            } else {
+                RowsChain rc_chain(n, np, pi, pj, pv, method);
+                rc = rc_chain.run(Z);
+                I.scanned = rc_chain.scanned;
+            }
+            if (rc) {
+                set_error(rc == DREPHIP_ERR_NOMEM ? "sparse linkage: host allocation failed"
+                                                  : "sparse linkage: inconsistent chain state");
+                return rc;
+            }
+            const double t1 = host_now_s();
+            I.chain_s = t1 - t0 - I.setup_s;
+            sort_and_label(Z, n);
+            std::copy(Z.begin(), Z.end(), Z_out);
+            I.finish_s = host_now_s() - t1;
+            if (std::getenv("DREPHIP_DEBUG"))
+                fprintf(stderr, "[drephip] sparse-row linkage: n=%u pairs=%llu largest=%u setup %.4f s chain %.4f s "
+                        "(%.3g entries read) finish %.4f s\n", n, (unsigned long long)np, I.largest, I.setup_s,
+                        I.chain_s, (double)I.scanned, I.finish_s);
+            return DREPHIP_OK;
+        }
         if (cells > max_cells || I.largest > max_comp) {
             set_error("sparse linkage: the components need " + std::to_string(cells) + " matrix cells (limit " +
                       std::to_string(max_cells) + "), the largest has " + std::to_string(I.largest) +

@@ -47,6 +47,7 @@
 namespace drephip {
 
 constexpr int kScWG = 256;
+constexpr uint32_t kItemBlock = 32;          // row tiles per XCD block of the LIST items
 
 // every entry (g, k < nhash[g]) at eoff[g] + k; one workgroup per genome
 __global__ __launch_bounds__(kScWG) void k_screen_keys(const uint64_t *__restrict__ H, const uint32_t *__restrict__ nh,
@@ -393,11 +394,14 @@ __global__ __launch_bounds__(kScWG) void k_screen_count(const uint32_t *__restri
 }
 
 // per row tile (one workgroup): its marked columns in ascending order at
-// coff[t], its items at ioff[t] (thread u takes words [u*per, (u+1)*per))
+// coff[t] (thread u takes words [u*per, (u+1)*per)).  Item j of tile t goes to launch slot ibase[t] + 8 j: slot w runs on XCD
+// w % 8, and the host deals blocks of kItemBlock consecutive row tiles to the
+// XCDs, so the tiles of one block (a genome family's rows, whose marked
+// columns largely coincide) stream their column sketches through one L2.
 __global__ __launch_bounds__(kScWG) void k_screen_lists(const uint32_t *__restrict__ bm, uint32_t NW, uint32_t C,
                                                         uint32_t row0, uint32_t R, const uint32_t *__restrict__ cnt,
                                                         const uint64_t *__restrict__ coff,
-                                                        const uint64_t *__restrict__ ioff, uint32_t *__restrict__ clist,
+                                                        const uint32_t *__restrict__ ibase, uint32_t *__restrict__ clist,
                                                         uint4 *__restrict__ items) {
     __shared__ uint32_t wsum[kScWG / 64];
     const uint32_t t = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
@@ -428,7 +432,8 @@ __global__ __launch_bounds__(kScWG) void k_screen_lists(const uint32_t *__restri
     const uint32_t n = cnt[t];
     const uint32_t ni = (n + C - 1) / C;
     for (uint32_t j = tid; j < ni; j += kScWG)
-        items[ioff[t] + j] = make_uint4(row0 + t * R, (uint32_t)(coff[t] + (uint64_t)j * C), min(C, n - j * C), 0);
+        items[(uint64_t)ibase[t] + 8ull * j] = make_uint4(row0 + t * R, (uint32_t)(coff[t] + (uint64_t)j * C),
+                                                          min(C, n - j * C), 0);
 }
 
 // denominators of the unscreened pairs: min(s, |A| + |B|) (no shared hash);
@@ -592,12 +597,11 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
     uint32_t rshift = 0;
     while ((1u << rshift) < R) rshift++;
     uint32_t *d_bm, *d_cnt, *d_itc;
-    uint64_t *d_coff, *d_ioff;
+    uint64_t *d_coff;
     if ((rc = scratch(ctx, "sc_bitmap", (uint64_t)ntiles * NW * 4, (void **)&d_bm))) return rc;
     if ((rc = scratch(ctx, "sc_tcnt", (ntiles + 1) * 4ull, (void **)&d_cnt))) return rc;
     if ((rc = scratch(ctx, "sc_titc", (ntiles + 1) * 4ull, (void **)&d_itc))) return rc;
     if ((rc = scratch(ctx, "sc_coff", (ntiles + 1) * 8ull, (void **)&d_coff))) return rc;
-    if ((rc = scratch(ctx, "sc_ioff", (ntiles + 1) * 8ull, (void **)&d_ioff))) return rc;
     // the pair map of the runs of two (k_screen_mark2), twice their count
     uint32_t pcap = 1024;
     while (pcap < 2ull * n2) pcap <<= 1;
@@ -640,24 +644,46 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
     hipLaunchKernelGGL(k_screen_count, dim3(ntiles), dim3(kScWG), 0, st, d_bm, NW, C, d_cnt, d_itc);
     // the last entry of each scan holds the totals: count entries ntiles + 1, the last one zero
     HIPC(hipMemsetAsync(d_cnt + ntiles, 0, 4, st));
-    HIPC(hipMemsetAsync(d_itc + ntiles, 0, 4, st));
     if ((rc = hip_scan(ctx, "sc_scan_tmp1", d_cnt, d_coff, ntiles + 1, st))) return rc;
-    if ((rc = hip_scan(ctx, "sc_scan_tmp2", d_itc, d_ioff, ntiles + 1, st))) return rc;
     prof.mark("count+scans", st);
+    uint32_t *h_itc, *ibase;
+    if ((rc = pinned_host(ctx, "sc_itc", ntiles * 4ull, (void **)&h_itc))) return rc;
+    if ((rc = pinned_host(ctx, "sc_ibase_h", ntiles * 4ull, (void **)&ibase))) return rc;
     HIPC(hipMemcpyAsync(h_tot, d_coff + ntiles, 8, hipMemcpyDeviceToHost, st));
-    HIPC(hipMemcpyAsync(h_tot + 1, d_ioff + ntiles, 8, hipMemcpyDeviceToHost, st));
     HIPC(hipMemcpyAsync(h_tot + 2, d_nsimple, 8, hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(h_itc, d_itc, ntiles * 4ull, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));
-    const uint64_t marked = h_tot[0], nitems = h_tot[1];
+    const uint64_t marked = h_tot[0];
     res->marked = marked;
     res->simple = h_tot[2];
+    // XCD placement: blocks of kItemBlock row tiles dealt in order to the
+    // least-loaded XCD; a tile's items sit at slots xcd + 8 (offset in that
+    // XCD's list + j); the lists are padded to one length with idle items
+    {
+        uint64_t load[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (uint32_t b0 = 0; b0 < ntiles; b0 += kItemBlock) {
+            uint32_t x = 0;
+            for (uint32_t k = 1; k < 8; k++) if (load[k] < load[x]) x = k;
+            for (uint32_t t = b0; t < std::min(ntiles, b0 + kItemBlock); t++) {
+                ibase[t] = (uint32_t)std::min<uint64_t>(x + 8 * load[x], 0xFFFFFFFFull);
+                load[x] += h_itc[t];
+            }
+        }
+        uint64_t lmax = 0;
+        for (uint32_t k = 0; k < 8; k++) lmax = std::max(lmax, load[k]);
+        h_tot[1] = 8 * lmax;
+    }
+    const uint64_t nitems = h_tot[1];
     if (marked >= (1ull << 32) || nitems >= (1ull << 31)) { timing_mark(ctx, 4, st, false); return DREPHIP_OK; }
-    uint32_t *d_list;
+    uint32_t *d_list, *d_ibase;
     uint4 *d_items;
     if ((rc = scratch(ctx, "sc_list", std::max<uint64_t>(marked, 1) * 4, (void **)&d_list))) return rc;
     if ((rc = scratch(ctx, "sc_items", std::max<uint64_t>(nitems, 1) * 16, (void **)&d_items))) return rc;
+    if ((rc = scratch(ctx, "sc_ibase", ntiles * 4ull, (void **)&d_ibase))) return rc;
+    HIPC(hipMemcpyAsync(d_ibase, ibase, ntiles * 4ull, hipMemcpyHostToDevice, st));
+    HIPC(hipMemsetAsync(d_items, 0xFF, std::max<uint64_t>(nitems, 1) * 16, st));       // idle items: i0 = ~0
     prof.mark("readback+alloc", st);
-    hipLaunchKernelGGL(k_screen_lists, dim3(ntiles), dim3(kScWG), 0, st, d_bm, NW, C, row0, R, d_cnt, d_coff, d_ioff,
+    hipLaunchKernelGGL(k_screen_lists, dim3(ntiles), dim3(kScWG), 0, st, d_bm, NW, C, row0, R, d_cnt, d_coff, d_ibase,
                        d_list, d_items);
     prof.mark("lists", st);
     timing_mark(ctx, 4, st, false);

@@ -507,19 +507,29 @@ def _sparse_instance(rng, n, kind):
     else:                                   # "dense": every pair below 1.0
         v = rng.integers(1, 50, m) / 64.0
     keep = (fam[iu[0]] == fam[iu[1]]) & (rng.random(m) < rng.random()) if kind != "dense" else np.ones(m, bool)
+    if kind == "chance":
+        # Mash at scale: families at continuous distances plus a few chance
+        # links between unrelated genomes at two distances (one or two shared
+        # hashes) -- one component, many ties at the chance level
+        v = np.where(fam[iu[0]] == fam[iu[1]], rng.random(m) * 0.2, rng.choice([0.33, 0.30], m))
+        keep = (fam[iu[0]] == fam[iu[1]]) | (rng.random(m) < 0.03)
     y = np.ones(m)
     y[keep] = v[keep]
     return y, iu
 
 
-@pytest.mark.parametrize("kind", ["ties", "cont", "near1", "dense"])
-def test_linkage_sparse_matches_scipy(kind):
+@pytest.mark.parametrize("rows", ["0", "2"])
+@pytest.mark.parametrize("kind", ["ties", "cont", "near1", "dense", "chance"])
+def test_linkage_sparse_matches_scipy(kind, rows, monkeypatch):
     """drephip_linkage_sparse (scipy's nn_chain / Prim replayed on the pairs
     below 1.0, every other pair at 1.0) == scipy.cluster.hierarchy.linkage of
     the dense matrix, bit for bit, for every method it serves -- including
     ties, clusters that lose every edge below 1.0 (complete linkage; weighted
-    averages rounding up to 1.0) and a set with no pair at 1.0."""
+    averages rounding up to 1.0) and a set with no pair at 1.0.  Both forms:
+    per-component matrices (rows 0) and the sparse-row chain / heap Prim
+    (rows 2, the form of one large component)."""
     import scipy.cluster.hierarchy as sch
+    monkeypatch.setenv("DREPHIP_LINK_ROWS", rows)
     rng = np.random.default_rng(len(kind))
     for trial in range(60):
         n = int(rng.integers(2, 120))
