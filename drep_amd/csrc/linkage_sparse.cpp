@@ -303,6 +303,7 @@ struct RowsChain {
     std::vector<double> vx, vy;
     std::vector<uint32_t> touched;
     std::vector<REnt> row;
+    bool dup = false;              // a pair listed twice (the caller refuses the list)
     uint64_t scanned = 0, appended = 0, scans = 0;
     double t_scan = 0, t_gather = 0, t_row = 0, t_append = 0;
     bool oom = false;
@@ -322,6 +323,21 @@ struct RowsChain {
             base[w[pj[t]]++] = REnt{pi[t], 0, pv[t]};
         }
         for (uint32_t v = 0; v < n; v++) { own[v].p = base.data() + off[v]; own[v].len = (uint32_t)(off[v + 1] - off[v]); }
+        // a pair listed twice shows as a repeated index in a row (host threads over row ranges)
+        const unsigned T = std::max(1u, std::min(host_threads(), n / 1024 + 1));
+        std::atomic<bool> d(false);
+        std::vector<std::thread> pool;
+        for (unsigned k = 0; k < T; k++)
+            pool.emplace_back([&, k] {
+                std::vector<uint32_t> mark(n, 0);
+                for (uint32_t v = (uint32_t)((uint64_t)n * k / T); v < (uint32_t)((uint64_t)n * (k + 1) / T); v++)
+                    for (uint64_t e = off[v]; e < off[v + 1]; e++) {
+                        if (mark[base[e].j] == v + 1) { d = true; return; }
+                        mark[base[e].j] = v + 1;
+                    }
+            });
+        for (auto &th : pool) th.join();
+        dup = d.load();
     }
     ~RowsChain() {
         for (auto &l : own) l.release();
@@ -478,6 +494,14 @@ int prim_rows(uint32_t n, uint64_t np, const uint32_t *pi, const uint32_t *pj, c
             adj[w[pj[t]]] = pi[t]; av[w[pj[t]]++] = pv[t];
         }
     }
+    {
+        std::vector<uint32_t> mark(n, 0);
+        for (uint32_t v = 0; v < n; v++)
+            for (uint64_t e = off[v]; e < off[v + 1]; e++) {
+                if (mark[adj[e]] == v + 1) return DREPHIP_ERR_ARG;
+                mark[adj[e]] = v + 1;
+            }
+    }
     std::vector<double> key(n, 1.0);
     std::vector<uint8_t> merged(n, 0);
     ActiveList act(n);
@@ -589,9 +613,10 @@ int linkage_sparse_impl(uint32_t n, uint64_t np, const uint32_t *pi, const uint3
                 rc = prim_rows(n, np, pi, pj, pv, Z, &I.scanned);
             } else {
                 RowsChain rc_chain(n, np, pi, pj, pv, method);
-                rc = rc_chain.run(Z);
+                rc = rc_chain.dup ? DREPHIP_ERR_ARG : rc_chain.run(Z);
                 I.scanned = rc_chain.scanned;
             }
+            if (rc == DREPHIP_ERR_ARG) { set_error("sparse linkage: a pair is listed twice"); return rc; }
             if (rc) {
                 set_error(rc == DREPHIP_ERR_NOMEM ? "sparse linkage: host allocation failed"
                                                   : "sparse linkage: inconsistent chain state");

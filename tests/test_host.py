@@ -545,9 +545,12 @@ def test_linkage_sparse_matches_scipy(kind, rows, monkeypatch):
             assert np.array_equal(Z, Zs), (kind, trial, n, method, np.argwhere(Z != Zs)[:4])
 
 
-def test_linkage_sparse_rejects_bad_lists():
+@pytest.mark.parametrize("rows", ["0", "2"])
+def test_linkage_sparse_rejects_bad_lists(rows, monkeypatch):
     """A pair listed twice, a value at or above 1.0 (not a sparse entry), an
-    index out of range or i == j is refused, not silently clustered."""
+    index out of range or i == j is refused, not silently clustered (both
+    forms)."""
+    monkeypatch.setenv("DREPHIP_LINK_ROWS", rows)
     with pytest.raises(_lib.DrepHipError, match="twice"):
         _lib.linkage_sparse(4, [0, 1], [1, 0], [0.5, 0.5], "average")
     with pytest.raises(_lib.DrepHipError, match="twice"):
