@@ -28,6 +28,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
@@ -64,17 +65,42 @@ __device__ __forceinline__ double lw_update(int method, double dxi, double dyi, 
     return __ddiv_rn(__dadd_rn(__dmul_rn((double)nx, dxi), __dmul_rn((double)ny, dyi)), (double)(nx + ny));
 }
 
+// Wave argmin by DPP (row_shr 1/2/4/8 within each 16-lane row, then
+// row_bcast 15/31 across rows): lane 63 ends with the wave's minimum, which
+// readlane broadcasts.  A step moves three dwords lane to lane in a few
+// cycles, where the __shfl_xor butterfly (ds_bpermute through the LDS
+// crossbar) took ~100 cycles per step -- the chain steps are latency-bound and
+// reduce twice each.  Lanes a shift leaves without a source keep the identity
+// (inf, INT_MAX).  Needs every lane of the wave active.
+template <int CTRL, int RM>
+__device__ __forceinline__ void dpp_argmin_step(double &v, int32_t &i) {
+    const long long b = __double_as_longlong(v);
+    const long long ib = __double_as_longlong((double)INFINITY);
+    const int olo = __builtin_amdgcn_update_dpp((int)ib, (int)b, CTRL, RM, 0xf, false);
+    const int ohi = __builtin_amdgcn_update_dpp((int)(ib >> 32), (int)(b >> 32), CTRL, RM, 0xf, false);
+    const int oi = __builtin_amdgcn_update_dpp(0x7fffffff, i, CTRL, RM, 0xf, false);
+    const double ov = __longlong_as_double((long long)(((unsigned long long)(unsigned)ohi << 32) | (unsigned)olo));
+    if (better(ov, oi, v, i)) { v = ov; i = oi; }
+}
+__device__ __forceinline__ void wave_argmin(double &v, int32_t &i) {
+    dpp_argmin_step<0x111, 0xf>(v, i);
+    dpp_argmin_step<0x112, 0xf>(v, i);
+    dpp_argmin_step<0x114, 0xf>(v, i);
+    dpp_argmin_step<0x118, 0xf>(v, i);
+    dpp_argmin_step<0x142, 0xa>(v, i);
+    dpp_argmin_step<0x143, 0xc>(v, i);
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, 63), hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+    v = __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+    i = __builtin_amdgcn_readlane(i, 63);
+}
+
 // Block argmin (smallest index among equal minima); result valid in thread 0.
 template <int WG>
 __device__ MinIdx block_argmin(double v, int32_t i) {
     __shared__ double sv[WG / 64];
     __shared__ int32_t si[WG / 64];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const double ov = __shfl_xor(v, o, 64);
-        const int32_t oi = __shfl_xor(i, o, 64);
-        if (better(ov, oi, v, i)) { v = ov; i = oi; }
-    }
+    wave_argmin(v, i);
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) { sv[w] = v; si[w] = i; }
     __syncthreads();
@@ -395,7 +421,12 @@ __global__ __launch_bounds__(WG) void k_mst_step(const double *__restrict__ D, u
 //
 // Races: within a launch the loops read the caches of the clusters they push
 // (P, the same list in every workgroup) and nothing else, so no cache in P is
-// written during the launch: the merge's maintenance skips them, and they --
+// written during the launch (a loop that read a cache another workgroup had
+// just rewritten would decide differently from the others).  y's cache is
+// left as it was by the merge that re-forms y: y's search result comes from
+// the P2 partials until the next launch's forwarding workgroup rewrites the
+// cache (or a merge re-forms y again, and its successor does).  The merge's
+// maintenance skips the clusters in P, and they --
 // with the new top after a merge, whose maintenance would need the value
 // another workgroup computes -- are invalidated by workgroup 0 of the next
 // launch (they are chain members: their caches are not needed unless a
@@ -417,6 +448,7 @@ struct alignas(64) CLinkState {
     int32_t bad;
     int32_t psa, psb, psbsz;        // sizes changed by this state's merge (as in LinkState)
     int32_t ninval;                 // rows whose caches the next launch invalidates (list: cinval[parity])
+    int32_t launches, pushes;       // working launches so far, pushes decided from caches
 };
 
 struct alignas(64) CLinkFwd {
@@ -426,43 +458,8 @@ struct alignas(64) CLinkFwd {
 
 __device__ __forceinline__ bool lex_lt(double v, int32_t i, double w, int32_t j) { return v < w || (v == w && i < j); }
 
-// wave-wide minimum of (v, i) by butterfly (every lane gets it)
-__device__ __forceinline__ void wave_min(double &v, int32_t &i) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const double ov = __shfl_xor(v, o, 64);
-        const int32_t oi = __shfl_xor(i, o, 64);
-        if (better(ov, oi, v, i)) { v = ov; i = oi; }
-    }
-}
-
-// The two smallest (v, i) of the workgroup from each lane's sorted pair
-// (a0 <= a1); result in thread 0 (r[0] <= r[1]).
-template <int WG>
-__device__ void block_min2(double a0v, int32_t a0i, double a1v, int32_t a1i, MinIdx r[2]) {
-    __shared__ MinIdx sw[WG / 64][2];
-    double v = a0v;
-    int32_t i = a0i;
-    wave_min(v, i);
-    const double w1v = v;
-    const int32_t w1i = i;
-    if (a0i == w1i && a0v == w1v) { a0v = a1v; a0i = a1i; }       // the winner's lane pops its head
-    v = a0v; i = a0i;
-    wave_min(v, i);
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) { sw[w][0] = MinIdx{w1v, w1i}; sw[w][1] = MinIdx{v, i}; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        MinIdx b0{INFINITY, 0x7fffffff}, b1{INFINITY, 0x7fffffff};
-        for (int k = 0; k < WG / 64; k++)
-            for (int e = 0; e < 2; e++) {
-                const MinIdx c = sw[k][e];
-                if (better(c.v, c.i, b0.v, b0.i)) { b1 = b0; b0 = c; }
-                else if (better(c.v, c.i, b1.v, b1.i)) b1 = c;
-            }
-        r[0] = b0; r[1] = b1;
-    }
-}
+// wave-wide minimum of (v, i) (every lane gets it)
+__device__ __forceinline__ void wave_min(double &v, int32_t &i) { wave_argmin(v, i); }
 
 // a sorted list of up to three entries in named slots (no private arrays:
 // dynamic indexing would put them in scratch memory); empty slots are
@@ -498,15 +495,6 @@ __device__ __forceinline__ void l3_pop_back(L3 &l) {
     l.b = sel(l.cnt == 2, E, l.b);
     l.a = sel(l.cnt == 1, E, l.a);
     l.cnt--;
-}
-
-// lane-local insertion into a sorted pair
-__device__ __forceinline__ void ins2(double v, int32_t i, double &a0v, int32_t &a0i, double &a1v, int32_t &a1i) {
-    const bool l0 = better(v, i, a0v, a0i), l1 = better(v, i, a1v, a1i);
-    a1v = l0 ? a0v : l1 ? v : a1v;
-    a1i = l0 ? a0i : l1 ? i : a1i;
-    a0v = l0 ? v : a0v;
-    a0i = l0 ? i : a0i;
 }
 
 // Initial caches: per row the three smallest entries (i != row): two cached,
@@ -558,6 +546,18 @@ __global__ __launch_bounds__(WG) void k_cache_init(const double *__restrict__ D,
     }
 }
 
+// A partial with its candidate's cache head and size attached (as of the end
+// of the launch that wrote it), so a push decided from a partial needs no
+// further load; hi = -1: no usable head.
+struct alignas(32) MinIdxP {
+    double v;
+    int32_t i, sz;
+    double hv;
+    int32_t hi, pad;
+};
+
+__device__ __forceinline__ MinIdx first_of(const MinIdxP &a) { return MinIdx{a.v, a.i}; }
+
 // Cache of row r from the P2 partials of the launch that formed r (each
 // workgroup's two smallest entries): entries outside every pair are >= the
 // smallest second entry U, so the cache takes the candidates below U (at most
@@ -565,7 +565,8 @@ __global__ __launch_bounds__(WG) void k_cache_init(const double *__restrict__ D,
 // (mx, my), that merge's effect (see the header above).  Block-wide; the
 // result is written by thread 0.
 template <int WG>
-__device__ void cache_refresh(const MinIdx *__restrict__ p2, uint32_t G, int32_t r, const double *__restrict__ D,
+__device__ void cache_refresh(const MinIdxP *__restrict__ p2a, const MinIdx *__restrict__ p2b, uint32_t G, int32_t r,
+                              const double *__restrict__ D,
                               uint32_t n, int method, bool merge, int32_t mx, int32_t my, int32_t mnx, int32_t mny,
                               int2 *__restrict__ ci, double2 *__restrict__ cv, double *__restrict__ cb,
                               int32_t *__restrict__ cbi) {
@@ -577,7 +578,7 @@ __device__ void cache_refresh(const MinIdx *__restrict__ p2, uint32_t G, int32_t
     double a0v = INFINITY, a1v = INFINITY, a2v = INFINITY;
     int32_t a0i = 0x7fffffff, a1i = 0x7fffffff, a2i = 0x7fffffff;
     for (uint32_t b = threadIdx.x; b < G; b += blockDim.x) {
-        const MinIdx e0 = p2[2 * b], e1 = p2[2 * b + 1];
+        const MinIdx e0 = first_of(p2a[b]), e1 = p2b[b];
         if (better(e1.v, e1.i, uv, ui)) { uv = e1.v; ui = e1.i; }
         for (int e = 0; e < 2; e++) {
             const MinIdx c = e ? e1 : e0;
@@ -637,41 +638,84 @@ __device__ void cache_refresh(const MinIdx *__restrict__ p2, uint32_t G, int32_t
     cbi[r] = B.i;
 }
 
+// block argmin of (v, i) carrying the payload; result valid in thread 0
+template <int WG>
+__device__ MinIdxP block_argmin_p(MinIdxP a) {
+    __shared__ MinIdxP sw[WG / 64];
+    // (v, i) by DPP; the payload read from the winning lane
+    double wv = a.v;
+    int32_t wi = a.i;
+    wave_argmin(wv, wi);
+    const unsigned long long m = __ballot(a.i == wi && a.v == wv);
+    const int lane = m ? (int)__ffsll((long long)m) - 1 : 0;
+    if ((threadIdx.x & 63) == 0) {
+        MinIdxP r;
+        r.v = wv;
+        r.i = wi;
+        r.sz = __builtin_amdgcn_readlane(a.sz, lane);
+        const long long hb = __double_as_longlong(a.hv);
+        r.hv = __longlong_as_double((long long)(((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(hb >> 32), lane) << 32) |
+                                                 (unsigned)__builtin_amdgcn_readlane((int)hb, lane)));
+        r.hi = __builtin_amdgcn_readlane(a.hi, lane);
+        r.pad = 0;
+        sw[threadIdx.x >> 6] = r;
+    }
+    __syncthreads();
+    MinIdxP r{INFINITY, 0x7fffffff, 0, INFINITY, -1, 0};
+    if (threadIdx.x == 0)
+        for (int k = 0; k < WG / 64; k++)
+            if (better(sw[k].v, sw[k].i, r.v, r.i)) r = sw[k];
+    return r;
+}
+
 template <int WG, int kLkPer>
 __global__ __launch_bounds__(WG) void k_nn_cstep(double *__restrict__ D, uint32_t n, int method,
                                                     int32_t *__restrict__ size, int32_t *__restrict__ chain,
                                                     CLinkState *__restrict__ st, CLinkFwd *__restrict__ fwd,
-                                                    MinIdx *__restrict__ parts1, MinIdx *__restrict__ parts2,
-                                                    int32_t *__restrict__ cinval,
+                                                    MinIdxP *__restrict__ parts1, MinIdxP *__restrict__ parts2,
+                                                    MinIdx *__restrict__ parts2b, int32_t *__restrict__ cinval,
                                                     int2 *__restrict__ ci, double2 *__restrict__ cv,
                                                     double *__restrict__ cb, int32_t *__restrict__ cbi,
-                                                    int32_t *__restrict__ done, double *__restrict__ Z, uint32_t q) {
+                                                    int32_t *__restrict__ done, double *__restrict__ Z, uint32_t q,
+                                                    long long *__restrict__ dbg) {
+    // phase timestamps of workgroups 0 and G in one launch (DREPHIP_LINK_TRACE_AT: its launch index)
+    const long long t_start = wall_clock64();
+#define LKC_T(slot)                                                                                              \
+    do {                                                                                                         \
+        if (dbg && threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1) &&                       \
+            S.launches == (int32_t)dbg[63]) {                                                                    \
+            dbg[(blockIdx.x == 0 ? 0 : 16) + (slot)] = wall_clock64() - t_start;                                 \
+        }                                                                                                        \
+    } while (0)
     __shared__ CLinkState sx;
     __shared__ int32_t s_pushed[kCPush];
     __shared__ int32_t s_skip[2 * kCInval + 2], s_nskip;
+    __shared__ int32_t s_sinval[kCInval];
     const uint32_t G = gridDim.x - 1;                          // step workgroups; workgroup G forwards
+    // everything the decision needs, loaded together: state, forwarded
+    // operands, the invalidation list, both partial sets
     const CLinkState S = st[q ^ 1];
     const CLinkFwd F = fwd[q ^ 1];
-    const MinIdx g1 = read_partials<WG>(parts1 + (uint64_t)(q ^ 1) * 1024, G);
-    // P2 minimum: the first entries of the pairs (stride 2)
-    double b2v = INFINITY;
-    int32_t b2i = 0x7fffffff;
+    if (threadIdx.x < kCInval) s_sinval[threadIdx.x] = cinval[(q ^ 1) * kCInval + threadIdx.x];
+    MinIdxP a1{INFINITY, 0x7fffffff, 0, INFINITY, -1, 0}, a2 = a1;
     for (uint32_t b = threadIdx.x; b < G; b += blockDim.x) {
-        const MinIdx m = parts2[((uint64_t)(q ^ 1) * 1024 + b) * 2];
-        if (better(m.v, m.i, b2v, b2i)) { b2v = m.v; b2i = m.i; }
+        const MinIdxP m1 = parts1[(uint64_t)(q ^ 1) * 1024 + b];
+        const MinIdxP m2 = parts2[(uint64_t)(q ^ 1) * 1024 + b];
+        if (better(m1.v, m1.i, a1.v, a1.i)) a1 = m1;
+        if (better(m2.v, m2.i, a2.v, a2.i)) a2 = m2;
     }
+    const MinIdxP g1 = block_argmin_p<WG>(a1);
     __syncthreads();
-    const MinIdx g2 = block_argmin<WG>(b2v, b2i);
+    const MinIdxP g2 = block_argmin_p<WG>(a2);
     if (S.k >= (int32_t)n - 1) return;
+    LKC_T(1);
     const bool w0 = blockIdx.x == 0;
-    auto size_prev = [&](int32_t i, int32_t stored) {
-        return i == S.psa ? 0 : i == S.psb ? S.psbsz : stored;
+    const int32_t spsa = S.psa, spsb = S.psb, spsbsz = S.psbsz;
+    auto size_prev = [=](int32_t i, int32_t stored) {          // (by value: a reference would put S in scratch)
+        return i == spsa ? 0 : i == spsb ? spsbsz : stored;
     };
     if (w0 && threadIdx.x == 0 && S.psa >= 0) { size[S.psa] = 0; size[S.psb] = S.psbsz; }
-    __shared__ int32_t s_sinval[kCInval];
     const int sninval = S.ninval;
-    if ((int)threadIdx.x < sninval) s_sinval[threadIdx.x] = cinval[(q ^ 1) * kCInval + threadIdx.x];
-    __syncthreads();
     if (threadIdx.x == 0) {
         // ---- the decision loop (replicated in every workgroup)
         CLinkState X = S;
@@ -682,8 +726,8 @@ __global__ __launch_bounds__(WG) void k_nn_cstep(double *__restrict__ D, uint32_
         int32_t szt = F.szt, szb = F.szb;
         int np = 0;
         bool have = S.decide != 0, merged = false;
-        MinIdx res = g1;
-        int2 nhi = make_int2(-1, -1);                                // the pushed row's cache head (loaded with its size)
+        MinIdxP res = g1;
+        int2 nhi = make_int2(-1, -1);                                // the pushed row's cache head
         double nhv = INFINITY;
         for (;;) {
             if (!have) {
@@ -691,8 +735,11 @@ __global__ __launch_bounds__(WG) void k_nn_cstep(double *__restrict__ D, uint32_
                 else {
                     bool inv = false;
                     for (int e = 0; e < sninval && !inv; e++) inv = s_sinval[e] == top;
+#ifdef LKC_NOCACHEREAD
+                    inv = true;                                         // A/B only: every cache treated as empty
+#endif
                     if (inv || nhi.x < 0) break;
-                    res = MinIdx{nhv, nhi.x};
+                    res = MinIdxP{nhv, nhi.x, -1, INFINITY, -1, 0};    // size and head: loaded below
                 }
             }
             have = false;
@@ -729,17 +776,29 @@ __global__ __launch_bounds__(WG) void k_nn_cstep(double *__restrict__ D, uint32_
             s_pushed[np++] = a;
             c4 = c3; c3 = below; below = top; top = a;
             dp = res.v;
-            // a's size and cache head, loaded together (the head is ignored
-            // when a's cache is being written this launch: see the header)
-            const int32_t sza = size[a];
-            nhi = ci[a];
-            nhv = cv[a].x;
-            szb = szt; szt = size_prev(a, sza);
+            szb = szt;
+            if (res.sz >= 0) {
+                // decided from a partial: a's size and cache head came with it
+                szt = res.sz;
+                nhi = make_int2(res.hi, -1);
+                nhv = res.hv;
+            } else {
+                // decided from a cache: a's size and head are loaded (the head
+                // is ignored when a's cache is being written this launch)
+                const int32_t sza = size[a];
+                nhi = ci[a];
+                nhv = cv[a].x;
+                szt = size_prev(a, sza);
+            }
             len++;
         }
+        LKC_T(2);
+        if (dbg && S.launches == (int32_t)dbg[63] && (blockIdx.x == 0)) dbg[10] = np, dbg[11] = merged;
         X.len = len; X.top = top; X.below = below;
         X.decide = 1;
         X.mrow = merged ? X.y : -1;
+        X.launches = S.launches + 1;
+        X.pushes = S.pushes + np;
         // caches to invalidate next launch: the pushed rows, and after a merge
         // the new top; rows no maintenance of this launch may write: those,
         // the rows workgroup 0 invalidates now (the previous list) and the
@@ -761,9 +820,10 @@ __global__ __launch_bounds__(WG) void k_nn_cstep(double *__restrict__ D, uint32_
                 if (s_sinval[e] != S.mrow) ci[s_sinval[e]] = make_int2(-1, -1);
         }
         if (blockIdx.x == G && X.k < (int32_t)n - 1) {
-            auto size_now = [&](int32_t i) { return i == X.psa ? 0 : i == X.psb ? X.psbsz : size_prev(i, size[i]); };
+            const int32_t xpsa = X.psa, xpsb = X.psb, xpsbsz = X.psbsz, slen = S.len;
+            auto size_now = [=](int32_t i) { return i == xpsa ? 0 : i == xpsb ? xpsbsz : size_prev(i, size[i]); };
             // chain entries: this launch's pushes from the loop's record (workgroup 0 is writing them)
-            auto chain_at = [&](int32_t p) { return p >= S.len ? s_pushed[p - S.len] : chain[p]; };
+            auto chain_at = [=](int32_t p) { return p >= slen ? s_pushed[p - slen] : chain[p]; };
             CLinkFwd f{0.0, 0, 0, 0, 0};
             f.szt = size_now(X.top);
             if (X.len > 1) {
@@ -776,21 +836,28 @@ __global__ __launch_bounds__(WG) void k_nn_cstep(double *__restrict__ D, uint32_
         }
     }
     __syncthreads();
+    LKC_T(3);
     const CLinkState X = sx;
     if (blockIdx.x == G) {
         // the forwarding workgroup: the cache of the row the previous launch formed
         const int32_t r = S.mrow;
         if (r >= 0 && X.k < (int32_t)n - 1 && !(X.pend && (r == X.x || r == X.y))) {
             const int32_t szr = r == X.psa ? 0 : r == X.psb ? X.psbsz : size_prev(r, size[r]);
+#ifndef LKC_NOREFRESH
             if (szr > 0)
-                cache_refresh<WG>(parts2 + (uint64_t)(q ^ 1) * 2048, G, r, D, n, method, X.pend != 0, X.x, X.y, X.nx,
-                                  X.ny, ci, cv, cb, cbi);
+#else
+            if (szr < 0)                                                // A/B only (timing)
+#endif
+                cache_refresh<WG>(parts2 + (uint64_t)(q ^ 1) * 1024, parts2b + (uint64_t)(q ^ 1) * 1024, G, r, D,
+                                  n, method, X.pend != 0, X.x, X.y, X.nx, X.ny, ci, cv, cb, cbi);
         }
+        LKC_T(4);
         return;
     }
     if (X.k >= (int32_t)n - 1) return;                        // all merged (the last merge needs no update)
     // ---- this step: the pending update fused with the search of row t, the
-    // merged row's two smallest per workgroup, and the caches' maintenance
+    // merged row's two smallest per workgroup, and the caches' maintenance;
+    // every candidate carries its row's cache head (after this launch) and size
     const bool pend = X.pend != 0;
     const int32_t x = X.x, y = X.y, nx = X.nx, ny = X.ny, t = X.top;
     const double *Dt = D + (uint64_t)t * n;
@@ -798,10 +865,8 @@ __global__ __launch_bounds__(WG) void k_nn_cstep(double *__restrict__ D, uint32_
     double *Dy = D + (uint64_t)y * n;
     const double dxt = pend ? Dx[t] : 0.0, dyt = pend ? Dy[t] : 0.0;
     const int nskip = s_nskip;
-    double bv = INFINITY;
-    int32_t bi = 0x7fffffff;
-    double m0v = INFINITY, m1v = INFINITY;                       // this lane's two smallest of the new row y
-    int32_t m0i = 0x7fffffff, m1i = 0x7fffffff;
+    MinIdxP b1{INFINITY, 0x7fffffff, 0, INFINITY, -1, 0};       // this lane's best of row t
+    MinIdxP m0 = b1, m1 = b1;                                    // its two smallest of the new row y
     const uint32_t stride = G * WG;
     for (uint32_t i0 = blockIdx.x * WG + threadIdx.x; i0 < n; i0 += kLkPer * stride) {
         int32_t sz[kLkPer];
@@ -816,9 +881,10 @@ __global__ __launch_bounds__(WG) void k_nn_cstep(double *__restrict__ D, uint32_
             const uint32_t ic = i < n ? i : n - 1;
             sz[k] = size[ic];
             dt[k] = Dt[ic];
+            hi[k] = ci[ic]; hv[k] = cv[ic];
             if (pend) {
                 dx[k] = Dx[ic]; dy[k] = Dy[ic];
-                hi[k] = ci[ic]; hv[k] = cv[ic]; hb[k] = cb[ic]; hbi[k] = cbi[ic];
+                hb[k] = cb[ic]; hbi[k] = cbi[ic];
             }
         }
 #pragma unroll
@@ -827,17 +893,22 @@ __global__ __launch_bounds__(WG) void k_nn_cstep(double *__restrict__ D, uint32_
             if (i >= n) continue;
             const int32_t szi = (int32_t)i == X.psa ? 0 : (int32_t)i == X.psb ? X.psbsz : size_prev((int32_t)i, sz[k]);
             if (szi == 0) continue;
+            // row i's cache head as it stands after this launch (none when a
+            // row's cache is not maintained now, or i is y or t)
+            bool skip = hi[k].x < 0 || (pend && ((int32_t)i == y || (int32_t)i == t));
+            for (int e = 0; e < nskip && !skip; e++) skip = s_skip[e] == (int32_t)i;
+            int32_t phi = skip ? -1 : hi[k].x;
+            double phv = hv[k].x;
             double v;
             if (pend && (int32_t)i != y && (int32_t)i != t) {
                 const double u = lw_update(method, dx[k], dy[k], nx, ny);
                 Dy[i] = u;
                 D[(uint64_t)i * n + y] = u;
-                ins2(u, (int32_t)i, m0v, m0i, m1v, m1i);
-                v = t == y ? u : dt[k];
-                // cache maintenance of row i: x and y leave, (u, y) enters below the bound
-                bool skip = hi[k].x < 0;
-                for (int e = 0; e < nskip && !skip; e++) skip = s_skip[e] == (int32_t)i;
+#ifdef LKC_NOMAINT
+                skip = true;                                            // A/B only (timing)
+#endif
                 if (!skip) {
+                    // cache maintenance of row i: x and y leave, (u, y) enters below the bound
                     L3 l = l3_empty();
                     bool changed = false;
                     if (hi[k].x == x || hi[k].x == y) changed = true; else l3_push_back(l, MinIdx{hv[k].x, hi[k].x});
@@ -857,33 +928,54 @@ __global__ __launch_bounds__(WG) void k_nn_cstep(double *__restrict__ D, uint32_
                         cb[i] = nbv;
                         cbi[i] = nbi;
                     }
+                    phi = l.cnt > 0 ? l.a.i : -1;
+                    phv = l.a.v;
                 }
+                const MinIdxP c{u, (int32_t)i, szi, phv, phi, 0};
+                if (better(c.v, c.i, m0.v, m0.i)) { m1 = m0; m0 = c; }
+                else if (better(c.v, c.i, m1.v, m1.i)) m1 = c;
+                v = t == y ? u : dt[k];
             } else if (pend && (int32_t)i == y && t != y) {
                 const double u = lw_update(method, dxt, dyt, nx, ny);
                 Dy[t] = u;
                 D[(uint64_t)t * n + y] = u;
-                ins2(u, t, m0v, m0i, m1v, m1i);
-                ci[y] = make_int2(-1, -1);                       // y's row is new: its cache comes from P2
+                const int32_t szt_ = t == X.psa ? 0 : t == X.psb ? X.psbsz : size_prev(t, size[t]);
+                const MinIdxP c{u, t, szt_, INFINITY, -1, 0};          // t's cache is not maintained now
+                if (better(c.v, c.i, m0.v, m0.i)) { m1 = m0; m0 = c; }
+                else if (better(c.v, c.i, m1.v, m1.i)) m1 = c;
                 v = u;
+                if (v < b1.v || (v == b1.v && (int32_t)i < b1.i)) b1 = MinIdxP{v, (int32_t)i, szi, INFINITY, -1, 0};
+                continue;                                             // (y's cache: stale, see the header)
             } else {
-                if (pend && (int32_t)i == y) ci[y] = make_int2(-1, -1);
                 if ((int32_t)i == t) continue;
                 v = dt[k];
             }
-            if (v < bv) { bv = v; bi = (int32_t)i; }
+            if (v < b1.v || (v == b1.v && (int32_t)i < b1.i)) b1 = MinIdxP{v, (int32_t)i, szi, phv, phi, 0};
         }
     }
-    const MinIdx part = block_argmin<WG>(bv, bi);
+    LKC_T(4);
+    const MinIdxP part = block_argmin_p<WG>(b1);
     if (threadIdx.x == 0) parts1[(uint64_t)q * 1024 + blockIdx.x] = part;
+    LKC_T(5);
     if (pend) {
+        // the workgroup's two smallest of row y: its first by block argmin
+        // (with payload), its second as the smallest after removing the first
         __syncthreads();
-        MinIdx r2[2];
-        block_min2<WG>(m0v, m0i, m1v, m1i, r2);
+        const MinIdxP f0 = block_argmin_p<WG>(m0);
+        __shared__ MinIdxP s_f0;
+        if (threadIdx.x == 0) s_f0 = f0;
+        __syncthreads();
+        const MinIdxP w = s_f0;
+        const MinIdxP rest = (m0.i == w.i && m0.v == w.v) ? m1 : m0;
+        __syncthreads();
+        const MinIdxP f1 = block_argmin_p<WG>(rest);
         if (threadIdx.x == 0) {
-            parts2[((uint64_t)q * 1024 + blockIdx.x) * 2] = r2[0];
-            parts2[((uint64_t)q * 1024 + blockIdx.x) * 2 + 1] = r2[1];
+            parts2[(uint64_t)q * 1024 + blockIdx.x] = f0;
+            parts2b[(uint64_t)q * 1024 + blockIdx.x] = MinIdx{f1.v, f1.i};
         }
+        LKC_T(6);
     }
+#undef LKC_T
 }
 
 // ------------------------------------------------------------ matrix build
@@ -1022,26 +1114,38 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     double2 *d_cv = nullptr;
     double *d_cb = nullptr;
     int32_t *d_cbi = nullptr;
-    MinIdx *d_parts2 = nullptr;
+    MinIdxP *d_parts1c = nullptr, *d_parts2 = nullptr;
+    MinIdx *d_parts2b = nullptr;
     int32_t *d_cinval = nullptr;
     CLinkState *d_cst = nullptr;
     CLinkFwd *d_cfwd = nullptr;
+    long long *d_dbg = nullptr;
     if (cached) {
         if ((rc = scratch(ctx, "lk_ci", n * 8ull, (void **)&d_ci))) return rc;
         if ((rc = scratch(ctx, "lk_cv", n * 16ull, (void **)&d_cv))) return rc;
         if ((rc = scratch(ctx, "lk_cb", n * 8ull, (void **)&d_cb))) return rc;
         if ((rc = scratch(ctx, "lk_cbi", n * 4ull, (void **)&d_cbi))) return rc;
-        if ((rc = scratch(ctx, "lk_parts2", 2 * 1024 * 2 * sizeof(MinIdx), (void **)&d_parts2))) return rc;
+        if ((rc = scratch(ctx, "lk_parts1c", 2 * 1024 * sizeof(MinIdxP), (void **)&d_parts1c))) return rc;
+        if ((rc = scratch(ctx, "lk_parts2", 2 * 1024 * sizeof(MinIdxP), (void **)&d_parts2))) return rc;
+        if ((rc = scratch(ctx, "lk_parts2b", 2 * 1024 * sizeof(MinIdx), (void **)&d_parts2b))) return rc;
         if ((rc = scratch(ctx, "lk_cst", 2 * sizeof(CLinkState), (void **)&d_cst))) return rc;
         if ((rc = scratch(ctx, "lk_cinval", 2 * kCInval * 4ull, (void **)&d_cinval))) return rc;
         if ((rc = scratch(ctx, "lk_cfwd", 2 * sizeof(CLinkFwd), (void **)&d_cfwd))) return rc;
-        HIPC(hipMemsetAsync(d_parts2, 0, 2 * 1024 * 2 * sizeof(MinIdx), st));
+        HIPC(hipMemsetAsync(d_parts1c, 0, 2 * 1024 * sizeof(MinIdxP), st));
+        HIPC(hipMemsetAsync(d_parts2, 0, 2 * 1024 * sizeof(MinIdxP), st));
+        HIPC(hipMemsetAsync(d_parts2b, 0, 2 * 1024 * sizeof(MinIdx), st));
         HIPC(hipMemsetAsync(d_cfwd, 0, 2 * sizeof(CLinkFwd), st));
         CLinkState h[2] = {};
         h[1].len = 1; h[1].top = 0; h[1].below = -1; h[1].first_active = 0;
         h[1].psa = h[1].psb = -1; h[1].decide = 0; h[1].mrow = -1; h[1].ninval = 0;
         h[0] = h[1];
         HIPC(hipMemcpyAsync(d_cst, h, sizeof(h), hipMemcpyHostToDevice, st));
+        if (const char *ta = getenv("DREPHIP_LINK_TRACE_AT")) {
+            if ((rc = scratch(ctx, "lk_dbg", 64 * 8, (void **)&d_dbg))) return rc;
+            long long h[64] = {};
+            h[63] = atoll(ta);
+            HIPC(hipMemcpyAsync(d_dbg, h, sizeof(h), hipMemcpyHostToDevice, st));
+        }
         hipLaunchKernelGGL(k_cache_init<256>, dim3(n), dim3(256), 0, st, (const double *)d_D, n, d_ci, d_cv, d_cb, d_cbi);
         HIPC(hipGetLastError());
     }
@@ -1082,9 +1186,8 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
         if (mst) hipLaunchKernelGGL((k_mst_step<W, P>), gm, blk, 0, st, d_D, n, d_size, d_Dmin, d_st, d_parts, d_done, \
                                     d_Z, q);                                                                     \
         else if (cached) hipLaunchKernelGGL((k_nn_cstep<W, P>), gn, blk, 0, st, d_D, n, method, d_size, d_chain,   \
-                                            d_cst, d_cfwd, d_parts, d_parts2, d_cinval, d_ci, d_cv, d_cb, d_cbi, \
-                                            d_done,                                                              \
-                                            d_Z, q);                                                             \
+                                            d_cst, d_cfwd, d_parts1c, d_parts2, d_parts2b, d_cinval, d_ci, d_cv, \
+                                            d_cb, d_cbi, d_done, d_Z, q, d_dbg);                                 \
         else hipLaunchKernelGGL((k_nn_step<W, P>), gn, blk, 0, st, d_D, n, method, d_size, d_chain, d_st, d_fwd,    \
                                 d_parts, d_done, d_Z, q);                                                        \
     } while (0)
@@ -1128,6 +1231,17 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
         CLinkState hs[2];
         HIPC(hipMemcpy(hs, d_cst, sizeof(hs), hipMemcpyDeviceToHost));
         bad = hs[0].bad | hs[1].bad;
+        const CLinkState &hl = hs[0].launches > hs[1].launches ? hs[0] : hs[1];
+        ctx->link.launches = hl.launches;
+        if (getenv("DREPHIP_DEBUG"))
+            fprintf(stderr, "[drephip] cached chain: n=%u launches %d (merges %u), pushes %d\n", n,
+                    hl.launches, n - 1, hl.pushes);
+        if (d_dbg) {
+            long long h[64];
+            HIPC(hipMemcpy(h, d_dbg, sizeof(h), hipMemcpyDeviceToHost));
+            fprintf(stderr, "[drephip] launch %lld phases (10 ns): wg0 %lld %lld %lld %lld %lld %lld pushes %lld merged %lld | fwd %lld %lld %lld %lld\n",
+                    h[63], h[1], h[2], h[3], h[4], h[5], h[6], h[10], h[11], h[17], h[18], h[19], h[20]);
+        }
     } else {
         LinkState hs[2];
         HIPC(hipMemcpy(hs, d_st, sizeof(hs), hipMemcpyDeviceToHost));
