@@ -851,7 +851,8 @@ DREPHIP_EXPORT int drephip_linkage_sparse(uint32_t n, uint64_t npairs, const uin
                                           const double *v, int method, double *Z) {
     if (n < 2) return DREPHIP_OK;
     if (!Z || (npairs && (!i || !j || !v))) { set_error("null argument"); return DREPHIP_ERR_ARG; }
-    return linkage_sparse_impl(n, npairs, i, j, v, method, kSparseMaxCells, 0xFFFFFFFFu, Z, nullptr);
+    // components too large for their matrices: the sparse-row chain
+    return linkage_sparse_impl(n, npairs, i, j, v, method, kSparseMaxCells, 0xFFFFFFFFu, Z, nullptr, 1);
 }
 
 // the sparse path from a host condensed vector: the pairs below 1.0 when no
@@ -917,7 +918,8 @@ static int linkage_condensed_sparse(drephip_ctx *ctx, const double *y, uint32_t 
     }
     const double t1 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
     const int r = linkage_sparse_impl(n, pi.size(), pi.data(), pj.data(), pv.data(), method, sparse_cells(ctx),
-                                      sparse_maxcomp(ctx), Z, &ctx->link.sp);
+                                      sparse_maxcomp(ctx), Z, &ctx->link.sp,
+                                      ctx->link_path == DREPHIP_LINK_PATH_SPARSE ? 1 : 0);
     if (r == DREPHIP_ERR_UNSUPPORTED && ctx->link_path != DREPHIP_LINK_PATH_SPARSE) return 0;
     if (r) { *rc = r; return 0; }
     ctx->link.sparse = 1;
@@ -998,7 +1000,7 @@ DREPHIP_EXPORT int drephip_linkage_counts_device(drephip_ctx *ctx, const uint16_
             std::vector<double> pv(np);
             for (uint64_t t = 0; t < np; t++) { pi[t] = ij[2 * t]; pj[t] = ij[2 * t + 1]; pv[t] = lut[lidx[t]]; }
             rc = linkage_sparse_impl(n, np, pi.data(), pj.data(), pv.data(), method, sparse_cells(ctx),
-                                     sparse_maxcomp(ctx), Z, &ctx->link.sp);
+                                     sparse_maxcomp(ctx), Z, &ctx->link.sp, forced ? 1 : 0);
             if (rc == DREPHIP_OK) {
                 done = true;
                 ctx->link.sparse = 1;

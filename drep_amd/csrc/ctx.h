@@ -73,7 +73,6 @@ struct LinkStats {            // last drephip_linkage* call, host wall clock (se
     double finish_s = 0;      // Z readback + stable sort + relabel on the host
     double wall_s = 0;        // the whole call
     int sparse = 0;           // 1: the sparse path produced Z
-    int launches = 0;         // cached chain: working step launches (0: the plain step ran)
     SparseLinkInfo sp;        // its figures (pairs also when the dense path was chosen)
 };
 

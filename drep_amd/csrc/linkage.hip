@@ -398,586 +398,6 @@ __global__ __launch_bounds__(WG) void k_mst_step(const double *__restrict__ D, u
     if (threadIdx.x == 0) parts[(uint64_t)q * 1024 + blockIdx.x] = part;
 }
 
-// ------------------------------------------------ the cache-driven chain
-// Round 5 of the step design: fewer launches.  Three of every ~5 chain steps
-// at Mash scale are pushes, and a push's only work is the row search of the
-// pushed cluster -- a whole launch (~5.5 us at n = 10^5, latency-bound).  Each
-// active cluster j keeps a row cache: up to two entries of its row, the
-// smallest ones ((value, index) order), and a bound (bv, bi): every entry of
-// the row not in the cache is >= (bv, bi).  The cache's first entry is then
-// the row's minimum with scipy's tie rule (lowest index among equal values),
-// so a push can be decided from the cache without reading the row.
-//
-// A launch's decision loop (replicated in every workgroup, as before) starts
-// from the previous launch's search of the chain top, then follows pushes
-// through the caches of the pushed clusters until a merge (the launch applies
-// it and searches the new top, fused as before) or a cache without an entry
-// (the launch searches that top).  The merged row y's entries are all new:
-// the merge launch also reduces them to per-workgroup two smallest (P2
-// partials), from which the NEXT launch takes y's minimum (if y is pushed)
-// and its forwarding workgroup writes y's cache.  A merge launch keeps every
-// other cache exact: entries for x and y leave, (D'[j][y], y) enters if it is
-// below the bound (the third entry becomes the bound).
-//
-// Races: within a launch the loops read the caches of the clusters they push
-// (P, the same list in every workgroup) and nothing else, so no cache in P is
-// written during the launch (a loop that read a cache another workgroup had
-// just rewritten would decide differently from the others).  y's cache is
-// left as it was by the merge that re-forms y: y's search result comes from
-// the P2 partials until the next launch's forwarding workgroup rewrites the
-// cache (or a merge re-forms y again, and its successor does).  The merge's
-// maintenance skips the clusters in P, and they --
-// with the new top after a merge, whose maintenance would need the value
-// another workgroup computes -- are invalidated by workgroup 0 of the next
-// launch (they are chain members: their caches are not needed unless a
-// cluster is pushed twice).  The row y whose cache the forwarding workgroup
-// writes is excluded from both; if the same launch merges (x', y') the
-// forwarding workgroup applies that merge to y's cache itself: D[y][x'] is
-// stable during the launch, D[y][y'] is not (being rewritten), so it uses y'
-// 's cached value when y' is in the cache, else a lower bound on the new
-// entry -- Lance-Williams of (m, m) with m <= both operands, rounding being
-// monotone -- and lowers the cache bound to it.
-constexpr int kCPush = 16;          // pushes one decision loop may make through caches
-constexpr int kCInval = kCPush + 1;
-
-struct alignas(64) CLinkState {
-    int32_t k, len, top, below, first_active;
-    int32_t pend, x, y, nx, ny;     // the merge this state's launch applies
-    int32_t decide;                 // 1: the launch that wrote this state searched `top` (P1 partials)
-    int32_t mrow;                   // the row that launch's merge formed (P2 partials), -1: none
-    int32_t bad;
-    int32_t psa, psb, psbsz;        // sizes changed by this state's merge (as in LinkState)
-    int32_t ninval;                 // rows whose caches the next launch invalidates (list: cinval[parity])
-    int32_t launches, pushes;       // working launches so far, pushes decided from caches
-};
-
-struct alignas(64) CLinkFwd {
-    double dp;
-    int32_t szt, szb, c3, c4;
-};
-
-__device__ __forceinline__ bool lex_lt(double v, int32_t i, double w, int32_t j) { return v < w || (v == w && i < j); }
-
-// wave-wide minimum of (v, i) (every lane gets it)
-__device__ __forceinline__ void wave_min(double &v, int32_t &i) { wave_argmin(v, i); }
-
-// a sorted list of up to three entries in named slots (no private arrays:
-// dynamic indexing would put them in scratch memory); empty slots are
-// (inf, INT_MAX)
-struct L3 {
-    MinIdx a, b, c;
-    int cnt;
-};
-__device__ __forceinline__ L3 l3_empty() {
-    const MinIdx E{INFINITY, 0x7fffffff};
-    return L3{E, E, E, 0};
-}
-// (written as selects: conditional assignments through the slots made the
-// compiler address them in scratch memory)
-__device__ __forceinline__ MinIdx sel(bool p, MinIdx a, MinIdx b) { return MinIdx{p ? a.v : b.v, p ? a.i : b.i}; }
-__device__ __forceinline__ void l3_push_back(L3 &l, MinIdx e) {       // e >= every entry
-    l.a = sel(l.cnt == 0, e, l.a);
-    l.b = sel(l.cnt == 1, e, l.b);
-    l.c = sel(l.cnt == 2, e, l.c);
-    l.cnt++;
-}
-__device__ __forceinline__ void l3_insert(L3 &l, MinIdx u) {          // l.cnt <= 2
-    const bool la = better(u.v, u.i, l.a.v, l.a.i), lb = better(u.v, u.i, l.b.v, l.b.i);
-    l.c = sel(lb, l.b, u);
-    l.b = sel(la, l.a, sel(lb, u, l.b));
-    l.a = sel(la, u, l.a);
-    l.cnt++;
-}
-__device__ __forceinline__ MinIdx l3_last(const L3 &l) { return sel(l.cnt == 1, l.a, sel(l.cnt == 2, l.b, l.c)); }
-__device__ __forceinline__ void l3_pop_back(L3 &l) {
-    const MinIdx E{INFINITY, 0x7fffffff};
-    l.c = sel(l.cnt == 3, E, l.c);
-    l.b = sel(l.cnt == 2, E, l.b);
-    l.a = sel(l.cnt == 1, E, l.a);
-    l.cnt--;
-}
-
-// Initial caches: per row the three smallest entries (i != row): two cached,
-// the third the bound.  One workgroup per row; O(n^2) reads once per linkage.
-template <int WG>
-__global__ __launch_bounds__(WG) void k_cache_init(const double *__restrict__ D, uint32_t n, int2 *__restrict__ ci,
-                                                   double2 *__restrict__ cv, double *__restrict__ cb,
-                                                   int32_t *__restrict__ cbi) {
-    __shared__ MinIdx sw[WG / 64][3];
-    const uint32_t r = blockIdx.x;
-    const double *Dr = D + (uint64_t)r * n;
-    double a0v = INFINITY, a1v = INFINITY, a2v = INFINITY;
-    int32_t a0i = 0x7fffffff, a1i = 0x7fffffff, a2i = 0x7fffffff;
-    for (uint32_t i = threadIdx.x; i < n; i += WG) {
-        if (i == r) continue;
-        const double v = Dr[i];
-        const int32_t ii = (int32_t)i;
-        if (!better(v, ii, a2v, a2i)) continue;
-        if (better(v, ii, a0v, a0i)) { a2v = a1v; a2i = a1i; a1v = a0v; a1i = a0i; a0v = v; a0i = ii; }
-        else if (better(v, ii, a1v, a1i)) { a2v = a1v; a2i = a1i; a1v = v; a1i = ii; }
-        else { a2v = v; a2i = ii; }
-    }
-    MinIdx win[3];
-#pragma unroll
-    for (int round = 0; round < 3; round++) {
-        double v = a0v;
-        int32_t i = a0i;
-        wave_min(v, i);
-        win[round] = MinIdx{v, i};
-        if (a0i == i && a0v == v) { a0v = a1v; a0i = a1i; a1v = a2v; a1i = a2i; a2v = INFINITY; a2i = 0x7fffffff; }
-    }
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) { sw[w][0] = win[0]; sw[w][1] = win[1]; sw[w][2] = win[2]; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        MinIdx b[3] = {{INFINITY, 0x7fffffff}, {INFINITY, 0x7fffffff}, {INFINITY, 0x7fffffff}};
-        for (int k = 0; k < WG / 64; k++)
-            for (int e = 0; e < 3; e++) {
-                const MinIdx c = sw[k][e];
-                if (better(c.v, c.i, b[0].v, b[0].i)) { b[2] = b[1]; b[1] = b[0]; b[0] = c; }
-                else if (better(c.v, c.i, b[1].v, b[1].i)) { b[2] = b[1]; b[1] = c; }
-                else if (better(c.v, c.i, b[2].v, b[2].i)) b[2] = c;
-            }
-        const bool h0 = b[0].i != 0x7fffffff, h1 = b[1].i != 0x7fffffff;
-        ci[r] = make_int2(h0 ? b[0].i : -1, h1 ? b[1].i : -1);
-        cv[r] = make_double2(b[0].v, b[1].v);
-        cb[r] = b[2].v;
-        cbi[r] = b[2].i;
-    }
-}
-
-// A partial with its candidate's cache head and size attached (as of the end
-// of the launch that wrote it), so a push decided from a partial needs no
-// further load; hi = -1: no usable head.
-struct alignas(32) MinIdxP {
-    double v;
-    int32_t i, sz;
-    double hv;
-    int32_t hi, pad;
-};
-
-__device__ __forceinline__ MinIdx first_of(const MinIdxP &a) { return MinIdx{a.v, a.i}; }
-
-// Cache of row r from the P2 partials of the launch that formed r (each
-// workgroup's two smallest entries): entries outside every pair are >= the
-// smallest second entry U, so the cache takes the candidates below U (at most
-// two) and the next candidate as its bound.  Then, if this launch merges
-// (mx, my), that merge's effect (see the header above).  Block-wide; the
-// result is written by thread 0.
-template <int WG>
-__device__ void cache_refresh(const MinIdxP *__restrict__ p2a, const MinIdx *__restrict__ p2b, uint32_t G, int32_t r,
-                              const double *__restrict__ D,
-                              uint32_t n, int method, bool merge, int32_t mx, int32_t my, int32_t mnx, int32_t mny,
-                              int2 *__restrict__ ci, double2 *__restrict__ cv, double *__restrict__ cb,
-                              int32_t *__restrict__ cbi) {
-    __shared__ MinIdx s_best;
-    // U: the smallest second entry over the workgroups (a workgroup whose slice
-    // had fewer than two entries reports +inf there: it has nothing unreported)
-    double uv = INFINITY;
-    int32_t ui = 0x7fffffff;
-    double a0v = INFINITY, a1v = INFINITY, a2v = INFINITY;
-    int32_t a0i = 0x7fffffff, a1i = 0x7fffffff, a2i = 0x7fffffff;
-    for (uint32_t b = threadIdx.x; b < G; b += blockDim.x) {
-        const MinIdx e0 = first_of(p2a[b]), e1 = p2b[b];
-        if (better(e1.v, e1.i, uv, ui)) { uv = e1.v; ui = e1.i; }
-        for (int e = 0; e < 2; e++) {
-            const MinIdx c = e ? e1 : e0;
-            if (!better(c.v, c.i, a2v, a2i)) continue;
-            if (better(c.v, c.i, a0v, a0i)) { a2v = a1v; a2i = a1i; a1v = a0v; a1i = a0i; a0v = c.v; a0i = c.i; }
-            else if (better(c.v, c.i, a1v, a1i)) { a2v = a1v; a2i = a1i; a1v = c.v; a1i = c.i; }
-            else { a2v = c.v; a2i = c.i; }
-        }
-    }
-    MinIdx c[3];
-#pragma unroll
-    for (int round = 0; round < 3; round++) {
-        const MinIdx m = block_argmin<WG>(a0v, a0i);
-        if (threadIdx.x == 0) s_best = m;
-        __syncthreads();
-        c[round] = s_best;
-        if (a0i == c[round].i && a0v == c[round].v) { a0v = a1v; a0i = a1i; a1v = a2v; a1i = a2i; a2v = INFINITY; a2i = 0x7fffffff; }
-        __syncthreads();
-    }
-    const MinIdx U = block_argmin<WG>(uv, ui);
-    if (threadIdx.x != 0) return;
-    // list: the candidates below U (c[0] always is: every U is some workgroup's
-    // second entry, above that workgroup's first); bound: the next candidate
-    L3 l = l3_empty();
-    MinIdx B;
-    const bool in0 = c[0].i != 0x7fffffff && better(c[0].v, c[0].i, U.v, U.i);
-    const bool in1 = in0 && c[1].i != 0x7fffffff && better(c[1].v, c[1].i, U.v, U.i);
-    if (in0) l3_push_back(l, c[0]);
-    if (in1) l3_push_back(l, c[1]);
-    B = in1 ? c[2] : in0 ? c[1] : c[0];
-    if (!better(B.v, B.i, U.v, U.i)) B = U;
-    if (merge && r != mx && r != my) {
-        const double a = D[(uint64_t)r * n + mx];              // stable: row/column mx are not rewritten
-        double b = 0.0;
-        bool bk = false;
-        L3 k = l3_empty();
-        if (l.cnt > 0) { if (l.a.i == my) { b = l.a.v; bk = true; } else if (l.a.i != mx) l3_push_back(k, l.a); }
-        if (l.cnt > 1) { if (l.b.i == my) { b = l.b.v; bk = true; } else if (l.b.i != mx) l3_push_back(k, l.b); }
-        l = k;
-        if (bk) {
-            const double u = lw_update(method, a, b, mnx, mny);
-            if (better(u, my, B.v, B.i)) {
-                l3_insert(l, MinIdx{u, my});
-                if (l.cnt > 2) { B = l.c; l3_pop_back(l); }
-            }
-        } else {
-            // D[r][my] >= B.v, so the new entry is >= lw(m, m) with m = min(a, B.v)
-            const double m = a < B.v ? a : B.v;
-            const double lo = lw_update(method, m, m, mnx, mny);
-            if (better(lo, -1, B.v, B.i)) B = MinIdx{lo, -1};
-            while (l.cnt > 0 && !better(l3_last(l).v, l3_last(l).i, B.v, B.i)) l3_pop_back(l);
-        }
-    }
-    ci[r] = make_int2(l.cnt > 0 ? l.a.i : -1, l.cnt > 1 ? l.b.i : -1);
-    cv[r] = make_double2(l.a.v, l.b.v);
-    cb[r] = B.v;
-    cbi[r] = B.i;
-}
-
-// block argmin of (v, i) carrying the payload; result valid in thread 0
-template <int WG>
-__device__ MinIdxP block_argmin_p(MinIdxP a) {
-    __shared__ MinIdxP sw[WG / 64];
-    // (v, i) by DPP; the payload read from the winning lane
-    double wv = a.v;
-    int32_t wi = a.i;
-    wave_argmin(wv, wi);
-    const unsigned long long m = __ballot(a.i == wi && a.v == wv);
-    const int lane = m ? (int)__ffsll((long long)m) - 1 : 0;
-    if ((threadIdx.x & 63) == 0) {
-        MinIdxP r;
-        r.v = wv;
-        r.i = wi;
-        r.sz = __builtin_amdgcn_readlane(a.sz, lane);
-        const long long hb = __double_as_longlong(a.hv);
-        r.hv = __longlong_as_double((long long)(((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(hb >> 32), lane) << 32) |
-                                                 (unsigned)__builtin_amdgcn_readlane((int)hb, lane)));
-        r.hi = __builtin_amdgcn_readlane(a.hi, lane);
-        r.pad = 0;
-        sw[threadIdx.x >> 6] = r;
-    }
-    __syncthreads();
-    MinIdxP r{INFINITY, 0x7fffffff, 0, INFINITY, -1, 0};
-    if (threadIdx.x == 0)
-        for (int k = 0; k < WG / 64; k++)
-            if (better(sw[k].v, sw[k].i, r.v, r.i)) r = sw[k];
-    return r;
-}
-
-template <int WG, int kLkPer>
-__global__ __launch_bounds__(WG) void k_nn_cstep(double *__restrict__ D, uint32_t n, int method,
-                                                    int32_t *__restrict__ size, int32_t *__restrict__ chain,
-                                                    CLinkState *__restrict__ st, CLinkFwd *__restrict__ fwd,
-                                                    MinIdxP *__restrict__ parts1, MinIdxP *__restrict__ parts2,
-                                                    MinIdx *__restrict__ parts2b, int32_t *__restrict__ cinval,
-                                                    int2 *__restrict__ ci, double2 *__restrict__ cv,
-                                                    double *__restrict__ cb, int32_t *__restrict__ cbi,
-                                                    int32_t *__restrict__ done, double *__restrict__ Z, uint32_t q,
-                                                    long long *__restrict__ dbg) {
-    // phase timestamps of workgroups 0 and G in one launch (DREPHIP_LINK_TRACE_AT: its launch index)
-    const long long t_start = wall_clock64();
-#define LKC_T(slot)                                                                                              \
-    do {                                                                                                         \
-        if (dbg && threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1) &&                       \
-            S.launches == (int32_t)dbg[63]) {                                                                    \
-            dbg[(blockIdx.x == 0 ? 0 : 16) + (slot)] = wall_clock64() - t_start;                                 \
-        }                                                                                                        \
-    } while (0)
-    __shared__ CLinkState sx;
-    __shared__ int32_t s_pushed[kCPush];
-    __shared__ int32_t s_skip[2 * kCInval + 2], s_nskip;
-    __shared__ int32_t s_sinval[kCInval];
-    const uint32_t G = gridDim.x - 1;                          // step workgroups; workgroup G forwards
-    // everything the decision needs, loaded together: state, forwarded
-    // operands, the invalidation list, both partial sets
-    const CLinkState S = st[q ^ 1];
-    const CLinkFwd F = fwd[q ^ 1];
-    if (threadIdx.x < kCInval) s_sinval[threadIdx.x] = cinval[(q ^ 1) * kCInval + threadIdx.x];
-    MinIdxP a1{INFINITY, 0x7fffffff, 0, INFINITY, -1, 0}, a2 = a1;
-    for (uint32_t b = threadIdx.x; b < G; b += blockDim.x) {
-        const MinIdxP m1 = parts1[(uint64_t)(q ^ 1) * 1024 + b];
-        const MinIdxP m2 = parts2[(uint64_t)(q ^ 1) * 1024 + b];
-        if (better(m1.v, m1.i, a1.v, a1.i)) a1 = m1;
-        if (better(m2.v, m2.i, a2.v, a2.i)) a2 = m2;
-    }
-    const MinIdxP g1 = block_argmin_p<WG>(a1);
-    __syncthreads();
-    const MinIdxP g2 = block_argmin_p<WG>(a2);
-    if (S.k >= (int32_t)n - 1) return;
-    LKC_T(1);
-    const bool w0 = blockIdx.x == 0;
-    const int32_t spsa = S.psa, spsb = S.psb, spsbsz = S.psbsz;
-    auto size_prev = [=](int32_t i, int32_t stored) {          // (by value: a reference would put S in scratch)
-        return i == spsa ? 0 : i == spsb ? spsbsz : stored;
-    };
-    if (w0 && threadIdx.x == 0 && S.psa >= 0) { size[S.psa] = 0; size[S.psb] = S.psbsz; }
-    const int sninval = S.ninval;
-    if (threadIdx.x == 0) {
-        // ---- the decision loop (replicated in every workgroup)
-        CLinkState X = S;
-        X.psa = -1; X.psb = -1; X.psbsz = 0;
-        X.pend = 0;
-        int32_t top = S.top, below = S.below, c3 = F.c3, c4 = F.c4, len = S.len;
-        double dp = F.dp;
-        int32_t szt = F.szt, szb = F.szb;
-        int np = 0;
-        bool have = S.decide != 0, merged = false;
-        MinIdxP res = g1;
-        int2 nhi = make_int2(-1, -1);                                // the pushed row's cache head
-        double nhv = INFINITY;
-        for (;;) {
-            if (!have) {
-                if (top == S.mrow && S.mrow >= 0) res = g2;
-                else {
-                    bool inv = false;
-                    for (int e = 0; e < sninval && !inv; e++) inv = s_sinval[e] == top;
-#ifdef LKC_NOCACHEREAD
-                    inv = true;                                         // A/B only: every cache treated as empty
-#endif
-                    if (inv || nhi.x < 0) break;
-                    res = MinIdxP{nhv, nhi.x, -1, INFINITY, -1, 0};    // size and head: loaded below
-                }
-            }
-            have = false;
-            if ((uint32_t)res.i >= n) { X.bad = 1; X.k = (int32_t)n - 1; break; }
-            if (len > 1 && !(res.v < dp)) {                       // merge top with below at dp
-                int32_t a = top, b = below, na = szt, nb = szb;
-                if (a > b) { a = below; b = top; na = szb; nb = szt; }
-                if (w0) {
-                    double *z = Z + 4ull * X.k;
-                    z[0] = a; z[1] = b; z[2] = dp; z[3] = na + nb;
-                }
-                X.psa = a; X.psb = b; X.psbsz = na + nb;
-                X.pend = 1; X.x = a; X.y = b; X.nx = na; X.ny = nb;
-                X.k = X.k + 1;
-                len -= 2;
-                top = c3;
-                below = len >= 2 ? c4 : -1;
-                if (len == 0 && X.k < (int32_t)n - 1) {             // restart at the first active cluster
-                    int32_t f = S.first_active;
-                    while (f < (int32_t)n && !(f == b || (f != a && size_prev(f, size[f]) > 0))) f++;
-                    if (f >= (int32_t)n) { X.bad = 1; X.k = (int32_t)n - 1; }
-                    else {
-                        if (w0) chain[0] = f;
-                        X.first_active = f; top = f; below = -1; len = 1;
-                    }
-                }
-                merged = true;
-                break;
-            }
-            if (len >= (int32_t)n) { X.bad = 1; X.k = (int32_t)n - 1; break; }
-            if (np >= kCPush) break;                                  // this launch searches the top again
-            const int32_t a = res.i;                                 // push
-            if (w0) chain[len] = a;
-            s_pushed[np++] = a;
-            c4 = c3; c3 = below; below = top; top = a;
-            dp = res.v;
-            szb = szt;
-            if (res.sz >= 0) {
-                // decided from a partial: a's size and cache head came with it
-                szt = res.sz;
-                nhi = make_int2(res.hi, -1);
-                nhv = res.hv;
-            } else {
-                // decided from a cache: a's size and head are loaded (the head
-                // is ignored when a's cache is being written this launch)
-                const int32_t sza = size[a];
-                nhi = ci[a];
-                nhv = cv[a].x;
-                szt = size_prev(a, sza);
-            }
-            len++;
-        }
-        LKC_T(2);
-        if (dbg && S.launches == (int32_t)dbg[63] && (blockIdx.x == 0)) dbg[10] = np, dbg[11] = merged;
-        X.len = len; X.top = top; X.below = below;
-        X.decide = 1;
-        X.mrow = merged ? X.y : -1;
-        X.launches = S.launches + 1;
-        X.pushes = S.pushes + np;
-        // caches to invalidate next launch: the pushed rows, and after a merge
-        // the new top; rows no maintenance of this launch may write: those,
-        // the rows workgroup 0 invalidates now (the previous list) and the
-        // refreshed row
-        int ns = 0;
-        for (int e = 0; e < np; e++) s_skip[ns++] = s_pushed[e];
-        if (merged) s_skip[ns++] = top;
-        X.ninval = ns;
-        for (int e = 0; e < sninval; e++) s_skip[ns++] = s_sinval[e];
-        if (S.mrow >= 0) s_skip[ns++] = S.mrow;
-        s_nskip = ns;
-        sx = X;
-        if (w0) {
-            st[q] = X;
-            for (int e = 0; e < X.ninval; e++) cinval[q * kCInval + e] = s_skip[e];
-            if (X.k >= (int32_t)n - 1) st[q ^ 1] = X;
-            *done = X.k;
-            for (int e = 0; e < sninval; e++)
-                if (s_sinval[e] != S.mrow) ci[s_sinval[e]] = make_int2(-1, -1);
-        }
-        if (blockIdx.x == G && X.k < (int32_t)n - 1) {
-            const int32_t xpsa = X.psa, xpsb = X.psb, xpsbsz = X.psbsz, slen = S.len;
-            auto size_now = [=](int32_t i) { return i == xpsa ? 0 : i == xpsb ? xpsbsz : size_prev(i, size[i]); };
-            // chain entries: this launch's pushes from the loop's record (workgroup 0 is writing them)
-            auto chain_at = [=](int32_t p) { return p >= slen ? s_pushed[p - slen] : chain[p]; };
-            CLinkFwd f{0.0, 0, 0, 0, 0};
-            f.szt = size_now(X.top);
-            if (X.len > 1) {
-                f.dp = D[(uint64_t)X.top * n + X.below];
-                f.szb = size_now(X.below);
-            }
-            if (X.len >= 3) f.c3 = chain_at(X.len - 3);
-            if (X.len >= 4) f.c4 = chain_at(X.len - 4);
-            fwd[q] = f;
-        }
-    }
-    __syncthreads();
-    LKC_T(3);
-    const CLinkState X = sx;
-    if (blockIdx.x == G) {
-        // the forwarding workgroup: the cache of the row the previous launch formed
-        const int32_t r = S.mrow;
-        if (r >= 0 && X.k < (int32_t)n - 1 && !(X.pend && (r == X.x || r == X.y))) {
-            const int32_t szr = r == X.psa ? 0 : r == X.psb ? X.psbsz : size_prev(r, size[r]);
-#ifndef LKC_NOREFRESH
-            if (szr > 0)
-#else
-            if (szr < 0)                                                // A/B only (timing)
-#endif
-                cache_refresh<WG>(parts2 + (uint64_t)(q ^ 1) * 1024, parts2b + (uint64_t)(q ^ 1) * 1024, G, r, D,
-                                  n, method, X.pend != 0, X.x, X.y, X.nx, X.ny, ci, cv, cb, cbi);
-        }
-        LKC_T(4);
-        return;
-    }
-    if (X.k >= (int32_t)n - 1) return;                        // all merged (the last merge needs no update)
-    // ---- this step: the pending update fused with the search of row t, the
-    // merged row's two smallest per workgroup, and the caches' maintenance;
-    // every candidate carries its row's cache head (after this launch) and size
-    const bool pend = X.pend != 0;
-    const int32_t x = X.x, y = X.y, nx = X.nx, ny = X.ny, t = X.top;
-    const double *Dt = D + (uint64_t)t * n;
-    const double *Dx = D + (uint64_t)x * n;
-    double *Dy = D + (uint64_t)y * n;
-    const double dxt = pend ? Dx[t] : 0.0, dyt = pend ? Dy[t] : 0.0;
-    const int nskip = s_nskip;
-    MinIdxP b1{INFINITY, 0x7fffffff, 0, INFINITY, -1, 0};       // this lane's best of row t
-    MinIdxP m0 = b1, m1 = b1;                                    // its two smallest of the new row y
-    const uint32_t stride = G * WG;
-    for (uint32_t i0 = blockIdx.x * WG + threadIdx.x; i0 < n; i0 += kLkPer * stride) {
-        int32_t sz[kLkPer];
-        double dt[kLkPer], dx[kLkPer], dy[kLkPer];
-        int2 hi[kLkPer];
-        double2 hv[kLkPer];
-        double hb[kLkPer];
-        int32_t hbi[kLkPer];
-#pragma unroll
-        for (int k = 0; k < kLkPer; k++) {
-            const uint32_t i = i0 + k * stride;
-            const uint32_t ic = i < n ? i : n - 1;
-            sz[k] = size[ic];
-            dt[k] = Dt[ic];
-            hi[k] = ci[ic]; hv[k] = cv[ic];
-            if (pend) {
-                dx[k] = Dx[ic]; dy[k] = Dy[ic];
-                hb[k] = cb[ic]; hbi[k] = cbi[ic];
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < kLkPer; k++) {
-            const uint32_t i = i0 + k * stride;
-            if (i >= n) continue;
-            const int32_t szi = (int32_t)i == X.psa ? 0 : (int32_t)i == X.psb ? X.psbsz : size_prev((int32_t)i, sz[k]);
-            if (szi == 0) continue;
-            // row i's cache head as it stands after this launch (none when a
-            // row's cache is not maintained now, or i is y or t)
-            bool skip = hi[k].x < 0 || (pend && ((int32_t)i == y || (int32_t)i == t));
-            for (int e = 0; e < nskip && !skip; e++) skip = s_skip[e] == (int32_t)i;
-            int32_t phi = skip ? -1 : hi[k].x;
-            double phv = hv[k].x;
-            double v;
-            if (pend && (int32_t)i != y && (int32_t)i != t) {
-                const double u = lw_update(method, dx[k], dy[k], nx, ny);
-                Dy[i] = u;
-                D[(uint64_t)i * n + y] = u;
-#ifdef LKC_NOMAINT
-                skip = true;                                            // A/B only (timing)
-#endif
-                if (!skip) {
-                    // cache maintenance of row i: x and y leave, (u, y) enters below the bound
-                    L3 l = l3_empty();
-                    bool changed = false;
-                    if (hi[k].x == x || hi[k].x == y) changed = true; else l3_push_back(l, MinIdx{hv[k].x, hi[k].x});
-                    if (hi[k].y >= 0) {
-                        if (hi[k].y == x || hi[k].y == y) changed = true; else l3_push_back(l, MinIdx{hv[k].y, hi[k].y});
-                    }
-                    double nbv = hb[k];
-                    int32_t nbi = hbi[k];
-                    if (better(u, y, nbv, nbi)) {
-                        l3_insert(l, MinIdx{u, y});
-                        if (l.cnt > 2) { nbv = l.c.v; nbi = l.c.i; l3_pop_back(l); }
-                        changed = true;
-                    }
-                    if (changed) {
-                        ci[i] = make_int2(l.cnt > 0 ? l.a.i : -1, l.cnt > 1 ? l.b.i : -1);
-                        cv[i] = make_double2(l.a.v, l.b.v);
-                        cb[i] = nbv;
-                        cbi[i] = nbi;
-                    }
-                    phi = l.cnt > 0 ? l.a.i : -1;
-                    phv = l.a.v;
-                }
-                const MinIdxP c{u, (int32_t)i, szi, phv, phi, 0};
-                if (better(c.v, c.i, m0.v, m0.i)) { m1 = m0; m0 = c; }
-                else if (better(c.v, c.i, m1.v, m1.i)) m1 = c;
-                v = t == y ? u : dt[k];
-            } else if (pend && (int32_t)i == y && t != y) {
-                const double u = lw_update(method, dxt, dyt, nx, ny);
-                Dy[t] = u;
-                D[(uint64_t)t * n + y] = u;
-                const int32_t szt_ = t == X.psa ? 0 : t == X.psb ? X.psbsz : size_prev(t, size[t]);
-                const MinIdxP c{u, t, szt_, INFINITY, -1, 0};          // t's cache is not maintained now
-                if (better(c.v, c.i, m0.v, m0.i)) { m1 = m0; m0 = c; }
-                else if (better(c.v, c.i, m1.v, m1.i)) m1 = c;
-                v = u;
-                if (v < b1.v || (v == b1.v && (int32_t)i < b1.i)) b1 = MinIdxP{v, (int32_t)i, szi, INFINITY, -1, 0};
-                continue;                                             // (y's cache: stale, see the header)
-            } else {
-                if ((int32_t)i == t) continue;
-                v = dt[k];
-            }
-            if (v < b1.v || (v == b1.v && (int32_t)i < b1.i)) b1 = MinIdxP{v, (int32_t)i, szi, phv, phi, 0};
-        }
-    }
-    LKC_T(4);
-    const MinIdxP part = block_argmin_p<WG>(b1);
-    if (threadIdx.x == 0) parts1[(uint64_t)q * 1024 + blockIdx.x] = part;
-    LKC_T(5);
-    if (pend) {
-        // the workgroup's two smallest of row y: its first by block argmin
-        // (with payload), its second as the smallest after removing the first
-        __syncthreads();
-        const MinIdxP f0 = block_argmin_p<WG>(m0);
-        __shared__ MinIdxP s_f0;
-        if (threadIdx.x == 0) s_f0 = f0;
-        __syncthreads();
-        const MinIdxP w = s_f0;
-        const MinIdxP rest = (m0.i == w.i && m0.v == w.v) ? m1 : m0;
-        __syncthreads();
-        const MinIdxP f1 = block_argmin_p<WG>(rest);
-        if (threadIdx.x == 0) {
-            parts2[(uint64_t)q * 1024 + blockIdx.x] = f0;
-            parts2b[(uint64_t)q * 1024 + blockIdx.x] = MinIdx{f1.v, f1.i};
-        }
-        LKC_T(6);
-    }
-#undef LKC_T
-}
-
 // ------------------------------------------------------------ matrix build
 // D (n x n f64, rows in perm order) from the condensed upper triangle, by
 // 64 x 64 tiles of (row block bi <= column block bj): a wave reads one row's
@@ -1107,48 +527,6 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     if ((rc = scratch(ctx, "lk_done", 4, (void **)&d_done))) return rc;
     const bool mst = method == DREPHIP_LINK_SINGLE;
     if (mst && (rc = scratch(ctx, "lk_dmin", n * 8ull, (void **)&d_Dmin))) return rc;
-    // the cache-driven chain (complete / average / weighted): DREPHIP_LINK_CACHE=1 (A/B, not yet the default)
-    const char *lc = getenv("DREPHIP_LINK_CACHE");
-    const bool cached = !mst && lc && atoi(lc) != 0;
-    int2 *d_ci = nullptr;
-    double2 *d_cv = nullptr;
-    double *d_cb = nullptr;
-    int32_t *d_cbi = nullptr;
-    MinIdxP *d_parts1c = nullptr, *d_parts2 = nullptr;
-    MinIdx *d_parts2b = nullptr;
-    int32_t *d_cinval = nullptr;
-    CLinkState *d_cst = nullptr;
-    CLinkFwd *d_cfwd = nullptr;
-    long long *d_dbg = nullptr;
-    if (cached) {
-        if ((rc = scratch(ctx, "lk_ci", n * 8ull, (void **)&d_ci))) return rc;
-        if ((rc = scratch(ctx, "lk_cv", n * 16ull, (void **)&d_cv))) return rc;
-        if ((rc = scratch(ctx, "lk_cb", n * 8ull, (void **)&d_cb))) return rc;
-        if ((rc = scratch(ctx, "lk_cbi", n * 4ull, (void **)&d_cbi))) return rc;
-        if ((rc = scratch(ctx, "lk_parts1c", 2 * 1024 * sizeof(MinIdxP), (void **)&d_parts1c))) return rc;
-        if ((rc = scratch(ctx, "lk_parts2", 2 * 1024 * sizeof(MinIdxP), (void **)&d_parts2))) return rc;
-        if ((rc = scratch(ctx, "lk_parts2b", 2 * 1024 * sizeof(MinIdx), (void **)&d_parts2b))) return rc;
-        if ((rc = scratch(ctx, "lk_cst", 2 * sizeof(CLinkState), (void **)&d_cst))) return rc;
-        if ((rc = scratch(ctx, "lk_cinval", 2 * kCInval * 4ull, (void **)&d_cinval))) return rc;
-        if ((rc = scratch(ctx, "lk_cfwd", 2 * sizeof(CLinkFwd), (void **)&d_cfwd))) return rc;
-        HIPC(hipMemsetAsync(d_parts1c, 0, 2 * 1024 * sizeof(MinIdxP), st));
-        HIPC(hipMemsetAsync(d_parts2, 0, 2 * 1024 * sizeof(MinIdxP), st));
-        HIPC(hipMemsetAsync(d_parts2b, 0, 2 * 1024 * sizeof(MinIdx), st));
-        HIPC(hipMemsetAsync(d_cfwd, 0, 2 * sizeof(CLinkFwd), st));
-        CLinkState h[2] = {};
-        h[1].len = 1; h[1].top = 0; h[1].below = -1; h[1].first_active = 0;
-        h[1].psa = h[1].psb = -1; h[1].decide = 0; h[1].mrow = -1; h[1].ninval = 0;
-        h[0] = h[1];
-        HIPC(hipMemcpyAsync(d_cst, h, sizeof(h), hipMemcpyHostToDevice, st));
-        if (const char *ta = getenv("DREPHIP_LINK_TRACE_AT")) {
-            if ((rc = scratch(ctx, "lk_dbg", 64 * 8, (void **)&d_dbg))) return rc;
-            long long h[64] = {};
-            h[63] = atoll(ta);
-            HIPC(hipMemcpyAsync(d_dbg, h, sizeof(h), hipMemcpyHostToDevice, st));
-        }
-        hipLaunchKernelGGL(k_cache_init<256>, dim3(n), dim3(256), 0, st, (const double *)d_D, n, d_ci, d_cv, d_cb, d_cbi);
-        HIPC(hipGetLastError());
-    }
     if (mst) {
         std::vector<double> inf(n, INFINITY);
         std::vector<int32_t> mg(n, 0);
@@ -1185,9 +563,6 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     do {                                                                                                         \
         if (mst) hipLaunchKernelGGL((k_mst_step<W, P>), gm, blk, 0, st, d_D, n, d_size, d_Dmin, d_st, d_parts, d_done, \
                                     d_Z, q);                                                                     \
-        else if (cached) hipLaunchKernelGGL((k_nn_cstep<W, P>), gn, blk, 0, st, d_D, n, method, d_size, d_chain,   \
-                                            d_cst, d_cfwd, d_parts1c, d_parts2, d_parts2b, d_cinval, d_ci, d_cv, \
-                                            d_cb, d_cbi, d_done, d_Z, q, d_dbg);                                 \
         else hipLaunchKernelGGL((k_nn_step<W, P>), gn, blk, 0, st, d_D, n, method, d_size, d_chain, d_st, d_fwd,    \
                                 d_parts, d_done, d_Z, q);                                                        \
     } while (0)
@@ -1226,27 +601,9 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     HIPC(hipMemcpyAsync(&done, d_done, 4, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));
     if (done != (int32_t)n - 1) { set_error("linkage did not finish"); return DREPHIP_ERR_INTERNAL; }
-    int32_t bad;
-    if (cached) {
-        CLinkState hs[2];
-        HIPC(hipMemcpy(hs, d_cst, sizeof(hs), hipMemcpyDeviceToHost));
-        bad = hs[0].bad | hs[1].bad;
-        const CLinkState &hl = hs[0].launches > hs[1].launches ? hs[0] : hs[1];
-        ctx->link.launches = hl.launches;
-        if (getenv("DREPHIP_DEBUG"))
-            fprintf(stderr, "[drephip] cached chain: n=%u launches %d (merges %u), pushes %d\n", n,
-                    hl.launches, n - 1, hl.pushes);
-        if (d_dbg) {
-            long long h[64];
-            HIPC(hipMemcpy(h, d_dbg, sizeof(h), hipMemcpyDeviceToHost));
-            fprintf(stderr, "[drephip] launch %lld phases (10 ns): wg0 %lld %lld %lld %lld %lld %lld pushes %lld merged %lld | fwd %lld %lld %lld %lld\n",
-                    h[63], h[1], h[2], h[3], h[4], h[5], h[6], h[10], h[11], h[17], h[18], h[19], h[20]);
-        }
-    } else {
-        LinkState hs[2];
-        HIPC(hipMemcpy(hs, d_st, sizeof(hs), hipMemcpyDeviceToHost));
-        bad = hs[0].bad | hs[1].bad;
-    }
+    LinkState hs[2];
+    HIPC(hipMemcpy(hs, d_st, sizeof(hs), hipMemcpyDeviceToHost));
+    const int32_t bad = hs[0].bad | hs[1].bad;
     if (bad) { set_error("linkage: a chain step found no valid partial"); return DREPHIP_ERR_INTERNAL; }
     const double t_fin = now_s();
     ctx->link.chain_s = t_fin - t_chain;

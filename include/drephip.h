@@ -289,10 +289,14 @@ int drephip_last_screen_stats(drephip_ctx *ctx, int *used, uint64_t *entries, ui
  *    matrix per connected component of those pairs; the counts path extracts
  *    them on the GPU).  Bit-identical to scipy.  Used automatically when the
  *    per-component matrices fit 2^28 f64 cells (DREPHIP_LINK_SPARSE_CELLS);
+ *    when the path is forced (and in drephip_linkage_sparse) components too
+ *    large for matrices run scipy's chain over sparse rows instead (no
+ *    matrix; host time grows with the rows' lengths: ~1 s at 2x10^4 genomes
+ *    with ~100 chance links each);
  *  - dense: the n x n f64 matrix in HBM, one GPU launch per chain step. */
 #define DREPHIP_LINK_PATH_AUTO 0
 #define DREPHIP_LINK_PATH_DENSE 1
-#define DREPHIP_LINK_PATH_SPARSE 2   /* fails (DREPHIP_ERR_UNSUPPORTED) where it does not apply */
+#define DREPHIP_LINK_PATH_SPARSE 2   /* fails (DREPHIP_ERR_UNSUPPORTED) where no sparse form exists */
 /* (a new context starts at DREPHIP_LINK_PATH_AUTO, or at the path named by the
  * environment variable DREPHIP_LINK_PATH = auto | dense | sparse) */
 int drephip_set_linkage_path(drephip_ctx *ctx, int path);

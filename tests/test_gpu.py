@@ -818,9 +818,8 @@ def test_gpu_linkage_matches_scipy(method, n, kind):
     all-equal distances, a few values whose Lance-Williams averages round
     (fewvals), family structure with 1.0 between families (mash), values
     above 1.0 and negative values (no sparse form; scipy accepts both): the dense GPU path at three grid densities of
-    the chain-step kernel (16 entries per lane: several passes), with and
-    without the row caches, and the automatic choice (the sparse path wherever
-    no value exceeds 1.0)."""
+    the chain-step kernel (16 entries per lane: several passes), and the
+    automatic choice (the sparse path wherever no value exceeds 1.0)."""
     import scipy.cluster.hierarchy as sch
     rng = np.random.default_rng(n * 31 + len(method))
     m = n * (n - 1) // 2
@@ -844,22 +843,22 @@ def test_gpu_linkage_matches_scipy(method, n, kind):
     else:
         y = np.full(m, 0.5)
     Zs = sch.linkage(y, method=method)
-    # grid densities of the chain-step kernel, with the row caches (the
-    # default) and the plain step (DREPHIP_LINK_CACHE=0)
-    variants = [(pl, "1") for pl in (("4", "1", "16") if n <= 2000 else ("4",))] + [("4", "0")]
-    for per_lane, cache in variants:
+    # grid densities of the chain-step kernel
+    variants = [(pl, {}) for pl in (("4", "1", "16") if n <= 2000 else ("4",))]
+
+    for per_lane, env in variants:
         os.environ["DREPHIP_LINK_PER_LANE"] = per_lane
-        os.environ["DREPHIP_LINK_CACHE"] = cache
+        os.environ.update(env)
         try:
             with _lib.Context(0, 21, S, 42) as ctx:
                 ctx.set_linkage_path(ctx.LINK_DENSE)
                 Z = ctx.linkage(y, method)
                 assert not ctx.linkage_info()["sparse"]
         finally:
-            os.environ.pop("DREPHIP_LINK_PER_LANE", None)
-            os.environ.pop("DREPHIP_LINK_CACHE", None)
+            for k in ["DREPHIP_LINK_PER_LANE"] + list(env):
+                os.environ.pop(k, None)
         assert Z.shape == Zs.shape
-        assert np.array_equal(Z, Zs), (per_lane, cache, np.argwhere(Z != Zs)[:5])
+        assert np.array_equal(Z, Zs), (per_lane, env, np.argwhere(Z != Zs)[:5])
     with _lib.Context(0, 21, S, 42) as ctx:
         Z = ctx.linkage(y, method)
         if kind in ("mash", "above1", "negative"):      # small components / no sparse form
