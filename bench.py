@@ -43,11 +43,11 @@ VALU_COSTS = os.path.join(ROOT, "profiles", "r01_valu_microbench.json")
 SKETCH_ISA = os.path.join(ROOT, "profiles", "r03_sketch_isa.json")
 # committed PMC summaries (tools/pmc_summary.py): VALU / LDS utilisation of the
 # two kernels, reported next to the live timings
-SKETCH_PMC = os.path.join(ROOT, "profiles", "r03_sketch_pmc_sq.json")
+SKETCH_PMC = os.path.join(ROOT, "profiles", "r04_sketch_pmc_sq.json")
 # all-pairs profiles of tools/profile_allpairs.sh, one per (N, s) case: the
 # bench line quotes the one of its own workload (never another N's)
-DIST_PROFILE = os.path.join(ROOT, "profiles", "r03_allpairs_N%d%s.json")
-SKETCH_TRAFFIC = os.path.join(ROOT, "profiles", "r03_sketch_traffic.json")
+DIST_PROFILE = os.path.join(ROOT, "profiles", "r04_allpairs_N%d%s.json")
+SKETCH_TRAFFIC = os.path.join(ROOT, "profiles", "r04_sketch_traffic.json")
 PROFILE_STEPS = 3              # untimed steps that time finalize / all-pairs / table build
 VERIFY_GENOMES = 16            # timed-step sketches re-derived by the C oracle (sampled, every run)
 VERIFY_PAIRS = 100_000         # timed-step counts re-derived by the C oracle (random pairs + one row)

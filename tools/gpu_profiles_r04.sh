@@ -16,5 +16,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/t
 AB_NOREF=1 AB_VAR=DREPHIP_AP_SCREEN timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_1e5 -o t -- \
     python tools/ap_ab.py 100000 1 3 > $OUT/trace_1e5.json 2> $OUT/trace_1e5.err || exit 1
 # the all-pairs kernels' counter passes at configs[2] and configs[4] (screened: the LIST kernels)
-CASES="N10000 N10000_s10000" ROUND=r04 bash tools/profile_allpairs.sh || exit 1
+CASES="N1000 N10000 N10000_s10000" ROUND=r04 bash tools/profile_allpairs.sh || exit 1
 echo done
