@@ -156,6 +156,8 @@ struct alignas(64) LinkState {
     int32_t psa, psb, psbsz;      // the sizes this state's merge changed (psa = -1: none), written to
                                   // size[] by workgroup 0 of the NEXT kernel, which every reader of
                                   // that kernel therefore overrides
+    int32_t mrow;                 // the row this state's merge forms (its minimum: the P2 partials), -1: none
+    int32_t launches, twice;      // working launches, launches that decided two steps (diagnostics)
 };
 
 // all partials of the previous kernel -> their minimum (thread 0)
@@ -184,68 +186,102 @@ struct alignas(64) LinkFwd {
     int32_t szt, szb, c3, c4;
 };
 
+// Round 4: a merge step also reduces the merged row y to its minimum (the
+// "P2" partials; the new values are computed there anyway).  When the next
+// step pushes y -- the new top's nearest neighbour is often the cluster just
+// formed -- y's own step is decided at once from P2 instead of by a launch
+// that searches y's row: up to two chain steps per launch.
 template <int WG, int kLkPer>
 __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t n, int method,
                                                    int32_t *__restrict__ size, int32_t *__restrict__ chain,
                                                    LinkState *__restrict__ st, LinkFwd *__restrict__ fwd,
-                                                   MinIdx *__restrict__ parts, int32_t *__restrict__ done,
-                                                   double *__restrict__ Z, uint32_t q) {
+                                                   MinIdx *__restrict__ parts, MinIdx *__restrict__ parts2,
+                                                   int32_t *__restrict__ done, double *__restrict__ Z, uint32_t q) {
     __shared__ LinkState sx;
     const uint32_t G = gridDim.x - 1;                          // step workgroups; workgroup G forwards operands
     const LinkState S = st[q ^ 1];
     const LinkFwd F = fwd[q ^ 1];
-    // the partials are read whether or not a decision is pending (valid memory
+    // both partial sets are read whether or not they are needed (valid memory
     // either way), so their loads are not held behind the state's
-    const MinIdx g = read_partials<WG>(parts + (uint64_t)(q ^ 1) * 1024, G);
+    double g1v = INFINITY, g2v = INFINITY;
+    int32_t g1i = 0x7fffffff, g2i = 0x7fffffff;
+    for (uint32_t b = threadIdx.x; b < G; b += blockDim.x) {
+        const MinIdx m1 = parts[(uint64_t)(q ^ 1) * 1024 + b];
+        const MinIdx m2 = parts2[(uint64_t)(q ^ 1) * 1024 + b];
+        if (better(m1.v, m1.i, g1v, g1i)) { g1v = m1.v; g1i = m1.i; }
+        if (better(m2.v, m2.i, g2v, g2i)) { g2v = m2.v; g2i = m2.i; }
+    }
+    const MinIdx g = block_argmin<WG>(g1v, g1i);
+    MinIdx g2{INFINITY, 0x7fffffff};
+    if (S.mrow >= 0) {
+        __syncthreads();
+        g2 = block_argmin<WG>(g2v, g2i);
+    }
     if (S.k >= (int32_t)n - 1) return;                         // all merged
     const bool w0 = blockIdx.x == 0;
     // size of cluster i as of the previous decision: workgroup 0 writes that
     // decision's two sizes during this kernel, so every reader overrides them
-    auto size_prev = [&](int32_t i, int32_t stored) {
-        return i == S.psa ? 0 : i == S.psb ? S.psbsz : stored;
-    };
+    const int32_t spsa = S.psa, spsb = S.psb, spsbsz = S.psbsz;
+    auto size_prev = [=](int32_t i, int32_t stored) { return i == spsa ? 0 : i == spsb ? spsbsz : stored; };
     if (w0 && threadIdx.x == 0 && S.psa >= 0) { size[S.psa] = 0; size[S.psb] = S.psbsz; }
-    // ---- the previous step's decision (replicated in every workgroup)
-    const double dp = F.dp;
-    const int32_t szt = F.szt, szb = F.szb, c3 = F.c3, c4 = F.c4;
+    // ---- the previous step's decision, and y's when it pushes y (replicated in every workgroup)
     if (threadIdx.x == 0) {
-        LinkState X = S;
-        X.psa = -1; X.psb = -1; X.psbsz = 0;
+        // (plain scalars, the state struct written once at the end: a struct
+        // updated across the branches was kept in private memory)
+        int32_t k = S.k, len = S.len, top = S.top, below = S.below, first_active = S.first_active;
+        int32_t pend = 0, px = S.x, py = S.y, pnx = S.nx, pny = S.ny, bad = S.bad, mrow = -1;
+        int32_t psa = -1, psb = -1, psbsz = 0, twice = S.twice;
         if (S.decide) {
-            X.pend = 0;
-            if ((uint32_t)g.i >= n) {                                  // no valid partial: stop
-                X.bad = 1; X.k = (int32_t)n - 1;
-            } else if (!(S.len > 1 && !(g.v < dp))) {                 // push (scipy: the previous element wins ties)
-                if (S.len >= (int32_t)n) { X.bad = 1; X.k = (int32_t)n - 1; }
-                else {
-                    if (w0) chain[S.len] = g.i;
-                    X.len = S.len + 1; X.below = S.top; X.top = g.i;
-                }
-            } else {                                                   // merge top with below at dp
-                int32_t a = S.top, b = S.below, na = szt, nb = szb;
-                if (a > b) { a = S.below; b = S.top; na = szb; nb = szt; }
-                if (w0) {
-                    double *z = Z + 4ull * S.k;
-                    z[0] = a; z[1] = b; z[2] = dp; z[3] = na + nb;
-                }
-                X.psa = a; X.psb = b; X.psbsz = na + nb;
-                X.pend = 1; X.x = a; X.y = b; X.nx = na; X.ny = nb;
-                X.k = S.k + 1;
-                X.len = S.len - 2;
-                X.top = c3;
-                X.below = X.len >= 2 ? c4 : -1;
-                if (X.len == 0 && X.k < (int32_t)n - 1) {             // restart at the first active cluster
-                    int32_t f = S.first_active;
-                    while (f < (int32_t)n && !(f == b || (f != a && size_prev(f, size[f]) > 0))) f++;
-                    if (f >= (int32_t)n) { X.bad = 1; X.k = (int32_t)n - 1; }
-                    else {
-                        if (w0) chain[0] = f;
-                        X.first_active = f; X.top = f; X.below = -1; X.len = 1;
+            int32_t c3 = F.c3, c4 = F.c4, szt = F.szt, szb = F.szb;
+            double dp = F.dp;
+            MinIdx r = g;
+            for (int d = 0; d < 2; d++) {
+                if ((uint32_t)r.i >= n) { bad = 1; k = (int32_t)n - 1; break; }      // no valid partial: stop
+                if (len > 1 && !(r.v < dp)) {                     // merge top with below at dp
+                    int32_t a = top, b = below, na = szt, nb = szb;
+                    if (a > b) { a = below; b = top; na = szb; nb = szt; }
+                    if (w0) {
+                        double *z = Z + 4ull * S.k;
+                        z[0] = a; z[1] = b; z[2] = dp; z[3] = na + nb;
                     }
+                    psa = a; psb = b; psbsz = na + nb;
+                    pend = 1; px = a; py = b; pnx = na; pny = nb;
+                    mrow = b;
+                    k = S.k + 1;
+                    len -= 2;
+                    top = c3;
+                    below = len >= 2 ? c4 : -1;
+                    if (len == 0 && k < (int32_t)n - 1) {           // restart at the first active cluster
+                        int32_t f = S.first_active;
+                        while (f < (int32_t)n && !(f == b || (f != a && size_prev(f, size[f]) > 0))) f++;
+                        if (f >= (int32_t)n) { bad = 1; k = (int32_t)n - 1; }
+                        else {
+                            if (w0) chain[0] = f;
+                            first_active = f; top = f; below = -1; len = 1;
+                        }
+                    }
+                    break;
                 }
+                // push (scipy: the previous element wins ties)
+                if (len >= (int32_t)n) { bad = 1; k = (int32_t)n - 1; break; }
+                if (w0) chain[len] = r.i;
+                c4 = c3; c3 = below; below = top; top = r.i;
+                dp = r.v;
+                szb = szt;
+                len++;
+                if (r.i != S.mrow || S.mrow < 0 || d == 1) break;   // the pushed row is searched by this launch
+                szt = S.psbsz;                                      // y: just formed, its size is the override
+                r = g2;                                             // y's minimum, from the merge step
+                twice++;
             }
         }
-        X.decide = 1;
+        LinkState X;
+        X.mx = S.mx;
+        X.k = k; X.len = len; X.top = top; X.below = below; X.first_active = first_active;
+        X.pend = pend; X.x = px; X.y = py; X.nx = pnx; X.ny = pny;
+        X.decide = 1; X.bad = bad;
+        X.psa = psa; X.psb = psb; X.psbsz = psbsz; X.mrow = mrow;
+        X.launches = S.launches + 1; X.twice = twice;
         sx = X;
         if (w0) {
             st[q] = X;
@@ -253,18 +289,17 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             *done = X.k;
         }
         if (blockIdx.x == G && X.k < (int32_t)n - 1) {
-            // the next decision's operands (sizes as of this decision)
-            auto size_now = [&](int32_t i) {
-                return i == X.psa ? 0 : i == X.psb ? X.psbsz : size_prev(i, size[i]);
-            };
+            // the next decision's operands (sizes as of this decision); the
+            // chain positions read here are below this launch's pushes
+            auto size_now = [&](int32_t i) { return i == psa ? 0 : i == psb ? psbsz : size_prev(i, size[i]); };
             LinkFwd f{0.0, 0, 0, 0, 0};
-            if (X.len > 1) {
-                f.dp = D[(uint64_t)X.top * n + X.below];
-                f.szt = size_now(X.top);
-                f.szb = size_now(X.below);
+            f.szt = size_now(top);                              // (also at len 1: a push and a merge may follow)
+            if (len > 1) {
+                f.dp = D[(uint64_t)top * n + below];
+                f.szb = size_now(below);
             }
-            if (X.len >= 3) f.c3 = chain[X.len - 3];
-            if (X.len >= 4) f.c4 = chain[X.len - 4];
+            if (len >= 3) f.c3 = chain[len - 3];
+            if (len >= 4) f.c4 = chain[len - 4];
             fwd[q] = f;
         }
     }
@@ -272,15 +307,16 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     __syncthreads();
     const LinkState X = sx;
     if (X.k >= (int32_t)n - 1) return;
-    // ---- this step: the pending update fused with the search of row t
+    // ---- this step: the pending update fused with the search of row t, and
+    // the minimum of the new row y
     const bool pend = X.pend != 0;
     const int32_t x = X.x, y = X.y, nx = X.nx, ny = X.ny, t = X.top;
     const double *Dt = D + (uint64_t)t * n;
     const double *Dx = D + (uint64_t)x * n;
     double *Dy = D + (uint64_t)y * n;
     const double dxt = pend ? Dx[t] : 0.0, dyt = pend ? Dy[t] : 0.0;
-    double bv = INFINITY;
-    int32_t bi = 0x7fffffff;
+    double bv = INFINITY, yv = INFINITY;
+    int32_t bi = 0x7fffffff, yi = 0x7fffffff;
     const uint32_t stride = G * WG;
     for (uint32_t i0 = blockIdx.x * WG + threadIdx.x; i0 < n; i0 += kLkPer * stride) {
         int32_t sz[kLkPer];
@@ -312,11 +348,13 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
 #else
                 D[(uint64_t)i * n + y] = u;
 #endif
+                if (better(u, (int32_t)i, yv, yi)) { yv = u; yi = (int32_t)i; }
                 v = t == y ? u : dt[k];
             } else if (pend && (int32_t)i == y && t != y) {
                 const double u = lw_update(method, dxt, dyt, nx, ny);
                 Dy[t] = u;
                 D[(uint64_t)t * n + y] = u;
+                if (better(u, t, yv, yi)) { yv = u; yi = t; }       // (D[y][t], produced by y's lane)
                 v = u;
             } else {
                 if ((int32_t)i == t) continue;
@@ -327,6 +365,11 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     }
     const MinIdx part = block_argmin<WG>(bv, bi);
     if (threadIdx.x == 0) parts[(uint64_t)q * 1024 + blockIdx.x] = part;
+    if (pend) {
+        __syncthreads();
+        const MinIdx p2 = block_argmin<WG>(yv, yi);
+        if (threadIdx.x == 0) parts2[(uint64_t)q * 1024 + blockIdx.x] = p2;
+    }
 }
 
 template <int WG, int kLkPer>
@@ -520,6 +563,8 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     if ((rc = scratch(ctx, "lk_chain", n * 4ull, (void **)&d_chain))) return rc;
     if ((rc = scratch(ctx, "lk_Z", (n - 1) * 32ull, (void **)&d_Z))) return rc;
     if ((rc = scratch(ctx, "lk_parts", 2 * 1024 * sizeof(MinIdx), (void **)&d_parts))) return rc;
+    MinIdx *d_parts2;
+    if ((rc = scratch(ctx, "lk_parts2", 2 * 1024 * sizeof(MinIdx), (void **)&d_parts2))) return rc;
     if ((rc = scratch(ctx, "lk_st", 2 * sizeof(LinkState), (void **)&d_st))) return rc;
     LinkFwd *d_fwd;
     if ((rc = scratch(ctx, "lk_fwd", 2 * sizeof(LinkFwd), (void **)&d_fwd))) return rc;
@@ -544,6 +589,7 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
         LinkState h[2] = {};
         h[1].len = 1; h[1].top = 0; h[1].below = -1; h[1].first_active = 0; h[1].mx = 0;
         h[1].psa = h[1].psb = -1;
+        h[1].mrow = -1;
         h[0] = h[1];
         HIPC(hipMemcpyAsync(d_st, h, sizeof(h), hipMemcpyHostToDevice, st));
         int32_t zero = 0;
@@ -564,7 +610,7 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
         if (mst) hipLaunchKernelGGL((k_mst_step<W, P>), gm, blk, 0, st, d_D, n, d_size, d_Dmin, d_st, d_parts, d_done, \
                                     d_Z, q);                                                                     \
         else hipLaunchKernelGGL((k_nn_step<W, P>), gn, blk, 0, st, d_D, n, method, d_size, d_chain, d_st, d_fwd,    \
-                                d_parts, d_done, d_Z, q);                                                        \
+                                d_parts, d_parts2, d_done, d_Z, q);                                              \
     } while (0)
         if (wg == 128) {
             if (tpl == 1) DREPHIP_LK_LAUNCH(128, 1);
@@ -604,6 +650,10 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     LinkState hs[2];
     HIPC(hipMemcpy(hs, d_st, sizeof(hs), hipMemcpyDeviceToHost));
     const int32_t bad = hs[0].bad | hs[1].bad;
+    if (getenv("DREPHIP_DEBUG") && !mst) {
+        const LinkState &hl = hs[0].launches > hs[1].launches ? hs[0] : hs[1];
+        fprintf(stderr, "[drephip] chain: n=%u launches %d, of which %d decided two steps\n", n, hl.launches, hl.twice);
+    }
     if (bad) { set_error("linkage: a chain step found no valid partial"); return DREPHIP_ERR_INTERNAL; }
     const double t_fin = now_s();
     ctx->link.chain_s = t_fin - t_chain;
