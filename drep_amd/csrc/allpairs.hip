@@ -1281,7 +1281,10 @@ static int launch_band_cfg(drephip_ctx *ctx, const uint64_t *d_hashes, const uin
 // 147 ms with 2^10 slots / cap 352 / two per CU, against 84 ms here
 // (profiles/r04_band_geometry_ab.json): the band bound is the tightest of R
 // rows, so more rows mean narrower bands, more table builds and more
-// per-column band overhead, which outweighs the halved column stream.
+// per-column band overhead, which outweighs the halved column stream.  Two
+// workgroups per CU cap the kernel at 64 VGPRs (15 spilled, 64 B/lane of
+// scratch); one per CU (82 VGPRs, no spills) measured slower: 19.2 vs 16.1 ms
+// screened at configs[4], 5.1 vs 4.3 ms dense at N = 2000, s = 10^4.
 constexpr uint32_t kBandR = 4;
 static int launch_band(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N,
                        uint32_t row0, uint32_t row1, uint64_t seg0, uint64_t npairs, uint16_t *d_common,

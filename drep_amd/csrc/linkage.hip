@@ -377,42 +377,39 @@ __global__ __launch_bounds__(WG) void k_mst_step(const double *__restrict__ D, u
                                                     int32_t *__restrict__ merged, double *__restrict__ Dmin,
                                                     LinkState *__restrict__ st, MinIdx *__restrict__ parts,
                                                     int32_t *__restrict__ done, double *__restrict__ Z, uint32_t q) {
-    __shared__ LinkState sx;
-    __shared__ int32_t s_ov;
-    const LinkState S = st[q ^ 1];
+    // (the state as scalars: a LinkState copied and edited in branches was
+    // kept in private memory promoted to LDS, see k_nn_step)
+    __shared__ int32_t s_k, s_mx, s_ov;
+    const int32_t sk = st[q ^ 1].k, smx = st[q ^ 1].mx, sdecide = st[q ^ 1].decide, sbad = st[q ^ 1].bad;
     const uint32_t G = gridDim.x;
     const MinIdx g = read_partials<WG>(parts + (uint64_t)(q ^ 1) * 1024, G);     // unconditional: not held behind S
-    if (S.k >= (int32_t)n - 1) return;
+    if (sk >= (int32_t)n - 1) return;
     if (threadIdx.x == 0) {
-        LinkState X = S;
-        int32_t ov = -1;
+        int32_t k = sk, mx = smx, bad = sbad, ov = -1;
         const bool w0 = blockIdx.x == 0;
-        if (S.decide) {
-            if ((uint32_t)g.i >= n) { X.bad = 1; X.k = (int32_t)n - 1; }
+        if (sdecide) {
+            if ((uint32_t)g.i >= n) { bad = 1; k = (int32_t)n - 1; }
             else {
                 if (w0) {
-                    double *z = Z + 4ull * S.k;
-                    z[0] = S.mx; z[1] = g.i; z[2] = g.v; z[3] = 0;
+                    double *z = Z + 4ull * sk;
+                    z[0] = smx; z[1] = g.i; z[2] = g.v; z[3] = 0;
                     merged[g.i] = 1;
                 }
                 ov = g.i;
-                X.mx = g.i;
-                X.k = S.k + 1;
+                mx = g.i;
+                k = sk + 1;
             }
         }
-        X.decide = 1;
-        sx = X;
-        s_ov = ov;
+        s_k = k; s_mx = mx; s_ov = ov;
         if (w0) {
-            st[q] = X;
-            if (X.k >= (int32_t)n - 1) st[q ^ 1] = X;
-            *done = X.k;
+            st[q].k = k; st[q].mx = mx; st[q].bad = bad; st[q].decide = 1;
+            if (k >= (int32_t)n - 1) { st[q ^ 1].k = k; st[q ^ 1].mx = mx; st[q ^ 1].bad = bad; st[q ^ 1].decide = 1; }
+            *done = k;
         }
     }
     __syncthreads();
-    const LinkState X = sx;
-    if (X.k >= (int32_t)n - 1) return;
-    const int32_t ov = s_ov, x = X.mx;
+    if (s_k >= (int32_t)n - 1) return;
+    const int32_t ov = s_ov, x = s_mx;
     const double *Dx = D + (uint64_t)x * n;
     double bv = INFINITY;
     int32_t bi = 0x7fffffff;
