@@ -1284,7 +1284,10 @@ static int launch_band_cfg(drephip_ctx *ctx, const uint64_t *d_hashes, const uin
 // per-column band overhead, which outweighs the halved column stream.  Two
 // workgroups per CU cap the kernel at 64 VGPRs (15 spilled, 64 B/lane of
 // scratch); one per CU (82 VGPRs, no spills) measured slower: 19.2 vs 16.1 ms
-// screened at configs[4], 5.1 vs 4.3 ms dense at N = 2000, s = 10^4.
+// screened at configs[4], 5.1 vs 4.3 ms dense at N = 2000, s = 10^4.  R = 8 in
+// the screened (LIST) mode, where the kernel streams column sketches at
+// ~5 TB/s: 21.8 vs 16.0 ms at configs[4], 11.4 vs 8.9 ms at N = 6000 -- the
+// union of eight rows' marked columns outgrows the halved stream.
 constexpr uint32_t kBandR = 4;
 static int launch_band(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N,
                        uint32_t row0, uint32_t row1, uint64_t seg0, uint64_t npairs, uint16_t *d_common,
