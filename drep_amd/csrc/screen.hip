@@ -394,10 +394,11 @@ __global__ __launch_bounds__(kScWG) void k_screen_count(const uint32_t *__restri
 }
 
 // per row tile (one workgroup): its marked columns in ascending order at
-// coff[t] (thread u takes words [u*per, (u+1)*per)).  Item j of tile t goes to launch slot ibase[t] + 8 j: slot w runs on XCD
-// w % 8, and the host deals blocks of kItemBlock consecutive row tiles to the
-// XCDs, so the tiles of one block (a genome family's rows, whose marked
-// columns largely coincide) stream their column sketches through one L2.
+// coff[t] (thread u takes words [u*per, (u+1)*per)).  Item j of tile t goes
+// to launch slot ibase[t] + 8 j: slot w runs on XCD w % 8, and the host deals
+// blocks of kItemBlock consecutive row tiles to the XCDs, so the tiles of one
+// block (a genome family's rows, whose marked columns largely coincide) stream
+// their column sketches through one L2 (measured neutral).
 __global__ __launch_bounds__(kScWG) void k_screen_lists(const uint32_t *__restrict__ bm, uint32_t NW, uint32_t C,
                                                         uint32_t row0, uint32_t R, const uint32_t *__restrict__ cnt,
                                                         const uint64_t *__restrict__ coff,
