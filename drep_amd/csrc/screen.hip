@@ -16,13 +16,16 @@
 //   keys    entry (g, k), k < nhash[g]: key lo32(H[g][k]), value g * s + k
 //   sort    radix sort of the (key, value) pairs on the 32-bit key (rocPRIM
 //           through hipCUB): equal hashes become adjacent
-//   runs    runs of >= 2 equal keys, appended by wave-aggregated atomics;
-//           sum of m(m-1)/2 = the pair checks the marking will make
-//   mark    one wave per run: every pair of the run's entries with equal
-//           64-bit hashes marks cell (row tile of the smaller genome, larger
-//           genome) in a bitmap [row tiles][N bits] (load first, atomicOr
-//           only when the bit is clear: a family's ~400 shared hashes mark
-//           the same cells)
+//   runs    runs of >= 2 equal keys, counted and written per block in two
+//           passes; sum of m(m-1)/2 = the pair checks the marking will make;
+//           two-entry runs kept apart
+//   mark    runs of >= 3 in first-genome order, a workgroup per 256 runs:
+//           every pair of a run's entries with equal 64-bit hashes marks cell
+//           (row tile of the smaller genome, larger genome) in a bitmap
+//           [row tiles][N bits] through an LDS window of it; two-entry runs
+//           go to a pair map (k_screen_mark2), and a pair sharing exactly one
+//           hash, both sketches full, is written by the screen itself
+//           (common = rank sum < s, k_screen_simple) instead of marked
 //   lists   per row tile: its marked columns in ascending order and its work
 //           items {i0, list offset, count <= C, 0} for the LIST kernels
 //
