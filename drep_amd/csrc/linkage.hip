@@ -158,6 +158,8 @@ struct alignas(64) LinkState {
                                   // that kernel therefore overrides
     int32_t mrow;                 // the row this state's merge forms (its minimum: the P2 partials), -1: none
     int32_t launches, twice;      // working launches, launches that decided two steps (diagnostics)
+    int32_t recip, scans;         // diagnostics: scan launches (no merge applied), and those whose row's
+                                  // step was a merge with the element below (the next launch's first decision)
 };
 
 // all partials of the previous kernel -> their minimum (thread 0)
@@ -230,7 +232,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
         // updated across the branches was kept in private memory)
         int32_t k = S.k, len = S.len, top = S.top, below = S.below, first_active = S.first_active;
         int32_t pend = 0, px = S.x, py = S.y, pnx = S.nx, pny = S.ny, bad = S.bad, mrow = -1;
-        int32_t psa = -1, psb = -1, psbsz = 0, twice = S.twice;
+        int32_t psa = -1, psb = -1, psbsz = 0, twice = S.twice, recip = S.recip, scans = S.scans;
         if (S.decide) {
             int32_t c3 = F.c3, c4 = F.c4, szt = F.szt, szb = F.szb;
             double dp = F.dp;
@@ -238,6 +240,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             for (int d = 0; d < 2; d++) {
                 if ((uint32_t)r.i >= n) { bad = 1; k = (int32_t)n - 1; break; }      // no valid partial: stop
                 if (len > 1 && !(r.v < dp)) {                     // merge top with below at dp
+                    if (d == 0 && !S.pend) recip++;
                     int32_t a = top, b = below, na = szt, nb = szb;
                     if (a > b) { a = below; b = top; na = szb; nb = szt; }
                     if (w0) {
@@ -282,6 +285,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
         X.decide = 1; X.bad = bad;
         X.psa = psa; X.psb = psb; X.psbsz = psbsz; X.mrow = mrow;
         X.launches = S.launches + 1; X.twice = twice;
+        X.recip = recip; X.scans = S.scans + (pend ? 0 : 1);
         sx = X;
         if (w0) {
             st[q] = X;
@@ -649,7 +653,9 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     const int32_t bad = hs[0].bad | hs[1].bad;
     if (getenv("DREPHIP_DEBUG") && !mst) {
         const LinkState &hl = hs[0].launches > hs[1].launches ? hs[0] : hs[1];
-        fprintf(stderr, "[drephip] chain: n=%u launches %d, of which %d decided two steps\n", n, hl.launches, hl.twice);
+        fprintf(stderr, "[drephip] chain: n=%u launches %d, of which %d decided two steps; %d scan launches, "
+                        "%d of them followed by a merge with the element below\n", n, hl.launches, hl.twice, hl.scans,
+                hl.recip);
     }
     if (bad) { set_error("linkage: a chain step found no valid partial"); return DREPHIP_ERR_INTERNAL; }
     const double t_fin = now_s();
