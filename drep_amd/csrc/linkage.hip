@@ -66,33 +66,46 @@ __device__ __forceinline__ double lw_update(int method, double dxi, double dyi, 
 }
 
 // Wave argmin by DPP (row_shr 1/2/4/8 within each 16-lane row, then
-// row_bcast 15/31 across rows): lane 63 ends with the wave's minimum, which
-// readlane broadcasts.  A step moves three dwords lane to lane in a few
-// cycles, where the __shfl_xor butterfly (ds_bpermute through the LDS
-// crossbar) took ~100 cycles per step -- the chain steps are latency-bound and
-// reduce twice each.  Lanes a shift leaves without a source keep the identity
-// (inf, INT_MAX).  Needs every lane of the wave active.
+// row_bcast 15/31 across rows: lane 63 ends with the wave's minimum, which
+// readlane broadcasts), in two passes: the minimum value (v_min_f64 of the
+// lane and its DPP-shifted neighbour), then the smallest index among the
+// lanes holding it (v_min_i32).  One pass over (value, index) pairs with the
+// lexicographic compare took ~12 instructions a step -- a wave reduction is
+// on a chain step's critical path several times, so it pays to keep it short.
+// Lanes a shift leaves without a source keep the identity (inf, INT_MAX).
+// Values are never NaN.  Needs every lane of the wave active.
 template <int CTRL, int RM>
-__device__ __forceinline__ void dpp_argmin_step(double &v, int32_t &i) {
+__device__ __forceinline__ double dpp_f64(double v) {
     const long long b = __double_as_longlong(v);
     const long long ib = __double_as_longlong((double)INFINITY);
-    const int olo = __builtin_amdgcn_update_dpp((int)ib, (int)b, CTRL, RM, 0xf, false);
-    const int ohi = __builtin_amdgcn_update_dpp((int)(ib >> 32), (int)(b >> 32), CTRL, RM, 0xf, false);
-    const int oi = __builtin_amdgcn_update_dpp(0x7fffffff, i, CTRL, RM, 0xf, false);
-    const double ov = __longlong_as_double((long long)(((unsigned long long)(unsigned)ohi << 32) | (unsigned)olo));
-    if (better(ov, oi, v, i)) { v = ov; i = oi; }
+    const int lo = __builtin_amdgcn_update_dpp((int)ib, (int)b, CTRL, RM, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(ib >> 32), (int)(b >> 32), CTRL, RM, 0xf, false);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ int32_t dpp_i32(int32_t i) {
+    return __builtin_amdgcn_update_dpp(0x7fffffff, i, CTRL, RM, 0xf, false);
 }
 __device__ __forceinline__ void wave_argmin(double &v, int32_t &i) {
-    dpp_argmin_step<0x111, 0xf>(v, i);
-    dpp_argmin_step<0x112, 0xf>(v, i);
-    dpp_argmin_step<0x114, 0xf>(v, i);
-    dpp_argmin_step<0x118, 0xf>(v, i);
-    dpp_argmin_step<0x142, 0xa>(v, i);
-    dpp_argmin_step<0x143, 0xc>(v, i);
-    const long long b = __double_as_longlong(v);
+    double m = v;
+    m = fmin(m, dpp_f64<0x111, 0xf>(m));
+    m = fmin(m, dpp_f64<0x112, 0xf>(m));
+    m = fmin(m, dpp_f64<0x114, 0xf>(m));
+    m = fmin(m, dpp_f64<0x118, 0xf>(m));
+    m = fmin(m, dpp_f64<0x142, 0xa>(m));
+    m = fmin(m, dpp_f64<0x143, 0xc>(m));
+    const long long b = __double_as_longlong(m);
     const int lo = __builtin_amdgcn_readlane((int)b, 63), hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
-    v = __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
-    i = __builtin_amdgcn_readlane(i, 63);
+    m = __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+    int32_t c = v == m ? i : 0x7fffffff;
+    c = min(c, dpp_i32<0x111, 0xf>(c));
+    c = min(c, dpp_i32<0x112, 0xf>(c));
+    c = min(c, dpp_i32<0x114, 0xf>(c));
+    c = min(c, dpp_i32<0x118, 0xf>(c));
+    c = min(c, dpp_i32<0x142, 0xa>(c));
+    c = min(c, dpp_i32<0x143, 0xc>(c));
+    v = m;
+    i = __builtin_amdgcn_readlane(c, 63);
 }
 
 // Block argmin (smallest index among equal minima); result valid in thread 0.
@@ -109,6 +122,34 @@ __device__ MinIdx block_argmin(double v, int32_t i) {
         for (int k = 0; k < WG / 64; k++)
             if (better(sv[k], si[k], r.v, r.i)) { r.v = sv[k]; r.i = si[k]; }
     return r;
+}
+
+// Up to three block argmins at once, one barrier (results in thread 0): a
+// chain step reduces one to three sets per launch and per decision.  b and c
+// are reduced only when the (block-uniform) flags ask for them: an unneeded
+// wave reduction measured as costly as the barrier it saves.
+template <int WG>
+__device__ void block_argmin3(MinIdx &a, MinIdx &b, MinIdx &c, bool with_b, bool with_c) {
+    __shared__ double sv[3][WG / 64];
+    __shared__ int32_t si[3][WG / 64];
+    wave_argmin(a.v, a.i);
+    if (with_b) wave_argmin(b.v, b.i);
+    if (with_c) wave_argmin(c.v, c.i);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        sv[0][w] = a.v; si[0][w] = a.i;
+        sv[1][w] = b.v; si[1][w] = b.i;
+        sv[2][w] = c.v; si[2][w] = c.i;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        a = b = c = MinIdx{INFINITY, 0x7fffffff};
+        for (int k = 0; k < WG / 64; k++) {
+            if (better(sv[0][k], si[0][k], a.v, a.i)) { a.v = sv[0][k]; a.i = si[0][k]; }
+            if (better(sv[1][k], si[1][k], b.v, b.i)) { b.v = sv[1][k]; b.i = si[1][k]; }
+            if (better(sv[2][k], si[2][k], c.v, c.i)) { c.v = sv[2][k]; c.i = si[2][k]; }
+        }
+    }
 }
 
 // ---------------------------------------------------------------- the steps
@@ -160,6 +201,9 @@ struct alignas(64) LinkState {
     int32_t launches, twice;      // working launches, launches that decided two steps (diagnostics)
     int32_t recip, scans;         // diagnostics: scan launches (no merge applied), and those whose row's
                                   // step was a merge with the element below (the next launch's first decision)
+    int32_t am_other, am_y, am_merge;   // diagnostics: the first decision after a merge launch
+    int32_t c3, spec;             // chain[len - 3] (w); 1: this launch searches w's row speculatively (P3)
+    int32_t specwin;              // diagnostics: launches saved by the speculation
 };
 
 // all partials of the previous kernel -> their minimum (thread 0)
@@ -167,7 +211,7 @@ template <int WG>
 __device__ __forceinline__ MinIdx read_partials(const MinIdx *parts, uint32_t G) {
     double bv = INFINITY;
     int32_t bi = 0x7fffffff;
-    for (uint32_t b = threadIdx.x; b < G; b += blockDim.x) {
+    for (uint32_t b = threadIdx.x; b < G; b += WG) {             // (WG: see k_nn_step)
         const MinIdx m = parts[b];
         if (better(m.v, m.i, bv, bi)) { bv = m.v; bi = m.i; }
     }
@@ -186,6 +230,9 @@ __device__ __forceinline__ MinIdx read_partials(const MinIdx *parts, uint32_t G)
 struct alignas(64) LinkFwd {
     double dp;
     int32_t szt, szb, c3, c4;
+    // the speculation of a search launch (spec = 1): see k_nn_step
+    double dp2;                   // D[w][c4], w = c3
+    int32_t spec;                 // 1: the P2 partials hold the would-be merged row's minimum, P3 w's
 };
 
 // Round 4: a merge step also reduces the merged row y to its minimum (the
@@ -198,26 +245,42 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                                                    int32_t *__restrict__ size, int32_t *__restrict__ chain,
                                                    LinkState *__restrict__ st, LinkFwd *__restrict__ fwd,
                                                    MinIdx *__restrict__ parts, MinIdx *__restrict__ parts2,
-                                                   int32_t *__restrict__ done, double *__restrict__ Z, uint32_t q) {
+                                                   MinIdx *__restrict__ parts3, int32_t *__restrict__ done,
+                                                   double *__restrict__ Z, uint32_t q, int spec_on) {
     __shared__ LinkState sx;
     const uint32_t G = gridDim.x - 1;                          // step workgroups; workgroup G forwards operands
     const LinkState S = st[q ^ 1];
     const LinkFwd F = fwd[q ^ 1];
-    // both partial sets are read whether or not they are needed (valid memory
-    // either way), so their loads are not held behind the state's
-    double g1v = INFINITY, g2v = INFINITY;
-    int32_t g1i = 0x7fffffff, g2i = 0x7fffffff;
-    for (uint32_t b = threadIdx.x; b < G; b += blockDim.x) {
-        const MinIdx m1 = parts[(uint64_t)(q ^ 1) * 1024 + b];
-        const MinIdx m2 = parts2[(uint64_t)(q ^ 1) * 1024 + b];
-        if (better(m1.v, m1.i, g1v, g1i)) { g1v = m1.v; g1i = m1.i; }
-        if (better(m2.v, m2.i, g2v, g2i)) { g2v = m2.v; g2i = m2.i; }
-    }
-    const MinIdx g = block_argmin<WG>(g1v, g1i);
-    MinIdx g2{INFINITY, 0x7fffffff};
-    if (S.mrow >= 0) {
-        __syncthreads();
-        g2 = block_argmin<WG>(g2v, g2i);
+    // The partial sets are reduced by wave 0 alone (the decision is thread
+    // 0's: no barrier), read whether or not they are needed (valid memory
+    // either way) so that their loads are not held behind the state's.  A
+    // lane takes partials lane, lane + 64, ... four at a time, all loads in
+    // flight before the first wait.  (The loop steps by a constant: a
+    // blockDim.x stride's kernarg load held the partial loads behind the state's.)
+    MinIdx g{INFINITY, 0x7fffffff}, g2{INFINITY, 0x7fffffff}, g3{INFINITY, 0x7fffffff};
+    if (threadIdx.x < 64) {
+        const MinIdx *P1 = parts + (uint64_t)(q ^ 1) * 1024, *P2 = parts2 + (uint64_t)(q ^ 1) * 1024,
+                     *P3 = parts3 + (uint64_t)(q ^ 1) * 1024;
+        for (uint32_t b0 = threadIdx.x; b0 < G; b0 += 256) {
+            MinIdx m1[4], m2[4], m3[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t b = min(b0 + 64u * u, G - 1);         // (a repeated partial changes no minimum)
+                m1[u] = P1[b]; m2[u] = P2[b]; m3[u] = P3[b];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                asm volatile("" : "+v"(m1[u].v), "+v"(m1[u].i), "+v"(m2[u].v), "+v"(m2[u].i), "+v"(m3[u].v), "+v"(m3[u].i));
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if (better(m1[u].v, m1[u].i, g.v, g.i)) g = m1[u];
+                if (better(m2[u].v, m2[u].i, g2.v, g2.i)) g2 = m2[u];
+                if (better(m3[u].v, m3[u].i, g3.v, g3.i)) g3 = m3[u];
+            }
+        }
+        wave_argmin(g.v, g.i);
+        if (S.mrow >= 0 || F.spec) wave_argmin(g2.v, g2.i);
+        if (F.spec) wave_argmin(g3.v, g3.i);
     }
     if (S.k >= (int32_t)n - 1) return;                         // all merged
     const bool w0 = blockIdx.x == 0;
@@ -232,13 +295,24 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
         // updated across the branches was kept in private memory)
         int32_t k = S.k, len = S.len, top = S.top, below = S.below, first_active = S.first_active;
         int32_t pend = 0, px = S.x, py = S.y, pnx = S.nx, pny = S.ny, bad = S.bad, mrow = -1;
-        int32_t psa = -1, psb = -1, psbsz = 0, twice = S.twice, recip = S.recip, scans = S.scans;
+        int32_t psa = -1, psb = -1, psbsz = 0, twice = S.twice, recip = S.recip;
+        int32_t am_other = S.am_other, am_y = S.am_y, am_merge = S.am_merge, specwin = S.specwin;
+        // c3, c4: chain[len - 3], chain[len - 4]; ck of them are known exactly
+        // (a merge exposes entries only the chain in memory holds; a push
+        // shifts known ones down)
+        int32_t c3 = F.c3, c4 = F.c4, ck = 2, dpo = 0;
+        double dpov = 0.0;
         if (S.decide) {
-            int32_t c3 = F.c3, c4 = F.c4, szt = F.szt, szb = F.szb;
+            int32_t szt = F.szt, szb = F.szb;
             double dp = F.dp;
             MinIdx r = g;
             for (int d = 0; d < 2; d++) {
                 if ((uint32_t)r.i >= n) { bad = 1; k = (int32_t)n - 1; break; }      // no valid partial: stop
+                if (d == 0 && S.pend) {
+                    if (len > 1 && !(r.v < dp)) am_merge++;
+                    else if (r.i == S.mrow) am_y++;
+                    else am_other++;
+                }
                 if (len > 1 && !(r.v < dp)) {                     // merge top with below at dp
                     if (d == 0 && !S.pend) recip++;
                     int32_t a = top, b = below, na = szt, nb = szb;
@@ -250,6 +324,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                     psa = a; psb = b; psbsz = na + nb;
                     pend = 1; px = a; py = b; pnx = na; pny = nb;
                     mrow = b;
+                    ck = 0;
                     k = S.k + 1;
                     len -= 2;
                     top = c3;
@@ -262,6 +337,33 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                             if (w0) chain[0] = f;
                             first_active = f; top = f; below = -1; len = 1;
                         }
+                    } else if (d == 0 && F.spec && len >= 1 && k < (int32_t)n - 1) {
+                        // the previous launch searched, speculatively, the new
+                        // top w's row as it is after this merge (P3) and the
+                        // merged row b (P2): decide w's step, and b's when w
+                        // pushes b, now.  A push makes this launch search the
+                        // pushed row instead of w; a merge is left to the next
+                        // launch (one merge per launch), with w or b searched here.
+                        // (b is pushed only together with b's own push: D[top][below]
+                        // must not involve b, whose row this launch rewrites,
+                        // except through dpo)
+                        const MinIdx r3 = g3;
+                        const bool wpush = (uint32_t)r3.i < n && !(len > 1 && !(r3.v < F.dp2)) && len + 1 < (int32_t)n;
+                        const bool bpush = r3.i == b && (uint32_t)g2.i < n && g2.v < r3.v;
+                        if (wpush && (r3.i != b || bpush)) {
+                            if (w0) chain[len] = r3.i;                  // w pushes r3.i
+                            c4 = c3; c3 = below; below = top; top = r3.i;
+                            ck = ck >= 1 ? 2 : 1;
+                            len++;
+                            specwin++;
+                            if (bpush) {
+                                if (w0) chain[len] = g2.i;              // b pushes g2.i
+                                c4 = c3; c3 = below; below = top; top = g2.i;
+                                ck = ck >= 1 ? 2 : 1;
+                                len++;
+                                dpo = 1; dpov = g2.v;                   // D[g2.i][b] as this launch writes it
+                            }
+                        }
                     }
                     break;
                 }
@@ -269,6 +371,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                 if (len >= (int32_t)n) { bad = 1; k = (int32_t)n - 1; break; }
                 if (w0) chain[len] = r.i;
                 c4 = c3; c3 = below; below = top; top = r.i;
+                ck = ck >= 1 ? 2 : 1;
                 dp = r.v;
                 szb = szt;
                 len++;
@@ -286,6 +389,11 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
         X.psa = psa; X.psb = psb; X.psbsz = psbsz; X.mrow = mrow;
         X.launches = S.launches + 1; X.twice = twice;
         X.recip = recip; X.scans = S.scans + (pend ? 0 : 1);
+        X.am_other = am_other; X.am_y = am_y; X.am_merge = am_merge; X.specwin = specwin;
+        // speculate in a search launch (no merge applied) whose top has two
+        // elements below it: search w's row too (P3)
+        X.c3 = c3;
+        X.spec = spec_on && !pend && len >= 3 && k < (int32_t)n - 1;
         sx = X;
         if (w0) {
             st[q] = X;
@@ -293,17 +401,30 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             *done = X.k;
         }
         if (blockIdx.x == G && X.k < (int32_t)n - 1) {
-            // the next decision's operands (sizes as of this decision); the
-            // chain positions read here are below this launch's pushes
-            auto size_now = [&](int32_t i) { return i == psa ? 0 : i == psb ? psbsz : size_prev(i, size[i]); };
+            // the next decision's operands, sizes as of this decision.  Every
+            // load is issued before any is waited for (one round trip): the
+            // chain entries read are below this launch's pushes, and a spec
+            // launch (no merge) knows c3 and c4 (ck = 2), so D[c3][c4] needs none
+            const bool two = len > 1, l3 = len >= 3 && ck < 1, l4 = len >= 4 && ck < 2;
+            const bool sp = X.spec && len >= 4;
+            int32_t rzt = size[top], rzb = size[two ? below : top];
+            double rdp = D[(uint64_t)top * n + (two ? below : top)];
+            int32_t r3 = chain[l3 ? len - 3 : 0], r4 = chain[l4 ? len - 4 : 0];
+            double rdp2 = D[sp ? (uint64_t)c3 * n + c4 : 0];
+            asm volatile("" : "+v"(rzt), "+v"(rzb), "+v"(rdp), "+v"(r3), "+v"(r4), "+v"(rdp2));
+            auto size_now = [&](int32_t i, int32_t stored) { return i == psa ? 0 : i == psb ? psbsz : size_prev(i, stored); };
             LinkFwd f{0.0, 0, 0, 0, 0};
-            f.szt = size_now(top);                              // (also at len 1: a push and a merge may follow)
-            if (len > 1) {
-                f.dp = D[(uint64_t)top * n + below];
-                f.szb = size_now(below);
+            f.szt = size_now(top, rzt);                         // (also at len 1: a push and a merge may follow)
+            if (two) {
+                f.dp = dpo ? dpov : rdp;
+                f.szb = size_now(below, rzb);
             }
-            if (len >= 3) f.c3 = chain[len - 3];
-            if (len >= 4) f.c4 = chain[len - 4];
+            if (len >= 3) f.c3 = ck >= 1 ? c3 : r3;
+            if (len >= 4) f.c4 = ck >= 2 ? c4 : r4;
+            if (X.spec) {
+                f.dp2 = sp ? rdp2 : 0.0;                        // D[w][c4], w = c3
+                f.spec = 1;
+            }
             fwd[q] = f;
         }
     }
@@ -318,13 +439,30 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     const double *Dt = D + (uint64_t)t * n;
     const double *Dx = D + (uint64_t)x * n;
     double *Dy = D + (uint64_t)y * n;
-    const double dxt = pend ? Dx[t] : 0.0, dyt = pend ? Dy[t] : 0.0;
-    double bv = INFINITY, yv = INFINITY;
-    int32_t bi = 0x7fffffff, yi = 0x7fffffff;
+    // D[x][t], D[y][t]: waited for with the first pass.  (Through a lane
+    // register offset: a uniform address made them scalar loads, which the
+    // compiler waited for before the pass.)
+    int32_t lz;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(lz));
+    double dxt = pend ? Dx[t + lz] : 0.0, dyt = pend ? Dy[t + lz] : 0.0;
+    // speculation (a search launch, X.spec): if t merges with the element
+    // below, sb, the merged row u = LW(D[t], D[sb]) gets index max(t, sb) and
+    // the new top is sw; P2 <- u's minimum, P3 <- sw's row's minimum after
+    // that merge (sw's row without t and sb, plus (u[sw], max(t, sb)))
+    const bool spec = X.spec != 0;
+    const int32_t sb = X.below, sw = X.c3;
+    const int32_t sy_ = spec ? (t < sb ? sb : t) : 0;
+    const double *Dsb = D + (uint64_t)(spec ? sb : 0) * n;
+    const double *Dw = D + (uint64_t)(spec ? sw : 0) * n;
+    // (t's and sb's sizes are loaded with the first pass's entries; see below)
+    int32_t rst = spec ? size[t] : 0, rsb = spec ? size[sb] : 0;
+    int32_t snx = 0, sny = 0;
+    double bv = INFINITY, yv = INFINITY, wv = INFINITY;
+    int32_t bi = 0x7fffffff, yi = 0x7fffffff, wi = 0x7fffffff;
     const uint32_t stride = G * WG;
     for (uint32_t i0 = blockIdx.x * WG + threadIdx.x; i0 < n; i0 += kLkPer * stride) {
         int32_t sz[kLkPer];
-        double dt[kLkPer], dx[kLkPer], dy[kLkPer];
+        double dt[kLkPer], dx[kLkPer], dy[kLkPer], dw[kLkPer], db[kLkPer];
 #pragma unroll
         for (int k = 0; k < kLkPer; k++) {
             const uint32_t i = i0 + k * stride;
@@ -332,6 +470,22 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             sz[k] = size[ic];
             dt[k] = Dt[ic];
             if (pend) { dx[k] = Dx[ic]; dy[k] = Dy[ic]; }
+            if (spec) { dw[k] = Dw[ic]; db[k] = Dsb[ic]; }
+        }
+        // every load of the pass in flight before any is waited for: left to
+        // itself the compiler sank D[t][i]'s load below the size test that
+        // uses size[i] (a second round trip per step), and waited for D[x][t],
+        // D[y][t] (their update, hoisted) and t's and sb's sizes before the pass
+#pragma unroll
+        for (int k = 0; k < kLkPer; k++) {
+            asm volatile("" : "+v"(sz[k]), "+v"(dt[k]));
+            if (pend) asm volatile("" : "+v"(dx[k]), "+v"(dy[k]), "+v"(dxt), "+v"(dyt));
+            if (spec) asm volatile("" : "+v"(dw[k]), "+v"(db[k]));
+        }
+        if (spec) {
+            asm volatile("" : "+v"(rst), "+v"(rsb));
+            const int32_t snt = size_prev(t, rst), snb = size_prev(sb, rsb);
+            snx = t < sb ? snt : snb; sny = t < sb ? snb : snt;
         }
 #pragma unroll
         for (int k = 0; k < kLkPer; k++) {
@@ -341,6 +495,16 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             // (being written by workgroup 0) and this one's (not yet written)
             const int32_t szi = (int32_t)i == X.psa ? 0 : (int32_t)i == X.psb ? X.psbsz : size_prev((int32_t)i, sz[k]);
             if (szi == 0) continue;
+            // (no merge is applied when speculating: the rows are as stored)
+            if (spec && (int32_t)i != t && (int32_t)i != sb) {
+                const double u = lw_update(method, t < sb ? dt[k] : db[k], t < sb ? db[k] : dt[k], snx, sny);
+                if (better(u, (int32_t)i, yv, yi)) { yv = u; yi = (int32_t)i; }
+                if ((int32_t)i == sw) {
+                    if (better(u, sy_, wv, wi)) { wv = u; wi = sy_; }          // D'[sw][max(t, sb)]
+                } else if (better(dw[k], (int32_t)i, wv, wi)) {
+                    wv = dw[k]; wi = (int32_t)i;
+                }
+            }
             double v;
             if (pend && (int32_t)i != y && (int32_t)i != t) {
                 const double u = lw_update(method, dx[k], dy[k], nx, ny);
@@ -367,12 +531,12 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             if (v < bv) { bv = v; bi = (int32_t)i; }
         }
     }
-    const MinIdx part = block_argmin<WG>(bv, bi);
-    if (threadIdx.x == 0) parts[(uint64_t)q * 1024 + blockIdx.x] = part;
-    if (pend) {
-        __syncthreads();
-        const MinIdx p2 = block_argmin<WG>(yv, yi);
-        if (threadIdx.x == 0) parts2[(uint64_t)q * 1024 + blockIdx.x] = p2;
+    MinIdx p1{bv, bi}, p2{yv, yi}, p3{wv, wi};
+    block_argmin3<WG>(p1, p2, p3, pend || spec, spec);
+    if (threadIdx.x == 0) {
+        parts[(uint64_t)q * 1024 + blockIdx.x] = p1;
+        if (pend || spec) parts2[(uint64_t)q * 1024 + blockIdx.x] = p2;
+        if (spec) parts3[(uint64_t)q * 1024 + blockIdx.x] = p3;
     }
 }
 
@@ -564,8 +728,11 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     if ((rc = scratch(ctx, "lk_chain", n * 4ull, (void **)&d_chain))) return rc;
     if ((rc = scratch(ctx, "lk_Z", (n - 1) * 32ull, (void **)&d_Z))) return rc;
     if ((rc = scratch(ctx, "lk_parts", 2 * 1024 * sizeof(MinIdx), (void **)&d_parts))) return rc;
-    MinIdx *d_parts2;
+    MinIdx *d_parts2, *d_parts3;
     if ((rc = scratch(ctx, "lk_parts2", 2 * 1024 * sizeof(MinIdx), (void **)&d_parts2))) return rc;
+    if ((rc = scratch(ctx, "lk_parts3", 2 * 1024 * sizeof(MinIdx), (void **)&d_parts3))) return rc;
+    const char *spe = getenv("DREPHIP_LINK_SPEC");                     // the speculative search (A/B: 0 off)
+    const int spec_on = spe ? atoi(spe) != 0 : 1;
     if ((rc = scratch(ctx, "lk_st", 2 * sizeof(LinkState), (void **)&d_st))) return rc;
     LinkFwd *d_fwd;
     if ((rc = scratch(ctx, "lk_fwd", 2 * sizeof(LinkFwd), (void **)&d_fwd))) return rc;
@@ -611,7 +778,7 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
         if (mst) hipLaunchKernelGGL((k_mst_step<W, P>), gm, blk, 0, st, d_D, n, d_size, d_Dmin, d_st, d_parts, d_done, \
                                     d_Z, q);                                                                     \
         else hipLaunchKernelGGL((k_nn_step<W, P>), gn, blk, 0, st, d_D, n, method, d_size, d_chain, d_st, d_fwd,    \
-                                d_parts, d_parts2, d_done, d_Z, q);                                              \
+                                d_parts, d_parts2, d_parts3, d_done, d_Z, q, spec_on);                           \
     } while (0)
         if (wg == 128) {
             if (tpl == 1) DREPHIP_LK_LAUNCH(128, 1);
@@ -656,6 +823,8 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
         fprintf(stderr, "[drephip] chain: n=%u launches %d, of which %d decided two steps; %d scan launches, "
                         "%d of them followed by a merge with the element below\n", n, hl.launches, hl.twice, hl.scans,
                 hl.recip);
+        fprintf(stderr, "[drephip] chain: first decision after a merge launch: push another %d, push the merged row %d, "
+                        "merge %d; speculation saved %d searches\n", hl.am_other, hl.am_y, hl.am_merge, hl.specwin);
     }
     if (bad) { set_error("linkage: a chain step found no valid partial"); return DREPHIP_ERR_INTERNAL; }
     const double t_fin = now_s();
