@@ -393,7 +393,11 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
         // speculate in a search launch (no merge applied) whose top has two
         // elements below it: search w's row too (P3)
         X.c3 = c3;
-        X.spec = spec_on && !pend && len >= 3 && k < (int32_t)n - 1;
+        X.spec = 0;
+        if (spec_on && len >= 3 && k < (int32_t)n - 1) {
+            if (!pend) X.spec = 1;                              // a search launch
+            else if (below == py && top != py) X.spec = 2;      // a merge launch, its row y below the top
+        }
         sx = X;
         if (w0) {
             st[q] = X;
@@ -445,17 +449,20 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     int32_t lz;
     asm volatile("v_mov_b32 %0, 0" : "=v"(lz));
     double dxt = pend ? Dx[t + lz] : 0.0, dyt = pend ? Dy[t + lz] : 0.0;
-    // speculation (a search launch, X.spec): if t merges with the element
-    // below, sb, the merged row u = LW(D[t], D[sb]) gets index max(t, sb) and
-    // the new top is sw; P2 <- u's minimum, P3 <- sw's row's minimum after
-    // that merge (sw's row without t and sb, plus (u[sw], max(t, sb)))
-    const bool spec = X.spec != 0;
+    // speculation (X.spec): if t merges with the element below, sb, the
+    // merged row U = LW(D[t], D[sb]) gets index max(t, sb) and the new top is
+    // sw; P2 <- U's minimum, P3 <- sw's row's minimum after that merge (sw's
+    // row without t and sb, plus (U[sw], max(t, sb))).  spec 1: a search
+    // launch, the rows as stored; spec 2: a merge launch whose merged row y is
+    // sb, D[sb][i] being the update u this launch computes for i (the real P2,
+    // y's minimum, is not needed then: y is already on the chain)
+    const bool spec1 = X.spec == 1, spec2 = X.spec == 2, spec = spec1 || spec2;
     const int32_t sb = X.below, sw = X.c3;
     const int32_t sy_ = spec ? (t < sb ? sb : t) : 0;
-    const double *Dsb = D + (uint64_t)(spec ? sb : 0) * n;
+    const double *Dsb = D + (uint64_t)(spec1 ? sb : 0) * n;
     const double *Dw = D + (uint64_t)(spec ? sw : 0) * n;
     // (t's and sb's sizes are loaded with the first pass's entries; see below)
-    int32_t rst = spec ? size[t] : 0, rsb = spec ? size[sb] : 0;
+    int32_t rst = spec ? size[t] : 0, rsb = spec1 ? size[sb] : 0;
     int32_t snx = 0, sny = 0;
     double bv = INFINITY, yv = INFINITY, wv = INFINITY;
     int32_t bi = 0x7fffffff, yi = 0x7fffffff, wi = 0x7fffffff;
@@ -470,7 +477,8 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             sz[k] = size[ic];
             dt[k] = Dt[ic];
             if (pend) { dx[k] = Dx[ic]; dy[k] = Dy[ic]; }
-            if (spec) { dw[k] = Dw[ic]; db[k] = Dsb[ic]; }
+            if (spec) dw[k] = Dw[ic];
+            if (spec1) db[k] = Dsb[ic];
         }
         // every load of the pass in flight before any is waited for: left to
         // itself the compiler sank D[t][i]'s load below the size test that
@@ -480,11 +488,12 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
         for (int k = 0; k < kLkPer; k++) {
             asm volatile("" : "+v"(sz[k]), "+v"(dt[k]));
             if (pend) asm volatile("" : "+v"(dx[k]), "+v"(dy[k]), "+v"(dxt), "+v"(dyt));
-            if (spec) asm volatile("" : "+v"(dw[k]), "+v"(db[k]));
+            if (spec) asm volatile("" : "+v"(dw[k]));
+            if (spec1) asm volatile("" : "+v"(db[k]));
         }
         if (spec) {
             asm volatile("" : "+v"(rst), "+v"(rsb));
-            const int32_t snt = size_prev(t, rst), snb = size_prev(sb, rsb);
+            const int32_t snt = size_prev(t, rst), snb = spec2 ? X.psbsz : size_prev(sb, rsb);
             snx = t < sb ? snt : snb; sny = t < sb ? snb : snt;
         }
 #pragma unroll
@@ -495,8 +504,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             // (being written by workgroup 0) and this one's (not yet written)
             const int32_t szi = (int32_t)i == X.psa ? 0 : (int32_t)i == X.psb ? X.psbsz : size_prev((int32_t)i, sz[k]);
             if (szi == 0) continue;
-            // (no merge is applied when speculating: the rows are as stored)
-            if (spec && (int32_t)i != t && (int32_t)i != sb) {
+            if (spec1 && (int32_t)i != t && (int32_t)i != sb) {
                 const double u = lw_update(method, t < sb ? dt[k] : db[k], t < sb ? db[k] : dt[k], snx, sny);
                 if (better(u, (int32_t)i, yv, yi)) { yv = u; yi = (int32_t)i; }
                 if ((int32_t)i == sw) {
@@ -516,13 +524,23 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
 #else
                 D[(uint64_t)i * n + y] = u;
 #endif
-                if (better(u, (int32_t)i, yv, yi)) { yv = u; yi = (int32_t)i; }
+                if (spec2) {                                        // (i is neither t nor sb = y)
+                    const double U = lw_update(method, t < sb ? dt[k] : u, t < sb ? u : dt[k], snx, sny);
+                    if (better(U, (int32_t)i, yv, yi)) { yv = U; yi = (int32_t)i; }
+                    if ((int32_t)i == sw) {
+                        if (better(U, sy_, wv, wi)) { wv = U; wi = sy_; }
+                    } else if (better(dw[k], (int32_t)i, wv, wi)) {
+                        wv = dw[k]; wi = (int32_t)i;
+                    }
+                } else if (better(u, (int32_t)i, yv, yi)) {
+                    yv = u; yi = (int32_t)i;
+                }
                 v = t == y ? u : dt[k];
             } else if (pend && (int32_t)i == y && t != y) {
                 const double u = lw_update(method, dxt, dyt, nx, ny);
                 Dy[t] = u;
                 D[(uint64_t)t * n + y] = u;
-                if (better(u, t, yv, yi)) { yv = u; yi = t; }       // (D[y][t], produced by y's lane)
+                if (!spec2 && better(u, t, yv, yi)) { yv = u; yi = t; }    // (D[y][t], produced by y's lane)
                 v = u;
             } else {
                 if ((int32_t)i == t) continue;
