@@ -51,6 +51,20 @@ static double now_s() {
 
 struct MinIdx { double v; int32_t i; };
 
+// Phase timestamps of the chain step (an A/B build only: make EXTRA=-DDREPHIP_LK_PHASES=1):
+// s_memrealtime (100 MHz) at fixed points of workgroup 0, the last step
+// workgroup and the forwarding workgroup, per launch; the host prints medians.
+#ifndef DREPHIP_LK_PHASES
+#define DREPHIP_LK_PHASES 0
+#endif
+#if DREPHIP_LK_PHASES
+constexpr int kPhCap = 65536;
+__device__ uint64_t *g_lk_ph;
+#define LK_T(v) v = __builtin_amdgcn_s_memrealtime()
+#else
+#define LK_T(v) (void)0
+#endif
+
 __device__ __forceinline__ bool better(double v, int32_t i, double bv, int32_t bi) {
     return v < bv || (v == bv && i < bi);
 }
@@ -251,14 +265,22 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     const uint32_t G = gridDim.x - 1;                          // step workgroups; workgroup G forwards operands
     const LinkState S = st[q ^ 1];
     const LinkFwd F = fwd[q ^ 1];
+#if DREPHIP_LK_PHASES
+    uint64_t ph0 = 0, ph1 = 0, ph2 = 0, ph3 = 0, ph4 = 0, ph5 = 0, ph6 = 0;
+#endif
+    LK_T(ph0);
     // The partial sets are reduced by wave 0 alone (the decision is thread
     // 0's: no barrier), read whether or not they are needed (valid memory
     // either way) so that their loads are not held behind the state's.  A
     // lane takes partials lane, lane + 64, ... four at a time, all loads in
     // flight before the first wait.  (The loop steps by a constant: a
     // blockDim.x stride's kernarg load held the partial loads behind the state's.)
+    // wave 0, as a wave-uniform condition (readfirstlane): the decision below
+    // runs on every lane of wave 0 as scalar code, its values in SGPRs (as
+    // one lane's divergent code it took ~0.8 us a launch)
+    const bool wave0 = __builtin_amdgcn_readfirstlane(threadIdx.x) < 64, lane0 = threadIdx.x == 0;
     MinIdx g{INFINITY, 0x7fffffff}, g2{INFINITY, 0x7fffffff}, g3{INFINITY, 0x7fffffff};
-    if (threadIdx.x < 64) {
+    if (wave0) {
         const MinIdx *P1 = parts + (uint64_t)(q ^ 1) * 1024, *P2 = parts2 + (uint64_t)(q ^ 1) * 1024,
                      *P3 = parts3 + (uint64_t)(q ^ 1) * 1024;
         for (uint32_t b0 = threadIdx.x; b0 < G; b0 += 256) {
@@ -282,6 +304,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
         if (S.mrow >= 0 || F.spec) wave_argmin(g2.v, g2.i);
         if (F.spec) wave_argmin(g3.v, g3.i);
     }
+    LK_T(ph1);
     if (S.k >= (int32_t)n - 1) return;                         // all merged
     const bool w0 = blockIdx.x == 0;
     // size of cluster i as of the previous decision: workgroup 0 writes that
@@ -289,8 +312,10 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     const int32_t spsa = S.psa, spsb = S.psb, spsbsz = S.psbsz;
     auto size_prev = [=](int32_t i, int32_t stored) { return i == spsa ? 0 : i == spsb ? spsbsz : stored; };
     if (w0 && threadIdx.x == 0 && S.psa >= 0) { size[S.psa] = 0; size[S.psb] = S.psbsz; }
-    // ---- the previous step's decision, and y's when it pushes y (replicated in every workgroup)
-    if (threadIdx.x == 0) {
+    // ---- the previous step's decision, and y's when it pushes y (replicated
+    // in every workgroup; its stores by lane 0 of workgroup 0)
+    const bool w0l = w0 && lane0;
+    if (wave0) {
         // (plain scalars, the state struct written once at the end: a struct
         // updated across the branches was kept in private memory)
         int32_t k = S.k, len = S.len, top = S.top, below = S.below, first_active = S.first_active;
@@ -317,7 +342,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                     if (d == 0 && !S.pend) recip++;
                     int32_t a = top, b = below, na = szt, nb = szb;
                     if (a > b) { a = below; b = top; na = szb; nb = szt; }
-                    if (w0) {
+                    if (w0l) {
                         double *z = Z + 4ull * S.k;
                         z[0] = a; z[1] = b; z[2] = dp; z[3] = na + nb;
                     }
@@ -334,7 +359,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                         while (f < (int32_t)n && !(f == b || (f != a && size_prev(f, size[f]) > 0))) f++;
                         if (f >= (int32_t)n) { bad = 1; k = (int32_t)n - 1; }
                         else {
-                            if (w0) chain[0] = f;
+                            if (w0l) chain[0] = f;
                             first_active = f; top = f; below = -1; len = 1;
                         }
                     } else if (d == 0 && F.spec && len >= 1 && k < (int32_t)n - 1) {
@@ -351,13 +376,13 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                         const bool wpush = (uint32_t)r3.i < n && !(len > 1 && !(r3.v < F.dp2)) && len + 1 < (int32_t)n;
                         const bool bpush = r3.i == b && (uint32_t)g2.i < n && g2.v < r3.v;
                         if (wpush && (r3.i != b || bpush)) {
-                            if (w0) chain[len] = r3.i;                  // w pushes r3.i
+                            if (w0l) chain[len] = r3.i;                 // w pushes r3.i
                             c4 = c3; c3 = below; below = top; top = r3.i;
                             ck = ck >= 1 ? 2 : 1;
                             len++;
                             specwin++;
                             if (bpush) {
-                                if (w0) chain[len] = g2.i;              // b pushes g2.i
+                                if (w0l) chain[len] = g2.i;             // b pushes g2.i
                                 c4 = c3; c3 = below; below = top; top = g2.i;
                                 ck = ck >= 1 ? 2 : 1;
                                 len++;
@@ -369,7 +394,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                 }
                 // push (scipy: the previous element wins ties)
                 if (len >= (int32_t)n) { bad = 1; k = (int32_t)n - 1; break; }
-                if (w0) chain[len] = r.i;
+                if (w0l) chain[len] = r.i;
                 c4 = c3; c3 = below; below = top; top = r.i;
                 ck = ck >= 1 ? 2 : 1;
                 dp = r.v;
@@ -398,8 +423,9 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             if (!pend) X.spec = 1;                              // a search launch
             else if (below == py && top != py) X.spec = 2;      // a merge launch, its row y below the top
         }
-        sx = X;
-        if (w0) {
+        if (lane0) sx = X;
+        LK_T(ph2);
+        if (w0l) {
             st[q] = X;
             if (X.k >= (int32_t)n - 1) st[q ^ 1] = X;           // the finished state in both buffers
             *done = X.k;
@@ -416,6 +442,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             int32_t r3 = chain[l3 ? len - 3 : 0], r4 = chain[l4 ? len - 4 : 0];
             double rdp2 = D[sp ? (uint64_t)c3 * n + c4 : 0];
             asm volatile("" : "+v"(rzt), "+v"(rzb), "+v"(rdp), "+v"(r3), "+v"(r4), "+v"(rdp2));
+            LK_T(ph3);
             auto size_now = [&](int32_t i, int32_t stored) { return i == psa ? 0 : i == psb ? psbsz : size_prev(i, stored); };
             LinkFwd f{0.0, 0, 0, 0, 0};
             f.szt = size_now(top, rzt);                         // (also at len 1: a push and a merge may follow)
@@ -429,12 +456,19 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                 f.dp2 = sp ? rdp2 : 0.0;                        // D[w][c4], w = c3
                 f.spec = 1;
             }
-            fwd[q] = f;
+            if (lane0) fwd[q] = f;
+#if DREPHIP_LK_PHASES
+            if (lane0) {
+                uint64_t *ph = g_lk_ph + (uint64_t)(S.launches % kPhCap) * 16;
+                ph[12] = ph0; ph[13] = ph1; ph[14] = ph2; ph[15] = ph3;
+            }
+#endif
         }
     }
     if (blockIdx.x == G) return;                               // the forwarding workgroup has no step work
     __syncthreads();
     const LinkState X = sx;
+    LK_T(ph3);
     if (X.k >= (int32_t)n - 1) return;
     // ---- this step: the pending update fused with the search of row t, and
     // the minimum of the new row y
@@ -491,6 +525,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             if (spec) asm volatile("" : "+v"(dw[k]));
             if (spec1) asm volatile("" : "+v"(db[k]));
         }
+        LK_T(ph4);
         if (spec) {
             asm volatile("" : "+v"(rst), "+v"(rsb));
             const int32_t snt = size_prev(t, rst), snb = spec2 ? X.psbsz : size_prev(sb, rsb);
@@ -549,8 +584,17 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             if (v < bv) { bv = v; bi = (int32_t)i; }
         }
     }
+    LK_T(ph5);
     MinIdx p1{bv, bi}, p2{yv, yi}, p3{wv, wi};
     block_argmin3<WG>(p1, p2, p3, pend || spec, spec);
+    LK_T(ph6);
+#if DREPHIP_LK_PHASES
+    if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == G - 1)) {
+        uint64_t *ph = g_lk_ph + (uint64_t)(S.launches % kPhCap) * 16;
+        if (blockIdx.x == 0) { ph[0] = ph0; ph[1] = ph1; ph[2] = ph2; ph[3] = ph3; ph[4] = ph4; ph[5] = ph5; ph[6] = ph6; }
+        else { ph[8] = ph0; ph[9] = ph3; ph[10] = ph6; }
+    }
+#endif
     if (threadIdx.x == 0) {
         parts[(uint64_t)q * 1024 + blockIdx.x] = p1;
         if (pend || spec) parts2[(uint64_t)q * 1024 + blockIdx.x] = p2;
@@ -781,6 +825,14 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
         int32_t zero = 0;
         HIPC(hipMemcpyAsync(d_done, &zero, 4, hipMemcpyHostToDevice, st));
     }
+#if DREPHIP_LK_PHASES
+    uint64_t *d_ph = nullptr;
+    if (!mst) {
+        HIPC(hipMalloc((void **)&d_ph, (size_t)kPhCap * 16 * 8));
+        HIPC(hipMemset(d_ph, 0, (size_t)kPhCap * 16 * 8));
+        HIPC(hipMemcpyToSymbol(HIP_SYMBOL(g_lk_ph), &d_ph, sizeof(d_ph)));
+    }
+#endif
     // batches of steps captured once in a graph, replayed until every merge is done
     constexpr int kBatch = 256;
     hipGraph_t graph = nullptr;
@@ -844,6 +896,33 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
         fprintf(stderr, "[drephip] chain: first decision after a merge launch: push another %d, push the merged row %d, "
                         "merge %d; speculation saved %d searches\n", hl.am_other, hl.am_y, hl.am_merge, hl.specwin);
     }
+#if DREPHIP_LK_PHASES
+    if (d_ph) {
+        std::vector<uint64_t> h((size_t)kPhCap * 16);
+        HIPC(hipMemcpy(h.data(), d_ph, h.size() * 8, hipMemcpyDeviceToHost));
+        (void)hipFree(d_ph);
+        const LinkState &hl = hs[0].launches > hs[1].launches ? hs[0] : hs[1];
+        const int L = std::min(hl.launches, kPhCap) - 1;
+        const char *names[] = {"wg0 partials reduced", "wg0 decided", "wg0 after barrier", "wg0 row loads in",
+                               "wg0 row done", "wg0 reduced", "last wg start", "last wg after barrier", "last wg reduced",
+                               "fwd start", "fwd partials reduced", "fwd decided", "fwd loads in", "next launch start"};
+        const int col[] = {1, 2, 3, 4, 5, 6, 8, 9, 10, 12, 13, 14, 15, -1};
+        for (int c = 0; c < 14; c++) {
+            std::vector<double> v;
+            for (int l = 100; l < L; l++) {
+                const uint64_t *r = &h[(size_t)l * 16];
+                if (!r[0] || !r[6]) continue;
+                const uint64_t b = col[c] < 0 ? h[(size_t)(l + 1) * 16] : r[col[c]];
+                if (!b) continue;
+                v.push_back(((double)(int64_t)(b - r[0])) * 0.01);
+            }
+            if (v.empty()) continue;
+            std::sort(v.begin(), v.end());
+            fprintf(stderr, "[drephip] phase %-24s med %6.2f us  p90 %6.2f us (%zu launches)\n", names[c], v[v.size() / 2],
+                    v[v.size() * 9 / 10], v.size());
+        }
+    }
+#endif
     if (bad) { set_error("linkage: a chain step found no valid partial"); return DREPHIP_ERR_INTERNAL; }
     const double t_fin = now_s();
     ctx->link.chain_s = t_fin - t_chain;
