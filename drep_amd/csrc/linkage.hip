@@ -100,26 +100,62 @@ template <int CTRL, int RM>
 __device__ __forceinline__ int32_t dpp_i32(int32_t i) {
     return __builtin_amdgcn_update_dpp(0x7fffffff, i, CTRL, RM, 0xf, false);
 }
+__device__ __forceinline__ double min_f64(double a, double b) { return fmin(a, b); }
+// N independent sets at once: their steps interleave, hiding each other's
+// DPP hazards and latencies
+template <int N>
+__device__ __forceinline__ void wave_argmin_n(double (&v)[N], int32_t (&i)[N]) {
+    double m[N];
+#pragma unroll
+    for (int s = 0; s < N; s++) m[s] = v[s];
+#define DREPHIP_DPP_MIN(C, R) _Pragma("unroll") for (int s = 0; s < N; s++) m[s] = min_f64(m[s], dpp_f64<C, R>(m[s]))
+    DREPHIP_DPP_MIN(0x111, 0xf);
+    DREPHIP_DPP_MIN(0x112, 0xf);
+    DREPHIP_DPP_MIN(0x114, 0xf);
+    DREPHIP_DPP_MIN(0x118, 0xf);
+    DREPHIP_DPP_MIN(0x142, 0xa);
+    DREPHIP_DPP_MIN(0x143, 0xc);
+#undef DREPHIP_DPP_MIN
+    int32_t c[N];
+#pragma unroll
+    for (int s = 0; s < N; s++) {
+        const long long b = __double_as_longlong(m[s]);
+        const int lo = __builtin_amdgcn_readlane((int)b, 63), hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+        m[s] = __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+        c[s] = v[s] == m[s] ? i[s] : 0x7fffffff;
+    }
+#define DREPHIP_DPP_MINI(C, R) _Pragma("unroll") for (int s = 0; s < N; s++) c[s] = min(c[s], dpp_i32<C, R>(c[s]))
+    DREPHIP_DPP_MINI(0x111, 0xf);
+    DREPHIP_DPP_MINI(0x112, 0xf);
+    DREPHIP_DPP_MINI(0x114, 0xf);
+    DREPHIP_DPP_MINI(0x118, 0xf);
+    DREPHIP_DPP_MINI(0x142, 0xa);
+    DREPHIP_DPP_MINI(0x143, 0xc);
+#undef DREPHIP_DPP_MINI
+#pragma unroll
+    for (int s = 0; s < N; s++) { v[s] = m[s]; i[s] = __builtin_amdgcn_readlane(c[s], 63); }
+}
 __device__ __forceinline__ void wave_argmin(double &v, int32_t &i) {
-    double m = v;
-    m = fmin(m, dpp_f64<0x111, 0xf>(m));
-    m = fmin(m, dpp_f64<0x112, 0xf>(m));
-    m = fmin(m, dpp_f64<0x114, 0xf>(m));
-    m = fmin(m, dpp_f64<0x118, 0xf>(m));
-    m = fmin(m, dpp_f64<0x142, 0xa>(m));
-    m = fmin(m, dpp_f64<0x143, 0xc>(m));
-    const long long b = __double_as_longlong(m);
-    const int lo = __builtin_amdgcn_readlane((int)b, 63), hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
-    m = __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
-    int32_t c = v == m ? i : 0x7fffffff;
-    c = min(c, dpp_i32<0x111, 0xf>(c));
-    c = min(c, dpp_i32<0x112, 0xf>(c));
-    c = min(c, dpp_i32<0x114, 0xf>(c));
-    c = min(c, dpp_i32<0x118, 0xf>(c));
-    c = min(c, dpp_i32<0x142, 0xa>(c));
-    c = min(c, dpp_i32<0x143, 0xc>(c));
-    v = m;
-    i = __builtin_amdgcn_readlane(c, 63);
+    double vv[1] = {v};
+    int32_t ii[1] = {i};
+    wave_argmin_n<1>(vv, ii);
+    v = vv[0]; i = ii[0];
+}
+// one, two or three sets (block-uniform counts), interleaved
+__device__ __forceinline__ void wave_argmin_upto3(MinIdx &a, MinIdx &b, MinIdx &c, bool with_b, bool with_c) {
+    if (with_c) {
+        double v[3] = {a.v, b.v, c.v};
+        int32_t i[3] = {a.i, b.i, c.i};
+        wave_argmin_n<3>(v, i);
+        a = MinIdx{v[0], i[0]}; b = MinIdx{v[1], i[1]}; c = MinIdx{v[2], i[2]};
+    } else if (with_b) {
+        double v[2] = {a.v, b.v};
+        int32_t i[2] = {a.i, b.i};
+        wave_argmin_n<2>(v, i);
+        a = MinIdx{v[0], i[0]}; b = MinIdx{v[1], i[1]};
+    } else {
+        wave_argmin(a.v, a.i);
+    }
 }
 
 // Block argmin (smallest index among equal minima); result valid in thread 0.
@@ -146,9 +182,7 @@ template <int WG>
 __device__ void block_argmin3(MinIdx &a, MinIdx &b, MinIdx &c, bool with_b, bool with_c) {
     __shared__ double sv[3][WG / 64];
     __shared__ int32_t si[3][WG / 64];
-    wave_argmin(a.v, a.i);
-    if (with_b) wave_argmin(b.v, b.i);
-    if (with_c) wave_argmin(c.v, c.i);
+    wave_argmin_upto3(a, b, c, with_b, with_c);
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
         sv[0][w] = a.v; si[0][w] = a.i;
@@ -300,9 +334,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                 if (better(m3[u].v, m3[u].i, g3.v, g3.i)) g3 = m3[u];
             }
         }
-        wave_argmin(g.v, g.i);
-        if (S.mrow >= 0 || F.spec) wave_argmin(g2.v, g2.i);
-        if (F.spec) wave_argmin(g3.v, g3.i);
+        wave_argmin_upto3(g, g2, g3, S.mrow >= 0 || F.spec, F.spec != 0);
     }
     LK_T(ph1);
     if (S.k >= (int32_t)n - 1) return;                         // all merged
