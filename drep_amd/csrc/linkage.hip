@@ -252,6 +252,7 @@ struct alignas(64) LinkState {
     int32_t am_other, am_y, am_merge;   // diagnostics: the first decision after a merge launch
     int32_t c3, spec;             // chain[len - 3] (w); 1: this launch searches w's row speculatively (P3)
     int32_t specwin;              // diagnostics: launches saved by the speculation
+    int32_t m0, m0m;              // diagnostics: merge launches without speculation, and those whose next decision merges
 };
 
 // all partials of the previous kernel -> their minimum (thread 0)
@@ -354,6 +355,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
         int32_t pend = 0, px = S.x, py = S.y, pnx = S.nx, pny = S.ny, bad = S.bad, mrow = -1;
         int32_t psa = -1, psb = -1, psbsz = 0, twice = S.twice, recip = S.recip;
         int32_t am_other = S.am_other, am_y = S.am_y, am_merge = S.am_merge, specwin = S.specwin;
+        int32_t m0m = S.m0m;
         // c3, c4: chain[len - 3], chain[len - 4]; ck of them are known exactly
         // (a merge exposes entries only the chain in memory holds; a push
         // shifts known ones down)
@@ -371,6 +373,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                     else am_other++;
                 }
                 if (len > 1 && !(r.v < dp)) {                     // merge top with below at dp
+                    if (d == 0 && S.pend && !F.spec) m0m++;
                     if (d == 0 && !S.pend) recip++;
                     int32_t a = top, b = below, na = szt, nb = szb;
                     if (a > b) { a = below; b = top; na = szb; nb = szt; }
@@ -447,6 +450,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
         X.launches = S.launches + 1; X.twice = twice;
         X.recip = recip; X.scans = S.scans + (pend ? 0 : 1);
         X.am_other = am_other; X.am_y = am_y; X.am_merge = am_merge; X.specwin = specwin;
+        X.m0m = m0m;
         // speculate in a search launch (no merge applied) whose top has two
         // elements below it: search w's row too (P3)
         X.c3 = c3;
@@ -455,6 +459,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             if (!pend) X.spec = 1;                              // a search launch
             else if (below == py && top != py) X.spec = 2;      // a merge launch, its row y below the top
         }
+        X.m0 = S.m0 + (pend && !X.spec ? 1 : 0);
         if (lane0) sx = X;
         LK_T(ph2);
         if (w0l) {
@@ -927,6 +932,8 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
                 hl.recip);
         fprintf(stderr, "[drephip] chain: first decision after a merge launch: push another %d, push the merged row %d, "
                         "merge %d; speculation saved %d searches\n", hl.am_other, hl.am_y, hl.am_merge, hl.specwin);
+        fprintf(stderr, "[drephip] chain: %d merge launches without speculation, %d of them followed by a merge\n", hl.m0,
+                hl.m0m);
     }
 #if DREPHIP_LK_PHASES
     if (d_ph) {
