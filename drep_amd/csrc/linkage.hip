@@ -18,9 +18,11 @@
 // over the chain top's row.  Steps are launched in batches captured in a
 // hipGraph; kernels after the last merge exit at once.
 // Roofline: latency -- a step reads one 8n-byte row (and after a merge two
-// more rows, writing a row and a strided column); at n = 10^5 (0.8 MB rows)
-// the kernel boundary and the dependent loads of a step (state -> partials
-// and decision -> row) dominate, ~6.4 us per step.
+// more rows, writing a row and a strided column; a speculating step reads two
+// more); at n = 10^5 (0.8 MB rows) the kernel boundary (~2 us) and the two
+// dependent round trips of a step (state + partials, then the rows) dominate,
+// ~5.5-7 us per launch, ~1.3 launches per merge with the speculation below
+// (DESIGN.md 4.4).
 
 #include "ctx.h"
 #include "../../include/drephip.h"
@@ -289,6 +291,14 @@ struct alignas(64) LinkFwd {
 // step pushes y -- the new top's nearest neighbour is often the cluster just
 // formed -- y's own step is decided at once from P2 instead of by a launch
 // that searches y's row: up to two chain steps per launch.
+//
+// Speculation: a launch whose top t may merge with the element below it, sb
+// (a search launch, or a merge launch whose merged row is sb), also reduces
+// the row that merge would form (P2) and the row of the element below sb, w,
+// as it would be after it (P3).  When the next decision is that merge, w's
+// step and (when w pushes the merged row) that row's step are decided from P3
+// and P2 in the same launch, which then searches the row pushed last: runs of
+// reciprocal merges take one launch per merge.
 template <int WG, int kLkPer>
 __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t n, int method,
                                                    int32_t *__restrict__ size, int32_t *__restrict__ chain,
