@@ -5,7 +5,7 @@ cd ${GRAFT_REPO_ROOT:-.}
 export TMPDIR=/tmp
 mkdir -p gpurun_out/lktr
 DREPHIP_DEBUG=1 timeout -k 10 300 python tools/link_ab.py ${N:-10000} > gpurun_out/lktr/run.json 2> gpurun_out/lktr/run.err || exit 1
-grep "chain:" gpurun_out/lktr/run.err | tail -2
+grep "chain:" gpurun_out/lktr/run.err | tail -3
 timeout -s KILL 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/lktr/tr -o t -- python tools/link_ab.py ${N:-10000} > gpurun_out/lktr/tr.log 2>&1 || exit 1
 f=$(find gpurun_out/lktr/tr -name "*kernel_trace.csv" | head -1)
 python3 - "$f" <<'PY'
@@ -20,3 +20,4 @@ for k, v in d.items():
     print(k, len(v), "dur med %.2f us p90 %.2f" % (np.median(dur) / 1e3, np.percentile(dur, 90) / 1e3),
           "gap med %.2f us p90 %.2f" % (np.median(gap) / 1e3, np.percentile(gap, 90) / 1e3))
 PY
+rm -rf gpurun_out/lktr/tr                                  # (the trace CSV: tens of MB)
