@@ -185,6 +185,7 @@ __device__ void block_argmin3(MinIdx &a, MinIdx &b, MinIdx &c, bool with_b, bool
     __shared__ double sv[3][WG / 64];
     __shared__ int32_t si[3][WG / 64];
     wave_argmin_upto3(a, b, c, with_b, with_c);
+    if constexpr (WG == 64) return;                            // one wave: every lane holds the result
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
         sv[0][w] = a.v; si[0][w] = a.i;
@@ -823,11 +824,16 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     const char *pl = getenv("DREPHIP_LINK_PER_LANE");
     const char *tg = getenv("DREPHIP_LINK_TARGET_WG");                 // A/B runs only
     const uint32_t kLkTarget = tg ? std::max(1, atoi(tg)) : 200;
+    // DREPHIP_LINK_WG=64 (A/B): one-wave step workgroups (no LDS broadcast or
+    // block reduction), up to 8 entries per lane per pass; not for single linkage
+    const char *wge = getenv("DREPHIP_LINK_WG");
+    const bool wave_wg = wge && atoi(wge) == 64 && method != DREPHIP_LINK_SINGLE;
+    const uint32_t wsz = wave_wg ? 64 : kLkWG;
     const uint32_t per = pl ? std::max(1, std::min(64, atoi(pl)))
-                            : std::max(1u, (n + kLkWG * kLkTarget - 1) / (kLkWG * kLkTarget));
-    const uint32_t wg = n <= kLkSmallN && !pl ? 128 : kLkWG;
+                            : std::max(1u, (n + wsz * kLkTarget - 1) / (wsz * kLkTarget));
+    const uint32_t wg = wave_wg ? 64 : n <= kLkSmallN && !pl ? 128 : kLkWG;
     const uint32_t grid = std::max(1u, std::min(1024u, (n + wg * per - 1) / (wg * per)));
-    const int tpl = per <= 1 ? 1 : per <= 2 ? 2 : 4;          // entries per lane per pass
+    const int tpl = per <= 1 ? 1 : per <= 2 ? 2 : per <= 4 || !wave_wg ? 4 : 8;     // entries per lane per pass
     int32_t *d_size, *d_chain, *d_done;
     double *d_Z, *d_Dmin;
     LinkState *d_st;
@@ -897,7 +903,16 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
         else hipLaunchKernelGGL((k_nn_step<W, P>), gn, blk, 0, st, d_D, n, method, d_size, d_chain, d_st, d_fwd,    \
                                 d_parts, d_parts2, d_parts3, d_done, d_Z, q, spec_on);                           \
     } while (0)
-        if (wg == 128) {
+        if (wg == 64) {
+#define DREPHIP_LK_LAUNCH64(P)                                                                                   \
+    hipLaunchKernelGGL((k_nn_step<64, P>), gn, blk, 0, st, d_D, n, method, d_size, d_chain, d_st, d_fwd, d_parts, \
+                       d_parts2, d_parts3, d_done, d_Z, q, spec_on)
+            if (tpl == 1) DREPHIP_LK_LAUNCH64(1);
+            else if (tpl == 2) DREPHIP_LK_LAUNCH64(2);
+            else if (tpl == 4) DREPHIP_LK_LAUNCH64(4);
+            else DREPHIP_LK_LAUNCH64(8);
+#undef DREPHIP_LK_LAUNCH64
+        } else if (wg == 128) {
             if (tpl == 1) DREPHIP_LK_LAUNCH(128, 1);
             else if (tpl == 2) DREPHIP_LK_LAUNCH(128, 2);
             else DREPHIP_LK_LAUNCH(128, 4);
