@@ -824,14 +824,22 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     const char *pl = getenv("DREPHIP_LINK_PER_LANE");
     const char *tg = getenv("DREPHIP_LINK_TARGET_WG");                 // A/B runs only
     const uint32_t kLkTarget = tg ? std::max(1, atoi(tg)) : 200;
-    // DREPHIP_LINK_WG=64 (A/B): one-wave step workgroups (no LDS broadcast or
-    // block reduction), up to 8 entries per lane per pass; not for single linkage
+    // One-wave step workgroups (no LDS broadcast, no block reduction) with one
+    // entry per lane up to n = kLkWaveN (<= 256 workgroups: the decision's wave
+    // reduces <= 4 partials a lane): 70.9 vs 75.2 ms of chain at 10^4.  With
+    // more entries per lane they lose (10^5: 1.21-1.41 s against 1.00 s for
+    // 256-lane workgroups at 2 per lane; profiles/r04_linkage_wg64_ab.txt).
+    // DREPHIP_LINK_WG = 64 / 128 / 256 forces the choice (A/B); a per-lane
+    // override keeps the 128/256-lane kernels unless 64 is asked for.  Not for
+    // single linkage (k_mst_step).
+    constexpr uint32_t kLkWaveN = 16384;
     const char *wge = getenv("DREPHIP_LINK_WG");
-    const bool wave_wg = wge && atoi(wge) == 64 && method != DREPHIP_LINK_SINGLE;
+    const int wreq = wge ? atoi(wge) : 0;
+    const bool wave_wg = method != DREPHIP_LINK_SINGLE && (wreq == 64 || (wreq == 0 && !pl && n <= kLkWaveN));
     const uint32_t wsz = wave_wg ? 64 : kLkWG;
     const uint32_t per = pl ? std::max(1, std::min(64, atoi(pl)))
                             : std::max(1u, (n + wsz * kLkTarget - 1) / (wsz * kLkTarget));
-    const uint32_t wg = wave_wg ? 64 : n <= kLkSmallN && !pl ? 128 : kLkWG;
+    const uint32_t wg = wave_wg ? 64 : wreq == 128 || wreq == 256 ? (uint32_t)wreq : n <= kLkSmallN && !pl ? 128 : kLkWG;
     const uint32_t grid = std::max(1u, std::min(1024u, (n + wg * per - 1) / (wg * per)));
     const int tpl = per <= 1 ? 1 : per <= 2 ? 2 : per <= 4 || !wave_wg ? 4 : 8;     // entries per lane per pass
     int32_t *d_size, *d_chain, *d_done;

@@ -843,11 +843,16 @@ def test_gpu_linkage_matches_scipy(method, n, kind):
     else:
         y = np.full(m, 0.5)
     Zs = sch.linkage(y, method=method)
-    # grid densities of the chain-step kernel
-    variants = [(pl, {}) for pl in (("4", "1", "16") if n <= 2000 else ("4",))]
+    # grid densities of the chain-step kernel: the default (one-wave
+    # workgroups up to n = 16384), 128/256-lane workgroups at 1, 4 and 16
+    # entries per lane, one-wave workgroups with several entries per lane
+    variants = [(None, {}), ("4", {})]
+    if n <= 2000:
+        variants += [("1", {}), ("16", {}), ("2", {"DREPHIP_LINK_WG": "64"}), ("8", {"DREPHIP_LINK_WG": "64"})]
 
     for per_lane, env in variants:
-        os.environ["DREPHIP_LINK_PER_LANE"] = per_lane
+        if per_lane is not None:
+            os.environ["DREPHIP_LINK_PER_LANE"] = per_lane
         os.environ.update(env)
         try:
             with _lib.Context(0, 21, S, 42) as ctx:
