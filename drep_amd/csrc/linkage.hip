@@ -176,6 +176,30 @@ __device__ MinIdx block_argmin(double v, int32_t i) {
     return r;
 }
 
+// A lane's share of the previous launch's partial sets: partials lane,
+// lane + 64, ... U at a time, every load in flight before the first wait
+template <int U>
+__device__ __forceinline__ void partial_pass(const MinIdx *P1, const MinIdx *P2, const MinIdx *P3, uint32_t G,
+                                             MinIdx &g, MinIdx &g2, MinIdx &g3) {
+    for (uint32_t b0 = threadIdx.x; b0 < G; b0 += 64 * U) {
+        MinIdx m1[U], m2[U], m3[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t b = min(b0 + 64u * u, G - 1);             // (a repeated partial changes no minimum)
+            m1[u] = P1[b]; m2[u] = P2[b]; m3[u] = P3[b];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            asm volatile("" : "+v"(m1[u].v), "+v"(m1[u].i), "+v"(m2[u].v), "+v"(m2[u].i), "+v"(m3[u].v), "+v"(m3[u].i));
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (better(m1[u].v, m1[u].i, g.v, g.i)) g = m1[u];
+            if (better(m2[u].v, m2[u].i, g2.v, g2.i)) g2 = m2[u];
+            if (better(m3[u].v, m3[u].i, g3.v, g3.i)) g3 = m3[u];
+        }
+    }
+}
+
 // Up to three block argmins at once, one barrier (results in thread 0): a
 // chain step reduces one to three sets per launch and per decision.  b and c
 // are reduced only when the (block-uniform) flags ask for them: an unneeded
@@ -329,23 +353,8 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     if (wave0) {
         const MinIdx *P1 = parts + (uint64_t)(q ^ 1) * 1024, *P2 = parts2 + (uint64_t)(q ^ 1) * 1024,
                      *P3 = parts3 + (uint64_t)(q ^ 1) * 1024;
-        for (uint32_t b0 = threadIdx.x; b0 < G; b0 += 256) {
-            MinIdx m1[4], m2[4], m3[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const uint32_t b = min(b0 + 64u * u, G - 1);         // (a repeated partial changes no minimum)
-                m1[u] = P1[b]; m2[u] = P2[b]; m3[u] = P3[b];
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-                asm volatile("" : "+v"(m1[u].v), "+v"(m1[u].i), "+v"(m2[u].v), "+v"(m2[u].i), "+v"(m3[u].v), "+v"(m3[u].i));
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                if (better(m1[u].v, m1[u].i, g.v, g.i)) g = m1[u];
-                if (better(m2[u].v, m2[u].i, g2.v, g2.i)) g2 = m2[u];
-                if (better(m3[u].v, m3[u].i, g3.v, g3.i)) g3 = m3[u];
-            }
-        }
+        if (G <= 256) partial_pass<4>(P1, P2, P3, G, g, g2, g3);
+        else partial_pass<8>(P1, P2, P3, G, g, g2, g3);              // (up to 512 workgroups in one pass)
         wave_argmin_upto3(g, g2, g3, S.mrow >= 0 || F.spec, F.spec != 0);
     }
     LK_T(ph1);
