@@ -44,6 +44,7 @@ vp = C.c_void_p
 # name -> (restype, argtypes); every symbol declared in include/drephip.h
 SIGNATURES = {
     "drephip_version": (C.c_int, []),
+    "drephip_build_id": (C.c_char_p, []),
     "drephip_last_error": (C.c_char_p, []),
     "drephip_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "drephip_create": (C.c_int, [C.c_int, C.c_int, C.c_uint32, C.c_uint32, C.POINTER(vp)]),
@@ -141,6 +142,28 @@ def lib():
             fn.argtypes = args
         _lib = L
         return L
+
+
+def source_digest(root: Optional[str] = None) -> str:
+    """sha256 of the library's sources as drep_amd/csrc/Makefile computes it
+    for drephip_build_id: the `sha256sum` listing of include/drephip.h and the
+    sorted drep_amd/csrc/*.{cpp,h,hip} + Makefile, hashed again."""
+    import glob
+    import hashlib
+    root = root or os.path.dirname(_HERE)
+    csrc = os.path.join(root, "drep_amd", "csrc")
+    names = sorted([os.path.basename(p) for ext in ("*.hip", "*.cpp", "*.h")
+                    for p in glob.glob(os.path.join(csrc, ext))] + ["Makefile"])
+    files = ["include/drephip.h"] + ["drep_amd/csrc/" + n for n in names]
+    listing = "".join("%s  %s\n" % (hashlib.sha256(open(os.path.join(root, f), "rb").read()).hexdigest(), f)
+                      for f in files)
+    return hashlib.sha256(listing.encode()).hexdigest()
+
+
+def build_id() -> dict:
+    """The loaded library's build identity (drephip_build_id) as a dict."""
+    raw = lib().drephip_build_id().decode()
+    return dict(kv.split("=", 1) for kv in raw.split(";") if "=" in kv)
 
 
 def check(rc: int, what: str) -> None:

@@ -136,6 +136,16 @@ static int refuse_if_pending(drephip_ctx *ctx) {
 
 DREPHIP_EXPORT int drephip_version(void) { return 100; }
 
+#ifndef DREPHIP_SRC_DIGEST
+#define DREPHIP_SRC_DIGEST "unknown"
+#endif
+#ifndef DREPHIP_BUILD_FLAGS
+#define DREPHIP_BUILD_FLAGS ""
+#endif
+DREPHIP_EXPORT const char *drephip_build_id(void) {
+    return "src=" DREPHIP_SRC_DIGEST ";arch=gfx950;extra=" DREPHIP_BUILD_FLAGS;
+}
+
 DREPHIP_EXPORT const char *drephip_last_error(void) { return g_err.c_str(); }
 
 DREPHIP_EXPORT int drephip_device_count(int *n) {

@@ -191,6 +191,7 @@ __global__ __launch_bounds__(kScWG) void k_run_write(const uint32_t *__restrict_
 // the bitmap: a pair that shares exactly one hash has count (i + j < s) --
 // the hash's rank in A u B is i + j -- and needs no kernel (k_screen_simple).
 constexpr uint64_t kPairEmpty = ~0ull;
+constexpr uint64_t kMaxPairMap = 1ull << 30;   // pair-map slots (16 B each); above it the screen gives way
 __device__ __forceinline__ uint32_t pair_slot(uint64_t key, uint32_t mask) {
     uint64_t h = key * 0x9E3779B97F4A7C15ull;
     return (uint32_t)(h >> 32) & mask;
@@ -378,7 +379,8 @@ __global__ __launch_bounds__(kMarkWG) void k_screen_mark(const uint32_t *__restr
 
 // per row tile (one workgroup): marked columns -> cnt[t], items -> itc[t]
 __global__ __launch_bounds__(kScWG) void k_screen_count(const uint32_t *__restrict__ bm, uint32_t NW, uint32_t C,
-                                                        uint32_t *__restrict__ cnt, uint32_t *__restrict__ itc) {
+                                                        uint32_t *__restrict__ cnt, uint64_t *__restrict__ cnt64,
+                                                        uint32_t *__restrict__ itc) {
     __shared__ uint32_t red[kScWG / 64];
     const uint32_t t = blockIdx.x;
     const uint32_t *row = bm + (uint64_t)t * NW;
@@ -392,6 +394,7 @@ __global__ __launch_bounds__(kScWG) void k_screen_count(const uint32_t *__restri
         uint32_t tot = 0;
         for (int k = 0; k < kScWG / 64; k++) tot += red[k];
         cnt[t] = tot;
+        cnt64[t] = tot;
         itc[t] = (tot + C - 1) / C;
     }
 }
@@ -478,8 +481,8 @@ struct ScreenProf {
     }
 };
 
-template <class T>
-static int hip_scan(drephip_ctx *ctx, const char *name, const uint32_t *in, T *out, uint32_t n, hipStream_t st) {
+template <class I, class T>
+static int hip_scan(drephip_ctx *ctx, const char *name, const I *in, T *out, uint32_t n, hipStream_t st) {
     size_t tb = 0;
     HIPC(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, n, st));
     void *tmp;
@@ -590,10 +593,14 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
     res->checks = E;
     // dense set: a pair check costs about as much as a few probes of the
     // dense kernels, which make ~s/2 probes per pair (DREPHIP_SCREEN_RATIO
-    // scales the bound; `force` skips it)
+    // scales the bound; `force` skips it).  E counts the checks of the whole
+    // triangle (every rank groups all N s entries), so it is weighed against
+    // the whole triangle's pairs, not this segment's: every rank of a sharded
+    // job, and the one-GPU call, take the same path
     const char *re = getenv("DREPHIP_SCREEN_RATIO");
     const double ratio = re ? atof(re) : 16.0;
-    if (!force && (double)E * ratio > (double)npairs * s) { timing_mark(ctx, 4, st, false); return DREPHIP_OK; }
+    const double all_pairs = (double)N * (double)(N - 1) / 2.0;
+    if (!force && (double)E * ratio > all_pairs * s) { timing_mark(ctx, 4, st, false); return DREPHIP_OK; }
 
     const uint32_t rows = row1 - row0;
     const uint32_t ntiles = (rows + R - 1) / R;
@@ -601,14 +608,17 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
     uint32_t rshift = 0;
     while ((1u << rshift) < R) rshift++;
     uint32_t *d_bm, *d_cnt, *d_itc;
-    uint64_t *d_coff;
+    uint64_t *d_coff, *d_cnt64;
     if ((rc = scratch(ctx, "sc_bitmap", (uint64_t)ntiles * NW * 4, (void **)&d_bm))) return rc;
     if ((rc = scratch(ctx, "sc_tcnt", (ntiles + 1) * 4ull, (void **)&d_cnt))) return rc;
+    if ((rc = scratch(ctx, "sc_tcnt64", (ntiles + 1) * 8ull, (void **)&d_cnt64))) return rc;
     if ((rc = scratch(ctx, "sc_titc", (ntiles + 1) * 4ull, (void **)&d_itc))) return rc;
     if ((rc = scratch(ctx, "sc_coff", (ntiles + 1) * 8ull, (void **)&d_coff))) return rc;
-    // the pair map of the runs of two (k_screen_mark2), twice their count
-    uint32_t pcap = 1024;
+    // the pair map of the runs of two (k_screen_mark2), twice their count; a
+    // map beyond kMaxPairMap slots (16 B each) is not built: the dense path runs
+    uint64_t pcap = 1024;
     while (pcap < 2ull * n2) pcap <<= 1;
+    if (pcap > kMaxPairMap) { timing_mark(ctx, 4, st, false); return DREPHIP_OK; }
     unsigned long long *pkey, *d_nsimple;
     uint32_t *pcnt, *ppos;
     if ((rc = scratch(ctx, "sc_pkey", pcap * 8ull, (void **)&pkey))) return rc;
@@ -639,16 +649,18 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
     if (n2) {
         const uint32_t g2 = std::max(1u, std::min(8192u, (n2 + kScWG - 1) / kScWG));
         hipLaunchKernelGGL(k_screen_mark2, dim3(g2), dim3(kScWG), 0, st, v_out, d_hashes, s, d_pairs, n2, row0, row1,
-                           pkey, pcnt, ppos, pcap - 1);
-        const uint32_t gs = std::max(1u, std::min(8192u, (pcap + kScWG - 1) / kScWG));
-        hipLaunchKernelGGL(k_screen_simple, dim3(gs), dim3(kScWG), 0, st, pkey, pcnt, ppos, pcap, d_nhash, s, N, row0,
+                           pkey, pcnt, ppos, (uint32_t)(pcap - 1));
+        const uint32_t gs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, (pcap + kScWG - 1) / kScWG));
+        hipLaunchKernelGGL(k_screen_simple, dim3(gs), dim3(kScWG), 0, st, pkey, pcnt, ppos, (uint32_t)pcap, d_nhash, s, N, row0,
                            rshift, NW, seg0, d_bm, d_common, d_nsimple);
     }
     prof.mark("mark", st);
-    hipLaunchKernelGGL(k_screen_count, dim3(ntiles), dim3(kScWG), 0, st, d_bm, NW, C, d_cnt, d_itc);
-    // the last entry of each scan holds the totals: count entries ntiles + 1, the last one zero
-    HIPC(hipMemsetAsync(d_cnt + ntiles, 0, 4, st));
-    if ((rc = hip_scan(ctx, "sc_scan_tmp1", d_cnt, d_coff, ntiles + 1, st))) return rc;
+    hipLaunchKernelGGL(k_screen_count, dim3(ntiles), dim3(kScWG), 0, st, d_bm, NW, C, d_cnt, d_cnt64, d_itc);
+    // the last entry of each scan holds the totals: count entries ntiles + 1, the last one zero.
+    // The column offsets are summed in 64 bits (the marked cells may pass 2^32;
+    // a 32-bit scan would wrap and the fallback below would never fire)
+    HIPC(hipMemsetAsync(d_cnt64 + ntiles, 0, 8, st));
+    if ((rc = hip_scan(ctx, "sc_scan_tmp1", d_cnt64, d_coff, ntiles + 1, st))) return rc;
     prof.mark("count+scans", st);
     uint32_t *h_itc, *ibase;
     if ((rc = pinned_host(ctx, "sc_itc", ntiles * 4ull, (void **)&h_itc))) return rc;

@@ -510,81 +510,89 @@ __global__ __launch_bounds__(1024) void k_sketch_finalize_bucket(
 // the LDS holds): the bucket counts stay in LDS, the candidates go to a
 // per-workgroup slice of a global buffer (gbuf + blockIdx.x * maxc, L2-resident
 // at these sizes) and each bucket (~2-3 hashes) is insertion-sorted there.
+// The grid is at most kFinGlobalSlices workgroups, each looping over the
+// genome list, so the buffer stays bounded (kFinGlobalSlices * maxc * 8 B,
+// 2 GiB at s = 32767) however many genomes one call sketches.
+constexpr uint32_t kFinGlobalSlices = 2048;
 template <int NB>
 __global__ __launch_bounds__(1024) void k_sketch_finalize_global(
     unsigned long long *__restrict__ sets, uint32_t *__restrict__ cnt,
-    const uint64_t *__restrict__ thr, const uint32_t *__restrict__ glist, uint32_t set_log2,
+    const uint64_t *__restrict__ thr, const uint32_t *__restrict__ glist, uint32_t ng, uint32_t set_log2,
     uint32_t maxc, uint32_t s, uint64_t *__restrict__ out, uint32_t *__restrict__ nhash,
     uint8_t *__restrict__ status, uint64_t *__restrict__ gbuf) {
     constexpr uint32_t WG = 1024, PER = NB / WG, LOGNB = __builtin_ctz(NB);
     static_assert(NB % WG == 0 && (NB & (NB - 1)) == 0, "NB: power of two, multiple of the workgroup");
     __shared__ uint32_t bk[NB];            // counts, then running end offsets
     __shared__ uint32_t wsum[WG / 64];
-    const uint32_t g = glist[blockIdx.x];
-    const uint32_t n = cnt[g];
     const uint32_t tid = threadIdx.x;
-    const uint64_t T = thr[g];
-    unsigned long long *S = sets + ((uint64_t)g << set_log2);
     uint64_t *buf = gbuf + (uint64_t)blockIdx.x * maxc;
     const uint32_t slots = 1u << set_log2;
-    if (n > maxc || (n < s && T < kMaxThr)) {
-        if (tid == 0) status[g] = n > maxc ? ST_DOWN : ST_UP;
-        finalize_reset(S, slots, cnt + g);
-        return;
-    }
-    const uint32_t tbits = 64 - __builtin_clzll(T | 1);
-    const uint32_t shift = tbits > LOGNB ? tbits - LOGNB : 0;
-    for (uint32_t i = tid; i < NB; i += WG) bk[i] = 0;
-    __syncthreads();
-    if (tid == 0) cnt[g] = 0;                          // every thread has read it
-    for (uint32_t i = tid; i < slots; i += WG) {
-        const uint64_t v = S[i];
-        if (v != kEmpty) atomicAdd(&bk[min((uint32_t)(v >> shift), (uint32_t)NB - 1u)], 1u);
-    }
-    __syncthreads();
-    uint32_t loc[PER], sum = 0;
-#pragma unroll
-    for (int j = 0; j < PER; j++) { loc[j] = sum; sum += bk[tid * PER + j]; }
-    uint32_t inc = sum;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(inc, d, 64);
-        if ((tid & 63) >= d) inc += y;
-    }
-    if ((tid & 63) == 63) wsum[tid >> 6] = inc;
-    __syncthreads();
-    uint32_t base = inc - sum;
-    for (uint32_t w = 0; w < (tid >> 6); w++) base += wsum[w];
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < PER; j++) bk[tid * PER + j] = base + loc[j];
-    __syncthreads();
-    for (uint32_t i = tid; i < slots; i += WG) {
-        const uint64_t v = S[i];
-        if (v != kEmpty) {
-            buf[atomicAdd(&bk[min((uint32_t)(v >> shift), (uint32_t)NB - 1u)], 1u)] = v;
-            S[i] = kEmpty;
+    for (uint32_t gi = blockIdx.x; gi < ng; gi += gridDim.x) {
+        const uint32_t g = glist[gi];
+        const uint32_t n = cnt[g];
+        const uint64_t T = thr[g];
+        unsigned long long *S = sets + ((uint64_t)g << set_log2);
+        if (n > maxc || (n < s && T < kMaxThr)) {         // (uniform over the workgroup)
+            if (tid == 0) status[g] = n > maxc ? ST_DOWN : ST_UP;
+            finalize_reset(S, slots, cnt + g);
+            __syncthreads();
+            continue;
         }
-    }
-    // the scatter's global stores are visible to the sorting threads of this
-    // workgroup after the barrier (same CU, device-coherent L2 path)
-    __threadfence_block();
-    __syncthreads();
-    for (uint32_t b = tid; b < NB; b += WG) {
-        const uint32_t lo = b ? bk[b - 1] : 0, hi = bk[b];
-        for (uint32_t i = lo + 1; i < hi; i++) {
-            const uint64_t v = buf[i];
-            uint32_t j = i;
-            while (j > lo && buf[j - 1] > v) { buf[j] = buf[j - 1]; j--; }
-            buf[j] = v;
+        const uint32_t tbits = 64 - __builtin_clzll(T | 1);
+        const uint32_t shift = tbits > LOGNB ? tbits - LOGNB : 0;
+        for (uint32_t i = tid; i < NB; i += WG) bk[i] = 0;
+        __syncthreads();
+        if (tid == 0) cnt[g] = 0;                          // every thread has read it
+        for (uint32_t i = tid; i < slots; i += WG) {
+            const uint64_t v = S[i];
+            if (v != kEmpty) atomicAdd(&bk[min((uint32_t)(v >> shift), (uint32_t)NB - 1u)], 1u);
         }
+        __syncthreads();
+        uint32_t loc[PER], sum = 0;
+#pragma unroll
+        for (int j = 0; j < PER; j++) { loc[j] = sum; sum += bk[tid * PER + j]; }
+        uint32_t inc = sum;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(inc, d, 64);
+            if ((tid & 63) >= d) inc += y;
+        }
+        if ((tid & 63) == 63) wsum[tid >> 6] = inc;
+        __syncthreads();
+        uint32_t base = inc - sum;
+        for (uint32_t w = 0; w < (tid >> 6); w++) base += wsum[w];
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < PER; j++) bk[tid * PER + j] = base + loc[j];
+        __syncthreads();
+        for (uint32_t i = tid; i < slots; i += WG) {
+            const uint64_t v = S[i];
+            if (v != kEmpty) {
+                buf[atomicAdd(&bk[min((uint32_t)(v >> shift), (uint32_t)NB - 1u)], 1u)] = v;
+                S[i] = kEmpty;
+            }
+        }
+        // the scatter's global stores are visible to the sorting threads of this
+        // workgroup after the barrier (same CU, device-coherent L2 path)
+        __threadfence_block();
+        __syncthreads();
+        for (uint32_t b = tid; b < NB; b += WG) {
+            const uint32_t lo = b ? bk[b - 1] : 0, hi = bk[b];
+            for (uint32_t i = lo + 1; i < hi; i++) {
+                const uint64_t v = buf[i];
+                uint32_t j = i;
+                while (j > lo && buf[j - 1] > v) { buf[j] = buf[j - 1]; j--; }
+                buf[j] = v;
+            }
+        }
+        __threadfence_block();
+        __syncthreads();
+        const uint32_t m = n < s ? n : s;
+        uint64_t *o = out + (uint64_t)g * s;
+        for (uint32_t i = tid; i < s; i += WG) o[i] = i < m ? buf[i] : kEmpty;
+        if (tid == 0) { nhash[g] = m; status[g] = ST_OK; }
+        __syncthreads();                                   // buf and bk are reused by the next genome
     }
-    __threadfence_block();
-    __syncthreads();
-    const uint32_t m = n < s ? n : s;
-    uint64_t *o = out + (uint64_t)g * s;
-    for (uint32_t i = tid; i < s; i += WG) o[i] = i < m ? buf[i] : kEmpty;
-    if (tid == 0) { nhash[g] = m; status[g] = ST_OK; }
 }
 
 __global__ void k_reset_sets(unsigned long long *__restrict__ sets, uint32_t *__restrict__ cnt,
@@ -790,14 +798,16 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
             }
             timing_mark(ctx, 0, st, false);
         }
-        uint64_t *d_gbuf = nullptr;                       // the global finalize's sort buffers
+        uint64_t *d_gbuf = nullptr;                       // the global finalize's sort buffers (bounded)
+        const uint32_t gslices = std::min<uint32_t>((uint32_t)todo.size(), kFinGlobalSlices);
         if (s > kLdsSortSketch &&
-            (rc = scratch(ctx, "sk_gbuf", (uint64_t)todo.size() * plan.maxc * 8ull, (void **)&d_gbuf)))
+            (rc = scratch(ctx, "sk_gbuf", (uint64_t)gslices * plan.maxc * 8ull, (void **)&d_gbuf)))
             return rc;
         timing_mark(ctx, 1, st, true);
         if (s > kLdsSortSketch)
-            hipLaunchKernelGGL((k_sketch_finalize_global<16384>), dim3((uint32_t)todo.size()), dim3(1024), 0, st,
-                               d_sets, d_cnt, thr_p, gl_p, plan.set_log2, plan.maxc, s, d_hashes, d_nhash, d_st, d_gbuf);
+            hipLaunchKernelGGL((k_sketch_finalize_global<16384>), dim3(gslices), dim3(1024), 0, st,
+                               d_sets, d_cnt, thr_p, gl_p, (uint32_t)todo.size(), plan.set_log2, plan.maxc, s,
+                               d_hashes, d_nhash, d_st, d_gbuf);
         else if (plan.maxc <= 4096)
             hipLaunchKernelGGL((k_sketch_finalize_bucket<4096, 4096>), dim3((uint32_t)todo.size()), dim3(1024), 0, st,
                                d_sets, d_cnt, thr_p, gl_p, plan.set_log2, plan.maxc, s, d_hashes, d_nhash, d_st);

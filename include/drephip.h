@@ -49,6 +49,12 @@ typedef struct drephip_ctx drephip_ctx;
 /* Library/ABI version (major*10000 + minor*100 + patch). */
 int drephip_version(void);
 
+/* Build identity: "src=<sha256 of the library's sources>;arch=gfx950;extra=<A/B
+ * build flags>" -- the digest is computed by drep_amd/csrc/Makefile over
+ * include/drephip.h and drep_amd/csrc/ (drep_amd/_lib.py:source_digest restates
+ * it), so a caller can prove which sources the loaded library was built from. */
+const char *drephip_build_id(void);
+
 /* Last error message of the calling thread ("" if none). */
 const char *drephip_last_error(void);
 
