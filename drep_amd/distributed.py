@@ -39,7 +39,8 @@ from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from .parallel import cond_start, gather_sketches, genome_shard, row_partition, segment_size
+from .parallel import (balanced_shards, cond_start, gather_sketches, genome_shard, row_partition, segment_size,
+                       shard_layout)
 
 
 @dataclass
@@ -47,19 +48,35 @@ class ShardPlan:
     N: int
     world: int
     rank: int
-    g0: int          # this rank's genomes [g0, g1), padded shard size nmax
+    g0: int          # contiguous shards: this rank's genomes [g0, g1) (balanced shards: -1)
     g1: int
-    nmax: int
+    nmax: int        # padded shard size (every rank's all-gather chunk)
     r0: int          # this rank's triangle rows [r0, r1)
     r1: int
     seg0: int        # condensed index of the segment's first pair
     seg_len: int
+    members: Optional[np.ndarray] = None    # this rank's genome indices, ascending (= arange(g0, g1) if contiguous)
+    pos: Optional[np.ndarray] = None        # balanced shards: gathered row of every genome (None: identity)
+
+    def genomes(self) -> np.ndarray:
+        return self.members if self.members is not None else np.arange(self.g0, self.g1)
 
 
-def plan(N: int, world: int, rank: int) -> ShardPlan:
-    g0, g1, nmax = genome_shard(N, world, rank)
+def plan(N: int, world: int, rank: int, weights: Optional[Sequence[float]] = None) -> ShardPlan:
+    """This rank's share of the job.  Without weights the genome shards are
+    contiguous and of equal count (synthetic genomes of one length); with
+    weights (the FASTA inputs' sizes) they are balanced by weight
+    (parallel.balanced_shards) and padded to the largest shard for the
+    all-gather, whose rows run_sharded then puts back in genome order."""
     r0, r1 = row_partition(N, world)[rank]
-    return ShardPlan(N, world, rank, g0, g1, nmax, r0, r1, cond_start(r0, N), segment_size(N, r0, r1))
+    if weights is None:
+        g0, g1, nmax = genome_shard(N, world, rank)
+        return ShardPlan(N, world, rank, g0, g1, nmax, r0, r1, cond_start(r0, N), segment_size(N, r0, r1),
+                         members=np.arange(g0, g1))
+    shards = balanced_shards(weights, world)
+    nmax, pos = shard_layout(shards, N)
+    return ShardPlan(N, world, rank, -1, -1, nmax, r0, r1, cond_start(r0, N), segment_size(N, r0, r1),
+                     members=shards[rank], pos=pos)
 
 
 def gather_segments(seg, N: int, root: int = 0, out=None):
@@ -124,19 +141,20 @@ LinkageFn = Callable[["object", Optional["object"], int, str], np.ndarray]
 
 def run_sharded(N: int, names: Sequence[str], s: int, sketch_fn: SketchFn, allpairs_fn: AllpairsFn,
                 linkage_fn: LinkageFn, method: str = "average", P_ani: float = 0.9, root: int = 0,
-                sync: Optional[Callable[[], None]] = None) -> Dict:
+                sync: Optional[Callable[[], None]] = None, weights: Optional[Sequence[float]] = None) -> Dict:
     """The sharded pipeline on this rank (torch.distributed initialised).
 
     Returns, on the root, {'Cdb', 'linkage', 'arguments', 'common', 'denom',
     'hashes', 'nhash', 'times'}; on the other ranks {'times'}.  `sync` waits
     for this rank's device work (torch.cuda.synchronize on GPU ranks) so the
-    stage times are real."""
+    stage times are real.  `weights` (per genome, e.g. FASTA sizes) balances
+    the sketch shards by work instead of by count (plan())."""
     import torch
     import torch.distributed as dist
     import scipy.cluster.hierarchy as sch
     from .d_cluster import _primary_cdb
     world, rank = dist.get_world_size(), dist.get_rank()
-    p = plan(N, world, rank)
+    p = plan(N, world, rank, weights)
     sync = sync or (lambda: None)
     times: Dict[str, float] = {}
 
@@ -152,7 +170,11 @@ def run_sharded(N: int, names: Sequence[str], s: int, sketch_fn: SketchFn, allpa
 
     loc_h, loc_n = stage("sketch_s", lambda: sketch_fn(p))
     H, NH = stage("allgather_s", lambda: gather_sketches(loc_h, loc_n))
-    H, NH = H[:N], NH[:N]
+    if p.pos is None:
+        H, NH = H[:N], NH[:N]
+    else:                                    # balanced shards: gathered rows back to genome order
+        idx = torch.from_numpy(p.pos).to(H.device)
+        H, NH = H[idx].contiguous(), NH[idx].contiguous()
     partial = bool((NH < s).any().item()) if N else False
     # the root's rows are written straight into its slice of the full condensed
     # vector, so gathering the segments copies nothing on the root (at 10^5
@@ -240,25 +262,26 @@ def hip_file_sketcher(ctx, paths: Sequence[str], threads: int, device, cached: O
         s = ctx.s
         loc_h = torch.full((p.nmax, s), -1, dtype=torch.int64, device=device)
         loc_n = torch.zeros(p.nmax, dtype=torch.int32, device=device)
-        n = p.g1 - p.g0
+        mine = p.genomes()
+        n = len(mine)
         if n <= 0:
             return loc_h, loc_n
         h = np.full((n, s), np.iinfo(np.uint64).max, dtype=np.uint64)
         nh = np.zeros(n, dtype=np.uint32)
         ln = np.zeros(n, dtype=np.uint64)
-        todo = [i for i in range(n) if p.g0 + i not in cached]
+        todo = [i for i in range(n) if int(mine[i]) not in cached]
         for i in range(n):
-            ref = cached.get(p.g0 + i)
+            ref = cached.get(int(mine[i]))
             if ref is not None:
                 m = min(len(ref.hashes), s)
                 h[i, :m] = ref.hashes[:m]
                 nh[i] = m
                 ln[i] = ref.length
         if todo:
-            th, tnh, tln = ctx.sketch_files([paths[p.g0 + i] for i in todo], threads=threads)
+            th, tnh, tln = ctx.sketch_files([paths[int(mine[i])] for i in todo], threads=threads)
             h[todo], nh[todo], ln[todo] = th, tnh, tln
         if lengths is not None:
-            lengths[p.g0:p.g1] = ln
+            lengths[mine] = ln
         loc_h[:n] = torch.from_numpy(h.view(np.int64)).to(device)
         loc_n[:n] = torch.from_numpy(nh.view(np.int32)).to(device)
         return loc_h, loc_n
@@ -284,6 +307,29 @@ def read_genome_list(bdb: Optional[str] = None, files: Optional[str] = None) -> 
         if line and line not in locs:
             locs.append(line)
     return [_get_genome_name_from_fasta(x) for x in locs], locs
+
+
+def file_weights(locations: Sequence[str], cached: Optional[Dict[int, object]] = None) -> np.ndarray:
+    """Sketch work per genome for balanced_shards: the FASTA's bases as far as
+    they are known without reading it -- the file size, or for a gzip file the
+    uncompressed size its trailer records (ISIZE: exact for the usual
+    single-member file) -- and 0 for a genome whose sketch is cached."""
+    cached = cached or {}
+    w = np.zeros(len(locations), dtype=np.float64)
+    for i, loc in enumerate(locations):
+        if i in cached:
+            continue
+        try:
+            size = os.path.getsize(loc)
+            if loc.endswith(".gz") and size >= 18:
+                with open(loc, "rb") as f:
+                    f.seek(-4, os.SEEK_END)
+                    isize = int.from_bytes(f.read(4), "little")
+                size = max(size, isize)
+        except OSError:
+            size = 0                     # unreadable: the sketch stage reports it
+        w[i] = size
+    return w
 
 
 def cached_sketches(data_folder: str, names: Sequence[str], s: int, group_size: int = 1000) -> Dict[int, object]:
@@ -425,11 +471,13 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
         lengths = np.zeros(N, dtype=np.uint64)
         cached = cached_sketches(a.data_folder, names, a.sketch, a.group_size) if a.data_folder else {}
         sketch_fn = hip_file_sketcher(ctx, locations, a.processors, dev, cached, lengths)
+        weights = file_weights(locations, cached)
     else:
         N = a.genomes
         names = locations = synthetic_names(N)
         lengths = np.full(N, a.genome_bp, np.uint64)
         sketch_fn = hip_synth_sketcher(ctx, a.genome_bp, a.family_size, a.seed, stream, dev)
+        weights = None                                   # one length: contiguous equal shards
     # the root's n x n linkage matrix (80 GB at 10^5: ~2 s of hipMalloc) is
     # allocated by a separate context on a helper thread while the sketch and
     # all-pairs stages run, so the serial clustering tail does not pay for it
@@ -448,7 +496,7 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
             res_wait["reserve_wait_s"] = time.perf_counter() - t0
             return inner(*args)
     res = run_sharded(N, names, a.sketch, sketch_fn, hip_allpairs(ctx, stream, dev), linkage_fn,
-                      a.method, a.P_ani, sync=lambda: torch.cuda.synchronize(dev))
+                      a.method, a.P_ani, sync=lambda: torch.cuda.synchronize(dev), weights=weights)
     if from_files and world > 1:
         # every rank filled its shard's lengths: the root takes the element-wise max
         allv = [None] * world
@@ -461,6 +509,9 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
                "backend": backend, "method": a.method, "P_ani": a.P_ani, "times": res["times"],
                "pairs": N * (N - 1) // 2, "primary_clusters": int(res["Cdb"]["primary_cluster"].nunique())}
         out.update(res_wait)
+        if weights is not None:          # the sketch shards' work (file bytes) per rank
+            out["shard_weights"] = [float(weights[m].sum()) for m in balanced_shards(weights, world)]
+            out["shard_genomes"] = [int(len(m)) for m in balanced_shards(weights, world)]
         out["linkage_phases_s"] = link_ctx.linkage_stats()
         t = res["times"]
         out["pairs_per_s_job"] = out["pairs"] / sum(v for k, v in t.items())

@@ -4,8 +4,9 @@ The reference runs everything in one process (mash dist -p threads,
 d_cluster.py:570); it has no distributed code.  On a node of MI355X the step
 splits as:
 
-* sketch: genome shards (contiguous, equal count) -- each rank sketches its
-  own genomes;
+* sketch: genome shards -- contiguous and of equal count for synthetic
+  genomes of one length, balanced by file size (balanced_shards) for FASTA
+  inputs -- each rank sketches its own genomes;
 * exchange: ONE collective, an all-gather of the uint64[N/W][s] sketch shards
   and their nhash counts (RCCL over xGMI with the "nccl" backend; gloo on CPU
   in the tests);
@@ -27,6 +28,40 @@ def genome_shard(N: int, world: int, rank: int) -> Tuple[int, int, int]:
     g0 = min(N, rank * nmax)
     g1 = min(N, g0 + nmax)
     return g0, g1, nmax
+
+
+def balanced_shards(weights: Sequence[float], world: int) -> List[np.ndarray]:
+    """Genome shards balanced by work ("greedily by total
+    bases"): genomes in decreasing weight order, each to the rank with the
+    least total so far (ties: the lowest rank), i.e. LPT list scheduling.
+    Every rank's total is then within one genome's weight of every other's
+    (the rank that ends heaviest was the lightest when it took its last
+    genome).  Returns each rank's genome indices, ascending.  The reference
+    fans the genomes out over a thread pool in Bdb order
+    (drep/d_cluster.py:527-549), where no balance is needed."""
+    import heapq
+    w = np.asarray(weights, dtype=np.float64)
+    order = np.argsort(-w, kind="stable")
+    heap = [(0.0, r) for r in range(world)]
+    heapq.heapify(heap)
+    members: List[List[int]] = [[] for _ in range(world)]
+    for g in order:
+        tot, r = heapq.heappop(heap)
+        members[r].append(int(g))
+        heapq.heappush(heap, (tot + float(w[g]), r))
+    return [np.sort(np.asarray(m, dtype=np.int64)) for m in members]
+
+
+def shard_layout(shards: Sequence[np.ndarray], N: int) -> Tuple[int, np.ndarray]:
+    """(nmax, pos) for an all-gather of shards padded to nmax rows: genome g
+    lands at gathered row pos[g] = rank * nmax + (its slot in the shard)."""
+    nmax = max(1, max(len(m) for m in shards))
+    pos = np.full(N, -1, dtype=np.int64)
+    for r, m in enumerate(shards):
+        pos[m] = r * nmax + np.arange(len(m))
+    if (pos < 0).any():
+        raise ValueError("the shards do not cover every genome")
+    return nmax, pos
 
 
 def cond_start(i: int, N: int) -> int:

@@ -47,7 +47,9 @@ def test_sharded_job_matches_single_rank(tmp_path):
     assert np.array_equal(cm1.nhash, nh)
     want, _ = oracle.allpairs(h, nh, 1000, r0=0, r1=12, threads=8)
     assert np.array_equal(cm1.common[:len(want)], want)
-    for world, port in ((2, 29621), (3, 29631)):
+    # world 8 as the driver's 8-GPU run has it (8 gloo ranks sharing this GPU):
+    # every partition edge of row_partition / genome_shard at 8 ranks
+    for world, port in ((2, 29621), (3, 29631), (8, 29711)):
         res = _run(world, str(tmp_path / ("w%d" % world)), port)
         assert res["n_gpus"] == world
         cm = load_condensed(str(tmp_path / ("w%d" % world)), mmap=False)
@@ -169,3 +171,60 @@ def test_sharded_job_on_files_matches_drop_in(tmp_path):
         assert np.array_equal(pl["linkage"], Z)
         assert np.array_equal(cdb["primary_cluster"].to_numpy(), Cdb["primary_cluster"].to_numpy())
         assert list(cdb["genome"]) == list(Cdb["genome"])
+
+
+def _uneven_file_set(tmp_path):
+    """FASTAs of very different lengths: each reference genome alone and
+    concatenated with 1-3 others as one multi-record file (~2.5-12 Mbp)."""
+    import gzip
+    golden = os.path.join(ROOT, "tests", "golden", "genomes")
+    fas = sorted(os.listdir(golden))
+    raw = [gzip.open(os.path.join(golden, f)).read() for f in fas]
+    gdir = tmp_path / "uneven"
+    gdir.mkdir()
+    locs = []
+    for k in range(10):
+        parts = [raw[(k + j) % len(raw)] for j in range(1 + (k * 7) % 4)]
+        dst = gdir / ("u%02d.fna" % k)
+        dst.write_bytes(b"".join(p if p.endswith(b"\n") else p + b"\n" for p in parts))
+        locs.append(str(dst))
+    return locs
+
+
+@pytest.mark.timeout(600)
+def test_sharded_job_balanced_file_shards_match_drop_in(tmp_path):
+    """--files with genomes of very different lengths: the sketch shards are
+    balanced by file size (parallel.balanced_shards), the
+    per-rank byte totals within one file of each other, and the stored names,
+    counts, lengths, Z and Cdb equal the single-process drop-in's
+    (reference: d_cluster.py:527-549 sketch fan-out, 170-185 clustering)."""
+    from drep_amd.d_cluster import all_vs_all_MASH_condensed, cluster_mash_condensed
+    locs = _uneven_file_set(tmp_path)
+    sizes = [os.path.getsize(x) for x in locs]
+    assert max(sizes) > 3 * min(sizes)
+    lst = tmp_path / "uneven.txt"
+    lst.write_text("\n".join(locs) + "\n")
+    Bdb = pd.DataFrame({"genome": [os.path.basename(x) for x in locs], "location": locs})
+    wd = tmp_path / "wd_single"
+    wd.mkdir()
+    cm = all_vs_all_MASH_condensed(Bdb, str(wd), processors=4)
+    Cdb, (Z, _, _) = cluster_mash_condensed(cm, clusterAlg="average", P_ani=0.9)
+    for world, port in ((3, 29721), (2, 29731)):
+        out = str(tmp_path / ("uout%d" % world))
+        env = dict(os.environ, DREPHIP_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+               "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "drep_amd.distributed",
+               "--files", str(lst), "--processors", "4", "--out", out]
+        p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0, p.stderr[-3000:]
+        res = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+        w = res["shard_weights"]
+        assert len(w) == world and max(w) - min(w) <= max(sizes)
+        got = load_condensed(out, mmap=False)
+        assert got.names == cm.names and got.locations == cm.locations
+        assert np.array_equal(got.common, cm.common) and np.array_equal(got.nhash, cm.nhash)
+        assert np.array_equal(got.length, cm.length)
+        assert np.array_equal(load_primary_linkage(out)["linkage"], Z)
+        cdb = pd.read_csv(os.path.join(out, "primary_Cdb.csv"))
+        assert list(cdb["genome"]) == list(Cdb["genome"])
+        assert np.array_equal(cdb["primary_cluster"].to_numpy(), Cdb["primary_cluster"].to_numpy())

@@ -182,3 +182,128 @@ def test_shard_plan_covers_everything():
             assert sum(p.g1 - p.g0 for p in ps) == N
             for a, b in zip(ps[:-1], ps[1:]):
                 assert a.seg0 + a.seg_len == b.seg0 or b.seg_len == 0
+
+
+def test_balanced_shards_by_weight():
+    """sketch shards balanced greedily by bases; every rank's
+    total within one genome's weight of every other's, every genome once."""
+    rng = np.random.default_rng(5)
+    for N in (1, 5, 29, 1000):
+        for W in (1, 2, 3, 8):
+            w = rng.integers(1, 10_000_000, N).astype(np.float64)
+            w[rng.random(N) < 0.1] = 0            # cached sketches weigh nothing
+            sh = parallel.balanced_shards(w, W)
+            got = np.sort(np.concatenate(sh))
+            assert np.array_equal(got, np.arange(N))
+            tot = np.array([w[m].sum() for m in sh])
+            assert tot.max() - tot.min() <= w.max()
+            nmax, pos = parallel.shard_layout(sh, N)
+            assert nmax == max(1, max(len(m) for m in sh))
+            for r, m in enumerate(sh):
+                assert np.array_equal(pos[m], r * nmax + np.arange(len(m)))
+
+
+def _len_of(g):
+    # genome lengths spread over 20x (5 kbp .. 100 kbp): a count split would be badly unbalanced
+    return 5_000 + (g * 37_813) % 95_000
+
+
+def _worker_weighted(rank, world, port, N, out_dir):
+    """run_sharded with balanced shards (weights = genome lengths): each rank
+    sketches a non-contiguous set of genomes; the gathered rows must come back
+    in genome order."""
+    import torch
+    import torch.distributed as dist
+    import oracle
+    from drep_amd import distributed as D
+    from drep_amd.d_cluster import CondensedMash, cluster_mash_condensed
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    names = D.synthetic_names(N)
+    weights = [float(_len_of(g)) for g in range(N)]
+
+    def sketch_fn(p):
+        assert p.pos is not None and p.g0 == -1
+        loc_h = torch.full((p.nmax, S), -1, dtype=torch.int64)
+        loc_n = torch.zeros(p.nmax, dtype=torch.int32)
+        for j, g in enumerate(p.genomes()):
+            h, nh = oracle.sketch_synth(int(g), 1, _len_of(int(g)), seed=4, family_size=5, s=S, threads=1)
+            loc_h[j] = torch.from_numpy(h[0].view(np.int64))
+            loc_n[j] = int(nh[0])
+        np.save(os.path.join(out_dir, "members%d.npy" % rank), p.genomes())
+        return loc_h, loc_n
+
+    def allpairs_fn(H, NH, p, out=None):
+        Hn = H.numpy().view(np.uint64)
+        Nn = NH.numpy().view(np.uint32)
+        if not p.seg_len:
+            return torch.zeros(1, dtype=torch.int16), torch.zeros(1, dtype=torch.int16)
+        c, d = oracle.allpairs(Hn, Nn, S, r0=p.r0, r1=min(p.r1, N - 1), threads=1)
+        return (torch.from_numpy(c[:p.seg_len].view(np.int16).copy()),
+                torch.from_numpy(d[:p.seg_len].view(np.int16).copy()))
+
+    def linkage_fn(common, denom, n, method):
+        c = common.numpy().view(np.uint16)
+        d = denom.numpy().view(np.uint16) if denom is not None else np.full(len(c), S, np.uint16)
+        cm = CondensedMash(names, names, c, d, np.zeros(n, np.uint32), np.zeros(n, np.uint64), S)
+        _, (Z, _, _) = cluster_mash_condensed(cm, clusterAlg=method)
+        return Z
+
+    res = D.run_sharded(N, names, S, sketch_fn, allpairs_fn, linkage_fn, "average", 0.9, weights=weights)
+    if rank == 0:
+        np.save(os.path.join(out_dir, "Z.npy"), res["linkage"])
+        np.save(os.path.join(out_dir, "common.npy"), res["common"].numpy().view(np.uint16))
+        np.save(os.path.join(out_dir, "H.npy"), res["hashes"].numpy().view(np.uint64))
+        res["Cdb"].to_csv(os.path.join(out_dir, "Cdb.csv"), index=False)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_balanced_shards_match_single_process(tmp_path, world):
+    """Genomes of very different lengths, sketch shards balanced by length:
+    per-rank totals within one genome of each other; the root's sketch matrix
+    (genome order), counts, Z and Cdb equal the single-process result."""
+    import pandas as pd
+    import torch.multiprocessing as mp
+    import oracle
+    from drep_amd import distributed as D
+    from drep_amd.d_cluster import CondensedMash, cluster_mash_condensed
+    N = 31
+    port = _free_port()
+    mp.start_processes(_worker_weighted, args=(world, port, N, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    mem = [np.load(os.path.join(tmp_path, "members%d.npy" % r)) for r in range(world)]
+    lens = np.array([_len_of(g) for g in range(N)])
+    tot = [lens[m].sum() for m in mem]
+    assert max(tot) - min(tot) <= lens.max()
+    assert not all(np.array_equal(m, np.arange(m[0], m[-1] + 1)) for m in mem if len(m))   # not contiguous
+    h = np.full((N, S), np.iinfo(np.uint64).max, dtype=np.uint64)
+    nh = np.zeros(N, dtype=np.uint32)
+    for g in range(N):
+        hg, ng = oracle.sketch_synth(g, 1, _len_of(g), seed=4, family_size=5, s=S, threads=1)
+        h[g], nh[g] = hg[0], ng[0]
+    assert np.array_equal(np.load(os.path.join(tmp_path, "H.npy")), h)
+    want_c, want_d = oracle.allpairs(h, nh, S)
+    assert np.array_equal(np.load(os.path.join(tmp_path, "common.npy")), want_c)
+    names = D.synthetic_names(N)
+    cm = CondensedMash(names, names, want_c, want_d, nh, np.zeros(N, np.uint64), S)
+    cdb, (Z, _, _) = cluster_mash_condensed(cm, clusterAlg="average", P_ani=0.9)
+    assert np.array_equal(np.load(os.path.join(tmp_path, "Z.npy")), Z)
+    got = pd.read_csv(os.path.join(tmp_path, "Cdb.csv"))
+    assert got["genome"].tolist() == cdb["genome"].tolist()
+    assert got["primary_cluster"].tolist() == cdb["primary_cluster"].tolist()
+
+
+def test_file_weights(tmp_path):
+    import gzip
+    from drep_amd import distributed as D
+    a = tmp_path / "a.fa"
+    a.write_bytes(b">x\n" + b"ACGT" * 1000 + b"\n")
+    b = tmp_path / "b.fa.gz"
+    with gzip.open(b, "wb") as f:
+        f.write(b">y\n" + b"A" * 50_000 + b"\n")
+    w = D.file_weights([str(a), str(b), str(tmp_path / "missing.fa"), str(a)], cached={3: object()})
+    assert w[0] == os.path.getsize(a)
+    assert w[1] == 50_000 + 4               # the gzip trailer's uncompressed size
+    assert w[2] == 0 and w[3] == 0           # unreadable; cached

@@ -1,0 +1,223 @@
+"""Host model of the GPU nearest-neighbour chain's launch protocol
+(drep_amd/csrc/linkage.hip, k_nn_step) -- a design tool, not product code.
+
+The GPU chain makes scipy's nn_chain decisions (drep/d_cluster.py:447-453 ->
+scipy.cluster.hierarchy.linkage) at the START of each launch from the row
+minima ("partials") the previous launch reduced: P1 = the chain top's row,
+P2 = the merged row or a speculated merged row, P3 = a speculated row of the
+element below.  This script replays that protocol on the host with numpy on a
+dense n x n float64 matrix, so a change of protocol can be judged by two
+numbers before any kernel is written: the launch count, and whether Z is
+still bit-identical to scipy's.
+
+  python tools/chain_sim.py <common.npy> [--policy r4|r5] [--n N]
+
+<common.npy>: the condensed shared-hash counts (uint16, s = 1000, every sketch
+full) of the configs workload, e.g. from oracle.sketch_synth + oracle.allpairs.
+"""
+import argparse
+import sys
+import time
+
+import numpy as np
+
+INF = np.inf
+
+
+class Sim:
+    def __init__(self, D, policy="r4"):
+        self.D = D
+        self.n = n = D.shape[0]
+        self.size = np.ones(n, dtype=np.int64)
+        self.chain = [0]
+        self.Z = []
+        self.policy = policy
+        self.stats = dict(launches=0, twice=0, scans=0, specwin=0, m0=0, double=0, merges=0)
+
+    # ---- row minima (smallest index among equal minima, as the GPU's argmin)
+    def rowmin(self, vals, mask):
+        v = np.where(mask, vals, INF)
+        i = int(np.argmin(v))
+        return (float(v[i]), i) if v[i] < INF else (INF, -1)
+
+    def active(self):
+        return self.size > 0
+
+    def lw(self, dx, dy, nx, ny):       # average linkage, scipy's rounding
+        return (nx * dx + ny * dy) / float(nx + ny)
+
+    def apply_merge(self, a, b):
+        """scipy: x = a < y = b; new row/column b, size[a] = 0"""
+        D, size = self.D, self.size
+        na, nb = size[a], size[b]
+        act = self.active().copy()
+        act[a] = act[b] = False
+        u = self.lw(D[a], D[b], float(na), float(nb))
+        D[b, act] = u[act]
+        D[act, b] = u[act]
+        size[a] = 0
+        size[b] = na + nb
+
+    def p1(self, t):
+        m = self.active().copy()
+        m[t] = False
+        return self.rowmin(self.D[t], m)
+
+    def spec_rows(self, t, sb, w):
+        """the row U = LW(D[t], D[sb]) would form (index max(t, sb)) and w's row
+        after that merge: their minima (P2, P3)"""
+        D, size = self.D, self.size
+        x, y = min(t, sb), max(t, sb)
+        m = self.active().copy()
+        m[t] = m[sb] = False
+        U = self.lw(D[x], D[y], float(size[x]), float(size[y]))
+        p2 = self.rowmin(U, m)
+        mw = m.copy()
+        mw[w] = False
+        vw = np.where(mw, D[w], INF)
+        iw = int(np.argmin(vw))
+        best = (float(vw[iw]), iw) if vw[iw] < INF else (INF, 1 << 30)
+        cand = (float(U[w]), y)
+        if cand[0] < best[0] or (cand[0] == best[0] and cand[1] < best[1]):
+            best = cand
+        return p2, best
+
+    def run(self):
+        n, D, st = self.n, self.D, self.stats
+        chain = self.chain
+        decide = False
+        P1 = P2 = P3 = None
+        mrow = -1
+        spec = 0
+        k = 0
+        while k < n - 1:
+            st["launches"] += 1
+            pend = None
+            # ---- decisions at the start of the launch
+            if decide:
+                r = P1
+                for d in range(2):
+                    top = chain[-1]
+                    below = chain[-2] if len(chain) > 1 else -1
+                    dp = D[top, below] if below >= 0 else INF
+                    if len(chain) > 1 and not (r[0] < dp):
+                        a, b = min(top, below), max(top, below)
+                        self.Z.append((a, b, dp, self.size[a] + self.size[b]))
+                        pend = (a, b)
+                        k += 1
+                        chain.pop(); chain.pop()
+                        if not chain and k < n - 1:
+                            act = self.active()
+                            f = next(i for i in range(n) if i == b or (i != a and act[i]))
+                            chain.append(f)
+                        elif d == 0 and spec and chain and k < n - 1:
+                            r3 = P3
+                            L = len(chain)
+                            dp2 = D[chain[-1], chain[-2]] if L > 1 else INF
+                            wpush = r3[1] >= 0 and not (L > 1 and not (r3[0] < dp2))
+                            bpush = r3[1] == b and P2[1] >= 0 and P2[0] < r3[0]
+                            if wpush and (r3[1] != b or bpush):
+                                chain.append(r3[1])
+                                st["specwin"] += 1
+                                if bpush:
+                                    chain.append(P2[1])
+                        break
+                    chain.append(r[1])
+                    if r[1] != mrow or mrow < 0 or d == 1:
+                        break
+                    r = P2
+                    st["twice"] += 1
+            decide = True
+            if k >= n - 1:
+                break
+            # ---- the launch's work: apply the merge, reduce the rows
+            if pend:
+                self.apply_merge(*pend)
+                st["merges"] += 1
+            else:
+                st["scans"] += 1
+            mrow = pend[1] if pend else -1
+            t = chain[-1]
+            L = len(chain)
+            P1 = self.p1(t)
+            spec = 0
+            if L >= 3:
+                if not pend:
+                    spec = 1
+                elif chain[-2] == pend[1] and t != pend[1]:
+                    spec = 2
+            if spec:
+                P2, P3 = self.spec_rows(t, chain[-2], chain[-3])
+            elif pend:
+                st["m0"] += 1
+                y = pend[1]
+                m = self.active().copy()
+                m[y] = False
+                P2 = self.rowmin(D[y], m)
+        return self.finish()
+
+    def finish(self):
+        n = self.n
+        Z = np.array(self.Z, dtype=np.float64)
+        Z = Z[np.argsort(Z[:, 2], kind="mergesort")]
+        parent = np.arange(2 * n - 1)
+        sz = np.ones(2 * n - 1, dtype=np.int64)
+
+        def find(x):
+            while parent[x] != x:
+                parent[x] = parent[parent[x]]
+                x = parent[x]
+            return x
+        for i in range(n - 1):
+            x, y = find(int(Z[i, 0])), find(int(Z[i, 1]))
+            Z[i, 0], Z[i, 1] = min(x, y), max(x, y)
+            parent[x] = parent[y] = n + i
+            sz[n + i] = sz[x] + sz[y]
+            Z[i, 3] = sz[n + i]
+        return Z
+
+
+def dense_from_counts(common, n, s=1000):
+    sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
+    from drep_amd.d_cluster import linkage_tables
+    lut, _ = linkage_tables(np.array([s]), s)
+    D = np.zeros((n, n))
+    iu = np.triu_indices(n, 1)
+    D[iu] = lut[common]
+    D.T[iu] = lut[common]
+    return D, lut[common]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("counts")
+    ap.add_argument("--policy", default="r4")
+    ap.add_argument("--n", type=int, default=0)
+    ap.add_argument("--scipy", action="store_true")
+    a = ap.parse_args()
+    c = np.load(a.counts)
+    n = int(round((1 + (1 + 8 * len(c)) ** 0.5) / 2))
+    if a.n:
+        # leading n x n block of the condensed triangle
+        idx = np.concatenate([np.arange(i * n - i * (i + 1) // 2, i * n - i * (i + 1) // 2 + a.n - i - 1)
+                              for i in range(a.n - 1)])
+        n0 = n
+        idx = np.concatenate([np.arange(i * n0 - i * (i + 1) // 2, i * n0 - i * (i + 1) // 2 + (a.n - i - 1))
+                              for i in range(a.n - 1)])
+        c = c[idx]
+        n = a.n
+    D, y = dense_from_counts(c, n)
+    t0 = time.time()
+    sim = Sim(D, a.policy)
+    Z = sim.run()
+    out = dict(n=n, policy=a.policy, sim_s=round(time.time() - t0, 1), **sim.stats)
+    out["launches_per_merge"] = sim.stats["launches"] / (n - 1)
+    if a.scipy:
+        import scipy.cluster.hierarchy as sch
+        Zs = sch.linkage(y, method="average")
+        out["Z_identical_to_scipy"] = bool(np.array_equal(Z, Zs))
+    print(out)
+
+
+if __name__ == "__main__":
+    main()
