@@ -32,7 +32,9 @@ class Sim:
         self.chain = [0]
         self.Z = []
         self.policy = policy
-        self.stats = dict(launches=0, twice=0, scans=0, specwin=0, m0=0, double=0, merges=0)
+        self.stats = dict(launches=0, twice=0, scans=0, specwin=0, m0=0, merges=0, w_merge=0, w_recip=0,
+                          known_merges=0, known_spec=0,
+                          rows_known_at_start=0, rows_known_after_partials=0, rows_known_after_decision=0)
 
     # ---- row minima (smallest index among equal minima, as the GPU's argmin)
     def rowmin(self, vals, mask):
@@ -90,11 +92,49 @@ class Sim:
         mrow = -1
         spec = 0
         k = 0
+        known = None
         while k < n - 1:
             st["launches"] += 1
             pend = None
+            prev_known, known = known, None
+            # rows a launch could start loading before its decision: those the
+            # state names (top, below and the two under them), and those the
+            # previous launch's partials name (their argmins)
+            cand0 = set(chain[-4:])
+            cand1 = cand0 | {r[1] for r in (P1, P2, P3) if r is not None and r[1] >= 0}
             # ---- decisions at the start of the launch
-            if decide:
+            if decide and prev_known:
+                # the previous launch knew this launch's first decision (a merge of
+                # the top with the element below) and speculated on it: no P1 needed
+                top, below = chain[-1], chain[-2]
+                a, b = min(top, below), max(top, below)
+                self.Z.append((a, b, D[top, below], self.size[a] + self.size[b]))
+                pend = (a, b)
+                k += 1
+                chain.pop(); chain.pop()
+                st["known_merges"] += 1
+                if not chain and k < n - 1:
+                    act = self.active()
+                    chain.append(next(i for i in range(n) if i == b or (i != a and act[i])))
+                elif chain and k < n - 1:
+                    r3 = P3
+                    L = len(chain)
+                    dp2 = D[chain[-1], chain[-2]] if L > 1 else INF
+                    wpush = r3[1] >= 0 and not (L > 1 and not (r3[0] < dp2))
+                    bpush = r3[1] == b and P2[1] >= 0 and P2[0] < r3[0]
+                    if wpush and (r3[1] != b or bpush):
+                        chain.append(r3[1])
+                        st["specwin"] += 1
+                        if bpush:
+                            chain.append(P2[1])
+                    elif r3[1] >= 0 and not wpush:
+                        st["w_merge"] += 1
+                        known = "wmerge"
+                    elif wpush and r3[1] == b:
+                        st["w_recip"] += 1
+                        chain.append(b)
+                        known = "recip"
+            elif decide:
                 r = P1
                 for d in range(2):
                     top = chain[-1]
@@ -121,6 +161,15 @@ class Sim:
                                 st["specwin"] += 1
                                 if bpush:
                                     chain.append(P2[1])
+                            elif r3[1] >= 0 and not wpush:
+                                st["w_merge"] += 1          # w's decision: merge with the element below it
+                                if self.policy == "r5":
+                                    known = "wmerge"
+                            elif wpush and r3[1] == b:
+                                st["w_recip"] += 1          # w pushes b, b merges back with w
+                                if self.policy == "r5":
+                                    chain.append(b)
+                                    known = "recip"
                         break
                     chain.append(r[1])
                     if r[1] != mrow or mrow < 0 or d == 1:
@@ -141,6 +190,32 @@ class Sim:
             L = len(chain)
             P1 = self.p1(t)
             spec = 0
+            need = set(pend) if pend else set()
+            if known:
+                need |= set(chain[-3:])
+            else:
+                need.add(t)
+                if L >= 3 and (not pend or (chain[-2] == pend[1] and t != pend[1])):
+                    need |= set(chain[-3:])
+            need.discard(pend[1] if pend else -1)   # (the merged row is computed, not loaded, where it is spec'd)
+            if pend:
+                need.add(pend[0]); need.add(pend[1])
+            if need <= cand0:
+                st["rows_known_at_start"] += 1
+            elif need <= cand1:
+                st["rows_known_after_partials"] += 1
+            else:
+                st["rows_known_after_decision"] += 1
+            if known:
+                # the next decision is a known merge of the top with the element
+                # below: speculate on it (its merged row P2, the row below P3)
+                # instead of searching the top's row
+                if L >= 3:
+                    P2, P3 = self.spec_rows(t, chain[-2], chain[-3])
+                else:
+                    P2, P3 = (INF, -1), (INF, -1)
+                st["known_spec"] += 1
+                continue
             if L >= 3:
                 if not pend:
                     spec = 1
