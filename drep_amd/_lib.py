@@ -87,6 +87,7 @@ SIGNATURES = {
     "drephip_last_linkage_info": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_uint64), C.POINTER(C.c_uint32),
                                             C.POINTER(C.c_uint32)]),
     "drephip_last_linkage_stats": (C.c_int, [vp] + [C.POINTER(C.c_double)] * 5),
+    "drephip_last_linkage_launches": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
     "drephip_set_timing": (C.c_int, [vp, C.c_int]),
     "drephip_last_kernel_ms": (C.c_int, [vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int)]),
     "drephip_set_allpairs_screen": (C.c_int, [vp, C.c_int]),
@@ -355,6 +356,12 @@ class Context:
         v = [C.c_double(0) for _ in range(5)]
         check(lib().drephip_last_linkage_stats(self._h, *[C.byref(x) for x in v]), "drephip_last_linkage_stats")
         return dict(zip(("alloc_s", "matrix_s", "chain_s", "finish_s", "wall_s"), (x.value for x in v)))
+
+    def linkage_launches(self) -> int:
+        """Step launches of the last dense-chain linkage call."""
+        v = C.c_uint64(0)
+        check(lib().drephip_last_linkage_launches(self._h, C.byref(v)), "drephip_last_linkage_launches")
+        return int(v.value)
 
     def set_timing(self, on: bool = True, kernels=None) -> None:
         """HIP-event timing of kernel launches: all kernels, or only the

@@ -1057,6 +1057,12 @@ DREPHIP_EXPORT int drephip_last_linkage_info(drephip_ctx *ctx, int *sparse, uint
     return DREPHIP_OK;
 }
 
+DREPHIP_EXPORT int drephip_last_linkage_launches(drephip_ctx *ctx, uint64_t *launches) {
+    if (!ctx || !launches) { set_error("null argument"); return DREPHIP_ERR_ARG; }
+    *launches = ctx->link.launches;
+    return DREPHIP_OK;
+}
+
 DREPHIP_EXPORT int drephip_last_linkage_stats(drephip_ctx *ctx, double *alloc_s, double *matrix_s, double *chain_s,
                                               double *finish_s, double *wall_s) {
     if (!ctx) { set_error("null context"); return DREPHIP_ERR_ARG; }

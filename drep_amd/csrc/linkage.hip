@@ -28,6 +28,7 @@
 #include "../../include/drephip.h"
 
 #include <algorithm>
+#include <cstddef>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -232,10 +233,9 @@ __device__ void block_argmin3(MinIdx &a, MinIdx &b, MinIdx &c, bool with_b, bool
 // column y) fused with the search of the chain top's row.  The search of row
 // t = chain top reads D[t][i]; the update rewrites only row/column y, so every
 // D[t][i] with i != y is untouched, and the one changed entry D[t][y] is
-// produced by the thread of i = y (the thread of i = t skips it), which also
-// uses it as its search value -- no cross-workgroup dependence within the
-// step.  After a chain restart t may be y itself: then the search value of i
-// is the freshly computed D[y][i].
+// produced by the lane of i = y from two uniform loads (D[x][t], D[y][t]) --
+// no cross-workgroup dependence within the step.  After a chain restart t may
+// be y itself: then the search value of i is the freshly computed D[y][i].
 //
 // A step's chain decision is made at the START of the next launch: kernel s
 // publishes its workgroup partials (plain stores -- the kernel boundary orders
@@ -263,36 +263,34 @@ __device__ void block_argmin3(MinIdx &a, MinIdx &b, MinIdx &c, bool with_b, bool
 // The decision's operands -- D[t][below] and the two sizes -- are loaded with
 // the partials: the chain's elements below the top are never x or y, so no
 // update touches them.
+//
+// The state is one 64-byte line (the sizes and the row a merge changes are
+// functions of pend, x, y, nx, ny); per-step diagnostic counters exist only in
+// a DREPHIP_LK_DIAG=1 build.
 struct alignas(64) LinkState {
     int32_t k, len, top, below, first_active;
-    int32_t pend, x, y, nx, ny;   // Lance-Williams update this state's step applies
-    int32_t decide;               // 1: the reader first decides the previous step from its partials
-    int32_t bad;
+    int32_t pend, x, y, nx, ny;   // the merge this state's launch applies: x < y, row/column y rewritten, x retired
+    int32_t c3;                   // chain[len - 3]
+    int32_t spec;                 // rows this launch reduces besides or instead of the top's (k_nn_step): 0-3
+    int32_t known;                // 1: the next launch's first decision is the merge of top and below
+    int32_t flags;                // 1: the reader first decides the previous step from its partials; 2: bad
     int32_t mx;                   // MST: current vertex
-    int32_t psa, psb, psbsz;      // the sizes this state's merge changed (psa = -1: none), written to
-                                  // size[] by workgroup 0 of the NEXT kernel, which every reader of
-                                  // that kernel therefore overrides
-    int32_t mrow;                 // the row this state's merge forms (its minimum: the P2 partials), -1: none
-    int32_t launches, twice;      // working launches, launches that decided two steps (diagnostics)
-    int32_t recip, scans;         // diagnostics: scan launches (no merge applied), and those whose row's
-                                  // step was a merge with the element below (the next launch's first decision)
-    int32_t am_other, am_y, am_merge;   // diagnostics: the first decision after a merge launch
-    int32_t c3, spec;             // chain[len - 3] (w); 1: this launch searches w's row speculatively (P3)
-    int32_t specwin;              // diagnostics: launches saved by the speculation
-    int32_t m0, m0m;              // diagnostics: merge launches without speculation, and those whose next decision merges
+    int32_t launches;             // working launches (reported: launches per merge)
 };
-
-// all partials of the previous kernel -> their minimum (thread 0)
-template <int WG>
-__device__ __forceinline__ MinIdx read_partials(const MinIdx *parts, uint32_t G) {
-    double bv = INFINITY;
-    int32_t bi = 0x7fffffff;
-    for (uint32_t b = threadIdx.x; b < G; b += WG) {             // (WG: see k_nn_step)
-        const MinIdx m = parts[b];
-        if (better(m.v, m.i, bv, bi)) { bv = m.v; bi = m.i; }
-    }
-    return block_argmin<WG>(bv, bi);
-}
+static_assert(sizeof(LinkState) == 64, "the step state is one 64-byte line");
+constexpr int32_t kLkDecide = 1, kLkBad = 2;
+#ifndef DREPHIP_LK_DIAG
+#define DREPHIP_LK_DIAG 0
+#endif
+#if DREPHIP_LK_DIAG
+// diagnostic build: counters kept by lane 0 of workgroup 0 (a dependent
+// load + store per launch; never in the product build)
+struct LinkDiag { int32_t twice, scans, specwin, known, m0, wmerge, recip; };
+__device__ LinkDiag *g_lk_diag;
+#define LK_DIAG(field) do { if (w0l) g_lk_diag->field++; } while (0)
+#else
+#define LK_DIAG(field) (void)0
+#endif
 
 // The decision's operands -- D[top][below], the two sizes and the chain
 // entries a merge exposes -- are loaded by one extra workgroup of the kernel
@@ -306,10 +304,41 @@ __device__ __forceinline__ MinIdx read_partials(const MinIdx *parts, uint32_t G)
 struct alignas(64) LinkFwd {
     double dp;
     int32_t szt, szb, c3, c4;
-    // the speculation of a search launch (spec = 1): see k_nn_step
-    double dp2;                   // D[w][c4], w = c3
-    int32_t spec;                 // 1: the P2 partials hold the would-be merged row's minimum, P3 w's
+    double dp2;                   // D[w][c4], w = c3 (the speculation's decision operand)
+    int32_t spec;                 // 1: the P2 partials hold a speculated merged row's minimum, P3 the row below's
 };
+static_assert(offsetof(LinkFwd, dp2) == 24 && offsetof(LinkFwd, spec) == 32, "LinkFwd word layout (fwd_from_words)");
+
+// a uniform 32-bit word held in a VGPR -> SGPR
+__device__ __forceinline__ int32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane((int32_t)v); }
+__device__ __forceinline__ LinkState state_from_words(uint4 a, uint4 b, uint4 c, uint4 d) {
+    LinkState S;
+    S.k = rfl(a.x); S.len = rfl(a.y); S.top = rfl(a.z); S.below = rfl(a.w);
+    S.first_active = rfl(b.x); S.pend = rfl(b.y); S.x = rfl(b.z); S.y = rfl(b.w);
+    S.nx = rfl(c.x); S.ny = rfl(c.y); S.c3 = rfl(c.z); S.spec = rfl(c.w);
+    S.known = rfl(d.x); S.flags = rfl(d.y); S.mx = rfl(d.z); S.launches = rfl(d.w);
+    return S;
+}
+__device__ __forceinline__ LinkFwd fwd_from_words(uint4 a, uint4 b, uint4 c) {
+    LinkFwd F;
+    F.dp = __longlong_as_double((long long)(((uint64_t)(uint32_t)rfl(a.y) << 32) | (uint32_t)rfl(a.x)));
+    F.szt = rfl(a.z); F.szb = rfl(a.w); F.c3 = rfl(b.x); F.c4 = rfl(b.y);
+    F.dp2 = __longlong_as_double((long long)(((uint64_t)(uint32_t)rfl(b.w) << 32) | (uint32_t)rfl(b.z)));
+    F.spec = rfl(c.x);
+    return F;
+}
+
+// all partials of the previous kernel -> their minimum (thread 0)
+template <int WG>
+__device__ __forceinline__ MinIdx read_partials(const MinIdx *parts, uint32_t G) {
+    double bv = INFINITY;
+    int32_t bi = 0x7fffffff;
+    for (uint32_t b = threadIdx.x; b < G; b += WG) {             // (WG: see k_nn_step)
+        const MinIdx m = parts[b];
+        if (better(m.v, m.i, bv, bi)) { bv = m.v; bi = m.i; }
+    }
+    return block_argmin<WG>(bv, bi);
+}
 
 // Round 4: a merge step also reduces the merged row y to its minimum (the
 // "P2" partials; the new values are computed there anyway).  When the next
@@ -317,13 +346,27 @@ struct alignas(64) LinkFwd {
 // formed -- y's own step is decided at once from P2 instead of by a launch
 // that searches y's row: up to two chain steps per launch.
 //
-// Speculation: a launch whose top t may merge with the element below it, sb
-// (a search launch, or a merge launch whose merged row is sb), also reduces
-// the row that merge would form (P2) and the row of the element below sb, w,
-// as it would be after it (P3).  When the next decision is that merge, w's
-// step and (when w pushes the merged row) that row's step are decided from P3
-// and P2 in the same launch, which then searches the row pushed last: runs of
-// reciprocal merges take one launch per merge.
+// Speculation on a merge of the top A with the element below it, B: the launch
+// reduces the row U that merge would form (index max(A, B); P2) and the row of
+// the element below B, W, as it would be after it (P3: W's row without A and
+// B, plus (U[W], max(A, B))).  When the next launch's decision is that merge,
+// it decides W's step from P3 -- and, when W pushes the merged row, that row's
+// step from P2 -- in the same launch.  The rows are taken as they are after
+// this launch's own merge (x, y): row y is the update u this launch computes,
+// and entry y of any other row R is U1[R] = LW(D[x][R], D[y][R]).
+//   spec 1: a search launch (no merge): A, B, W as stored;
+//   spec 2: a merge launch whose merged row is B (just pushed back below the top);
+//   spec 3 (round 5): the next decision is KNOWN to be the merge of A and B
+//           -- W's decision from P3 was a merge with the element below it, or
+//           W pushed the merged row b and b's own minimum (P2) ties with W, so b
+//           merges back -- and the launch speculates on that merge INSTEAD of
+//           searching the top's row (which would only confirm it): the next
+//           launch applies it and decides the step after it at once.  In the
+//           round-4 protocol the launch searched the top again, the next one
+//           merged without speculation, and a third searched the new top:
+//           launches per merge 1.318 -> 1.225 at 10^4 (tools/chain_sim.py,
+//           the host model of this protocol, Z identical to scipy's).
+// One merge per launch stays the rule.
 template <int WG, int kLkPer>
 __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t n, int method,
                                                    int32_t *__restrict__ size, int32_t *__restrict__ chain,
@@ -333,38 +376,55 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                                                    double *__restrict__ Z, uint32_t q, int spec_on) {
     __shared__ LinkState sx;
     const uint32_t G = gridDim.x - 1;                          // step workgroups; workgroup G forwards operands
-    const LinkState S = st[q ^ 1];
-    const LinkFwd F = fwd[q ^ 1];
-#if DREPHIP_LK_PHASES
-    uint64_t ph0 = 0, ph1 = 0, ph2 = 0, ph3 = 0, ph4 = 0, ph5 = 0, ph6 = 0;
-#endif
-    LK_T(ph0);
-    // The partial sets are reduced by wave 0 alone (the decision is thread
-    // 0's: no barrier), read whether or not they are needed (valid memory
-    // either way) so that their loads are not held behind the state's.  A
-    // lane takes partials lane, lane + 64, ... four at a time, all loads in
-    // flight before the first wait.  (The loop steps by a constant: a
-    // blockDim.x stride's kernarg load held the partial loads behind the state's.)
+    // The partial sets are reduced by wave 0 alone (the decision is wave 0's:
+    // no barrier), read whether or not they are needed (valid memory either
+    // way).  Their loads are issued before the state's: a state load landing
+    // in a scalar register the compiler reuses waited for the state before
+    // the partial loads went out (one round trip more per step).  A lane
+    // takes partials lane, lane + 64, ... four at a time, all loads in flight
+    // before the first wait.  (The loop steps by a constant: a blockDim.x
+    // stride's kernarg load held the partial loads behind the state's.)
     // wave 0, as a wave-uniform condition (readfirstlane): the decision below
     // runs on every lane of wave 0 as scalar code, its values in SGPRs (as
     // one lane's divergent code it took ~0.8 us a launch)
     const bool wave0 = __builtin_amdgcn_readfirstlane(threadIdx.x) < 64, lane0 = threadIdx.x == 0;
     MinIdx g{INFINITY, 0x7fffffff}, g2{INFINITY, 0x7fffffff}, g3{INFINITY, 0x7fffffff};
+    // state and forwarded operands: vector loads through an opaque zero lane
+    // offset, issued first, so the partial loads go out behind them and one
+    // wait covers both (as scalar loads, a state field landing in a scalar
+    // register the compiler reused made it wait for the state before issuing
+    // the partial loads: one more round trip per step); then read into SGPRs
+    int32_t lz0;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(lz0));
+    const uint4 *sv = (const uint4 *)(st + (q ^ 1)) + lz0;
+    const uint4 *fv = (const uint4 *)(fwd + (q ^ 1)) + lz0;
+    uint4 sw0 = sv[0], sw1 = sv[1], sw2 = sv[2], sw3 = sv[3], fw0 = fv[0], fw1 = fv[1], fw2 = fv[2];
     if (wave0) {
         const MinIdx *P1 = parts + (uint64_t)(q ^ 1) * 1024, *P2 = parts2 + (uint64_t)(q ^ 1) * 1024,
                      *P3 = parts3 + (uint64_t)(q ^ 1) * 1024;
         if (G <= 256) partial_pass<4>(P1, P2, P3, G, g, g2, g3);
         else partial_pass<8>(P1, P2, P3, G, g, g2, g3);              // (up to 512 workgroups in one pass)
-        wave_argmin_upto3(g, g2, g3, S.mrow >= 0 || F.spec, F.spec != 0);
     }
+    asm volatile("" : "+v"(sw0.x), "+v"(sw0.y), "+v"(sw0.z), "+v"(sw0.w), "+v"(sw1.x), "+v"(sw1.y), "+v"(sw1.z),
+                 "+v"(sw1.w), "+v"(sw2.x), "+v"(sw2.y), "+v"(sw2.z), "+v"(sw2.w), "+v"(sw3.x), "+v"(sw3.y),
+                 "+v"(sw3.z), "+v"(sw3.w));
+    asm volatile("" : "+v"(fw0.x), "+v"(fw0.y), "+v"(fw0.z), "+v"(fw0.w), "+v"(fw1.x), "+v"(fw1.y), "+v"(fw1.z),
+                 "+v"(fw1.w), "+v"(fw2.x));
+    const LinkState S = state_from_words(sw0, sw1, sw2, sw3);
+    const LinkFwd F = fwd_from_words(fw0, fw1, fw2);
+#if DREPHIP_LK_PHASES
+    uint64_t ph0 = 0, ph1 = 0, ph2 = 0, ph3 = 0, ph4 = 0, ph5 = 0, ph6 = 0;
+#endif
+    LK_T(ph0);
+    if (wave0) wave_argmin_upto3(g, g2, g3, S.pend || F.spec, F.spec != 0);
     LK_T(ph1);
     if (S.k >= (int32_t)n - 1) return;                         // all merged
     const bool w0 = blockIdx.x == 0;
     // size of cluster i as of the previous decision: workgroup 0 writes that
     // decision's two sizes during this kernel, so every reader overrides them
-    const int32_t spsa = S.psa, spsb = S.psb, spsbsz = S.psbsz;
+    const int32_t spsa = S.pend ? S.x : -1, spsb = S.pend ? S.y : -1, spsbsz = S.nx + S.ny;
     auto size_prev = [=](int32_t i, int32_t stored) { return i == spsa ? 0 : i == spsb ? spsbsz : stored; };
-    if (w0 && threadIdx.x == 0 && S.psa >= 0) { size[S.psa] = 0; size[S.psb] = S.psbsz; }
+    if (w0 && threadIdx.x == 0 && S.pend) { size[S.x] = 0; size[S.y] = spsbsz; }
     // ---- the previous step's decision, and y's when it pushes y (replicated
     // in every workgroup; its stores by lane 0 of workgroup 0)
     const bool w0l = w0 && lane0;
@@ -372,38 +432,30 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
         // (plain scalars, the state struct written once at the end: a struct
         // updated across the branches was kept in private memory)
         int32_t k = S.k, len = S.len, top = S.top, below = S.below, first_active = S.first_active;
-        int32_t pend = 0, px = S.x, py = S.y, pnx = S.nx, pny = S.ny, bad = S.bad, mrow = -1;
-        int32_t psa = -1, psb = -1, psbsz = 0, twice = S.twice, recip = S.recip;
-        int32_t am_other = S.am_other, am_y = S.am_y, am_merge = S.am_merge, specwin = S.specwin;
-        int32_t m0m = S.m0m;
+        int32_t pend = 0, px = S.x, py = S.y, pnx = S.nx, pny = S.ny, bad = S.flags & kLkBad, known = 0;
+        const int32_t mrow = S.pend ? S.y : -1;                // the row the previous launch's merge formed
         // c3, c4: chain[len - 3], chain[len - 4]; ck of them are known exactly
         // (a merge exposes entries only the chain in memory holds; a push
         // shifts known ones down)
         int32_t c3 = F.c3, c4 = F.c4, ck = 2, dpo = 0;
         double dpov = 0.0;
-        if (S.decide) {
+        if (S.flags & kLkDecide) {
             int32_t szt = F.szt, szb = F.szb;
             double dp = F.dp;
             MinIdx r = g;
             for (int d = 0; d < 2; d++) {
-                if ((uint32_t)r.i >= n) { bad = 1; k = (int32_t)n - 1; break; }      // no valid partial: stop
-                if (d == 0 && S.pend) {
-                    if (len > 1 && !(r.v < dp)) am_merge++;
-                    else if (r.i == S.mrow) am_y++;
-                    else am_other++;
-                }
-                if (len > 1 && !(r.v < dp)) {                     // merge top with below at dp
-                    if (d == 0 && S.pend && !F.spec) m0m++;
-                    if (d == 0 && !S.pend) recip++;
+                // a known merge (spec 3) needs no search result: the previous
+                // launch decided it and speculated on it
+                const bool kn = d == 0 && S.known;
+                if (!kn && (uint32_t)r.i >= n) { bad = kLkBad; k = (int32_t)n - 1; break; }   // no valid partial: stop
+                if (kn || (len > 1 && !(r.v < dp))) {              // merge top with below at dp
                     int32_t a = top, b = below, na = szt, nb = szb;
                     if (a > b) { a = below; b = top; na = szb; nb = szt; }
                     if (w0l) {
                         double *z = Z + 4ull * S.k;
                         z[0] = a; z[1] = b; z[2] = dp; z[3] = na + nb;
                     }
-                    psa = a; psb = b; psbsz = na + nb;
                     pend = 1; px = a; py = b; pnx = na; pny = nb;
-                    mrow = b;
                     ck = 0;
                     k = S.k + 1;
                     len -= 2;
@@ -412,7 +464,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                     if (len == 0 && k < (int32_t)n - 1) {           // restart at the first active cluster
                         int32_t f = S.first_active;
                         while (f < (int32_t)n && !(f == b || (f != a && size_prev(f, size[f]) > 0))) f++;
-                        if (f >= (int32_t)n) { bad = 1; k = (int32_t)n - 1; }
+                        if (f >= (int32_t)n) { bad = kLkBad; k = (int32_t)n - 1; }
                         else {
                             if (w0l) chain[0] = f;
                             first_active = f; top = f; below = -1; len = 1;
@@ -422,20 +474,24 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                         // top w's row as it is after this merge (P3) and the
                         // merged row b (P2): decide w's step, and b's when w
                         // pushes b, now.  A push makes this launch search the
-                        // pushed row instead of w; a merge is left to the next
-                        // launch (one merge per launch), with w or b searched here.
-                        // (b is pushed only together with b's own push: D[top][below]
+                        // pushed row instead of w.  A merge is left to the next
+                        // launch (one merge per launch), which then knows it:
+                        // this launch speculates on it (spec 3) instead of
+                        // searching.  (b is pushed only together with b's own
+                        // push, or as a known merge back with w: D[top][below]
                         // must not involve b, whose row this launch rewrites,
                         // except through dpo)
                         const MinIdx r3 = g3;
-                        const bool wpush = (uint32_t)r3.i < n && !(len > 1 && !(r3.v < F.dp2)) && len + 1 < (int32_t)n;
+                        const bool r3ok = (uint32_t)r3.i < n;
+                        const bool wmerge = r3ok && len > 1 && !(r3.v < F.dp2);
+                        const bool wpush = r3ok && !wmerge && len + 1 < (int32_t)n;
                         const bool bpush = r3.i == b && (uint32_t)g2.i < n && g2.v < r3.v;
                         if (wpush && (r3.i != b || bpush)) {
                             if (w0l) chain[len] = r3.i;                 // w pushes r3.i
                             c4 = c3; c3 = below; below = top; top = r3.i;
                             ck = ck >= 1 ? 2 : 1;
                             len++;
-                            specwin++;
+                            LK_DIAG(specwin);
                             if (bpush) {
                                 if (w0l) chain[len] = g2.i;             // b pushes g2.i
                                 c4 = c3; c3 = below; below = top; top = g2.i;
@@ -443,43 +499,55 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                                 len++;
                                 dpo = 1; dpov = g2.v;                   // D[g2.i][b] as this launch writes it
                             }
+                        } else if (wmerge && spec_on > 1) {
+                            known = 1;                                  // w merges with the element below it
+                            LK_DIAG(wmerge);
+                        } else if (wpush && r3.i == b && spec_on > 1) {
+                            if (w0l) chain[len] = b;                    // w pushes b, b merges back with w
+                            c4 = c3; c3 = below; below = top; top = b;
+                            ck = ck >= 1 ? 2 : 1;
+                            len++;
+                            dpo = 1; dpov = r3.v;                       // D[b][w] as this launch writes it
+                            known = 1;
+                            LK_DIAG(recip);
                         }
                     }
                     break;
                 }
                 // push (scipy: the previous element wins ties)
-                if (len >= (int32_t)n) { bad = 1; k = (int32_t)n - 1; break; }
+                if (len >= (int32_t)n) { bad = kLkBad; k = (int32_t)n - 1; break; }
                 if (w0l) chain[len] = r.i;
                 c4 = c3; c3 = below; below = top; top = r.i;
                 ck = ck >= 1 ? 2 : 1;
                 dp = r.v;
                 szb = szt;
                 len++;
-                if (r.i != S.mrow || S.mrow < 0 || d == 1) break;   // the pushed row is searched by this launch
-                szt = S.psbsz;                                      // y: just formed, its size is the override
+                if (r.i != mrow || mrow < 0 || d == 1) break;      // the pushed row is searched by this launch
+                szt = spsbsz;                                       // y: just formed, its size is the override
                 r = g2;                                             // y's minimum, from the merge step
-                twice++;
+                LK_DIAG(twice);
             }
         }
         LinkState X;
         X.mx = S.mx;
         X.k = k; X.len = len; X.top = top; X.below = below; X.first_active = first_active;
         X.pend = pend; X.x = px; X.y = py; X.nx = pnx; X.ny = pny;
-        X.decide = 1; X.bad = bad;
-        X.psa = psa; X.psb = psb; X.psbsz = psbsz; X.mrow = mrow;
-        X.launches = S.launches + 1; X.twice = twice;
-        X.recip = recip; X.scans = S.scans + (pend ? 0 : 1);
-        X.am_other = am_other; X.am_y = am_y; X.am_merge = am_merge; X.specwin = specwin;
-        X.m0m = m0m;
-        // speculate in a search launch (no merge applied) whose top has two
-        // elements below it: search w's row too (P3)
+        X.flags = kLkDecide | bad;
+        X.launches = S.launches + 1;
         X.c3 = c3;
+        X.known = known;
         X.spec = 0;
-        if (spec_on && len >= 3 && k < (int32_t)n - 1) {
+        if (known) {
+            X.spec = 3;                                         // speculate on the known merge, no search
+            LK_DIAG(known);
+        } else if (spec_on && len >= 3 && k < (int32_t)n - 1) {
             if (!pend) X.spec = 1;                              // a search launch
             else if (below == py && top != py) X.spec = 2;      // a merge launch, its row y below the top
         }
-        X.m0 = S.m0 + (pend && !X.spec ? 1 : 0);
+#if DREPHIP_LK_DIAG
+        if (!pend) LK_DIAG(scans);
+        else if (!X.spec) LK_DIAG(m0);
+#endif
         if (lane0) sx = X;
         LK_T(ph2);
         if (w0l) {
@@ -500,7 +568,9 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             double rdp2 = D[sp ? (uint64_t)c3 * n + c4 : 0];
             asm volatile("" : "+v"(rzt), "+v"(rzb), "+v"(rdp), "+v"(r3), "+v"(r4), "+v"(rdp2));
             LK_T(ph3);
-            auto size_now = [&](int32_t i, int32_t stored) { return i == psa ? 0 : i == psb ? psbsz : size_prev(i, stored); };
+            auto size_now = [&](int32_t i, int32_t stored) {
+                return pend && i == px ? 0 : pend && i == py ? pnx + pny : size_prev(i, stored);
+            };
             LinkFwd f{0.0, 0, 0, 0, 0};
             f.szt = size_now(top, rzt);                         // (also at len 1: a push and a merge may follow)
             if (two) {
@@ -527,87 +597,88 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     const LinkState X = sx;
     LK_T(ph3);
     if (X.k >= (int32_t)n - 1) return;
-    // ---- this step: the pending update fused with the search of row t, and
-    // the minimum of the new row y
+    // ---- this step: the pending update of row y fused with the search of row
+    // t (P1), and either y's new row (P2) or the speculation's rows (P2, P3)
     const bool pend = X.pend != 0;
     const int32_t x = X.x, y = X.y, nx = X.nx, ny = X.ny, t = X.top;
-    const double *Dt = D + (uint64_t)t * n;
+    const int spec = X.spec;
+    const bool search = spec != 3, sp = spec != 0;
+    // speculation rows: A = t, B = below, W = chain[len - 3] (spec 3 at len 2: no W)
+    const int32_t A = t, B = X.below, W = X.c3;
+    const bool hasW = sp && X.len >= 3;
+    const bool yA = pend && A == y, yB = pend && B == y, yW = pend && W == y;
+    const int32_t ys = A < B ? B : A;                          // the speculated merge's row index, max(A, B)
     const double *Dx = D + (uint64_t)x * n;
     double *Dy = D + (uint64_t)y * n;
-    // D[x][t], D[y][t]: waited for with the first pass.  (Through a lane
-    // register offset: a uniform address made them scalar loads, which the
-    // compiler waited for before the pass.)
+    const double *Da = D + (uint64_t)(yA ? 0 : A) * n;
+    const double *Db = D + (uint64_t)(sp && !yB ? B : 0) * n;
+    const double *Dw = D + (uint64_t)(hasW && !yW ? W : 0) * n;
+    // entry y of the rows read (as after this launch's merge): U1[R] =
+    // LW(D[x][R], D[y][R]), from uniform loads, used by the lane of i = y.
+    // (Through a lane register offset: a uniform address made them scalar
+    // loads, which the compiler waited for before the pass.)
     int32_t lz;
     asm volatile("v_mov_b32 %0, 0" : "=v"(lz));
-    double dxt = pend ? Dx[t + lz] : 0.0, dyt = pend ? Dy[t + lz] : 0.0;
-    // speculation (X.spec): if t merges with the element below, sb, the
-    // merged row U = LW(D[t], D[sb]) gets index max(t, sb) and the new top is
-    // sw; P2 <- U's minimum, P3 <- sw's row's minimum after that merge (sw's
-    // row without t and sb, plus (U[sw], max(t, sb))).  spec 1: a search
-    // launch, the rows as stored; spec 2: a merge launch whose merged row y is
-    // sb, D[sb][i] being the update u this launch computes for i (the real P2,
-    // y's minimum, is not needed then: y is already on the chain)
-    const bool spec1 = X.spec == 1, spec2 = X.spec == 2, spec = spec1 || spec2;
-    const int32_t sb = X.below, sw = X.c3;
-    const int32_t sy_ = spec ? (t < sb ? sb : t) : 0;
-    const double *Dsb = D + (uint64_t)(spec1 ? sb : 0) * n;
-    const double *Dw = D + (uint64_t)(spec ? sw : 0) * n;
-    // (t's and sb's sizes are loaded with the first pass's entries; see below)
-    int32_t rst = spec ? size[t] : 0, rsb = spec1 ? size[sb] : 0;
-    int32_t snx = 0, sny = 0;
+    const bool fa = pend && !yA, fb = pend && sp && !yB, fw = pend && hasW && !yW;
+    double xa = fa ? Dx[A + lz] : 0.0, ya_ = fa ? Dy[A + lz] : 0.0;
+    double xb = fb ? Dx[B + lz] : 0.0, yb = fb ? Dy[B + lz] : 0.0;
+    double xw = fw ? Dx[W + lz] : 0.0, yw = fw ? Dy[W + lz] : 0.0;
+    // the sizes of A and B as of this step's decision (for the speculated merge)
+    int32_t rsa = sp ? size[A + lz] : 0, rsb = sp ? size[B + lz] : 0;
+    auto size_x = [&](int32_t i, int32_t stored) {
+        return pend && i == x ? 0 : pend && i == y ? nx + ny : size_prev(i, stored);
+    };
     double bv = INFINITY, yv = INFINITY, wv = INFINITY;
     int32_t bi = 0x7fffffff, yi = 0x7fffffff, wi = 0x7fffffff;
+    int32_t sxs = 0, sys = 0;                                   // the speculated merge's sizes
     const uint32_t stride = G * WG;
+    bool first = true;
     for (uint32_t i0 = blockIdx.x * WG + threadIdx.x; i0 < n; i0 += kLkPer * stride) {
         int32_t sz[kLkPer];
-        double dt[kLkPer], dx[kLkPer], dy[kLkPer], dw[kLkPer], db[kLkPer];
+        double da[kLkPer], dx[kLkPer], dy[kLkPer], dw[kLkPer], db[kLkPer];
 #pragma unroll
         for (int k = 0; k < kLkPer; k++) {
             const uint32_t i = i0 + k * stride;
             const uint32_t ic = i < n ? i : n - 1;
             sz[k] = size[ic];
-            dt[k] = Dt[ic];
+            if (!yA) da[k] = Da[ic];
             if (pend) { dx[k] = Dx[ic]; dy[k] = Dy[ic]; }
-            if (spec) dw[k] = Dw[ic];
-            if (spec1) db[k] = Dsb[ic];
+            if (sp && !yB) db[k] = Db[ic];
+            if (hasW && !yW) dw[k] = Dw[ic];
         }
         // every load of the pass in flight before any is waited for: left to
-        // itself the compiler sank D[t][i]'s load below the size test that
-        // uses size[i] (a second round trip per step), and waited for D[x][t],
-        // D[y][t] (their update, hoisted) and t's and sb's sizes before the pass
+        // itself the compiler sank the row loads below the size test that
+        // uses size[i] (a second round trip per step), and waited for the
+        // uniform loads before the pass
 #pragma unroll
         for (int k = 0; k < kLkPer; k++) {
-            asm volatile("" : "+v"(sz[k]), "+v"(dt[k]));
-            if (pend) asm volatile("" : "+v"(dx[k]), "+v"(dy[k]), "+v"(dxt), "+v"(dyt));
-            if (spec) asm volatile("" : "+v"(dw[k]));
-            if (spec1) asm volatile("" : "+v"(db[k]));
+            asm volatile("" : "+v"(sz[k]));
+            if (!yA) asm volatile("" : "+v"(da[k]));
+            if (pend) asm volatile("" : "+v"(dx[k]), "+v"(dy[k]));
+            if (sp && !yB) asm volatile("" : "+v"(db[k]));
+            if (hasW && !yW) asm volatile("" : "+v"(dw[k]));
         }
         LK_T(ph4);
-        if (spec) {
-            asm volatile("" : "+v"(rst), "+v"(rsb));
-            const int32_t snt = size_prev(t, rst), snb = spec2 ? X.psbsz : size_prev(sb, rsb);
-            snx = t < sb ? snt : snb; sny = t < sb ? snb : snt;
+        if (first) {
+            first = false;
+            asm volatile("" : "+v"(xa), "+v"(ya_), "+v"(xb), "+v"(yb), "+v"(xw), "+v"(yw), "+v"(rsa), "+v"(rsb));
+            if (sp) {
+                const int32_t sa = size_x(A, rsa), sb_ = size_x(B, rsb);
+                sxs = A < B ? sa : sb_;
+                sys = A < B ? sb_ : sa;
+            }
         }
 #pragma unroll
         for (int k = 0; k < kLkPer; k++) {
-            const uint32_t i = i0 + k * stride;
-            if (i >= n) continue;
+            const int32_t i = (int32_t)(i0 + k * stride);
+            if (i >= (int32_t)n) continue;
             // the sizes as of this step's decision: the previous decision's
             // (being written by workgroup 0) and this one's (not yet written)
-            const int32_t szi = (int32_t)i == X.psa ? 0 : (int32_t)i == X.psb ? X.psbsz : size_prev((int32_t)i, sz[k]);
-            if (szi == 0) continue;
-            if (spec1 && (int32_t)i != t && (int32_t)i != sb) {
-                const double u = lw_update(method, t < sb ? dt[k] : db[k], t < sb ? db[k] : dt[k], snx, sny);
-                if (better(u, (int32_t)i, yv, yi)) { yv = u; yi = (int32_t)i; }
-                if ((int32_t)i == sw) {
-                    if (better(u, sy_, wv, wi)) { wv = u; wi = sy_; }          // D'[sw][max(t, sb)]
-                } else if (better(dw[k], (int32_t)i, wv, wi)) {
-                    wv = dw[k]; wi = (int32_t)i;
-                }
-            }
-            double v;
-            if (pend && (int32_t)i != y && (int32_t)i != t) {
-                const double u = lw_update(method, dx[k], dy[k], nx, ny);
+            if (size_x(i, sz[k]) == 0) continue;                // (retires x)
+            // this launch's merge: row y's new value at i, stored to row and column y
+            double u = 0.0;
+            if (pend && i != y) {
+                u = lw_update(method, dx[k], dy[k], nx, ny);
                 Dy[i] = u;
 #if DREPHIP_LK_COLSTORE == 0
                 // timing-only A/B build: no column-y stores (Z is wrong)
@@ -616,34 +687,41 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
 #else
                 D[(uint64_t)i * n + y] = u;
 #endif
-                if (spec2) {                                        // (i is neither t nor sb = y)
-                    const double U = lw_update(method, t < sb ? dt[k] : u, t < sb ? u : dt[k], snx, sny);
-                    if (better(U, (int32_t)i, yv, yi)) { yv = U; yi = (int32_t)i; }
-                    if ((int32_t)i == sw) {
-                        if (better(U, sy_, wv, wi)) { wv = U; wi = sy_; }
-                    } else if (better(dw[k], (int32_t)i, wv, wi)) {
-                        wv = dw[k]; wi = (int32_t)i;
-                    }
-                } else if (better(u, (int32_t)i, yv, yi)) {
-                    yv = u; yi = (int32_t)i;
-                }
-                v = t == y ? u : dt[k];
-            } else if (pend && (int32_t)i == y && t != y) {
-                const double u = lw_update(method, dxt, dyt, nx, ny);
-                Dy[t] = u;
-                D[(uint64_t)t * n + y] = u;
-                if (!spec2 && better(u, t, yv, yi)) { yv = u; yi = t; }    // (D[y][t], produced by y's lane)
-                v = u;
-            } else {
-                if ((int32_t)i == t) continue;
-                v = dt[k];
             }
-            if (v < bv) { bv = v; bi = (int32_t)i; }
+            // the rows as they are after that merge: row y is u; entry y of a
+            // row R is U1[R]
+            double ca, cb = 0.0, cw = 0.0;
+            if (pend && i == y) {
+                ca = yA ? 0.0 : lw_update(method, xa, ya_, nx, ny);
+                if (sp) cb = yB ? 0.0 : lw_update(method, xb, yb, nx, ny);
+                if (hasW) cw = yW ? 0.0 : lw_update(method, xw, yw, nx, ny);
+            } else {
+                ca = yA ? u : da[k];
+                if (sp) cb = yB ? u : db[k];
+                if (hasW) cw = yW ? u : dw[k];
+            }
+            if (search && i != t && ca < bv) { bv = ca; bi = i; }          // P1: the top's row
+            if (sp) {
+                if (i != A && i != B) {
+                    // P2: the speculated merged row; P3: W's row after that merge
+                    const double U = lw_update(method, A < B ? ca : cb, A < B ? cb : ca, sxs, sys);
+                    if (better(U, i, yv, yi)) { yv = U; yi = i; }
+                    if (hasW) {
+                        if (i == W) {
+                            if (better(U, ys, wv, wi)) { wv = U; wi = ys; }
+                        } else if (better(cw, i, wv, wi)) {
+                            wv = cw; wi = i;
+                        }
+                    }
+                }
+            } else if (pend && i != y && better(u, i, yv, yi)) {   // P2: y's new row
+                yv = u; yi = i;
+            }
         }
     }
     LK_T(ph5);
     MinIdx p1{bv, bi}, p2{yv, yi}, p3{wv, wi};
-    block_argmin3<WG>(p1, p2, p3, pend || spec, spec);
+    block_argmin3<WG>(p1, p2, p3, pend || sp, hasW);
     LK_T(ph6);
 #if DREPHIP_LK_PHASES
     if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == G - 1)) {
@@ -653,9 +731,9 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     }
 #endif
     if (threadIdx.x == 0) {
-        parts[(uint64_t)q * 1024 + blockIdx.x] = p1;
-        if (pend || spec) parts2[(uint64_t)q * 1024 + blockIdx.x] = p2;
-        if (spec) parts3[(uint64_t)q * 1024 + blockIdx.x] = p3;
+        if (search) parts[(uint64_t)q * 1024 + blockIdx.x] = p1;
+        if (pend || sp) parts2[(uint64_t)q * 1024 + blockIdx.x] = p2;
+        if (hasW) parts3[(uint64_t)q * 1024 + blockIdx.x] = p3;
     }
 }
 
@@ -667,15 +745,15 @@ __global__ __launch_bounds__(WG) void k_mst_step(const double *__restrict__ D, u
     // (the state as scalars: a LinkState copied and edited in branches was
     // kept in private memory promoted to LDS, see k_nn_step)
     __shared__ int32_t s_k, s_mx, s_ov;
-    const int32_t sk = st[q ^ 1].k, smx = st[q ^ 1].mx, sdecide = st[q ^ 1].decide, sbad = st[q ^ 1].bad;
     const uint32_t G = gridDim.x;
     const MinIdx g = read_partials<WG>(parts + (uint64_t)(q ^ 1) * 1024, G);     // unconditional: not held behind S
+    const int32_t sk = st[q ^ 1].k, smx = st[q ^ 1].mx, sflags = st[q ^ 1].flags;
     if (sk >= (int32_t)n - 1) return;
     if (threadIdx.x == 0) {
-        int32_t k = sk, mx = smx, bad = sbad, ov = -1;
+        int32_t k = sk, mx = smx, bad = sflags & kLkBad, ov = -1;
         const bool w0 = blockIdx.x == 0;
-        if (sdecide) {
-            if ((uint32_t)g.i >= n) { bad = 1; k = (int32_t)n - 1; }
+        if (sflags & kLkDecide) {
+            if ((uint32_t)g.i >= n) { bad = kLkBad; k = (int32_t)n - 1; }
             else {
                 if (w0) {
                     double *z = Z + 4ull * sk;
@@ -689,8 +767,8 @@ __global__ __launch_bounds__(WG) void k_mst_step(const double *__restrict__ D, u
         }
         s_k = k; s_mx = mx; s_ov = ov;
         if (w0) {
-            st[q].k = k; st[q].mx = mx; st[q].bad = bad; st[q].decide = 1;
-            if (k >= (int32_t)n - 1) { st[q ^ 1].k = k; st[q ^ 1].mx = mx; st[q ^ 1].bad = bad; st[q ^ 1].decide = 1; }
+            st[q].k = k; st[q].mx = mx; st[q].flags = kLkDecide | bad;
+            if (k >= (int32_t)n - 1) { st[q ^ 1].k = k; st[q ^ 1].mx = mx; st[q ^ 1].flags = kLkDecide | bad; }
             *done = k;
         }
     }
@@ -863,8 +941,10 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     MinIdx *d_parts2, *d_parts3;
     if ((rc = scratch(ctx, "lk_parts2", 2 * 1024 * sizeof(MinIdx), (void **)&d_parts2))) return rc;
     if ((rc = scratch(ctx, "lk_parts3", 2 * 1024 * sizeof(MinIdx), (void **)&d_parts3))) return rc;
-    const char *spe = getenv("DREPHIP_LINK_SPEC");                     // the speculative search (A/B: 0 off)
-    const int spec_on = spe ? atoi(spe) != 0 : 1;
+    // the speculation (A/B): 0 off; 1 the round-4 protocol (no known-merge
+    // launches); 2 (default) with the known-merge speculation (spec 3)
+    const char *spe = getenv("DREPHIP_LINK_SPEC");
+    const int spec_on = spe ? std::max(0, std::min(2, atoi(spe))) : 2;
     if ((rc = scratch(ctx, "lk_st", 2 * sizeof(LinkState), (void **)&d_st))) return rc;
     LinkFwd *d_fwd;
     if ((rc = scratch(ctx, "lk_fwd", 2 * sizeof(LinkFwd), (void **)&d_fwd))) return rc;
@@ -888,13 +968,18 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
         // first kernel (parity 0) reads buffer 1, with no decision pending
         LinkState h[2] = {};
         h[1].len = 1; h[1].top = 0; h[1].below = -1; h[1].first_active = 0; h[1].mx = 0;
-        h[1].psa = h[1].psb = -1;
-        h[1].mrow = -1;
+        h[1].c3 = -1;
         h[0] = h[1];
         HIPC(hipMemcpyAsync(d_st, h, sizeof(h), hipMemcpyHostToDevice, st));
         int32_t zero = 0;
         HIPC(hipMemcpyAsync(d_done, &zero, 4, hipMemcpyHostToDevice, st));
     }
+#if DREPHIP_LK_DIAG
+    LinkDiag *d_diag = nullptr;
+    HIPC(hipMalloc((void **)&d_diag, sizeof(LinkDiag)));
+    HIPC(hipMemset(d_diag, 0, sizeof(LinkDiag)));
+    HIPC(hipMemcpyToSymbol(HIP_SYMBOL(g_lk_diag), &d_diag, sizeof(d_diag)));
+#endif
 #if DREPHIP_LK_PHASES
     uint64_t *d_ph = nullptr;
     if (!mst) {
@@ -966,17 +1051,21 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     if (done != (int32_t)n - 1) { set_error("linkage did not finish"); return DREPHIP_ERR_INTERNAL; }
     LinkState hs[2];
     HIPC(hipMemcpy(hs, d_st, sizeof(hs), hipMemcpyDeviceToHost));
-    const int32_t bad = hs[0].bad | hs[1].bad;
-    if (getenv("DREPHIP_DEBUG") && !mst) {
-        const LinkState &hl = hs[0].launches > hs[1].launches ? hs[0] : hs[1];
-        fprintf(stderr, "[drephip] chain: n=%u launches %d, of which %d decided two steps; %d scan launches, "
-                        "%d of them followed by a merge with the element below\n", n, hl.launches, hl.twice, hl.scans,
-                hl.recip);
-        fprintf(stderr, "[drephip] chain: first decision after a merge launch: push another %d, push the merged row %d, "
-                        "merge %d; speculation saved %d searches\n", hl.am_other, hl.am_y, hl.am_merge, hl.specwin);
-        fprintf(stderr, "[drephip] chain: %d merge launches without speculation, %d of them followed by a merge\n", hl.m0,
-                hl.m0m);
+    const int32_t bad = (hs[0].flags | hs[1].flags) & kLkBad;
+    ctx->link.launches = (uint64_t)std::max(hs[0].launches, hs[1].launches);
+    if (getenv("DREPHIP_DEBUG"))
+        fprintf(stderr, "[drephip] chain: n=%u launches %llu (%.4f per merge), speculation %d\n", n,
+                (unsigned long long)ctx->link.launches, (double)ctx->link.launches / (double)(n - 1), spec_on);
+#if DREPHIP_LK_DIAG
+    {
+        LinkDiag hd;
+        HIPC(hipMemcpy(&hd, d_diag, sizeof(hd), hipMemcpyDeviceToHost));
+        (void)hipFree(d_diag);
+        fprintf(stderr, "[drephip] chain diag: twice %d scans %d specwin %d known %d (wmerge %d, recip %d) "
+                        "merge launches without speculation %d\n", hd.twice, hd.scans, hd.specwin, hd.known,
+                hd.wmerge, hd.recip, hd.m0);
     }
+#endif
 #if DREPHIP_LK_PHASES
     if (d_ph) {
         std::vector<uint64_t> h((size_t)kPhCap * 16);

@@ -340,6 +340,11 @@ int drephip_last_linkage_info(drephip_ctx *ctx, int *sparse, uint64_t *pairs, ui
  * sketch/all-pairs stages.  Same limits as drephip_linkage. */
 int drephip_linkage_reserve(drephip_ctx *ctx, uint32_t n);
 
+/* Step launches of the last linkage call's nearest-neighbour chain that did
+ * work (complete / average / weighted on the dense GPU path: ~1.2-1.35 per
+ * merge); 0 after the sparse path and for single linkage (Prim). */
+int drephip_last_linkage_launches(drephip_ctx *ctx, uint64_t *launches);
+
 /* Host wall-clock split of the last drephip_linkage* call on this context
  * (seconds): the matrix allocation (0 when reserved/reused), the matrix build,
  * the chain (or MST) steps including their setup, the Z readback + scipy's

@@ -46,6 +46,9 @@ for rep in range(2):
     out["wall_s_%d" % rep] = time.perf_counter() - t0
     out["phases_%d" % rep] = ctx.linkage_stats()
     out["chain_kernel_ms_%d" % rep] = ctx.kernel_ms(2)[0]
+    out["launches_%d" % rep] = ctx.linkage_launches()
+out["launches_per_merge"] = out["launches_1"] / (N - 1)
+out["spec"] = os.environ.get("DREPHIP_LINK_SPEC", "default")
 out["Z_sha1"] = hashlib.sha1(np.ascontiguousarray(Z, dtype="<f8").tobytes()).hexdigest()
 golden = json.load(open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
                                      "scale_linkage_sha1.json"))).get(str(N)) if method == "average" else None
