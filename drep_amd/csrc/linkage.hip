@@ -44,7 +44,8 @@ namespace drephip {
 // 10^5 -- profiles/r03_linkage_wg_ab.txt)
 constexpr int kLkWG = 256;
 #ifndef DREPHIP_LK_COLSTORE
-#define DREPHIP_LK_COLSTORE 1     // column-y stores of a merge step: 1 plain, 2 nontemporal, 0 none (A/B timing only)
+#define DREPHIP_LK_COLSTORE 1     // column-y stores of a merge step: 1 plain, 2 nontemporal, 3 write-through (sc1),
+                                  // 0 none (A/B timing only)
 #endif
 constexpr uint32_t kLkSmallN = 30000;
 
@@ -684,6 +685,9 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                 // timing-only A/B build: no column-y stores (Z is wrong)
 #elif DREPHIP_LK_COLSTORE == 2
                 __builtin_nontemporal_store(u, &D[(uint64_t)i * n + y]);
+#elif DREPHIP_LK_COLSTORE == 3
+                // write-through (sc1): the line leaves L2 now instead of at the kernel boundary
+                __hip_atomic_store(&D[(uint64_t)i * n + y], u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #else
                 D[(uint64_t)i * n + y] = u;
 #endif

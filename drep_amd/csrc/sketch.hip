@@ -224,14 +224,31 @@ struct MEnt { u32x4 e1; u32x2 f1; u32x4 e2; u32x2 f2; uint64_t k3; };
 // as kernel arguments (sh = 4 | 3 << 8, held in SGPRs): with literal shifts the
 // compiler rematerialised 4 and 3 into VGPRs for the byte-select shifts of
 // every k-mer (two v_mov_b32 each)
+#ifndef DREPHIP_SK_ABLATE
+#define DREPHIP_SK_ABLATE 0
+#endif
 __device__ __forceinline__ MEnt fetch_ent(const SketchTablesQ &tb, uint32_t hi, uint32_t lo, uint32_t sh) {
     const char *base = (const char *)&tb;
+#if DREPHIP_SK_ABLATE
+    // A/B build for the binding-resource measurement (tools/sketch_ablate.py;
+    // never the product): every table index is ANDed with a mask from the
+    // kernel argument -- all ones (real lookups, +5 VALU per k-mer) or zero
+    // (every lane reads entry 0: broadcast, no bank conflicts) -- so the two
+    // runs issue the same instructions and differ only in the LDS bank traffic
+    const uint32_t s16 = sh & 0xfu, s8 = (sh >> 8) & 0xfu, km = sh >> 16;
+    return MEnt{*(const u32x4 *)(base + (((hi >> 24) & km) << s16)),
+                *(const u32x2 *)(base + offsetof(SketchTablesQ, b1) + (((hi >> 16) & km & 0xffu) << s8)),
+                *(const u32x4 *)(base + offsetof(SketchTablesQ, e2) + (((hi >> 8) & km & 0xffu) << s16)),
+                *(const u32x2 *)(base + offsetof(SketchTablesQ, b2) + ((hi & km & 0xffu) << s8)),
+                tb.t3[(lo >> 22) & km]};
+#else
     const uint32_t s16 = sh & 0xffu, s8 = sh >> 8;
     return MEnt{*(const u32x4 *)(base + ((hi >> 24) << s16)),
                 *(const u32x2 *)(base + offsetof(SketchTablesQ, b1) + (((hi >> 16) & 0xffu) << s8)),
                 *(const u32x4 *)(base + offsetof(SketchTablesQ, e2) + (((hi >> 8) & 0xffu) << s16)),
                 *(const u32x2 *)(base + offsetof(SketchTablesQ, b2) + ((hi & 0xffu) << s8)),
                 tb.t3[lo >> 22]};
+#endif
 }
 __device__ __forceinline__ void murmur21_ent(const MEnt &E, uint32_t seed, uint64_t &q1, uint64_t &q2) {
     constexpr uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
@@ -665,6 +682,17 @@ static SketchPlan plan_for(uint32_t s) {
     return p;
 }
 
+// the hash kernel's `sh` argument: the table entry shifts; in the ablation
+// build also the index mask (DREPHIP_SK_KMASK, default all ones)
+static uint32_t sk_shifts() {
+#if DREPHIP_SK_ABLATE
+    const char *m = getenv("DREPHIP_SK_KMASK");
+    return kSketchTabShifts | ((m ? (uint32_t)strtoul(m, nullptr, 0) : 0x3FFu) & 0xFFFFu) << 16;
+#else
+    return kSketchTabShifts;
+#endif
+}
+
 int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t *d_valid,
                        const uint64_t *base_off, const uint64_t *padded, const uint64_t *nkmers,
                        uint32_t n, uint64_t *d_hashes, uint32_t *d_nhash, hipStream_t st,
@@ -794,7 +822,7 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
                 const uint32_t *tbg = tb_tiles_g + t0;
                 hipLaunchKernelGGL((k_sketch_hash21<kHashLane, DREPHIP_SK_BATCH>), dim3(ntc), dim3(kTile / kHashLane), 0, st,
                                    d_img, d_codes, d_valid, tbb, tbg, thr_p, d_sets, d_cnt, plan.set_log2, limit,
-                                   ctx->seed, wlast, kSketchTabShifts);
+                                   ctx->seed, wlast, sk_shifts());
             }
             timing_mark(ctx, 0, st, false);
         }
@@ -838,6 +866,9 @@ int sketch_device_impl(drephip_ctx *ctx, const uint32_t *d_codes, const uint32_t
         }
         HIPC(hipStreamSynchronize(st));
         first = false;
+#if DREPHIP_SK_ABLATE
+        if (getenv("DREPHIP_SK_ONE_ROUND")) { todo.clear(); break; }   // timing only: the first round's kernels
+#endif
         if (getenv("DREPHIP_DEBUG")) {
             uint32_t nu = 0, nd = 0;
             for (uint32_t g : todo) { nu += status[g] == ST_UP; nd += status[g] == ST_DOWN; }

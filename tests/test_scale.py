@@ -46,13 +46,19 @@ pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # (genomes, sketch size, BASELINE.json config)
-CASES = [pytest.param(1_000, 1000, "BASELINE.json configs[1] (the bench workload)", id="1000"),
-         pytest.param(10_000, 1000, "BASELINE.json configs[2] (1 GPU)", id="10000"),
-         pytest.param(100_000, 1000, "BASELINE.json configs[3] (1 GPU)", id="100000"),
-         pytest.param(10_000, 10_000, "BASELINE.json configs[4] (1 GPU)", id="10000-s10000")]
+CASES = [pytest.param(1_000, 1000, 100, "BASELINE.json configs[1] (the bench workload)", id="1000"),
+         pytest.param(10_000, 1000, 100, "BASELINE.json configs[2] (1 GPU)", id="10000"),
+         pytest.param(100_000, 1000, 100, "BASELINE.json configs[3] (1 GPU)", id="100000"),
+         pytest.param(10_000, 10_000, 100, "BASELINE.json configs[4] (1 GPU)", id="10000-s10000"),
+         # dRep's common job: one species, every pair related (a single family
+         # of 10^4 genomes from one ancestor): the screen gives way to the
+         # dense kernel; its attempt is timed against the screen forced off
+         pytest.param(10_000, 1000, 10_000, "configs[2] size, one species (dense: every pair shares hashes)",
+                      id="10000-dense")]
 if os.environ.get("DREPHIP_SCALE_N"):
     _n = int(os.environ["DREPHIP_SCALE_N"])
-    CASES.append(pytest.param(_n, int(os.environ.get("DREPHIP_SCALE_S", 1000)), "custom", id="custom%d" % _n))
+    CASES.append(pytest.param(_n, int(os.environ.get("DREPHIP_SCALE_S", 1000)),
+                              int(os.environ.get("DREPHIP_SCALE_FAM", 100)), "custom", id="custom%d" % _n))
 if os.environ.get("DREPHIP_SCALE_ONLY"):
     CASES = [c for c in CASES if c.id in os.environ["DREPHIP_SCALE_ONLY"].split(",")]
 # scipy's Z digest per workload (test id), committed after a run in which Z
@@ -103,16 +109,15 @@ def full_triangle_check(ctx, hh, nn, N, d_common, note, parts=16):
     return bad, time.perf_counter() - t0, ex
 
 
-@pytest.mark.parametrize("N,s,config", CASES)
+@pytest.mark.parametrize("N,s,fam,config", CASES)
 @pytest.mark.timeout(900)
-def test_scale(N, s, config):
+def test_scale(N, s, fam, config):
     import torch
     L = int(os.environ.get("DREPHIP_SCALE_L", 5_000_000))
-    fam = 100
     seed = 0xD2E9
     CH = min(N, int(os.environ.get("DREPHIP_SCALE_CHUNK", 10000)))
     out_path = os.environ.get("DREPHIP_SCALE_OUT", os.path.join(
-        ROOT, "gpurun_out", "scale_%d%s.json" % (N, "" if s == 1000 else "_s%d" % s)))
+        ROOT, "gpurun_out", "scale_%d%s%s.json" % (N, "" if s == 1000 else "_s%d" % s, "" if fam == 100 else "_dense")))
     os.makedirs(os.path.dirname(out_path), exist_ok=True)
     log = open(os.path.splitext(out_path)[0] + ".progress", "a")
 
@@ -170,12 +175,47 @@ def test_scale(N, s, config):
     npairs = N * (N - 1) // 2
     d_common = torch.zeros(npairs, dtype=torch.int16, device=dev)
     torch.cuda.synchronize()
+    ctx.set_timing(True, kernels=[2, 4])                 # the all-pairs kernels and the screen (HIP events)
     t0 = time.perf_counter()
     ctx.allpairs_device(hh.data_ptr(), nn.data_ptr(), N, 0, N, d_common.data_ptr(), None, stream)
     torch.cuda.synchronize()
     res["allpairs_s"] = time.perf_counter() - t0
     res["allpairs_pairs_per_s"] = npairs / res["allpairs_s"]
-    note("allpairs %.3f s (%.3g pairs/s)" % (res["allpairs_s"], res["allpairs_pairs_per_s"]))
+    res["allpairs_screen"] = ctx.screen_stats()
+    res["allpairs_screen_ms"] = ctx.kernel_ms(4)[0]
+    res["allpairs_kernel_ms"] = ctx.kernel_ms(2)[0]
+    note("allpairs %.3f s (%.3g pairs/s) screen %s (%.2f ms) kernel %.2f ms"
+         % (res["allpairs_s"], res["allpairs_pairs_per_s"], json.dumps(res["allpairs_screen"]),
+            res["allpairs_screen_ms"], res["allpairs_kernel_ms"]))
+    if fam != 100:
+        # the same call with the screen off: what the screen's attempt (runs
+        # counted, then given way to the dense kernel) costs on a dense set
+        d2 = torch.zeros(npairs, dtype=torch.int16, device=dev)
+        ctx.set_allpairs_screen(ctx.SCREEN_OFF)
+        for rep in range(2):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            ctx.allpairs_device(hh.data_ptr(), nn.data_ptr(), N, 0, N, d2.data_ptr(), None, stream)
+            torch.cuda.synchronize()
+        res["allpairs_screen_off_s"] = time.perf_counter() - t0
+        res["allpairs_screen_off_kernel_ms"] = ctx.kernel_ms(2)[0]
+        res["allpairs_screen_off_pairs_per_s"] = npairs / res["allpairs_screen_off_s"]
+        res["dense_kernel_pairs_per_s"] = npairs / (res["allpairs_screen_off_kernel_ms"] * 1e-3)
+        ctx.set_allpairs_screen(ctx.SCREEN_AUTO)
+        assert bool((d2 == d_common).all().item())
+        # and again in auto mode, warm: the screen's attempt before it gives way
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ctx.allpairs_device(hh.data_ptr(), nn.data_ptr(), N, 0, N, d2.data_ptr(), None, stream)
+        torch.cuda.synchronize()
+        res["allpairs_auto_warm_s"] = time.perf_counter() - t0
+        res["allpairs_auto_warm_screen_ms"] = ctx.kernel_ms(4)[0]
+        res["allpairs_auto_warm_kernel_ms"] = ctx.kernel_ms(2)[0]
+        note("dense set: screen off %.3f s (kernel %.2f ms, %.3g pairs/s); auto (warm) %.3f s, screen attempt %.2f ms"
+             % (res["allpairs_screen_off_s"], res["allpairs_screen_off_kernel_ms"], res["dense_kernel_pairs_per_s"],
+                res["allpairs_auto_warm_s"], res["allpairs_auto_warm_screen_ms"]))
+        del d2
+    ctx.set_timing(False)
 
     # ---- parity: the whole triangle against the literal-merge kernel
     nbad, t_full, ex = full_triangle_check(ctx, hh, nn, N, d_common, note)
@@ -246,6 +286,8 @@ def test_scale(N, s, config):
     res["linkage_matrix_build_ms"] = link_ctx.kernel_ms(3)[0]
     res["linkage_chain_ms"] = link_ctx.kernel_ms(2)[0]
     res["linkage_phases_s"] = link_ctx.linkage_stats()
+    res["linkage_chain_launches"] = link_ctx.linkage_launches()
+    res["linkage_launches_per_merge"] = res["linkage_chain_launches"] / (N - 1)
     note("linkage (%s) %.3f s %s %s (matrix reserved in %.2f s beside sketch/all-pairs, waited %.3f s)"
          % ("sparse" if res["linkage_info"]["sparse"] else "dense", res["linkage_s"],
             json.dumps(res["linkage_phases_s"]), json.dumps(res["linkage_info"]),
@@ -270,7 +312,7 @@ def test_scale(N, s, config):
     fcl = sch.fcluster(Z, 0.1, criterion="distance")
     res["primary_clusters_at_P_ani_0.9"] = int(fcl.max())
     res["linkage_sha1"] = z_digest(Z)
-    case = "%d" % N if s == 1000 else "%d-s%d" % (N, s)
+    case = ("%d" % N if s == 1000 else "%d-s%d" % (N, s)) + ("" if fam == 100 else "-dense")
     golden = json.load(open(DIGESTS)).get(case) if os.path.exists(DIGESTS) else None
     res["linkage_sha1_golden"] = golden
     note("Z sha1 %s (golden %s)" % (res["linkage_sha1"], golden))

@@ -19,3 +19,14 @@ for N in ${LINK_NS:-10000 100000}; do
     python3 -c "import json; d=json.load(open('$O/$N.spec$SP.json')); print('N=$N spec=$SP chain ms %.1f / %.1f' % (d['chain_kernel_ms_0'], d['chain_kernel_ms_1']), 'launches %d (%.4f/merge)' % (d['launches_1'], d['launches_per_merge']), 'wall %.3f s' % d['wall_s_1'], 'scipy', d['Z_equals_scipy_digest'])" | tee -a $O/summary.txt
   done
 done
+# column-y store flavour at 10^5 (the merged column leaves ~10^5 dirty lines per merge launch):
+# plain (product) vs write-through sc1 (lib_ab/col3) vs nontemporal (lib_ab/col2), interleaved
+if [ "${COLSTORE_AB:-1}" = 1 ]; then
+for LIB in default col3 col2 default col3; do
+  if [ $LIB = default ]; then unset DREPHIP_LIB; else export DREPHIP_LIB=drep_amd/lib_ab/$LIB/libdrephip.so; fi
+  timeout -k 10 400 python tools/link_ab.py 100000 > $O/col_$LIB.json 2> $O/col_$LIB.err \
+      || { echo "colstore $LIB failed"; grep -v amdgpu.ids $O/col_$LIB.err | tail -5; exit 1; }
+  python3 -c "import json; d=json.load(open('$O/col_$LIB.json')); print('colstore $LIB N=100000 chain ms %.1f / %.1f' % (d['chain_kernel_ms_0'], d['chain_kernel_ms_1']), 'launches %d' % d['launches_1'], 'scipy', d['Z_equals_scipy_digest'])" | tee -a $O/summary.txt
+done
+unset DREPHIP_LIB
+fi
