@@ -288,7 +288,7 @@ constexpr int32_t kLkDecide = 1, kLkBad = 2;
 // load + store per launch; never in the product build)
 struct LinkDiag { int32_t twice, scans, specwin, known, m0, wmerge, recip; };
 __device__ LinkDiag *g_lk_diag;
-#define LK_DIAG(field) do { if (w0l) g_lk_diag->field++; } while (0)
+#define LK_DIAG(field) do { if (w0l) g_lk_diag->field++; } while (0)   // (a divergent store: diagnostic builds only)
 #else
 #define LK_DIAG(field) (void)0
 #endif
@@ -307,8 +307,11 @@ struct alignas(64) LinkFwd {
     int32_t szt, szb, c3, c4;
     double dp2;                   // D[w][c4], w = c3 (the speculation's decision operand)
     int32_t spec;                 // 1: the P2 partials hold a speculated merged row's minimum, P3 the row below's
+    int32_t c5, c6;               // chain[len - 5], chain[len - 6]: chain[len - 3], chain[len - 4] after a merge
+                                  // (a known merge's row W and its decision operand D[W][below W])
 };
-static_assert(offsetof(LinkFwd, dp2) == 24 && offsetof(LinkFwd, spec) == 32, "LinkFwd word layout (fwd_from_words)");
+static_assert(offsetof(LinkFwd, dp2) == 24 && offsetof(LinkFwd, spec) == 32 && offsetof(LinkFwd, c6) == 40,
+              "LinkFwd word layout (fwd_from_words)");
 
 // a uniform 32-bit word held in a VGPR -> SGPR
 __device__ __forceinline__ int32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane((int32_t)v); }
@@ -325,7 +328,7 @@ __device__ __forceinline__ LinkFwd fwd_from_words(uint4 a, uint4 b, uint4 c) {
     F.dp = __longlong_as_double((long long)(((uint64_t)(uint32_t)rfl(a.y) << 32) | (uint32_t)rfl(a.x)));
     F.szt = rfl(a.z); F.szb = rfl(a.w); F.c3 = rfl(b.x); F.c4 = rfl(b.y);
     F.dp2 = __longlong_as_double((long long)(((uint64_t)(uint32_t)rfl(b.w) << 32) | (uint32_t)rfl(b.z)));
-    F.spec = rfl(c.x);
+    F.spec = rfl(c.x); F.c5 = rfl(c.y); F.c6 = rfl(c.z);
     return F;
 }
 
@@ -410,7 +413,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                  "+v"(sw1.w), "+v"(sw2.x), "+v"(sw2.y), "+v"(sw2.z), "+v"(sw2.w), "+v"(sw3.x), "+v"(sw3.y),
                  "+v"(sw3.z), "+v"(sw3.w));
     asm volatile("" : "+v"(fw0.x), "+v"(fw0.y), "+v"(fw0.z), "+v"(fw0.w), "+v"(fw1.x), "+v"(fw1.y), "+v"(fw1.z),
-                 "+v"(fw1.w), "+v"(fw2.x));
+                 "+v"(fw1.w), "+v"(fw2.x), "+v"(fw2.y), "+v"(fw2.z));
     const LinkState S = state_from_words(sw0, sw1, sw2, sw3);
     const LinkFwd F = fwd_from_words(fw0, fw1, fw2);
 #if DREPHIP_LK_PHASES
@@ -435,11 +438,21 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
         int32_t k = S.k, len = S.len, top = S.top, below = S.below, first_active = S.first_active;
         int32_t pend = 0, px = S.x, py = S.y, pnx = S.nx, pny = S.ny, bad = S.flags & kLkBad, known = 0;
         const int32_t mrow = S.pend ? S.y : -1;                // the row the previous launch's merge formed
-        // c3, c4: chain[len - 3], chain[len - 4]; ck of them are known exactly
-        // (a merge exposes entries only the chain in memory holds; a push
-        // shifts known ones down)
-        int32_t c3 = F.c3, c4 = F.c4, ck = 2, dpo = 0;
+        // c3..c6: chain[len - 3] .. chain[len - 6]; the first ck of them are
+        // known exactly (a merge exposes two entries only the chain in memory
+        // holds; a push shifts known ones down)
+        int32_t c3 = F.c3, c4 = F.c4, c5 = F.c5, c6 = F.c6, ck = 4, dpo = 0;
         double dpov = 0.0;
+        // the decision's stores (Z row, chain pushes, a restart) are recorded
+        // here and made by lane 0 of workgroup 0 after it: a lane-divergent
+        // store inside the decision made the compiler keep the whole decision
+        // in VGPRs under exec masks instead of scalar code
+        int32_t zmerge = 0, za = 0, zb = 0, zn = 0, npush = 0, pp0 = 0, pv0 = 0, pp1 = 0, pv1 = 0, restart = -1;
+        double zd = 0.0;
+        auto push_rec = [&](int32_t pos, int32_t v) {
+            if (npush == 0) { pp0 = pos; pv0 = v; } else { pp1 = pos; pv1 = v; }
+            npush++;
+        };
         if (S.flags & kLkDecide) {
             int32_t szt = F.szt, szb = F.szb;
             double dp = F.dp;
@@ -452,22 +465,20 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                 if (kn || (len > 1 && !(r.v < dp))) {              // merge top with below at dp
                     int32_t a = top, b = below, na = szt, nb = szb;
                     if (a > b) { a = below; b = top; na = szb; nb = szt; }
-                    if (w0l) {
-                        double *z = Z + 4ull * S.k;
-                        z[0] = a; z[1] = b; z[2] = dp; z[3] = na + nb;
-                    }
+                    zmerge = 1; za = a; zb = b; zd = dp; zn = na + nb;
                     pend = 1; px = a; py = b; pnx = na; pny = nb;
-                    ck = 0;
                     k = S.k + 1;
                     len -= 2;
                     top = c3;
                     below = len >= 2 ? c4 : -1;
+                    c3 = c5; c4 = c6;                               // (ck is 4 at either merge: at d = 0,
+                    ck = ck - 2;                                    // or after one push)
                     if (len == 0 && k < (int32_t)n - 1) {           // restart at the first active cluster
                         int32_t f = S.first_active;
                         while (f < (int32_t)n && !(f == b || (f != a && size_prev(f, size[f]) > 0))) f++;
                         if (f >= (int32_t)n) { bad = kLkBad; k = (int32_t)n - 1; }
                         else {
-                            if (w0l) chain[0] = f;
+                            restart = f;
                             first_active = f; top = f; below = -1; len = 1;
                         }
                     } else if (d == 0 && F.spec && len >= 1 && k < (int32_t)n - 1) {
@@ -488,15 +499,15 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                         const bool wpush = r3ok && !wmerge && len + 1 < (int32_t)n;
                         const bool bpush = r3.i == b && (uint32_t)g2.i < n && g2.v < r3.v;
                         if (wpush && (r3.i != b || bpush)) {
-                            if (w0l) chain[len] = r3.i;                 // w pushes r3.i
-                            c4 = c3; c3 = below; below = top; top = r3.i;
-                            ck = ck >= 1 ? 2 : 1;
+                            push_rec(len, r3.i);                        // w pushes r3.i
+                            c6 = c5; c5 = c4; c4 = c3; c3 = below; below = top; top = r3.i;
+                            ck = ck >= 4 ? 4 : ck + 1;
                             len++;
                             LK_DIAG(specwin);
                             if (bpush) {
-                                if (w0l) chain[len] = g2.i;             // b pushes g2.i
-                                c4 = c3; c3 = below; below = top; top = g2.i;
-                                ck = ck >= 1 ? 2 : 1;
+                                push_rec(len, g2.i);                    // b pushes g2.i
+                                c6 = c5; c5 = c4; c4 = c3; c3 = below; below = top; top = g2.i;
+                                ck = ck >= 4 ? 4 : ck + 1;
                                 len++;
                                 dpo = 1; dpov = g2.v;                   // D[g2.i][b] as this launch writes it
                             }
@@ -504,9 +515,9 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                             known = 1;                                  // w merges with the element below it
                             LK_DIAG(wmerge);
                         } else if (wpush && r3.i == b && spec_on > 1) {
-                            if (w0l) chain[len] = b;                    // w pushes b, b merges back with w
-                            c4 = c3; c3 = below; below = top; top = b;
-                            ck = ck >= 1 ? 2 : 1;
+                            push_rec(len, b);                           // w pushes b, b merges back with w
+                            c6 = c5; c5 = c4; c4 = c3; c3 = below; below = top; top = b;
+                            ck = ck >= 4 ? 4 : ck + 1;
                             len++;
                             dpo = 1; dpov = r3.v;                       // D[b][w] as this launch writes it
                             known = 1;
@@ -517,9 +528,9 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                 }
                 // push (scipy: the previous element wins ties)
                 if (len >= (int32_t)n) { bad = kLkBad; k = (int32_t)n - 1; break; }
-                if (w0l) chain[len] = r.i;
-                c4 = c3; c3 = below; below = top; top = r.i;
-                ck = ck >= 1 ? 2 : 1;
+                push_rec(len, r.i);
+                c6 = c5; c5 = c4; c4 = c3; c3 = below; below = top; top = r.i;
+                ck = ck >= 4 ? 4 : ck + 1;
                 dp = r.v;
                 szb = szt;
                 len++;
@@ -552,6 +563,13 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
         if (lane0) sx = X;
         LK_T(ph2);
         if (w0l) {
+            if (zmerge) {
+                double *z = Z + 4ull * S.k;
+                z[0] = za; z[1] = zb; z[2] = zd; z[3] = zn;
+            }
+            if (restart >= 0) chain[0] = restart;
+            if (npush > 0) chain[pp0] = pv0;
+            if (npush > 1) chain[pp1] = pv1;
             st[q] = X;
             if (X.k >= (int32_t)n - 1) st[q ^ 1] = X;           // the finished state in both buffers
             *done = X.k;
@@ -561,18 +579,23 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             // load is issued before any is waited for (one round trip): the
             // chain entries read are below this launch's pushes, and a spec
             // launch (no merge) knows c3 and c4 (ck = 2), so D[c3][c4] needs none
-            const bool two = len > 1, l3 = len >= 3 && ck < 1, l4 = len >= 4 && ck < 2;
-            const bool sp = X.spec && len >= 4;
+            const bool two = len > 1, l3 = len >= 3 && ck < 1, l4 = len >= 4 && ck < 2, l5 = len >= 5 && ck < 3,
+                       l6 = len >= 6 && ck < 4;
+            // D[c3][c4], the speculation's decision operand: c3 and c4 are
+            // known in every spec launch (ck >= 2: pushes, or a merge with
+            // c5 and c6 forwarded)
+            const bool sp = X.spec && len >= 4 && ck >= 2;
             int32_t rzt = size[top], rzb = size[two ? below : top];
             double rdp = D[(uint64_t)top * n + (two ? below : top)];
-            int32_t r3 = chain[l3 ? len - 3 : 0], r4 = chain[l4 ? len - 4 : 0];
+            int32_t r3 = chain[l3 ? len - 3 : 0], r4 = chain[l4 ? len - 4 : 0], r5 = chain[l5 ? len - 5 : 0],
+                    r6 = chain[l6 ? len - 6 : 0];
             double rdp2 = D[sp ? (uint64_t)c3 * n + c4 : 0];
-            asm volatile("" : "+v"(rzt), "+v"(rzb), "+v"(rdp), "+v"(r3), "+v"(r4), "+v"(rdp2));
+            asm volatile("" : "+v"(rzt), "+v"(rzb), "+v"(rdp), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(rdp2));
             LK_T(ph3);
             auto size_now = [&](int32_t i, int32_t stored) {
                 return pend && i == px ? 0 : pend && i == py ? pnx + pny : size_prev(i, stored);
             };
-            LinkFwd f{0.0, 0, 0, 0, 0};
+            LinkFwd f{};
             f.szt = size_now(top, rzt);                         // (also at len 1: a push and a merge may follow)
             if (two) {
                 f.dp = dpo ? dpov : rdp;
@@ -580,6 +603,8 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             }
             if (len >= 3) f.c3 = ck >= 1 ? c3 : r3;
             if (len >= 4) f.c4 = ck >= 2 ? c4 : r4;
+            if (len >= 5) f.c5 = ck >= 3 ? c5 : r5;
+            if (len >= 6) f.c6 = ck >= 4 ? c6 : r6;
             if (X.spec) {
                 f.dp2 = sp ? rdp2 : 0.0;                        // D[w][c4], w = c3
                 f.spec = 1;

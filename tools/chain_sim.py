@@ -25,7 +25,8 @@ INF = np.inf
 
 
 class Sim:
-    def __init__(self, D, policy="r4"):
+    def __init__(self, D, policy="r4", method="average"):
+        self.method = method
         self.D = D
         self.n = n = D.shape[0]
         self.size = np.ones(n, dtype=np.int64)
@@ -45,7 +46,11 @@ class Sim:
     def active(self):
         return self.size > 0
 
-    def lw(self, dx, dy, nx, ny):       # average linkage, scipy's rounding
+    def lw(self, dx, dy, nx, ny):       # scipy's Lance-Williams updates and rounding
+        if self.method == "complete":
+            return np.maximum(dx, dy)
+        if self.method == "weighted":
+            return 0.5 * (dx + dy)
         return (nx * dx + ny * dy) / float(nx + ny)
 
     def apply_merge(self, a, b):
