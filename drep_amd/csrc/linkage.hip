@@ -43,9 +43,18 @@ namespace drephip {
 // per row at small n: 136 vs 143 ms of chain at n = 10^4; 256 is faster at
 // 10^5 -- profiles/r03_linkage_wg_ab.txt)
 constexpr int kLkWG = 256;
+// Column-y stores of a merge step: 3 write-through (sc1, default), 1 plain, 2
+// nontemporal, 0 none (A/B timing only).  A merge leaves one dirty line per
+// row of column y (10^5 lines = 6.4 MB at n = 10^5) that a plain store leaves
+// in L2 until the kernel boundary's write-back (~1 us at ~6 TB/s on the chain's
+// critical path); written through, the lines leave during the step: chain at
+// 10^5 967 -> 917 ms (nontemporal 945 ms; profiles/r05_linkage_protocol_colstore_ab.txt)
 #ifndef DREPHIP_LK_COLSTORE
-#define DREPHIP_LK_COLSTORE 1     // column-y stores of a merge step: 1 plain, 2 nontemporal, 3 write-through (sc1),
-                                  // 0 none (A/B timing only)
+#define DREPHIP_LK_COLSTORE 3
+#endif
+// Row-y stores (contiguous, 8n bytes per merge): 1 plain (default), 3 write-through (A/B)
+#ifndef DREPHIP_LK_ROWSTORE
+#define DREPHIP_LK_ROWSTORE 1
 #endif
 constexpr uint32_t kLkSmallN = 30000;
 
@@ -315,6 +324,11 @@ static_assert(offsetof(LinkFwd, dp2) == 24 && offsetof(LinkFwd, spec) == 32 && o
 
 // a uniform 32-bit word held in a VGPR -> SGPR
 __device__ __forceinline__ int32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane((int32_t)v); }
+__device__ __forceinline__ MinIdx uni(MinIdx m) {       // a wave-uniform (value, index) into SGPRs
+    const uint64_t b = (uint64_t)__double_as_longlong(m.v);
+    const uint32_t lo = (uint32_t)rfl((uint32_t)b), hi = (uint32_t)rfl((uint32_t)(b >> 32));
+    return MinIdx{__longlong_as_double((long long)(((uint64_t)hi << 32) | lo)), rfl((uint32_t)m.i)};
+}
 __device__ __forceinline__ LinkState state_from_words(uint4 a, uint4 b, uint4 c, uint4 d) {
     LinkState S;
     S.k = rfl(a.x); S.len = rfl(a.y); S.top = rfl(a.z); S.below = rfl(a.w);
@@ -433,6 +447,11 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     // in every workgroup; its stores by lane 0 of workgroup 0)
     const bool w0l = w0 && lane0;
     if (wave0) {
+        // The partial minima as scalars: g .. g3 are per-lane values in the
+        // other waves, so after the `if (wave0)` above the compiler held them
+        // (and everything the decision derives from them) in VGPRs under exec
+        // masks -- ~1,000 cycles of one wave's vector code per launch
+        g = uni(g); g2 = uni(g2); g3 = uni(g3);
         // (plain scalars, the state struct written once at the end: a struct
         // updated across the branches was kept in private memory)
         int32_t k = S.k, len = S.len, top = S.top, below = S.below, first_active = S.first_active;
@@ -475,7 +494,9 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                     ck = ck - 2;                                    // or after one push)
                     if (len == 0 && k < (int32_t)n - 1) {           // restart at the first active cluster
                         int32_t f = S.first_active;
-                        while (f < (int32_t)n && !(f == b || (f != a && size_prev(f, size[f]) > 0))) f++;
+                        // (the loaded size read into an SGPR: a VGPR load result in this loop
+                        // made the compiler treat the whole decision as divergent)
+                        while (f < (int32_t)n && !(f == b || (f != a && size_prev(f, rfl((uint32_t)size[f])) > 0))) f++;
                         if (f >= (int32_t)n) { bad = kLkBad; k = (int32_t)n - 1; }
                         else {
                             restart = f;
@@ -705,7 +726,11 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             double u = 0.0;
             if (pend && i != y) {
                 u = lw_update(method, dx[k], dy[k], nx, ny);
+#if DREPHIP_LK_ROWSTORE == 3
+                __hip_atomic_store(&Dy[i], u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
                 Dy[i] = u;
+#endif
 #if DREPHIP_LK_COLSTORE == 0
                 // timing-only A/B build: no column-y stores (Z is wrong)
 #elif DREPHIP_LK_COLSTORE == 2
