@@ -86,6 +86,8 @@ __device__ __forceinline__ bool better(double v, int32_t i, double bv, int32_t b
 // every operation rounded on its own, as in scipy's x86-64 build (this file is
 // compiled with -ffp-contract=off; see the Makefile)
 __device__ __forceinline__ double lw_update(int method, double dxi, double dyi, int32_t nx, int32_t ny) {
+    // (method is a template argument of the step kernels: the switch folds away;
+    // as a runtime argument every update in the row pass branched three ways)
     if (method == DREPHIP_LINK_COMPLETE) return fmax(dxi, dyi);
     if (method == DREPHIP_LINK_WEIGHTED) return __dmul_rn(0.5, __dadd_rn(dxi, dyi));
     // average: (size_x * d_xi + size_y * d_yi) / (size_x + size_y)
@@ -385,8 +387,8 @@ __device__ __forceinline__ MinIdx read_partials(const MinIdx *parts, uint32_t G)
 //           launches per merge 1.318 -> 1.225 at 10^4 (tools/chain_sim.py,
 //           the host model of this protocol, Z identical to scipy's).
 // One merge per launch stays the rule.
-template <int WG, int kLkPer>
-__global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t n, int method,
+template <int WG, int kLkPer, int method>
+__global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t n,
                                                    int32_t *__restrict__ size, int32_t *__restrict__ chain,
                                                    LinkState *__restrict__ st, LinkFwd *__restrict__ fwd,
                                                    MinIdx *__restrict__ parts, MinIdx *__restrict__ parts2,
@@ -949,6 +951,19 @@ static void launch_dist_tiles_condensed(const DmFromCondensed &v, uint32_t n, do
 
 // ------------------------------------------------------------- host driver
 // (sort_and_label: linkage_sparse.cpp, shared with the sparse path)
+struct NnArgs {
+    double *D; uint32_t n; int32_t *size, *chain; LinkState *st; LinkFwd *fwd;
+    MinIdx *parts, *parts2, *parts3; int32_t *done; double *Z; uint32_t q; int spec_on;
+};
+template <int W, int P>
+static void launch_nn(int method, dim3 grid, dim3 blk, hipStream_t st, const NnArgs &a) {
+#define DREPHIP_LK_NN(M) hipLaunchKernelGGL((k_nn_step<W, P, M>), grid, blk, 0, st, a.D, a.n, a.size, a.chain, a.st, \
+                                            a.fwd, a.parts, a.parts2, a.parts3, a.done, a.Z, a.q, a.spec_on)
+    if (method == DREPHIP_LINK_COMPLETE) DREPHIP_LK_NN(DREPHIP_LINK_COMPLETE);
+    else if (method == DREPHIP_LINK_WEIGHTED) DREPHIP_LK_NN(DREPHIP_LINK_WEIGHTED);
+    else DREPHIP_LK_NN(DREPHIP_LINK_AVERAGE);
+#undef DREPHIP_LK_NN
+}
 int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, double *Z_out, hipStream_t st) {
     if (n < 2) return DREPHIP_OK;
     const double t_chain = now_s();           // chain_s: scratch, graph capture and the steps
@@ -977,10 +992,11 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     const char *wge = getenv("DREPHIP_LINK_WG");
     const int wreq = wge ? atoi(wge) : 0;
     const bool wave_wg = method != DREPHIP_LINK_SINGLE && (wreq == 64 || (wreq == 0 && !pl && n <= kLkWaveN));
-    const uint32_t wsz = wave_wg ? 64 : kLkWG;
+    const uint32_t wsz = wave_wg ? 64 : wreq == 512 && method != DREPHIP_LINK_SINGLE ? 512 : kLkWG;
     const uint32_t per = pl ? std::max(1, std::min(64, atoi(pl)))
                             : std::max(1u, (n + wsz * kLkTarget - 1) / (wsz * kLkTarget));
-    const uint32_t wg = wave_wg ? 64 : wreq == 128 || wreq == 256 ? (uint32_t)wreq : n <= kLkSmallN && !pl ? 128 : kLkWG;
+    const uint32_t wg = wave_wg ? 64 : wreq == 128 || wreq == 256 || (wreq == 512 && method != DREPHIP_LINK_SINGLE)
+                                           ? (uint32_t)wreq : n <= kLkSmallN && !pl ? 128 : kLkWG;
     const uint32_t grid = std::max(1u, std::min(1024u, (n + wg * per - 1) / (wg * per)));
     const int tpl = per <= 1 ? 1 : per <= 2 ? 2 : per <= 4 || !wave_wg ? 4 : 8;     // entries per lane per pass
     int32_t *d_size, *d_chain, *d_done;
@@ -1052,26 +1068,25 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     for (int b = 0; b < kBatch; b++) {
         const uint32_t q = (uint32_t)(b & 1);
         const dim3 gm(grid), gn(grid + 1), blk(wg);
+        const NnArgs a{d_D, n, d_size, d_chain, d_st, d_fwd, d_parts, d_parts2, d_parts3, d_done, d_Z, q, spec_on};
 #define DREPHIP_LK_LAUNCH(W, P)                                                                                      \
     do {                                                                                                         \
         if (mst) hipLaunchKernelGGL((k_mst_step<W, P>), gm, blk, 0, st, d_D, n, d_size, d_Dmin, d_st, d_parts, d_done, \
                                     d_Z, q);                                                                     \
-        else hipLaunchKernelGGL((k_nn_step<W, P>), gn, blk, 0, st, d_D, n, method, d_size, d_chain, d_st, d_fwd,    \
-                                d_parts, d_parts2, d_parts3, d_done, d_Z, q, spec_on);                           \
+        else launch_nn<W, P>(method, gn, blk, st, a);                                                            \
     } while (0)
         if (wg == 64) {
-#define DREPHIP_LK_LAUNCH64(P)                                                                                   \
-    hipLaunchKernelGGL((k_nn_step<64, P>), gn, blk, 0, st, d_D, n, method, d_size, d_chain, d_st, d_fwd, d_parts, \
-                       d_parts2, d_parts3, d_done, d_Z, q, spec_on)
-            if (tpl == 1) DREPHIP_LK_LAUNCH64(1);
-            else if (tpl == 2) DREPHIP_LK_LAUNCH64(2);
-            else if (tpl == 4) DREPHIP_LK_LAUNCH64(4);
-            else DREPHIP_LK_LAUNCH64(8);
-#undef DREPHIP_LK_LAUNCH64
+            if (tpl == 1) launch_nn<64, 1>(method, gn, blk, st, a);
+            else if (tpl == 2) launch_nn<64, 2>(method, gn, blk, st, a);
+            else if (tpl == 4) launch_nn<64, 4>(method, gn, blk, st, a);
+            else launch_nn<64, 8>(method, gn, blk, st, a);
         } else if (wg == 128) {
             if (tpl == 1) DREPHIP_LK_LAUNCH(128, 1);
             else if (tpl == 2) DREPHIP_LK_LAUNCH(128, 2);
             else DREPHIP_LK_LAUNCH(128, 4);
+        } else if (wg == 512 && !mst) {
+            if (tpl == 1) launch_nn<512, 1>(method, gn, blk, st, a);
+            else launch_nn<512, 2>(method, gn, blk, st, a);
         } else {
             if (tpl == 1) DREPHIP_LK_LAUNCH(256, 1);
             else if (tpl == 2) DREPHIP_LK_LAUNCH(256, 2);
