@@ -156,9 +156,15 @@ __device__ __forceinline__ void wave_argmin(double &v, int32_t &i) {
     wave_argmin_n<1>(vv, ii);
     v = vv[0]; i = ii[0];
 }
-// one, two or three sets (block-uniform counts), interleaved
-__device__ __forceinline__ void wave_argmin_upto3(MinIdx &a, MinIdx &b, MinIdx &c, bool with_b, bool with_c) {
-    if (with_c) {
+// one to four sets (block-uniform counts; d implies b and c), interleaved
+__device__ __forceinline__ void wave_argmin_upto4(MinIdx &a, MinIdx &b, MinIdx &c, MinIdx &d, bool with_b, bool with_c,
+                                                  bool with_d) {
+    if (with_d) {
+        double v[4] = {a.v, b.v, c.v, d.v};
+        int32_t i[4] = {a.i, b.i, c.i, d.i};
+        wave_argmin_n<4>(v, i);
+        a = MinIdx{v[0], i[0]}; b = MinIdx{v[1], i[1]}; c = MinIdx{v[2], i[2]}; d = MinIdx{v[3], i[3]};
+    } else if (with_c) {
         double v[3] = {a.v, b.v, c.v};
         int32_t i[3] = {a.i, b.i, c.i};
         wave_argmin_n<3>(v, i);
@@ -192,23 +198,26 @@ __device__ MinIdx block_argmin(double v, int32_t i) {
 // A lane's share of the previous launch's partial sets: partials lane,
 // lane + 64, ... U at a time, every load in flight before the first wait
 template <int U>
-__device__ __forceinline__ void partial_pass(const MinIdx *P1, const MinIdx *P2, const MinIdx *P3, uint32_t G,
-                                             MinIdx &g, MinIdx &g2, MinIdx &g3) {
+__device__ __forceinline__ void partial_pass(const MinIdx *P1, const MinIdx *P2, const MinIdx *P3, const MinIdx *P4,
+                                             uint32_t G, MinIdx &g, MinIdx &g2, MinIdx &g3, MinIdx &g4) {
     for (uint32_t b0 = threadIdx.x; b0 < G; b0 += 64 * U) {
-        MinIdx m1[U], m2[U], m3[U];
+        MinIdx m1[U], m2[U], m3[U], m4[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const uint32_t b = min(b0 + 64u * u, G - 1);             // (a repeated partial changes no minimum)
-            m1[u] = P1[b]; m2[u] = P2[b]; m3[u] = P3[b];
+            m1[u] = P1[b]; m2[u] = P2[b]; m3[u] = P3[b]; m4[u] = P4[b];
         }
 #pragma unroll
-        for (int u = 0; u < U; u++)
+        for (int u = 0; u < U; u++) {
             asm volatile("" : "+v"(m1[u].v), "+v"(m1[u].i), "+v"(m2[u].v), "+v"(m2[u].i), "+v"(m3[u].v), "+v"(m3[u].i));
+            asm volatile("" : "+v"(m4[u].v), "+v"(m4[u].i));
+        }
 #pragma unroll
         for (int u = 0; u < U; u++) {
             if (better(m1[u].v, m1[u].i, g.v, g.i)) g = m1[u];
             if (better(m2[u].v, m2[u].i, g2.v, g2.i)) g2 = m2[u];
             if (better(m3[u].v, m3[u].i, g3.v, g3.i)) g3 = m3[u];
+            if (better(m4[u].v, m4[u].i, g4.v, g4.i)) g4 = m4[u];
         }
     }
 }
@@ -218,24 +227,26 @@ __device__ __forceinline__ void partial_pass(const MinIdx *P1, const MinIdx *P2,
 // are reduced only when the (block-uniform) flags ask for them: an unneeded
 // wave reduction measured as costly as the barrier it saves.
 template <int WG>
-__device__ void block_argmin3(MinIdx &a, MinIdx &b, MinIdx &c, bool with_b, bool with_c) {
-    __shared__ double sv[3][WG / 64];
-    __shared__ int32_t si[3][WG / 64];
-    wave_argmin_upto3(a, b, c, with_b, with_c);
+__device__ void block_argmin4(MinIdx &a, MinIdx &b, MinIdx &c, MinIdx &d, bool with_b, bool with_c, bool with_d) {
+    __shared__ double sv[4][WG / 64];
+    __shared__ int32_t si[4][WG / 64];
+    wave_argmin_upto4(a, b, c, d, with_b, with_c, with_d);
     if constexpr (WG == 64) return;                            // one wave: every lane holds the result
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
         sv[0][w] = a.v; si[0][w] = a.i;
         sv[1][w] = b.v; si[1][w] = b.i;
         sv[2][w] = c.v; si[2][w] = c.i;
+        sv[3][w] = d.v; si[3][w] = d.i;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        a = b = c = MinIdx{INFINITY, 0x7fffffff};
+        a = b = c = d = MinIdx{INFINITY, 0x7fffffff};
         for (int k = 0; k < WG / 64; k++) {
             if (better(sv[0][k], si[0][k], a.v, a.i)) { a.v = sv[0][k]; a.i = si[0][k]; }
             if (better(sv[1][k], si[1][k], b.v, b.i)) { b.v = sv[1][k]; b.i = si[1][k]; }
             if (better(sv[2][k], si[2][k], c.v, c.i)) { c.v = sv[2][k]; c.i = si[2][k]; }
+            if (better(sv[3][k], si[3][k], d.v, d.i)) { d.v = sv[3][k]; d.i = si[3][k]; }
         }
     }
 }
@@ -392,9 +403,15 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                                                    int32_t *__restrict__ size, int32_t *__restrict__ chain,
                                                    LinkState *__restrict__ st, LinkFwd *__restrict__ fwd,
                                                    MinIdx *__restrict__ parts, MinIdx *__restrict__ parts2,
-                                                   MinIdx *__restrict__ parts3, int32_t *__restrict__ done,
-                                                   double *__restrict__ Z, uint32_t q, int spec_on) {
+                                                   MinIdx *__restrict__ parts3, MinIdx *__restrict__ parts4,
+                                                   int32_t *__restrict__ done, double *__restrict__ Z, uint32_t q,
+                                                   int spec_on) {
     __shared__ LinkState sx;
+    // every kernel argument into SGPRs with the first argument loads: left to
+    // itself the compiler loaded n and the pointers the decision uses in the
+    // middle of it, each load a scalar-cache round trip on the critical path
+    asm volatile("" ::"s"(D), "s"(n), "s"(size), "s"(chain), "s"(st), "s"(fwd), "s"(parts), "s"(parts2), "s"(parts3),
+                 "s"(parts4), "s"(done), "s"(Z), "s"(q), "s"(spec_on));
     const uint32_t G = gridDim.x - 1;                          // step workgroups; workgroup G forwards operands
     // The partial sets are reduced by wave 0 alone (the decision is wave 0's:
     // no barrier), read whether or not they are needed (valid memory either
@@ -408,7 +425,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     // runs on every lane of wave 0 as scalar code, its values in SGPRs (as
     // one lane's divergent code it took ~0.8 us a launch)
     const bool wave0 = __builtin_amdgcn_readfirstlane(threadIdx.x) < 64, lane0 = threadIdx.x == 0;
-    MinIdx g{INFINITY, 0x7fffffff}, g2{INFINITY, 0x7fffffff}, g3{INFINITY, 0x7fffffff};
+    MinIdx g{INFINITY, 0x7fffffff}, g2{INFINITY, 0x7fffffff}, g3{INFINITY, 0x7fffffff}, g4{INFINITY, 0x7fffffff};
     // state and forwarded operands: vector loads through an opaque zero lane
     // offset, issued first, so the partial loads go out behind them and one
     // wait covers both (as scalar loads, a state field landing in a scalar
@@ -421,9 +438,9 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     uint4 sw0 = sv[0], sw1 = sv[1], sw2 = sv[2], sw3 = sv[3], fw0 = fv[0], fw1 = fv[1], fw2 = fv[2];
     if (wave0) {
         const MinIdx *P1 = parts + (uint64_t)(q ^ 1) * 1024, *P2 = parts2 + (uint64_t)(q ^ 1) * 1024,
-                     *P3 = parts3 + (uint64_t)(q ^ 1) * 1024;
-        if (G <= 256) partial_pass<4>(P1, P2, P3, G, g, g2, g3);
-        else partial_pass<8>(P1, P2, P3, G, g, g2, g3);              // (up to 512 workgroups in one pass)
+                     *P3 = parts3 + (uint64_t)(q ^ 1) * 1024, *P4 = parts4 + (uint64_t)(q ^ 1) * 1024;
+        if (G <= 256) partial_pass<4>(P1, P2, P3, P4, G, g, g2, g3, g4);
+        else partial_pass<8>(P1, P2, P3, P4, G, g, g2, g3, g4);      // (up to 512 workgroups in one pass)
     }
     asm volatile("" : "+v"(sw0.x), "+v"(sw0.y), "+v"(sw0.z), "+v"(sw0.w), "+v"(sw1.x), "+v"(sw1.y), "+v"(sw1.z),
                  "+v"(sw1.w), "+v"(sw2.x), "+v"(sw2.y), "+v"(sw2.z), "+v"(sw2.w), "+v"(sw3.x), "+v"(sw3.y),
@@ -436,7 +453,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     uint64_t ph0 = 0, ph1 = 0, ph2 = 0, ph3 = 0, ph4 = 0, ph5 = 0, ph6 = 0;
 #endif
     LK_T(ph0);
-    if (wave0) wave_argmin_upto3(g, g2, g3, S.pend || F.spec, F.spec != 0);
+    if (wave0) wave_argmin_upto4(g, g2, g3, g4, S.pend || F.spec, F.spec != 0, S.spec == 4);
     LK_T(ph1);
     if (S.k >= (int32_t)n - 1) return;                         // all merged
     const bool w0 = blockIdx.x == 0;
@@ -453,7 +470,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
         // other waves, so after the `if (wave0)` above the compiler held them
         // (and everything the decision derives from them) in VGPRs under exec
         // masks -- ~1,000 cycles of one wave's vector code per launch
-        g = uni(g); g2 = uni(g2); g3 = uni(g3);
+        g = uni(g); g2 = uni(g2); g3 = uni(g3); g4 = uni(g4);
         // (plain scalars, the state struct written once at the end: a struct
         // updated across the branches was kept in private memory)
         int32_t k = S.k, len = S.len, top = S.top, below = S.below, first_active = S.first_active;
@@ -559,7 +576,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                 len++;
                 if (r.i != mrow || mrow < 0 || d == 1) break;      // the pushed row is searched by this launch
                 szt = spsbsz;                                       // y: just formed, its size is the override
-                r = g2;                                             // y's minimum, from the merge step
+                r = S.spec == 4 ? g4 : g2;                          // y's minimum, from the merge step
                 LK_DIAG(twice);
             }
         }
@@ -578,6 +595,8 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
         } else if (spec_on && len >= 3 && k < (int32_t)n - 1) {
             if (!pend) X.spec = 1;                              // a search launch
             else if (below == py && top != py) X.spec = 2;      // a merge launch, its row y below the top
+            else if (spec_on > 2) X.spec = 4;                   // any other merge launch (round 5): speculate,
+                                                                // y's own minimum in P4 for a push of y
         }
 #if DREPHIP_LK_DIAG
         if (!pend) LK_DIAG(scans);
@@ -677,8 +696,9 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     auto size_x = [&](int32_t i, int32_t stored) {
         return pend && i == x ? 0 : pend && i == y ? nx + ny : size_prev(i, stored);
     };
-    double bv = INFINITY, yv = INFINITY, wv = INFINITY;
-    int32_t bi = 0x7fffffff, yi = 0x7fffffff, wi = 0x7fffffff;
+    double bv = INFINITY, yv = INFINITY, wv = INFINITY, zv = INFINITY;
+    int32_t bi = 0x7fffffff, yi = 0x7fffffff, wi = 0x7fffffff, zi = 0x7fffffff;
+    const bool y4 = spec == 4;                                  // y's own minimum apart from the speculation
     int32_t sxs = 0, sys = 0;                                   // the speculated merge's sizes
     const uint32_t stride = G * WG;
     bool first = true;
@@ -773,11 +793,12 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             } else if (pend && i != y && better(u, i, yv, yi)) {   // P2: y's new row
                 yv = u; yi = i;
             }
+            if (y4 && i != y && better(u, i, zv, zi)) { zv = u; zi = i; }   // P4: y's new row (spec 4)
         }
     }
     LK_T(ph5);
-    MinIdx p1{bv, bi}, p2{yv, yi}, p3{wv, wi};
-    block_argmin3<WG>(p1, p2, p3, pend || sp, hasW);
+    MinIdx p1{bv, bi}, p2{yv, yi}, p3{wv, wi}, p4{zv, zi};
+    block_argmin4<WG>(p1, p2, p3, p4, pend || sp, hasW || y4, y4);
     LK_T(ph6);
 #if DREPHIP_LK_PHASES
     if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == G - 1)) {
@@ -790,6 +811,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
         if (search) parts[(uint64_t)q * 1024 + blockIdx.x] = p1;
         if (pend || sp) parts2[(uint64_t)q * 1024 + blockIdx.x] = p2;
         if (hasW) parts3[(uint64_t)q * 1024 + blockIdx.x] = p3;
+        if (y4) parts4[(uint64_t)q * 1024 + blockIdx.x] = p4;
     }
 }
 
@@ -953,12 +975,12 @@ static void launch_dist_tiles_condensed(const DmFromCondensed &v, uint32_t n, do
 // (sort_and_label: linkage_sparse.cpp, shared with the sparse path)
 struct NnArgs {
     double *D; uint32_t n; int32_t *size, *chain; LinkState *st; LinkFwd *fwd;
-    MinIdx *parts, *parts2, *parts3; int32_t *done; double *Z; uint32_t q; int spec_on;
+    MinIdx *parts, *parts2, *parts3, *parts4; int32_t *done; double *Z; uint32_t q; int spec_on;
 };
 template <int W, int P>
 static void launch_nn(int method, dim3 grid, dim3 blk, hipStream_t st, const NnArgs &a) {
 #define DREPHIP_LK_NN(M) hipLaunchKernelGGL((k_nn_step<W, P, M>), grid, blk, 0, st, a.D, a.n, a.size, a.chain, a.st, \
-                                            a.fwd, a.parts, a.parts2, a.parts3, a.done, a.Z, a.q, a.spec_on)
+                                            a.fwd, a.parts, a.parts2, a.parts3, a.parts4, a.done, a.Z, a.q, a.spec_on)
     if (method == DREPHIP_LINK_COMPLETE) DREPHIP_LK_NN(DREPHIP_LINK_COMPLETE);
     else if (method == DREPHIP_LINK_WEIGHTED) DREPHIP_LK_NN(DREPHIP_LINK_WEIGHTED);
     else DREPHIP_LK_NN(DREPHIP_LINK_AVERAGE);
@@ -1008,13 +1030,15 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     if ((rc = scratch(ctx, "lk_chain", n * 4ull, (void **)&d_chain))) return rc;
     if ((rc = scratch(ctx, "lk_Z", (n - 1) * 32ull, (void **)&d_Z))) return rc;
     if ((rc = scratch(ctx, "lk_parts", 2 * 1024 * sizeof(MinIdx), (void **)&d_parts))) return rc;
-    MinIdx *d_parts2, *d_parts3;
+    MinIdx *d_parts2, *d_parts3, *d_parts4;
     if ((rc = scratch(ctx, "lk_parts2", 2 * 1024 * sizeof(MinIdx), (void **)&d_parts2))) return rc;
     if ((rc = scratch(ctx, "lk_parts3", 2 * 1024 * sizeof(MinIdx), (void **)&d_parts3))) return rc;
-    // the speculation (A/B): 0 off; 1 the round-4 protocol (no known-merge
-    // launches); 2 (default) with the known-merge speculation (spec 3)
+    if ((rc = scratch(ctx, "lk_parts4", 2 * 1024 * sizeof(MinIdx), (void **)&d_parts4))) return rc;
+    // the speculation (A/B): 0 off; 1 the round-4 protocol; 2 with the
+    // known-merge speculation (spec 3); 3 (default) also in every other merge
+    // launch (spec 4)
     const char *spe = getenv("DREPHIP_LINK_SPEC");
-    const int spec_on = spe ? std::max(0, std::min(2, atoi(spe))) : 2;
+    const int spec_on = spe ? std::max(0, std::min(3, atoi(spe))) : 3;
     if ((rc = scratch(ctx, "lk_st", 2 * sizeof(LinkState), (void **)&d_st))) return rc;
     LinkFwd *d_fwd;
     if ((rc = scratch(ctx, "lk_fwd", 2 * sizeof(LinkFwd), (void **)&d_fwd))) return rc;
@@ -1068,7 +1092,8 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     for (int b = 0; b < kBatch; b++) {
         const uint32_t q = (uint32_t)(b & 1);
         const dim3 gm(grid), gn(grid + 1), blk(wg);
-        const NnArgs a{d_D, n, d_size, d_chain, d_st, d_fwd, d_parts, d_parts2, d_parts3, d_done, d_Z, q, spec_on};
+        const NnArgs a{d_D, n, d_size, d_chain, d_st, d_fwd, d_parts, d_parts2, d_parts3, d_parts4, d_done, d_Z, q,
+                       spec_on};
 #define DREPHIP_LK_LAUNCH(W, P)                                                                                      \
     do {                                                                                                         \
         if (mst) hipLaunchKernelGGL((k_mst_step<W, P>), gm, blk, 0, st, d_D, n, d_size, d_Dmin, d_st, d_parts, d_done, \

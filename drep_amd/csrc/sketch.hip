@@ -235,7 +235,14 @@ __device__ __forceinline__ MEnt fetch_ent(const SketchTablesQ &tb, uint32_t hi, 
     // kernel argument -- all ones (real lookups, +5 VALU per k-mer) or zero
     // (every lane reads entry 0: broadcast, no bank conflicts) -- so the two
     // runs issue the same instructions and differ only in the LDS bank traffic
-    const uint32_t s16 = sh & 0xfu, s8 = (sh >> 8) & 0xfu, km = sh >> 16;
+    const uint32_t s16 = sh & 0xfu, s8 = (sh >> 8) & 0xfu, km = (sh >> 16) & 0x3ffu;
+#if DREPHIP_SK_ABLATE == 2
+    // no tables at all: the entries are the k-mer's own words (no LDS read, no
+    // address arithmetic; the hash is garbage) -- the VALU-only time of the rest
+    (void)base; (void)s16; (void)s8; (void)km;
+    return MEnt{u32x4{hi, lo, hi, lo}, u32x2{lo, hi}, u32x4{lo, hi, lo, hi}, u32x2{hi, lo},
+                ((uint64_t)hi << 32) | lo};
+#endif
     return MEnt{*(const u32x4 *)(base + (((hi >> 24) & km) << s16)),
                 *(const u32x2 *)(base + offsetof(SketchTablesQ, b1) + (((hi >> 16) & km & 0xffu) << s8)),
                 *(const u32x4 *)(base + offsetof(SketchTablesQ, e2) + (((hi >> 8) & km & 0xffu) << s16)),

@@ -98,6 +98,7 @@ class Sim:
         spec = 0
         k = 0
         known = None
+        P2y = None
         while k < n - 1:
             st["launches"] += 1
             pend = None
@@ -168,18 +169,18 @@ class Sim:
                                     chain.append(P2[1])
                             elif r3[1] >= 0 and not wpush:
                                 st["w_merge"] += 1          # w's decision: merge with the element below it
-                                if self.policy == "r5":
+                                if self.policy in ("r5", "r5c"):
                                     known = "wmerge"
                             elif wpush and r3[1] == b:
                                 st["w_recip"] += 1          # w pushes b, b merges back with w
-                                if self.policy == "r5":
+                                if self.policy in ("r5", "r5c"):
                                     chain.append(b)
                                     known = "recip"
                         break
                     chain.append(r[1])
                     if r[1] != mrow or mrow < 0 or d == 1:
                         break
-                    r = P2
+                    r = P2y if P2y is not None else P2
                     st["twice"] += 1
             decide = True
             if k >= n - 1:
@@ -226,6 +227,13 @@ class Sim:
                     spec = 1
                 elif chain[-2] == pend[1] and t != pend[1]:
                     spec = 2
+            P2y = None
+            if not spec and pend and L >= 3 and self.policy == "r5c":
+                spec = 4              # a merge launch whose row y is not below the top: speculate too,
+                y = pend[1]           # y's own minimum kept apart (P2y) for a push of y
+                m = self.active().copy()
+                m[y] = False
+                P2y = self.rowmin(D[y], m)
             if spec:
                 P2, P3 = self.spec_rows(t, chain[-2], chain[-3])
             elif pend:
