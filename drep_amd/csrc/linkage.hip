@@ -52,6 +52,14 @@ constexpr int kLkWG = 256;
 #ifndef DREPHIP_LK_COLSTORE
 #define DREPHIP_LK_COLSTORE 3
 #endif
+// Deferred column (round 5): a merge launch writes only row y; the NEXT launch
+// scatters column y (D[i][y] = D[y][i]) early, beside its own decision and row
+// loads, so the scattered stores drain during that launch instead of at the end
+// of the merge launch.  Until then every read of an entry (R, y) goes to row y
+// (D[y][R]).  0: the column written in the merge launch itself (A/B)
+#ifndef DREPHIP_LK_DEFERCOL
+#define DREPHIP_LK_DEFERCOL 1
+#endif
 // Row-y stores (contiguous, 8n bytes per merge): 1 plain (default), 3 write-through (A/B)
 #ifndef DREPHIP_LK_ROWSTORE
 #define DREPHIP_LK_ROWSTORE 1
@@ -628,10 +636,20 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             // c5 and c6 forwarded)
             const bool sp = X.spec && len >= 4 && ck >= 2;
             int32_t rzt = size[top], rzb = size[two ? below : top];
-            double rdp = D[(uint64_t)top * n + (two ? below : top)];
+            // (an entry (a, pc) of the previous merge's column pc, not yet
+            // scattered, is read from row pc)
+#if DREPHIP_LK_DEFERCOL
+            const int32_t pc = S.pend && S.y != px && !(pend && S.y == py) ? S.y : -1;
+#else
+            const int32_t pc = -1;
+#endif
+            auto dat = [&](int32_t a, int32_t b) -> uint64_t {
+                return b == pc ? (uint64_t)b * n + a : (uint64_t)a * n + b;
+            };
+            double rdp = D[two ? dat(top, below) : (uint64_t)top * n + top];
             int32_t r3 = chain[l3 ? len - 3 : 0], r4 = chain[l4 ? len - 4 : 0], r5 = chain[l5 ? len - 5 : 0],
                     r6 = chain[l6 ? len - 6 : 0];
-            double rdp2 = D[sp ? (uint64_t)c3 * n + c4 : 0];
+            double rdp2 = D[sp ? dat(c3, c4) : 0];
             asm volatile("" : "+v"(rzt), "+v"(rzb), "+v"(rdp), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(rdp2));
             LK_T(ph3);
             auto size_now = [&](int32_t i, int32_t stored) {
@@ -687,10 +705,27 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     // loads, which the compiler waited for before the pass.)
     int32_t lz;
     asm volatile("v_mov_b32 %0, 0" : "=v"(lz));
+    // the previous launch's merged row pc, whose column this launch scatters
+    // (not when this launch's merge retires or rewrites it): entries (R, pc)
+    // of the rows read are taken from row pc
+#if DREPHIP_LK_DEFERCOL
+    const int32_t pc = S.pend && S.y != x && !(pend && S.y == y) ? S.y : -1;
+#else
+    const int32_t pc = -1;
+#endif
+    const bool hpc = pc >= 0;
+    const double *Dpc = D + (uint64_t)(hpc ? pc : 0) * n;
+    auto Duni = [&](int32_t a, int32_t b) -> double {          // D[a][b] as of this launch's start
+        return b == pc ? Dpc[a + lz] : D[(uint64_t)a * n + b + lz];
+    };
     const bool fa = pend && !yA, fb = pend && sp && !yB, fw = pend && hasW && !yW;
-    double xa = fa ? Dx[A + lz] : 0.0, ya_ = fa ? Dy[A + lz] : 0.0;
-    double xb = fb ? Dx[B + lz] : 0.0, yb = fb ? Dy[B + lz] : 0.0;
-    double xw = fw ? Dx[W + lz] : 0.0, yw = fw ? Dy[W + lz] : 0.0;
+    double xa = fa ? Duni(x, A) : 0.0, ya_ = fa ? Duni(y, A) : 0.0;
+    double xb = fb ? Duni(x, B) : 0.0, yb = fb ? Duni(y, B) : 0.0;
+    double xw = fw ? Duni(x, W) : 0.0, yw = fw ? Duni(y, W) : 0.0;
+    // entry pc of the rows read from memory: row pc's entries
+    double qa = hpc && !yA ? Dpc[A + lz] : 0.0, qb = hpc && sp && !yB ? Dpc[B + lz] : 0.0;
+    double qw = hpc && hasW && !yW ? Dpc[W + lz] : 0.0;
+    double qx = hpc && pend ? Dpc[x + lz] : 0.0, qy = hpc && pend ? Dpc[y + lz] : 0.0;
     // the sizes of A and B as of this step's decision (for the speculated merge)
     int32_t rsa = sp ? size[A + lz] : 0, rsb = sp ? size[B + lz] : 0;
     auto size_x = [&](int32_t i, int32_t stored) {
@@ -704,7 +739,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     bool first = true;
     for (uint32_t i0 = blockIdx.x * WG + threadIdx.x; i0 < n; i0 += kLkPer * stride) {
         int32_t sz[kLkPer];
-        double da[kLkPer], dx[kLkPer], dy[kLkPer], dw[kLkPer], db[kLkPer];
+        double da[kLkPer], dx[kLkPer], dy[kLkPer], dw[kLkPer], db[kLkPer], dp[kLkPer];
 #pragma unroll
         for (int k = 0; k < kLkPer; k++) {
             const uint32_t i = i0 + k * stride;
@@ -714,6 +749,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             if (pend) { dx[k] = Dx[ic]; dy[k] = Dy[ic]; }
             if (sp && !yB) db[k] = Db[ic];
             if (hasW && !yW) dw[k] = Dw[ic];
+            if (hpc) dp[k] = Dpc[ic];                           // row pc: the column scatter's values
         }
         // every load of the pass in flight before any is waited for: left to
         // itself the compiler sank the row loads below the size test that
@@ -726,11 +762,13 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             if (pend) asm volatile("" : "+v"(dx[k]), "+v"(dy[k]));
             if (sp && !yB) asm volatile("" : "+v"(db[k]));
             if (hasW && !yW) asm volatile("" : "+v"(dw[k]));
+            if (hpc) asm volatile("" : "+v"(dp[k]));
         }
         LK_T(ph4);
         if (first) {
             first = false;
             asm volatile("" : "+v"(xa), "+v"(ya_), "+v"(xb), "+v"(yb), "+v"(xw), "+v"(yw), "+v"(rsa), "+v"(rsb));
+            asm volatile("" : "+v"(qa), "+v"(qb), "+v"(qw), "+v"(qx), "+v"(qy));
             if (sp) {
                 const int32_t sa = size_x(A, rsa), sb_ = size_x(B, rsb);
                 sxs = A < B ? sa : sb_;
@@ -744,6 +782,16 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             // the sizes as of this step's decision: the previous decision's
             // (being written by workgroup 0) and this one's (not yet written)
             if (size_x(i, sz[k]) == 0) continue;                // (retires x)
+            if (hpc) {
+                if (i == pc) {                                  // entry pc of the rows read: from row pc
+                    da[k] = qa; db[k] = qb; dw[k] = qw; dx[k] = qx; dy[k] = qy;
+                } else if (!(pend && i == y)) {
+                    // the deferred column: D[i][pc] = D[pc][i] (write-through: the
+                    // lines leave during this launch; row y's own entry pc is written
+                    // with its new value by the row store below)
+                    __hip_atomic_store(&D[(uint64_t)i * n + pc], dp[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
             // this launch's merge: row y's new value at i, stored to row and column y
             double u = 0.0;
             if (pend && i != y) {
@@ -753,8 +801,9 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
 #else
                 Dy[i] = u;
 #endif
-#if DREPHIP_LK_COLSTORE == 0
-                // timing-only A/B build: no column-y stores (Z is wrong)
+#if DREPHIP_LK_DEFERCOL || DREPHIP_LK_COLSTORE == 0
+                // the column: scattered by the next launch (or, in a timing-only
+                // A/B build with DREPHIP_LK_COLSTORE=0, not at all: Z is wrong)
 #elif DREPHIP_LK_COLSTORE == 2
                 __builtin_nontemporal_store(u, &D[(uint64_t)i * n + y]);
 #elif DREPHIP_LK_COLSTORE == 3
