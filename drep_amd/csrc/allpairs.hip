@@ -889,15 +889,41 @@ __host__ __device__ constexpr size_t band_lds_bytes() {
 static_assert(kBandCols <= 256, "live lists hold column indices in bytes");
 static_assert(band_lds_bytes<4, 11, 768>() <= 80 * 1024 - 128, "R = 4: two workgroups per CU");
 
+// Value rounds (round 5).  Each launch of the ROUNDS kernel takes every item
+// of a chunk through one global value range [ends[k-1], ends[k]): its bands
+// stop at ends[k], and the item's per-column state (cursors, counts,
+// shared-so-far, live lists) and row positions go to global memory until the
+// next launch.  The items running together on one XCD -- the row tiles of one
+// family, placed there by the screen -- then read the same short segment of
+// each family column (s / rounds elements) within one launch, so the column
+// stream is fetched from HBM about once per family and re-read from that
+// XCD's L2, instead of once per (row tile, column) cell: without rounds the
+// tiles of a family drift apart by whole bands, and an L2 line lives a few
+// microseconds under the stream (profiles/r04_allpairs_N10000_s10000.json: L2
+// hit 0.17, HBM 48x the algorithmic bytes).  Bands and counts are the same
+// arithmetic as one launch; only the band cuts fall at the round ends too.
+// State blob: the LDS words from cur to the end of the lists, then a header.
+template <int R>
+__host__ __device__ constexpr uint32_t band_blob_words() {
+    return (kBandCols * 4 + 2 * R * kBandCols * 2 + 2 * kBandCols) / 4;
+}
+template <int R>
+__host__ __device__ constexpr uint32_t band_state_words() {     // blob + header, in 64-B lines
+    return (band_blob_words<R>() + R + 8 + 15) / 16 * 16;
+}
+enum : uint32_t { kBsDone = 1u };
+
 // LIST (the screened path, screen.hip): items are {i0, list offset, count, 0}
 // (litems) over the column list clist; otherwise {i0, c0} over kBandCols
-// consecutive columns.
-template <int R, int BB, int CAP, int WG, int MINW, bool LIST = false>
+// consecutive columns.  ROUNDS: one value round per launch (above); bstate
+// holds this launch's items' states, ends the rounds' upper bounds.
+template <int R, int BB, int CAP, int WG, int MINW, bool LIST = false, bool ROUNDS = false>
 __global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
     const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ nhash, uint32_t s, uint32_t N,
     uint32_t row1, uint32_t cap, const uint2 *__restrict__ items, uint16_t *__restrict__ common,
     uint16_t *__restrict__ denom, uint64_t seg0, uint32_t *__restrict__ nfail, uint64_t *__restrict__ prof,
-    const uint4 *__restrict__ litems, const uint32_t *__restrict__ clist) {
+    const uint4 *__restrict__ litems, const uint32_t *__restrict__ clist, uint32_t *__restrict__ bstate,
+    const uint64_t *__restrict__ ends, uint32_t round) {
     constexpr uint32_t H = 1u << BB, hm = H - 1, TS = 2 * H;
     constexpr uint32_t NW = WG / 64;
     static_assert(CAP < H, "band positions stay below the empty word's position hm");
@@ -909,12 +935,16 @@ __global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
     uint16_t *pm = pcnt + R * kBandCols;                             // [R][kBandCols] shared so far (<= s)
     uint8_t *lists = (uint8_t *)(pm + R * kBandCols);                // [2][kBandCols] live columns per band
     __shared__ uint32_t s_p[R], s_q[R], s_nlive[2];
-    __shared__ uint64_t s_hi;
+    __shared__ uint64_t s_hi, s_lo;
     __shared__ int s_done, s_fail, s_abort, s_twin;
 
     const uint32_t i0 = LIST ? litems[blockIdx.x].x : items[blockIdx.x].x;
     const uint32_t c0 = LIST ? 0 : items[blockIdx.x].y;
     if (i0 == 0xFFFFFFFFu) return;                      // idle padding item (make_items)
+    constexpr uint32_t BW = band_blob_words<R>();
+    uint32_t *gst = ROUNDS ? bstate + (size_t)blockIdx.x * band_state_words<R>() : nullptr;
+    const uint64_t rend = ROUNDS ? ends[round] : kEmpty;
+    if (ROUNDS && round > 0 && (gst[BW + R + 3] & kBsDone)) return;          // finished in an earlier round
     const uint32_t nrows = min((uint32_t)R, row1 - i0);
     const uint32_t *cl = LIST ? clist + litems[blockIdx.x].y : nullptr;
     const uint32_t ncols = LIST ? litems[blockIdx.x].z : min(c0 + kBandCols, N) - c0;
@@ -933,19 +963,47 @@ __global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
 #pragma unroll
     for (int r = 0; r < R; r++)
         if (nA[r]) { const uint64_t v = hashes[(uint64_t)(i0 + r) * s + nA[r] - 1]; maxlast = v > maxlast ? v : maxlast; }
-    for (uint32_t k = tid; k < kBandCols; k += WG) cur[k] = 0;
-    for (uint32_t k = tid; k < R * kBandCols; k += WG) { pcnt[k] = 0; pm[k] = 0; }
-    if (tid < (uint32_t)R) s_p[tid] = 0;
-    if (tid == 0) { s_abort = 0; s_nlive[0] = 0; s_nlive[1] = 0; }
-    __syncthreads();
-    // the first band's list: every column right of the tile's first row
-    // (columns left of every row have no pair in the item)
-    for (uint32_t k = tid; k < ncols; k += WG)
-        if (i0 < (LIST ? cl[k] : c0 + k)) lists[atomicAdd(&s_nlive[0], 1u)] = (uint8_t)k;
+    uint32_t band0 = 0;
+    if (ROUNDS && round > 0) {
+        // the state the previous round left (the blob is the LDS image from cur on)
+        for (uint32_t k = tid; k < BW; k += WG) cur[k] = gst[k];
+        if (tid < (uint32_t)R) s_p[tid] = gst[BW + tid];
+        if (tid == 0) {
+            s_nlive[0] = gst[BW + R];
+            s_nlive[1] = gst[BW + R + 1];
+            s_lo = (uint64_t)gst[BW + R + 4] | ((uint64_t)gst[BW + R + 5] << 32);
+            s_abort = 0;
+        }
+        band0 = gst[BW + R + 2];
+    } else {
+        for (uint32_t k = tid; k < kBandCols; k += WG) cur[k] = 0;
+        for (uint32_t k = tid; k < R * kBandCols; k += WG) { pcnt[k] = 0; pm[k] = 0; }
+        if (tid < (uint32_t)R) s_p[tid] = 0;
+        if (tid == 0) { s_abort = 0; s_nlive[0] = 0; s_nlive[1] = 0; s_lo = 0; }
+        __syncthreads();
+        // the first band's list: every column right of the tile's first row
+        // (columns left of every row have no pair in the item)
+        for (uint32_t k = tid; k < ncols; k += WG)
+            if (i0 < (LIST ? cl[k] : c0 + k)) lists[atomicAdd(&s_nlive[0], 1u)] = (uint8_t)k;
+    }
 
-    for (uint32_t band = 0;; band++) {
+    for (uint32_t band = band0;; band++) {
         const uint32_t lb = band & 1u;                   // this band's list; the next band's is lb ^ 1
         __syncthreads();
+        if (ROUNDS && rend != kEmpty && s_lo >= rend) {
+            // this round's values are done: park the state for the next launch
+            for (uint32_t k = tid; k < BW; k += WG) gst[k] = cur[k];
+            if (tid < (uint32_t)R) gst[BW + tid] = s_p[tid];
+            if (tid == 0) {
+                gst[BW + R] = s_nlive[0];
+                gst[BW + R + 1] = s_nlive[1];
+                gst[BW + R + 2] = band;
+                gst[BW + R + 3] = 0;
+                gst[BW + R + 4] = (uint32_t)s_lo;
+                gst[BW + R + 5] = (uint32_t)(s_lo >> 32);
+            }
+            return;
+        }
         if (wave == 0) {
             // band bound: the (cap+1)-th remaining element of the tightest row
             uint64_t v = kEmpty;
@@ -961,7 +1019,8 @@ __global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
             v = wave_min_u64(v);
             const bool any_left = __ballot(left) != 0;
             if (lane == 0) {
-                s_hi = v < maxlast + 1 ? v : maxlast + 1;
+                v = v < maxlast + 1 ? v : maxlast + 1;
+                s_hi = v < rend ? v : rend;                  // (a round's end cuts the band too)
                 s_done = !any_left || s_nlive[lb] == 0;
                 s_fail = 0;
                 s_nlive[lb ^ 1u] = 0;
@@ -1037,6 +1096,7 @@ __global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
                                                       c0, cl, i0, nrows, wave, hi, fam, pr, pn);
         __syncthreads();
         if (tid < (uint32_t)R) s_p[tid] += s_q[tid];
+        if (tid == 0) s_lo = hi;
         if (prof && tid == 0) {
             const uint64_t t_e = wall_clock64();
             atomicAdd((unsigned long long *)&prof[0], (unsigned long long)(t_c0 - t_b0));
@@ -1045,6 +1105,7 @@ __global__ __launch_bounds__(WG, MINW) void k_allpairs_band(
         }
     }
     __syncthreads();
+    if (ROUNDS && tid == 0) gst[BW + R + 3] = kBsDone;     // later rounds skip the item
     if (s_abort) return;
     if (LIST) {
         // the screened columns: one pair per (row, list entry) right of the row
@@ -1218,15 +1279,62 @@ static int launch_merge(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32
     return DREPHIP_OK;
 }
 
+// The value rounds' upper bounds: block k < nr - 1 takes, over up to 1024
+// genomes spread evenly over the set, the element at quantile (k + 1) / nr of
+// each sketch and writes their median; the last round ends at kEmpty (no
+// bound).  Medians of per-sketch quantiles rise with k, so the rounds tile the
+// value line in order.  Any bounds give the same counts; these only aim each
+// round at ~s / nr elements per row.
+__global__ __launch_bounds__(1024) void k_band_ends(const uint64_t *__restrict__ hashes,
+                                                    const uint32_t *__restrict__ nhash, uint32_t s, uint32_t N,
+                                                    uint32_t nr, uint64_t *__restrict__ ends) {
+    __shared__ uint64_t v[1024];
+    const uint32_t k = blockIdx.x, t = threadIdx.x;
+    if (k == nr - 1) {
+        if (t == 0) ends[k] = kEmpty;
+        return;
+    }
+    const uint32_t m = min(N, 1024u);
+    uint64_t x = kEmpty;
+    if (t < m) {
+        const uint32_t g = (uint32_t)((uint64_t)t * N / m);
+        const uint32_t nh = min(nhash[g], s);
+        const uint32_t idx = (uint32_t)((uint64_t)(k + 1) * nh / nr);
+        if (idx < nh) x = hashes[(uint64_t)g * s + idx];
+    }
+    v[t] = x;
+    for (uint32_t kk = 2; kk <= 1024; kk <<= 1)          // bitonic sort, ascending
+        for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+            __syncthreads();
+            const uint32_t p = t ^ j;
+            if (p > t) {
+                const uint64_t a = v[t], b = v[p];
+                if ((a > b) == ((t & kk) == 0)) { v[t] = b; v[p] = a; }
+            }
+        }
+    __syncthreads();
+    if (t == 0) ends[k] = v[m / 2];
+}
+
+// Items per round chunk: every round of a chunk runs before the next chunk
+// starts, so the state buffer stays bounded (kBandChunk x ~3 KB) at any N.
+constexpr uint64_t kBandChunk = 16384;
+static_assert(kBandChunk % 8 == 0, "chunks keep the XCD-interleaved item order");
+
 // One band-kernel geometry: R rows per tile, 2^BB slots per choice, CAP
 // elements per row per band, MINW = 8 (two workgroups per CU) or 4 (one).
 // scr: the screened lists (LIST kernel over them, every other pair filled as
-// no-shared-hash), or null for the dense item plan.
+// no-shared-hash), or null for the dense item plan.  Value rounds: ~`per`
+// elements per row per round (ctx->band_round, DREPHIP_BAND_ROUND; 0 = one
+// launch per item as before round 5).
 template <int R, int BB, int CAP, int MINW>
 static int launch_band_cfg(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N,
                            uint32_t row0, uint32_t row1, uint64_t seg0, uint64_t npairs, uint16_t *d_common,
                            uint16_t *d_denom, hipStream_t st, const ScreenResult *scr) {
     const uint32_t cap = std::min(std::max(ctx->band_cap, 1u), (uint32_t)CAP);
+    uint32_t per = ctx->band_round;
+    if (const char *e = getenv("DREPHIP_BAND_ROUND")) per = (uint32_t)atoi(e);
+    const uint32_t nr = per ? (ctx->s + per - 1) / per : 1;
     uint2 *d_items = nullptr;
     uint64_t nitems;
     uint32_t *d_nfail;
@@ -1251,13 +1359,36 @@ static int launch_band_cfg(drephip_ctx *ctx, const uint64_t *d_hashes, const uin
         HIPC(hipMemsetAsync(d_prof, 0, 64, st));
     }
     constexpr size_t lds = band_lds_bytes<R, BB, CAP>();
-    auto kern = scr ? k_allpairs_band<R, BB, CAP, 1024, MINW, true> : k_allpairs_band<R, BB, CAP, 1024, MINW, false>;
+    const bool rounds = nr > 1;
+    auto kern = scr ? (rounds ? k_allpairs_band<R, BB, CAP, 1024, MINW, true, true>
+                              : k_allpairs_band<R, BB, CAP, 1024, MINW, true, false>)
+                    : (rounds ? k_allpairs_band<R, BB, CAP, 1024, MINW, false, true>
+                              : k_allpairs_band<R, BB, CAP, 1024, MINW, false, false>);
     HIPC(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    uint32_t *d_state = nullptr;
+    uint64_t *d_ends = nullptr;
+    if (rounds) {
+        if ((rc = scratch(ctx, "apb_state", std::min(nitems, kBandChunk) * band_state_words<R>() * 4ull,
+                          (void **)&d_state)))
+            return rc;
+        if ((rc = scratch(ctx, "apb_ends", nr * 8ull, (void **)&d_ends))) return rc;
+    }
     timing_mark(ctx, 2, st, true);
-    for (uint64_t i0 = 0; i0 < nitems; i0 += max_blocks(1024))
-        hipLaunchKernelGGL(kern, dim3((uint32_t)std::min<uint64_t>(nitems - i0, max_blocks(1024))), dim3(1024), lds, st,
-                           d_hashes, d_nhash, ctx->s, N, row1, cap, scr ? nullptr : d_items + i0, d_common, d_denom, seg0,
-                           d_nfail, d_prof, scr ? scr->items + i0 : nullptr, scr ? scr->clist : nullptr);
+    if (rounds)
+        hipLaunchKernelGGL(k_band_ends, dim3(nr), dim3(1024), 0, st, d_hashes, d_nhash, ctx->s, N, nr, d_ends);
+    uint64_t chunk = rounds ? kBandChunk : nitems;
+    if (const char *e = getenv("DREPHIP_BAND_CHUNK"))          // tests only: several chunks at small sizes
+        if (rounds && atoll(e) > 0) chunk = std::min<uint64_t>(kBandChunk, std::max<uint64_t>(8, atoll(e) / 8 * 8));
+    for (uint64_t b0 = 0; b0 < nitems; b0 += chunk) {
+        const uint64_t b1 = std::min(nitems, b0 + chunk);
+        for (uint32_t k = 0; k < nr; k++)
+            for (uint64_t i0 = b0; i0 < b1; i0 += max_blocks(1024))
+                hipLaunchKernelGGL(kern, dim3((uint32_t)std::min<uint64_t>(b1 - i0, max_blocks(1024))), dim3(1024), lds,
+                                   st, d_hashes, d_nhash, ctx->s, N, row1, cap, scr ? nullptr : d_items + i0, d_common,
+                                   d_denom, seg0, d_nfail, d_prof, scr ? scr->items + i0 : nullptr,
+                                   scr ? scr->clist : nullptr, rounds ? d_state + (i0 - b0) * band_state_words<R>() : nullptr,
+                                   d_ends, k);
+    }
     timing_mark(ctx, 2, st, false);
     HIPC(hipGetLastError());
     uint32_t nfail = 0;

@@ -106,6 +106,7 @@ struct drephip_ctx {
     ScreenResult last_screen; // the last all-pairs call's screen (stats; pointers into scratch)
     int link_path = 0;        // DREPHIP_LINK_PATH_*: 0 auto (sparse when it applies, else dense)
     uint32_t band_cap = 1024; // elements per row per band of the banded all-pairs kernel (clamped to its LDS budget)
+    uint32_t band_round = 0;  // elements per row per value round of the band kernel (0: no rounds; A/B)
     // named grow-only device scratch buffers
     std::map<std::string, DevBuf> bufs;
     // per-kernel timing of the last call: {sum ms, launches}

@@ -56,13 +56,22 @@ constexpr int kLkWG = 256;
 // scatters column y (D[i][y] = D[y][i]) early, beside its own decision and row
 // loads, so the scattered stores drain during that launch instead of at the end
 // of the merge launch.  Until then every read of an entry (R, y) goes to row y
-// (D[y][R]).  0: the column written in the merge launch itself (A/B)
+// (D[y][R]).  0 (default): the column written in the merge launch itself.
+// Measured slower (chain at 10^5: 997 ms deferred vs 932 ms not, same
+// protocol, profiles/r05_linkage_ab_defer_spec4.txt): the next launch then
+// carries row pc's loads and the scatter on its own critical path
 #ifndef DREPHIP_LK_DEFERCOL
-#define DREPHIP_LK_DEFERCOL 1
+#define DREPHIP_LK_DEFERCOL 0
 #endif
 // Row-y stores (contiguous, 8n bytes per merge): 1 plain (default), 3 write-through (A/B)
 #ifndef DREPHIP_LK_ROWSTORE
 #define DREPHIP_LK_ROWSTORE 1
+#endif
+// Candidate-row prefetch (round 5): the step loads its entries of six
+// candidate rows before the decision instead of the decided rows after it
+// (k_nn_step).  0: the rows loaded after the decision (A/B)
+#ifndef DREPHIP_LK_PREFETCH
+#define DREPHIP_LK_PREFETCH 1
 #endif
 constexpr uint32_t kLkSmallN = 30000;
 
@@ -457,6 +466,59 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                  "+v"(fw1.w), "+v"(fw2.x), "+v"(fw2.y), "+v"(fw2.z));
     const LinkState S = state_from_words(sw0, sw1, sw2, sw3);
     const LinkFwd F = fwd_from_words(fw0, fw1, fw2);
+#if DREPHIP_LK_PREFETCH
+    // Candidate rows: in a merge launch every row the step reads is known
+    // before its decision -- the merged pair is the top and the element below
+    // it (or the previous merge's row and the top), the speculation's rows are
+    // the chain entries c3..c5 (forwarded), and the deferred column's row is the
+    // previous merge's y.  Each step workgroup issues its entries of these six
+    // rows (and of size) here, so that they land during the decision instead
+    // of after it; a decided row outside them (a pushed nearest neighbour) is
+    // loaded after the decision as before.  The candidates' pairwise entries
+    // (the uniform operands of the pass), read as Duni does (an entry of the
+    // previous merge's row y is taken from row y, whose column may not be
+    // scattered yet), and their sizes go to LDS (kPairs).
+    constexpr int kCand = 6;
+    __shared__ double s_pair[kCand * kCand];
+    __shared__ int32_t s_csz[kCand];
+    int32_t cand[kCand] = {S.top, S.below, S.pend ? S.y : -1, S.len >= 3 ? F.c3 : -1, S.len >= 4 ? F.c4 : -1,
+                           S.len >= 5 ? F.c5 : -1};
+#pragma unroll
+    for (int j = 0; j < kCand; j++) if ((uint32_t)cand[j] >= n) cand[j] = -1;
+    double pre[kCand][kLkPer], pairv = 0.0;
+    int32_t psz[kLkPer], pszc = 0;
+    const uint32_t pwave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    constexpr uint32_t kPairWave = WG / 64 - 1;                // the last wave loads the pair entries
+    if (blockIdx.x != gridDim.x - 1) {
+        const uint32_t pstride = (gridDim.x - 1) * WG;
+#pragma unroll
+        for (int k = 0; k < kLkPer; k++) {
+            const uint32_t i = blockIdx.x * WG + threadIdx.x + k * pstride;
+            const uint32_t ic = i < n ? i : n - 1;
+            psz[k] = size[ic];
+#pragma unroll
+            for (int j = 0; j < kCand; j++) pre[j][k] = D[(uint64_t)(cand[j] < 0 ? 0 : cand[j]) * n + ic];
+        }
+        if (pwave == kPairWave) {
+            // lane l < 36: entry (cand[l / 6], cand[l % 6]); lane 36 + j: size
+            // of cand[j].  Every lane loads (invalid ones entry 0): no divergent
+            // branch -- a load into a register the other branch also wrote made
+            // the wave wait for all of its prefetch loads here
+            const uint32_t l = threadIdx.x & 63;
+            int32_t a = -1, b = -1, c = -1;
+#pragma unroll
+            for (int j = 0; j < kCand; j++) {
+                a = l / kCand == (uint32_t)j ? cand[j] : a;
+                b = l % kCand == (uint32_t)j ? cand[j] : b;
+                c = l == (uint32_t)(kCand * kCand + j) ? cand[j] : c;
+            }
+            const bool ok = l < kCand * kCand && a >= 0 && b >= 0;
+            const bool by = S.pend && b == S.y;                  // entry (a, y): from row y
+            pairv = D[!ok ? 0 : by ? (uint64_t)b * n + a : (uint64_t)a * n + b];
+            pszc = size[c >= 0 ? c : 0];
+        }
+    }
+#endif
 #if DREPHIP_LK_PHASES
     uint64_t ph0 = 0, ph1 = 0, ph2 = 0, ph3 = 0, ph4 = 0, ph5 = 0, ph6 = 0;
 #endif
@@ -679,6 +741,13 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
         }
     }
     if (blockIdx.x == G) return;                               // the forwarding workgroup has no step work
+#if DREPHIP_LK_PREFETCH
+    if (pwave == kPairWave) {
+        const uint32_t l = threadIdx.x & 63;
+        if (l < kCand * kCand) s_pair[l] = pairv;
+        else if (l < kCand * kCand + kCand) s_csz[l - kCand * kCand] = pszc;
+    }
+#endif
     __syncthreads();
     const LinkState X = sx;
     LK_T(ph3);
@@ -719,6 +788,40 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
         return b == pc ? Dpc[a + lz] : D[(uint64_t)a * n + b + lz];
     };
     const bool fa = pend && !yA, fb = pend && sp && !yB, fw = pend && hasW && !yW;
+#if DREPHIP_LK_PREFETCH
+    // the decided rows among the candidates (-1: not a candidate, loaded below)
+    auto cidx = [&](int32_t r) -> int {
+        int j = -1;
+#pragma unroll
+        for (int jj = kCand - 1; jj >= 0; jj--) if (r >= 0 && r == cand[jj]) j = jj;
+        return j;
+    };
+    const int jx = pend ? cidx(x) : -1, jy = pend ? cidx(y) : -1, jA = cidx(A), jB = sp ? cidx(B) : -1,
+              jW = hasW ? cidx(W) : -1, jpc = hpc ? cidx(pc) : -1;
+    // entry (a, b) as of this launch's start: from the candidates' pair
+    // entries, else loaded (Duni)
+    auto Dpair = [&](int ja, int jb, int32_t a, int32_t b) -> double {
+        return ja >= 0 && jb >= 0 ? s_pair[ja * kCand + jb] : Duni(a, b);
+    };
+    // the prefetched row of candidate j (a uniform select), entry k.  The
+    // entries pass through an empty asm first, so the select is one of values:
+    // a select between array elements was folded into one load at a computed
+    // index, which put the array in scratch (each prefetch load was then
+    // waited for at once, to be stored there)
+    static_assert(kCand == 6, "sel names the six candidates");
+    auto sel = [&](int j, int k) -> double {
+        double a0 = pre[0][k], a1 = pre[1][k], a2 = pre[2][k], a3 = pre[3][k], a4 = pre[4][k], a5 = pre[5][k];
+        asm volatile("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5));
+        return j == 0 ? a0 : j == 1 ? a1 : j == 2 ? a2 : j == 3 ? a3 : j == 4 ? a4 : a5;
+    };
+    double xa = fa ? Dpair(jx, jA, x, A) : 0.0, ya_ = fa ? Dpair(jy, jA, y, A) : 0.0;
+    double xb = fb ? Dpair(jx, jB, x, B) : 0.0, yb = fb ? Dpair(jy, jB, y, B) : 0.0;
+    double xw = fw ? Dpair(jx, jW, x, W) : 0.0, yw = fw ? Dpair(jy, jW, y, W) : 0.0;
+    double qa = hpc && !yA ? Dpair(jpc, jA, pc, A) : 0.0, qb = hpc && sp && !yB ? Dpair(jpc, jB, pc, B) : 0.0;
+    double qw = hpc && hasW && !yW ? Dpair(jpc, jW, pc, W) : 0.0;
+    double qx = hpc && pend ? Dpair(jpc, jx, pc, x) : 0.0, qy = hpc && pend ? Dpair(jpc, jy, pc, y) : 0.0;
+    int32_t rsa = sp ? (jA >= 0 ? s_csz[jA] : size[A + lz]) : 0, rsb = sp ? (jB >= 0 ? s_csz[jB] : size[B + lz]) : 0;
+#else
     double xa = fa ? Duni(x, A) : 0.0, ya_ = fa ? Duni(y, A) : 0.0;
     double xb = fb ? Duni(x, B) : 0.0, yb = fb ? Duni(y, B) : 0.0;
     double xw = fw ? Duni(x, W) : 0.0, yw = fw ? Duni(y, W) : 0.0;
@@ -728,6 +831,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     double qx = hpc && pend ? Dpc[x + lz] : 0.0, qy = hpc && pend ? Dpc[y + lz] : 0.0;
     // the sizes of A and B as of this step's decision (for the speculated merge)
     int32_t rsa = sp ? size[A + lz] : 0, rsb = sp ? size[B + lz] : 0;
+#endif
     auto size_x = [&](int32_t i, int32_t stored) {
         return pend && i == x ? 0 : pend && i == y ? nx + ny : size_prev(i, stored);
     };
@@ -740,6 +844,21 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     for (uint32_t i0 = blockIdx.x * WG + threadIdx.x; i0 < n; i0 += kLkPer * stride) {
         int32_t sz[kLkPer];
         double da[kLkPer], dx[kLkPer], dy[kLkPer], dw[kLkPer], db[kLkPer], dp[kLkPer];
+#if DREPHIP_LK_PREFETCH
+        if (first) {                                            // the prefetched pass (same i as the prefetch)
+#pragma unroll
+            for (int k = 0; k < kLkPer; k++) {
+                const uint32_t i = i0 + k * stride;
+                const uint32_t ic = i < n ? i : n - 1;
+                sz[k] = psz[k];
+                if (!yA) da[k] = jA >= 0 ? sel(jA, k) : Da[ic];
+                if (pend) { dx[k] = jx >= 0 ? sel(jx, k) : Dx[ic]; dy[k] = jy >= 0 ? sel(jy, k) : Dy[ic]; }
+                if (sp && !yB) db[k] = jB >= 0 ? sel(jB, k) : Db[ic];
+                if (hasW && !yW) dw[k] = jW >= 0 ? sel(jW, k) : Dw[ic];
+                if (hpc) dp[k] = jpc >= 0 ? sel(jpc, k) : Dpc[ic];
+            }
+        } else
+#endif
 #pragma unroll
         for (int k = 0; k < kLkPer; k++) {
             const uint32_t i = i0 + k * stride;
@@ -1083,11 +1202,13 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     if ((rc = scratch(ctx, "lk_parts2", 2 * 1024 * sizeof(MinIdx), (void **)&d_parts2))) return rc;
     if ((rc = scratch(ctx, "lk_parts3", 2 * 1024 * sizeof(MinIdx), (void **)&d_parts3))) return rc;
     if ((rc = scratch(ctx, "lk_parts4", 2 * 1024 * sizeof(MinIdx), (void **)&d_parts4))) return rc;
-    // the speculation (A/B): 0 off; 1 the round-4 protocol; 2 with the
-    // known-merge speculation (spec 3); 3 (default) also in every other merge
-    // launch (spec 4)
+    // the speculation (A/B): 0 off; 1 the round-4 protocol; 2 (default) with
+    // the known-merge speculation (spec 3); 3 also in every other merge launch
+    // (spec 4: launches per merge at 10^5 1.2617 -> 1.2457, but each merge
+    // launch reduces a fourth partial set, and the chain took longer: 997 vs
+    // 991 ms, both with the deferred column; profiles/r05_linkage_ab_defer_spec4.txt)
     const char *spe = getenv("DREPHIP_LINK_SPEC");
-    const int spec_on = spe ? std::max(0, std::min(3, atoi(spe))) : 3;
+    const int spec_on = spe ? std::max(0, std::min(3, atoi(spe))) : 2;
     if ((rc = scratch(ctx, "lk_st", 2 * sizeof(LinkState), (void **)&d_st))) return rc;
     LinkFwd *d_fwd;
     if ((rc = scratch(ctx, "lk_fwd", 2 * sizeof(LinkFwd), (void **)&d_fwd))) return rc;

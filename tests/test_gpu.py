@@ -495,6 +495,33 @@ def test_allpairs_band_kernel_vs_oracle(s, cap):
         assert c.max() > s // 2
 
 
+@pytest.mark.parametrize("screen", ["on", "off"])
+@pytest.mark.parametrize("per,cap,chunk", [(0, 768, 0), (1, 768, 0), (37, 300, 8), (300, 300, 0), (640, 768, 16),
+                                           (640, 200, 0), (5000, 768, 0)])
+def test_allpairs_band_value_rounds(per, cap, chunk, screen, monkeypatch):
+    """The band kernel's value rounds (one launch per global value range,
+    item state parked in HBM between launches): any round size -- none, one
+    element, rounds narrower and wider than the band cap, a single round --
+    and item chunks of 8-16 (every chunk runs all rounds before the next)
+    give the oracle's counts and denominators, screened (LIST) and dense."""
+    s = 4096
+    h, nh = oracle.sketch_synth(0, 72, 150_000, seed=per + cap, family_size=9, s=s, threads=8)
+    nh = nh.copy()
+    h = h.copy()
+    h[5, 1000:] = UMAX; nh[5] = 1000                  # a partial row and an empty one
+    h[17, :] = UMAX; nh[17] = 0
+    monkeypatch.setenv("DREPHIP_BAND_ROUND", str(per))
+    if chunk:
+        monkeypatch.setenv("DREPHIP_BAND_CHUNK", str(chunk))
+    with _lib.Context(0, 21, s, 42) as ctx:
+        ctx.set_allpairs_path(ctx.AP_BAND, cap)
+        ctx.set_allpairs_screen(ctx.SCREEN_ON if screen == "on" else ctx.SCREEN_OFF)
+        c, d = ctx.allpairs(h, nh, want_denom=True)
+    oc, od = oracle.allpairs(h, nh, s, threads=8)
+    assert np.array_equal(c, oc) and np.array_equal(d, od)
+    assert c.max() > s // 2
+
+
 def test_allpairs_band_partial_and_segments(family, ctx1000):
     """Band kernel on partial sketches (denominator from the full intersection)
     and on row-range segments."""
