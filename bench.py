@@ -32,15 +32,18 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
-# VALU issue model: MI355X_MICROARCH.md gives one wave64 VALU instruction per
-# 2 cycles per SIMD (SIMD-32) as the issue peak: 1024 SIMDs x 2.4 GHz / 2.
-# The measured throughput of the sketch loop's own instruction mix
-# (profiles/r01_valu_microbench.json: simple VOP2 ops ~1.45 cycles, 3-operand,
-# 64-bit and multiply ops 2.6-2.9) gives a second, mix-priced peak.
+# VALU issue: MI355X_MICROARCH.md gives one wave64 VALU instruction per 2
+# cycles per SIMD (SIMD-32) as the issue peak: 1024 SIMDs x 2.4 GHz / 2 (the
+# all-pairs kernel's VALU fraction is quoted against it).  The sketch hash
+# kernel's model is its own instruction floor (profiles/r05_sketch_ablation.json,
+# tools/sketch_ablation_json.py): every build of its hot loop -- product, +6
+# VALU, conflict-free LDS, no LDS at all -- takes ~3.8 SIMD-cycles per wave64
+# VALU instruction, so its time is its VALU count at that rate; the no-LDS
+# build's rate is the floor the live launch is compared with.
 N_SIMD = 256 * 4
 VALU_PEAK_WAVE_INST = N_SIMD * 2.4e9 / 2
-VALU_COSTS = os.path.join(ROOT, "profiles", "r01_valu_microbench.json")
-SKETCH_ISA = os.path.join(ROOT, "profiles", "r03_sketch_isa.json")
+SKETCH_PHASES = os.path.join(ROOT, "profiles", "r05_sketch_isa_phases.json")
+SKETCH_ABLATION = os.path.join(ROOT, "profiles", "r05_sketch_ablation.json")
 # committed PMC summaries (tools/pmc_summary.py): VALU / LDS utilisation of the
 # two kernels, reported next to the live timings
 SKETCH_PMC = os.path.join(ROOT, "profiles", "r04_sketch_pmc_sq.json")
@@ -51,23 +54,6 @@ SKETCH_TRAFFIC = os.path.join(ROOT, "profiles", "r04_sketch_traffic.json")
 PROFILE_STEPS = 3              # untimed steps that time finalize / all-pairs / table build
 VERIFY_GENOMES = 16            # timed-step sketches re-derived by the C oracle (sampled, every run)
 VERIFY_PAIRS = 100_000         # timed-step counts re-derived by the C oracle (random pairs + one row)
-
-
-def mix_priced_cycles(isa):
-    """SIMD-cycles one wave spends issuing the hot loop's instructions for 64
-    k-mers, each mnemonic priced at its measured throughput (VALU_COSTS);
-    mnemonics not measured take their class price (VOP2 e32 1.45, else 2.6)."""
-    if not os.path.exists(VALU_COSTS) or "valu_mix_per_kmer" not in isa:
-        return None
-    cost = {r["inst"]: r["cycles_per_wave_inst_per_simd"] for r in json.load(open(VALU_COSTS))["results"]}
-    total = 0.0
-    for op, n in isa["valu_mix_per_kmer"].items():
-        base = op.replace("_e32", "").replace("_e64", "").replace("_sdwa", "")
-        c = cost.get(op, cost.get(base))
-        if c is None or op.startswith("v_cndmask"):      # the microbench's cndmask chain waits on vcc
-            c = 1.45 if op.endswith("_e32") else 2.6
-        total += n * c
-    return total
 
 
 def dist_roofline(N, s, pairs_per_launch, launch_ms):
@@ -106,7 +92,11 @@ def pmc_block(path):
         d = json.load(open(path))
     except Exception:
         return None
-    keep = ("valu_issue_frac_2cyc", "valu_active_quad_frac", "lds_busy_frac", "lds_bank_conflict_frac", "wait_any_frac",
+    # (valu_active_quad_frac is not kept: SQ_ACTIVE_INST_VALU equals
+    # SQ_INSTS_VALU in the sketch profile, i.e. it counts one quad-cycle per
+    # instruction, so that "fraction" is the instruction count priced at 4
+    # cycles, not a measured VALU occupancy)
+    keep = ("valu_issue_frac_2cyc", "lds_busy_frac", "lds_bank_conflict_frac", "wait_any_frac",
             "wait_inst_any_frac", "active_inst_any_frac", "valu_insts_per_window_end", "effective_clock_ghz")
     out = {k: d["derived"][k] for k in keep if k in d.get("derived", {})}
     out["source"] = os.path.relpath(path, ROOT)
@@ -576,32 +566,33 @@ def main():
     kmers_per_s = nloc * (L - 20) / avg_launch_s if avg_launch_s > 0 else 0.0
     window_ends = nloc * P                           # every padded position is a window end the kernel visits
     valu = {"kmers_per_s": kmers_per_s}
-    if os.path.exists(SKETCH_ISA):
-        isa = json.load(open(SKETCH_ISA))["variants"].get("default")
-        if isa:
-            valu.update({"kernel": isa["kernel"], "valu_per_kmer_hot_loop": isa["valu_per_kmer"],
-                         "lds_reads_per_kmer": isa["lds_reads_per_kmer"],
-                         "isa_source": os.path.relpath(SKETCH_ISA, ROOT) + " (tools/isa_count.py)"})
+    if os.path.exists(SKETCH_PHASES):
+        ph = json.load(open(SKETCH_PHASES))
+        valu.update({"kernel": ph["kernel"], "valu_per_kmer_hot_loop": ph["valu_per_kmer"],
+                     "valu_per_kmer_by_phase": {k: v["valu_per_kmer"] for k, v in ph["phases"].items()},
+                     "isa_source": os.path.relpath(SKETCH_PHASES, ROOT) + " (tools/isa_phases.py)"})
     pmc_sk = pmc_block(SKETCH_PMC)
-    if pmc_sk and pmc_sk.get("valu_insts_per_window_end"):
-        # wave64 VALU instructions per launch (PMC count per window end, the
-        # table copy and every loop overhead included) / launch time, against
-        # 1024 SIMDs x 2.4 GHz / 2 cycles per wave instruction (VALU_PEAK_WAVE_INST)
-        wi = pmc_sk["valu_insts_per_window_end"] * window_ends / 64
-        ach = wi / avg_launch_s if avg_launch_s > 0 else 0.0
-        valu.update({"bound": "valu_issue", "achieved": ach, "peak": VALU_PEAK_WAVE_INST,
-                     "unit": "wave64 VALU instructions/s", "frac": ach / VALU_PEAK_WAVE_INST,
-                     "valu_insts_per_kmer_measured": pmc_sk["valu_insts_per_window_end"],
-                     "note": "peak = the guide's 2-cycle wave64 issue on every SIMD; time follows "
-                             "the VALU count (profiles/r02_sketch_ab.json)"})
-        priced = mix_priced_cycles(isa) if isa else None
-        if priced:
-            # SIMD-cycles per 64 window ends of the hot loop at the microbench's
-            # measured per-instruction throughput -> window ends per second
-            peak_we = N_SIMD * 2.4e9 * 64 / priced
-            valu.update({"mix_priced_cycles_per_64_kmers": priced,
-                         "mix_priced_frac": (window_ends / avg_launch_s) / peak_we if avg_launch_s > 0 else 0.0,
-                         "mix_costs_source": os.path.relpath(VALU_COSTS, ROOT)})
+    if os.path.exists(SKETCH_ABLATION) and valu.get("valu_per_kmer_hot_loop") and avg_launch_s > 0:
+        # One binding resource: VALU issue of the hot loop's instruction
+        # stream.  achieved = the hot loop's wave64 VALU instructions per launch
+        # / this launch's live time; peak = the same instructions at the floor
+        # rate (the no-LDS build's SIMD-cycles per instruction, same box class)
+        ab = json.load(open(SKETCH_ABLATION))
+        floor_cyc = ab["floor"]["cycles_per_wave_inst_per_simd"]
+        wi = valu["valu_per_kmer_hot_loop"] * window_ends / 64
+        ach = wi / avg_launch_s
+        peak = N_SIMD * 2.4e9 / floor_cyc
+        valu.update({"bound": "valu_issue", "achieved": ach, "peak": peak, "unit": "wave64 VALU instructions/s",
+                     "frac": ach / peak,
+                     "cycles_per_wave_inst_per_simd": N_SIMD * 2.4e9 / ach,
+                     "floor_cycles_per_wave_inst_per_simd": floor_cyc,
+                     "floor_source": os.path.relpath(SKETCH_ABLATION, ROOT) + " (tools/sketch_ablation_json.py)",
+                     "frac_of_2cyc_issue_peak": ach / VALU_PEAK_WAVE_INST,
+                     "note": "binding resource: VALU issue. Time = VALU count x ~3.8 SIMD-cycles per wave64 "
+                             "instruction in every ablation build (product; +6 VALU; conflict-free LDS; no LDS "
+                             "reads), so `frac` is the live rate over the no-LDS build's rate (the instruction "
+                             "floor); the guide's 2-cycle dual-wave peak is not reached by this dependent 64-bit "
+                             "mix (SQ_WAIT_INST_ANY 0.58 of wave-cycles)"})
 
     # ---- output segment D2H (PCIe-inclusive leg; not part of `value`)
     torch.cuda.synchronize()
@@ -709,8 +700,8 @@ def main():
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": traffic,
                 "note": "algorithmic bytes = 0.375 B/base (2-bit code + validity bit) x bases per "
-                        "launch; HBM is not the limit: the kernel is VALU-issue bound (Murmur3, ~65 "
-                        "VALU instructions per k-mer), see valu_model",
+                        "launch; HBM is not the limit: the kernel is VALU-issue bound (Murmur3, 63 "
+                        "VALU instructions per k-mer in the hot loop), see valu_model",
                 "valu_model": valu,
                 "pmc": pmc_sk,
             },
