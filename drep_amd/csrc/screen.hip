@@ -192,6 +192,7 @@ __global__ __launch_bounds__(kScWG) void k_run_write(const uint32_t *__restrict_
 // the hash's rank in A u B is i + j -- and needs no kernel (k_screen_simple).
 constexpr uint64_t kPairEmpty = ~0ull;
 constexpr uint64_t kMaxPairMap = 1ull << 30;   // pair-map slots (16 B each); above it the screen gives way
+constexpr uint64_t kLightBudget = 1ull << 30;  // bytes of the light screen's per-cell run ids (sc_crun)
 __device__ __forceinline__ uint32_t pair_slot(uint64_t key, uint32_t mask) {
     uint64_t h = key * 0x9E3779B97F4A7C15ull;
     return (uint32_t)(h >> 32) & mask;
@@ -232,16 +233,26 @@ __global__ __launch_bounds__(kScWG) void k_screen_simple(const unsigned long lon
                                                          const uint32_t *__restrict__ nh, uint32_t s, uint32_t N,
                                                          uint32_t row0, uint32_t rshift, uint32_t NW,
                                                          uint64_t seg0, uint32_t *__restrict__ bm,
+                                                         uint32_t *__restrict__ bmH,
                                                          uint16_t *__restrict__ common, unsigned long long *__restrict__ nsimple) {
     uint32_t mine = 0;
     for (uint32_t q = blockIdx.x * kScWG + threadIdx.x; q < pcap; q += gridDim.x * kScWG) {
         const unsigned long long key = pkey[q];
         if (key == kPairEmpty) continue;
         const uint32_t a = (uint32_t)(key >> 32), b = (uint32_t)key;
-        uint32_t *w = bm + (uint64_t)((a - row0) >> rshift) * NW + (b >> 5);
+        const uint64_t wo = (uint64_t)((a - row0) >> rshift) * NW + (b >> 5);
+        uint32_t *w = bm + wo;
         const uint32_t bit = 1u << (b & 31);
-        if (pcnt[q] >= 2 || nh[a] != s || nh[b] != s) { atomicOr(w, bit); continue; }
-        if (*w & bit) continue;                                       // a longer run holds the pair too
+        // (bmH, the light screen's heavy cells: the cell needs the LIST kernel)
+        if (pcnt[q] >= 2 || nh[a] != s || nh[b] != s) {
+            atomicOr(w, bit);
+            if (bmH) atomicOr(bmH + wo, bit);
+            continue;
+        }
+        if (*w & bit) {                                               // a longer run holds the pair too
+            if (bmH) atomicOr(bmH + wo, bit);
+            continue;
+        }
         const uint32_t pos = ppos[q];
         const uint64_t o = (uint64_t)a * N - (uint64_t)a * (a + 1) / 2 + (b - a - 1) - seg0;
         common[o] = (uint16_t)(((pos >> 16) + (pos & 0xFFFFu)) < s ? 1 : 0);
@@ -271,31 +282,55 @@ constexpr uint32_t kMarkTiles = 128;
 constexpr uint32_t kMarkCols = 2048;
 constexpr uint32_t kMarkWords = kMarkCols / 32;
 constexpr uint32_t kMarkStride = kMarkWords + 1;
+template <bool LIGHT>
 __global__ __launch_bounds__(kMarkWG) void k_screen_mark(const uint32_t *__restrict__ vals, const uint64_t *__restrict__ H,
                                                        uint32_t s, const uint2 *__restrict__ runs,
                                                        const uint32_t *__restrict__ order,
                                                        const uint32_t *__restrict__ rfirst_sorted, uint32_t nruns,
                                                        uint32_t row0, uint32_t row1, uint32_t rshift, uint32_t NW,
-                                                       uint32_t *__restrict__ bm) {
+                                                       uint32_t *__restrict__ bm, uint32_t *__restrict__ bmH,
+                                                       uint32_t *__restrict__ crun, uint32_t N) {
     __shared__ uint32_t win[kMarkTiles * kMarkStride];
+    __shared__ uint32_t winH[LIGHT ? kMarkTiles * kMarkStride : 1];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t q0 = blockIdx.x * kMarkChunk;
     const uint32_t q1 = min(q0 + kMarkChunk, nruns);
-    for (uint32_t i = threadIdx.x; i < kMarkTiles * kMarkStride; i += kMarkWG) win[i] = 0;
+    for (uint32_t i = threadIdx.x; i < kMarkTiles * kMarkStride; i += kMarkWG) {
+        win[i] = 0;
+        if (LIGHT) winH[i] = 0;
+    }
     // window: row tiles [t_lo, t_lo + kMarkTiles), columns [c_lo, c_lo + kMarkCols)
     const uint32_t g_lo = rfirst_sorted[q0];
     const uint32_t t_lo = g_lo > row0 ? (g_lo - row0) >> rshift : 0;
     const uint32_t c_lo = g_lo & ~31u;
     __syncthreads();
-    // one cell mark: the LDS window when (tile, column) falls in it, else the bitmap
-    auto mark = [&](uint32_t t, uint32_t col, uint32_t bits) {
-        if (t - t_lo < kMarkTiles && col - c_lo < kMarkCols)
-            atomicOr(&win[(t - t_lo) * kMarkStride + ((col - c_lo) >> 5)], bits);
-        else
-            atomicOr(bm + (uint64_t)t * NW + (col >> 5), bits);
+    // one cell mark: the LDS window when (tile, column) falls in it, else the
+    // bitmap.  LIGHT: a cell marked before (by another run) goes to the heavy
+    // bitmap (winH / bmH); a cell marked for the first time records the run
+    // (crun), and a run whose entries do not all hold one hash (`heavy`) marks
+    // its cells heavy at once
+    auto mark = [&](uint32_t t, uint32_t col, uint32_t bits, uint32_t run_id, bool heavy) {
+        uint32_t old;
+        if (t - t_lo < kMarkTiles && col - c_lo < kMarkCols) {
+            const uint32_t wi = (t - t_lo) * kMarkStride + ((col - c_lo) >> 5);
+            old = atomicOr(&win[wi], bits);
+            if (LIGHT && ((old & bits) || heavy)) atomicOr(&winH[wi], heavy ? bits : old & bits);
+        } else {
+            old = atomicOr(bm + (uint64_t)t * NW + (col >> 5), bits);
+            if (LIGHT && ((old & bits) || heavy)) atomicOr(bmH + (uint64_t)t * NW + (col >> 5), heavy ? bits : old & bits);
+        }
+        if (LIGHT && !heavy) {
+            uint32_t nb = bits & ~old;
+            while (nb) {
+                const uint32_t b = __ffs(nb) - 1;
+                nb &= nb - 1;
+                crun[(uint64_t)t * N + (col & ~31u) + b] = run_id;
+            }
+        }
     };
     for (uint32_t q = q0 + wave; q < q1; q += kMarkWG / 64) {
-        const uint2 run = runs[order[q]];
+        const uint32_t run_id = order[q];
+        const uint2 run = runs[run_id];
         const uint32_t start = run.x, m = run.y;
         // a run whose entries all hold one 64-bit hash (a hash shared by m
         // genomes; only a low-word collision breaks this) takes the fast path
@@ -306,6 +341,7 @@ __global__ __launch_bounds__(kMarkWG) void k_screen_mark(const uint32_t *__restr
             const uint64_t v = x < m ? H[vals[start + x]] : v0;
             same = __ballot(v != v0) == 0;
         }
+        uint32_t tcarry = 0xFFFFFFFFu;                       // the previous x block's last row tile
         for (uint32_t xb = 0; xb + 1 < m; xb += 64) {
             const uint32_t x = xb + lane;
             const uint32_t ix = vals[start + (x < m ? x : m - 1)];
@@ -313,9 +349,12 @@ __global__ __launch_bounds__(kMarkWG) void k_screen_mark(const uint32_t *__restr
             const uint64_t vx = H[ix];
             const bool x_ok = x < m && gx >= row0 && gx < row1;
             const uint32_t tx = x_ok ? (gx - row0) >> rshift : 0xFFFFFFFFu;
-            // first lane of its row tile among the x tile (lanes are in genome order)
+            // first lane of its row tile among the x entries (lanes are in
+            // genome order; a tile continued from the previous x block has its
+            // head there, which marked every y after it: one mark per run and cell)
             const uint32_t tprev = __shfl_up(tx, 1, 64);
-            const bool tile_head = lane == 0 || tprev != tx;
+            const bool tile_head = lane == 0 ? tx != tcarry || tx == 0xFFFFFFFFu : tprev != tx;
+            tcarry = __builtin_amdgcn_readlane(tx, 63);
             for (uint32_t yb = xb; yb < m; yb += 64) {
                 const uint32_t yl = yb + lane;
                 const bool y_ok = yl < m;
@@ -344,7 +383,7 @@ __global__ __launch_bounds__(kMarkWG) void k_screen_mark(const uint32_t *__restr
                         heads &= heads - 1;
                         const uint32_t T = __builtin_amdgcn_readlane(tx, p);
                         const int32_t qd = (int32_t)(xb + p) - (int32_t)yb;      // y lanes after the tile's first x
-                        if (y_ok && (int32_t)lane > qd && (seg_head || (int32_t)lane == qd + 1)) mark(T, gyl, suf);
+                        if (y_ok && (int32_t)lane > qd && (seg_head || (int32_t)lane == qd + 1)) mark(T, gyl, suf, run_id, false);
                     }
                     continue;
                 }
@@ -362,7 +401,7 @@ __global__ __launch_bounds__(kMarkWG) void k_screen_mark(const uint32_t *__restr
                     // the first ok lane of each row tile marks (lane - 1 not ok, or another tile)
                     const bool prev_ok = lane > 0 && ((okm >> (lane - 1)) & 1ull);
                     if (!ok || (prev_ok && !tile_head)) continue;
-                    mark(tx, gy, 1u << (gy & 31));
+                    mark(tx, gy, 1u << (gy & 31), run_id, true);
                 }
             }
         }
@@ -373,8 +412,79 @@ __global__ __launch_bounds__(kMarkWG) void k_screen_mark(const uint32_t *__restr
         const uint32_t v = win[i];
         if (!v) continue;
         const uint32_t t = t_lo + i / kMarkStride, w = (c_lo >> 5) + i % kMarkStride;
-        if (t < tmax && w < NW) atomicOr(bm + (uint64_t)t * NW + w, v);
+        if (t < tmax && w < NW) {
+            const uint32_t old = atomicOr(bm + (uint64_t)t * NW + w, v);
+            if (LIGHT) {
+                const uint32_t hv = winH[i] | (old & v);          // marked here twice, or by another chunk too
+                if (hv) atomicOr(bmH + (uint64_t)t * NW + w, hv);
+            }
+        }
     }
+}
+
+// The light cells (round 5): a (row tile, column) cell marked by exactly one
+// run of >= 3 entries that all hold one 64-bit hash h, and by no run of two
+// (k_screen_simple marks those heavy).  Each of the tile's rows r < c that
+// holds h shares exactly h with column c -- a second shared hash would be a
+// second run marking the cell -- so its count is (i + j < s), i and j the
+// positions of h in r and in c (h's rank in A u B), and its denominator is s
+// when both sketches are full: the screen writes it here, over the
+// no-shared-hash fill, and the LIST kernel never streams the column.  At
+// configs[4] these are most cells: unrelated families sharing one hash by
+// chance (each such hash marks family x family cells).  A cell with a partial
+// sketch goes heavy.  One thread per bitmap word.
+__global__ __launch_bounds__(kScWG) void k_screen_light(const uint32_t *__restrict__ bm, uint32_t *__restrict__ bmH,
+                                                        const uint32_t *__restrict__ crun, const uint2 *__restrict__ runs,
+                                                        const uint32_t *__restrict__ vals, const uint32_t *__restrict__ nh,
+                                                        uint32_t s, uint32_t N, uint32_t row0, uint32_t row1, uint32_t R,
+                                                        uint32_t NW, uint64_t nwords, uint64_t seg0,
+                                                        uint16_t *__restrict__ common,
+                                                        unsigned long long *__restrict__ nlight) {
+    uint32_t mine = 0;
+    for (uint64_t wi = (uint64_t)blockIdx.x * kScWG + threadIdx.x; wi < nwords; wi += (uint64_t)gridDim.x * kScWG) {
+        uint32_t L = bm[wi] & ~bmH[wi];
+        if (!L) continue;
+        const uint32_t t = (uint32_t)(wi / NW), w = (uint32_t)(wi % NW);
+        const uint32_t r0 = row0 + t * R;
+        uint32_t heavy = 0;
+        while (L) {
+            const uint32_t b = __ffs(L) - 1;
+            L &= L - 1;
+            const uint32_t c = w * 32 + b;
+            const uint2 run = runs[crun[(uint64_t)t * N + c]];
+            // position of genome g's entry in the run (entries in genome order), or -1
+            auto find = [&](uint32_t g) -> int32_t {
+                uint32_t lo = 0, hi = run.y;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (vals[run.x + mid] / s < g) lo = mid + 1; else hi = mid;
+                }
+                if (lo < run.y && vals[run.x + lo] / s == g) return (int32_t)(vals[run.x + lo] - g * s);
+                return -1;
+            };
+            bool part = nh[c] != s;
+            for (uint32_t j = 0; j < R; j++) {
+                const uint32_t r = r0 + j;
+                if (r >= row1 || r >= c) break;
+                part |= nh[r] != s;
+            }
+            const int32_t pc = find(c);
+            if (part || pc < 0) { heavy |= 1u << b; continue; }
+            for (uint32_t j = 0; j < R; j++) {
+                const uint32_t r = r0 + j;
+                if (r >= row1 || r >= c) break;
+                const int32_t pr = find(r);
+                if (pr < 0) continue;                                  // r shares no hash with c
+                const uint64_t o = (uint64_t)r * N - (uint64_t)r * (r + 1) / 2 + (c - r - 1) - seg0;
+                common[o] = (uint16_t)((uint32_t)(pr + pc) < s ? 1 : 0);
+                mine++;
+            }
+        }
+        if (heavy) atomicOr(bmH + wi, heavy);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
+    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(nlight, (unsigned long long)mine);
 }
 
 // per row tile (one workgroup): marked columns -> cnt[t], items -> itc[t]
@@ -610,6 +720,16 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
     uint32_t *d_bm, *d_cnt, *d_itc;
     uint64_t *d_coff, *d_cnt64;
     if ((rc = scratch(ctx, "sc_bitmap", (uint64_t)ntiles * NW * 4, (void **)&d_bm))) return rc;
+    // Light cells (k_screen_light): a heavy-cell bitmap and each cell's first
+    // marking run, (ntiles x N) words -- taken when that fits kLightBudget
+    // (N = 10^4 with R = 4: 100 MB); DREPHIP_SCREEN_LIGHT=0 turns it off (A/B)
+    const char *le = getenv("DREPHIP_SCREEN_LIGHT");
+    const bool light = (!le || atoi(le) != 0) && (uint64_t)ntiles * N * 4 <= kLightBudget;
+    uint32_t *d_bmH = nullptr, *d_crun = nullptr;
+    if (light) {
+        if ((rc = scratch(ctx, "sc_bitmap_heavy", (uint64_t)ntiles * NW * 4, (void **)&d_bmH))) return rc;
+        if ((rc = scratch(ctx, "sc_crun", (uint64_t)ntiles * N * 4, (void **)&d_crun))) return rc;
+    }
     if ((rc = scratch(ctx, "sc_tcnt", (ntiles + 1) * 4ull, (void **)&d_cnt))) return rc;
     if ((rc = scratch(ctx, "sc_tcnt64", (ntiles + 1) * 8ull, (void **)&d_cnt64))) return rc;
     if ((rc = scratch(ctx, "sc_titc", (ntiles + 1) * 4ull, (void **)&d_itc))) return rc;
@@ -631,6 +751,7 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
     if ((rc = screen_fill_impl(ctx, d_nhash, N, row0, row1, seg0, npairs, d_common, d_denom, st))) return rc;
     prof.mark("fill", st);
     HIPC(hipMemsetAsync(d_bm, 0, (uint64_t)ntiles * NW * 4, st));
+    if (light) HIPC(hipMemsetAsync(d_bmH, 0, (uint64_t)ntiles * NW * 4, st));
     HIPC(hipMemsetAsync(pkey, 0xFF, pcap * 8ull, st));
     HIPC(hipMemsetAsync(pcnt, 0, pcap * 4ull, st));
     HIPC(hipMemsetAsync(d_nsimple, 0, 8, st));
@@ -643,8 +764,14 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
         if ((rc = scratch(ctx, "sc_sort_tmp2", std::max<size_t>(tb, 16), &tmp))) return rc;
         HIPC(hipcub::DeviceRadixSort::SortPairs(tmp, tb, rfirst, rfirst_s, ridx, ridx_s, nruns, 0, 32, st));
         prof.mark("run-sort", st);
-        hipLaunchKernelGGL(k_screen_mark, dim3((nruns + kMarkChunk - 1) / kMarkChunk), dim3(kMarkWG), 0, st, v_out,
-                           d_hashes, s, d_runs, ridx_s, rfirst_s, nruns, row0, row1, rshift, NW, d_bm);
+        if (light)
+            hipLaunchKernelGGL(k_screen_mark<true>, dim3((nruns + kMarkChunk - 1) / kMarkChunk), dim3(kMarkWG), 0, st,
+                               v_out, d_hashes, s, d_runs, ridx_s, rfirst_s, nruns, row0, row1, rshift, NW, d_bm, d_bmH,
+                               d_crun, N);
+        else
+            hipLaunchKernelGGL(k_screen_mark<false>, dim3((nruns + kMarkChunk - 1) / kMarkChunk), dim3(kMarkWG), 0, st,
+                               v_out, d_hashes, s, d_runs, ridx_s, rfirst_s, nruns, row0, row1, rshift, NW, d_bm, nullptr,
+                               nullptr, N);
     }
     if (n2) {
         const uint32_t g2 = std::max(1u, std::min(8192u, (n2 + kScWG - 1) / kScWG));
@@ -652,10 +779,19 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
                            pkey, pcnt, ppos, (uint32_t)(pcap - 1));
         const uint32_t gs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, (pcap + kScWG - 1) / kScWG));
         hipLaunchKernelGGL(k_screen_simple, dim3(gs), dim3(kScWG), 0, st, pkey, pcnt, ppos, (uint32_t)pcap, d_nhash, s, N, row0,
-                           rshift, NW, seg0, d_bm, d_common, d_nsimple);
+                           rshift, NW, seg0, d_bm, d_bmH, d_common, d_nsimple);
     }
     prof.mark("mark", st);
-    hipLaunchKernelGGL(k_screen_count, dim3(ntiles), dim3(kScWG), 0, st, d_bm, NW, C, d_cnt, d_cnt64, d_itc);
+    if (light && nruns) {
+        const uint64_t nwords = (uint64_t)ntiles * NW;
+        const uint32_t gl = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(16384, (nwords + kScWG - 1) / kScWG));
+        hipLaunchKernelGGL(k_screen_light, dim3(gl), dim3(kScWG), 0, st, d_bm, d_bmH, d_crun, d_runs, v_out, d_nhash, s, N,
+                           row0, row1, R, NW, nwords, seg0, d_common, d_nsimple);
+        prof.mark("light", st);
+    }
+    // the LIST kernels take the heavy cells (every marked cell without the light screen)
+    const uint32_t *d_bl = light ? d_bmH : d_bm;
+    hipLaunchKernelGGL(k_screen_count, dim3(ntiles), dim3(kScWG), 0, st, d_bl, NW, C, d_cnt, d_cnt64, d_itc);
     // the last entry of each scan holds the totals: count entries ntiles + 1, the last one zero.
     // The column offsets are summed in 64 bits (the marked cells may pass 2^32;
     // a 32-bit scan would wrap and the fallback below would never fire)
@@ -699,7 +835,7 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
     HIPC(hipMemcpyAsync(d_ibase, ibase, ntiles * 4ull, hipMemcpyHostToDevice, st));
     HIPC(hipMemsetAsync(d_items, 0xFF, std::max<uint64_t>(nitems, 1) * 16, st));       // idle items: i0 = ~0
     prof.mark("readback+alloc", st);
-    hipLaunchKernelGGL(k_screen_lists, dim3(ntiles), dim3(kScWG), 0, st, d_bm, NW, C, row0, R, d_cnt, d_coff, d_ibase,
+    hipLaunchKernelGGL(k_screen_lists, dim3(ntiles), dim3(kScWG), 0, st, d_bl, NW, C, row0, R, d_cnt, d_coff, d_ibase,
                        d_list, d_items);
     prof.mark("lists", st);
     timing_mark(ctx, 4, st, false);

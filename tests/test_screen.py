@@ -176,6 +176,52 @@ def test_screen_single_shared_hash_pairs():
     assert planted > 500 and (oc == 1).sum() > 100 and ((oc == 0) & (od == s)).sum() > 1000
 
 
+@pytest.mark.parametrize("s,N", [(300, 400), (4096, 260)])
+def test_screen_light_cells(s, N, monkeypatch):
+    """Light cells (k_screen_light): values shared by groups of 3..150
+    genomes (runs of >= 3 entries, some longer than a wave, so row tiles
+    straddle x blocks), most pairs of a group sharing only that value, planted
+    at ranks on both sides of i + j = s; some pairs share two group values or
+    a group value and a two-genome value (heavy: the LIST kernel), some
+    sketches are partial (heavy), some values agree in their low word only.
+    The screen writes the light pairs itself: bit-exact against the oracle and
+    against the screen without the light path, which leaves more cells to the
+    kernel."""
+    rng = np.random.default_rng(s + N)
+    H = np.sort(rng.integers(1, 1 << 62, size=(N, s), dtype=np.uint64), axis=1)
+    NH = np.full(N, s, dtype=np.uint32)
+    for g in range(0, N, 23):
+        NH[g] = rng.integers(s // 3, s)
+        H[g, NH[g]:] = UMAX
+
+    def plant(members, v):
+        for g in members:
+            if v in H[g, :NH[g]]:
+                continue
+            j = int(rng.integers(0, NH[g]))
+            row = np.sort(np.concatenate([np.delete(H[g, :NH[g]], j), [v]]))
+            H[g, :NH[g]] = row
+    for k in range(160):
+        m = int(rng.choice([3, 4, 7, 12, 40, 70, 150]))
+        plant(rng.choice(N, m, replace=False), np.uint64(rng.integers(1, 1 << 62)))
+    for _ in range(80):                                  # two-genome values on top (simple or heavy)
+        plant(rng.choice(N, 2, replace=False), np.uint64(rng.integers(1, 1 << 62)))
+    for _ in range(30):                                  # low-word twins: equal sort keys, no shared hash
+        a, b = rng.choice(N, 2, replace=False)
+        v = H[a, rng.integers(0, NH[a])]
+        plant([b], (v & np.uint64(0xFFFFFFFF)) | (np.uint64(rng.integers(1, 1 << 30)) << np.uint64(32)))
+    oc, od = oracle.allpairs(H, NH, s, threads=8)
+    with _lib.Context(0, 21, s, 42) as ctx:
+        c, d, st = run(ctx, H, NH, ctx.SCREEN_ON)
+        assert np.array_equal(c, oc) and np.array_equal(d, od)
+        monkeypatch.setenv("DREPHIP_SCREEN_LIGHT", "0")
+        c2, d2, st2 = run(ctx, H, NH, ctx.SCREEN_ON)
+        assert np.array_equal(c2, oc) and np.array_equal(d2, od)
+    # the light path wrote pairs itself and left fewer cells to the kernel
+    assert st["simple"] > st2["simple"] + 1000 and st["marked"] < st2["marked"], (st, st2)
+    assert (oc == 1).sum() > 1000 and ((oc == 0) & (od == s)).sum() > 1000
+
+
 def test_screen_mode_argument_checked():
     with _lib.Context(0, 21, 1000, 42) as ctx:
         with pytest.raises(_lib.DrepHipError, match="unknown screen mode"):
