@@ -52,26 +52,9 @@ constexpr int kLkWG = 256;
 #ifndef DREPHIP_LK_COLSTORE
 #define DREPHIP_LK_COLSTORE 3
 #endif
-// Deferred column (round 5): a merge launch writes only row y; the NEXT launch
-// scatters column y (D[i][y] = D[y][i]) early, beside its own decision and row
-// loads, so the scattered stores drain during that launch instead of at the end
-// of the merge launch.  Until then every read of an entry (R, y) goes to row y
-// (D[y][R]).  0 (default): the column written in the merge launch itself.
-// Measured slower (chain at 10^5: 997 ms deferred vs 932 ms not, same
-// protocol, profiles/r05_linkage_ab_defer_spec4.txt): the next launch then
-// carries row pc's loads and the scatter on its own critical path
-#ifndef DREPHIP_LK_DEFERCOL
-#define DREPHIP_LK_DEFERCOL 0
-#endif
 // Row-y stores (contiguous, 8n bytes per merge): 1 plain (default), 3 write-through (A/B)
 #ifndef DREPHIP_LK_ROWSTORE
 #define DREPHIP_LK_ROWSTORE 1
-#endif
-// Candidate-row prefetch (round 5): the step loads its entries of six
-// candidate rows before the decision instead of the decided rows after it
-// (k_nn_step).  0: the rows loaded after the decision (A/B)
-#ifndef DREPHIP_LK_PREFETCH
-#define DREPHIP_LK_PREFETCH 1
 #endif
 constexpr uint32_t kLkSmallN = 30000;
 
@@ -173,15 +156,9 @@ __device__ __forceinline__ void wave_argmin(double &v, int32_t &i) {
     wave_argmin_n<1>(vv, ii);
     v = vv[0]; i = ii[0];
 }
-// one to four sets (block-uniform counts; d implies b and c), interleaved
-__device__ __forceinline__ void wave_argmin_upto4(MinIdx &a, MinIdx &b, MinIdx &c, MinIdx &d, bool with_b, bool with_c,
-                                                  bool with_d) {
-    if (with_d) {
-        double v[4] = {a.v, b.v, c.v, d.v};
-        int32_t i[4] = {a.i, b.i, c.i, d.i};
-        wave_argmin_n<4>(v, i);
-        a = MinIdx{v[0], i[0]}; b = MinIdx{v[1], i[1]}; c = MinIdx{v[2], i[2]}; d = MinIdx{v[3], i[3]};
-    } else if (with_c) {
+// one, two or three sets (block-uniform counts), interleaved
+__device__ __forceinline__ void wave_argmin_upto3(MinIdx &a, MinIdx &b, MinIdx &c, bool with_b, bool with_c) {
+    if (with_c) {
         double v[3] = {a.v, b.v, c.v};
         int32_t i[3] = {a.i, b.i, c.i};
         wave_argmin_n<3>(v, i);
@@ -215,26 +192,23 @@ __device__ MinIdx block_argmin(double v, int32_t i) {
 // A lane's share of the previous launch's partial sets: partials lane,
 // lane + 64, ... U at a time, every load in flight before the first wait
 template <int U>
-__device__ __forceinline__ void partial_pass(const MinIdx *P1, const MinIdx *P2, const MinIdx *P3, const MinIdx *P4,
-                                             uint32_t G, MinIdx &g, MinIdx &g2, MinIdx &g3, MinIdx &g4) {
+__device__ __forceinline__ void partial_pass(const MinIdx *P1, const MinIdx *P2, const MinIdx *P3, uint32_t G,
+                                             MinIdx &g, MinIdx &g2, MinIdx &g3) {
     for (uint32_t b0 = threadIdx.x; b0 < G; b0 += 64 * U) {
-        MinIdx m1[U], m2[U], m3[U], m4[U];
+        MinIdx m1[U], m2[U], m3[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const uint32_t b = min(b0 + 64u * u, G - 1);             // (a repeated partial changes no minimum)
-            m1[u] = P1[b]; m2[u] = P2[b]; m3[u] = P3[b]; m4[u] = P4[b];
+            m1[u] = P1[b]; m2[u] = P2[b]; m3[u] = P3[b];
         }
 #pragma unroll
-        for (int u = 0; u < U; u++) {
+        for (int u = 0; u < U; u++)
             asm volatile("" : "+v"(m1[u].v), "+v"(m1[u].i), "+v"(m2[u].v), "+v"(m2[u].i), "+v"(m3[u].v), "+v"(m3[u].i));
-            asm volatile("" : "+v"(m4[u].v), "+v"(m4[u].i));
-        }
 #pragma unroll
         for (int u = 0; u < U; u++) {
             if (better(m1[u].v, m1[u].i, g.v, g.i)) g = m1[u];
             if (better(m2[u].v, m2[u].i, g2.v, g2.i)) g2 = m2[u];
             if (better(m3[u].v, m3[u].i, g3.v, g3.i)) g3 = m3[u];
-            if (better(m4[u].v, m4[u].i, g4.v, g4.i)) g4 = m4[u];
         }
     }
 }
@@ -244,26 +218,24 @@ __device__ __forceinline__ void partial_pass(const MinIdx *P1, const MinIdx *P2,
 // are reduced only when the (block-uniform) flags ask for them: an unneeded
 // wave reduction measured as costly as the barrier it saves.
 template <int WG>
-__device__ void block_argmin4(MinIdx &a, MinIdx &b, MinIdx &c, MinIdx &d, bool with_b, bool with_c, bool with_d) {
-    __shared__ double sv[4][WG / 64];
-    __shared__ int32_t si[4][WG / 64];
-    wave_argmin_upto4(a, b, c, d, with_b, with_c, with_d);
+__device__ void block_argmin3(MinIdx &a, MinIdx &b, MinIdx &c, bool with_b, bool with_c) {
+    __shared__ double sv[3][WG / 64];
+    __shared__ int32_t si[3][WG / 64];
+    wave_argmin_upto3(a, b, c, with_b, with_c);
     if constexpr (WG == 64) return;                            // one wave: every lane holds the result
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
         sv[0][w] = a.v; si[0][w] = a.i;
         sv[1][w] = b.v; si[1][w] = b.i;
         sv[2][w] = c.v; si[2][w] = c.i;
-        sv[3][w] = d.v; si[3][w] = d.i;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        a = b = c = d = MinIdx{INFINITY, 0x7fffffff};
+        a = b = c = MinIdx{INFINITY, 0x7fffffff};
         for (int k = 0; k < WG / 64; k++) {
             if (better(sv[0][k], si[0][k], a.v, a.i)) { a.v = sv[0][k]; a.i = si[0][k]; }
             if (better(sv[1][k], si[1][k], b.v, b.i)) { b.v = sv[1][k]; b.i = si[1][k]; }
             if (better(sv[2][k], si[2][k], c.v, c.i)) { c.v = sv[2][k]; c.i = si[2][k]; }
-            if (better(sv[3][k], si[3][k], d.v, d.i)) { d.v = sv[3][k]; d.i = si[3][k]; }
         }
     }
 }
@@ -420,15 +392,9 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                                                    int32_t *__restrict__ size, int32_t *__restrict__ chain,
                                                    LinkState *__restrict__ st, LinkFwd *__restrict__ fwd,
                                                    MinIdx *__restrict__ parts, MinIdx *__restrict__ parts2,
-                                                   MinIdx *__restrict__ parts3, MinIdx *__restrict__ parts4,
-                                                   int32_t *__restrict__ done, double *__restrict__ Z, uint32_t q,
-                                                   int spec_on) {
+                                                   MinIdx *__restrict__ parts3, int32_t *__restrict__ done,
+                                                   double *__restrict__ Z, uint32_t q, int spec_on) {
     __shared__ LinkState sx;
-    // every kernel argument into SGPRs with the first argument loads: left to
-    // itself the compiler loaded n and the pointers the decision uses in the
-    // middle of it, each load a scalar-cache round trip on the critical path
-    asm volatile("" ::"s"(D), "s"(n), "s"(size), "s"(chain), "s"(st), "s"(fwd), "s"(parts), "s"(parts2), "s"(parts3),
-                 "s"(parts4), "s"(done), "s"(Z), "s"(q), "s"(spec_on));
     const uint32_t G = gridDim.x - 1;                          // step workgroups; workgroup G forwards operands
     // The partial sets are reduced by wave 0 alone (the decision is wave 0's:
     // no barrier), read whether or not they are needed (valid memory either
@@ -442,7 +408,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     // runs on every lane of wave 0 as scalar code, its values in SGPRs (as
     // one lane's divergent code it took ~0.8 us a launch)
     const bool wave0 = __builtin_amdgcn_readfirstlane(threadIdx.x) < 64, lane0 = threadIdx.x == 0;
-    MinIdx g{INFINITY, 0x7fffffff}, g2{INFINITY, 0x7fffffff}, g3{INFINITY, 0x7fffffff}, g4{INFINITY, 0x7fffffff};
+    MinIdx g{INFINITY, 0x7fffffff}, g2{INFINITY, 0x7fffffff}, g3{INFINITY, 0x7fffffff};
     // state and forwarded operands: vector loads through an opaque zero lane
     // offset, issued first, so the partial loads go out behind them and one
     // wait covers both (as scalar loads, a state field landing in a scalar
@@ -455,9 +421,9 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     uint4 sw0 = sv[0], sw1 = sv[1], sw2 = sv[2], sw3 = sv[3], fw0 = fv[0], fw1 = fv[1], fw2 = fv[2];
     if (wave0) {
         const MinIdx *P1 = parts + (uint64_t)(q ^ 1) * 1024, *P2 = parts2 + (uint64_t)(q ^ 1) * 1024,
-                     *P3 = parts3 + (uint64_t)(q ^ 1) * 1024, *P4 = parts4 + (uint64_t)(q ^ 1) * 1024;
-        if (G <= 256) partial_pass<4>(P1, P2, P3, P4, G, g, g2, g3, g4);
-        else partial_pass<8>(P1, P2, P3, P4, G, g, g2, g3, g4);      // (up to 512 workgroups in one pass)
+                     *P3 = parts3 + (uint64_t)(q ^ 1) * 1024;
+        if (G <= 256) partial_pass<4>(P1, P2, P3, G, g, g2, g3);
+        else partial_pass<8>(P1, P2, P3, G, g, g2, g3);              // (up to 512 workgroups in one pass)
     }
     asm volatile("" : "+v"(sw0.x), "+v"(sw0.y), "+v"(sw0.z), "+v"(sw0.w), "+v"(sw1.x), "+v"(sw1.y), "+v"(sw1.z),
                  "+v"(sw1.w), "+v"(sw2.x), "+v"(sw2.y), "+v"(sw2.z), "+v"(sw2.w), "+v"(sw3.x), "+v"(sw3.y),
@@ -466,64 +432,11 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                  "+v"(fw1.w), "+v"(fw2.x), "+v"(fw2.y), "+v"(fw2.z));
     const LinkState S = state_from_words(sw0, sw1, sw2, sw3);
     const LinkFwd F = fwd_from_words(fw0, fw1, fw2);
-#if DREPHIP_LK_PREFETCH
-    // Candidate rows: in a merge launch every row the step reads is known
-    // before its decision -- the merged pair is the top and the element below
-    // it (or the previous merge's row and the top), the speculation's rows are
-    // the chain entries c3..c5 (forwarded), and the deferred column's row is the
-    // previous merge's y.  Each step workgroup issues its entries of these six
-    // rows (and of size) here, so that they land during the decision instead
-    // of after it; a decided row outside them (a pushed nearest neighbour) is
-    // loaded after the decision as before.  The candidates' pairwise entries
-    // (the uniform operands of the pass), read as Duni does (an entry of the
-    // previous merge's row y is taken from row y, whose column may not be
-    // scattered yet), and their sizes go to LDS (kPairs).
-    constexpr int kCand = 6;
-    __shared__ double s_pair[kCand * kCand];
-    __shared__ int32_t s_csz[kCand];
-    int32_t cand[kCand] = {S.top, S.below, S.pend ? S.y : -1, S.len >= 3 ? F.c3 : -1, S.len >= 4 ? F.c4 : -1,
-                           S.len >= 5 ? F.c5 : -1};
-#pragma unroll
-    for (int j = 0; j < kCand; j++) if ((uint32_t)cand[j] >= n) cand[j] = -1;
-    double pre[kCand][kLkPer], pairv = 0.0;
-    int32_t psz[kLkPer], pszc = 0;
-    const uint32_t pwave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    constexpr uint32_t kPairWave = WG / 64 - 1;                // the last wave loads the pair entries
-    if (blockIdx.x != gridDim.x - 1) {
-        const uint32_t pstride = (gridDim.x - 1) * WG;
-#pragma unroll
-        for (int k = 0; k < kLkPer; k++) {
-            const uint32_t i = blockIdx.x * WG + threadIdx.x + k * pstride;
-            const uint32_t ic = i < n ? i : n - 1;
-            psz[k] = size[ic];
-#pragma unroll
-            for (int j = 0; j < kCand; j++) pre[j][k] = D[(uint64_t)(cand[j] < 0 ? 0 : cand[j]) * n + ic];
-        }
-        if (pwave == kPairWave) {
-            // lane l < 36: entry (cand[l / 6], cand[l % 6]); lane 36 + j: size
-            // of cand[j].  Every lane loads (invalid ones entry 0): no divergent
-            // branch -- a load into a register the other branch also wrote made
-            // the wave wait for all of its prefetch loads here
-            const uint32_t l = threadIdx.x & 63;
-            int32_t a = -1, b = -1, c = -1;
-#pragma unroll
-            for (int j = 0; j < kCand; j++) {
-                a = l / kCand == (uint32_t)j ? cand[j] : a;
-                b = l % kCand == (uint32_t)j ? cand[j] : b;
-                c = l == (uint32_t)(kCand * kCand + j) ? cand[j] : c;
-            }
-            const bool ok = l < kCand * kCand && a >= 0 && b >= 0;
-            const bool by = S.pend && b == S.y;                  // entry (a, y): from row y
-            pairv = D[!ok ? 0 : by ? (uint64_t)b * n + a : (uint64_t)a * n + b];
-            pszc = size[c >= 0 ? c : 0];
-        }
-    }
-#endif
 #if DREPHIP_LK_PHASES
     uint64_t ph0 = 0, ph1 = 0, ph2 = 0, ph3 = 0, ph4 = 0, ph5 = 0, ph6 = 0;
 #endif
     LK_T(ph0);
-    if (wave0) wave_argmin_upto4(g, g2, g3, g4, S.pend || F.spec, F.spec != 0, S.spec == 4);
+    if (wave0) wave_argmin_upto3(g, g2, g3, S.pend || F.spec, F.spec != 0);
     LK_T(ph1);
     if (S.k >= (int32_t)n - 1) return;                         // all merged
     const bool w0 = blockIdx.x == 0;
@@ -540,7 +453,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
         // other waves, so after the `if (wave0)` above the compiler held them
         // (and everything the decision derives from them) in VGPRs under exec
         // masks -- ~1,000 cycles of one wave's vector code per launch
-        g = uni(g); g2 = uni(g2); g3 = uni(g3); g4 = uni(g4);
+        g = uni(g); g2 = uni(g2); g3 = uni(g3);
         // (plain scalars, the state struct written once at the end: a struct
         // updated across the branches was kept in private memory)
         int32_t k = S.k, len = S.len, top = S.top, below = S.below, first_active = S.first_active;
@@ -646,7 +559,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                 len++;
                 if (r.i != mrow || mrow < 0 || d == 1) break;      // the pushed row is searched by this launch
                 szt = spsbsz;                                       // y: just formed, its size is the override
-                r = S.spec == 4 ? g4 : g2;                          // y's minimum, from the merge step
+                r = g2;                                             // y's minimum, from the merge step
                 LK_DIAG(twice);
             }
         }
@@ -665,8 +578,6 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
         } else if (spec_on && len >= 3 && k < (int32_t)n - 1) {
             if (!pend) X.spec = 1;                              // a search launch
             else if (below == py && top != py) X.spec = 2;      // a merge launch, its row y below the top
-            else if (spec_on > 2) X.spec = 4;                   // any other merge launch (round 5): speculate,
-                                                                // y's own minimum in P4 for a push of y
         }
 #if DREPHIP_LK_DIAG
         if (!pend) LK_DIAG(scans);
@@ -698,20 +609,10 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             // c5 and c6 forwarded)
             const bool sp = X.spec && len >= 4 && ck >= 2;
             int32_t rzt = size[top], rzb = size[two ? below : top];
-            // (an entry (a, pc) of the previous merge's column pc, not yet
-            // scattered, is read from row pc)
-#if DREPHIP_LK_DEFERCOL
-            const int32_t pc = S.pend && S.y != px && !(pend && S.y == py) ? S.y : -1;
-#else
-            const int32_t pc = -1;
-#endif
-            auto dat = [&](int32_t a, int32_t b) -> uint64_t {
-                return b == pc ? (uint64_t)b * n + a : (uint64_t)a * n + b;
-            };
-            double rdp = D[two ? dat(top, below) : (uint64_t)top * n + top];
+            double rdp = D[(uint64_t)top * n + (two ? below : top)];
             int32_t r3 = chain[l3 ? len - 3 : 0], r4 = chain[l4 ? len - 4 : 0], r5 = chain[l5 ? len - 5 : 0],
                     r6 = chain[l6 ? len - 6 : 0];
-            double rdp2 = D[sp ? dat(c3, c4) : 0];
+            double rdp2 = D[sp ? (uint64_t)c3 * n + c4 : 0];
             asm volatile("" : "+v"(rzt), "+v"(rzb), "+v"(rdp), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(rdp2));
             LK_T(ph3);
             auto size_now = [&](int32_t i, int32_t stored) {
@@ -741,13 +642,6 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
         }
     }
     if (blockIdx.x == G) return;                               // the forwarding workgroup has no step work
-#if DREPHIP_LK_PREFETCH
-    if (pwave == kPairWave) {
-        const uint32_t l = threadIdx.x & 63;
-        if (l < kCand * kCand) s_pair[l] = pairv;
-        else if (l < kCand * kCand + kCand) s_csz[l - kCand * kCand] = pszc;
-    }
-#endif
     __syncthreads();
     const LinkState X = sx;
     LK_T(ph3);
@@ -774,91 +668,23 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     // loads, which the compiler waited for before the pass.)
     int32_t lz;
     asm volatile("v_mov_b32 %0, 0" : "=v"(lz));
-    // the previous launch's merged row pc, whose column this launch scatters
-    // (not when this launch's merge retires or rewrites it): entries (R, pc)
-    // of the rows read are taken from row pc
-#if DREPHIP_LK_DEFERCOL
-    const int32_t pc = S.pend && S.y != x && !(pend && S.y == y) ? S.y : -1;
-#else
-    const int32_t pc = -1;
-#endif
-    const bool hpc = pc >= 0;
-    const double *Dpc = D + (uint64_t)(hpc ? pc : 0) * n;
-    auto Duni = [&](int32_t a, int32_t b) -> double {          // D[a][b] as of this launch's start
-        return b == pc ? Dpc[a + lz] : D[(uint64_t)a * n + b + lz];
-    };
     const bool fa = pend && !yA, fb = pend && sp && !yB, fw = pend && hasW && !yW;
-#if DREPHIP_LK_PREFETCH
-    // the decided rows among the candidates (-1: not a candidate, loaded below)
-    auto cidx = [&](int32_t r) -> int {
-        int j = -1;
-#pragma unroll
-        for (int jj = kCand - 1; jj >= 0; jj--) if (r >= 0 && r == cand[jj]) j = jj;
-        return j;
-    };
-    const int jx = pend ? cidx(x) : -1, jy = pend ? cidx(y) : -1, jA = cidx(A), jB = sp ? cidx(B) : -1,
-              jW = hasW ? cidx(W) : -1, jpc = hpc ? cidx(pc) : -1;
-    // entry (a, b) as of this launch's start: from the candidates' pair
-    // entries, else loaded (Duni)
-    auto Dpair = [&](int ja, int jb, int32_t a, int32_t b) -> double {
-        return ja >= 0 && jb >= 0 ? s_pair[ja * kCand + jb] : Duni(a, b);
-    };
-    // the prefetched row of candidate j (a uniform select), entry k.  The
-    // entries pass through an empty asm first, so the select is one of values:
-    // a select between array elements was folded into one load at a computed
-    // index, which put the array in scratch (each prefetch load was then
-    // waited for at once, to be stored there)
-    static_assert(kCand == 6, "sel names the six candidates");
-    auto sel = [&](int j, int k) -> double {
-        double a0 = pre[0][k], a1 = pre[1][k], a2 = pre[2][k], a3 = pre[3][k], a4 = pre[4][k], a5 = pre[5][k];
-        asm volatile("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5));
-        return j == 0 ? a0 : j == 1 ? a1 : j == 2 ? a2 : j == 3 ? a3 : j == 4 ? a4 : a5;
-    };
-    double xa = fa ? Dpair(jx, jA, x, A) : 0.0, ya_ = fa ? Dpair(jy, jA, y, A) : 0.0;
-    double xb = fb ? Dpair(jx, jB, x, B) : 0.0, yb = fb ? Dpair(jy, jB, y, B) : 0.0;
-    double xw = fw ? Dpair(jx, jW, x, W) : 0.0, yw = fw ? Dpair(jy, jW, y, W) : 0.0;
-    double qa = hpc && !yA ? Dpair(jpc, jA, pc, A) : 0.0, qb = hpc && sp && !yB ? Dpair(jpc, jB, pc, B) : 0.0;
-    double qw = hpc && hasW && !yW ? Dpair(jpc, jW, pc, W) : 0.0;
-    double qx = hpc && pend ? Dpair(jpc, jx, pc, x) : 0.0, qy = hpc && pend ? Dpair(jpc, jy, pc, y) : 0.0;
-    int32_t rsa = sp ? (jA >= 0 ? s_csz[jA] : size[A + lz]) : 0, rsb = sp ? (jB >= 0 ? s_csz[jB] : size[B + lz]) : 0;
-#else
-    double xa = fa ? Duni(x, A) : 0.0, ya_ = fa ? Duni(y, A) : 0.0;
-    double xb = fb ? Duni(x, B) : 0.0, yb = fb ? Duni(y, B) : 0.0;
-    double xw = fw ? Duni(x, W) : 0.0, yw = fw ? Duni(y, W) : 0.0;
-    // entry pc of the rows read from memory: row pc's entries
-    double qa = hpc && !yA ? Dpc[A + lz] : 0.0, qb = hpc && sp && !yB ? Dpc[B + lz] : 0.0;
-    double qw = hpc && hasW && !yW ? Dpc[W + lz] : 0.0;
-    double qx = hpc && pend ? Dpc[x + lz] : 0.0, qy = hpc && pend ? Dpc[y + lz] : 0.0;
+    double xa = fa ? Dx[A + lz] : 0.0, ya_ = fa ? Dy[A + lz] : 0.0;
+    double xb = fb ? Dx[B + lz] : 0.0, yb = fb ? Dy[B + lz] : 0.0;
+    double xw = fw ? Dx[W + lz] : 0.0, yw = fw ? Dy[W + lz] : 0.0;
     // the sizes of A and B as of this step's decision (for the speculated merge)
     int32_t rsa = sp ? size[A + lz] : 0, rsb = sp ? size[B + lz] : 0;
-#endif
     auto size_x = [&](int32_t i, int32_t stored) {
         return pend && i == x ? 0 : pend && i == y ? nx + ny : size_prev(i, stored);
     };
-    double bv = INFINITY, yv = INFINITY, wv = INFINITY, zv = INFINITY;
-    int32_t bi = 0x7fffffff, yi = 0x7fffffff, wi = 0x7fffffff, zi = 0x7fffffff;
-    const bool y4 = spec == 4;                                  // y's own minimum apart from the speculation
+    double bv = INFINITY, yv = INFINITY, wv = INFINITY;
+    int32_t bi = 0x7fffffff, yi = 0x7fffffff, wi = 0x7fffffff;
     int32_t sxs = 0, sys = 0;                                   // the speculated merge's sizes
     const uint32_t stride = G * WG;
     bool first = true;
     for (uint32_t i0 = blockIdx.x * WG + threadIdx.x; i0 < n; i0 += kLkPer * stride) {
         int32_t sz[kLkPer];
-        double da[kLkPer], dx[kLkPer], dy[kLkPer], dw[kLkPer], db[kLkPer], dp[kLkPer];
-#if DREPHIP_LK_PREFETCH
-        if (first) {                                            // the prefetched pass (same i as the prefetch)
-#pragma unroll
-            for (int k = 0; k < kLkPer; k++) {
-                const uint32_t i = i0 + k * stride;
-                const uint32_t ic = i < n ? i : n - 1;
-                sz[k] = psz[k];
-                if (!yA) da[k] = jA >= 0 ? sel(jA, k) : Da[ic];
-                if (pend) { dx[k] = jx >= 0 ? sel(jx, k) : Dx[ic]; dy[k] = jy >= 0 ? sel(jy, k) : Dy[ic]; }
-                if (sp && !yB) db[k] = jB >= 0 ? sel(jB, k) : Db[ic];
-                if (hasW && !yW) dw[k] = jW >= 0 ? sel(jW, k) : Dw[ic];
-                if (hpc) dp[k] = jpc >= 0 ? sel(jpc, k) : Dpc[ic];
-            }
-        } else
-#endif
+        double da[kLkPer], dx[kLkPer], dy[kLkPer], dw[kLkPer], db[kLkPer];
 #pragma unroll
         for (int k = 0; k < kLkPer; k++) {
             const uint32_t i = i0 + k * stride;
@@ -868,7 +694,6 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             if (pend) { dx[k] = Dx[ic]; dy[k] = Dy[ic]; }
             if (sp && !yB) db[k] = Db[ic];
             if (hasW && !yW) dw[k] = Dw[ic];
-            if (hpc) dp[k] = Dpc[ic];                           // row pc: the column scatter's values
         }
         // every load of the pass in flight before any is waited for: left to
         // itself the compiler sank the row loads below the size test that
@@ -881,13 +706,11 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             if (pend) asm volatile("" : "+v"(dx[k]), "+v"(dy[k]));
             if (sp && !yB) asm volatile("" : "+v"(db[k]));
             if (hasW && !yW) asm volatile("" : "+v"(dw[k]));
-            if (hpc) asm volatile("" : "+v"(dp[k]));
         }
         LK_T(ph4);
         if (first) {
             first = false;
             asm volatile("" : "+v"(xa), "+v"(ya_), "+v"(xb), "+v"(yb), "+v"(xw), "+v"(yw), "+v"(rsa), "+v"(rsb));
-            asm volatile("" : "+v"(qa), "+v"(qb), "+v"(qw), "+v"(qx), "+v"(qy));
             if (sp) {
                 const int32_t sa = size_x(A, rsa), sb_ = size_x(B, rsb);
                 sxs = A < B ? sa : sb_;
@@ -901,16 +724,6 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             // the sizes as of this step's decision: the previous decision's
             // (being written by workgroup 0) and this one's (not yet written)
             if (size_x(i, sz[k]) == 0) continue;                // (retires x)
-            if (hpc) {
-                if (i == pc) {                                  // entry pc of the rows read: from row pc
-                    da[k] = qa; db[k] = qb; dw[k] = qw; dx[k] = qx; dy[k] = qy;
-                } else if (!(pend && i == y)) {
-                    // the deferred column: D[i][pc] = D[pc][i] (write-through: the
-                    // lines leave during this launch; row y's own entry pc is written
-                    // with its new value by the row store below)
-                    __hip_atomic_store(&D[(uint64_t)i * n + pc], dp[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
             // this launch's merge: row y's new value at i, stored to row and column y
             double u = 0.0;
             if (pend && i != y) {
@@ -920,9 +733,8 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
 #else
                 Dy[i] = u;
 #endif
-#if DREPHIP_LK_DEFERCOL || DREPHIP_LK_COLSTORE == 0
-                // the column: scattered by the next launch (or, in a timing-only
-                // A/B build with DREPHIP_LK_COLSTORE=0, not at all: Z is wrong)
+#if DREPHIP_LK_COLSTORE == 0
+                // timing-only A/B build: no column-y stores (Z is wrong)
 #elif DREPHIP_LK_COLSTORE == 2
                 __builtin_nontemporal_store(u, &D[(uint64_t)i * n + y]);
 #elif DREPHIP_LK_COLSTORE == 3
@@ -961,12 +773,11 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             } else if (pend && i != y && better(u, i, yv, yi)) {   // P2: y's new row
                 yv = u; yi = i;
             }
-            if (y4 && i != y && better(u, i, zv, zi)) { zv = u; zi = i; }   // P4: y's new row (spec 4)
         }
     }
     LK_T(ph5);
-    MinIdx p1{bv, bi}, p2{yv, yi}, p3{wv, wi}, p4{zv, zi};
-    block_argmin4<WG>(p1, p2, p3, p4, pend || sp, hasW || y4, y4);
+    MinIdx p1{bv, bi}, p2{yv, yi}, p3{wv, wi};
+    block_argmin3<WG>(p1, p2, p3, pend || sp, hasW);
     LK_T(ph6);
 #if DREPHIP_LK_PHASES
     if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == G - 1)) {
@@ -979,7 +790,6 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
         if (search) parts[(uint64_t)q * 1024 + blockIdx.x] = p1;
         if (pend || sp) parts2[(uint64_t)q * 1024 + blockIdx.x] = p2;
         if (hasW) parts3[(uint64_t)q * 1024 + blockIdx.x] = p3;
-        if (y4) parts4[(uint64_t)q * 1024 + blockIdx.x] = p4;
     }
 }
 
@@ -1143,12 +953,12 @@ static void launch_dist_tiles_condensed(const DmFromCondensed &v, uint32_t n, do
 // (sort_and_label: linkage_sparse.cpp, shared with the sparse path)
 struct NnArgs {
     double *D; uint32_t n; int32_t *size, *chain; LinkState *st; LinkFwd *fwd;
-    MinIdx *parts, *parts2, *parts3, *parts4; int32_t *done; double *Z; uint32_t q; int spec_on;
+    MinIdx *parts, *parts2, *parts3; int32_t *done; double *Z; uint32_t q; int spec_on;
 };
 template <int W, int P>
 static void launch_nn(int method, dim3 grid, dim3 blk, hipStream_t st, const NnArgs &a) {
 #define DREPHIP_LK_NN(M) hipLaunchKernelGGL((k_nn_step<W, P, M>), grid, blk, 0, st, a.D, a.n, a.size, a.chain, a.st, \
-                                            a.fwd, a.parts, a.parts2, a.parts3, a.parts4, a.done, a.Z, a.q, a.spec_on)
+                                            a.fwd, a.parts, a.parts2, a.parts3, a.done, a.Z, a.q, a.spec_on)
     if (method == DREPHIP_LINK_COMPLETE) DREPHIP_LK_NN(DREPHIP_LINK_COMPLETE);
     else if (method == DREPHIP_LINK_WEIGHTED) DREPHIP_LK_NN(DREPHIP_LINK_WEIGHTED);
     else DREPHIP_LK_NN(DREPHIP_LINK_AVERAGE);
@@ -1198,17 +1008,13 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     if ((rc = scratch(ctx, "lk_chain", n * 4ull, (void **)&d_chain))) return rc;
     if ((rc = scratch(ctx, "lk_Z", (n - 1) * 32ull, (void **)&d_Z))) return rc;
     if ((rc = scratch(ctx, "lk_parts", 2 * 1024 * sizeof(MinIdx), (void **)&d_parts))) return rc;
-    MinIdx *d_parts2, *d_parts3, *d_parts4;
+    MinIdx *d_parts2, *d_parts3;
     if ((rc = scratch(ctx, "lk_parts2", 2 * 1024 * sizeof(MinIdx), (void **)&d_parts2))) return rc;
     if ((rc = scratch(ctx, "lk_parts3", 2 * 1024 * sizeof(MinIdx), (void **)&d_parts3))) return rc;
-    if ((rc = scratch(ctx, "lk_parts4", 2 * 1024 * sizeof(MinIdx), (void **)&d_parts4))) return rc;
-    // the speculation (A/B): 0 off; 1 the round-4 protocol; 2 (default) with
-    // the known-merge speculation (spec 3); 3 also in every other merge launch
-    // (spec 4: launches per merge at 10^5 1.2617 -> 1.2457, but each merge
-    // launch reduces a fourth partial set, and the chain took longer: 997 vs
-    // 991 ms, both with the deferred column; profiles/r05_linkage_ab_defer_spec4.txt)
+    // the speculation (A/B): 0 off; 1 the round-4 protocol (no known-merge
+    // launches); 2 (default) with the known-merge speculation (spec 3)
     const char *spe = getenv("DREPHIP_LINK_SPEC");
-    const int spec_on = spe ? std::max(0, std::min(3, atoi(spe))) : 2;
+    const int spec_on = spe ? std::max(0, std::min(2, atoi(spe))) : 2;
     if ((rc = scratch(ctx, "lk_st", 2 * sizeof(LinkState), (void **)&d_st))) return rc;
     LinkFwd *d_fwd;
     if ((rc = scratch(ctx, "lk_fwd", 2 * sizeof(LinkFwd), (void **)&d_fwd))) return rc;
@@ -1262,8 +1068,7 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     for (int b = 0; b < kBatch; b++) {
         const uint32_t q = (uint32_t)(b & 1);
         const dim3 gm(grid), gn(grid + 1), blk(wg);
-        const NnArgs a{d_D, n, d_size, d_chain, d_st, d_fwd, d_parts, d_parts2, d_parts3, d_parts4, d_done, d_Z, q,
-                       spec_on};
+        const NnArgs a{d_D, n, d_size, d_chain, d_st, d_fwd, d_parts, d_parts2, d_parts3, d_done, d_Z, q, spec_on};
 #define DREPHIP_LK_LAUNCH(W, P)                                                                                      \
     do {                                                                                                         \
         if (mst) hipLaunchKernelGGL((k_mst_step<W, P>), gm, blk, 0, st, d_D, n, d_size, d_Dmin, d_st, d_parts, d_done, \

@@ -176,21 +176,23 @@ def test_screen_single_shared_hash_pairs():
     assert planted > 500 and (oc == 1).sum() > 100 and ((oc == 0) & (od == s)).sum() > 1000
 
 
-@pytest.mark.parametrize("s,N", [(300, 400), (4096, 260)])
+@pytest.mark.parametrize("s,N", [(300, 400), (4096, 264)])
 def test_screen_light_cells(s, N, monkeypatch):
-    """Light cells (k_screen_light): values shared by groups of 3..150
-    genomes (runs of >= 3 entries, some longer than a wave, so row tiles
-    straddle x blocks), most pairs of a group sharing only that value, planted
-    at ranks on both sides of i + j = s; some pairs share two group values or
-    a group value and a two-genome value (heavy: the LIST kernel), some
-    sketches are partial (heavy), some values agree in their low word only.
-    The screen writes the light pairs itself: bit-exact against the oracle and
-    against the screen without the light path, which leaves more cells to the
-    kernel."""
+    """Light cells (k_screen_light), planted as configs[4] has them: families
+    of 8 genomes share 30 values each (heavy cells); a value shared by chance
+    between members of two families (a run of >= 3 entries) gives their
+    cross pairs exactly one shared hash (light cells), at ranks on both sides
+    of i + j = s; hub values in ~70 genomes across families (runs longer than
+    a wave: row tiles straddle x blocks); some family pairs linked by two chance
+    values, or by a chance value and a two-genome value (heavy); partial
+    sketches (heavy); values that agree in their low word only.  The screen
+    writes the light pairs itself: bit-exact against the oracle and against
+    the screen without the light path, which leaves more cells to the kernel."""
     rng = np.random.default_rng(s + N)
+    F = 8
     H = np.sort(rng.integers(1, 1 << 62, size=(N, s), dtype=np.uint64), axis=1)
     NH = np.full(N, s, dtype=np.uint32)
-    for g in range(0, N, 23):
+    for g in range(5, N, 29):
         NH[g] = rng.integers(s // 3, s)
         H[g, NH[g]:] = UMAX
 
@@ -201,11 +203,25 @@ def test_screen_light_cells(s, N, monkeypatch):
             j = int(rng.integers(0, NH[g]))
             row = np.sort(np.concatenate([np.delete(H[g, :NH[g]], j), [v]]))
             H[g, :NH[g]] = row
-    for k in range(160):
-        m = int(rng.choice([3, 4, 7, 12, 40, 70, 150]))
-        plant(rng.choice(N, m, replace=False), np.uint64(rng.integers(1, 1 << 62)))
-    for _ in range(80):                                  # two-genome values on top (simple or heavy)
-        plant(rng.choice(N, 2, replace=False), np.uint64(rng.integers(1, 1 << 62)))
+
+    def fam(f):
+        return np.arange(f * F, min(N, f * F + F))
+    nf = N // F
+    for f in range(nf):
+        for _ in range(30):
+            plant(fam(f), np.uint64(rng.integers(1, 1 << 62)))
+    pairs = rng.permutation([(a, b) for a in range(nf) for b in range(a + 1, nf)])
+    for a, b in pairs[:60]:                              # one chance value: light cross pairs
+        ma = rng.choice(fam(a), int(rng.integers(1, F + 1)), replace=False)
+        mb = rng.choice(fam(b), int(rng.integers(2, F + 1)), replace=False)
+        plant(np.concatenate([ma, mb]), np.uint64(rng.integers(1, 1 << 62)))
+    for a, b in pairs[60:70]:                            # two chance values: heavy
+        for _ in range(2):
+            plant(np.concatenate([fam(a)[:3], fam(b)[:3]]), np.uint64(rng.integers(1, 1 << 62)))
+    for a, b in pairs[:8]:                               # a two-genome value on top of a chance one
+        plant([fam(a)[0], fam(b)[-1]], np.uint64(rng.integers(1, 1 << 62)))
+    for _ in range(3):                                   # hubs: runs of ~70
+        plant(rng.choice(N, 70, replace=False), np.uint64(rng.integers(1, 1 << 62)))
     for _ in range(30):                                  # low-word twins: equal sort keys, no shared hash
         a, b = rng.choice(N, 2, replace=False)
         v = H[a, rng.integers(0, NH[a])]
@@ -218,8 +234,8 @@ def test_screen_light_cells(s, N, monkeypatch):
         c2, d2, st2 = run(ctx, H, NH, ctx.SCREEN_ON)
         assert np.array_equal(c2, oc) and np.array_equal(d2, od)
     # the light path wrote pairs itself and left fewer cells to the kernel
-    assert st["simple"] > st2["simple"] + 1000 and st["marked"] < st2["marked"], (st, st2)
-    assert (oc == 1).sum() > 1000 and ((oc == 0) & (od == s)).sum() > 1000
+    assert st["simple"] > st2["simple"] + 500 and st["marked"] < st2["marked"] - 200, (st, st2)
+    assert (oc == 1).sum() > 500 and ((oc == 0) & (od == s)).sum() > 1000
 
 
 def test_screen_mode_argument_checked():
