@@ -94,6 +94,27 @@ __device__ __forceinline__ double lw_update(int method, double dxi, double dyi, 
     return __ddiv_rn(__dadd_rn(__dmul_rn((double)nx, dxi), __dmul_rn((double)ny, dyi)), (double)(nx + ny));
 }
 
+// The same update with the average's division by the step-uniform n = nx + ny
+// done as Markstein's correction step: with r = RN(1/n) (one IEEE division per
+// launch) and q = RN(a r), within an ulp of a/n, e = a - q n is exact (one
+// FMA) and RN(q + e r) = RN(a/n) -- the correctly rounded quotient, i.e. the
+// same bits as the division, for every a and n without overflow or underflow
+// (here a in [0, 2 x 10^5], n an integer <= 10^5; tools/div_check.c checks 4 x
+// 10^8 cases of this exact expression on the host).  Three dependent f64
+// operations instead of the division's ~12 on the row pass's critical path.
+struct LwDiv { double n, r; };
+__device__ __forceinline__ LwDiv lw_div(int32_t nx, int32_t ny) {
+    const double n = (double)(nx + ny);
+    return LwDiv{n, __ddiv_rn(1.0, n)};
+}
+__device__ __forceinline__ double lw_update(int method, double dxi, double dyi, int32_t nx, int32_t ny, LwDiv dv) {
+    if (method != DREPHIP_LINK_AVERAGE) return lw_update(method, dxi, dyi, nx, ny);
+    const double a = __dadd_rn(__dmul_rn((double)nx, dxi), __dmul_rn((double)ny, dyi));
+    const double q = __dmul_rn(a, dv.r);
+    const double e = __fma_rn(-q, dv.n, a);
+    return __fma_rn(e, dv.r, q);
+}
+
 // Wave argmin by DPP (row_shr 1/2/4/8 within each 16-lane row, then
 // row_bcast 15/31 across rows: lane 63 ends with the wave's minimum, which
 // readlane broadcasts), in two passes: the minimum value (v_min_f64 of the
@@ -680,6 +701,8 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     double bv = INFINITY, yv = INFINITY, wv = INFINITY;
     int32_t bi = 0x7fffffff, yi = 0x7fffffff, wi = 0x7fffffff;
     int32_t sxs = 0, sys = 0;                                   // the speculated merge's sizes
+    const LwDiv dvxy = lw_div(nx, ny);                          // (average: this step's divisor)
+    LwDiv dvs{1.0, 1.0};
     const uint32_t stride = G * WG;
     bool first = true;
     for (uint32_t i0 = blockIdx.x * WG + threadIdx.x; i0 < n; i0 += kLkPer * stride) {
@@ -715,6 +738,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                 const int32_t sa = size_x(A, rsa), sb_ = size_x(B, rsb);
                 sxs = A < B ? sa : sb_;
                 sys = A < B ? sb_ : sa;
+                dvs = lw_div(sxs, sys);
             }
         }
 #pragma unroll
@@ -727,7 +751,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             // this launch's merge: row y's new value at i, stored to row and column y
             double u = 0.0;
             if (pend && i != y) {
-                u = lw_update(method, dx[k], dy[k], nx, ny);
+                u = lw_update(method, dx[k], dy[k], nx, ny, dvxy);
 #if DREPHIP_LK_ROWSTORE == 3
                 __hip_atomic_store(&Dy[i], u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #else
@@ -748,9 +772,9 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             // row R is U1[R]
             double ca, cb = 0.0, cw = 0.0;
             if (pend && i == y) {
-                ca = yA ? 0.0 : lw_update(method, xa, ya_, nx, ny);
-                if (sp) cb = yB ? 0.0 : lw_update(method, xb, yb, nx, ny);
-                if (hasW) cw = yW ? 0.0 : lw_update(method, xw, yw, nx, ny);
+                ca = yA ? 0.0 : lw_update(method, xa, ya_, nx, ny, dvxy);
+                if (sp) cb = yB ? 0.0 : lw_update(method, xb, yb, nx, ny, dvxy);
+                if (hasW) cw = yW ? 0.0 : lw_update(method, xw, yw, nx, ny, dvxy);
             } else {
                 ca = yA ? u : da[k];
                 if (sp) cb = yB ? u : db[k];
@@ -760,7 +784,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             if (sp) {
                 if (i != A && i != B) {
                     // P2: the speculated merged row; P3: W's row after that merge
-                    const double U = lw_update(method, A < B ? ca : cb, A < B ? cb : ca, sxs, sys);
+                    const double U = lw_update(method, A < B ? ca : cb, A < B ? cb : ca, sxs, sys, dvs);
                     if (better(U, i, yv, yi)) { yv = U; yi = i; }
                     if (hasW) {
                         if (i == W) {
