@@ -49,7 +49,7 @@ SKETCH_ABLATION = os.path.join(ROOT, "profiles", "r05_sketch_ablation.json")
 SKETCH_PMC = os.path.join(ROOT, "profiles", "r04_sketch_pmc_sq.json")
 # all-pairs profiles of tools/profile_allpairs.sh, one per (N, s) case: the
 # bench line quotes the one of its own workload (never another N's)
-DIST_PROFILE = os.path.join(ROOT, "profiles", "r04_allpairs_N%d%s.json")
+DIST_PROFILES = [os.path.join(ROOT, "profiles", r + "_allpairs_N%d%s.json") for r in ("r05", "r04")]   # newest first
 SKETCH_TRAFFIC = os.path.join(ROOT, "profiles", "r04_sketch_traffic.json")
 PROFILE_STEPS = 3              # untimed steps that time finalize / all-pairs / table build
 VERIFY_GENOMES = 16            # timed-step sketches re-derived by the C oracle (sampled, every run)
@@ -62,9 +62,10 @@ def dist_roofline(N, s, pairs_per_launch, launch_ms):
     2-cycle wave64 peak (the PMC's VALU instructions per pair x this launch's
     pairs / this launch's live HIP-event time), LDS busy, HBM traffic and L2
     hit rate of the profiled dispatches."""
-    path = DIST_PROFILE % (N, "" if s == 1000 else "_s%d" % s)
-    if not os.path.exists(path):
-        return {"note": "no all-pairs profile committed for N=%d s=%d (%s)" % (N, s, os.path.relpath(path, ROOT))}
+    cands = [p % (N, "" if s == 1000 else "_s%d" % s) for p in DIST_PROFILES]
+    path = next((p for p in cands if os.path.exists(p)), None)
+    if path is None:
+        return {"note": "no all-pairs profile committed for N=%d s=%d (%s)" % (N, s, os.path.relpath(cands[0], ROOT))}
     d = json.load(open(path))
     dv = d.get("derived", {})
     out = {"kernel": (d.get("kernel") or "")[:60], "source": os.path.relpath(path, ROOT),
@@ -82,6 +83,26 @@ def dist_roofline(N, s, pairs_per_launch, launch_ms):
             out[k] = dv[k]
     out["traffic"] = dv.get("hbm_bytes_x2")
     return out
+
+
+def list_profile(N, s, launch_ms):
+    """The screened LIST kernel's committed profile of this exact workload, if
+    one was taken on the LIST kernel (kernel name ends in LIST = true): HBM
+    traffic against the algorithmic bytes, L2 hit rate, and the profiled vs
+    this run's kernel time."""
+    for p in DIST_PROFILES:
+        path = p % (N, "" if s == 1000 else "_s%d" % s)
+        if not os.path.exists(path):
+            continue
+        d = json.load(open(path))
+        if "true>" not in (d.get("kernel") or "") and "true," not in (d.get("kernel") or ""):
+            continue
+        dv = d.get("derived", {})
+        return {"source": os.path.relpath(path, ROOT), "kernel": (d.get("kernel") or "")[:60],
+                "profiled_avg_call_ms": d.get("avg_call_ms"), "this_run_ms": launch_ms,
+                **{k: dv[k] for k in ("hbm_bytes_x2", "algorithmic_bytes", "hbm_over_algorithmic_x2", "l2_hit_rate",
+                                      "hbm_GBps_x2", "lds_busy_frac", "valu_issue_frac_2cyc") if k in dv}}
+    return None
 
 
 def pmc_block(path):
@@ -721,7 +742,8 @@ def main():
                                       "per-pair profile does not apply",
                               "screen_ms_avg": kms[4][0] / max(kms[4][1], 1),
                               "sort_bytes_per_launch_est": 4 * 16 * screen.get("entries", 0),
-                              "marked_cells": screen.get("marked"), "pair_checks": screen.get("checks")}),
+                              "marked_cells": screen.get("marked"), "pair_checks": screen.get("checks"),
+                              "list_kernel_profile": list_profile(N, args.sketch, kms[2][0] / max(kms[2][1], 1))}),
             },
             "cpu_baseline": cpu,
         }

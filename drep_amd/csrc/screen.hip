@@ -519,7 +519,7 @@ __global__ __launch_bounds__(kScWG) void k_screen_lists(const uint32_t *__restri
                                                         uint32_t row0, uint32_t R, const uint32_t *__restrict__ cnt,
                                                         const uint64_t *__restrict__ coff,
                                                         const uint32_t *__restrict__ ibase, uint32_t *__restrict__ clist,
-                                                        uint4 *__restrict__ items) {
+                                                        uint4 *__restrict__ items, int desc) {
     __shared__ uint32_t wsum[kScWG / 64];
     const uint32_t t = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const uint32_t *row = bm + (uint64_t)t * NW;
@@ -538,15 +538,18 @@ __global__ __launch_bounds__(kScWG) void k_screen_lists(const uint32_t *__restri
     uint32_t pos = inc - mine;
     for (uint32_t k = 0; k < (tid >> 6); k++) pos += wsum[k];
     uint32_t *out = clist + coff[t];
+    const uint32_t n = cnt[t];
     for (uint32_t w = w0; w < w1; w++) {
         uint32_t bits = row[w];
         while (bits) {
             const uint32_t b = __ffs(bits) - 1;
             bits &= bits - 1;
-            out[pos++] = w * 32 + b;
+            // (desc, A/B: descending, so that the row tiles of a family, whose lists
+            // end at different columns but share the family's last ones, start together)
+            out[desc ? n - 1 - pos : pos] = w * 32 + b;
+            pos++;
         }
     }
-    const uint32_t n = cnt[t];
     const uint32_t ni = (n + C - 1) / C;
     for (uint32_t j = tid; j < ni; j += kScWG)
         items[(uint64_t)ibase[t] + 8ull * j] = make_uint4(row0 + t * R, (uint32_t)(coff[t] + (uint64_t)j * C),
@@ -835,8 +838,9 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
     HIPC(hipMemcpyAsync(d_ibase, ibase, ntiles * 4ull, hipMemcpyHostToDevice, st));
     HIPC(hipMemsetAsync(d_items, 0xFF, std::max<uint64_t>(nitems, 1) * 16, st));       // idle items: i0 = ~0
     prof.mark("readback+alloc", st);
+    const char *de = getenv("DREPHIP_SCREEN_DESC");
     hipLaunchKernelGGL(k_screen_lists, dim3(ntiles), dim3(kScWG), 0, st, d_bl, NW, C, row0, R, d_cnt, d_coff, d_ibase,
-                       d_list, d_items);
+                       d_list, d_items, de ? atoi(de) : 0);
     prof.mark("lists", st);
     timing_mark(ctx, 4, st, false);
     HIPC(hipGetLastError());
