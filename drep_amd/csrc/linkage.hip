@@ -57,6 +57,16 @@ constexpr int kLkWG = 256;
 #define DREPHIP_LK_ROWSTORE 1
 #endif
 constexpr uint32_t kLkSmallN = 30000;
+// Per-wave partials (round 5, A/B): each wave of a step workgroup stores its
+// own argmin partials (no LDS exchange, no barrier at the end of the step); the
+// next decision reduces WG / 64 times as many.  Measured slower at 10^5 (chain
+// 898-908 vs 854-856 ms with one partial per workgroup, profiles/r05_linkage_ab_waveparts.txt):
+// the decision's pass over 4x the partials (16 per lane, 234 VGPRs) costs more
+// than the block reduction it saves.  0 (default): one partial per workgroup
+#ifndef DREPHIP_LK_WAVEPARTS
+#define DREPHIP_LK_WAVEPARTS 0
+#endif
+constexpr uint32_t kLkPartStride = 4096;        // partials per parity: up to 1024 workgroups x 4 waves
 
 static double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -441,10 +451,13 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     const uint4 *fv = (const uint4 *)(fwd + (q ^ 1)) + lz0;
     uint4 sw0 = sv[0], sw1 = sv[1], sw2 = sv[2], sw3 = sv[3], fw0 = fv[0], fw1 = fv[1], fw2 = fv[2];
     if (wave0) {
-        const MinIdx *P1 = parts + (uint64_t)(q ^ 1) * 1024, *P2 = parts2 + (uint64_t)(q ^ 1) * 1024,
-                     *P3 = parts3 + (uint64_t)(q ^ 1) * 1024;
-        if (G <= 256) partial_pass<4>(P1, P2, P3, G, g, g2, g3);
-        else partial_pass<8>(P1, P2, P3, G, g, g2, g3);              // (up to 512 workgroups in one pass)
+        const MinIdx *P1 = parts + (uint64_t)(q ^ 1) * kLkPartStride, *P2 = parts2 + (uint64_t)(q ^ 1) * kLkPartStride,
+                     *P3 = parts3 + (uint64_t)(q ^ 1) * kLkPartStride;
+        // partials: one per step wave (DREPHIP_LK_WAVEPARTS) or per step workgroup
+        const uint32_t NP = DREPHIP_LK_WAVEPARTS ? G * (WG / 64) : G;
+        if (NP <= 256) partial_pass<4>(P1, P2, P3, NP, g, g2, g3);
+        else if (NP <= 512) partial_pass<8>(P1, P2, P3, NP, g, g2, g3);
+        else partial_pass<16>(P1, P2, P3, NP, g, g2, g3);           // (up to 1024 in one pass)
     }
     asm volatile("" : "+v"(sw0.x), "+v"(sw0.y), "+v"(sw0.z), "+v"(sw0.w), "+v"(sw1.x), "+v"(sw1.y), "+v"(sw1.z),
                  "+v"(sw1.w), "+v"(sw2.x), "+v"(sw2.y), "+v"(sw2.z), "+v"(sw2.w), "+v"(sw3.x), "+v"(sw3.y),
@@ -801,7 +814,15 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     }
     LK_T(ph5);
     MinIdx p1{bv, bi}, p2{yv, yi}, p3{wv, wi};
+#if DREPHIP_LK_WAVEPARTS
+    wave_argmin_upto3(p1, p2, p3, pend || sp, hasW);
+    const uint32_t pslot = blockIdx.x * (WG / 64) + (threadIdx.x >> 6);
+    const bool pwrite = (threadIdx.x & 63) == 0;
+#else
     block_argmin3<WG>(p1, p2, p3, pend || sp, hasW);
+    const uint32_t pslot = blockIdx.x;
+    const bool pwrite = threadIdx.x == 0;
+#endif
     LK_T(ph6);
 #if DREPHIP_LK_PHASES
     if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == G - 1)) {
@@ -810,10 +831,10 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
         else { ph[8] = ph0; ph[9] = ph3; ph[10] = ph6; }
     }
 #endif
-    if (threadIdx.x == 0) {
-        if (search) parts[(uint64_t)q * 1024 + blockIdx.x] = p1;
-        if (pend || sp) parts2[(uint64_t)q * 1024 + blockIdx.x] = p2;
-        if (hasW) parts3[(uint64_t)q * 1024 + blockIdx.x] = p3;
+    if (pwrite) {
+        if (search) parts[(uint64_t)q * kLkPartStride + pslot] = p1;
+        if (pend || sp) parts2[(uint64_t)q * kLkPartStride + pslot] = p2;
+        if (hasW) parts3[(uint64_t)q * kLkPartStride + pslot] = p3;
     }
 }
 
@@ -826,7 +847,7 @@ __global__ __launch_bounds__(WG) void k_mst_step(const double *__restrict__ D, u
     // kept in private memory promoted to LDS, see k_nn_step)
     __shared__ int32_t s_k, s_mx, s_ov;
     const uint32_t G = gridDim.x;
-    const MinIdx g = read_partials<WG>(parts + (uint64_t)(q ^ 1) * 1024, G);     // unconditional: not held behind S
+    const MinIdx g = read_partials<WG>(parts + (uint64_t)(q ^ 1) * kLkPartStride, G);     // unconditional: not held behind S
     const int32_t sk = st[q ^ 1].k, smx = st[q ^ 1].mx, sflags = st[q ^ 1].flags;
     if (sk >= (int32_t)n - 1) return;
     if (threadIdx.x == 0) {
@@ -880,7 +901,7 @@ __global__ __launch_bounds__(WG) void k_mst_step(const double *__restrict__ D, u
         }
     }
     const MinIdx part = block_argmin<WG>(bv, bi);
-    if (threadIdx.x == 0) parts[(uint64_t)q * 1024 + blockIdx.x] = part;
+    if (threadIdx.x == 0) parts[(uint64_t)q * kLkPartStride + blockIdx.x] = part;
 }
 
 // ------------------------------------------------------------ matrix build
@@ -1031,10 +1052,10 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     if ((rc = scratch(ctx, "lk_size", n * 4ull, (void **)&d_size))) return rc;
     if ((rc = scratch(ctx, "lk_chain", n * 4ull, (void **)&d_chain))) return rc;
     if ((rc = scratch(ctx, "lk_Z", (n - 1) * 32ull, (void **)&d_Z))) return rc;
-    if ((rc = scratch(ctx, "lk_parts", 2 * 1024 * sizeof(MinIdx), (void **)&d_parts))) return rc;
+    if ((rc = scratch(ctx, "lk_parts", 2 * kLkPartStride * sizeof(MinIdx), (void **)&d_parts))) return rc;
     MinIdx *d_parts2, *d_parts3;
-    if ((rc = scratch(ctx, "lk_parts2", 2 * 1024 * sizeof(MinIdx), (void **)&d_parts2))) return rc;
-    if ((rc = scratch(ctx, "lk_parts3", 2 * 1024 * sizeof(MinIdx), (void **)&d_parts3))) return rc;
+    if ((rc = scratch(ctx, "lk_parts2", 2 * kLkPartStride * sizeof(MinIdx), (void **)&d_parts2))) return rc;
+    if ((rc = scratch(ctx, "lk_parts3", 2 * kLkPartStride * sizeof(MinIdx), (void **)&d_parts3))) return rc;
     // the speculation (A/B): 0 off; 1 the round-4 protocol (no known-merge
     // launches); 2 (default) with the known-merge speculation (spec 3)
     const char *spe = getenv("DREPHIP_LINK_SPEC");

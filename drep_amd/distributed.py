@@ -197,6 +197,8 @@ def run_sharded(N: int, names: Sequence[str], s: int, sketch_fn: SketchFn, allpa
         left = int((full_c == POISON).sum().item())
         if left:
             raise RuntimeError("%d pairs of the condensed vector were never written" % left)
+    if full_c is not None and os.environ.get("DREPHIP_DUMP_COUNTS"):       # (debugging: the gathered counts)
+        np.save(os.environ["DREPHIP_DUMP_COUNTS"], full_c.cpu().numpy())
     full_d = None
     if partial:
         if seg_d is None:
