@@ -456,7 +456,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
         // partials: one per step wave (DREPHIP_LK_WAVEPARTS) or per step workgroup
         const uint32_t NP = DREPHIP_LK_WAVEPARTS ? G * (WG / 64) : G;
         if (NP <= 256) partial_pass<4>(P1, P2, P3, NP, g, g2, g3);
-        else if (NP <= 512) partial_pass<8>(P1, P2, P3, NP, g, g2, g3);
+        else if (!DREPHIP_LK_WAVEPARTS || NP <= 512) partial_pass<8>(P1, P2, P3, NP, g, g2, g3);   // (512 a pass)
         else partial_pass<16>(P1, P2, P3, NP, g, g2, g3);           // (up to 1024 in one pass)
     }
     asm volatile("" : "+v"(sw0.x), "+v"(sw0.y), "+v"(sw0.z), "+v"(sw0.w), "+v"(sw1.x), "+v"(sw1.y), "+v"(sw1.z),
