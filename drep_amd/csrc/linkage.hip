@@ -703,9 +703,13 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     int32_t lz;
     asm volatile("v_mov_b32 %0, 0" : "=v"(lz));
     const bool fa = pend && !yA, fb = pend && sp && !yB, fw = pend && hasW && !yW;
-    double xa = fa ? Dx[A + lz] : 0.0, ya_ = fa ? Dy[A + lz] : 0.0;
-    double xb = fb ? Dx[B + lz] : 0.0, yb = fb ? Dy[B + lz] : 0.0;
-    double xw = fw ? Dx[W + lz] : 0.0, yw = fw ? Dy[W + lz] : 0.0;
+    // (entry (y, R) from its column copy D[R][y], which only the lane of i = y
+    // writes in this launch, after this load: the row copy D[y][R] is the lane
+    // of i = R's to rewrite -- reading it here raced with that store)
+    auto colY = [&](int32_t r) { return D[(uint64_t)r * n + y + lz]; };
+    double xa = fa ? Dx[A + lz] : 0.0, ya_ = fa ? colY(A) : 0.0;
+    double xb = fb ? Dx[B + lz] : 0.0, yb = fb ? colY(B) : 0.0;
+    double xw = fw ? Dx[W + lz] : 0.0, yw = fw ? colY(W) : 0.0;
     // the sizes of A and B as of this step's decision (for the speculated merge)
     int32_t rsa = sp ? size[A + lz] : 0, rsb = sp ? size[B + lz] : 0;
     auto size_x = [&](int32_t i, int32_t stored) {
@@ -762,24 +766,34 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             // (being written by workgroup 0) and this one's (not yet written)
             if (size_x(i, sz[k]) == 0) continue;                // (retires x)
             // this launch's merge: row y's new value at i, stored to row and column y
-            double u = 0.0;
-            if (pend && i != y) {
-                u = lw_update(method, dx[k], dy[k], nx, ny, dvxy);
+            // (one entry's two copies, D[y][i] and D[i][y])
+            auto store_row = [&](int32_t c, double v) {
 #if DREPHIP_LK_ROWSTORE == 3
-                __hip_atomic_store(&Dy[i], u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&Dy[c], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #else
-                Dy[i] = u;
+                Dy[c] = v;
 #endif
+            };
+            auto store_col = [&](int32_t c, double v) {
 #if DREPHIP_LK_COLSTORE == 0
                 // timing-only A/B build: no column-y stores (Z is wrong)
 #elif DREPHIP_LK_COLSTORE == 2
-                __builtin_nontemporal_store(u, &D[(uint64_t)i * n + y]);
+                __builtin_nontemporal_store(v, &D[(uint64_t)c * n + y]);
 #elif DREPHIP_LK_COLSTORE == 3
                 // write-through (sc1): the line leaves L2 now instead of at the kernel boundary
-                __hip_atomic_store(&D[(uint64_t)i * n + y], u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&D[(uint64_t)c * n + y], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #else
-                D[(uint64_t)i * n + y] = u;
+                D[(uint64_t)c * n + y] = v;
 #endif
+            };
+            double u = 0.0;
+            if (pend && i != y) {
+                u = lw_update(method, dx[k], dy[k], nx, ny, dvxy);
+                store_row(i, u);
+                // the column copy D[R][y] of the rows R = A, B, W whose entry y the
+                // lane of i = y recomputes (U1[R], from D[x][R] and D[R][y]) is that
+                // lane's to store, after its load of it
+                if (!((fa && i == A) || (fb && i == B) || (fw && i == W))) store_col(i, u);
             }
             // the rows as they are after that merge: row y is u; entry y of a
             // row R is U1[R]
@@ -788,6 +802,10 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                 ca = yA ? 0.0 : lw_update(method, xa, ya_, nx, ny, dvxy);
                 if (sp) cb = yB ? 0.0 : lw_update(method, xb, yb, nx, ny, dvxy);
                 if (hasW) cw = yW ? 0.0 : lw_update(method, xw, yw, nx, ny, dvxy);
+                // (the same bits as those lanes' u: the same operands and update)
+                if (fa) store_col(A, ca);
+                if (fb) store_col(B, cb);
+                if (fw) store_col(W, cw);
             } else {
                 ca = yA ? u : da[k];
                 if (sp) cb = yB ? u : db[k];
