@@ -319,14 +319,8 @@ struct alignas(64) LinkState {
     int32_t flags;                // 1: the reader first decides the previous step from its partials; 2: bad
     int32_t mx;                   // MST: current vertex
     int32_t launches;             // working launches (reported: launches per merge)
-    // a known merge applied by the same launch as its discovery (DREPHIP_LK_FUSE):
-    // fused = 1: this state's launch also merges a2 (the top before it) with b2
-    // (the element below), the state above being the one after that merge; n2,
-    // the merged size, is written by that launch's row pass (workgroup 0)
-    int32_t fused, a2, b2, n2;
-    int32_t pad[12];
 };
-static_assert(sizeof(LinkState) == 128, "the step state is two 64-byte lines");
+static_assert(sizeof(LinkState) == 64, "the step state is one 64-byte line");
 constexpr int32_t kLkDecide = 1, kLkBad = 2;
 #ifndef DREPHIP_LK_DIAG
 #define DREPHIP_LK_DIAG 0
@@ -334,7 +328,7 @@ constexpr int32_t kLkDecide = 1, kLkBad = 2;
 #if DREPHIP_LK_DIAG
 // diagnostic build: counters kept by lane 0 of workgroup 0 (a dependent
 // load + store per launch; never in the product build)
-struct LinkDiag { int32_t twice, scans, specwin, known, m0, wmerge, recip, fusedm; };
+struct LinkDiag { int32_t twice, scans, specwin, known, m0, wmerge, recip; };
 __device__ LinkDiag *g_lk_diag;
 #define LK_DIAG(field) do { if (w0l) g_lk_diag->field++; } while (0)   // (a divergent store: diagnostic builds only)
 #else
@@ -368,13 +362,12 @@ __device__ __forceinline__ MinIdx uni(MinIdx m) {       // a wave-uniform (value
     const uint32_t lo = (uint32_t)rfl((uint32_t)b), hi = (uint32_t)rfl((uint32_t)(b >> 32));
     return MinIdx{__longlong_as_double((long long)(((uint64_t)hi << 32) | lo)), rfl((uint32_t)m.i)};
 }
-__device__ __forceinline__ LinkState state_from_words(uint4 a, uint4 b, uint4 c, uint4 d, uint4 e) {
+__device__ __forceinline__ LinkState state_from_words(uint4 a, uint4 b, uint4 c, uint4 d) {
     LinkState S;
     S.k = rfl(a.x); S.len = rfl(a.y); S.top = rfl(a.z); S.below = rfl(a.w);
     S.first_active = rfl(b.x); S.pend = rfl(b.y); S.x = rfl(b.z); S.y = rfl(b.w);
     S.nx = rfl(c.x); S.ny = rfl(c.y); S.c3 = rfl(c.z); S.spec = rfl(c.w);
     S.known = rfl(d.x); S.flags = rfl(d.y); S.mx = rfl(d.z); S.launches = rfl(d.w);
-    S.fused = rfl(e.x); S.a2 = rfl(e.y); S.b2 = rfl(e.z); S.n2 = rfl(e.w);
     return S;
 }
 __device__ __forceinline__ LinkFwd fwd_from_words(uint4 a, uint4 b, uint4 c) {
@@ -431,7 +424,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                                                    LinkState *__restrict__ st, LinkFwd *__restrict__ fwd,
                                                    MinIdx *__restrict__ parts, MinIdx *__restrict__ parts2,
                                                    MinIdx *__restrict__ parts3, int32_t *__restrict__ done,
-                                                   double *__restrict__ Z, uint32_t q, int spec_on, int fuse_on) {
+                                                   double *__restrict__ Z, uint32_t q, int spec_on) {
     __shared__ LinkState sx;
     const uint32_t G = gridDim.x - 1;                          // step workgroups; workgroup G forwards operands
     // The partial sets are reduced by wave 0 alone (the decision is wave 0's:
@@ -456,7 +449,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     asm volatile("v_mov_b32 %0, 0" : "=v"(lz0));
     const uint4 *sv = (const uint4 *)(st + (q ^ 1)) + lz0;
     const uint4 *fv = (const uint4 *)(fwd + (q ^ 1)) + lz0;
-    uint4 sw0 = sv[0], sw1 = sv[1], sw2 = sv[2], sw3 = sv[3], sw4 = sv[4], fw0 = fv[0], fw1 = fv[1], fw2 = fv[2];
+    uint4 sw0 = sv[0], sw1 = sv[1], sw2 = sv[2], sw3 = sv[3], fw0 = fv[0], fw1 = fv[1], fw2 = fv[2];
     if (wave0) {
         const MinIdx *P1 = parts + (uint64_t)(q ^ 1) * kLkPartStride, *P2 = parts2 + (uint64_t)(q ^ 1) * kLkPartStride,
                      *P3 = parts3 + (uint64_t)(q ^ 1) * kLkPartStride;
@@ -468,10 +461,10 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     }
     asm volatile("" : "+v"(sw0.x), "+v"(sw0.y), "+v"(sw0.z), "+v"(sw0.w), "+v"(sw1.x), "+v"(sw1.y), "+v"(sw1.z),
                  "+v"(sw1.w), "+v"(sw2.x), "+v"(sw2.y), "+v"(sw2.z), "+v"(sw2.w), "+v"(sw3.x), "+v"(sw3.y),
-                 "+v"(sw3.z), "+v"(sw3.w), "+v"(sw4.x), "+v"(sw4.y), "+v"(sw4.z), "+v"(sw4.w));
+                 "+v"(sw3.z), "+v"(sw3.w));
     asm volatile("" : "+v"(fw0.x), "+v"(fw0.y), "+v"(fw0.z), "+v"(fw0.w), "+v"(fw1.x), "+v"(fw1.y), "+v"(fw1.z),
                  "+v"(fw1.w), "+v"(fw2.x), "+v"(fw2.y), "+v"(fw2.z));
-    const LinkState S = state_from_words(sw0, sw1, sw2, sw3, sw4);
+    const LinkState S = state_from_words(sw0, sw1, sw2, sw3);
     const LinkFwd F = fwd_from_words(fw0, fw1, fw2);
 #if DREPHIP_LK_PHASES
     uint64_t ph0 = 0, ph1 = 0, ph2 = 0, ph3 = 0, ph4 = 0, ph5 = 0, ph6 = 0;
@@ -483,18 +476,9 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     const bool w0 = blockIdx.x == 0;
     // size of cluster i as of the previous decision: workgroup 0 writes that
     // decision's two sizes during this kernel, so every reader overrides them
-    // (and, when that launch also applied a known merge (fused), that merge's:
-    // it is the later one, so its sizes win -- a recip merge retires or
-    // regrows the row the first merge formed)
     const int32_t spsa = S.pend ? S.x : -1, spsb = S.pend ? S.y : -1, spsbsz = S.nx + S.ny;
-    const int32_t sfa = S.fused ? min(S.a2, S.b2) : -1, sfb = S.fused ? max(S.a2, S.b2) : -1, sfbsz = S.n2;
-    auto size_prev = [=](int32_t i, int32_t stored) {
-        return i == sfa ? 0 : i == sfb ? sfbsz : i == spsa ? 0 : i == spsb ? spsbsz : stored;
-    };
-    if (w0 && threadIdx.x == 0) {
-        if (S.pend) { size[S.x] = 0; size[S.y] = spsbsz; }
-        if (S.fused) { size[sfa] = 0; size[sfb] = sfbsz; }
-    }
+    auto size_prev = [=](int32_t i, int32_t stored) { return i == spsa ? 0 : i == spsb ? spsbsz : stored; };
+    if (w0 && threadIdx.x == 0 && S.pend) { size[S.x] = 0; size[S.y] = spsbsz; }
     // ---- the previous step's decision, and y's when it pushes y (replicated
     // in every workgroup; its stores by lane 0 of workgroup 0)
     const bool w0l = w0 && lane0;
@@ -519,60 +503,12 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
         // store inside the decision made the compiler keep the whole decision
         // in VGPRs under exec masks instead of scalar code
         int32_t zmerge = 0, za = 0, zb = 0, zn = 0, npush = 0, pp0 = 0, pv0 = 0, pp1 = 0, pv1 = 0, restart = -1;
-        double zd = 0.0, kdist = 0.0, z2d = 0.0;
-        int32_t z2k = 0, z2a = 0, z2b = 0;
+        double zd = 0.0;
         auto push_rec = [&](int32_t pos, int32_t v) {
             if (npush == 0) { pp0 = pos; pv0 = v; } else { pp1 = pos; pv1 = v; }
             npush++;
         };
-        // Right after a merge of b (the merged row) whose launch speculated on
-        // it: the new top w's row as it is after the merge (P3) and b's (P2)
-        // decide w's step, and b's when w pushes b, now.  A push makes this
-        // launch search the pushed row instead of w.  A merge is known:
-        // known = 1, w merges with the element below it (at dp2 = D[w][below
-        // w]); known = 2, w pushes b and b merges back (at r3.v).  (b is pushed only
-        // together with b's own push, or as a known merge back with w:
-        // D[top][below] must not involve b, whose row this launch rewrites,
-        // except through dpo)
-        auto post_eval = [&](int32_t b, double dp2) {
-            const MinIdx r3 = g3;
-            const bool r3ok = (uint32_t)r3.i < n;
-            const bool wmerge = r3ok && len > 1 && !(r3.v < dp2);
-            const bool wpush = r3ok && !wmerge && len + 1 < (int32_t)n;
-            const bool bpush = r3.i == b && (uint32_t)g2.i < n && g2.v < r3.v;
-            if (wpush && (r3.i != b || bpush)) {
-                push_rec(len, r3.i);                        // w pushes r3.i
-                c6 = c5; c5 = c4; c4 = c3; c3 = below; below = top; top = r3.i;
-                ck = ck >= 4 ? 4 : ck + 1;
-                len++;
-                LK_DIAG(specwin);
-                if (bpush) {
-                    push_rec(len, g2.i);                    // b pushes g2.i
-                    c6 = c5; c5 = c4; c4 = c3; c3 = below; below = top; top = g2.i;
-                    ck = ck >= 4 ? 4 : ck + 1;
-                    len++;
-                    dpo = 1; dpov = g2.v;                   // D[g2.i][b] as this launch writes it
-                }
-            } else if (wmerge && spec_on > 1) {
-                known = 1;                                  // w merges with the element below it
-                LK_DIAG(wmerge);
-            } else if (wpush && r3.i == b && spec_on > 1) {
-                push_rec(len, b);                           // w pushes b, b merges back with w
-                c6 = c5; c5 = c4; c4 = c3; c3 = below; below = top; top = b;
-                ck = ck >= 4 ? 4 : ck + 1;
-                len++;
-                dpo = 1; dpov = r3.v;                       // D[b][w] as this launch writes it
-                known = 2;
-                LK_DIAG(recip);
-            }
-        };
-        if ((S.flags & kLkDecide) && S.fused) {
-            // the previous launch applied a known merge (a2, b2) and speculated
-            // on the state after it: decide the new top's step from P3 / P2
-            // as right after that merge (its D[top][below] is F.dp)
-            if (F.spec && len >= 1 && k < (int32_t)n - 1) post_eval(sfb, F.dp);
-            kdist = known == 1 ? F.dp : g3.v;
-        } else if (S.flags & kLkDecide) {
+        if (S.flags & kLkDecide) {
             int32_t szt = F.szt, szb = F.szb;
             double dp = F.dp;
             MinIdx r = g;
@@ -605,9 +541,45 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                     } else if (d == 0 && F.spec && len >= 1 && k < (int32_t)n - 1) {
                         // the previous launch searched, speculatively, the new
                         // top w's row as it is after this merge (P3) and the
-                        // merged row b (P2): post_eval
-                        post_eval(b, F.dp2);
-                        kdist = known == 1 ? F.dp2 : g3.v;
+                        // merged row b (P2): decide w's step, and b's when w
+                        // pushes b, now.  A push makes this launch search the
+                        // pushed row instead of w.  A merge is left to the next
+                        // launch (one merge per launch), which then knows it:
+                        // this launch speculates on it (spec 3) instead of
+                        // searching.  (b is pushed only together with b's own
+                        // push, or as a known merge back with w: D[top][below]
+                        // must not involve b, whose row this launch rewrites,
+                        // except through dpo)
+                        const MinIdx r3 = g3;
+                        const bool r3ok = (uint32_t)r3.i < n;
+                        const bool wmerge = r3ok && len > 1 && !(r3.v < F.dp2);
+                        const bool wpush = r3ok && !wmerge && len + 1 < (int32_t)n;
+                        const bool bpush = r3.i == b && (uint32_t)g2.i < n && g2.v < r3.v;
+                        if (wpush && (r3.i != b || bpush)) {
+                            push_rec(len, r3.i);                        // w pushes r3.i
+                            c6 = c5; c5 = c4; c4 = c3; c3 = below; below = top; top = r3.i;
+                            ck = ck >= 4 ? 4 : ck + 1;
+                            len++;
+                            LK_DIAG(specwin);
+                            if (bpush) {
+                                push_rec(len, g2.i);                    // b pushes g2.i
+                                c6 = c5; c5 = c4; c4 = c3; c3 = below; below = top; top = g2.i;
+                                ck = ck >= 4 ? 4 : ck + 1;
+                                len++;
+                                dpo = 1; dpov = g2.v;                   // D[g2.i][b] as this launch writes it
+                            }
+                        } else if (wmerge && spec_on > 1) {
+                            known = 1;                                  // w merges with the element below it
+                            LK_DIAG(wmerge);
+                        } else if (wpush && r3.i == b && spec_on > 1) {
+                            push_rec(len, b);                           // w pushes b, b merges back with w
+                            c6 = c5; c5 = c4; c4 = c3; c3 = below; below = top; top = b;
+                            ck = ck >= 4 ? 4 : ck + 1;
+                            len++;
+                            dpo = 1; dpov = r3.v;                       // D[b][w] as this launch writes it
+                            known = 1;
+                            LK_DIAG(recip);
+                        }
                     }
                     break;
                 }
@@ -625,28 +597,8 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                 LK_DIAG(twice);
             }
         }
-        // A known merge is applied by this launch too (fused) when the chain
-        // keeps an element after it (its row is the speculation's W) and it is
-        // not the last merge: its bookkeeping now, its row (the speculated
-        // merged row U) stored by this launch's row pass, which also writes
-        // its size (Z and the state's n2).  Otherwise the next launch applies it.
-        int32_t fused = 0, fa2 = 0, fb2 = 0;
-        if (known && fuse_on && len - 2 >= 1 && k + 1 < (int32_t)n - 1) {
-            fused = 1; fa2 = top; fb2 = below;
-            z2k = k; z2a = min(top, below); z2b = max(top, below); z2d = kdist;
-            k += 1;
-            len -= 2;
-            top = c3;
-            below = len >= 2 ? c4 : -1;
-            c3 = c5; c4 = c6;
-            ck = ck >= 2 ? ck - 2 : 0;
-            known = 0;
-            dpo = 0;
-            LK_DIAG(fusedm);
-        }
         LinkState X;
         X.mx = S.mx;
-        X.fused = fused; X.a2 = fa2; X.b2 = fb2; X.n2 = 0;
         X.k = k; X.len = len; X.top = top; X.below = below; X.first_active = first_active;
         X.pend = pend; X.x = px; X.y = py; X.nx = pnx; X.ny = pny;
         X.flags = kLkDecide | bad;
@@ -654,9 +606,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
         X.c3 = c3;
         X.known = known;
         X.spec = 0;
-        if (fused) {
-            X.spec = 3;                                         // speculate on the state after the fused merge
-        } else if (known) {
+        if (known) {
             X.spec = 3;                                         // speculate on the known merge, no search
             LK_DIAG(known);
         } else if (spec_on && len >= 3 && k < (int32_t)n - 1) {
@@ -673,10 +623,6 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             if (zmerge) {
                 double *z = Z + 4ull * S.k;
                 z[0] = za; z[1] = zb; z[2] = zd; z[3] = zn;
-            }
-            if (fused) {                                        // (z[3], the size: the row pass)
-                double *z = Z + 4ull * z2k;
-                z[0] = z2a; z[1] = z2b; z[2] = z2d;
             }
             if (restart >= 0) chain[0] = restart;
             if (npush > 0) chain[pp0] = pv0;
@@ -740,20 +686,11 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     const int32_t x = X.x, y = X.y, nx = X.nx, ny = X.ny, t = X.top;
     const int spec = X.spec;
     const bool search = spec != 3, sp = spec != 0;
-    // speculation rows: A = t, B = below, W = chain[len - 3] (spec 3 at len 2: no W).
-    // A fused known merge (X.fused) of a2 and b2 is that speculation made
-    // real: A = a2, B = b2, W = the top after it, and the merged row U is
-    // stored (row and column ys); the state above is the one after it
-    const bool fused = X.fused != 0;
-    const int32_t A = fused ? X.a2 : t, B = fused ? X.b2 : X.below, W = fused ? t : X.c3;
-    const bool hasW = sp && (fused ? X.len >= 1 : X.len >= 3);
+    // speculation rows: A = t, B = below, W = chain[len - 3] (spec 3 at len 2: no W)
+    const int32_t A = t, B = X.below, W = X.c3;
+    const bool hasW = sp && X.len >= 3;
     const bool yA = pend && A == y, yB = pend && B == y, yW = pend && W == y;
-    // a fused merge that takes this launch's merged row y (w pushed y, y merged
-    // back: recip) retires or rewrites row y: no store of this launch's merge
-    // at all; one of two other rows (wmerge) supersedes entries A and B of it
-    const bool m1_gone = fused && (yA || yB), m1_skipAB = fused && !m1_gone;
     const int32_t ys = A < B ? B : A;                          // the speculated merge's row index, max(A, B)
-    double *Dys = D + (uint64_t)(fused ? ys : 0) * n;
     const double *Dx = D + (uint64_t)x * n;
     double *Dy = D + (uint64_t)y * n;
     const double *Da = D + (uint64_t)(yA ? 0 : A) * n;
@@ -819,12 +756,6 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                 sxs = A < B ? sa : sb_;
                 sys = A < B ? sb_ : sa;
                 dvs = lw_div(sxs, sys);
-                // a fused merge's size: its Z row and the state's n2 (the next
-                // launch's size override), by the thread that wrote both
-                if (fused && blockIdx.x == 0 && threadIdx.x == 0) {
-                    Z[4ull * (X.k - 1) + 3] = (double)(sxs + sys);
-                    st[q].n2 = sxs + sys;
-                }
             }
         }
 #pragma unroll
@@ -858,13 +789,11 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             double u = 0.0;
             if (pend && i != y) {
                 u = lw_update(method, dx[k], dy[k], nx, ny, dvxy);
-                if (!m1_gone && !(m1_skipAB && (i == A || i == B))) {
-                    store_row(i, u);
-                    // the column copy D[R][y] of the rows R = A, B, W whose entry y the
-                    // lane of i = y recomputes (U1[R], from D[x][R] and D[R][y]) is that
-                    // lane's to store, after its load of it
-                    if (!((fa && i == A) || (fb && i == B) || (fw && i == W))) store_col(i, u);
-                }
+                store_row(i, u);
+                // the column copy D[R][y] of the rows R = A, B, W whose entry y the
+                // lane of i = y recomputes (U1[R], from D[x][R] and D[R][y]) is that
+                // lane's to store, after its load of it
+                if (!((fa && i == A) || (fb && i == B) || (fw && i == W))) store_col(i, u);
             }
             // the rows as they are after that merge: row y is u; entry y of a
             // row R is U1[R]
@@ -873,11 +802,10 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                 ca = yA ? 0.0 : lw_update(method, xa, ya_, nx, ny, dvxy);
                 if (sp) cb = yB ? 0.0 : lw_update(method, xb, yb, nx, ny, dvxy);
                 if (hasW) cw = yW ? 0.0 : lw_update(method, xw, yw, nx, ny, dvxy);
-                // (the same bits as those lanes' u: the same operands and update;
-                // entries A and B belong to a fused merge's row instead)
-                if (fa && !fused) store_col(A, ca);
-                if (fb && !fused) store_col(B, cb);
-                if (fw && !m1_gone) store_col(W, cw);
+                // (the same bits as those lanes' u: the same operands and update)
+                if (fa) store_col(A, ca);
+                if (fb) store_col(B, cb);
+                if (fw) store_col(W, cw);
             } else {
                 ca = yA ? u : da[k];
                 if (sp) cb = yB ? u : db[k];
@@ -888,13 +816,6 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                 if (i != A && i != B) {
                     // P2: the speculated merged row; P3: W's row after that merge
                     const double U = lw_update(method, A < B ? ca : cb, A < B ? cb : ca, sxs, sys, dvs);
-                    if (fused) {
-                        // the fused merge's row ys = max(A, B) and its column: D[ys][i] is
-                        // read only by this lane (its own column), D[i][ys] by the lane of
-                        // i = ys, which ignores it (rows A and B take no part in P2 / P3)
-                        Dys[i] = U;
-                        __hip_atomic_store(&D[(uint64_t)i * n + ys], U, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    }
                     if (better(U, i, yv, yi)) { yv = U; yi = i; }
                     if (hasW) {
                         if (i == W) {
@@ -1095,12 +1016,12 @@ static void launch_dist_tiles_condensed(const DmFromCondensed &v, uint32_t n, do
 // (sort_and_label: linkage_sparse.cpp, shared with the sparse path)
 struct NnArgs {
     double *D; uint32_t n; int32_t *size, *chain; LinkState *st; LinkFwd *fwd;
-    MinIdx *parts, *parts2, *parts3; int32_t *done; double *Z; uint32_t q; int spec_on, fuse_on;
+    MinIdx *parts, *parts2, *parts3; int32_t *done; double *Z; uint32_t q; int spec_on;
 };
 template <int W, int P>
 static void launch_nn(int method, dim3 grid, dim3 blk, hipStream_t st, const NnArgs &a) {
 #define DREPHIP_LK_NN(M) hipLaunchKernelGGL((k_nn_step<W, P, M>), grid, blk, 0, st, a.D, a.n, a.size, a.chain, a.st, \
-                                            a.fwd, a.parts, a.parts2, a.parts3, a.done, a.Z, a.q, a.spec_on, a.fuse_on)
+                                            a.fwd, a.parts, a.parts2, a.parts3, a.done, a.Z, a.q, a.spec_on)
     if (method == DREPHIP_LINK_COMPLETE) DREPHIP_LK_NN(DREPHIP_LINK_COMPLETE);
     else if (method == DREPHIP_LINK_WEIGHTED) DREPHIP_LK_NN(DREPHIP_LINK_WEIGHTED);
     else DREPHIP_LK_NN(DREPHIP_LINK_AVERAGE);
@@ -1157,10 +1078,6 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     // launches); 2 (default) with the known-merge speculation (spec 3)
     const char *spe = getenv("DREPHIP_LINK_SPEC");
     const int spec_on = spe ? std::max(0, std::min(2, atoi(spe))) : 2;
-    // known merges applied by the launch that discovers them (fused, k_nn_step;
-    // needs spec_on 2): DREPHIP_LINK_FUSE=0 leaves them to the next launch (A/B)
-    const char *fue = getenv("DREPHIP_LINK_FUSE");
-    const int fuse_on = (fue ? atoi(fue) != 0 : true) && spec_on > 1;
     if ((rc = scratch(ctx, "lk_st", 2 * sizeof(LinkState), (void **)&d_st))) return rc;
     LinkFwd *d_fwd;
     if ((rc = scratch(ctx, "lk_fwd", 2 * sizeof(LinkFwd), (void **)&d_fwd))) return rc;
@@ -1214,8 +1131,7 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     for (int b = 0; b < kBatch; b++) {
         const uint32_t q = (uint32_t)(b & 1);
         const dim3 gm(grid), gn(grid + 1), blk(wg);
-        const NnArgs a{d_D, n, d_size, d_chain, d_st, d_fwd, d_parts, d_parts2, d_parts3, d_done, d_Z, q, spec_on,
-                       fuse_on};
+        const NnArgs a{d_D, n, d_size, d_chain, d_st, d_fwd, d_parts, d_parts2, d_parts3, d_done, d_Z, q, spec_on};
 #define DREPHIP_LK_LAUNCH(W, P)                                                                                      \
     do {                                                                                                         \
         if (mst) hipLaunchKernelGGL((k_mst_step<W, P>), gm, blk, 0, st, d_D, n, d_size, d_Dmin, d_st, d_parts, d_done, \
@@ -1278,8 +1194,8 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
         HIPC(hipMemcpy(&hd, d_diag, sizeof(hd), hipMemcpyDeviceToHost));
         (void)hipFree(d_diag);
         fprintf(stderr, "[drephip] chain diag: twice %d scans %d specwin %d known %d (wmerge %d, recip %d) "
-                        "merge launches without speculation %d, fused known merges %d\n", hd.twice, hd.scans,
-                hd.specwin, hd.known, hd.wmerge, hd.recip, hd.m0, hd.fusedm);
+                        "merge launches without speculation %d\n", hd.twice, hd.scans, hd.specwin, hd.known,
+                hd.wmerge, hd.recip, hd.m0);
     }
 #endif
 #if DREPHIP_LK_PHASES
