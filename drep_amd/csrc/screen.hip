@@ -355,6 +355,10 @@ __global__ __launch_bounds__(kMarkWG) void k_screen_mark(const uint32_t *__restr
             const uint32_t tprev = __shfl_up(tx, 1, 64);
             const bool tile_head = lane == 0 ? tx != tcarry || tx == 0xFFFFFFFFu : tprev != tx;
             tcarry = __builtin_amdgcn_readlane(tx, 63);
+            // an x block with no genome among this call's rows marks nothing: a
+            // rank of a sharded job walks only its own part of each long run
+            // (the run's entries are in genome order, so that part is contiguous)
+            if (__ballot(x_ok) == 0) continue;
             for (uint32_t yb = xb; yb < m; yb += 64) {
                 const uint32_t yl = yb + lane;
                 const bool y_ok = yl < m;
