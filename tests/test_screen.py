@@ -227,9 +227,19 @@ def test_screen_light_cells(s, N, monkeypatch):
         v = H[a, rng.integers(0, NH[a])]
         plant([b], (v & np.uint64(0xFFFFFFFF)) | (np.uint64(rng.integers(1, 1 << 30)) << np.uint64(32)))
     oc, od = oracle.allpairs(H, NH, s, threads=8)
+
+    def start(i):
+        return i * N - i * (i + 1) // 2
     with _lib.Context(0, 21, s, 42) as ctx:
         c, d, st = run(ctx, H, NH, ctx.SCREEN_ON)
         assert np.array_equal(c, oc) and np.array_equal(d, od)
+        # row ranges (a sharded rank's slice: the marking walks only the part of
+        # each run -- hubs span several 64-entry blocks -- among its rows)
+        for r0, r1 in ((0, N // 3), (N // 3, 2 * N // 3 + 5), (2 * N // 3 + 5, N - 1)):
+            n = start(r1) - start(r0)
+            co, do = np.zeros(n, np.uint16), np.zeros(n, np.uint16)
+            ctx.allpairs_rows(H, NH, r0, r1, co, do)
+            assert np.array_equal(co, oc[start(r0):start(r1)]) and np.array_equal(do, od[start(r0):start(r1)]), (r0, r1)
         monkeypatch.setenv("DREPHIP_SCREEN_LIGHT", "0")
         c2, d2, st2 = run(ctx, H, NH, ctx.SCREEN_ON)
         assert np.array_equal(c2, oc) and np.array_equal(d2, od)
