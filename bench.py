@@ -46,11 +46,11 @@ SKETCH_PHASES = os.path.join(ROOT, "profiles", "r05_sketch_isa_phases.json")
 SKETCH_ABLATION = os.path.join(ROOT, "profiles", "r05_sketch_ablation.json")
 # committed PMC summaries (tools/pmc_summary.py): VALU / LDS utilisation of the
 # two kernels, reported next to the live timings
-SKETCH_PMC = os.path.join(ROOT, "profiles", "r04_sketch_pmc_sq.json")
+SKETCH_PMC = os.path.join(ROOT, "profiles", "r05_sketch_pmc_sq.json")
 # all-pairs profiles of tools/profile_allpairs.sh, one per (N, s) case: the
 # bench line quotes the one of its own workload (never another N's)
 DIST_PROFILES = [os.path.join(ROOT, "profiles", r + "_allpairs_N%d%s.json") for r in ("r05", "r04")]   # newest first
-SKETCH_TRAFFIC = os.path.join(ROOT, "profiles", "r04_sketch_traffic.json")
+SKETCH_TRAFFIC = os.path.join(ROOT, "profiles", "r05_sketch_traffic.json")
 PROFILE_STEPS = 3              # untimed steps that time finalize / all-pairs / table build
 VERIFY_GENOMES = 16            # timed-step sketches re-derived by the C oracle (sampled, every run)
 VERIFY_PAIRS = 100_000         # timed-step counts re-derived by the C oracle (random pairs + one row)
