@@ -1500,7 +1500,8 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
         // columns; the whole-row kernel takes up to kListCols per item, so a
         // row tile's image is loaded once for most tiles
         int rc = screen_impl(ctx, d_hashes, d_nhash, N, row0, row1, R, path == DREPHIP_AP_BAND ? kBandCols : kListCols,
-                             seg0, npairs, d_common, d_denom, smode == DREPHIP_SCREEN_ON, st, &scr);
+                             seg0, npairs, d_common, d_denom, smode == DREPHIP_SCREEN_ON, path == DREPHIP_AP_BAND, st,
+                             &scr);
         if (rc) return rc;
         ctx->last_screen = scr;
     }

@@ -205,10 +205,11 @@ int allpairs_wait_impl(drephip_ctx *ctx);
 // exactly one hash (outside the listed cells); the LIST kernels complete it.
 // res->use = false when the set is too dense for it to pay (unless force) or
 // too large for its 32-bit indices; the dense path runs then (and rewrites
-// every pair).  Synchronises the stream.
+// every pair).  `band`: the LIST kernel is the band kernel (s > 2048), the
+// only one the light cells pay for.  Synchronises the stream.
 int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N, uint32_t row0,
                 uint32_t row1, uint32_t R, uint32_t C, uint64_t seg0, uint64_t npairs, uint16_t *d_common,
-                uint16_t *d_denom, bool force, hipStream_t st, ScreenResult *res);
+                uint16_t *d_denom, bool force, bool band, hipStream_t st, ScreenResult *res);
 // Every pair of the segment as an unscreened one: common 0, denominator
 // min(s, |A| + |B|); the LIST kernels then overwrite the screened pairs.
 int screen_fill_impl(drephip_ctx *ctx, const uint32_t *d_nhash, uint32_t N, uint32_t row0, uint32_t row1,

@@ -611,7 +611,7 @@ static int hip_scan(drephip_ctx *ctx, const char *name, const I *in, T *out, uin
 
 int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N, uint32_t row0,
                 uint32_t row1, uint32_t R, uint32_t C, uint64_t seg0, uint64_t npairs, uint16_t *d_common,
-                uint16_t *d_denom, bool force, hipStream_t st, ScreenResult *res) {
+                uint16_t *d_denom, bool force, bool band, hipStream_t st, ScreenResult *res) {
     *res = ScreenResult{};
     const uint32_t s = ctx->s;
     if ((uint64_t)N * s >= (1ull << 32)) return DREPHIP_OK;          // entry values g * s + k are 32-bit
@@ -729,9 +729,12 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
     if ((rc = scratch(ctx, "sc_bitmap", (uint64_t)ntiles * NW * 4, (void **)&d_bm))) return rc;
     // Light cells (k_screen_light): a heavy-cell bitmap and each cell's first
     // marking run, (ntiles x N) words -- taken when that fits kLightBudget
-    // (N = 10^4 with R = 4: 100 MB); DREPHIP_SCREEN_LIGHT=0 turns it off (A/B)
+    // (N = 10^4 with R = 4: 100 MB), for the band kernel only: at configs[4]
+    // its LIST time 9.0 -> 4.0 ms for +0.9 ms of screen; at configs[2] (the q
+    // kernel, s = 1000) 0.39 -> 0.35 ms of LIST for +0.33 ms of screen
+    // (profiles/r05_screen_light_c2_ab.txt).  DREPHIP_SCREEN_LIGHT=0/1 forces it (A/B)
     const char *le = getenv("DREPHIP_SCREEN_LIGHT");
-    const bool light = (!le || atoi(le) != 0) && (uint64_t)ntiles * N * 4 <= kLightBudget;
+    const bool light = (le ? atoi(le) != 0 : band) && (uint64_t)ntiles * N * 4 <= kLightBudget;
     uint32_t *d_bmH = nullptr, *d_crun = nullptr;
     if (light) {
         if ((rc = scratch(ctx, "sc_bitmap_heavy", (uint64_t)ntiles * NW * 4, (void **)&d_bmH))) return rc;

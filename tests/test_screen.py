@@ -231,6 +231,7 @@ def test_screen_light_cells(s, N, monkeypatch):
     def start(i):
         return i * N - i * (i + 1) // 2
     with _lib.Context(0, 21, s, 42) as ctx:
+        monkeypatch.setenv("DREPHIP_SCREEN_LIGHT", "1")        # (by default only with the band kernel, s > 2048)
         c, d, st = run(ctx, H, NH, ctx.SCREEN_ON)
         assert np.array_equal(c, oc) and np.array_equal(d, od)
         # row ranges (a sharded rank's slice: the marking walks only the part of
@@ -243,6 +244,9 @@ def test_screen_light_cells(s, N, monkeypatch):
         monkeypatch.setenv("DREPHIP_SCREEN_LIGHT", "0")
         c2, d2, st2 = run(ctx, H, NH, ctx.SCREEN_ON)
         assert np.array_equal(c2, oc) and np.array_equal(d2, od)
+        monkeypatch.delenv("DREPHIP_SCREEN_LIGHT")
+        _, _, st3 = run(ctx, H, NH, ctx.SCREEN_ON)            # the default: light with the band kernel only
+        assert (st3["simple"], st3["marked"]) == ((st["simple"], st["marked"]) if s > 2048 else (st2["simple"], st2["marked"]))
     # the light path wrote pairs itself and left fewer cells to the kernel
     assert st["simple"] > st2["simple"] + 500 and st["marked"] < st2["marked"] - 200, (st, st2)
     assert (oc == 1).sum() > 500 and ((oc == 0) & (od == s)).sum() > 1000
