@@ -71,6 +71,7 @@ struct LinkStats {            // last drephip_linkage* call, host wall clock (se
                               // sparse path: the pair extraction (kernel + readback)
     double chain_s = 0;       // nn-chain / MST steps (graph replays; sparse path: host setup + steps)
     uint64_t launches = 0;    // dense chain: step launches that did work (0: sparse path / none)
+    uint64_t compactions = 0; // dense chain: matrix compactions (linkage.hip, k_lk_cmp_rank)
     double finish_s = 0;      // Z readback + stable sort + relabel on the host
     double wall_s = 0;        // the whole call
     int sparse = 0;           // 1: the sparse path produced Z

@@ -922,6 +922,122 @@ __global__ __launch_bounds__(WG) void k_mst_step(const double *__restrict__ D, u
     if (threadIdx.x == 0) parts[(uint64_t)q * kLkPartStride + blockIdx.x] = part;
 }
 
+// ------------------------------------------------------------ compaction
+// Round 5: the matrix follows the active clusters.  A merge retires a row and
+// column for good, but the step kernels keep reading full n-long rows (and
+// size[] entries) of the original n x n matrix, so at 10^5 the second half of
+// the chain pays 10^5-entry rows for <= 5 x 10^4 clusters.  Between graph
+// replays, once at most half of the matrix's rows are active, the active rows
+// and columns are moved to the front as an m x m matrix (stride m) in the same
+// allocation, in index order, and the chain's state is renumbered: scipy's
+// decisions depend only on the distances and on the ORDER of indices (ties:
+// the previous chain element, then the lowest index), which an order-keeping
+// renumbering preserves, so Z in local numbers maps back to the same rows.
+// The step grid is then chosen for m (fewer entries per lane, narrower
+// workgroups: 7.0 us per launch at 10^5, 6.3 at 5 x 10^4, 5.9 at 2.5 x 10^4).
+//
+// At a replay boundary the last launch has decided and applied a merge (x, y)
+// whose two sizes are still to be written by the next launch (state buffer 1,
+// pend): x counts as retired and y as merged here; x's number becomes m (a
+// dummy slot of the new size array, which the next launch writes 0 to).
+constexpr uint32_t kCmpWG = 1024;
+__device__ __forceinline__ int32_t cmp_size(const LinkState &S, const int32_t *size, uint32_t i) {
+    return S.pend && (int32_t)i == S.x ? 0 : S.pend && (int32_t)i == S.y ? S.nx + S.ny : size[i];
+}
+// one workgroup: rank[i] = active clusters below i (rank[m] = their count),
+// the new sizes and the new -> old map
+__global__ __launch_bounds__(kCmpWG) void k_lk_cmp_rank(const int32_t *__restrict__ size, const LinkState *__restrict__ st,
+                                                        uint32_t m, uint32_t *__restrict__ rank,
+                                                        int32_t *__restrict__ size2, int32_t *__restrict__ orig) {
+    __shared__ uint32_t sc[kCmpWG];
+    const LinkState S = st[1];
+    const uint32_t per = (m + kCmpWG - 1) / kCmpWG, b0 = min(m, threadIdx.x * per), b1 = min(m, b0 + per);
+    uint32_t c = 0;
+    for (uint32_t i = b0; i < b1; i++) c += cmp_size(S, size, i) > 0;
+    sc[threadIdx.x] = c;
+    __syncthreads();
+    for (uint32_t o = 1; o < kCmpWG; o <<= 1) {                 // inclusive scan of the counts
+        const uint32_t v = threadIdx.x >= o ? sc[threadIdx.x - o] : 0;
+        __syncthreads();
+        sc[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t r = sc[threadIdx.x] - c;
+    for (uint32_t i = b0; i < b1; i++) {
+        rank[i] = r;
+        const int32_t e = cmp_size(S, size, i);
+        if (e > 0) { size2[r] = e; orig[r] = (int32_t)i; r++; }
+    }
+    if (threadIdx.x == kCmpWG - 1) rank[m] = sc[kCmpWG - 1];
+}
+// one workgroup of 256: the state, the forwarded operands, the chain and the
+// last launch's partial sets renumbered; each partial set reduced to its
+// minimum in slot 0 (the next launch's grid reads np_new slots), the rest
+// empty.  Indices outside [0, m) (-1, INT_MAX) are kept.
+__global__ __launch_bounds__(256) void k_lk_cmp_state(LinkState *__restrict__ st, LinkFwd *__restrict__ fwd,
+                                                      MinIdx *__restrict__ parts, MinIdx *__restrict__ parts2,
+                                                      MinIdx *__restrict__ parts3, int32_t *__restrict__ chain,
+                                                      const uint32_t *__restrict__ rank, uint32_t m, uint32_t np_old,
+                                                      uint32_t np_new, int32_t *__restrict__ size2,
+                                                      int32_t *__restrict__ done) {
+    const LinkState S = st[1];
+    const uint32_t mn = rank[m];
+    auto tr = [&](int32_t v) { return v >= 0 && (uint32_t)v < m ? (int32_t)rank[v] : v; };
+    MinIdx *P1 = parts + kLkPartStride, *P2 = parts2 + kLkPartStride, *P3 = parts3 + kLkPartStride;
+    MinIdx a{INFINITY, 0x7fffffff}, b = a, c = a;
+    for (uint32_t s = threadIdx.x; s < np_old; s += 256) {
+        if (better(P1[s].v, P1[s].i, a.v, a.i)) a = P1[s];
+        if (better(P2[s].v, P2[s].i, b.v, b.i)) b = P2[s];
+        if (better(P3[s].v, P3[s].i, c.v, c.i)) c = P3[s];
+    }
+    block_argmin3<256>(a, b, c, true, true);                   // (every slot read before the barrier in it)
+    const MinIdx none{INFINITY, 0x7fffffff};
+    for (uint32_t s = threadIdx.x; s < np_new; s += 256)
+        if (s) { P1[s] = none; P2[s] = none; P3[s] = none; }
+    for (int32_t p = threadIdx.x; p < S.len; p += 256) chain[p] = tr(chain[p]);
+    __syncthreads();                                            // (every read of st[1] before its rewrite)
+    if (threadIdx.x == 0) {
+        P1[0] = MinIdx{a.v, tr(a.i)}; P2[0] = MinIdx{b.v, tr(b.i)}; P3[0] = MinIdx{c.v, tr(c.i)};
+        LinkState X = S;
+        X.k = S.k - (int32_t)(m - mn);                          // 0: the new epoch's merges count from here
+        X.top = tr(S.top); X.below = tr(S.below); X.first_active = tr(S.first_active); X.c3 = tr(S.c3);
+        if (S.pend) { X.x = (int32_t)mn; X.y = tr(S.y); }
+        st[1] = X;
+        LinkFwd F = fwd[1];
+        F.c3 = tr(F.c3); F.c4 = tr(F.c4); F.c5 = tr(F.c5); F.c6 = tr(F.c6);
+        fwd[1] = F;
+        size2[mn] = 0;                                          // the retired x's dummy slot
+        *done = X.k;
+    }
+}
+// new rows [r0, r1) (stride sn) of the active rows and columns of the old
+// matrix (stride so), written at dst row r - d0.  In place (src == dst) for a
+// chunk with r1 <= 2 r0 when sn <= so / 2: its writes end below r1 sn <= r0 so,
+// i.e. they only cover old rows below r0, which only new rows below r0 read
+// (orig[r] >= r) -- earlier chunks, finished (stream order).  The first rows
+// go through a scratch buffer (row 0 overlaps itself).
+__global__ __launch_bounds__(256) void k_lk_cmp_rows(const double *src, uint32_t so, double *dst, uint32_t sn,
+                                                     const int32_t *__restrict__ orig, uint32_t r0, uint32_t r1,
+                                                     uint32_t d0) {
+    const uint32_t nb = (sn + 1023) / 1024;
+    const uint64_t items = (uint64_t)(r1 - r0) * nb;
+    for (uint64_t it = blockIdx.x; it < items; it += gridDim.x) {
+        const uint32_t r = r0 + (uint32_t)(it / nb), c0 = (uint32_t)(it % nb) * 1024 + threadIdx.x;
+        const double *s = src + (uint64_t)orig[r] * so;
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t c = c0 + 256u * u;
+            v[u] = c < sn ? s[orig[c]] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t c = c0 + 256u * u;
+            if (c < sn) dst[(uint64_t)(r - d0) * sn + c] = v[u];
+        }
+    }
+}
+
 // ------------------------------------------------------------ matrix build
 // D (n x n f64, rows in perm order) from the condensed upper triangle, by
 // 64 x 64 tiles of (row block bi <= column block bj): a wave reads one row's
@@ -1054,14 +1170,21 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     constexpr uint32_t kLkWaveN = 16384;
     const char *wge = getenv("DREPHIP_LINK_WG");
     const int wreq = wge ? atoi(wge) : 0;
-    const bool wave_wg = method != DREPHIP_LINK_SINGLE && (wreq == 64 || (wreq == 0 && !pl && n <= kLkWaveN));
-    const uint32_t wsz = wave_wg ? 64 : wreq == 512 && method != DREPHIP_LINK_SINGLE ? 512 : kLkWG;
-    const uint32_t per = pl ? std::max(1, std::min(64, atoi(pl)))
-                            : std::max(1u, (n + wsz * kLkTarget - 1) / (wsz * kLkTarget));
-    const uint32_t wg = wave_wg ? 64 : wreq == 128 || wreq == 256 || (wreq == 512 && method != DREPHIP_LINK_SINGLE)
-                                           ? (uint32_t)wreq : n <= kLkSmallN && !pl ? 128 : kLkWG;
-    const uint32_t grid = std::max(1u, std::min(1024u, (n + wg * per - 1) / (wg * per)));
-    const int tpl = per <= 1 ? 1 : per <= 2 ? 2 : per <= 4 || !wave_wg ? 4 : 8;     // entries per lane per pass
+    struct StepCfg { uint32_t wg, grid; int tpl; };
+    // (a function of the matrix's current size m: the compaction below shrinks it)
+    auto cfg_for = [&](uint32_t m) {
+        const bool wave_wg = method != DREPHIP_LINK_SINGLE && (wreq == 64 || (wreq == 0 && !pl && m <= kLkWaveN));
+        const uint32_t wsz = wave_wg ? 64 : wreq == 512 && method != DREPHIP_LINK_SINGLE ? 512 : kLkWG;
+        const uint32_t per = pl ? std::max(1, std::min(64, atoi(pl)))
+                                : std::max(1u, (m + wsz * kLkTarget - 1) / (wsz * kLkTarget));
+        StepCfg c;
+        c.wg = wave_wg ? 64 : wreq == 128 || wreq == 256 || (wreq == 512 && method != DREPHIP_LINK_SINGLE)
+                                  ? (uint32_t)wreq : m <= kLkSmallN && !pl ? 128 : kLkWG;
+        c.grid = std::max(1u, std::min(1024u, (m + c.wg * per - 1) / (c.wg * per)));
+        c.tpl = per <= 1 ? 1 : per <= 2 ? 2 : per <= 4 || !wave_wg ? 4 : 8;     // entries per lane per pass
+        return c;
+    };
+    StepCfg cfg = cfg_for(n);
     int32_t *d_size, *d_chain, *d_done;
     double *d_Z, *d_Dmin;
     LinkState *d_st;
@@ -1121,73 +1244,155 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
         HIPC(hipMemcpyToSymbol(HIP_SYMBOL(g_lk_ph), &d_ph, sizeof(d_ph)));
     }
 #endif
-    // batches of steps captured once in a graph, replayed until every merge is done
-    constexpr int kBatch = 256;
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t exec = nullptr;
-    HIPC(hipStreamSynchronize(st));
-    HIPC(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-    static_assert(kBatch % 2 == 0, "step parity must restart at 0 with every replay");
-    for (int b = 0; b < kBatch; b++) {
-        const uint32_t q = (uint32_t)(b & 1);
-        const dim3 gm(grid), gn(grid + 1), blk(wg);
-        const NnArgs a{d_D, n, d_size, d_chain, d_st, d_fwd, d_parts, d_parts2, d_parts3, d_done, d_Z, q, spec_on};
+    // batches of steps captured in a graph, replayed until every merge is done
+    // (DREPHIP_LINK_BATCH: an even batch length, and DREPHIP_LINK_POLL: the
+    // replays between reads of the merge count -- small values for the tests,
+    // which put compactions at many different chain states)
+    const char *be = getenv("DREPHIP_LINK_BATCH"), *pe = getenv("DREPHIP_LINK_POLL");
+    const int kBatch = be ? std::max(2, std::min(4096, atoi(be) & ~1)) : 256;
+    const uint64_t poll = pe ? (uint64_t)std::max(1, atoi(pe)) : 4;
+    // the compaction (above k_lk_cmp_rank): on for the chain methods unless
+    // DREPHIP_LINK_COMPACT=0; while at least DREPHIP_LINK_COMPACT_MIN (2048)
+    // clusters are active
+    const char *ce = getenv("DREPHIP_LINK_COMPACT"), *cme = getenv("DREPHIP_LINK_COMPACT_MIN");
+    const bool compact_on = !mst && (!ce || atoi(ce) != 0);
+    const uint32_t compact_min = cme ? (uint32_t)std::max(2, atoi(cme)) : 2048;
+    uint32_t m = n;                                 // the matrix's current size (stride)
+    int32_t *d_sz = d_size, *d_sz2 = nullptr;       // sizes; the other buffer of a compaction
+    uint32_t *d_rank = nullptr;
+    int32_t *d_orig = nullptr;
+    double *d_ctmp = nullptr;
+    uint64_t kbase = 0;                              // merges before the current epoch
+    std::vector<std::pair<uint64_t, std::vector<int32_t>>> epochs;   // (first Z row, local -> original index)
+    auto capture = [&](hipGraphExec_t *exec) -> int {
+        hipGraph_t graph = nullptr;
+        HIPC(hipStreamSynchronize(st));
+        HIPC(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+        double *Zc = d_Z + 4 * kbase;
+        const uint32_t wg = cfg.wg, grid = cfg.grid;
+        const int tpl = cfg.tpl;
+        for (int b = 0; b < kBatch; b++) {          // (even: step parity restarts at 0 with every replay)
+            const uint32_t q = (uint32_t)(b & 1);
+            const dim3 gm(grid), gn(grid + 1), blk(wg);
+            const NnArgs a{d_D, m, d_sz, d_chain, d_st, d_fwd, d_parts, d_parts2, d_parts3, d_done, Zc, q, spec_on};
 #define DREPHIP_LK_LAUNCH(W, P)                                                                                      \
     do {                                                                                                         \
-        if (mst) hipLaunchKernelGGL((k_mst_step<W, P>), gm, blk, 0, st, d_D, n, d_size, d_Dmin, d_st, d_parts, d_done, \
-                                    d_Z, q);                                                                     \
+        if (mst) hipLaunchKernelGGL((k_mst_step<W, P>), gm, blk, 0, st, d_D, m, d_sz, d_Dmin, d_st, d_parts, d_done, \
+                                    Zc, q);                                                                      \
         else launch_nn<W, P>(method, gn, blk, st, a);                                                            \
     } while (0)
-        if (wg == 64) {
-            if (tpl == 1) launch_nn<64, 1>(method, gn, blk, st, a);
-            else if (tpl == 2) launch_nn<64, 2>(method, gn, blk, st, a);
-            else if (tpl == 4) launch_nn<64, 4>(method, gn, blk, st, a);
-            else launch_nn<64, 8>(method, gn, blk, st, a);
-        } else if (wg == 128) {
-            if (tpl == 1) DREPHIP_LK_LAUNCH(128, 1);
-            else if (tpl == 2) DREPHIP_LK_LAUNCH(128, 2);
-            else DREPHIP_LK_LAUNCH(128, 4);
-        } else if (wg == 512 && !mst) {
-            if (tpl == 1) launch_nn<512, 1>(method, gn, blk, st, a);
-            else launch_nn<512, 2>(method, gn, blk, st, a);
-        } else {
-            if (tpl == 1) DREPHIP_LK_LAUNCH(256, 1);
-            else if (tpl == 2) DREPHIP_LK_LAUNCH(256, 2);
-            else DREPHIP_LK_LAUNCH(256, 4);
-        }
+            if (wg == 64) {
+                if (tpl == 1) launch_nn<64, 1>(method, gn, blk, st, a);
+                else if (tpl == 2) launch_nn<64, 2>(method, gn, blk, st, a);
+                else if (tpl == 4) launch_nn<64, 4>(method, gn, blk, st, a);
+                else launch_nn<64, 8>(method, gn, blk, st, a);
+            } else if (wg == 128) {
+                if (tpl == 1) DREPHIP_LK_LAUNCH(128, 1);
+                else if (tpl == 2) DREPHIP_LK_LAUNCH(128, 2);
+                else DREPHIP_LK_LAUNCH(128, 4);
+            } else if (wg == 512 && !mst) {
+                if (tpl == 1) launch_nn<512, 1>(method, gn, blk, st, a);
+                else launch_nn<512, 2>(method, gn, blk, st, a);
+            } else {
+                if (tpl == 1) DREPHIP_LK_LAUNCH(256, 1);
+                else if (tpl == 2) DREPHIP_LK_LAUNCH(256, 2);
+                else DREPHIP_LK_LAUNCH(256, 4);
+            }
 #undef DREPHIP_LK_LAUNCH
-    }
-    HIPC(hipStreamEndCapture(st, &graph));
-    hipError_t e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-    if (e != hipSuccess) { (void)hipGraphDestroy(graph); HIPC(e); }
+        }
+        HIPC(hipStreamEndCapture(st, &graph));
+        const hipError_t e = hipGraphInstantiate(exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        HIPC(e);
+        return DREPHIP_OK;
+    };
+    // done = the merges of the current epoch; at most half of the m rows
+    // active: the compaction, then the steps for the new m
+    auto compact = [&](int32_t done) -> int {
+        int rc;
+        if (!d_sz2) {
+            if ((rc = scratch(ctx, "lk_size2", (n + 1) * 4ull, (void **)&d_sz2))) return rc;
+            if ((rc = scratch(ctx, "lk_rank", (n + 1) * 4ull, (void **)&d_rank))) return rc;
+            if ((rc = scratch(ctx, "lk_orig", n * 4ull, (void **)&d_orig))) return rc;
+            if ((rc = scratch(ctx, "lk_ctmp", 64ull * (n / 2 + 1) * 8, (void **)&d_ctmp))) return rc;
+        }
+        const uint32_t np_old = DREPHIP_LK_WAVEPARTS ? cfg.grid * (cfg.wg / 64) : cfg.grid;
+        hipLaunchKernelGGL(k_lk_cmp_rank, dim3(1), dim3(kCmpWG), 0, st, d_sz, d_st, m, d_rank, d_sz2, d_orig);
+        uint32_t mn = 0;
+        HIPC(hipMemcpyAsync(&mn, d_rank + m, 4, hipMemcpyDeviceToHost, st));
+        HIPC(hipStreamSynchronize(st));
+        if (mn != m - (uint32_t)done || mn > m / 2 || mn < 2) {
+            set_error("linkage compaction: active clusters do not match the merge count");
+            return DREPHIP_ERR_INTERNAL;
+        }
+        const StepCfg nc = cfg_for(mn);
+        const uint32_t np_new = DREPHIP_LK_WAVEPARTS ? nc.grid * (nc.wg / 64) : nc.grid;
+        hipLaunchKernelGGL(k_lk_cmp_state, dim3(1), dim3(256), 0, st, d_st, d_fwd, d_parts, d_parts2, d_parts3, d_chain,
+                           d_rank, m, np_old, np_new, d_sz2, d_done);
+        auto rows = [&](const double *src, double *dst, uint32_t r0, uint32_t r1, uint32_t d0) {
+            const uint64_t items = (uint64_t)(r1 - r0) * ((mn + 1023) / 1024);
+            const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, items));
+            hipLaunchKernelGGL(k_lk_cmp_rows, dim3(g), dim3(256), 0, st, src, m, dst, mn, d_orig, r0, r1, d0);
+        };
+        const uint32_t R0 = std::min(64u, mn);
+        rows(d_D, d_ctmp, 0, R0, 0);
+        HIPC(hipMemcpyAsync(d_D, d_ctmp, (uint64_t)R0 * mn * 8, hipMemcpyDeviceToDevice, st));
+        for (uint32_t r0 = R0, r1; r0 < mn; r0 = r1) {
+            r1 = std::min(2 * r0, mn);
+            rows(d_D, d_D, r0, r1, 0);
+        }
+        HIPC(hipGetLastError());
+        std::vector<int32_t> loc(mn);
+        HIPC(hipMemcpyAsync(loc.data(), d_orig, mn * 4ull, hipMemcpyDeviceToHost, st));
+        HIPC(hipStreamSynchronize(st));
+        if (!epochs.empty())
+            for (auto &v : loc) v = epochs.back().second[v];
+        kbase += (uint64_t)done;
+        epochs.emplace_back(kbase, std::move(loc));
+        std::swap(d_sz, d_sz2);
+        m = mn;
+        cfg = nc;
+        return DREPHIP_OK;
+    };
+    hipGraphExec_t exec = nullptr;
+    if ((rc = capture(&exec))) return rc;
     // every search step either extends the chain or merges; the chain is at
     // most n long, so 3n steps always suffice (the bound only guards a hang)
     const uint64_t max_batches = (3ull * n) / kBatch + 2;
     int32_t done = 0;
+    hipError_t e = hipSuccess;
+    int crc = DREPHIP_OK;
     timing_mark(ctx, 2, st, true);
     for (uint64_t it = 0; it < max_batches; it++) {
         e = hipGraphLaunch(exec, st);
         if (e != hipSuccess) break;
-        if ((it & 3) == 3 || it + 1 == max_batches) {
+        if (it % poll == poll - 1 || it + 1 == max_batches) {
             e = hipMemcpyAsync(&done, d_done, 4, hipMemcpyDeviceToHost, st);
             if (e == hipSuccess) e = hipStreamSynchronize(st);
-            if (e != hipSuccess || done >= (int32_t)n - 1) break;
+            if (e != hipSuccess || done >= (int32_t)m - 1) break;
+            if (compact_on && m - (uint32_t)done <= m / 2 && m - (uint32_t)done >= compact_min) {
+                (void)hipGraphExecDestroy(exec);
+                exec = nullptr;
+                if ((crc = compact(done)) || (crc = capture(&exec))) break;
+            }
         }
     }
     timing_mark(ctx, 2, st, false);
-    (void)hipGraphExecDestroy(exec);
-    (void)hipGraphDestroy(graph);
+    if (exec) (void)hipGraphExecDestroy(exec);
+    if (crc) return crc;
     HIPC(e);
     HIPC(hipMemcpyAsync(&done, d_done, 4, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));
-    if (done != (int32_t)n - 1) { set_error("linkage did not finish"); return DREPHIP_ERR_INTERNAL; }
+    if (done != (int32_t)m - 1) { set_error("linkage did not finish"); return DREPHIP_ERR_INTERNAL; }
+    ctx->link.compactions = epochs.size();
     LinkState hs[2];
     HIPC(hipMemcpy(hs, d_st, sizeof(hs), hipMemcpyDeviceToHost));
     const int32_t bad = (hs[0].flags | hs[1].flags) & kLkBad;
     ctx->link.launches = (uint64_t)std::max(hs[0].launches, hs[1].launches);
     if (getenv("DREPHIP_DEBUG"))
-        fprintf(stderr, "[drephip] chain: n=%u launches %llu (%.4f per merge), speculation %d\n", n,
-                (unsigned long long)ctx->link.launches, (double)ctx->link.launches / (double)(n - 1), spec_on);
+        fprintf(stderr, "[drephip] chain: n=%u launches %llu (%.4f per merge), speculation %d, compactions %zu\n", n,
+                (unsigned long long)ctx->link.launches, (double)ctx->link.launches / (double)(n - 1), spec_on,
+                epochs.size());
 #if DREPHIP_LK_DIAG
     {
         LinkDiag hd;
@@ -1230,6 +1435,13 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     ctx->link.chain_s = t_fin - t_chain;
     std::vector<double> Z(4ull * (n - 1));
     HIPC(hipMemcpy(Z.data(), d_Z, Z.size() * 8, hipMemcpyDeviceToHost));
+    // rows merged after a compaction hold that epoch's numbers: the original ones
+    for (size_t e = 0; e < epochs.size(); e++) {
+        const uint64_t k1 = e + 1 < epochs.size() ? epochs[e + 1].first : n - 1;
+        const std::vector<int32_t> &g = epochs[e].second;
+        for (uint64_t k = epochs[e].first; k < k1; k++)
+            for (int c = 0; c < 2; c++) Z[4 * k + c] = (double)g[(size_t)Z[4 * k + c]];
+    }
     sort_and_label(Z, n);
     std::copy(Z.begin(), Z.end(), Z_out);
     ctx->link.finish_s = now_s() - t_fin;

@@ -876,6 +876,12 @@ def test_gpu_linkage_matches_scipy(method, n, kind):
     variants = [(None, {}), ("4", {})]
     if n <= 2000:
         variants += [("1", {}), ("16", {}), ("2", {"DREPHIP_LINK_WG": "64"}), ("8", {"DREPHIP_LINK_WG": "64"})]
+    # the matrix compacted as clusters retire, at many chain states: short
+    # graph batches, the merge count read after each, down to 4 active clusters
+    variants += [(None, {"DREPHIP_LINK_COMPACT_MIN": "4", "DREPHIP_LINK_BATCH": "16", "DREPHIP_LINK_POLL": "1"}),
+                 (None, {"DREPHIP_LINK_COMPACT_MIN": "4", "DREPHIP_LINK_BATCH": "6", "DREPHIP_LINK_POLL": "1"})]
+    if n <= 2000:
+        variants += [("2", {"DREPHIP_LINK_COMPACT_MIN": "4", "DREPHIP_LINK_BATCH": "10", "DREPHIP_LINK_POLL": "1"})]
 
     for per_lane, env in variants:
         if per_lane is not None:
@@ -904,6 +910,42 @@ def test_gpu_linkage_matches_scipy(method, n, kind):
             Z = ctx.linkage(y, method)
             assert ctx.linkage_info()["sparse"]
             assert np.array_equal(Z, Zs), ("sparse", np.argwhere(Z != Zs)[:5])
+
+
+@pytest.mark.parametrize("method", ["complete", "average", "weighted"])
+def test_gpu_linkage_compaction_runs(method, capfd, monkeypatch):
+    """The compaction (linkage.hip, k_lk_cmp_rank) happens where it should --
+    each time at most half the matrix's rows are active, not below
+    DREPHIP_LINK_COMPACT_MIN -- and Z stays scipy's; off with
+    DREPHIP_LINK_COMPACT=0."""
+    import re
+    import scipy.cluster.hierarchy as sch
+    n = 3000
+    rng = np.random.default_rng(7)
+    fam = rng.integers(0, 60, n)
+    iu = np.triu_indices(n, 1)
+    y = np.where(fam[iu[0]] == fam[iu[1]], np.round(rng.random(len(iu[0])) * 0.2, 3), 1.0)
+    Zs = sch.linkage(y, method=method)
+    monkeypatch.setenv("DREPHIP_DEBUG", "1")
+    monkeypatch.setenv("DREPHIP_LINK_BATCH", "32")
+    monkeypatch.setenv("DREPHIP_LINK_POLL", "1")
+    for cmin, want in (("100", range(4, 6)), ("2", range(6, 13))):
+        monkeypatch.setenv("DREPHIP_LINK_COMPACT_MIN", cmin)
+        capfd.readouterr()
+        with _lib.Context(0, 21, S, 42) as ctx:
+            ctx.set_linkage_path(ctx.LINK_DENSE)
+            Z = ctx.linkage(y, method)
+        err = capfd.readouterr().err
+        got = int(re.search(r"compactions (\d+)", err).group(1))
+        assert got in want, (cmin, got, err[-500:])
+        assert np.array_equal(Z, Zs), (cmin, np.argwhere(Z != Zs)[:5])
+    monkeypatch.setenv("DREPHIP_LINK_COMPACT", "0")
+    capfd.readouterr()
+    with _lib.Context(0, 21, S, 42) as ctx:
+        ctx.set_linkage_path(ctx.LINK_DENSE)
+        Z = ctx.linkage(y, method)
+    assert "compactions 0" in capfd.readouterr().err
+    assert np.array_equal(Z, Zs)
 
 
 @pytest.mark.parametrize("path", ["auto", "dense", "sparse"])
