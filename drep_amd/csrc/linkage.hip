@@ -712,13 +712,21 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     double xw = fw ? Dx[W + lz] : 0.0, yw = fw ? colY(W) : 0.0;
     // the sizes of A and B as of this step's decision (for the speculated merge)
     int32_t rsa = sp ? size[A + lz] : 0, rsb = sp ? size[B + lz] : 0;
+    // (as selects: the nested conditional form compiled to exec-mask branches)
     auto size_x = [&](int32_t i, int32_t stored) {
-        return pend && i == x ? 0 : pend && i == y ? nx + ny : size_prev(i, stored);
+        int32_t s = i == spsb ? spsbsz : stored;               // size_prev
+        s = i == spsa ? 0 : s;
+        if (pend) {
+            s = i == y ? nx + ny : s;
+            s = i == x ? 0 : s;
+        }
+        return s;
     };
+    double cay = 0.0, cby = 0.0, cwy = 0.0;                     // the y lane's entries U1[A], U1[B], U1[W]
     double bv = INFINITY, yv = INFINITY, wv = INFINITY;
     int32_t bi = 0x7fffffff, yi = 0x7fffffff, wi = 0x7fffffff;
     int32_t sxs = 0, sys = 0;                                   // the speculated merge's sizes
-    const LwDiv dvxy = lw_div(nx, ny);                          // (average: this step's divisor)
+    LwDiv dvxy = lw_div(nx, ny);                                // (average: this step's divisor)
     LwDiv dvs{1.0, 1.0};
     const uint32_t stride = G * WG;
     bool first = true;
@@ -735,6 +743,9 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
             if (sp && !yB) db[k] = Db[ic];
             if (hasW && !yW) dw[k] = Dw[ic];
         }
+        // the divisor's reciprocal while the loads are in flight (the compiler
+        // had sunk its IEEE division below the wait for them)
+        if (method == DREPHIP_LINK_AVERAGE && pend) asm volatile("" : "+v"(dvxy.n), "+v"(dvxy.r));
         // every load of the pass in flight before any is waited for: left to
         // itself the compiler sank the row loads below the size test that
         // uses size[i] (a second round trip per step), and waited for the
@@ -757,14 +768,21 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
                 sys = A < B ? sb_ : sa;
                 dvs = lw_div(sxs, sys);
             }
+            // (the same bits as those lanes' u: the same operands and update)
+            if (fa) cay = lw_update(method, xa, ya_, nx, ny, dvxy);
+            if (fb) cby = lw_update(method, xb, yb, nx, ny, dvxy);
+            if (fw) cwy = lw_update(method, xw, yw, nx, ny, dvxy);
         }
 #pragma unroll
         for (int k = 0; k < kLkPer; k++) {
             const int32_t i = (int32_t)(i0 + k * stride);
-            if (i >= (int32_t)n) continue;
             // the sizes as of this step's decision: the previous decision's
-            // (being written by workgroup 0) and this one's (not yet written)
-            if (size_x(i, sz[k]) == 0) continue;                // (retires x)
+            // (being written by workgroup 0) and this one's (not yet written).
+            // Written as selects on `live` rather than `continue`s and nested
+            // ifs: the branchy form compiled to a cascade of exec-mask branches
+            // (~half the pass's instructions at one wave per SIMD)
+            const bool live = i < (int32_t)n && size_x(i, sz[k]) != 0;   // (retires x)
+            const bool isy = pend && i == y;
             // this launch's merge: row y's new value at i, stored to row and column y
             // (one entry's two copies, D[y][i] and D[i][y])
             auto store_row = [&](int32_t c, double v) {
@@ -787,46 +805,58 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
 #endif
             };
             double u = 0.0;
-            if (pend && i != y) {
+            if (pend) {
                 u = lw_update(method, dx[k], dy[k], nx, ny, dvxy);
-                store_row(i, u);
-                // the column copy D[R][y] of the rows R = A, B, W whose entry y the
-                // lane of i = y recomputes (U1[R], from D[x][R] and D[R][y]) is that
-                // lane's to store, after its load of it
-                if (!((fa && i == A) || (fb && i == B) || (fw && i == W))) store_col(i, u);
+                if (live && !isy) {
+                    store_row(i, u);
+                    // the column copy D[R][y] of the rows R = A, B, W whose entry y the
+                    // lane of i = y recomputes (U1[R], from D[x][R] and D[R][y]) is that
+                    // lane's to store, after its load of it
+                    if (!((fa && i == A) || (fb && i == B) || (fw && i == W))) store_col(i, u);
+                }
+                if (isy) {
+                    if (fa) store_col(A, cay);
+                    if (fb) store_col(B, cby);
+                    if (fw) store_col(W, cwy);
+                }
             }
             // the rows as they are after that merge: row y is u; entry y of a
             // row R is U1[R]
-            double ca, cb = 0.0, cw = 0.0;
-            if (pend && i == y) {
-                ca = yA ? 0.0 : lw_update(method, xa, ya_, nx, ny, dvxy);
-                if (sp) cb = yB ? 0.0 : lw_update(method, xb, yb, nx, ny, dvxy);
-                if (hasW) cw = yW ? 0.0 : lw_update(method, xw, yw, nx, ny, dvxy);
-                // (the same bits as those lanes' u: the same operands and update)
-                if (fa) store_col(A, ca);
-                if (fb) store_col(B, cb);
-                if (fw) store_col(W, cw);
-            } else {
-                ca = yA ? u : da[k];
-                if (sp) cb = yB ? u : db[k];
-                if (hasW) cw = yW ? u : dw[k];
+            double ca = yA ? u : da[k];
+            double cb = sp ? (yB ? u : db[k]) : 0.0;
+            double cw = hasW ? (yW ? u : dw[k]) : 0.0;
+            if (pend) {
+                ca = isy ? cay : ca;
+                cb = isy ? cby : cb;
+                cw = isy ? cwy : cw;
             }
-            if (search && i != t && ca < bv) { bv = ca; bi = i; }          // P1: the top's row
+            // (a lane visits its entries in increasing i, so a candidate at i
+            // beats an earlier one only when strictly smaller -- except P3's
+            // entry for W, which carries index ys: there the full rule)
+            if (search) {                                                // P1: the top's row
+                const bool lt = live & (i != t) & (ca < bv);
+                bv = lt ? ca : bv;
+                bi = lt ? i : bi;
+            }
             if (sp) {
-                if (i != A && i != B) {
-                    // P2: the speculated merged row; P3: W's row after that merge
-                    const double U = lw_update(method, A < B ? ca : cb, A < B ? cb : ca, sxs, sys, dvs);
-                    if (better(U, i, yv, yi)) { yv = U; yi = i; }
-                    if (hasW) {
-                        if (i == W) {
-                            if (better(U, ys, wv, wi)) { wv = U; wi = ys; }
-                        } else if (better(cw, i, wv, wi)) {
-                            wv = cw; wi = i;
-                        }
-                    }
+                // P2: the speculated merged row; P3: W's row after that merge
+                const bool ok = live & (i != A) & (i != B);
+                const double U = lw_update(method, A < B ? ca : cb, A < B ? cb : ca, sxs, sys, dvs);
+                const bool y_lt = ok & (U < yv);
+                yv = y_lt ? U : yv;
+                yi = y_lt ? i : yi;
+                if (hasW) {
+                    const bool isW = i == W;
+                    const double cv = isW ? U : cw;
+                    const int32_t ci = isW ? ys : i;
+                    const bool w_lt = ok & ((cv < wv) | ((cv == wv) & (ci < wi)));
+                    wv = w_lt ? cv : wv;
+                    wi = w_lt ? ci : wi;
                 }
-            } else if (pend && i != y && better(u, i, yv, yi)) {   // P2: y's new row
-                yv = u; yi = i;
+            } else if (pend) {                                           // P2: y's new row
+                const bool lt = live & !isy & (u < yv);
+                yv = lt ? u : yv;
+                yi = lt ? i : yi;
             }
         }
     }
@@ -1308,7 +1338,9 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     };
     // done = the merges of the current epoch; at most half of the m rows
     // active: the compaction, then the steps for the new m
+    double compact_s = 0;                           // (host wall of the compactions, DREPHIP_DEBUG)
     auto compact = [&](int32_t done) -> int {
+        const double t0 = now_s();
         int rc;
         if (!d_sz2) {
             if ((rc = scratch(ctx, "lk_size2", (n + 1) * 4ull, (void **)&d_sz2))) return rc;
@@ -1352,6 +1384,7 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
         std::swap(d_sz, d_sz2);
         m = mn;
         cfg = nc;
+        compact_s += now_s() - t0;
         return DREPHIP_OK;
     };
     hipGraphExec_t exec = nullptr;
@@ -1390,9 +1423,9 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     const int32_t bad = (hs[0].flags | hs[1].flags) & kLkBad;
     ctx->link.launches = (uint64_t)std::max(hs[0].launches, hs[1].launches);
     if (getenv("DREPHIP_DEBUG"))
-        fprintf(stderr, "[drephip] chain: n=%u launches %llu (%.4f per merge), speculation %d, compactions %zu\n", n,
-                (unsigned long long)ctx->link.launches, (double)ctx->link.launches / (double)(n - 1), spec_on,
-                epochs.size());
+        fprintf(stderr, "[drephip] chain: n=%u launches %llu (%.4f per merge), speculation %d, compactions %zu (%.2f ms)\n",
+                n, (unsigned long long)ctx->link.launches, (double)ctx->link.launches / (double)(n - 1), spec_on,
+                epochs.size(), compact_s * 1e3);
 #if DREPHIP_LK_DIAG
     {
         LinkDiag hd;
