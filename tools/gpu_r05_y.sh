@@ -1,0 +1,12 @@
+#!/bin/bash
+# The whole GPU suite (writes gpurun_out/scale_*.json: configs[1..4] and the
+# dense set, Z against scipy's digests), then the 10^5 chain trace.
+set -o pipefail
+cd ${GRAFT_REPO_ROOT:-.}
+O=gpurun_out/r05y
+mkdir -p $O
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $O/gputest.txt 2>&1 \
+    || { tail -30 $O/gputest.txt; exit 1; }
+tail -3 $O/gputest.txt
+N=100000 bash tools/gpu_link_trace.sh > $O/trace_1e5.txt 2>&1 || { tail -20 $O/trace_1e5.txt; exit 1; }
+cat $O/trace_1e5.txt
