@@ -73,6 +73,11 @@ static double now_s() {
 }
 
 struct MinIdx { double v; int32_t i; };
+// a step workgroup's three partial minima (P1 the top's row, P2 the merged or
+// speculated merged row, P3 the speculated row below), one 48-byte record: one
+// base address for the three sets (their loads and stores take immediate offsets)
+struct PartRec { MinIdx p1, p2, p3; };
+static_assert(sizeof(PartRec) == 48, "PartRec layout");
 
 // Phase timestamps of the chain step (an A/B build only: make EXTRA=-DDREPHIP_LK_PHASES=1):
 // s_memrealtime (100 MHz) at fixed points of workgroup 0, the last step
@@ -223,14 +228,13 @@ __device__ MinIdx block_argmin(double v, int32_t i) {
 // A lane's share of the previous launch's partial sets: partials lane,
 // lane + 64, ... U at a time, every load in flight before the first wait
 template <int U>
-__device__ __forceinline__ void partial_pass(const MinIdx *P1, const MinIdx *P2, const MinIdx *P3, uint32_t G,
-                                             MinIdx &g, MinIdx &g2, MinIdx &g3) {
+__device__ __forceinline__ void partial_pass(const PartRec *P, uint32_t G, MinIdx &g, MinIdx &g2, MinIdx &g3) {
     for (uint32_t b0 = threadIdx.x; b0 < G; b0 += 64 * U) {
         MinIdx m1[U], m2[U], m3[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const uint32_t b = min(b0 + 64u * u, G - 1);             // (a repeated partial changes no minimum)
-            m1[u] = P1[b]; m2[u] = P2[b]; m3[u] = P3[b];
+            m1[u] = P[b].p1; m2[u] = P[b].p2; m3[u] = P[b].p3;
         }
 #pragma unroll
         for (int u = 0; u < U; u++)
@@ -422,8 +426,7 @@ template <int WG, int kLkPer, int method>
 __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t n,
                                                    int32_t *__restrict__ size, int32_t *__restrict__ chain,
                                                    LinkState *__restrict__ st, LinkFwd *__restrict__ fwd,
-                                                   MinIdx *__restrict__ parts, MinIdx *__restrict__ parts2,
-                                                   MinIdx *__restrict__ parts3, int32_t *__restrict__ done,
+                                                   PartRec *__restrict__ parts, int32_t *__restrict__ done,
                                                    double *__restrict__ Z, uint32_t q, int spec_on) {
     __shared__ LinkState sx;
     const uint32_t G = gridDim.x - 1;                          // step workgroups; workgroup G forwards operands
@@ -451,13 +454,12 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     const uint4 *fv = (const uint4 *)(fwd + (q ^ 1)) + lz0;
     uint4 sw0 = sv[0], sw1 = sv[1], sw2 = sv[2], sw3 = sv[3], fw0 = fv[0], fw1 = fv[1], fw2 = fv[2];
     if (wave0) {
-        const MinIdx *P1 = parts + (uint64_t)(q ^ 1) * kLkPartStride, *P2 = parts2 + (uint64_t)(q ^ 1) * kLkPartStride,
-                     *P3 = parts3 + (uint64_t)(q ^ 1) * kLkPartStride;
+        const PartRec *P = parts + (uint64_t)(q ^ 1) * kLkPartStride;
         // partials: one per step wave (DREPHIP_LK_WAVEPARTS) or per step workgroup
         const uint32_t NP = DREPHIP_LK_WAVEPARTS ? G * (WG / 64) : G;
-        if (NP <= 256) partial_pass<4>(P1, P2, P3, NP, g, g2, g3);
-        else if (!DREPHIP_LK_WAVEPARTS || NP <= 512) partial_pass<8>(P1, P2, P3, NP, g, g2, g3);   // (512 a pass)
-        else partial_pass<16>(P1, P2, P3, NP, g, g2, g3);           // (up to 1024 in one pass)
+        if (NP <= 256) partial_pass<4>(P, NP, g, g2, g3);
+        else if (!DREPHIP_LK_WAVEPARTS || NP <= 512) partial_pass<8>(P, NP, g, g2, g3);   // (512 a pass)
+        else partial_pass<16>(P, NP, g, g2, g3);                    // (up to 1024 in one pass)
     }
     asm volatile("" : "+v"(sw0.x), "+v"(sw0.y), "+v"(sw0.z), "+v"(sw0.w), "+v"(sw1.x), "+v"(sw1.y), "+v"(sw1.z),
                  "+v"(sw1.w), "+v"(sw2.x), "+v"(sw2.y), "+v"(sw2.z), "+v"(sw2.w), "+v"(sw3.x), "+v"(sw3.y),
@@ -880,9 +882,10 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     }
 #endif
     if (pwrite) {
-        if (search) parts[(uint64_t)q * kLkPartStride + pslot] = p1;
-        if (pend || sp) parts2[(uint64_t)q * kLkPartStride + pslot] = p2;
-        if (hasW) parts3[(uint64_t)q * kLkPartStride + pslot] = p3;
+        PartRec *pr = parts + (uint64_t)q * kLkPartStride + pslot;
+        if (search) pr->p1 = p1;
+        if (pend || sp) pr->p2 = p2;
+        if (hasW) pr->p3 = p3;
     }
 }
 
@@ -1005,29 +1008,29 @@ __global__ __launch_bounds__(kCmpWG) void k_lk_cmp_rank(const int32_t *__restric
 // minimum in slot 0 (the next launch's grid reads np_new slots), the rest
 // empty.  Indices outside [0, m) (-1, INT_MAX) are kept.
 __global__ __launch_bounds__(256) void k_lk_cmp_state(LinkState *__restrict__ st, LinkFwd *__restrict__ fwd,
-                                                      MinIdx *__restrict__ parts, MinIdx *__restrict__ parts2,
-                                                      MinIdx *__restrict__ parts3, int32_t *__restrict__ chain,
+                                                      PartRec *__restrict__ parts, int32_t *__restrict__ chain,
                                                       const uint32_t *__restrict__ rank, uint32_t m, uint32_t np_old,
                                                       uint32_t np_new, int32_t *__restrict__ size2,
                                                       int32_t *__restrict__ done) {
     const LinkState S = st[1];
     const uint32_t mn = rank[m];
     auto tr = [&](int32_t v) { return v >= 0 && (uint32_t)v < m ? (int32_t)rank[v] : v; };
-    MinIdx *P1 = parts + kLkPartStride, *P2 = parts2 + kLkPartStride, *P3 = parts3 + kLkPartStride;
+    PartRec *P = parts + kLkPartStride;
     MinIdx a{INFINITY, 0x7fffffff}, b = a, c = a;
     for (uint32_t s = threadIdx.x; s < np_old; s += 256) {
-        if (better(P1[s].v, P1[s].i, a.v, a.i)) a = P1[s];
-        if (better(P2[s].v, P2[s].i, b.v, b.i)) b = P2[s];
-        if (better(P3[s].v, P3[s].i, c.v, c.i)) c = P3[s];
+        const PartRec r = P[s];
+        if (better(r.p1.v, r.p1.i, a.v, a.i)) a = r.p1;
+        if (better(r.p2.v, r.p2.i, b.v, b.i)) b = r.p2;
+        if (better(r.p3.v, r.p3.i, c.v, c.i)) c = r.p3;
     }
     block_argmin3<256>(a, b, c, true, true);                   // (every slot read before the barrier in it)
     const MinIdx none{INFINITY, 0x7fffffff};
     for (uint32_t s = threadIdx.x; s < np_new; s += 256)
-        if (s) { P1[s] = none; P2[s] = none; P3[s] = none; }
+        if (s) P[s] = PartRec{none, none, none};
     for (int32_t p = threadIdx.x; p < S.len; p += 256) chain[p] = tr(chain[p]);
     __syncthreads();                                            // (every read of st[1] before its rewrite)
     if (threadIdx.x == 0) {
-        P1[0] = MinIdx{a.v, tr(a.i)}; P2[0] = MinIdx{b.v, tr(b.i)}; P3[0] = MinIdx{c.v, tr(c.i)};
+        P[0] = PartRec{MinIdx{a.v, tr(a.i)}, MinIdx{b.v, tr(b.i)}, MinIdx{c.v, tr(c.i)}};
         LinkState X = S;
         X.k = S.k - (int32_t)(m - mn);                          // 0: the new epoch's merges count from here
         X.top = tr(S.top); X.below = tr(S.below); X.first_active = tr(S.first_active); X.c3 = tr(S.c3);
@@ -1198,12 +1201,12 @@ static void launch_dist_tiles_condensed(const DmFromCondensed &v, uint32_t n, do
 // (sort_and_label: linkage_sparse.cpp, shared with the sparse path)
 struct NnArgs {
     double *D; uint32_t n; int32_t *size, *chain; LinkState *st; LinkFwd *fwd;
-    MinIdx *parts, *parts2, *parts3; int32_t *done; double *Z; uint32_t q; int spec_on;
+    PartRec *parts; int32_t *done; double *Z; uint32_t q; int spec_on;
 };
 template <int W, int P>
 static void launch_nn(int method, dim3 grid, dim3 blk, hipStream_t st, const NnArgs &a) {
 #define DREPHIP_LK_NN(M) hipLaunchKernelGGL((k_nn_step<W, P, M>), grid, blk, 0, st, a.D, a.n, a.size, a.chain, a.st, \
-                                            a.fwd, a.parts, a.parts2, a.parts3, a.done, a.Z, a.q, a.spec_on)
+                                            a.fwd, a.parts, a.done, a.Z, a.q, a.spec_on)
     if (method == DREPHIP_LINK_COMPLETE) DREPHIP_LK_NN(DREPHIP_LINK_COMPLETE);
     else if (method == DREPHIP_LINK_WEIGHTED) DREPHIP_LK_NN(DREPHIP_LINK_WEIGHTED);
     else DREPHIP_LK_NN(DREPHIP_LINK_AVERAGE);
@@ -1260,9 +1263,8 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     if ((rc = scratch(ctx, "lk_chain", n * 4ull, (void **)&d_chain))) return rc;
     if ((rc = scratch(ctx, "lk_Z", (n - 1) * 32ull, (void **)&d_Z))) return rc;
     if ((rc = scratch(ctx, "lk_parts", 2 * kLkPartStride * sizeof(MinIdx), (void **)&d_parts))) return rc;
-    MinIdx *d_parts2, *d_parts3;
-    if ((rc = scratch(ctx, "lk_parts2", 2 * kLkPartStride * sizeof(MinIdx), (void **)&d_parts2))) return rc;
-    if ((rc = scratch(ctx, "lk_parts3", 2 * kLkPartStride * sizeof(MinIdx), (void **)&d_parts3))) return rc;
+    PartRec *d_prec;                                 // the chain steps' partial records (d_parts: MST's)
+    if ((rc = scratch(ctx, "lk_prec", 2 * kLkPartStride * sizeof(PartRec), (void **)&d_prec))) return rc;
     // the speculation (A/B): 0 off; 1 the round-4 protocol (no known-merge
     // launches); 2 (default) with the known-merge speculation (spec 3)
     const char *spe = getenv("DREPHIP_LINK_SPEC");
@@ -1340,7 +1342,7 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
         for (int b = 0; b < kBatch; b++) {          // (even: step parity restarts at 0 with every replay)
             const uint32_t q = (uint32_t)(b & 1);
             const dim3 gm(grid), gn(grid + 1), blk(wg);
-            const NnArgs a{d_D, m, d_sz, d_chain, d_st, d_fwd, d_parts, d_parts2, d_parts3, d_done, Zc, q, spec_on};
+            const NnArgs a{d_D, m, d_sz, d_chain, d_st, d_fwd, d_prec, d_done, Zc, q, spec_on};
 #define DREPHIP_LK_LAUNCH(W, P)                                                                                      \
     do {                                                                                                         \
         if (mst) hipLaunchKernelGGL((k_mst_step<W, P>), gm, blk, 0, st, d_D, m, d_sz, d_Dmin, d_st, d_parts, d_done, \
@@ -1395,7 +1397,7 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
         }
         const StepCfg nc = cfg_for(mn);
         const uint32_t np_new = DREPHIP_LK_WAVEPARTS ? nc.grid * (nc.wg / 64) : nc.grid;
-        hipLaunchKernelGGL(k_lk_cmp_state, dim3(1), dim3(256), 0, st, d_st, d_fwd, d_parts, d_parts2, d_parts3, d_chain,
+        hipLaunchKernelGGL(k_lk_cmp_state, dim3(1), dim3(256), 0, st, d_st, d_fwd, d_prec, d_chain,
                            d_rank, m, np_old, np_new, d_sz2, d_done);
         auto rows = [&](const double *src, double *dst, uint32_t r0, uint32_t r1, uint32_t d0) {
             const uint64_t items = (uint64_t)(r1 - r0) * ((mn + 1023) / 1024);
