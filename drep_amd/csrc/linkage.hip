@@ -359,6 +359,15 @@ struct alignas(64) LinkFwd {
 static_assert(offsetof(LinkFwd, dp2) == 24 && offsetof(LinkFwd, spec) == 32 && offsetof(LinkFwd, c6) == 40,
               "LinkFwd word layout (fwd_from_words)");
 
+// the chain's control block: both parities of the state and of the forwarded
+// operands, and the merge count the host polls -- one base address (immediate
+// offsets) for the step kernel instead of three pointers in SGPRs
+struct alignas(64) LinkCtl {
+    LinkState st[2];
+    LinkFwd fwd[2];
+    int32_t done;
+};
+
 // a uniform 32-bit word held in a VGPR -> SGPR
 __device__ __forceinline__ int32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane((int32_t)v); }
 __device__ __forceinline__ MinIdx uni(MinIdx m) {       // a wave-uniform (value, index) into SGPRs
@@ -425,10 +434,12 @@ __device__ __forceinline__ MinIdx read_partials(const MinIdx *parts, uint32_t G)
 template <int WG, int kLkPer, int method>
 __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t n,
                                                    int32_t *__restrict__ size, int32_t *__restrict__ chain,
-                                                   LinkState *__restrict__ st, LinkFwd *__restrict__ fwd,
-                                                   PartRec *__restrict__ parts, int32_t *__restrict__ done,
+                                                   LinkCtl *__restrict__ ctl, PartRec *__restrict__ parts,
                                                    double *__restrict__ Z, uint32_t q, int spec_on) {
     __shared__ LinkState sx;
+    LinkState *const st = ctl->st;
+    LinkFwd *const fwd = ctl->fwd;
+    int32_t *const done = &ctl->done;
     const uint32_t G = gridDim.x - 1;                          // step workgroups; workgroup G forwards operands
     // The partial sets are reduced by wave 0 alone (the decision is wave 0's:
     // no barrier), read whether or not they are needed (valid memory either
@@ -1200,13 +1211,13 @@ static void launch_dist_tiles_condensed(const DmFromCondensed &v, uint32_t n, do
 // ------------------------------------------------------------- host driver
 // (sort_and_label: linkage_sparse.cpp, shared with the sparse path)
 struct NnArgs {
-    double *D; uint32_t n; int32_t *size, *chain; LinkState *st; LinkFwd *fwd;
-    PartRec *parts; int32_t *done; double *Z; uint32_t q; int spec_on;
+    double *D; uint32_t n; int32_t *size, *chain; LinkCtl *ctl;
+    PartRec *parts; double *Z; uint32_t q; int spec_on;
 };
 template <int W, int P>
 static void launch_nn(int method, dim3 grid, dim3 blk, hipStream_t st, const NnArgs &a) {
-#define DREPHIP_LK_NN(M) hipLaunchKernelGGL((k_nn_step<W, P, M>), grid, blk, 0, st, a.D, a.n, a.size, a.chain, a.st, \
-                                            a.fwd, a.parts, a.done, a.Z, a.q, a.spec_on)
+#define DREPHIP_LK_NN(M) hipLaunchKernelGGL((k_nn_step<W, P, M>), grid, blk, 0, st, a.D, a.n, a.size, a.chain, a.ctl, \
+                                            a.parts, a.Z, a.q, a.spec_on)
     if (method == DREPHIP_LINK_COMPLETE) DREPHIP_LK_NN(DREPHIP_LINK_COMPLETE);
     else if (method == DREPHIP_LINK_WEIGHTED) DREPHIP_LK_NN(DREPHIP_LINK_WEIGHTED);
     else DREPHIP_LK_NN(DREPHIP_LINK_AVERAGE);
@@ -1269,11 +1280,12 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
     // launches); 2 (default) with the known-merge speculation (spec 3)
     const char *spe = getenv("DREPHIP_LINK_SPEC");
     const int spec_on = spe ? std::max(0, std::min(2, atoi(spe))) : 2;
-    if ((rc = scratch(ctx, "lk_st", 2 * sizeof(LinkState), (void **)&d_st))) return rc;
-    LinkFwd *d_fwd;
-    if ((rc = scratch(ctx, "lk_fwd", 2 * sizeof(LinkFwd), (void **)&d_fwd))) return rc;
+    LinkCtl *d_ctl;
+    if ((rc = scratch(ctx, "lk_ctl", sizeof(LinkCtl), (void **)&d_ctl))) return rc;
+    d_st = d_ctl->st;                               // (device addresses inside the block)
+    LinkFwd *d_fwd = d_ctl->fwd;
+    d_done = &d_ctl->done;
     HIPC(hipMemsetAsync(d_fwd, 0, 2 * sizeof(LinkFwd), st));
-    if ((rc = scratch(ctx, "lk_done", 4, (void **)&d_done))) return rc;
     const bool mst = method == DREPHIP_LINK_SINGLE;
     if (mst && (rc = scratch(ctx, "lk_dmin", n * 8ull, (void **)&d_Dmin))) return rc;
     if (mst) {
@@ -1342,7 +1354,7 @@ int linkage_device_impl(drephip_ctx *ctx, double *d_D, uint32_t n, int method, d
         for (int b = 0; b < kBatch; b++) {          // (even: step parity restarts at 0 with every replay)
             const uint32_t q = (uint32_t)(b & 1);
             const dim3 gm(grid), gn(grid + 1), blk(wg);
-            const NnArgs a{d_D, m, d_sz, d_chain, d_st, d_fwd, d_prec, d_done, Zc, q, spec_on};
+            const NnArgs a{d_D, m, d_sz, d_chain, d_ctl, d_prec, Zc, q, spec_on};
 #define DREPHIP_LK_LAUNCH(W, P)                                                                                      \
     do {                                                                                                         \
         if (mst) hipLaunchKernelGGL((k_mst_step<W, P>), gm, blk, 0, st, d_D, m, d_sz, d_Dmin, d_st, d_parts, d_done, \
