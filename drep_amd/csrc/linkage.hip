@@ -52,9 +52,11 @@ constexpr int kLkWG = 256;
 #ifndef DREPHIP_LK_COLSTORE
 #define DREPHIP_LK_COLSTORE 3
 #endif
-// Row-y stores (contiguous, 8n bytes per merge): 1 plain (default), 3 write-through (A/B)
+// Row-y stores (contiguous, 8n bytes per merge): 3 write-through (default since round 5:
+// the row leaves L2 during the step instead of at the kernel boundary; chain at
+// 10^5 -0.8 %, profiles/r05_linkage_ab_stores.txt), 1 plain
 #ifndef DREPHIP_LK_ROWSTORE
-#define DREPHIP_LK_ROWSTORE 1
+#define DREPHIP_LK_ROWSTORE 3
 #endif
 constexpr uint32_t kLkSmallN = 30000;
 // Per-wave partials (round 5, A/B): each wave of a step workgroup stores its
