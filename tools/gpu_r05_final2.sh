@@ -3,7 +3,7 @@
 # (scale JSONs included), smoke(), then the 10^5 chain trace.
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-.}
-O=gpurun_out/r05final2
+O=gpurun_out/${OUT_DIR:-r05final2}
 mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > $O/gputest.txt 2>&1 \
     || { tail -30 $O/gputest.txt; exit 1; }
