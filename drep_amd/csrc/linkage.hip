@@ -692,7 +692,15 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     }
     if (blockIdx.x == G) return;                               // the forwarding workgroup has no step work
     __syncthreads();
-    const LinkState X = sx;
+    // the decision as wave-uniform scalars (an LDS read lands in VGPRs, which
+    // the compiler then treats as per-lane values: the pass's conditions became
+    // exec-mask branches and its row addresses per-lane 64-bit arithmetic)
+    LinkState X;
+    {
+        const uint4 *xv = (const uint4 *)&sx;
+        const uint4 a = xv[0], b = xv[1], c = xv[2], d = xv[3];
+        X = state_from_words(a, b, c, d);
+    }
     LK_T(ph3);
     if (X.k >= (int32_t)n - 1) return;
     // ---- this step: the pending update of row y fused with the search of row
