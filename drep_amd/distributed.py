@@ -197,8 +197,6 @@ def run_sharded(N: int, names: Sequence[str], s: int, sketch_fn: SketchFn, allpa
         left = int((full_c == POISON).sum().item())
         if left:
             raise RuntimeError("%d pairs of the condensed vector were never written" % left)
-    if full_c is not None and os.environ.get("DREPHIP_DUMP_COUNTS"):       # (debugging: the gathered counts)
-        np.save(os.environ["DREPHIP_DUMP_COUNTS"], full_c.cpu().numpy())
     full_d = None
     if partial:
         if seg_d is None:
@@ -311,11 +309,35 @@ def read_genome_list(bdb: Optional[str] = None, files: Optional[str] = None) -> 
     return [_get_genome_name_from_fasta(x) for x in locs], locs
 
 
+# uncompressed / compressed size of a gzip'd FASTA whose trailer does not tell
+# (bgzip / multi-member files): nucleotide text deflates about 3.5x
+GZIP_DNA_RATIO = 3.5
+
+
+def gzip_bases_estimate(path: str, size: int) -> float:
+    """Uncompressed size of a gzip file without inflating it.  The trailer's
+    ISIZE is the LAST member's size mod 2^32: exact for the usual
+    single-member file, but 0 for bgzip (BGZF ends with an empty member) and
+    too small for other multi-member files or files over 4 GiB.  A BGZF header
+    (FEXTRA with a 'BC' subfield), or an ISIZE below the compressed size
+    (nucleotide text always deflates), falls back to size x GZIP_DNA_RATIO;
+    the result is an estimate for balancing, never a length."""
+    with open(path, "rb") as f:
+        head = f.read(18)
+        f.seek(-4, os.SEEK_END)
+        isize = int.from_bytes(f.read(4), "little")
+    bgzf = len(head) >= 16 and head[:2] == b"\x1f\x8b" and head[3] & 4 and head[12:14] == b"BC"
+    if bgzf or isize < size:
+        return float(size) * GZIP_DNA_RATIO
+    return float(isize)
+
+
 def file_weights(locations: Sequence[str], cached: Optional[Dict[int, object]] = None) -> np.ndarray:
     """Sketch work per genome for balanced_shards: the FASTA's bases as far as
-    they are known without reading it -- the file size, or for a gzip file the
-    uncompressed size its trailer records (ISIZE: exact for the usual
-    single-member file) -- and 0 for a genome whose sketch is cached."""
+    they are known without reading it -- the file size, or for a gzip file
+    gzip_bases_estimate -- and 0 for a genome whose sketch is cached.  In a
+    sharded job only the root calls it and broadcasts the result
+    (main()): every rank's shard plan must come from the same weights."""
     cached = cached or {}
     w = np.zeros(len(locations), dtype=np.float64)
     for i, loc in enumerate(locations):
@@ -323,14 +345,9 @@ def file_weights(locations: Sequence[str], cached: Optional[Dict[int, object]] =
             continue
         try:
             size = os.path.getsize(loc)
-            if loc.endswith(".gz") and size >= 18:
-                with open(loc, "rb") as f:
-                    f.seek(-4, os.SEEK_END)
-                    isize = int.from_bytes(f.read(4), "little")
-                size = max(size, isize)
+            w[i] = gzip_bases_estimate(loc, size) if loc.endswith(".gz") and size >= 18 else size
         except OSError:
-            size = 0                     # unreadable: the sketch stage reports it
-        w[i] = size
+            w[i] = 0                     # unreadable: the sketch stage reports it
     return w
 
 
@@ -473,7 +490,13 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
         lengths = np.zeros(N, dtype=np.uint64)
         cached = cached_sketches(a.data_folder, names, a.sketch, a.group_size) if a.data_folder else {}
         sketch_fn = hip_file_sketcher(ctx, locations, a.processors, dev, cached, lengths)
-        weights = file_weights(locations, cached)
+        # the root's weights for every rank: a rank that saw another file size
+        # or another cached set would build another shard plan, and the
+        # gathered rows would land in the wrong genome order without an error
+        box = [file_weights(locations, cached) if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(box, src=0)
+        weights = box[0]
     else:
         N = a.genomes
         names = locations = synthetic_names(N)

@@ -36,19 +36,34 @@ def balanced_shards(weights: Sequence[float], world: int) -> List[np.ndarray]:
     least total so far (ties: the lowest rank), i.e. LPT list scheduling.
     Every rank's total is then within one genome's weight of every other's
     (the rank that ends heaviest was the lightest when it took its last
-    genome).  Returns each rank's genome indices, ascending.  The reference
-    fans the genomes out over a thread pool in Bdb order
-    (drep/d_cluster.py:527-549), where no balance is needed."""
+    genome).  Genomes of zero weight (cached sketches, unreadable files) cost
+    no sketch work but still a row of the all-gather, which pads every shard
+    to the largest: they go, after the others, each to the rank holding the
+    fewest genomes (ties in weight likewise go to the rank holding fewer), so
+    an all-cached rerun gets equal counts instead of every genome on rank 0.
+    Returns each rank's genome indices, ascending.  The reference fans the
+    genomes out over a thread pool in Bdb order (drep/d_cluster.py:527-549),
+    where no balance is needed."""
     import heapq
     w = np.asarray(weights, dtype=np.float64)
     order = np.argsort(-w, kind="stable")
-    heap = [(0.0, r) for r in range(world)]
+    heap = [(0.0, 0, r) for r in range(world)]
     heapq.heapify(heap)
     members: List[List[int]] = [[] for _ in range(world)]
+    zeros = []
     for g in order:
-        tot, r = heapq.heappop(heap)
+        if not w[g] > 0:
+            zeros.append(int(g))
+            continue
+        tot, cnt, r = heapq.heappop(heap)
         members[r].append(int(g))
-        heapq.heappush(heap, (tot + float(w[g]), r))
+        heapq.heappush(heap, (tot + float(w[g]), cnt + 1, r))
+    by_count = [(len(members[r]), r) for r in range(world)]
+    heapq.heapify(by_count)
+    for g in zeros:
+        cnt, r = heapq.heappop(by_count)
+        members[r].append(g)
+        heapq.heappush(by_count, (cnt + 1, r))
     return [np.sort(np.asarray(m, dtype=np.int64)) for m in members]
 
 

@@ -203,6 +203,22 @@ def test_balanced_shards_by_weight():
                 assert np.array_equal(pos[m], r * nmax + np.arange(len(m)))
 
 
+def test_balanced_shards_zero_weights_spread():
+    """A rerun with every sketch cached weighs every genome 0: the shards must
+    still be of near-equal count (the all-gather pads to the largest)."""
+    for N in (1, 7, 100, 1001):
+        for W in (1, 2, 3, 8):
+            sh = parallel.balanced_shards(np.zeros(N), W)
+            assert max(len(m) for m in sh) == -(-N // W)
+            nmax, _ = parallel.shard_layout(sh, N)
+            assert nmax == max(1, -(-N // W))
+            # mostly cached: the few real genomes balance, the rest fill up evenly
+            w = np.zeros(N)
+            w[: max(1, N // 50)] = 5e6
+            sh = parallel.balanced_shards(w, W)
+            assert max(len(m) for m in sh) - min(len(m) for m in sh) <= 1
+
+
 def _len_of(g):
     # genome lengths spread over 20x (5 kbp .. 100 kbp): a count split would be badly unbalanced
     return 5_000 + (g * 37_813) % 95_000
@@ -307,3 +323,34 @@ def test_file_weights(tmp_path):
     assert w[0] == os.path.getsize(a)
     assert w[1] == 50_000 + 4               # the gzip trailer's uncompressed size
     assert w[2] == 0 and w[3] == 0           # unreadable; cached
+
+
+def test_file_weights_multi_member_and_bgzf(tmp_path):
+    """The gzip trailer only holds the last member's size: a bgzip file (last
+    member empty, ISIZE 0) and a multi-member file whose last member is small
+    are estimated from the compressed size instead of being under-counted."""
+    import gzip
+    import random
+    import struct
+    import zlib
+    from drep_amd import distributed as D
+    rnd = random.Random(3)
+    seq = b">z\n" + bytes(rnd.choice(b"ACGT") for _ in range(200_000)) + b"\n"
+    multi = tmp_path / "m.fa.gz"
+    multi.write_bytes(gzip.compress(seq) + gzip.compress(b">t\nAC\n"))
+    size = os.path.getsize(multi)
+    assert D.file_weights([str(multi)])[0] == size * D.GZIP_DNA_RATIO
+
+    def bgzf_block(data):
+        co = zlib.compressobj(6, zlib.DEFLATED, -15)
+        cdata = co.compress(data) + co.flush()
+        bsize = 18 + len(cdata) + 8 - 1
+        hdr = b"\x1f\x8b\x08\x04" + b"\x00" * 4 + b"\x00\xff" + struct.pack("<H", 6) + b"BC" + struct.pack("<HH", 2, bsize)
+        return hdr + cdata + struct.pack("<II", zlib.crc32(data) & 0xFFFFFFFF, len(data))
+    bg = tmp_path / "b.fa.gz"
+    bg.write_bytes(bgzf_block(seq[:60_000]) + bgzf_block(seq[60_000:]) + bgzf_block(b""))
+    assert gzip.decompress(bg.read_bytes()) == seq
+    assert D.file_weights([str(bg)])[0] == os.path.getsize(bg) * D.GZIP_DNA_RATIO
+    single = tmp_path / "s.fa.gz"
+    single.write_bytes(gzip.compress(seq))
+    assert D.file_weights([str(single)])[0] == len(seq)
