@@ -81,6 +81,14 @@ SIGNATURES = {
     "drephip_linkage_counts_device": (C.c_int, [vp, vp, vp, C.c_uint32, u32p, f64p, C.c_uint32,
                                                 np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS"),
                                                 C.c_int, f64p, vp]),
+    "drephip_linkage_square": (C.c_int, [vp, np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS"),
+                                         C.c_uint32, C.c_int, f64p]),
+    "drephip_mdb_square": (C.c_int, [C.c_uint32, vp, vp, C.c_uint32, vp, C.c_uint32, vp, vp, C.c_int, vp, vp, vp,
+                                     vp, C.c_int]),
+    "drephip_pivot_scan": (C.c_int, [C.c_uint64, vp, vp, C.c_int, C.c_uint32, u8p, u8p, C.POINTER(C.c_uint64),
+                                     C.c_int]),
+    "drephip_pivot_fill": (C.c_int, [C.c_uint64, vp, vp, C.c_int, vp, vp, C.c_uint32, vp, C.c_uint32, C.c_uint32,
+                                     C.c_uint64, vp, C.c_int]),
     "drephip_linkage_reserve": (C.c_int, [vp, C.c_uint32]),
     "drephip_set_linkage_path": (C.c_int, [vp, C.c_int]),
     "drephip_linkage_sparse": (C.c_int, [C.c_uint32, C.c_uint64, u32p, u32p, f64p, C.c_int, f64p]),
@@ -230,6 +238,69 @@ def fasta_info(path: str, k: int = 21):
     return {"length": length.value, "padded": padded.value, "n_records": nrec.value, "n_kmers": nk.value}
 
 
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data
+
+
+def mdb_square(N: int, common: np.ndarray, denom: Optional[np.ndarray], s: int, lut32: np.ndarray,
+               lut_off: np.ndarray, codes: np.ndarray, threads: int = 0, want_sim: bool = True):
+    """drephip_mdb_square (host): the N^2-row Mdb columns from the condensed
+    counts -- (g1 codes, g2 codes, dist, similarity) in all_vs_all_MASH's row
+    order; codes' dtype (int8/16/32) is the category code width."""
+    common = np.ascontiguousarray(common, dtype=np.uint16)
+    den = None if denom is None else np.ascontiguousarray(denom, dtype=np.uint16)
+    lut32 = np.ascontiguousarray(lut32, dtype=np.float32)
+    lut_off = np.ascontiguousarray(lut_off, dtype=np.int32)
+    codes = np.ascontiguousarray(codes)
+    if codes.dtype not in (np.int8, np.int16, np.int32) or len(codes) != N or len(lut_off) != s + 1:
+        raise ValueError("codes must be N int8/int16/int32 category codes and lut_off s+1 offsets")
+    npairs = N * (N - 1) // 2
+    if len(common) != npairs or (den is not None and len(den) != npairs):
+        raise ValueError("condensed arrays must hold N(N-1)/2 = %d entries" % npairs)
+    codes32 = codes.astype(np.int32)
+    g1 = np.empty(N * N, dtype=codes.dtype)
+    g2 = np.empty(N * N, dtype=codes.dtype)
+    dist = np.empty(N * N, dtype=np.float32)
+    sim = np.empty(N * N, dtype=np.float32) if want_sim else None
+    check(lib().drephip_mdb_square(N, _ptr(common) if npairs else None, _ptr(den) if npairs else None, int(s),
+                                   _ptr(lut32), len(lut32), _ptr(lut_off), _ptr(codes32), codes.dtype.itemsize,
+                                   _ptr(g1), _ptr(g2), _ptr(dist), _ptr(sim), int(threads)), "drephip_mdb_square")
+    return g1, g2, dist, sim
+
+
+def pivot_scan(codes1: np.ndarray, codes2: np.ndarray, ncat: int, threads: int = 0):
+    """drephip_pivot_scan: (present1, present2, period) of two category-code
+    columns; raises DrepHipError(-5) on a missing (negative) code."""
+    codes1 = np.ascontiguousarray(codes1)
+    codes2 = np.ascontiguousarray(codes2)
+    if codes1.dtype != codes2.dtype or codes1.dtype not in (np.int8, np.int16, np.int32) or len(codes1) != len(codes2):
+        raise ValueError("codes1/codes2 must be equal-length int8/int16/int32 arrays")
+    p1 = np.zeros(max(ncat, 1), np.uint8)
+    p2 = np.zeros(max(ncat, 1), np.uint8)
+    period = C.c_uint64(0)
+    check(lib().drephip_pivot_scan(len(codes1), _ptr(codes1), _ptr(codes2), codes1.dtype.itemsize, int(ncat), p1, p2,
+                                   C.byref(period), int(threads)), "drephip_pivot_scan")
+    return p1[:ncat].astype(bool), p2[:ncat].astype(bool), int(period.value)
+
+
+def pivot_fill(codes1: np.ndarray, codes2: np.ndarray, pos1: np.ndarray, pos2: np.ndarray, vals: np.ndarray,
+               n1: int, n2: int, period: int = 0, threads: int = 0) -> np.ndarray:
+    """drephip_pivot_fill: the n1 x n2 float32 pivot of `vals`; raises
+    DrepHipError(-1, "Index contains duplicate entries...") like pandas."""
+    codes1 = np.ascontiguousarray(codes1)
+    codes2 = np.ascontiguousarray(codes2)
+    pos1 = np.ascontiguousarray(pos1, dtype=np.int32)
+    pos2 = np.ascontiguousarray(pos2, dtype=np.int32)
+    vals = np.ascontiguousarray(vals, dtype=np.float32)
+    if not (len(codes1) == len(codes2) == len(vals)) or len(pos1) != len(pos2):
+        raise ValueError("codes/vals lengths or pos lengths differ")
+    out = np.empty((n1, n2), dtype=np.float32)
+    check(lib().drephip_pivot_fill(len(vals), _ptr(codes1), _ptr(codes2), codes1.dtype.itemsize, _ptr(pos1), _ptr(pos2),
+                                   len(pos1), _ptr(vals), int(n1), int(n2), int(period), _ptr(out), int(threads)),
+          "drephip_pivot_fill")
+    return out
+
+
 # scipy linkage method codes (include/drephip.h DREPHIP_LINK_*)
 LINK_METHODS = {"single": 0, "complete": 1, "average": 2, "weighted": 6}
 
@@ -330,6 +401,20 @@ class Context:
         if n >= 2:
             check(lib().drephip_linkage(self._h, y, n, self.LINK_METHODS[method], Z.reshape(-1)),
                   "drephip_linkage")
+        return Z
+
+    def linkage_square(self, M: np.ndarray, method: str) -> np.ndarray:
+        """scipy.cluster.hierarchy.linkage(squareform(M), method) on the GPU,
+        bit-identical, with squareform's and linkage's checks (DrepHipError
+        carrying scipy's message when one fails); M: n x n float32."""
+        M = np.ascontiguousarray(M, dtype=np.float32)
+        if M.ndim != 2 or M.shape[0] != M.shape[1]:
+            raise ValueError("M must be a square matrix")
+        n = M.shape[0]
+        Z = np.zeros((max(n - 1, 0), 4), dtype=np.float64)
+        if n >= 2:
+            check(lib().drephip_linkage_square(self._h, M, n, self.LINK_METHODS[method], Z.reshape(-1)),
+                  "drephip_linkage_square")
         return Z
 
     def linkage_counts_device(self, d_common: int, d_denom: Optional[int], n: int, perm: np.ndarray,

@@ -961,6 +961,34 @@ DREPHIP_EXPORT int drephip_linkage(drephip_ctx *ctx, const double *y, uint32_t n
     return DREPHIP_OK;
 }
 
+DREPHIP_EXPORT int drephip_linkage_square(drephip_ctx *ctx, const float *M, uint32_t n, int method, double *Z) {
+    GUARD_CTX(ctx);
+    if (n < 2) return DREPHIP_OK;
+    if (!M || !Z) { set_error("null argument"); return DREPHIP_ERR_ARG; }
+    if (n > 200000) { set_error("linkage supports n <= 200000 (n x n f64 matrix in HBM)"); return DREPHIP_ERR_UNSUPPORTED; }
+    if (method != DREPHIP_LINK_SINGLE && method != DREPHIP_LINK_COMPLETE && method != DREPHIP_LINK_AVERAGE &&
+        method != DREPHIP_LINK_WEIGHTED) {
+        set_error("linkage method must be single, complete, average or weighted");
+        return DREPHIP_ERR_UNSUPPORTED;
+    }
+    timing_begin(ctx);
+    ctx->link = LinkStats{};
+    const auto t0 = std::chrono::steady_clock::now();
+    double *d_D;
+    uint32_t flags = 0;
+    int rc = dist_from_square_impl(ctx, M, n, &d_D, &flags, ctx->stream);
+    if (rc) return rc;
+    // scipy's order: squareform's symmetry check, its diagonal check, then linkage's finiteness check
+    if (flags & 1) { set_error("Distance matrix 'X' must be symmetric."); return DREPHIP_ERR_ARG; }
+    if (flags & 2) { set_error("Distance matrix 'X' diagonal must be zero."); return DREPHIP_ERR_ARG; }
+    if (flags & 4) { set_error("The condensed distance matrix must contain only finite values."); return DREPHIP_ERR_ARG; }
+    rc = linkage_device_impl(ctx, d_D, n, method, Z, ctx->stream);
+    if (rc) return rc;
+    timing_collect(ctx);
+    ctx->link.wall_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return DREPHIP_OK;
+}
+
 DREPHIP_EXPORT int drephip_linkage_counts_device(drephip_ctx *ctx, const uint16_t *d_common, const uint16_t *d_denom,
                                                  uint32_t n, const uint32_t *perm, const double *lut,
                                                  uint32_t lut_len, const int32_t *lut_off, int method, double *Z,

@@ -222,6 +222,10 @@ int dist_matrix_impl(drephip_ctx *ctx, const uint16_t *d_common, const uint16_t 
                      const uint32_t *perm, const double *lut, uint32_t lut_len, const int32_t *lut_off,
                      double **d_D_out, hipStream_t st);
 int dist_from_condensed_impl(drephip_ctx *ctx, const double *y, uint32_t n, double **d_D_out, hipStream_t st);
+// from a host n x n float32 matrix (the pivot's values); *flags: bit 0 not
+// symmetric, bit 1 a nonzero diagonal entry, bit 2 a non-finite value
+int dist_from_square_impl(drephip_ctx *ctx, const float *M, uint32_t n, double **d_D_out, uint32_t *flags,
+                          hipStream_t st);
 // pairs below 1.0 of the device counts (rows/columns through perm), as (perm i, perm j, lut index) in
 // pinned context buffers (*h_ij, *h_lidx; valid until the next call);
 // *np = their count (> cap: not written); *flags bit 0: a pair's denominator has no table or its count

@@ -1207,6 +1207,49 @@ __global__ __launch_bounds__(256) void k_dist_tiles(V val, uint32_t n, uint32_t 
     }
 }
 
+// The linkage input from the pivot's n x n float32 matrix M (host copy in
+// HBM), with squareform's and linkage's checks (d_cluster.py:445-453): tile
+// (bi <= bj) holds M's upper tile U = M[i0..][j0..] and its mirror
+// W = M[j0..][i0..]; U[r][c] must equal W[c][r] (==: NaN never does, +0 and
+// -0 do), the diagonal must be 0 and the upper triangle finite.  Both halves
+// of D take the upper value, as squareform keeps only X[i][j], i < j.
+// bad: bit 0 asymmetric, 1 diagonal, 2 non-finite.  HBM-bound: 4 B read and
+// 8 B written per cell.
+__global__ __launch_bounds__(256) void k_square_tiles(const float *__restrict__ M, uint32_t n, uint32_t nb,
+                                                      double *__restrict__ D, uint32_t *__restrict__ bad) {
+    __shared__ float U[kDmT][kDmT + 1], W[kDmT][kDmT + 1];
+    uint32_t bi, bj;
+    dm_tile(blockIdx.x, nb, bi, bj);
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t i0 = bi * kDmT, j0 = bj * kDmT;
+    for (uint32_t r = w; r < kDmT; r += 4) {
+        const uint32_t i = i0 + r, j = j0 + r, c = lane;
+        U[r][c] = i < n && j0 + c < n ? M[(uint64_t)i * n + j0 + c] : 0.0f;
+        W[r][c] = j < n && i0 + c < n ? M[(uint64_t)j * n + i0 + c] : 0.0f;
+    }
+    __syncthreads();
+    uint32_t flags = 0;
+    for (uint32_t r = w; r < kDmT; r += 4) {              // row i of the upper tile, column j = lane
+        const uint32_t i = i0 + r, j = j0 + lane;
+        if (i >= n || j >= n || j < i) continue;
+        const float a = U[r][lane], b = W[lane][r];       // M[i][j], M[j][i]
+        if (!(a == b)) flags |= 1;
+        if (j == i) {
+            if (!(a == 0.0f)) flags |= 2;
+            D[(uint64_t)i * n + i] = 0.0;
+        } else {
+            if (!isfinite(a)) flags |= 4;
+            D[(uint64_t)i * n + j] = (double)a;
+        }
+    }
+    for (uint32_t c = w; c < kDmT; c += 4) {              // the lower half: row j = j0 + c, column i = i0 + lane
+        const uint32_t j = j0 + c, i = i0 + lane;
+        if (j >= n || i >= n || j <= i) continue;
+        D[(uint64_t)j * n + i] = (double)U[lane][c];
+    }
+    if (flags) atomicOr(bad, flags);
+}
+
 static void launch_dist_tiles_counts(const DmFromCounts &v, uint32_t n, const uint32_t *perm, double *D, hipStream_t st) {
     const uint32_t nb = (n + kDmT - 1) / kDmT;
     hipLaunchKernelGGL((k_dist_tiles<DmFromCounts>), dim3((uint32_t)((uint64_t)nb * (nb + 1) / 2)), dim3(256), 0, st,
@@ -1592,6 +1635,35 @@ int dist_from_condensed_impl(drephip_ctx *ctx, const double *y, uint32_t n, doub
     timing_mark(ctx, 3, st, false);
     HIPC(hipGetLastError());
     HIPC(hipStreamSynchronize(st));
+    ctx->link.matrix_s = now_s() - t1;
+    *d_D_out = d_D;
+    return DREPHIP_OK;
+}
+
+int dist_from_square_impl(drephip_ctx *ctx, const float *M, uint32_t n, double **d_D_out, uint32_t *flags,
+                          hipStream_t st) {
+    double *d_D;
+    float *d_M;
+    uint32_t *d_bad, *h_bad;
+    int rc;
+    const double t0 = now_s();
+    if ((rc = scratch(ctx, "lk_D", (uint64_t)n * n * 8, (void **)&d_D))) return rc;
+    const double t1 = now_s();
+    ctx->link.alloc_s = t1 - t0;
+    if ((rc = scratch(ctx, "lk_sq", (uint64_t)n * n * 4, (void **)&d_M))) return rc;
+    if ((rc = scratch(ctx, "lk_bad", 4, (void **)&d_bad))) return rc;
+    if ((rc = pinned_host(ctx, "lk_bad", 4, (void **)&h_bad))) return rc;
+    HIPC(hipMemsetAsync(d_bad, 0, 4, st));
+    HIPC(hipMemcpyAsync(d_M, M, (uint64_t)n * n * 4, hipMemcpyHostToDevice, st));
+    timing_mark(ctx, 3, st, true);
+    const uint32_t nb = (n + kDmT - 1) / kDmT;
+    hipLaunchKernelGGL(k_square_tiles, dim3((uint32_t)((uint64_t)nb * (nb + 1) / 2)), dim3(256), 0, st, d_M, n, nb,
+                       d_D, d_bad);
+    timing_mark(ctx, 3, st, false);
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(h_bad, d_bad, 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    *flags = *h_bad;
     ctx->link.matrix_s = now_s() - t1;
     *d_D_out = d_D;
     return DREPHIP_OK;

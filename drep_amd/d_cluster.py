@@ -45,6 +45,24 @@ from .parallel import cond_start, row_partition, segment_size
 MASH_K = 21          # Mash default, never overridden by dRep (d_cluster.py:543)
 MASH_SEED = 42       # Mash default hash seed
 
+# host wall-clock seconds of the stages of the last all_vs_all_MASH /
+# cluster_mash_database call in this process (tools/dropin_bench.py reports
+# them; nothing reads them on the product path)
+STAGE_TIMES: Dict[str, float] = {}
+
+
+class _Stage:
+    def __init__(self, name: str):
+        self.name = name
+
+    def __enter__(self):
+        import time
+        self.t0 = time.perf_counter()
+
+    def __exit__(self, *a):
+        import time
+        STAGE_TIMES[self.name] = time.perf_counter() - self.t0
+
 
 # --------------------------------------------------------------- genomes
 def _get_genome_name_from_fasta(fasta):
@@ -82,36 +100,61 @@ def mash_distance_float32(common: np.ndarray, denom: np.ndarray, k: int = MASH_K
     return out
 
 
-def _square(vec: np.ndarray, N: int, diag: np.ndarray) -> np.ndarray:
-    M = np.zeros((N, N), dtype=vec.dtype)
-    iu = np.triu_indices(N, 1)
-    M[iu] = vec
-    M = M + M.T
-    M[np.arange(N), np.arange(N)] = diag
-    return M
+def float32_tables(denominators, s: int, k: int = MASH_K):
+    """(lut32, lut_off) for every denominator d that occurs: lut32[lut_off[d] +
+    c] = the float32 "dist" of (common c, denominator d) as the reference
+    parses it (mash_distance_float32); lut_off has s + 1 entries, -1 where d
+    does not occur."""
+    lut_off = np.full(s + 1, -1, dtype=np.int32)
+    parts, pos = [], 0
+    for d in np.asarray(denominators, dtype=np.int64):
+        d = int(d)
+        c = np.arange(d + 1, dtype=np.uint16)
+        parts.append(mash_distance_float32(c, np.full(d + 1, d, dtype=np.uint16), k))
+        lut_off[d] = pos
+        pos += d + 1
+    lut32 = np.concatenate(parts).astype(np.float32) if parts else np.zeros(1, np.float32)
+    return lut32, lut_off
+
+
+def _denominators(denom: np.ndarray, s: int):
+    """(distinct denominators, whether every pair has denominator s) without
+    sorting the condensed vector (5x10^7 entries at 10^4 genomes)."""
+    denom = np.asarray(denom)
+    if denom.size == 0 or (denom == s).all():
+        return np.array([s]), True
+    seen = np.bincount(denom.astype(np.int64, copy=False), minlength=s + 1) > 0
+    return np.nonzero(seen)[0], False
 
 
 def mdb_from_condensed(names: Sequence[str], common: np.ndarray, denom: np.ndarray,
-                       nhash: np.ndarray, s: int, k: int = MASH_K) -> pd.DataFrame:
+                       nhash: np.ndarray, s: int, k: int = MASH_K, threads: int = 0) -> pd.DataFrame:
     """Long-form Mdb (genome1, genome2, dist, similarity) from the condensed
     all-pairs result, with the reference's row order (outer loop = query =
     genome2, inner = reference = genome1, as `mash dist` prints), dtypes
     (ordered categoricals sorted by name; float32) and values
-    (d_cluster.py:575-596)."""
+    (d_cluster.py:575-596).
+
+    The N^2 rows are filled by libdrephip on host threads
+    (drephip_mdb_square): the float32 distances from one table per
+    denominator (the reference's %g / read_csv values, float32_tables), the
+    diagonal 0 -- a genome against itself has common = denom = its hash count
+    (or 0 for an empty sketch), distance 0 either way --, similarity = 1 - dist
+    in float32, and the category codes of both columns; the DataFrame wraps
+    those arrays without copying them."""
     N = len(names)
-    # distances of the N(N-1)/2 pairs, then the symmetric square (row q, col r);
-    # a genome against itself has common = denom = its hash count (or 0 for an
-    # empty sketch), distance 0 either way, so the diagonal is 0
-    dist = ssd.squareform(mash_distance_float32(np.asarray(common, dtype=np.uint16),
-                                            np.asarray(denom, dtype=np.uint16), k), checks=False).reshape(-1)
+    common = np.asarray(common, dtype=np.uint16)
+    dens, full = _denominators(np.asarray(denom, dtype=np.uint16), s)
+    lut32, lut_off = float32_tables(dens, s, k)
     cats = sorted(set(names))
+    dtype = pd.CategoricalDtype(cats, ordered=True)
+    code_t = pd.Categorical([], dtype=dtype).codes.dtype        # pandas' code width for len(cats)
     pos = {n: i for i, n in enumerate(cats)}
-    codes = np.array([pos[n] for n in names], dtype=np.int32)
-    g1 = pd.Categorical.from_codes(np.tile(codes, N), categories=cats, ordered=True)
-    g2 = pd.Categorical.from_codes(np.repeat(codes, N), categories=cats, ordered=True)
-    Mdb = pd.DataFrame({'genome1': g1, 'genome2': g2, 'dist': dist})
-    Mdb['similarity'] = 1 - Mdb['dist']
-    return Mdb
+    codes = np.array([pos[n] for n in names], dtype=code_t)
+    g1, g2, dist, sim = _lib.mdb_square(N, common, None if full else denom, s, lut32, lut_off, codes, threads)
+    return pd.DataFrame({'genome1': pd.Categorical.from_codes(g1, dtype=dtype, validate=False),
+                         'genome2': pd.Categorical.from_codes(g2, dtype=dtype, validate=False),
+                         'dist': dist, 'similarity': sim}, copy=False)
 
 
 # ---------------------------------------------------------- devices
@@ -196,6 +239,8 @@ def sketch_genomes(Bdb: pd.DataFrame, data_folder: str, **kwargs) -> SketchSet:
     todo: List[int] = []
     idx = 0
     chunk_members: List[List[int]] = []
+    cache = _Stage('sketch_cache_s')
+    cache.__enter__()
     for i, chunk in enumerate(chunks):
         chunk_folder = os.path.join(sketch_folder, "chunk_{0}".format(i))
         os.makedirs(chunk_folder, exist_ok=True)
@@ -214,7 +259,11 @@ def sketch_genomes(Bdb: pd.DataFrame, data_folder: str, **kwargs) -> SketchSet:
             members.append(idx)
             idx += 1
         chunk_members.append(members)
+    cache.__exit__()
+    STAGE_TIMES['sketched_genomes'] = len(todo)
 
+    sk = _Stage('sketch_gpu_s')
+    sk.__enter__()
     if todo:
         devs = _devices(kwargs)
         sizes = [os.path.getsize(locations[i]) if os.path.exists(locations[i]) else 1 for i in todo]
@@ -231,7 +280,10 @@ def sketch_genomes(Bdb: pd.DataFrame, data_folder: str, **kwargs) -> SketchSet:
             length[shards[k]] = ln
         _on_devices(devs, run)
         logging.debug("sketched %d genomes on HIP devices %s", len(todo), devs)
+    sk.__exit__()
 
+    wr = _Stage('sketch_write_s')
+    wr.__enter__()
     if write_sketches:
         def ref_of(i):
             return MashReference(locations[i], '', int(length[i]), hashes[i, :nhash[i]])
@@ -244,6 +296,7 @@ def sketch_genomes(Bdb: pd.DataFrame, data_folder: str, **kwargs) -> SketchSet:
             alls.append(all_file)
         write_msh(os.path.join(MASH_folder, 'ALL.msh'), [ref_of(i) for i in range(N)],
                   MASH_K, MASH_s, MASH_SEED)
+    wr.__exit__()
     return SketchSet(names, locations, hashes, nhash, length, MASH_s)
 
 
@@ -262,7 +315,8 @@ def all_vs_all_MASH_condensed(Bdb, data_folder, **kwargs) -> CondensedMash:
     """Sketch (or load cached sketches) and run the HIP all-pairs kernel;
     return the condensed shared-hash counts instead of an N^2-row table."""
     sk = sketch_genomes(Bdb, data_folder, **kwargs)
-    common, denom = condensed_allpairs(sk.hashes, sk.nhash, sk.s, _devices(kwargs))
+    with _Stage('allpairs_s'):
+        common, denom = condensed_allpairs(sk.hashes, sk.nhash, sk.s, _devices(kwargs))
     return CondensedMash(sk.names, sk.locations, common, denom, sk.nhash, sk.length, sk.s)
 
 
@@ -328,10 +382,14 @@ def all_vs_all_MASH(Bdb, data_folder, **kwargs):
               % (len(Bdb), kwargs.get('gpu', os.environ.get('DREPHIP_DEVICE', 0))))
         return _parse_mash_table(table, Bdb)
 
+    STAGE_TIMES.clear()
     cm = all_vs_all_MASH_condensed(Bdb, data_folder, **kwargs)
     if kwargs.get('write_table', False):
-        write_mash_table(MASH_folder + 'MASH_table.tsv', cm)
-    Mdb = mdb_from_condensed(cm.names, cm.common, cm.denom, cm.nhash, cm.s)
+        with _Stage('mash_table_s'):
+            write_mash_table(MASH_folder + 'MASH_table.tsv', cm)
+    with _Stage('mdb_s'):
+        Mdb = mdb_from_condensed(cm.names, cm.common, cm.denom, cm.nhash, cm.s,
+                                 threads=int(kwargs.get('processors', 6)))
 
     # Filter out those genomes that are not in Bdb (reference 586-594).  When
     # every sketched genome is in Bdb (the drop-in sketches Bdb's own genomes)
@@ -434,18 +492,94 @@ def _primary_cdb(labels, names) -> pd.DataFrame:
     return pd.DataFrame({'primary_cluster': np.asarray(labels), 'genome': list(names)})
 
 
+def _pivot_dist(db: pd.DataFrame) -> pd.DataFrame:
+    """db.pivot(index="genome1", columns="genome2", values="dist")
+    (d_cluster.py:620; keyword form -- pandas >= 2 rejects the positional one),
+    the same DataFrame, filled by libdrephip on category codes
+    (drephip_pivot_scan / drephip_pivot_fill) when the table is what the
+    Mash step produces: both genome columns categorical over one sorted list
+    of names (the reference's parse sorts them, d_cluster.py:591-594) and a
+    float32 dist.  Index and columns are then the names that occur, in
+    category order, as CategoricalIndex of the column's dtype (pandas' pivot of
+    a categorical); missing cells NaN; a cell named twice raises pandas'
+    ValueError.  Any other table goes through pandas itself."""
+    g1, g2, dist = db['genome1'], db['genome2'], db['dist']
+    fast = (isinstance(g1.dtype, pd.CategoricalDtype) and isinstance(g2.dtype, pd.CategoricalDtype)
+            and g1.dtype.categories.equals(g2.dtype.categories) and g1.dtype.ordered == g2.dtype.ordered
+            and g1.dtype.categories.is_monotonic_increasing and dist.dtype == np.float32 and len(db) > 0)
+    if fast:
+        c1 = g1.cat.codes.to_numpy()
+        c2 = g2.cat.codes.to_numpy()
+        fast = c1.dtype == c2.dtype and c1.dtype in (np.int8, np.int16, np.int32)
+    if not fast:
+        return db.pivot(index="genome1", columns="genome2", values="dist")
+    ncat = len(g1.dtype.categories)
+    try:
+        p1, p2, period = _lib.pivot_scan(c1, c2, ncat)
+    except _lib.DrepHipError:                   # a missing genome (NaN category): pandas' own handling
+        return db.pivot(index="genome1", columns="genome2", values="dist")
+    if not (p1.all() and p2.all()):
+        # a category unused in either column: pandas' unstack then orders the
+        # names in a way of its own (not the category order) -- leave it to pandas
+        return db.pivot(index="genome1", columns="genome2", values="dist")
+    pos1 = np.where(p1, np.cumsum(p1) - 1, -1).astype(np.int32)
+    pos2 = np.where(p2, np.cumsum(p2) - 1, -1).astype(np.int32)
+    n1, n2 = int(p1.sum()), int(p2.sum())
+    try:
+        M = _lib.pivot_fill(c1, c2, pos1, pos2, dist.to_numpy(), n1, n2, period)
+    except _lib.DrepHipError as e:
+        raise ValueError("Index contains duplicate entries, cannot reshape") from e
+
+    def index(present, name, dtype):
+        return pd.CategoricalIndex(pd.Categorical.from_codes(np.nonzero(present)[0], dtype=dtype), name=name)
+    return pd.DataFrame(M, index=index(p1, "genome1", g1.dtype), columns=index(p2, "genome2", g2.dtype), copy=False)
+
+
+def _linkage_gpu(kwargs) -> Optional[int]:
+    """The HIP device of the primary linkage: kwargs `gpu` (None = scipy on
+    the host), else $DREPHIP_DEVICE, else 0."""
+    if 'gpu' in kwargs:
+        return None if kwargs['gpu'] is None else int(kwargs['gpu'])
+    return int(os.environ.get('DREPHIP_DEVICE', 0))
+
+
+def _square_linkage(M: np.ndarray, method: str, gpu: int) -> np.ndarray:
+    """scipy.cluster.hierarchy.linkage(squareform(M), method) on the GPU (Z
+    bit-identical): float32 M through drephip_linkage_square (squareform's and
+    linkage's checks on the device), float64 M through squareform +
+    drephip_linkage.  A failed check raises scipy's ValueError."""
+    with _lib.Context(device=gpu, k=MASH_K, s=1, seed=MASH_SEED) as ctx:
+        if M.dtype == np.float32:
+            try:
+                return ctx.linkage_square(M, method)
+            except _lib.DrepHipError as e:
+                msg = _lib.lib().drephip_last_error().decode("utf-8", "replace")
+                if msg in ("Distance matrix 'X' must be symmetric.", "Distance matrix 'X' diagonal must be zero.",
+                           "The condensed distance matrix must contain only finite values."):
+                    raise ValueError(msg) from e
+                raise
+        y = ssd.squareform(np.asarray(M, dtype=np.float64))
+        if not np.all(np.isfinite(y)):
+            raise ValueError("The condensed distance matrix must contain only finite values.")
+        return ctx.linkage(y, method)
+
+
 def cluster_mash_database(db, **kwargs):
     """
     From a Mash database, cluster and return Cdb (reference
     drep/d_cluster.py:598-630, with its cluster_hierarchical 429-461).  Same
     in-place update of db['dist'] from db['similarity'] as the reference, the
-    same pivot (with keywords: pandas >= 2 rejects the positional form) and
-    the same scipy calls on the pivot's squareform, so Cdb and linkage equal
-    the reference's.
+    same pivot (pandas' DataFrame, filled from the category codes by
+    libdrephip: _pivot_dist) and the same linkage of its squareform -- run on
+    the GPU for single / complete / average / weighted (scipy's algorithms
+    restated, Z bit-identical; drephip_linkage_square), by scipy for the other
+    methods -- so Cdb, linkage and linkage_db equal the reference's.
 
     Keyword arguments:
         clusterAlg: how to cluster database (default = single)
         P_ani: threshold to cluster at (default = 0.9)
+        gpu: HIP device of the linkage (default $DREPHIP_DEVICE or 0); None
+            runs scipy's linkage on the host, as the reference does
 
     Returns:
         list: [Cdb, [linkage, linkage_db, arguments]]
@@ -453,14 +587,26 @@ def cluster_mash_database(db, **kwargs):
     logging.debug('Clustering MASH database')
     method = kwargs.get('clusterAlg', 'single')
     cutoff = 1 - kwargs.get('P_ani', .9)
-    db['dist'] = 1 - db['similarity']
-    linkage_db = db.pivot(index="genome1", columns="genome2", values="dist")
+    with _Stage('dist_update_s'):
+        db['dist'] = 1 - db['similarity']
+    with _Stage('pivot_s'):
+        linkage_db = _pivot_dist(db)
+    gpu = _linkage_gpu(kwargs)
+    M = np.asarray(linkage_db)
+    link = _Stage('linkage_s')
+    link.__enter__()
     try:
-        y = ssd.squareform(np.asarray(linkage_db))       # raises unless symmetric with a zero diagonal
-    except ValueError:
-        logging.error("The database passed in is not symmetrical!")
+        if (gpu is not None and method in GPU_LINKAGE_METHODS and M.ndim == 2 and M.shape[0] == M.shape[1]
+                and M.shape[0] >= 2 and M.dtype in (np.float32, np.float64)):
+            linkage = _square_linkage(M, method, gpu)
+        else:
+            y = ssd.squareform(M)       # raises unless symmetric with a zero diagonal
+            linkage = scipy.cluster.hierarchy.linkage(y, method=method)
+    except ValueError as e:
+        if "symmetric" in str(e) or "diagonal" in str(e) or "square" in str(e):    # squareform's checks
+            logging.error("The database passed in is not symmetrical!")
         raise
-    linkage = scipy.cluster.hierarchy.linkage(y, method=method)
+    link.__exit__()
     labels = scipy.cluster.hierarchy.fcluster(linkage, cutoff, criterion='distance')
     Cdb = _primary_cdb(labels, linkage_db.columns)
     arguments = {'linkage_method': method, 'linkage_cutoff': cutoff, 'comparison_algorithm': 'MASH'}
@@ -519,13 +665,13 @@ def cluster_mash_condensed(cm: CondensedMash, **kwargs):
     """Primary clustering straight from the condensed result (no N^2 Mdb):
     same linkage input as cluster_mash_database builds via pivot+squareform.
 
-    gpu=<device> runs the linkage itself on the GPU (libdrephip
-    drephip_linkage_counts_device: scipy's nn_chain / MST restated, Z
-    bit-identical; the n x n matrix is built in HBM from the counts); other
-    methods, or gpu=None, use scipy on the host."""
+    The linkage runs on the GPU (libdrephip drephip_linkage_counts_device:
+    scipy's nn_chain / MST restated, Z bit-identical; the n x n matrix is
+    built in HBM from the counts) on device `gpu` (default $DREPHIP_DEVICE or
+    0); other methods, or gpu=None, use scipy on the host."""
     P_Lmethod = kwargs.get('clusterAlg', 'single')
     P_Lcutoff = 1 - kwargs.get('P_ani', .9)
-    gpu = kwargs.get('gpu', None)
+    gpu = _linkage_gpu(kwargs)
     names = sorted(cm.names)
     N = len(cm.names)
     if gpu is not None and P_Lmethod in GPU_LINKAGE_METHODS and N >= 2:

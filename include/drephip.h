@@ -320,6 +320,55 @@ int drephip_linkage_counts_device(drephip_ctx *ctx, const uint16_t *d_common, co
                                   uint32_t n, const uint32_t *perm, const double *lut, uint32_t lut_len,
                                   const int32_t *lut_off, int method, double *Z /* (n-1)*4 */, void *stream);
 
+/* From the host n x n float32 matrix the reference's pivot produces
+ * (cluster_mash_database, drep/d_cluster.py:619-621: db.pivot(genome1,
+ * genome2, dist) -> cluster_hierarchical's squareform -> linkage, 445-453):
+ * Z = scipy.cluster.hierarchy.linkage(squareform(M), method).  The matrix is
+ * copied to the device, where squareform's checks run (M == M^T element by
+ * element, a zero diagonal) and linkage's (finite values), and the f64 linkage
+ * input is built from the upper triangle, as squareform takes it.  A failed
+ * check fails the call with DREPHIP_ERR_ARG and scipy's message ("Distance
+ * matrix 'X' must be symmetric.", "Distance matrix 'X' diagonal must be
+ * zero.", "The condensed distance matrix must contain only finite values.").  Dense path;
+ * blocking. */
+int drephip_linkage_square(drephip_ctx *ctx, const float *M, uint32_t n, int method, double *Z /* (n-1)*4 */);
+
+/* ------------------------------------------------------------ Mdb on the host
+ * The N^2-row Mdb table all_vs_all_MASH returns (drep/d_cluster.py:575-596),
+ * filled from the condensed all-pairs result without the reference's text
+ * round trip: row t = q N + r is (genome1 = genome r, genome2 = genome q) --
+ * `mash dist` prints the query as the outer loop -- with
+ *   dist[t] = 0 for r == q, else lut32[lut_off[denom] + common] of the pair
+ *            (the float32 values the reference's read_csv parses from Mash's
+ *            %g text, one table per denominator; denom NULL = s for every pair),
+ *   sim[t]  = 1.0f - dist[t] (d_cluster.py:584, IEEE float32),
+ *   g1[t] = codes[r], g2[t] = codes[q] (category codes, code_bytes 1, 2 or 4).
+ * A pair whose denominator has no table, or whose count exceeds it, fails the
+ * call (DREPHIP_ERR_ARG).  sim, g1, g2 nullable.  Host threads (0 = all). */
+int drephip_mdb_square(uint32_t N, const uint16_t *common, const uint16_t *denom /* nullable */, uint32_t s,
+                       const float *lut32, uint32_t lut_len, const int32_t *lut_off /* s+1 */,
+                       const int32_t *codes /* N */, int code_bytes, void *g1, void *g2, float *dist,
+                       float *sim, int threads);
+
+/* The pivot of cluster_mash_database (d_cluster.py:620,
+ * db.pivot(index="genome1", columns="genome2", values="dist")) on category
+ * codes.  drephip_pivot_scan: which of the ncat categories occur in each
+ * column (present1/present2), and *period = n when the rows have the layout
+ * all_vs_all_MASH returns (codes1 repeating with period n, codes2 constant on
+ * each block of n rows), else 0.  A negative code (a missing value) fails with
+ * DREPHIP_ERR_UNSUPPORTED (the caller pivots with pandas).
+ * drephip_pivot_fill: out[pos1[c1] * n2 + pos2[c2]] = vals of every row
+ * (pos: the category's row/column of the pivot, -1 if absent); cells no row
+ * names are NaN; two rows naming one cell fail with DREPHIP_ERR_ARG ("Index
+ * contains duplicate entries, cannot reshape", pandas' error).  A period from
+ * the scan (with n == n1 and nrows == n1 n2) takes the blocked transpose
+ * instead of the scatter.  Host threads (0 = all). */
+int drephip_pivot_scan(uint64_t nrows, const void *codes1, const void *codes2, int code_bytes, uint32_t ncat,
+                       uint8_t *present1, uint8_t *present2, uint64_t *period, int threads);
+int drephip_pivot_fill(uint64_t nrows, const void *codes1, const void *codes2, int code_bytes, const int32_t *pos1,
+                       const int32_t *pos2, uint32_t ncat, const float *vals, uint32_t n1, uint32_t n2,
+                       uint64_t period, float *out, int threads);
+
 /* The sparse path on its own, no context or GPU: the npairs pairs (i[t], j[t])
  * with distance v[t] in [0, 1), each unordered pair at most once; every pair
  * not listed is at 1.0.  Z as scipy.cluster.hierarchy.linkage(squareform(D),

@@ -703,12 +703,108 @@ def test_all_vs_all_MASH_dropin_reproduces_reference(golden, tmp_path, gpus):
     assert len(glob.glob(str(wd / "MASH_files" / "sketches" / "*"))) == 1
     assert len(glob.glob(str(wd / "MASH_files" / "sketches" / "*" / "*"))) == 6
     for alg in ("average", "single"):
-        Cdb, ret = d_cluster.cluster_mash_database(Mdb.copy(), clusterAlg=alg, P_ani=0.9)
+        mdb = Mdb.copy()
+        Cdb, ret = d_cluster.cluster_mash_database(mdb, clusterAlg=alg, P_ani=0.9)      # GPU linkage
         exp_c = pd.read_csv(os.path.join(golden, "ref", "cdb_%s.csv" % alg))
         assert Cdb.to_dict("list") == exp_c.to_dict("list")
+        ref = Mdb.copy()
+        ref["dist"] = 1 - ref["similarity"]
+        pd.testing.assert_frame_equal(ret[1], ref.pivot(index="genome1", columns="genome2", values="dist"),
+                                      check_exact=True)
+        assert list(mdb["dist"].to_numpy().view(np.uint32)) == link_bits_after(golden, alg)
         link = json.load(open(os.path.join(golden, "ref", "linkage_%s.json" % alg)))
         got = [[float(v).hex() for v in row] for row in ret[0]]
         assert got == link["linkage"]
+
+
+def link_bits_after(golden, alg):
+    import json
+    return json.load(open(os.path.join(golden, "ref", "linkage_%s.json" % alg)))["dist_bits_after"]
+
+
+def _device_synth_sketches(N, L, fam, seed, s=S):
+    """Sketches of the bench's synthetic genomes (on-device generator + the
+    product sketch kernel; the generator and kernel are oracle-pinned above)."""
+    import torch
+    tile = _lib.tile_bases()
+    P = _lib.padded_bases([L])
+    with _lib.Context(0, 21, s, 42) as ctx:
+        st = torch.cuda.current_stream().cuda_stream
+        codes = torch.zeros((tile + N * P) // 16, dtype=torch.int32, device="cuda")
+        valid = torch.zeros((tile + N * P) // 32, dtype=torch.int32, device="cuda")
+        ctx.synth_device(seed, 0, N, fam, L, codes.data_ptr(), valid.data_ptr(), st)
+        hh = torch.zeros((N, s), dtype=torch.int64, device="cuda")
+        nn = torch.zeros(N, dtype=torch.int32, device="cuda")
+        ctx.sketch_device(codes.data_ptr(), valid.data_ptr(), np.array([tile + i * P for i in range(N)], np.uint64),
+                          np.full(N, P, np.uint64), np.full(N, L - 20, np.uint64), N, hh.data_ptr(), nn.data_ptr(), st)
+        torch.cuda.synchronize()
+    return hh.cpu().numpy().view(np.uint64), nn.cpu().numpy().view(np.uint32)
+
+
+@pytest.mark.parametrize("method", ["average", "single", "complete", "weighted"])
+def test_cluster_mash_database_gpu_equals_reference_steps(method):
+    """dRep's own entry point on the GPU: cluster_mash_database (native pivot,
+    drephip_linkage_square) on the Mdb all_vs_all_MASH builds for 10^3
+    synthetic genomes (shuffled names) equals the reference's steps run
+    literally -- in-place dist update, pandas pivot, squareform, scipy linkage,
+    fcluster (d_cluster.py:445-459, 619-623): linkage_db, Z, Cdb and the
+    updated dist column bit for bit."""
+    import scipy.cluster.hierarchy as sch
+    import scipy.spatial.distance as ssd
+    from drep_amd import d_cluster
+    N = 1000
+    h, nh = _device_synth_sketches(N, 200_000, 25, 0xD2E9 + 3)
+    with _lib.Context(0, 21, S, 42) as ctx:
+        c, d = ctx.allpairs(h, nh)
+    names = ["g%05d.fna" % i for i in np.random.default_rng(4).permutation(N)]
+    Mdb = d_cluster.mdb_from_condensed(names, c, d, nh, S)
+    ref = Mdb.copy()
+    ref["dist"] = 1 - ref["similarity"]
+    lp = ref.pivot(index="genome1", columns="genome2", values="dist")
+    Z = sch.linkage(ssd.squareform(np.asarray(lp)), method=method)
+    fcl = sch.fcluster(Z, 1 - 0.95, criterion="distance")
+    Cdb, (Zg, ldb, args) = d_cluster.cluster_mash_database(Mdb, clusterAlg=method, P_ani=0.95)
+    pd.testing.assert_frame_equal(ldb, lp, check_exact=True)
+    assert type(ldb.index) is type(lp.index) and ldb.index.dtype == lp.index.dtype
+    assert np.array_equal(Zg, Z), np.argwhere(Zg != Z)[:5]
+    assert list(Cdb["primary_cluster"]) == list(fcl) and list(Cdb["genome"]) == list(lp.columns)
+    assert np.array_equal(Mdb["dist"].to_numpy().view(np.uint32), ref["dist"].to_numpy().view(np.uint32))
+    assert 1 < Cdb["primary_cluster"].nunique() < N
+    assert args == {"linkage_method": method, "linkage_cutoff": 1 - 0.95, "comparison_algorithm": "MASH"}
+
+
+def test_linkage_square_checks_like_scipy():
+    """drephip_linkage_square raises squareform's / linkage's ValueErrors
+    (asymmetric, nonzero diagonal, NaN, inf) with scipy's messages, and a
+    -0.0 / +0.0 mirror pair or a float64 pivot still gives scipy's Z."""
+    import scipy.cluster.hierarchy as sch
+    import scipy.spatial.distance as ssd
+    from drep_amd import d_cluster
+    rng = np.random.default_rng(8)
+    n = 300
+    y = np.round(rng.random(n * (n - 1) // 2), 2).astype(np.float32)
+    M = ssd.squareform(y)
+    for method in ("average", "single"):
+        want = sch.linkage(ssd.squareform(M), method=method)
+        assert np.array_equal(d_cluster._square_linkage(M, method, 0), want)
+        assert np.array_equal(d_cluster._square_linkage(M.astype(np.float64), method, 0),
+                              sch.linkage(ssd.squareform(M.astype(np.float64)), method=method))
+    M0 = M.copy()
+    M0[3, 9] = np.float32(0.0)
+    M0[9, 3] = np.float32(-0.0)
+    assert np.array_equal(d_cluster._square_linkage(M0, "average", 0),
+                          sch.linkage(ssd.squareform(M0), method="average"))
+    cases = []
+    A = M.copy(); A[4, 7] = np.float32(0.5); A[7, 4] = np.float32(0.25); cases.append(A)
+    B = M.copy(); B[5, 5] = np.float32(0.1); cases.append(B)
+    Cn = M.copy(); Cn[2, 6] = Cn[6, 2] = np.nan; cases.append(Cn)
+    Ci = M.copy(); Ci[2, 6] = Ci[6, 2] = np.inf; cases.append(Ci)
+    for X in cases:
+        with pytest.raises(ValueError) as want:
+            sch.linkage(ssd.squareform(X), method="average")
+        with pytest.raises(ValueError) as got:
+            d_cluster._square_linkage(X, "average", 0)
+        assert str(got.value) == str(want.value)
 
 
 def _dropin_bdb(golden, tmp_path):
@@ -964,7 +1060,7 @@ def test_cluster_mash_condensed_gpu_equals_reference_path(family, ctx1000, metho
     rng = np.random.default_rng(5)
     names = ["g%04d.fna" % i for i in rng.permutation(N)]
     cm = CondensedMash(names, names, c, d, nh, np.full(N, 400_000, np.uint64), S)
-    cdb_cpu, (z_cpu, _, _) = cluster_mash_condensed(cm, clusterAlg=method, P_ani=0.95)
+    cdb_cpu, (z_cpu, _, _) = cluster_mash_condensed(cm, clusterAlg=method, P_ani=0.95, gpu=None)
     cdb_gpu, (z_gpu, _, _) = cluster_mash_condensed(cm, clusterAlg=method, P_ani=0.95, gpu=0)
     assert np.array_equal(z_gpu, z_cpu)
     assert cdb_gpu.equals(cdb_cpu)

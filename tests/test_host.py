@@ -125,6 +125,16 @@ def test_msh_roundtrip_and_fixture(golden, tmp_path):
     assert (r.kmer, r.sketch_size, r.seed, len(r.references[0].hashes)) == (21, 3, 7, 0)
 
 
+def _square(vec, N, diag):
+    """Symmetric N x N matrix of a condensed vector (scipy order) and a diagonal."""
+    M = np.zeros((N, N), dtype=vec.dtype)
+    iu = np.triu_indices(N, 1)
+    M[iu] = vec
+    M = M + M.T
+    M[np.arange(N), np.arange(N)] = diag
+    return M
+
+
 def _fixture_condensed(golden):
     refs = read_msh(os.path.join(golden, "MASH_files", "ALL.msh")).references
     H = np.stack([r.hashes for r in refs])
@@ -152,7 +162,7 @@ def test_mdb_from_condensed_matches_reference_parse(golden):
 def test_cluster_mash_database_matches_reference(golden, alg):
     cm = _fixture_condensed(golden)
     Mdb = d_cluster.mdb_from_condensed(cm.names, cm.common, cm.denom, cm.nhash, cm.s)
-    Cdb, ret = d_cluster.cluster_mash_database(Mdb, clusterAlg=alg, P_ani=0.9)
+    Cdb, ret = d_cluster.cluster_mash_database(Mdb, clusterAlg=alg, P_ani=0.9, gpu=None)
     exp = pd.read_csv(os.path.join(golden, "ref", "cdb_%s.csv" % alg))
     assert Cdb.to_dict("list") == exp.to_dict("list")
     link = json.load(open(os.path.join(golden, "ref", "linkage_%s.json" % alg)))
@@ -161,7 +171,7 @@ def test_cluster_mash_database_matches_reference(golden, alg):
     # in-place update of Mdb['dist'] exactly as the reference leaves it
     assert list(Mdb["dist"].to_numpy().view(np.uint32)) == link["dist_bits_after"]
     # the condensed path (no N^2 table) gives the same linkage and clusters
-    Cdb2, ret2 = d_cluster.cluster_mash_condensed(cm, clusterAlg=alg, P_ani=0.9)
+    Cdb2, ret2 = d_cluster.cluster_mash_condensed(cm, clusterAlg=alg, P_ani=0.9, gpu=None)
     assert Cdb2.to_dict("list") == exp.to_dict("list")
     assert np.array_equal(ret2[0], ret[0])
 
@@ -175,8 +185,8 @@ def test_condensed_clustering_equals_pivot_path_unsorted_names():
     cm = d_cluster.CondensedMash(names, names, c, d, nh, np.full(n, 150_000, np.uint64), S)
     Mdb = d_cluster.mdb_from_condensed(names, c, d, nh, S)
     for alg in ("average", "single", "complete"):
-        Cdb, ret = d_cluster.cluster_mash_database(Mdb.copy(), clusterAlg=alg, P_ani=0.95)
-        Cdb2, ret2 = d_cluster.cluster_mash_condensed(cm, clusterAlg=alg, P_ani=0.95)
+        Cdb, ret = d_cluster.cluster_mash_database(Mdb.copy(), clusterAlg=alg, P_ani=0.95, gpu=None)
+        Cdb2, ret2 = d_cluster.cluster_mash_condensed(cm, clusterAlg=alg, P_ani=0.95, gpu=None)
         assert np.array_equal(ret[0], ret2[0])
         assert Cdb.to_dict("list") == Cdb2.to_dict("list")
 
@@ -370,7 +380,7 @@ def test_condensed_store_roundtrip(tmp_path, partial):
     m0 = mdb_from_condensed(cm.names, cm.common, cm.denom, cm.nhash, s)
     m1 = mdb_from_condensed(back.names, back.common, back.denom, back.nhash, s)
     assert m0.equals(m1)
-    cdb, (Z, db, args) = cluster_mash_condensed(back, clusterAlg="average", P_ani=0.9)
+    cdb, (Z, db, args) = cluster_mash_condensed(back, clusterAlg="average", P_ani=0.9, gpu=None)
     store_primary_linkage(str(tmp_path), Z, db, args)
     pl = load_primary_linkage(str(tmp_path))
     assert np.array_equal(pl["linkage"], Z) and pl["db"] is None and pl["arguments"] == args
@@ -477,8 +487,8 @@ def test_write_mash_table_vs_line_by_line(tmp_path):
     cm = d_cluster.CondensedMash(names, names, c, d, nh, length, S)
     out = tmp_path / "t.tsv"
     d_cluster.write_mash_table(str(out), cm, threads=3)
-    Cm = d_cluster._square(c, n, np.minimum(nh, S).astype(np.uint16)).astype(np.int64)
-    Dm = d_cluster._square(d, n, np.minimum(nh, S).astype(np.uint16)).astype(np.int64)
+    Cm = _square(c, n, np.minimum(nh, S).astype(np.uint16)).astype(np.int64)
+    Dm = _square(d, n, np.minimum(nh, S).astype(np.uint16)).astype(np.int64)
     lines = []
     for q in range(n):
         for r in range(n):
@@ -622,3 +632,122 @@ print(json.dumps(out))
     assert res[0] == res[1]
     assert res[0][len(fas)] == res[0][1]            # the members concatenated: the original file
     assert res[0][-1] == "error" or res[0][-1][0] != 0 or res[0][-1][1] < len(raw)
+
+
+# ------------------------------------------ Mdb table and pivot (host, native)
+def _mdb_numpy(names, common, denom, s):
+    """The Mdb as the earlier pure-numpy restatement built it: squareform of the
+    float32 distances, tile/repeat of the category codes."""
+    import scipy.spatial.distance as ssd
+    N = len(names)
+    dist = ssd.squareform(d_cluster.mash_distance_float32(common, denom), checks=False).reshape(-1)
+    cats = sorted(set(names))
+    codes = np.array([cats.index(n) for n in names])
+    g1 = pd.Categorical.from_codes(np.tile(codes, N), categories=cats, ordered=True)
+    g2 = pd.Categorical.from_codes(np.repeat(codes, N), categories=cats, ordered=True)
+    Mdb = pd.DataFrame({"genome1": g1, "genome2": g2, "dist": dist})
+    Mdb["similarity"] = 1 - Mdb["dist"]
+    return Mdb
+
+
+@pytest.mark.parametrize("n,partial", [(2, False), (37, True), (130, False), (300, True)])
+def test_mdb_from_condensed_native_equals_numpy(n, partial):
+    """drephip_mdb_square against the numpy restatement: every cell's float32
+    bits, the category codes and dtypes (int8 codes below 127 names, int16
+    above), partial sketches (one table per denominator), unsorted names."""
+    rng = np.random.default_rng(n)
+    npairs = n * (n - 1) // 2
+    denom = np.full(npairs, S, np.uint16)
+    if partial:
+        denom[rng.random(npairs) < 0.2] = rng.integers(0, 700, 1)[0]
+        denom[rng.random(npairs) < 0.05] = 0
+    common = np.minimum(rng.integers(0, S + 1, npairs), denom).astype(np.uint16)
+    names = ["g%04d.fa" % i for i in rng.permutation(n)]
+    got = d_cluster.mdb_from_condensed(names, common, denom, None, S, threads=3)
+    want = _mdb_numpy(names, common, denom, S)
+    pd.testing.assert_frame_equal(got, want, check_exact=True)
+    for c in ("dist", "similarity"):
+        assert np.array_equal(got[c].to_numpy().view(np.uint32), want[c].to_numpy().view(np.uint32))
+    assert got["genome1"].cat.codes.dtype == (np.int8 if n < 127 else np.int16)
+    bad = common.copy()
+    bad[0] = S + 1 if not partial else denom[0] + 1
+    with pytest.raises(_lib.DrepHipError, match="exceeds"):
+        d_cluster.mdb_from_condensed(names, bad, denom, None, S)
+
+
+def _pivot_ref(db):
+    return db.pivot(index="genome1", columns="genome2", values="dist")
+
+
+def _assert_pivot_equal(got, want):
+    pd.testing.assert_frame_equal(got, want, check_exact=True)
+    for a, b in ((got.index, want.index), (got.columns, want.columns)):
+        assert type(a) is type(b) and a.name == b.name and a.dtype == b.dtype
+    assert np.array_equal(got.to_numpy().view(np.uint32), want.to_numpy().view(np.uint32))
+
+
+def test_pivot_native_equals_pandas():
+    """_pivot_dist (drephip_pivot_scan/fill) against pandas' own pivot on the
+    layouts a Mdb can have: all_vs_all_MASH's (blocked transpose), rows
+    shuffled (scatter), rows missing (NaN cells), unused categories, genome
+    names with 1-byte and 2-byte codes; duplicates raise pandas' error; tables
+    outside the fast path (unsorted categories, float64 dist, object columns)
+    go through pandas and still match."""
+    rng = np.random.default_rng(3)
+    for n in (1, 2, 5, 140):
+        npairs = n * (n - 1) // 2
+        common = rng.integers(0, 40, npairs).astype(np.uint16)
+        names = ["g%03d.fa" % i for i in rng.permutation(n)]
+        Mdb = d_cluster.mdb_from_condensed(names, common, np.full(npairs, S, np.uint16), None, S)
+        Mdb["dist"] = 1 - Mdb["similarity"]
+        _assert_pivot_equal(d_cluster._pivot_dist(Mdb), _pivot_ref(Mdb))
+        if n < 5:
+            continue
+        sh = Mdb.sample(frac=1.0, random_state=1).reset_index(drop=True)        # any row order
+        _assert_pivot_equal(d_cluster._pivot_dist(sh), _pivot_ref(sh))
+        miss = sh.iloc[3:].reset_index(drop=True)                               # missing cells -> NaN
+        _assert_pivot_equal(d_cluster._pivot_dist(miss), _pivot_ref(miss))
+        part = Mdb[Mdb["genome1"] != names[0]].reset_index(drop=True)          # a name only in genome2
+        _assert_pivot_equal(d_cluster._pivot_dist(part), _pivot_ref(part))
+        extra = Mdb.copy()                                                      # an unused category
+        for g in ("genome1", "genome2"):
+            extra[g] = extra[g].cat.add_categories(["zzz_unused.fa"])
+        _assert_pivot_equal(d_cluster._pivot_dist(extra), _pivot_ref(extra))
+        dup = pd.concat([Mdb, Mdb.iloc[[7]]], ignore_index=True)
+        with pytest.raises(ValueError, match="duplicate entries"):
+            _pivot_ref(dup)
+        with pytest.raises(ValueError, match="duplicate entries"):
+            d_cluster._pivot_dist(dup)
+        for other in (Mdb.astype({"dist": np.float64}),
+                      Mdb.assign(genome1=Mdb["genome1"].astype(str), genome2=Mdb["genome2"].astype(str)),
+                      Mdb.assign(genome1=Mdb["genome1"].cat.reorder_categories(sorted(names, reverse=True)),
+                                 genome2=Mdb["genome2"].cat.reorder_categories(sorted(names, reverse=True)))):
+            _assert_pivot_equal(d_cluster._pivot_dist(other), _pivot_ref(other))
+
+
+def test_cluster_mash_database_host_path_equals_reference_steps():
+    """cluster_mash_database(gpu=None) -- the native pivot, then scipy -- equals
+    the reference's steps literally (d_cluster.py:619-623, 445-459) on a
+    shuffled family set: linkage_db, Z, Cdb and the in-place dist bits; an
+    asymmetric table logs and raises squareform's error."""
+    import scipy.cluster.hierarchy as sch
+    import scipy.spatial.distance as ssd
+    n = 60
+    h, nh = oracle.sketch_synth(0, n, 120_000, seed=9, family_size=6, threads=4)
+    c, d = oracle.allpairs(h, nh, S)
+    names = ["g%03d.fa" % i for i in np.random.default_rng(2).permutation(n)]
+    Mdb = d_cluster.mdb_from_condensed(names, c, d, nh, S)
+    ref = Mdb.copy()
+    ref["dist"] = 1 - ref["similarity"]
+    lp = ref.pivot(index="genome1", columns="genome2", values="dist")
+    Z = sch.linkage(ssd.squareform(np.asarray(lp)), method="average")
+    fcl = sch.fcluster(Z, 1 - 0.95, criterion="distance")
+    Cdb, (Zg, ldb, args) = d_cluster.cluster_mash_database(Mdb, clusterAlg="average", P_ani=0.95, gpu=None)
+    _assert_pivot_equal(ldb, lp)
+    assert np.array_equal(Zg, Z)
+    assert list(Cdb["primary_cluster"]) == list(fcl) and list(Cdb["genome"]) == list(lp.columns)
+    assert np.array_equal(Mdb["dist"].to_numpy().view(np.uint32), ref["dist"].to_numpy().view(np.uint32))
+    asym = Mdb.copy()
+    asym.loc[5, "similarity"] = np.float32(0.5)
+    with pytest.raises(ValueError, match="symmetric"):
+        d_cluster.cluster_mash_database(asym, clusterAlg="average", gpu=None)

@@ -126,7 +126,7 @@ def _worker_pipeline(rank, world, port, N, out_dir, partial):
         c = common.numpy().view(np.uint16)
         d = denom.numpy().view(np.uint16) if denom is not None else np.full(len(c), S, np.uint16)
         cm = CondensedMash(names, names, c, d, np.zeros(n, np.uint32), np.zeros(n, np.uint64), S)
-        _, (Z, _, _) = cluster_mash_condensed(cm, clusterAlg=method)
+        _, (Z, _, _) = cluster_mash_condensed(cm, clusterAlg=method, gpu=None)
         return Z
 
     res = D.run_sharded(N, names, S, sketch_fn, allpairs_fn, linkage_fn, "average", 0.9)
@@ -165,7 +165,7 @@ def test_gloo_sharded_clustering_matches_single_process(tmp_path, world, partial
         assert (want_d < S).any()
     names = D.synthetic_names(N)
     cm = CondensedMash(names, names, want_c, want_d, nh, np.zeros(N, np.uint64), S)
-    cdb, (Z, _, _) = cluster_mash_condensed(cm, clusterAlg="average", P_ani=0.9)
+    cdb, (Z, _, _) = cluster_mash_condensed(cm, clusterAlg="average", P_ani=0.9, gpu=None)
     assert np.array_equal(np.load(os.path.join(tmp_path, "Z.npy")), Z)
     got = pd.read_csv(os.path.join(tmp_path, "Cdb.csv"))
     assert got["genome"].tolist() == cdb["genome"].tolist()
@@ -263,7 +263,7 @@ def _worker_weighted(rank, world, port, N, out_dir):
         c = common.numpy().view(np.uint16)
         d = denom.numpy().view(np.uint16) if denom is not None else np.full(len(c), S, np.uint16)
         cm = CondensedMash(names, names, c, d, np.zeros(n, np.uint32), np.zeros(n, np.uint64), S)
-        _, (Z, _, _) = cluster_mash_condensed(cm, clusterAlg=method)
+        _, (Z, _, _) = cluster_mash_condensed(cm, clusterAlg=method, gpu=None)
         return Z
 
     res = D.run_sharded(N, names, S, sketch_fn, allpairs_fn, linkage_fn, "average", 0.9, weights=weights)
@@ -304,7 +304,7 @@ def test_gloo_balanced_shards_match_single_process(tmp_path, world):
     assert np.array_equal(np.load(os.path.join(tmp_path, "common.npy")), want_c)
     names = D.synthetic_names(N)
     cm = CondensedMash(names, names, want_c, want_d, nh, np.zeros(N, np.uint64), S)
-    cdb, (Z, _, _) = cluster_mash_condensed(cm, clusterAlg="average", P_ani=0.9)
+    cdb, (Z, _, _) = cluster_mash_condensed(cm, clusterAlg="average", P_ani=0.9, gpu=None)
     assert np.array_equal(np.load(os.path.join(tmp_path, "Z.npy")), Z)
     got = pd.read_csv(os.path.join(tmp_path, "Cdb.csv"))
     assert got["genome"].tolist() == cdb["genome"].tolist()
