@@ -44,33 +44,76 @@ N_SIMD = 256 * 4
 VALU_PEAK_WAVE_INST = N_SIMD * 2.4e9 / 2
 SKETCH_PHASES = os.path.join(ROOT, "profiles", "r05_sketch_isa_phases.json")
 SKETCH_ABLATION = os.path.join(ROOT, "profiles", "r05_sketch_ablation.json")
-# committed PMC summaries (tools/pmc_summary.py): VALU / LDS utilisation of the
-# two kernels, reported next to the live timings
-SKETCH_PMC = os.path.join(ROOT, "profiles", "r05_sketch_pmc_sq.json")
-# all-pairs profiles of tools/profile_allpairs.sh, one per (N, s) case: the
-# bench line quotes the one of its own workload (never another N's)
-DIST_PROFILES = [os.path.join(ROOT, "profiles", r + "_allpairs_N%d%s.json") for r in ("r05", "r04")]   # newest first
-SKETCH_TRAFFIC = os.path.join(ROOT, "profiles", "r05_sketch_traffic.json")
+# Committed rocprofv3 summaries this line quotes.  A profile carries the
+# library build it was taken on (drephip_build_id, "build_id") and the
+# workload; the line quotes one only when both are this run's -- a profile of
+# another build or workload is named in a note, never used for a fraction.
+#   sketch: tools/profile_round.sh (traffic_json.py / pmc_summary.py)
+#   all-pairs: tools/profile_allpairs.sh (allpairs_traffic_json.py), one file
+#   per workload: rNN_allpairs_N<N>_s<s>_f<family size>.json, newest round first
+PROFILES = os.path.join(ROOT, "profiles")
+SKETCH_PMC_NAME = "sketch_pmc_sq.json"
+SKETCH_TRAFFIC_NAME = "sketch_traffic.json"
 PROFILE_STEPS = 3              # untimed steps that time finalize / all-pairs / table build
 VERIFY_GENOMES = 16            # timed-step sketches re-derived by the C oracle (sampled, every run)
 VERIFY_PAIRS = 100_000         # timed-step counts re-derived by the C oracle (random pairs + one row)
 
 
-def dist_roofline(N, s, pairs_per_launch, launch_ms):
-    """Roofline block of the all-pairs kernel from the committed profile of
-    this exact workload (tools/profile_allpairs.sh): VALU issue against the
-    2-cycle wave64 peak (the PMC's VALU instructions per pair x this launch's
-    pairs / this launch's live HIP-event time), LDS busy, HBM traffic and L2
-    hit rate of the profiled dispatches."""
-    cands = [p % (N, "" if s == 1000 else "_s%d" % s) for p in DIST_PROFILES]
-    path = next((p for p in cands if os.path.exists(p)), None)
-    if path is None:
-        return {"note": "no all-pairs profile committed for N=%d s=%d (%s)" % (N, s, os.path.relpath(cands[0], ROOT))}
-    d = json.load(open(path))
+def lib_build_src():
+    from drep_amd import _lib
+    return _lib.build_id().get("src")
+
+
+def find_profile(name, accept=None):
+    """The newest profiles/rNN_<name> taken on THIS library build (and, given
+    `accept`, whose content it accepts).  Returns (doc, path, note): doc None
+    when no such profile exists, with the reason in `note`."""
+    import glob
+    import re
+    src = lib_build_src()
+    cands = sorted(glob.glob(os.path.join(PROFILES, "r[0-9][0-9]_" + name)),
+                   key=lambda p: int(re.search(r"/r(\d\d)_", p).group(1)), reverse=True)
+    seen = []
+    for path in cands:
+        try:
+            d = json.load(open(path))
+        except Exception:
+            continue
+        rel = os.path.relpath(path, ROOT)
+        b = (d.get("build_id") or {}).get("src")
+        if b != src:
+            seen.append("%s: build %s" % (rel, (b or "unrecorded")[:12]))
+            continue
+        if accept is not None and not accept(d):
+            seen.append("%s: another workload/kernel" % rel)
+            continue
+        return d, rel, None
+    return None, None, ("no profiles/rNN_%s of this library build (src %s)%s" %
+                        (name, (src or "?")[:12], ("; not used: " + "; ".join(seen)) if seen else ""))
+
+
+def dist_roofline(N, s, fam, screened, pairs_per_launch, launch_ms):
+    """Roofline block of the all-pairs kernel this run used -- the dense
+    k_allpairs_q / k_allpairs_band template, or the screened LIST one -- from
+    the committed profile of exactly this workload (N, s, family size) and
+    kernel template on this library build (tools/profile_allpairs.sh): VALU
+    issue against the 2-cycle wave64 peak (the PMC's VALU instructions per pair
+    x this launch's pairs / this launch's live HIP-event time), LDS busy, HBM
+    traffic against the algorithmic bytes and the L2 hit rate of the profiled
+    dispatches.  No matching profile: no fraction, only the reason."""
+    variant = "LIST" if screened else "dense"
+
+    def accept(d):
+        w = d.get("workload") or {}
+        return (w.get("genomes"), w.get("sketch"), w.get("family_size"), w.get("kernel_variant")) == (N, s, fam, variant)
+    d, rel, note = find_profile("allpairs_N%d_s%d_f%d.json" % (N, s, fam), accept)
+    if d is None:
+        return {"kernel_variant": variant, "note": note}
     dv = d.get("derived", {})
-    out = {"kernel": (d.get("kernel") or "")[:60], "source": os.path.relpath(path, ROOT),
-           "profiled_avg_call_ms": d.get("avg_call_ms")}
-    if dv.get("valu_wave_insts_per_pair") and launch_ms:
+    out = {"kernel": (d.get("kernel") or "")[:60], "kernel_variant": variant, "source": rel,
+           "build_id": d["build_id"].get("src"), "profiled_avg_call_ms": d.get("avg_call_ms"),
+           "this_run_ms": launch_ms}
+    if dv.get("valu_wave_insts_per_pair") and launch_ms and not screened:
         ach = dv["valu_wave_insts_per_pair"] * pairs_per_launch / (launch_ms * 1e-3)
         out.update({"bound": "valu+lds", "achieved": ach, "peak": VALU_PEAK_WAVE_INST,
                     "unit": "wave64 VALU instructions/s", "frac": ach / VALU_PEAK_WAVE_INST,
@@ -78,40 +121,16 @@ def dist_roofline(N, s, pairs_per_launch, launch_ms):
                     "salu_over_valu": dv.get("salu_over_valu")})
     for k in ("lds_busy_frac", "lds_bank_conflict_frac", "valu_issue_frac_2cyc", "wait_inst_any_frac",
               "wait_any_frac", "l2_hit_rate", "hbm_bytes_x2", "hbm_GBps_x2", "hbm_frac_of_8TBps_x2",
-              "algorithmic_bytes", "effective_clock_ghz"):
+              "algorithmic_bytes", "hbm_over_algorithmic_x2", "effective_clock_ghz", "pairs_per_s"):
         if k in dv:
             out[k] = dv[k]
     out["traffic"] = dv.get("hbm_bytes_x2")
     return out
 
 
-def list_profile(N, s, launch_ms):
-    """The screened LIST kernel's committed profile of this exact workload, if
-    one was taken on the LIST kernel (kernel name ends in LIST = true): HBM
-    traffic against the algorithmic bytes, L2 hit rate, and the profiled vs
-    this run's kernel time."""
-    for p in DIST_PROFILES:
-        path = p % (N, "" if s == 1000 else "_s%d" % s)
-        if not os.path.exists(path):
-            continue
-        d = json.load(open(path))
-        if "true>" not in (d.get("kernel") or "") and "true," not in (d.get("kernel") or ""):
-            continue
-        dv = d.get("derived", {})
-        return {"source": os.path.relpath(path, ROOT), "kernel": (d.get("kernel") or "")[:60],
-                "profiled_avg_call_ms": d.get("avg_call_ms"), "this_run_ms": launch_ms,
-                **{k: dv[k] for k in ("hbm_bytes_x2", "algorithmic_bytes", "hbm_over_algorithmic_x2", "l2_hit_rate",
-                                      "hbm_GBps_x2", "lds_busy_frac", "valu_issue_frac_2cyc") if k in dv}}
-    return None
-
-
-def pmc_block(path):
+def pmc_block(doc, rel):
     """Utilisation fractions from a committed PMC summary, or None."""
-    if not os.path.exists(path):
-        return None
-    try:
-        d = json.load(open(path))
-    except Exception:
+    if doc is None:
         return None
     # (valu_active_quad_frac is not kept: SQ_ACTIVE_INST_VALU equals
     # SQ_INSTS_VALU in the sketch profile, i.e. it counts one quad-cycle per
@@ -119,9 +138,10 @@ def pmc_block(path):
     # cycles, not a measured VALU occupancy)
     keep = ("valu_issue_frac_2cyc", "lds_busy_frac", "lds_bank_conflict_frac", "wait_any_frac",
             "wait_inst_any_frac", "active_inst_any_frac", "valu_insts_per_window_end", "effective_clock_ghz")
-    out = {k: d["derived"][k] for k in keep if k in d.get("derived", {})}
-    out["source"] = os.path.relpath(path, ROOT)
-    out["profiled_kernel"] = (d.get("kernel") or "")[:80]
+    out = {k: doc["derived"][k] for k in keep if k in doc.get("derived", {})}
+    out["source"] = rel
+    out["build_id"] = (doc.get("build_id") or {}).get("src")
+    out["profiled_kernel"] = (doc.get("kernel") or "")[:80]
     return out
 
 
@@ -140,7 +160,6 @@ def parse():
                     help="queue each step before checking the previous one (1) or one step at a time (0)")
     ap.add_argument("--defer-check", type=int, default=1,
                     help="check the sketch's threshold status after queuing the all-pairs (1) or before (0)")
-    ap.add_argument("--traffic-json", default=SKETCH_TRAFFIC)
     ap.add_argument("--check", type=int, default=1,
                     help="after timing (untimed): check a sample of the timed steps' own sketches and "
                          "shared-hash counts against the C oracle (test infrastructure); 'verified' in "
@@ -576,14 +595,10 @@ def main():
     avg_launch_s = (sk_ms / max(sk_n, 1)) / 1e3
     alg_bytes = nloc * P * 3 / 8                     # 2-bit codes + 1 validity bit per base
     achieved = alg_bytes / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
-    traffic = None
-    if os.path.exists(args.traffic_json):
-        try:
-            tj = json.load(open(args.traffic_json))
-            if tj.get("genomes_per_launch") == nloc:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    # HBM bytes per launch from the committed PMC passes of this build and this
+    # launch size (tools/profile_round.sh), else null with the reason
+    tj, traffic_src, traffic_note = find_profile(SKETCH_TRAFFIC_NAME, lambda d: d.get("genomes_per_launch") == nloc)
+    traffic = tj.get("hbm_bytes_per_launch") if tj else None
     kmers_per_s = nloc * (L - 20) / avg_launch_s if avg_launch_s > 0 else 0.0
     window_ends = nloc * P                           # every padded position is a window end the kernel visits
     valu = {"kmers_per_s": kmers_per_s}
@@ -592,7 +607,8 @@ def main():
         valu.update({"kernel": ph["kernel"], "valu_per_kmer_hot_loop": ph["valu_per_kmer"],
                      "valu_per_kmer_by_phase": {k: v["valu_per_kmer"] for k, v in ph["phases"].items()},
                      "isa_source": os.path.relpath(SKETCH_PHASES, ROOT) + " (tools/isa_phases.py)"})
-    pmc_sk = pmc_block(SKETCH_PMC)
+    pmc_doc, pmc_src, pmc_note = find_profile(SKETCH_PMC_NAME)
+    pmc_sk = pmc_block(pmc_doc, pmc_src) or {"note": pmc_note}
     if os.path.exists(SKETCH_ABLATION) and valu.get("valu_per_kmer_hot_loop") and avg_launch_s > 0:
         # One binding resource: VALU issue of the hot loop's instruction
         # stream.  achieved = the hot loop's wave64 VALU instructions per launch
@@ -720,6 +736,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": traffic,
+                "traffic_source": traffic_src or traffic_note,
                 "note": "algorithmic bytes = 0.375 B/base (2-bit code + validity bit) x bases per "
                         "launch; HBM is not the limit: the kernel is VALU-issue bound (Murmur3, 63 "
                         "VALU instructions per k-mer in the hot loop), see valu_model",
@@ -735,15 +752,15 @@ def main():
                 "pairs_per_launch": segment_size(N, r0, r1),
                 "pairs_per_s_per_gpu": (segment_size(N, r0, r1) / (kms[2][0] / max(kms[2][1], 1) / 1e3)
                                         if kms[2][0] else None),
-                "roofline": (dist_roofline(N, args.sketch, segment_size(N, r0, r1), kms[2][0] / max(kms[2][1], 1))
-                             if not screen.get("used") else
-                             {"note": "screened path (DESIGN.md 4.6): the sort/mark/list passes, the no-shared-hash fill "
-                                      "and the LIST kernel on the marked (row tile, column) cells; the dense kernel's "
-                                      "per-pair profile does not apply",
-                              "screen_ms_avg": kms[4][0] / max(kms[4][1], 1),
-                              "sort_bytes_per_launch_est": 4 * 16 * screen.get("entries", 0),
-                              "marked_cells": screen.get("marked"), "pair_checks": screen.get("checks"),
-                              "list_kernel_profile": list_profile(N, args.sketch, kms[2][0] / max(kms[2][1], 1))}),
+                "roofline": dist_roofline(N, args.sketch, args.family_size, bool(screen.get("used")),
+                                          segment_size(N, r0, r1), kms[2][0] / max(kms[2][1], 1)),
+                "screened_stage": ({"note": "screened path (DESIGN.md 4.6): the sort/mark/list passes, the "
+                                            "no-shared-hash fill and the LIST kernel on the marked (row tile, column) "
+                                            "cells; the roofline above is the LIST kernel's",
+                                    "screen_ms_avg": kms[4][0] / max(kms[4][1], 1),
+                                    "sort_bytes_per_launch_est": 4 * 16 * screen.get("entries", 0),
+                                    "marked_cells": screen.get("marked"), "pair_checks": screen.get("checks")}
+                                   if screen.get("used") else None),
             },
             "cpu_baseline": cpu,
         }

@@ -398,7 +398,7 @@ __device__ __forceinline__ uint64_t ld_chunk_at(__amdgpu_buffer_rsrc_t rs, uint3
 // LIST (the screened path, screen.hip): the item's columns are clist[0..cend)
 // -- ascending, each sharing a hash with a row of the tile -- and c_first /
 // c_step walk that list instead of the column range.
-template <int R, int NCH, bool FAST, int KB, bool MASKED, bool LIST = false>
+template <int R, int NCH, bool FAST, int KB, bool MASKED, bool LIST = false, bool HITQ = false>
 __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ nhash,
                                            const uint32_t *T, const uint32_t *V, uint32_t H, uint32_t hm, uint32_t s,
                                            uint32_t N, uint32_t i0, uint32_t nrows, uint32_t cend, uint32_t c_first,
@@ -509,6 +509,30 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
                 if (((actmask >> r) & 1u) && (mrun[r] != 0 || !(b0 > thr[r]))) all_past = false;
             return all_past;
         };
+        // HITQ: the union-rank end for rows WITH shared hashes too.  b at
+        // column position jb ranks u(b) = jb + #{A_r < b} - mrun_r in A_r u B
+        // (mrun_r: the shared hashes before it), so u(b) >= s once A_r holds
+        // s - jb + mrun_r elements below b, i.e. once b > A_r[p], p = s - jb +
+        // mrun_r - 1 -- tested on the high words in LDS (V: hi(b) > V_r[p]
+        // implies b > A_r[p]; an equal high word just continues the scan).  A
+        // row of one species shares a few hashes with most columns, so the
+        // thresholds above (rows without matches) never end its scan, which
+        // then ran to A's last element: ~2x the chunks of the cutoff near
+        // s (1 + J) / 2.  p >= nA (a partial row) cannot end it.
+        auto past_v = [&](uint64_t bv, uint32_t jb) {                       // wave-uniform
+            const uint32_t hb = rfl((uint32_t)(bv >> 32));
+            uint32_t vr[R], pr[R];
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                pr[r] = s + mrun[r] - jb - 1;                                 // >= 0: jb < s
+                vr[r] = V[min(pr[r], s - 1) * R + r];
+            }
+            bool all_past = true;
+#pragma unroll
+            for (int r = 0; r < R; r++)
+                if (((actmask >> r) & 1u) && !(pr[r] < nA[r] && hb > rfl(vr[r]))) all_past = false;
+            return all_past;
+        };
         for (uint32_t kb = 0; kb < nch; kb += kRing) {
             {
                 const uint64_t b = rg[0];
@@ -517,7 +541,7 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
                 const uint64_t b0 = ((uint64_t)rfl((uint32_t)(b >> 32)) << 32) | rfl((uint32_t)b);
                 if (b0 == kEmpty || b0 > amax) break;
 #if DREPHIP_AP_MID
-                if (kb > kb1 && past(b, thr2)) break;                      // wave-uniform
+                if (!HITQ && kb > kb1 && past(b, thr2)) break;             // wave-uniform
 #else
                 if (kb >= kb1 && past(b, kb == kb1 ? thr1 : thr2)) break;    // wave-uniform
 #endif
@@ -558,7 +582,13 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
 #if DREPHIP_AP_MID
                 // the first union-rank test one chunk into group kb1: B[64 (kb1 + 1)]
                 // against A_r[s - 64 (kb1 + 1) - 1] (thr1) after chunk kb1's probe
-                if (u == 0 && kb == kb1 && kb1 + 1 < nch && past(rg[1], thr1)) goto column_done;
+                if constexpr (HITQ) {
+                    // every group from kb1 on, one chunk in: B[64 (kb + 1)] with the
+                    // matches of every chunk before it
+                    if (u == 0 && kb >= kb1 && kb + 1 < nch && past_v(rg[1], 64 * (kb + 1))) goto column_done;
+                } else {
+                    if (u == 0 && kb == kb1 && kb1 + 1 < nch && past(rg[1], thr1)) goto column_done;
+                }
 #endif
             }
         }
@@ -603,7 +633,8 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
     const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ nhash,
     const uint32_t *__restrict__ blk, uint32_t stride, const uint8_t *__restrict__ fam, uint32_t s, uint32_t N,
     uint32_t row0, uint32_t row1, uint32_t B, const uint4 *__restrict__ items,
-    uint16_t *__restrict__ common, uint16_t *__restrict__ denom, uint64_t seg0, const uint32_t *__restrict__ clist) {
+    uint16_t *__restrict__ common, uint16_t *__restrict__ denom, uint64_t seg0, const uint32_t *__restrict__ clist,
+    int hitq) {
     constexpr int WG = kApWG;
     extern __shared__ __align__(16) uint32_t lds[];    // 16-B aligned: slot words are read with ds_read_b128
     const uint32_t H = 1u << B, hm = H - 1, TS = 2 * H;
@@ -682,7 +713,11 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
     // The kernel declares no static LDS (.group_segment_fixed_size 0, checked
     // by tests/test_host.py), so `lds` is LDS address 0 (read_slots).
     constexpr int KB = NCH == 16 ? 11 : 0;
-    if (fast && !zero_key)
+    if (fast && !zero_key && hitq)
+        ap_columns<R, NCH, true, KB, false, LIST, true>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend, cfirst + wave,
+                                                  WG / 64, ilist, nA, o1, o2, alast, thr1, thr2, ~failmask,
+                                                  any_partial_row, common, denom, seg0);
+    else if (fast && !zero_key)
         ap_columns<R, NCH, true, KB, false, LIST>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend, cfirst + wave, WG / 64, ilist,
                                             nA, o1, o2, alast, thr1, thr2, ~failmask, any_partial_row, common, denom,
                                             seg0);
@@ -1435,11 +1470,14 @@ static int launch_q(drephip_ctx *ctx, uint32_t nitems, size_t lds, hipStream_t s
                     uint64_t seg0, const uint32_t *clist) {
     HIPC(hipFuncSetAttribute((const void *)k_allpairs_q<R, NCH, MINW, LIST>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)lds));
+    // the dense-hit probe (probe_rows_q): DREPHIP_AP_HIT=0 keeps probe_rows (A/B)
+    const char *he = getenv("DREPHIP_AP_HIT");
+    const int hitq = he ? atoi(he) : 1;
     timing_mark(ctx, 2, st, true);
     for (uint32_t i0 = 0; i0 < nitems; i0 += (uint32_t)max_blocks(kApWG))
         hipLaunchKernelGGL((k_allpairs_q<R, NCH, MINW, LIST>),
                            dim3(std::min<uint32_t>(nitems - i0, (uint32_t)max_blocks(kApWG))), dim3(kApWG), lds, st, h,
-                           nh, blk, stride, fam, ctx->s, N, row0, row1, B, items + i0, cm, dn, seg0, clist);
+                           nh, blk, stride, fam, ctx->s, N, row0, row1, B, items + i0, cm, dn, seg0, clist, hitq);
     timing_mark(ctx, 2, st, false);
     HIPC(hipGetLastError());
     return DREPHIP_OK;

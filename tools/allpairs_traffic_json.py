@@ -6,7 +6,12 @@ HBM -- so both the raw and the doubled read figure are given: the column loads
 here are 8 B per lane, an uncalibrated width), the L2 hit rate, and the SQ
 issue/stall fractions (tools/pmc_summary.py's definitions).
 
-usage: python tools/allpairs_traffic_json.py <kernel substring> <dir> <case> N s calls
+usage: python tools/allpairs_traffic_json.py <kernel substring> <dir> <case> N s calls [family_size]
+
+The summary names the workload (N, s, the generator's family size, whether the
+profiled dispatches are the screened LIST template or the dense one) and the
+library build (drephip_build_id of drep_amd/lib/libdrephip.so, loaded here
+without a GPU): bench.py quotes a profile only for its own workload and build.
 
 `calls` = all-pairs calls the profiled command made (bench.py --steps 1
 --warmup 0: 4, its three timing steps included; tools/ap_bench.py with
@@ -41,6 +46,7 @@ def per_dispatch(files, key):
 def main():
     key, d, case, N, s = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5])
     ncalls = int(sys.argv[6])
+    family = int(sys.argv[7]) if len(sys.argv) > 7 else 100
     stats = glob.glob(os.path.join(d, case + "_trace", "**", "*kernel_stats.csv"), recursive=True)
     avg_ms, ndisp = None, None
     for r in csv.DictReader(open(stats[0])):
@@ -55,7 +61,12 @@ def main():
     # GRBM_GUI_ACTIVE rides in every pass (summed over 8 XCDs): its dispatch
     # count above spans all passes, hence the division by the pass count
     cyc = c.get("GRBM_GUI_ACTIVE", 0.0) / 8
-    out = {"case": case, "kernel": name, "genomes": N, "sketch": s, "pairs": N * (N - 1) // 2,
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from drep_amd import _lib
+    variant = "LIST" if name and ("true>" in name or "true," in name) else "dense"
+    out = {"case": case, "kernel": name, "kernel_variant": variant, "build_id": _lib.build_id(),
+           "workload": {"genomes": N, "sketch": s, "family_size": family, "kernel_variant": variant},
+           "genomes": N, "sketch": s, "pairs": N * (N - 1) // 2,
            "calls": ncalls, "dispatches_per_call": (ndisp or 0) / ncalls, "avg_call_ms": avg_ms,
            "counters_per_call": c, "dispatches_per_counter": nd}
     dv = out["derived"] = {}

@@ -17,7 +17,7 @@ N = int(sys.argv[1]) if len(sys.argv) > 1 else 10000
 cfgs = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "4,8").split(",") if x]
 VAR = os.environ.get("AB_VAR", "DREPHIP_AP_R")
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3
-s, L, fam, seed = int(os.environ.get("AB_S", 1000)), 5_000_000, 100, 0xD2E9
+s, L, fam, seed = int(os.environ.get("AB_S", 1000)), 5_000_000, int(os.environ.get("AB_FAM", 100)), 0xD2E9
 dev = torch.device("cuda", 0)
 ctx = _lib.Context(0, 21, s, 42)
 st = torch.cuda.current_stream(dev).cuda_stream

@@ -80,6 +80,11 @@ def main():
         ld = max(len(disp.get("SQ_LDS_IDX_ACTIVE", ())), 1)
         if c.get("SQ_LDS_IDX_ACTIVE"):
             d["lds_busy_frac"] = c["SQ_LDS_IDX_ACTIVE"] / ld / (N_CU * cyc)
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from drep_amd import _lib
+    out["build_id"] = _lib.build_id()          # the library the profiled command loaded
     print(json.dumps(out, indent=1))
 
 

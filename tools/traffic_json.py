@@ -34,8 +34,10 @@ def main():
     fetch_kb, write_kb = sum(f) / len(f), sum(w) / len(w)
     alg = G * P * 3 / 8
     hbm = 2 * fetch_kb * 1024 + write_kb * 1024
+    from drep_amd import _lib
     print(json.dumps({
         "kernel": sorted(names)[0] if names else KERNEL,
+        "build_id": _lib.build_id(),
         "command": "rocprofv3 --pmc <C> -- python bench.py --steps 1 --warmup 0 --cpu-baseline 0 (one pass per counter)",
         "dispatches": [len(f), len(w)],
         "genomes_per_launch": G,
