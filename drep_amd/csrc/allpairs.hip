@@ -351,6 +351,66 @@ __device__ __forceinline__ void probe_rows(const Slots<R> &sl, uint64_t b, uint3
     }
 }
 
+// The whole-row kernel's probe for chunks where many lanes hit (genomes of one
+// species share ~20-30 % of their sketches: c ~ 180-280 of 1000, a hit in
+// most rows of most chunks).  probe_rows tests each row behind a uniform
+// branch -- row active, any hit -- and its high-word read waits right there,
+// so a chunk's rows cost four dependent LDS round trips, ~11 scalar
+// instructions and three branches each.  Here, once the all-rows test finds
+// a hit: every row's position f and high word V[f] are read first (R LDS
+// reads in flight together), then each row is straight-line mask arithmetic
+// with no branch -- a row with no hit adds 0, an inactive row's counts are
+// never written:
+//   m    = ballot(V[f] == hi(b)) & ballot(f < nA)        shared hashes
+//   rank = ballot(f + j - (s + mrun) < mbcnt(m))          union rank < s
+//          (signed: f + j < s + mrun + shared hashes in lower lanes)
+//   cnt += popc(rank & m);  mrun += popc(m)
+// nb[r] = -(s + mrun) is kept instead of mrun, so the rank operand is one
+// three-input add with a scalar (v_add3) and mbcnt needs no scalar base.
+template <int R>
+__device__ __forceinline__ void probe_rows_v(const Slots<R> &sl, uint64_t b, uint32_t jl, const uint32_t *V,
+                                             uint32_t hm, uint32_t s, const uint32_t (&nA)[R], int32_t (&nb)[R],
+                                             uint32_t (&cnt)[R]) {
+    const uint32_t blo = (uint32_t)b, bhi = (uint32_t)(b >> 32);
+    const uint32_t b4 = rotr32(blo, 4), b20 = rotr32(blo, 20);
+    uint32_t xs1[R], xs2[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        xs1[r] = sl.e1[r] ^ b4;
+        xs2[r] = sl.e2[r] ^ b20;
+    }
+    {
+        uint32_t mn;
+        if constexpr (R == 4) {
+            const uint32_t m1 = min(min(xs1[0], xs1[1]), xs1[2]);
+            const uint32_t m2 = min(min(xs1[3], xs2[0]), xs2[1]);
+            mn = min(min(m1, m2), min(xs2[2], xs2[3]));
+        } else {
+            mn = min(xs1[0], xs2[0]);
+#pragma unroll
+            for (int r = 1; r < R; r++) mn = min(mn, min(xs1[r], xs2[r]));
+        }
+        if (__builtin_amdgcn_ballot_w64(mn <= hm) == 0) return;
+    }
+    uint32_t f[R], vh[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        f[r] = min(xs1[r], xs2[r]);
+        vh[r] = V[min(f[r], s - 1) * R + r];                          // row-interleaved high words
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) asm volatile("" : "+v"(vh[r]));     // all R reads issued before the first use
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const uint64_t m = __builtin_amdgcn_ballot_w64(vh[r] == bhi) & __builtin_amdgcn_ballot_w64(f[r] < nA[r]);
+        const int32_t pre = (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        const int32_t key = (int32_t)(f[r] + jl) + nb[r];
+        cnt[r] += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(key < pre) & m);
+        nb[r] -= (int32_t)__popcll(m);
+    }
+}
+
 // ------------------------------------------------------- whole-row tables
 // The columns of one work item, processed by one wave.  The column elements
 // stream through a ring of kRing chunks in registers, loaded kRing chunks
@@ -398,7 +458,7 @@ __device__ __forceinline__ uint64_t ld_chunk_at(__amdgpu_buffer_rsrc_t rs, uint3
 // LIST (the screened path, screen.hip): the item's columns are clist[0..cend)
 // -- ascending, each sharing a hash with a row of the tile -- and c_first /
 // c_step walk that list instead of the column range.
-template <int R, int NCH, bool FAST, int KB, bool MASKED, bool LIST = false, bool HITQ = false>
+template <int R, int NCH, bool FAST, int KB, bool MASKED, bool LIST = false, bool HITQ = false, bool HITV = false>
 __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ nhash,
                                            const uint32_t *T, const uint32_t *V, uint32_t H, uint32_t hm, uint32_t s,
                                            uint32_t N, uint32_t i0, uint32_t nrows, uint32_t cend, uint32_t c_first,
@@ -454,11 +514,13 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
         cnext = kn < cend ? column_of(kn) : 0;
         if (kn < cend) first_chunks(column_rsrc(hashes + (uint64_t)cnext * s, s));
         uint32_t cnt[R], mrun[R], actmask = act_full;
+        int32_t nb[R];                                                // HITV: -(s + matches so far), probe_rows_v
         // elements past every active row's largest hash cannot match: the
         // scan ends at the first chunk whose smallest element is past them
         uint64_t amax = amax_full;
 #pragma unroll
-        for (int r = 0; r < R; r++) { cnt[r] = 0; mrun[r] = 0; }
+        for (int r = 0; r < R; r++) { cnt[r] = 0; mrun[r] = 0; nb[r] = -(int32_t)s; }
+        auto mrun_of = [&](int r) -> uint32_t { return HITV ? (uint32_t)(-nb[r] - (int32_t)s) : mrun[r]; };
         if (c < i0 + R) {                                             // the diagonal tile: rows right of c drop out
             actmask = 0;
             amax = 0;
@@ -506,7 +568,7 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
             bool all_past = true;
 #pragma unroll
             for (int r = 0; r < R; r++)
-                if (((actmask >> r) & 1u) && (mrun[r] != 0 || !(b0 > thr[r]))) all_past = false;
+                if (((actmask >> r) & 1u) && (mrun_of(r) != 0 || !(b0 > thr[r]))) all_past = false;
             return all_past;
         };
         // HITQ: the union-rank end for rows WITH shared hashes too.  b at
@@ -524,7 +586,7 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
             uint32_t vr[R], pr[R];
 #pragma unroll
             for (int r = 0; r < R; r++) {
-                pr[r] = s + mrun[r] - jb - 1;                                 // >= 0: jb < s
+                pr[r] = s + mrun_of(r) - jb - 1;                              // >= 0: jb < s
                 vr[r] = V[min(pr[r], s - 1) * R + r];
             }
             bool all_past = true;
@@ -562,9 +624,13 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
                 // probe: the ring and slot updates above stay unconditional, or
                 // the compiler merges the ring registers through a copy that
                 // waits for the refill load issued in the same chunk
-                if (!MASKED || k < nch)                                   // wave-uniform
+                if constexpr (HITV) {
+                    static_assert(FAST && !MASKED, "probe_rows_v: the FAST unmasked path");
+                    probe_rows_v<R>(sb[u], b, k * 64 + lane, V, hm, s, nA, nb, cnt);
+                } else if (!MASKED || k < nch) {                          // wave-uniform
                     probe_rows<R, FAST, !FAST, true>(sb[u], b, k * 64 + lane, V, s, hm, o1, o2, actmask, lm, zero, nA, s,
                                                mrun, cnt);
+                }
                 // refill the ring unconditionally and after the chunk's last use,
                 // so the load reuses the chunk's registers: a conditional update,
                 // or one while the old value is live, makes the compiler copy the
@@ -609,7 +675,7 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
                 if (denom) {
                     uint32_t dd = s;
                     if (partial) {
-                        const uint32_t u = nA[r] + nB - mrun[r];  // |A u B|; mrun = |A n B| when partial
+                        const uint32_t u = nA[r] + nB - mrun_of(r);  // |A u B|; mrun = |A n B| when partial
                         dd = u < s ? u : s;
                     }
                     denom[o] = (uint16_t)dd;
@@ -714,9 +780,9 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
     // by tests/test_host.py), so `lds` is LDS address 0 (read_slots).
     constexpr int KB = NCH == 16 ? 11 : 0;
     if (fast && !zero_key && hitq)
-        ap_columns<R, NCH, true, KB, false, LIST, true>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend, cfirst + wave,
-                                                  WG / 64, ilist, nA, o1, o2, alast, thr1, thr2, ~failmask,
-                                                  any_partial_row, common, denom, seg0);
+        ap_columns<R, NCH, true, KB, false, LIST, true, true>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend,
+                                                        cfirst + wave, WG / 64, ilist, nA, o1, o2, alast, thr1, thr2,
+                                                        ~failmask, any_partial_row, common, denom, seg0);
     else if (fast && !zero_key)
         ap_columns<R, NCH, true, KB, false, LIST>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend, cfirst + wave, WG / 64, ilist,
                                             nA, o1, o2, alast, thr1, thr2, ~failmask, any_partial_row, common, denom,
@@ -1470,7 +1536,9 @@ static int launch_q(drephip_ctx *ctx, uint32_t nitems, size_t lds, hipStream_t s
                     uint64_t seg0, const uint32_t *clist) {
     HIPC(hipFuncSetAttribute((const void *)k_allpairs_q<R, NCH, MINW, LIST>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)lds));
-    // the dense-hit probe (probe_rows_q): DREPHIP_AP_HIT=0 keeps probe_rows (A/B)
+    // the branch-free hit probe and the union-rank end for rows with matches
+    // (probe_rows_v, ap_columns HITQ/HITV); DREPHIP_AP_HIT=0 runs the round-5
+    // probe and ends (A/B)
     const char *he = getenv("DREPHIP_AP_HIT");
     const int hitq = he ? atoi(he) : 1;
     timing_mark(ctx, 2, st, true);

@@ -95,6 +95,24 @@ __device__ uint64_t *g_lk_ph;
 #define LK_T(v) (void)0
 #endif
 
+// Adverse workgroup order (a test build only: make EXTRA=-DDREPHIP_LK_ADVERSE=1
+// or 2): the step and compaction kernels' even (1) or odd (2) workgroups sleep
+// ~14 us before their main loads, so the other workgroups of the same launch
+// have finished their stores by the time those loads run.  Every value a
+// kernel reads must then still be the one of the launch before it -- the
+// rule "no workgroup reads what another workgroup of the same launch writes"
+// (the producer/consumer table) -- or Z departs from scipy's
+// (tests/test_gpu.py::test_linkage_adverse_workgroup_order).
+#ifndef DREPHIP_LK_ADVERSE
+#define DREPHIP_LK_ADVERSE 0
+#endif
+__device__ __forceinline__ void adverse_delay() {
+#if DREPHIP_LK_ADVERSE
+    if ((blockIdx.x & 1u) == (DREPHIP_LK_ADVERSE == 1 ? 0u : 1u))
+        for (int k = 0; k < 4; k++) __builtin_amdgcn_s_sleep(127);
+#endif
+}
+
 __device__ __forceinline__ bool better(double v, int32_t i, double bv, int32_t bi) {
     return v < bv || (v == bv && i < bi);
 }
@@ -725,6 +743,7 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     // loads, which the compiler waited for before the pass.)
     int32_t lz;
     asm volatile("v_mov_b32 %0, 0" : "=v"(lz));
+    adverse_delay();
     const bool fa = pend && !yA, fb = pend && sp && !yB, fw = pend && hasW && !yW;
     // (entry (y, R) from its column copy D[R][y], which only the lane of i = y
     // writes in this launch, after this load: the row copy D[y][R] is the lane
@@ -947,6 +966,7 @@ __global__ __launch_bounds__(WG) void k_mst_step(const double *__restrict__ D, u
     }
     __syncthreads();
     if (s_k >= (int32_t)n - 1) return;
+    adverse_delay();
     const int32_t ov = s_ov, x = s_mx;
     const double *Dx = D + (uint64_t)x * n;
     double bv = INFINITY;
@@ -1073,6 +1093,7 @@ __global__ __launch_bounds__(256) void k_lk_cmp_state(LinkState *__restrict__ st
 __global__ __launch_bounds__(256) void k_lk_cmp_rows(const double *src, uint32_t so, double *dst, uint32_t sn,
                                                      const int32_t *__restrict__ orig, uint32_t r0, uint32_t r1,
                                                      uint32_t d0) {
+    adverse_delay();
     const uint32_t nb = (sn + 1023) / 1024;
     const uint64_t items = (uint64_t)(r1 - r0) * nb;
     for (uint64_t it = blockIdx.x; it < items; it += gridDim.x) {

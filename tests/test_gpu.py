@@ -13,6 +13,7 @@ from drep_amd import _lib
 from drep_amd.mash_io import read_msh
 
 pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 S = 1000
 UMAX = np.iinfo(np.uint64).max
 
@@ -1198,3 +1199,57 @@ def test_linkage_counts_device_rejects_missing_tables(ctx1000):
     c_big[2] = 701                                           # count above its denominator
     with pytest.raises(_lib.DrepHipError, match="exceeds"):
         ctx1000.linkage_counts_device(c_big.data_ptr(), d_small.data_ptr(), n, perm, lut7, off7, "average", st)
+
+
+_ADVERSE_SCRIPT = r"""
+import json, os, sys
+import numpy as np
+import scipy.cluster.hierarchy as sch
+sys.path.insert(0, os.getcwd())
+from drep_amd import _lib
+out = {"build": _lib.build_id(), "cases": []}
+rng = np.random.default_rng(17)
+for n, fams in ((300, 12), (3000, 60)):
+    fam = rng.integers(0, fams, n)
+    iu = np.triu_indices(n, 1)
+    y = np.where(fam[iu[0]] == fam[iu[1]], np.round(rng.random(len(iu[0])) * 0.2, 3), 1.0)
+    for method in ("single", "complete", "average", "weighted"):
+        Zs = sch.linkage(y, method=method)
+        for wg in ("64", "256"):
+            if method == "single" and wg == "64":
+                continue
+            os.environ["DREPHIP_LINK_WG"] = wg
+            with _lib.Context(0, 21, 1000, 42) as ctx:
+                ctx.set_linkage_path(ctx.LINK_DENSE)
+                Z = ctx.linkage(y, method)
+            out["cases"].append({"n": n, "method": method, "wg": wg, "equal": bool(np.array_equal(Z, Zs))})
+print(json.dumps(out))
+"""
+
+
+@pytest.mark.parametrize("order", ["even", "odd"])
+def test_linkage_adverse_workgroup_order(order):
+    """The chain step, MST step and compaction kernels rest on "no workgroup
+    reads what another workgroup of the same launch writes" (DESIGN 4.4,
+    producer/consumer table).  Under a debug build whose even (odd) workgroups
+    sleep ~14 us before their loads -- every other workgroup of the launch has
+    stored by then -- Z must still be scipy's, for all four methods, one-wave
+    and 256-lane step workgroups, with compactions at many chain states.  The
+    variant libraries are built by __graft_entry__.build() (tools/build_ab.sh,
+    EXTRA=-DDREPHIP_LK_ADVERSE=1/2) and run in a child process."""
+    import json
+    import subprocess
+    import sys
+    lib = os.path.join(ROOT, "drep_amd", "lib_ab", "adverse_" + order, "libdrephip.so")
+    if not os.path.exists(lib):
+        pytest.skip("adverse-order build missing (run __graft_entry__.build())")
+    env = dict(os.environ, DREPHIP_LIB=lib, DREPHIP_LINK_BATCH="32", DREPHIP_LINK_POLL="1",
+               DREPHIP_LINK_COMPACT_MIN="100")
+    r = subprocess.run([sys.executable, "-c", _ADVERSE_SCRIPT], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert "DREPHIP_LK_ADVERSE=%d" % (1 if order == "even" else 2) in res["build"].get("extra", "")
+    assert len(res["cases"]) == 14
+    bad = [c for c in res["cases"] if not c["equal"]]
+    assert not bad, bad
