@@ -748,7 +748,14 @@ __global__ __launch_bounds__(WG) void k_nn_step(double *__restrict__ D, uint32_t
     // (entry (y, R) from its column copy D[R][y], which only the lane of i = y
     // writes in this launch, after this load: the row copy D[y][R] is the lane
     // of i = R's to rewrite -- reading it here raced with that store)
+#if DREPHIP_LK_RACE_REPRO
+    // (test build only: the round-5 race reintroduced -- entry (y, R) from the
+    // row copy D[y][R], which the lane of i = R rewrites in this launch; the
+    // adverse-order test must catch it)
+    auto colY = [&](int32_t r) { return D[(uint64_t)y * n + r + lz]; };
+#else
     auto colY = [&](int32_t r) { return D[(uint64_t)r * n + y + lz]; };
+#endif
     double xa = fa ? Dx[A + lz] : 0.0, ya_ = fa ? colY(A) : 0.0;
     double xb = fb ? Dx[B + lz] : 0.0, yb = fb ? colY(B) : 0.0;
     double xw = fw ? Dx[W + lz] : 0.0, yw = fw ? colY(W) : 0.0;
