@@ -35,15 +35,15 @@ HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 # VALU issue: MI355X_MICROARCH.md gives one wave64 VALU instruction per 2
 # cycles per SIMD (SIMD-32) as the issue peak: 1024 SIMDs x 2.4 GHz / 2 (the
 # all-pairs kernel's VALU fraction is quoted against it).  The sketch hash
-# kernel's model is its own instruction floor (profiles/r05_sketch_ablation.json,
-# tools/sketch_ablation_json.py): every build of its hot loop -- product, +6
-# VALU, conflict-free LDS, no LDS at all -- takes ~3.8 SIMD-cycles per wave64
-# VALU instruction, so its time is its VALU count at that rate; the no-LDS
-# build's rate is the floor the live launch is compared with.
+# kernel's peak is its priced instruction stream (profiles/r06_sketch_priced.json,
+# tools/sketch_priced.py): every instruction of the hot loop at its class's
+# measured wall time per wave64 instruction per SIMD with 8 waves on every SIMD
+# (tools/valu_microbench.hip) -- full-rate classes ~1.0 ns, the 64-bit,
+# multiply, 3-operand and byte-select classes ~1.75 ns.
 N_SIMD = 256 * 4
 VALU_PEAK_WAVE_INST = N_SIMD * 2.4e9 / 2
 SKETCH_PHASES = os.path.join(ROOT, "profiles", "r05_sketch_isa_phases.json")
-SKETCH_ABLATION = os.path.join(ROOT, "profiles", "r05_sketch_ablation.json")
+SKETCH_PRICED = os.path.join(ROOT, "profiles", "r06_sketch_priced.json")
 # Committed rocprofv3 summaries this line quotes.  A profile carries the
 # library build it was taken on (drephip_build_id, "build_id") and the
 # workload; the line quotes one only when both are this run's -- a profile of
@@ -609,27 +609,30 @@ def main():
                      "isa_source": os.path.relpath(SKETCH_PHASES, ROOT) + " (tools/isa_phases.py)"})
     pmc_doc, pmc_src, pmc_note = find_profile(SKETCH_PMC_NAME)
     pmc_sk = pmc_block(pmc_doc, pmc_src) or {"note": pmc_note}
-    if os.path.exists(SKETCH_ABLATION) and valu.get("valu_per_kmer_hot_loop") and avg_launch_s > 0:
-        # One binding resource: VALU issue of the hot loop's instruction
-        # stream.  achieved = the hot loop's wave64 VALU instructions per launch
-        # / this launch's live time; peak = the same instructions at the floor
-        # rate (the no-LDS build's SIMD-cycles per instruction, same box class)
-        ab = json.load(open(SKETCH_ABLATION))
-        floor_cyc = ab["floor"]["cycles_per_wave_inst_per_simd"]
+    if os.path.exists(SKETCH_PRICED) and valu.get("valu_per_kmer_hot_loop") and avg_launch_s > 0:
+        # One binding resource: VALU issue of the hot loop's instruction stream.
+        # achieved = the hot loop's wave64 VALU instructions per launch / this
+        # launch's live time; peak = the same stream at its measured prices
+        # (the priced model's mean ns per instruction, every SIMD busy)
+        pr = json.load(open(SKETCH_PRICED))
         wi = valu["valu_per_kmer_hot_loop"] * window_ends / 64
         ach = wi / avg_launch_s
-        peak = N_SIMD * 2.4e9 / floor_cyc
+        ns = pr["valu_ns_per_instruction_avg"]
+        peak = N_SIMD / (ns * 1e-9)
         valu.update({"bound": "valu_issue", "achieved": ach, "peak": peak, "unit": "wave64 VALU instructions/s",
                      "frac": ach / peak,
-                     "cycles_per_wave_inst_per_simd": N_SIMD * 2.4e9 / ach,
-                     "floor_cycles_per_wave_inst_per_simd": floor_cyc,
-                     "floor_source": os.path.relpath(SKETCH_ABLATION, ROOT) + " (tools/sketch_ablation_json.py)",
+                     "priced_ns_per_wave_inst_per_simd": ns,
+                     "priced_valu_per_kmer": pr["valu_per_kmer"],
+                     "peak_source": os.path.relpath(SKETCH_PRICED, ROOT) + " (tools/sketch_priced.py)",
                      "frac_of_2cyc_issue_peak": ach / VALU_PEAK_WAVE_INST,
-                     "note": "binding resource: VALU issue. Time = VALU count x ~3.8 SIMD-cycles per wave64 "
-                             "instruction in every ablation build (product; +6 VALU; conflict-free LDS; no LDS "
-                             "reads), so `frac` is the live rate over the no-LDS build's rate (the instruction "
-                             "floor); the guide's 2-cycle dual-wave peak is not reached by this dependent 64-bit "
-                             "mix (SQ_WAIT_INST_ANY 0.58 of wave-cycles)"})
+                     "note": "binding resource: VALU issue. peak = the hot loop's own instructions at their measured "
+                             "prices (tools/valu_microbench.hip, 8 waves/SIMD); the priced model predicts "
+                             "%.2f ms for the configs[1] launch against %.2f ms measured on the same box; LDS reads "
+                             "and SALU add no measurable time to a VALU-bound stream" %
+                             (pr["predicted_ms"], pr["measured_hash_ms"])})
+        if abs(pr["valu_per_kmer"] - valu["valu_per_kmer_hot_loop"]) > 1e-6:
+            valu["note"] += "; the priced mix (%.3f VALU/k-mer) is not this build's (%.3f)" % (
+                pr["valu_per_kmer"], valu["valu_per_kmer_hot_loop"])
 
     # ---- output segment D2H (PCIe-inclusive leg; not part of `value`)
     torch.cuda.synchronize()

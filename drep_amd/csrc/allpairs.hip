@@ -38,9 +38,6 @@
 
 namespace drephip {
 
-#ifndef DREPHIP_AP_EXIT2
-#define DREPHIP_AP_EXIT2 0        // A/B: the union-rank end tested twice per group (chunks 0 and 2)
-#endif
 #ifndef DREPHIP_AP_MID
 #define DREPHIP_AP_MID 1          // first union-rank test one chunk into its group (ap_columns); 0: at the group start
 #endif
@@ -654,13 +651,9 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
                 if constexpr (HITQ) {
                     // every group from kb1 on, one chunk in: B[64 (kb + 1)] with the
                     // matches of every chunk before it
-                    if constexpr (DREPHIP_AP_EXIT2) {
-                        if ((u == 0 || u == 2) && k >= kb1 && k + 1 < nch &&
-                            past_v(rg[(u + 1) % kRing], 64 * (k + 1)))
-                            goto column_done;
-                    } else {
-                        if (u == 0 && kb >= kb1 && kb + 1 < nch && past_v(rg[1], 64 * (kb + 1))) goto column_done;
-                    }
+                    // (tested twice per group, chunks 0 and 2: 2 % slower on the dense
+                    // 10^4 set, equal elsewhere -- profiles/r06_allpairs_hit_ab.txt)
+                    if (u == 0 && kb >= kb1 && kb + 1 < nch && past_v(rg[1], 64 * (kb + 1))) goto column_done;
                 } else {
                     if (u == 0 && kb == kb1 && kb1 + 1 < nch && past(rg[1], thr1)) goto column_done;
                 }

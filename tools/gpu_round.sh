@@ -19,6 +19,7 @@
 #   job          drep_amd.distributed --genomes JOB_N on JOB_W gloo ranks (JOB_ARGS)
 #   rank_screen  tools/rank_screen.py (RS_ARGS)
 #   scale        tools/gpu_scale.sh "$SCALE_SPECS"
+#   price        tools/valu_microbench.hip (instruction prices) + the sketch hash kernel at configs[1] (tools/sketch_ablate.py)
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-.}
 export TMPDIR=/tmp
@@ -85,6 +86,18 @@ for step in ${STEPS:-tests smoke bench}; do
       timeout -k 10 300 python tools/rank_screen.py $RS_ARGS > $O/rank_screen.json 2> $O/rank_screen.err || fail rank_screen $O/rank_screen.err
       tail -c 1500 $O/rank_screen.json ;;
     scale) bash tools/gpu_scale.sh "$SCALE_SPECS" || exit 1 ;;
+    price)
+      # instruction prices at 8 waves/SIMD, then the sketch hash kernel's own time
+      # at configs[1] (product library), PRICE_REPS times interleaved
+      /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -o $O/valu_microbench tools/valu_microbench.hip \
+          > $O/price_build.log 2>&1 || fail price_build $O/price_build.log
+      for r in $(seq ${PRICE_REPS:-2}); do
+        timeout -k 10 120 $O/valu_microbench > $O/valu_microbench_$r.json 2> $O/price.err || fail price $O/price.err
+        DREPHIP_SK_ONE_ROUND=1 timeout -k 10 300 python tools/sketch_ablate.py 10 > $O/sketch_ms_$r.json 2>> $O/price.err \
+            || fail sketch_ms $O/price.err
+        echo "rep $r: $(cat $O/sketch_ms_$r.json)"
+      done
+      rm -f $O/valu_microbench ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
