@@ -1553,6 +1553,54 @@ static int launch_q(drephip_ctx *ctx, uint32_t nitems, size_t lds, hipStream_t s
     return DREPHIP_OK;
 }
 
+// the screen mode (DREPHIP_SCREEN_*; DREPHIP_AP_SCREEN overrides) and whether
+// it screens an all-pairs call over N genomes
+int screen_mode(drephip_ctx *ctx) {
+    int smode = ctx->screen;
+    if (const char *e = getenv("DREPHIP_AP_SCREEN")) smode = atoi(e);
+    return smode;
+}
+bool screen_applies(drephip_ctx *ctx, uint32_t N) {
+    const int smode = screen_mode(ctx);
+    const char *mn = getenv("DREPHIP_SCREEN_MIN_N");
+    const uint32_t min_n = mn ? (uint32_t)atoi(mn) : kScreenMinN;
+    return (smode == DREPHIP_SCREEN_ON || (smode == DREPHIP_SCREEN_AUTO && N >= min_n)) &&
+           (uint64_t)N * ctx->s < (1ull << 32) && ctx->ap_path != DREPHIP_AP_MERGE;
+}
+
+// Rows per work item / row tile and the kernel path for this context's s:
+// whole-row LDS tables (B-bit fields, 2H slots, H = 2^B >= 2s) when they fit,
+// else value bands.  The sharded screen's parts tile rows by the same R.
+int allpairs_geometry(drephip_ctx *ctx, uint32_t *R_out, int *path_out) {
+    const uint32_t s = ctx->s;
+    // table: 2H slots, H = 2^B >= 2s (load <= 1/4, and every position and the
+    // empty word's 2^B - 1 fit the field); 32-bit families need B <= 12
+    uint32_t B = 4;
+    while ((1u << B) < 2 * s) B++;
+    const uint32_t TS = 2u << B;
+    const bool fits = B <= 12 && q_lds_bytes(1, TS, s) <= kLdsBudget;
+    int path = ctx->ap_path;
+    if (path == DREPHIP_AP_AUTO) path = fits ? DREPHIP_AP_TABLE : DREPHIP_AP_BAND;
+    if (path == DREPHIP_AP_TABLE && !fits) {
+        set_error("whole-row table all-pairs kernel needs s <= 2048");
+        return DREPHIP_ERR_UNSUPPORTED;
+    }
+    // rows per workgroup: the most (8, 4, 2, 1) whose tables + high words fit
+    static const uint32_t kR[] = {8, 4, 2, 1};
+    uint32_t R = 1;
+    for (uint32_t r : kR) if (q_lds_bytes(r, TS, s) + 16 <= kLdsBudget) { R = r; break; }
+    if (const char *e = getenv("DREPHIP_AP_R")) {
+        // A/B override: R rows per workgroup if their tables fit the whole
+        // 160 KiB of a CU (one workgroup per CU above 80 KiB)
+        const uint32_t r = (uint32_t)atoi(e);
+        if ((r == 1 || r == 2 || r == 4 || r == 8) && q_lds_bytes(r, TS, s) <= 160 * 1024) R = r;
+    }
+    if (path == DREPHIP_AP_BAND) R = kBandR;
+    *R_out = R;
+    *path_out = path;
+    return DREPHIP_OK;
+}
+
 int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N,
                          uint32_t row0, uint32_t row1, uint16_t *d_common, uint16_t *d_denom,
                          hipStream_t st, bool force_merge, bool defer) {
@@ -1569,41 +1617,32 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
     const uint64_t seg0 = cond_index(row0, row0 + 1, N);
     const uint64_t seg1 = row1 < N - 1 ? cond_index(row1, row1 + 1, N) : (uint64_t)N * (N - 1) / 2;
     const uint64_t npairs = seg1 - seg0;
-    // table: 2H slots, H = 2^B >= 2s (load <= 1/4, and every position and the
-    // empty word's 2^B - 1 fit the field); 32-bit families need B <= 12
+    uint32_t R = 1;
+    int path = DREPHIP_AP_MERGE;
+    const int rc0 = allpairs_geometry(ctx, &R, &path);
+    if (force_merge) path = DREPHIP_AP_MERGE;         // (the literal merge needs no table)
+    else if (rc0) return rc0;
     uint32_t B = 4;
     while ((1u << B) < 2 * s) B++;
     const uint32_t TS = 2u << B;
-    const bool fits = B <= 12 && q_lds_bytes(1, TS, s) <= kLdsBudget;
-    int path = force_merge ? DREPHIP_AP_MERGE : ctx->ap_path;
-    if (path == DREPHIP_AP_AUTO) path = fits ? DREPHIP_AP_TABLE : DREPHIP_AP_BAND;
-    if (path == DREPHIP_AP_TABLE && !fits) {
-        set_error("whole-row table all-pairs kernel needs s <= 2048");
-        return DREPHIP_ERR_UNSUPPORTED;
-    }
     ctx->last_screen = ScreenResult{};
     if (path == DREPHIP_AP_MERGE)
         return launch_merge(ctx, d_hashes, d_nhash, N, seg0, npairs, d_common, d_denom, st);
 
-    // rows per workgroup: the most (8, 4, 2, 1) whose tables + high words fit
-    static const uint32_t kR[] = {8, 4, 2, 1};
-    uint32_t R = 1;
-    for (uint32_t r : kR) if (q_lds_bytes(r, TS, s) + 16 <= kLdsBudget) { R = r; break; }
-    if (const char *e = getenv("DREPHIP_AP_R")) {
-        // A/B override: R rows per workgroup if their tables fit the whole
-        // 160 KiB of a CU (one workgroup per CU above 80 KiB)
-        const uint32_t r = (uint32_t)atoi(e);
-        if ((r == 1 || r == 2 || r == 4 || r == 8) && q_lds_bytes(r, TS, s) <= 160 * 1024) R = r;
-    }
-    if (path == DREPHIP_AP_BAND) R = kBandR;
-
     // the shared-hash screen (screen.hip): auto from kScreenMinN genomes on
-    int smode = ctx->screen;
-    if (const char *e = getenv("DREPHIP_AP_SCREEN")) smode = atoi(e);
+    const int smode = screen_mode(ctx);
     const char *mn = getenv("DREPHIP_SCREEN_MIN_N");
     const uint32_t min_n = mn ? (uint32_t)atoi(mn) : kScreenMinN;
     ScreenResult scr;
-    if (smode == DREPHIP_SCREEN_ON || (smode == DREPHIP_SCREEN_AUTO && N >= min_n)) {
+    if (ctx->ext.active) {
+        // the sharded screen: this call's rows from every part's marks
+        // (drephip_allpairs_device_marked); no light cells
+        int rc = screen_marked_impl(ctx, d_nhash, N, row0, row1, R, path == DREPHIP_AP_BAND ? kBandCols : kListCols,
+                                    seg0, npairs, d_common, d_denom, ctx->ext.bitmaps, ctx->ext.nparts, ctx->ext.rec,
+                                    ctx->ext.nrec, st, &scr);
+        if (rc) return rc;
+        ctx->last_screen = scr;
+    } else if (smode == DREPHIP_SCREEN_ON || (smode == DREPHIP_SCREEN_AUTO && N >= min_n)) {
         // LIST items: the band kernel's per-column LDS state holds kBandCols
         // columns; the whole-row kernel takes up to kListCols per item, so a
         // row tile's image is loaded once for most tiles

@@ -91,6 +91,28 @@ struct ScreenResult {
     uint64_t simple = 0;          // pairs sharing exactly one hash, written by the screen itself
 };
 
+// The last hash part a sharded screen grouped (screen_part_impl): its bitmap
+// of (row tile from row 0, column) cells and its records of runs of two, in
+// the context's scratch until the next screen call.
+struct PartResult {
+    bool valid = false;
+    uint32_t N = 0, R = 0;
+    const uint32_t *bitmap = nullptr;   // ceil(N / R) x ceil(N / 32) words
+    uint64_t bitmap_words = 0;
+    const uint4 *rec = nullptr;         // {a, b, (i << 16) | j, 0}
+    uint32_t nrec = 0;
+    uint64_t entries = 0, runs = 0;
+};
+// Marks handed to the next all-pairs call (drephip_allpairs_device_marked):
+// every part's bitmap and records; the call screens its rows from them.
+struct ExtMarks {
+    bool active = false;
+    const uint32_t *bitmaps = nullptr;  // nparts x ceil(N / R) x ceil(N / 32) words
+    uint32_t nparts = 0;
+    const uint4 *rec = nullptr;
+    uint64_t nrec = 0;
+};
+
 // A run of all-pairs work items (allpairs.hip, plan_items): `size` row tiles
 // from i0 (step R) against column tile c0, at offset `off` of its XCD's list.
 struct ApItemGroup { uint32_t i0, c0, off, size; };
@@ -105,6 +127,8 @@ struct drephip_ctx {
     int ap_path = 0;          // DREPHIP_AP_*: 0 auto (table for s <= 2048, else band)
     int screen = 0;           // DREPHIP_SCREEN_*: 0 auto, 1 on, 2 off
     ScreenResult last_screen; // the last all-pairs call's screen (stats; pointers into scratch)
+    PartResult part;          // the last sharded-screen part (drephip_screen_part)
+    ExtMarks ext;             // marks for the current drephip_allpairs_device_marked call
     int link_path = 0;        // DREPHIP_LINK_PATH_*: 0 auto (sparse when it applies, else dense)
     uint32_t band_cap = 1024; // elements per row per band of the banded all-pairs kernel (clamped to its LDS budget)
     uint32_t band_round = 0;  // elements per row per value round of the band kernel (0: no rounds; A/B)
@@ -211,6 +235,21 @@ int allpairs_wait_impl(drephip_ctx *ctx);
 int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N, uint32_t row0,
                 uint32_t row1, uint32_t R, uint32_t C, uint64_t seg0, uint64_t npairs, uint16_t *d_common,
                 uint16_t *d_denom, bool force, bool band, hipStream_t st, ScreenResult *res);
+// The sharded screen (screen.hip): one hash part's marks for every row
+// (ctx->part), and a rank's rows screened from every part's marks.
+int screen_part_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N, uint32_t R,
+                     uint32_t part, uint32_t nparts, hipStream_t st, uint64_t *checks, uint32_t *nrec);
+int screen_marked_impl(drephip_ctx *ctx, const uint32_t *d_nhash, uint32_t N, uint32_t row0, uint32_t row1,
+                       uint32_t R, uint32_t C, uint64_t seg0, uint64_t npairs, uint16_t *d_common, uint16_t *d_denom,
+                       const uint32_t *d_gbm, uint32_t nparts, const uint4 *d_rec, uint64_t nrec, hipStream_t st,
+                       ScreenResult *res);
+// the dense-set rule on the whole triangle's pair checks E
+bool screen_worth(uint32_t N, uint32_t s, uint64_t E);
+// rows per row tile and the all-pairs path (table / band) the all-pairs call
+// takes for this context's s (the sharded screen's parts and ranks share it)
+int allpairs_geometry(drephip_ctx *ctx, uint32_t *R, int *path);
+int screen_mode(drephip_ctx *ctx);
+bool screen_applies(drephip_ctx *ctx, uint32_t N);
 // Every pair of the segment as an unscreened one: common 0, denominator
 // min(s, |A| + |B|); the LIST kernels then overwrite the screened pairs.
 int screen_fill_impl(drephip_ctx *ctx, const uint32_t *d_nhash, uint32_t N, uint32_t row0, uint32_t row1,

@@ -71,27 +71,146 @@ __global__ void k_screen_total(const uint32_t *__restrict__ nh, uint64_t *__rest
     if (threadIdx.x == 0) eoff[N] = eoff[N - 1] + nh[N - 1];
 }
 
-// Runs of equal keys in the sorted keys, without a serial walk: head flags
-// (k_run_flags), their inclusive scan = run id + 1 per position, the heads and
-// tails writing each run's bounds (k_run_bounds), then the runs of >= 2
-// entries appended with their first genome (k_run_collect).  (A head thread
-// walking its run measured 35.6 ms at 10^8 entries, the walks' dependent
-// loads holding every wave with a head.)
-__global__ __launch_bounds__(kScWG) void k_run_flags(const uint32_t *__restrict__ keys, uint32_t M,
-                                                     uint32_t *__restrict__ flag) {
-    for (uint32_t i = blockIdx.x * kScWG + threadIdx.x; i < M; i += gridDim.x * kScWG)
-        flag[i] = (i == 0 || keys[i - 1] != keys[i]) ? 1u : 0u;
+// one counter bump per workgroup: the waves' sums through LDS (a bump per wave
+// from thousands of workgroups serialised on the counter: ~0.2 ms)
+__device__ __forceinline__ void block_count_add(uint32_t mine, unsigned long long *counter) {
+    __shared__ uint32_t red[kScWG / 64];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mine;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < kScWG / 64; w++) t += red[w];
+        if (t) atomicAdd(counter, (unsigned long long)t);
+    }
 }
 
-__global__ __launch_bounds__(kScWG) void k_run_bounds(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ rid,
-                                                      uint32_t M, uint32_t *__restrict__ rstart,
-                                                      uint32_t *__restrict__ rend) {
-    for (uint32_t i = blockIdx.x * kScWG + threadIdx.x; i < M; i += gridDim.x * kScWG) {
-        const uint32_t k = keys[i];
-        const uint32_t r = rid[i] - 1;
-        if (i == 0 || keys[i - 1] != k) rstart[r] = i;
-        if (i + 1 == M || keys[i + 1] != k) rend[r] = i + 1;
+// Hash parts (the sharded screen, screen_part_impl): part p of P holds the
+// entries whose key (low word) lies in [p 2^32 / P, (p + 1) 2^32 / P), so a run
+// of equal keys lies in one part.  Keys are uniform (Murmur3 low words).
+__device__ __forceinline__ uint32_t key_part(uint32_t key, uint32_t nparts) {
+    return (uint32_t)(((uint64_t)key * nparts) >> 32);
+}
+// entries of genome g in the part (one workgroup per genome)
+constexpr uint32_t kPartPer = 4;
+__global__ __launch_bounds__(kScWG) void k_part_count(const uint64_t *__restrict__ H, const uint32_t *__restrict__ nh,
+                                                      uint32_t s, uint32_t part, uint32_t nparts,
+                                                      uint32_t *__restrict__ cnt) {
+    __shared__ uint32_t red[kScWG / 64];
+    const uint32_t g = blockIdx.x, n = nh[g];
+    const uint64_t *A = H + (uint64_t)g * s;
+    uint32_t c = 0;
+    for (uint32_t k = threadIdx.x; k < n; k += kScWG * kPartPer) {
+#pragma unroll
+        for (uint32_t e = 0; e < kPartPer; e++)
+            c += k + e * kScWG < n && key_part((uint32_t)A[k + e * kScWG], nparts) == part;
     }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < kScWG / 64; w++) t += red[w];
+        cnt[g] = t;
+    }
+}
+// the part's entries in genome order: the sorted runs list their genomes in
+// ascending order, as k_screen_keys' full set does.  (Within a genome the
+// order is free: a genome's entries are distinct hashes, so two of them never
+// share a run's hash.)  A step covers kScWG x kPartPer entries, loads
+// coalesced (entry k0 + e kScWG + thread); each thread's count is placed by a
+// wave scan and the waves' totals
+__global__ __launch_bounds__(kScWG) void k_part_keys(const uint64_t *__restrict__ H, const uint32_t *__restrict__ nh,
+                                                     const uint64_t *__restrict__ eoff, uint32_t s, uint32_t part,
+                                                     uint32_t nparts, uint32_t *__restrict__ keys,
+                                                     uint32_t *__restrict__ vals) {
+    __shared__ uint32_t wsum[2][kScWG / 64];
+    const uint32_t g = blockIdx.x, n = nh[g], lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t *A = H + (uint64_t)g * s;
+    uint64_t o = eoff[g];
+    int buf = 0;
+    for (uint32_t k0 = 0; k0 < n; k0 += kScWG * kPartPer) {            // uniform trip count
+        const uint32_t k = k0 + threadIdx.x;
+        uint32_t key[kPartPer], c = 0, inmask = 0;
+#pragma unroll
+        for (uint32_t e = 0; e < kPartPer; e++) {
+            key[e] = k + e * kScWG < n ? (uint32_t)A[k + e * kScWG] : 0u;
+            const bool in = k + e * kScWG < n && key_part(key[e], nparts) == part;
+            inmask |= (uint32_t)in << e;
+            c += in;
+        }
+        uint32_t inc = c;                                              // inclusive wave scan of the counts
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(inc, d, 64);
+            if (lane >= (uint32_t)d) inc += y;
+        }
+        if (lane == 63) wsum[buf][wave] = inc;
+        __syncthreads();
+        uint32_t base = inc - c, tot = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < kScWG / 64; w++) {
+            if (w < wave) base += wsum[buf][w];
+            tot += wsum[buf][w];
+        }
+        buf ^= 1;                                                      // the next step writes the other copy
+#pragma unroll
+        for (uint32_t e = 0; e < kPartPer; e++) {
+            if ((inmask >> e) & 1u) {
+                keys[o + base] = key[e];
+                vals[o + base] = g * s + k + e * kScWG;
+                base++;
+            }
+        }
+        o += tot;
+    }
+}
+
+// Runs of equal keys in the sorted keys, without a serial walk: the heads
+// (position 0 and every key change) counted per chunk of the sorted keys
+// (k_head_count), the counts scanned, and each chunk writing its heads' run
+// bounds at its offset in order (k_head_write): run r = [rstart[r], rend[r]).
+// Two read passes over the keys (round 5 wrote a head flag per position,
+// scanned all M of them and read them back: 1.1 ms at 10^8 entries).  (A head
+// thread walking its run measured 35.6 ms at 10^8 entries, the walks'
+// dependent loads holding every wave with a head.)
+__global__ __launch_bounds__(kScWG) void k_head_count(const uint32_t *__restrict__ keys, uint32_t M, uint32_t chunk,
+                                                      uint32_t *__restrict__ bcount) {
+    __shared__ uint32_t red[kScWG / 64];
+    const uint32_t i0 = blockIdx.x * chunk, i1 = min(i0 + chunk, M);
+    uint32_t c = 0;
+    for (uint32_t i = i0 + threadIdx.x; i < i1; i += kScWG) c += i == 0 || keys[i - 1] != keys[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < kScWG / 64; w++) t += red[w];
+        bcount[blockIdx.x] = t;
+    }
+}
+__device__ __forceinline__ uint32_t block_exclusive_count(bool f, uint32_t *wsum, uint32_t *total);
+__global__ __launch_bounds__(kScWG) void k_head_write(const uint32_t *__restrict__ keys, uint32_t M, uint32_t chunk,
+                                                      const uint32_t *__restrict__ boff, uint32_t nb,
+                                                      uint32_t *__restrict__ rstart, uint32_t *__restrict__ rend) {
+    __shared__ uint32_t wsum[kScWG / 64];
+    const uint32_t i0 = blockIdx.x * chunk, i1 = min(i0 + chunk, M);
+    uint32_t r0 = boff[blockIdx.x];
+    for (uint32_t ib = i0; ib < i1; ib += kScWG) {                    // uniform trip count
+        const uint32_t i = ib + threadIdx.x;
+        const bool head = i < i1 && (i == 0 || keys[i - 1] != keys[i]);
+        uint32_t tot;
+        const uint32_t r = r0 + block_exclusive_count(head, wsum, &tot);
+        if (head) {
+            rstart[r] = i;
+            if (r > 0) rend[r - 1] = i;                                // the previous run ends here
+        }
+        r0 += tot;
+    }
+    if (blockIdx.x == nb - 1 && threadIdx.x == 0) rend[boff[nb] - 1] = M;
 }
 
 // runs of >= 2 entries: (start, length) and their first (smallest) genome --
@@ -220,6 +339,95 @@ __global__ __launch_bounds__(kScWG) void k_screen_mark2(const uint32_t *__restri
     }
 }
 
+// The sharded screen's runs of two: instead of this part's own pair map, one
+// record {a, b, (i << 16) | j, 0} per run whose two entries hold one 64-bit hash
+// in two genomes (a < b; i, j their positions), for every row: the rank owning
+// row a builds the pair map from every part's records (k_screen_map2).  One
+// device counter, bumped once per wave.
+__global__ __launch_bounds__(kScWG) void k_screen_emit2(const uint32_t *__restrict__ vals, const uint64_t *__restrict__ H,
+                                                        uint32_t s, const uint32_t *__restrict__ pairs, uint32_t n2,
+                                                        uint4 *__restrict__ rec, uint32_t *__restrict__ nrec) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t q0 = blockIdx.x * kScWG; q0 < n2; q0 += gridDim.x * kScWG) {   // wave-uniform trip count
+        const uint32_t q = q0 + threadIdx.x;
+        bool ok = false;
+        uint32_t ix = 0, iy = 0, gx = 0, gy = 0;
+        if (q < n2) {
+            const uint32_t st = pairs[q];
+            ix = vals[st];
+            iy = vals[st + 1];
+            gx = ix / s;
+            gy = iy / s;
+            ok = gx != gy && H[ix] == H[iy];
+        }
+        const uint64_t m = __ballot(ok);
+        if (m == 0) continue;
+        uint32_t base = 0;
+        if (lane == (uint32_t)(__ffsll((long long)m) - 1)) base = atomicAdd(nrec, (uint32_t)__popcll(m));
+        base = __shfl(base, __ffsll((long long)m) - 1, 64);
+        if (ok) {
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+            rec[base + below] = make_uint4(gx, gy, ((ix - gx * s) << 16) | (iy - gy * s), 0u);
+        }
+    }
+}
+
+// the records of rows [row0, row1) (the pair map's size); one counter bump per wave
+__global__ __launch_bounds__(kScWG) void k_rec_count(const uint4 *__restrict__ rec, uint64_t nrec, uint32_t row0,
+                                                     uint32_t row1, unsigned long long *__restrict__ cnt) {
+    uint32_t mine = 0;
+    for (uint64_t q = (uint64_t)blockIdx.x * kScWG + threadIdx.x; q < nrec; q += (uint64_t)gridDim.x * kScWG) {
+        const uint32_t a = rec[q].x;
+        mine += a >= row0 && a < row1;
+    }
+    block_count_add(mine, cnt);
+}
+
+// the pair map of rows [row0, row1) from every part's records (k_screen_emit2):
+// the insert of k_screen_mark2
+__global__ __launch_bounds__(kScWG) void k_screen_map2(const uint4 *__restrict__ rec, uint64_t nrec, uint32_t row0,
+                                                       uint32_t row1, unsigned long long *__restrict__ pkey,
+                                                       uint32_t *__restrict__ pcnt, uint32_t *__restrict__ ppos,
+                                                       uint32_t pmask) {
+    for (uint64_t q = (uint64_t)blockIdx.x * kScWG + threadIdx.x; q < nrec; q += (uint64_t)gridDim.x * kScWG) {
+        const uint4 r = rec[q];
+        if (r.x < row0 || r.x >= row1) continue;
+        const unsigned long long key = ((unsigned long long)r.x << 32) | r.y;
+        for (uint32_t slot = pair_slot(key, pmask);; slot = (slot + 1) & pmask) {
+            const unsigned long long k = atomicCAS(&pkey[slot], kPairEmpty, key);
+            if (k == kPairEmpty) {
+                ppos[slot] = r.z;
+                atomicAdd(&pcnt[slot], 1u);
+                break;
+            }
+            if (k == key) { atomicAdd(&pcnt[slot], 1u); break; }
+        }
+    }
+}
+
+// The rank's bitmap from every part's: the parts mark (row tile, column) cells
+// with row tiles counted from row 0 (tile T = rows [T R, (T + 1) R)); this
+// rank's tiles start at row0.  Local tile t's word w is the OR, over the
+// parts, of the global tiles holding its rows -- a superset of its cells when
+// row0 is not a multiple of R (an extra cell costs kernel work, never
+// exactness: the kernels rewrite every pair of a marked cell).
+__global__ __launch_bounds__(kScWG) void k_screen_remap(const uint32_t *__restrict__ gbm, uint32_t nparts,
+                                                        uint32_t ntg, uint32_t NW, uint32_t row0, uint32_t row1,
+                                                        uint32_t rshift, uint32_t ntiles,
+                                                        uint32_t *__restrict__ bm) {
+    const uint64_t nwords = (uint64_t)ntiles * NW, gwords = (uint64_t)ntg * NW;
+    for (uint64_t wi = (uint64_t)blockIdx.x * kScWG + threadIdx.x; wi < nwords; wi += (uint64_t)gridDim.x * kScWG) {
+        const uint32_t t = (uint32_t)(wi / NW), w = (uint32_t)(wi % NW);
+        const uint32_t ra = row0 + (t << rshift);
+        const uint32_t rb = min(row1, ra + (1u << rshift)) - 1;
+        const uint32_t T0 = ra >> rshift, T1 = min(rb >> rshift, ntg - 1);
+        uint32_t v = 0;
+        for (uint32_t p = 0; p < nparts; p++)
+            for (uint32_t T = T0; T <= T1; T++) v |= gbm[p * gwords + (uint64_t)T * NW + w];
+        bm[wi] = v;
+    }
+}
+
 // The pair map: a pair held by one run of two with both sketches full shares
 // exactly one hash unless a longer run holds it too -- and then that run has
 // marked its cell -- so when its cell is unmarked its count is written here,
@@ -258,9 +466,7 @@ __global__ __launch_bounds__(kScWG) void k_screen_simple(const unsigned long lon
         common[o] = (uint16_t)(((pos >> 16) + (pos & 0xFFFFu)) < s ? 1 : 0);
         mine++;
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
-    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(nsimple, (unsigned long long)mine);
+    block_count_add(mine, nsimple);
 }
 
 // Marking, one workgroup per chunk of kMarkChunk runs taken in order of their
@@ -276,6 +482,9 @@ __global__ __launch_bounds__(kScWG) void k_screen_simple(const unsigned long lon
 // The x entries are in ascending genome order, so lanes of one row tile are
 // adjacent: only the first ok lane of each tile marks (one LDS atomic per
 // tile and y, none on a shared word).
+#ifndef DREPHIP_SC_ABL
+#define DREPHIP_SC_ABL 0    // timing ablations (never the product): 1 no marking by same-hash runs, 2 no same-hash check
+#endif
 constexpr uint32_t kMarkWG = 1024;
 constexpr uint32_t kMarkChunk = 256;
 constexpr uint32_t kMarkTiles = 128;
@@ -334,13 +543,18 @@ __global__ __launch_bounds__(kMarkWG) void k_screen_mark(const uint32_t *__restr
         const uint32_t start = run.x, m = run.y;
         // a run whose entries all hold one 64-bit hash (a hash shared by m
         // genomes; only a low-word collision breaks this) takes the fast path
-        const uint64_t v0 = H[vals[start]];
         bool same = true;
+#if DREPHIP_SC_ABL != 2
+        const uint64_t v0 = H[vals[start]];
         for (uint32_t b = 0; b < m && same; b += 64) {
             const uint32_t x = b + lane;
             const uint64_t v = x < m ? H[vals[start + x]] : v0;
             same = __ballot(v != v0) == 0;
         }
+#endif
+#if DREPHIP_SC_ABL == 1
+        if (same) continue;
+#endif
         uint32_t tcarry = 0xFFFFFFFFu;                       // the previous x block's last row tile
         for (uint32_t xb = 0; xb + 1 < m; xb += 64) {
             const uint32_t x = xb + lane;
@@ -486,9 +700,7 @@ __global__ __launch_bounds__(kScWG) void k_screen_light(const uint32_t *__restri
         }
         if (heavy) atomicOr(bmH + wi, heavy);
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
-    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(nlight, (unsigned long long)mine);
+    block_count_add(mine, nlight);
 }
 
 // per row tile (one workgroup): marked columns -> cnt[t], items -> itc[t]
@@ -609,42 +821,53 @@ static int hip_scan(drephip_ctx *ctx, const char *name, const I *in, T *out, uin
     return DREPHIP_OK;
 }
 
-int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N, uint32_t row0,
-                uint32_t row1, uint32_t R, uint32_t C, uint64_t seg0, uint64_t npairs, uint16_t *d_common,
-                uint16_t *d_denom, bool force, bool band, hipStream_t st, ScreenResult *res) {
-    *res = ScreenResult{};
+// ---------------------------------------------------------------- host phases
+// front: the entries (all, or one hash part's) grouped by key, and their runs
+struct ScreenFront {
+    uint32_t M = 0;                 // entries grouped
+    uint32_t nr = 0;                // distinct keys
+    uint32_t n2 = 0, nruns = 0;     // runs of two; of three or more
+    uint64_t E = 0;                 // pair checks of the runs: sum of m (m - 1) / 2
+    uint32_t *v_out = nullptr;      // entry values g s + k in key order
+    uint2 *runs = nullptr;          // {start, length} of the runs of >= 3
+    uint32_t *rfirst = nullptr, *ridx = nullptr;      // their first genome, index (unsorted)
+    uint32_t *pairs = nullptr;      // start of each run of two
+};
+
+static int screen_front(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N,
+                        uint32_t part, uint32_t nparts, hipStream_t st, ScreenProf &prof, ScreenFront *F) {
     const uint32_t s = ctx->s;
-    if ((uint64_t)N * s >= (1ull << 32)) return DREPHIP_OK;          // entry values g * s + k are 32-bit
     int rc;
     uint64_t *d_eoff, *h_tot;
+    uint32_t *d_pcnt = nullptr;
     if ((rc = scratch(ctx, "sc_eoff", (N + 1) * 8ull, (void **)&d_eoff))) return rc;
     if ((rc = pinned_host(ctx, "sc_tot", 64, (void **)&h_tot))) return rc;
-    timing_mark(ctx, 4, st, true);
-    ScreenProf prof;
-    prof.mark("start", st);
-    if ((rc = hip_scan(ctx, "sc_scan_tmp0", d_nhash, d_eoff, N, st))) return rc;
-    hipLaunchKernelGGL(k_screen_total, dim3(1), dim3(64), 0, st, d_nhash, d_eoff, N);
+    if (nparts > 1) {
+        // the part's entries per genome, then their offsets
+        if ((rc = scratch(ctx, "sc_part_cnt", (N + 1) * 4ull, (void **)&d_pcnt))) return rc;
+        hipLaunchKernelGGL(k_part_count, dim3(N), dim3(kScWG), 0, st, d_hashes, d_nhash, s, part, nparts, d_pcnt);
+        if ((rc = hip_scan(ctx, "sc_scan_tmp0", (const uint32_t *)d_pcnt, d_eoff, N, st))) return rc;
+        hipLaunchKernelGGL(k_screen_total, dim3(1), dim3(64), 0, st, d_pcnt, d_eoff, N);
+    } else {
+        if ((rc = hip_scan(ctx, "sc_scan_tmp0", d_nhash, d_eoff, N, st))) return rc;
+        hipLaunchKernelGGL(k_screen_total, dim3(1), dim3(64), 0, st, d_nhash, d_eoff, N);
+    }
     HIPC(hipMemcpyAsync(h_tot, d_eoff + N, 8, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));
     const uint32_t M = (uint32_t)h_tot[0];
-    if (M < 2) {
-        // fewer than two sketch entries: no pair shares a hash; every pair
-        // gets the no-shared-hash fill, no LIST work
-        if ((rc = screen_fill_impl(ctx, d_nhash, N, row0, row1, seg0, npairs, d_common, d_denom, st))) return rc;
-        timing_mark(ctx, 4, st, false);
-        res->entries = M;
-        res->use = true;
-        return DREPHIP_OK;
-    }
+    F->M = M;
+    if (M < 2) return DREPHIP_OK;
     uint32_t *k_in, *k_out, *v_in, *v_out;
-    uint2 *d_runs;
     if ((rc = scratch(ctx, "sc_kin", M * 4ull + 16, (void **)&k_in))) return rc;
     if ((rc = scratch(ctx, "sc_kout", M * 4ull + 16, (void **)&k_out))) return rc;
     if ((rc = scratch(ctx, "sc_vin", M * 4ull + 16, (void **)&v_in))) return rc;
     if ((rc = scratch(ctx, "sc_vout", M * 4ull + 16, (void **)&v_out))) return rc;
-    if ((rc = scratch(ctx, "sc_runs", (M / 2 + 1) * 8ull, (void **)&d_runs))) return rc;
+    if ((rc = scratch(ctx, "sc_runs", (M / 2 + 1) * 8ull, (void **)&F->runs))) return rc;
     prof.mark("offsets+alloc", st);
-    hipLaunchKernelGGL(k_screen_keys, dim3(N), dim3(kScWG), 0, st, d_hashes, d_nhash, d_eoff, s, k_in, v_in);
+    if (nparts > 1)
+        hipLaunchKernelGGL(k_part_keys, dim3(N), dim3(kScWG), 0, st, d_hashes, d_nhash, d_eoff, s, part, nparts, k_in, v_in);
+    else
+        hipLaunchKernelGGL(k_screen_keys, dim3(N), dim3(kScWG), 0, st, d_hashes, d_nhash, d_eoff, s, k_in, v_in);
     prof.mark("keys", st);
     {
         size_t tb = 0;
@@ -654,45 +877,43 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
         HIPC(hipcub::DeviceRadixSort::SortPairs(tmp, tb, k_in, k_out, v_in, v_out, M, 0, 32, st));
     }
     prof.mark("sort", st);
-    const uint32_t rgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, (M + kScWG - 1) / kScWG));
-    // runs: flags -> run ids (scan) -> bounds -> runs of >= 2 with their first genome
-    uint32_t *flag = k_in, *rid = v_in, *rstart, *rend, *rfirst, *ridx, *rfirst_s, *ridx_s;
+    // runs: heads counted per chunk -> offsets -> run bounds
+    uint32_t *rstart, *rend, *hcnt, *hoff;
     if ((rc = scratch(ctx, "sc_rstart", M * 4ull + 16, (void **)&rstart))) return rc;
     if ((rc = scratch(ctx, "sc_rend", M * 4ull + 16, (void **)&rend))) return rc;
-    hipLaunchKernelGGL(k_run_flags, dim3(rgrid), dim3(kScWG), 0, st, k_out, M, flag);
-    {
-        size_t tb = 0;
-        HIPC(hipcub::DeviceScan::InclusiveSum(nullptr, tb, flag, rid, M, st));
-        void *tmp;
-        if ((rc = scratch(ctx, "sc_scan_tmp3", std::max<size_t>(tb, 16), &tmp))) return rc;
-        HIPC(hipcub::DeviceScan::InclusiveSum(tmp, tb, flag, rid, M, st));
-    }
-    hipLaunchKernelGGL(k_run_bounds, dim3(rgrid), dim3(kScWG), 0, st, k_out, rid, M, rstart, rend);
-    HIPC(hipMemcpyAsync(h_tot, rid + (M - 1), 4, hipMemcpyDeviceToHost, st));
+    const uint32_t hchunk = std::max<uint32_t>(4096, (M + 8191) / 8192);
+    const uint32_t nhb = (M + hchunk - 1) / hchunk;
+    if ((rc = scratch(ctx, "sc_hcnt", (nhb + 1) * 4ull, (void **)&hcnt))) return rc;
+    if ((rc = scratch(ctx, "sc_hoff", (nhb + 1) * 4ull, (void **)&hoff))) return rc;
+    HIPC(hipMemsetAsync(hcnt + nhb, 0, 4, st));
+    hipLaunchKernelGGL(k_head_count, dim3(nhb), dim3(kScWG), 0, st, k_out, M, hchunk, hcnt);
+    if ((rc = hip_scan(ctx, "sc_scan_tmp3", hcnt, hoff, nhb + 1, st))) return rc;
+    hipLaunchKernelGGL(k_head_write, dim3(nhb), dim3(kScWG), 0, st, k_out, M, hchunk, hoff, nhb, rstart, rend);
+    HIPC(hipMemcpyAsync(h_tot, hoff + nhb, 4, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));
+    uint32_t *flag = k_in, *rid = v_in;                           // free after the sort
     const uint32_t nr = ((const uint32_t *)h_tot)[0];             // distinct keys
+    F->nr = nr;
     // the run lists (at most M / 2 runs of >= 2); rfirst / ridx reuse the key
     // and value inputs of the sort, which are free now
-    rfirst = flag;
-    ridx = rid;
-    if ((rc = scratch(ctx, "sc_rfirst_s", (M / 2 + 1) * 4ull, (void **)&rfirst_s))) return rc;
-    if ((rc = scratch(ctx, "sc_ridx_s", (M / 2 + 1) * 4ull, (void **)&ridx_s))) return rc;
+    F->rfirst = flag;
+    F->ridx = rid;
     const uint32_t per = (nr + kRunBlocks - 1) / kRunBlocks;
-    uint32_t *bcnt2, *bcnt3, *boff2, *boff3, *d_pairs;
+    uint32_t *bcnt2, *bcnt3, *boff2, *boff3;
     unsigned long long *bchk;
     if ((rc = scratch(ctx, "sc_bcnt2", (kRunBlocks + 1) * 4ull, (void **)&bcnt2))) return rc;
     if ((rc = scratch(ctx, "sc_bcnt3", (kRunBlocks + 1) * 4ull, (void **)&bcnt3))) return rc;
     if ((rc = scratch(ctx, "sc_boff2", (kRunBlocks + 1) * 4ull, (void **)&boff2))) return rc;
     if ((rc = scratch(ctx, "sc_boff3", (kRunBlocks + 1) * 4ull, (void **)&boff3))) return rc;
     if ((rc = scratch(ctx, "sc_bchk", kRunBlocks * 8ull, (void **)&bchk))) return rc;
-    if ((rc = scratch(ctx, "sc_pairs", (M / 2 + 1) * 4ull, (void **)&d_pairs))) return rc;
+    if ((rc = scratch(ctx, "sc_pairs", (M / 2 + 1) * 4ull, (void **)&F->pairs))) return rc;
     HIPC(hipMemsetAsync(bcnt2 + kRunBlocks, 0, 4, st));
     HIPC(hipMemsetAsync(bcnt3 + kRunBlocks, 0, 4, st));
     hipLaunchKernelGGL(k_run_count, dim3(kRunBlocks), dim3(kScWG), 0, st, rstart, rend, nr, per, bcnt2, bcnt3, bchk);
     if ((rc = hip_scan(ctx, "sc_scan_tmp4", bcnt2, boff2, kRunBlocks + 1, st))) return rc;
     if ((rc = hip_scan(ctx, "sc_scan_tmp5", bcnt3, boff3, kRunBlocks + 1, st))) return rc;
     hipLaunchKernelGGL(k_run_write, dim3(kRunBlocks), dim3(kScWG), 0, st, rstart, rend, nr, per, boff2, boff3, v_out, s,
-                       d_pairs, d_runs, rfirst, ridx);
+                       F->pairs, F->runs, F->rfirst, F->ridx);
     HIPC(hipGetLastError());
     unsigned long long *h_chk;
     if ((rc = pinned_host(ctx, "sc_chk", kRunBlocks * 8ull, (void **)&h_chk))) return rc;
@@ -701,106 +922,70 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
     HIPC(hipMemcpyAsync((uint32_t *)h_tot + 1, boff3 + kRunBlocks, 4, hipMemcpyDeviceToHost, st));
     prof.mark("runs", st);
     HIPC(hipStreamSynchronize(st));
-    const uint32_t n2 = ((const uint32_t *)h_tot)[0];           // runs of two entries
-    const uint32_t nruns = ((const uint32_t *)h_tot)[1];        // runs of three or more
+    F->n2 = ((const uint32_t *)h_tot)[0];                         // runs of two entries
+    F->nruns = ((const uint32_t *)h_tot)[1];                      // runs of three or more
     uint64_t E = 0;
     for (uint32_t b = 0; b < kRunBlocks; b++) E += h_chk[b];
-    res->entries = M;
-    res->runs = (uint64_t)n2 + nruns;
-    res->checks = E;
-    // dense set: a pair check costs about as much as a few probes of the
-    // dense kernels, which make ~s/2 probes per pair (DREPHIP_SCREEN_RATIO
-    // scales the bound; `force` skips it).  E counts the checks of the whole
-    // triangle (every rank groups all N s entries), so it is weighed against
-    // the whole triangle's pairs, not this segment's: every rank of a sharded
-    // job, and the one-GPU call, take the same path
-    const char *re = getenv("DREPHIP_SCREEN_RATIO");
-    const double ratio = re ? atof(re) : 16.0;
-    const double all_pairs = (double)N * (double)(N - 1) / 2.0;
-    if (!force && (double)E * ratio > all_pairs * s) { timing_mark(ctx, 4, st, false); return DREPHIP_OK; }
+    F->E = E;
+    F->v_out = v_out;
+    return DREPHIP_OK;
+}
 
-    const uint32_t rows = row1 - row0;
-    const uint32_t ntiles = (rows + R - 1) / R;
-    const uint32_t NW = (N + 31) / 32;
-    uint32_t rshift = 0;
-    while ((1u << rshift) < R) rshift++;
-    uint32_t *d_bm, *d_cnt, *d_itc;
-    uint64_t *d_coff, *d_cnt64;
-    if ((rc = scratch(ctx, "sc_bitmap", (uint64_t)ntiles * NW * 4, (void **)&d_bm))) return rc;
-    // Light cells (k_screen_light): a heavy-cell bitmap and each cell's first
-    // marking run, (ntiles x N) words -- taken when that fits kLightBudget
-    // (N = 10^4 with R = 4: 100 MB), for the band kernel only: at configs[4]
-    // its LIST time 9.0 -> 4.0 ms for +0.9 ms of screen; at configs[2] (the q
-    // kernel, s = 1000) 0.39 -> 0.35 ms of LIST for +0.33 ms of screen
-    // (profiles/r05_screen_light_c2_ab.txt).  DREPHIP_SCREEN_LIGHT=0/1 forces it (A/B)
-    const char *le = getenv("DREPHIP_SCREEN_LIGHT");
-    const bool light = (le ? atoi(le) != 0 : band) && (uint64_t)ntiles * N * 4 <= kLightBudget;
-    uint32_t *d_bmH = nullptr, *d_crun = nullptr;
-    if (light) {
-        if ((rc = scratch(ctx, "sc_bitmap_heavy", (uint64_t)ntiles * NW * 4, (void **)&d_bmH))) return rc;
-        if ((rc = scratch(ctx, "sc_crun", (uint64_t)ntiles * N * 4, (void **)&d_crun))) return rc;
-    }
+// the runs of >= 3 in first-genome order, marked into bm (row tiles from row0)
+static int screen_mark_runs(drephip_ctx *ctx, const ScreenFront &F, const uint64_t *d_hashes, uint32_t N,
+                            uint32_t row0, uint32_t row1, uint32_t rshift, uint32_t NW, uint32_t *d_bm,
+                            uint32_t *d_bmH, uint32_t *d_crun, hipStream_t st, ScreenProf &prof) {
+    if (!F.nruns) return DREPHIP_OK;
+    const uint32_t s = ctx->s, M = F.M;
+    int rc;
+    uint32_t *rfirst_s, *ridx_s;
+    if ((rc = scratch(ctx, "sc_rfirst_s", (M / 2 + 1) * 4ull, (void **)&rfirst_s))) return rc;
+    if ((rc = scratch(ctx, "sc_ridx_s", (M / 2 + 1) * 4ull, (void **)&ridx_s))) return rc;
+    size_t tb = 0;
+    HIPC(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, F.rfirst, rfirst_s, F.ridx, ridx_s, F.nruns, 0, 32, st));
+    void *tmp;
+    if ((rc = scratch(ctx, "sc_sort_tmp2", std::max<size_t>(tb, 16), &tmp))) return rc;
+    HIPC(hipcub::DeviceRadixSort::SortPairs(tmp, tb, F.rfirst, rfirst_s, F.ridx, ridx_s, F.nruns, 0, 32, st));
+    prof.mark("run-sort", st);
+    const dim3 grid((F.nruns + kMarkChunk - 1) / kMarkChunk);
+    if (d_bmH)
+        hipLaunchKernelGGL(k_screen_mark<true>, grid, dim3(kMarkWG), 0, st, F.v_out, d_hashes, s, F.runs, ridx_s,
+                           rfirst_s, F.nruns, row0, row1, rshift, NW, d_bm, d_bmH, d_crun, N);
+    else
+        hipLaunchKernelGGL(k_screen_mark<false>, grid, dim3(kMarkWG), 0, st, F.v_out, d_hashes, s, F.runs, ridx_s,
+                           rfirst_s, F.nruns, row0, row1, rshift, NW, d_bm, nullptr, nullptr, N);
+    HIPC(hipGetLastError());
+    return DREPHIP_OK;
+}
+
+// the pair map (pcap slots, a power of two) cleared
+static int screen_pair_map(drephip_ctx *ctx, uint64_t n, hipStream_t st, uint64_t *pcap_out,
+                           unsigned long long **pkey, uint32_t **pcnt, uint32_t **ppos) {
+    uint64_t pcap = 1024;
+    while (pcap < 2ull * n) pcap <<= 1;
+    *pcap_out = pcap;
+    if (pcap > kMaxPairMap) return DREPHIP_OK;                       // too large: the caller gives way
+    int rc;
+    if ((rc = scratch(ctx, "sc_pkey", pcap * 8ull, (void **)pkey))) return rc;
+    if ((rc = scratch(ctx, "sc_pcnt", pcap * 4ull, (void **)pcnt))) return rc;
+    if ((rc = scratch(ctx, "sc_ppos", pcap * 4ull, (void **)ppos))) return rc;
+    HIPC(hipMemsetAsync(*pkey, 0xFF, pcap * 8ull, st));
+    HIPC(hipMemsetAsync(*pcnt, 0, pcap * 4ull, st));
+    return DREPHIP_OK;
+}
+
+// marked cells (d_bl) -> each row tile's column list and the LIST items
+static int screen_lists(drephip_ctx *ctx, const uint32_t *d_bl, uint32_t ntiles, uint32_t NW, uint32_t C,
+                        uint32_t row0, uint32_t R, const unsigned long long *d_nsimple, hipStream_t st,
+                        ScreenProf &prof, ScreenResult *res) {
+    int rc;
+    uint32_t *d_cnt, *d_itc;
+    uint64_t *d_coff, *d_cnt64, *h_tot;
+    if ((rc = pinned_host(ctx, "sc_tot", 64, (void **)&h_tot))) return rc;
     if ((rc = scratch(ctx, "sc_tcnt", (ntiles + 1) * 4ull, (void **)&d_cnt))) return rc;
     if ((rc = scratch(ctx, "sc_tcnt64", (ntiles + 1) * 8ull, (void **)&d_cnt64))) return rc;
     if ((rc = scratch(ctx, "sc_titc", (ntiles + 1) * 4ull, (void **)&d_itc))) return rc;
     if ((rc = scratch(ctx, "sc_coff", (ntiles + 1) * 8ull, (void **)&d_coff))) return rc;
-    // the pair map of the runs of two (k_screen_mark2), twice their count; a
-    // map beyond kMaxPairMap slots (16 B each) is not built: the dense path runs
-    uint64_t pcap = 1024;
-    while (pcap < 2ull * n2) pcap <<= 1;
-    if (pcap > kMaxPairMap) { timing_mark(ctx, 4, st, false); return DREPHIP_OK; }
-    unsigned long long *pkey, *d_nsimple;
-    uint32_t *pcnt, *ppos;
-    if ((rc = scratch(ctx, "sc_pkey", pcap * 8ull, (void **)&pkey))) return rc;
-    if ((rc = scratch(ctx, "sc_pcnt", pcap * 4ull, (void **)&pcnt))) return rc;
-    if ((rc = scratch(ctx, "sc_ppos", pcap * 4ull, (void **)&ppos))) return rc;
-    if ((rc = scratch(ctx, "sc_nsimple", 8, (void **)&d_nsimple))) return rc;
-    prof.mark("readback+alloc", st);
-    // every pair as no-shared-hash first: the simple pairs are written over it
-    // below, the LIST kernel over both
-    if ((rc = screen_fill_impl(ctx, d_nhash, N, row0, row1, seg0, npairs, d_common, d_denom, st))) return rc;
-    prof.mark("fill", st);
-    HIPC(hipMemsetAsync(d_bm, 0, (uint64_t)ntiles * NW * 4, st));
-    if (light) HIPC(hipMemsetAsync(d_bmH, 0, (uint64_t)ntiles * NW * 4, st));
-    HIPC(hipMemsetAsync(pkey, 0xFF, pcap * 8ull, st));
-    HIPC(hipMemsetAsync(pcnt, 0, pcap * 4ull, st));
-    HIPC(hipMemsetAsync(d_nsimple, 0, 8, st));
-    prof.mark("bitmap-clear", st);
-    if (nruns) {
-        // runs in order of their first genome (a family's runs together)
-        size_t tb = 0;
-        HIPC(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, rfirst, rfirst_s, ridx, ridx_s, nruns, 0, 32, st));
-        void *tmp;
-        if ((rc = scratch(ctx, "sc_sort_tmp2", std::max<size_t>(tb, 16), &tmp))) return rc;
-        HIPC(hipcub::DeviceRadixSort::SortPairs(tmp, tb, rfirst, rfirst_s, ridx, ridx_s, nruns, 0, 32, st));
-        prof.mark("run-sort", st);
-        if (light)
-            hipLaunchKernelGGL(k_screen_mark<true>, dim3((nruns + kMarkChunk - 1) / kMarkChunk), dim3(kMarkWG), 0, st,
-                               v_out, d_hashes, s, d_runs, ridx_s, rfirst_s, nruns, row0, row1, rshift, NW, d_bm, d_bmH,
-                               d_crun, N);
-        else
-            hipLaunchKernelGGL(k_screen_mark<false>, dim3((nruns + kMarkChunk - 1) / kMarkChunk), dim3(kMarkWG), 0, st,
-                               v_out, d_hashes, s, d_runs, ridx_s, rfirst_s, nruns, row0, row1, rshift, NW, d_bm, nullptr,
-                               nullptr, N);
-    }
-    if (n2) {
-        const uint32_t g2 = std::max(1u, std::min(8192u, (n2 + kScWG - 1) / kScWG));
-        hipLaunchKernelGGL(k_screen_mark2, dim3(g2), dim3(kScWG), 0, st, v_out, d_hashes, s, d_pairs, n2, row0, row1,
-                           pkey, pcnt, ppos, (uint32_t)(pcap - 1));
-        const uint32_t gs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, (pcap + kScWG - 1) / kScWG));
-        hipLaunchKernelGGL(k_screen_simple, dim3(gs), dim3(kScWG), 0, st, pkey, pcnt, ppos, (uint32_t)pcap, d_nhash, s, N, row0,
-                           rshift, NW, seg0, d_bm, d_bmH, d_common, d_nsimple);
-    }
-    prof.mark("mark", st);
-    if (light && nruns) {
-        const uint64_t nwords = (uint64_t)ntiles * NW;
-        const uint32_t gl = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(16384, (nwords + kScWG - 1) / kScWG));
-        hipLaunchKernelGGL(k_screen_light, dim3(gl), dim3(kScWG), 0, st, d_bm, d_bmH, d_crun, d_runs, v_out, d_nhash, s, N,
-                           row0, row1, R, NW, nwords, seg0, d_common, d_nsimple);
-        prof.mark("light", st);
-    }
-    // the LIST kernels take the heavy cells (every marked cell without the light screen)
-    const uint32_t *d_bl = light ? d_bmH : d_bm;
     hipLaunchKernelGGL(k_screen_count, dim3(ntiles), dim3(kScWG), 0, st, d_bl, NW, C, d_cnt, d_cnt64, d_itc);
     // the last entry of each scan holds the totals: count entries ntiles + 1, the last one zero.
     // The column offsets are summed in 64 bits (the marked cells may pass 2^32;
@@ -836,7 +1021,7 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
         h_tot[1] = 8 * lmax;
     }
     const uint64_t nitems = h_tot[1];
-    if (marked >= (1ull << 32) || nitems >= (1ull << 31)) { timing_mark(ctx, 4, st, false); return DREPHIP_OK; }
+    if (marked >= (1ull << 32) || nitems >= (1ull << 31)) return DREPHIP_OK;     // res->use stays false
     uint32_t *d_list, *d_ibase;
     uint4 *d_items;
     if ((rc = scratch(ctx, "sc_list", std::max<uint64_t>(marked, 1) * 4, (void **)&d_list))) return rc;
@@ -849,13 +1034,231 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
     hipLaunchKernelGGL(k_screen_lists, dim3(ntiles), dim3(kScWG), 0, st, d_bl, NW, C, row0, R, d_cnt, d_coff, d_ibase,
                        d_list, d_items, de ? atoi(de) : 0);
     prof.mark("lists", st);
-    timing_mark(ctx, 4, st, false);
     HIPC(hipGetLastError());
     res->use = true;
     res->clist = d_list;
     res->items = d_items;
     res->nitems = (uint32_t)nitems;
     return DREPHIP_OK;
+}
+
+static uint32_t tile_shift(uint32_t R) {
+    uint32_t rshift = 0;
+    while ((1u << rshift) < R) rshift++;
+    return rshift;
+}
+
+// the dense-set rule: a pair check costs about as much as a few probes of the
+// dense kernels, which make ~s/2 probes per pair (DREPHIP_SCREEN_RATIO scales
+// the bound).  E counts the checks of the whole triangle (every entry is
+// grouped), weighed against the whole triangle's pairs: every rank of a
+// sharded job, and the one-GPU call, take the same path
+bool screen_worth(uint32_t N, uint32_t s, uint64_t E) {
+    const char *re = getenv("DREPHIP_SCREEN_RATIO");
+    const double ratio = re ? atof(re) : 16.0;
+    const double all_pairs = (double)N * (double)(N - 1) / 2.0;
+    return (double)E * ratio <= all_pairs * s;
+}
+
+int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N, uint32_t row0,
+                uint32_t row1, uint32_t R, uint32_t C, uint64_t seg0, uint64_t npairs, uint16_t *d_common,
+                uint16_t *d_denom, bool force, bool band, hipStream_t st, ScreenResult *res) {
+    *res = ScreenResult{};
+    const uint32_t s = ctx->s;
+    if ((uint64_t)N * s >= (1ull << 32)) return DREPHIP_OK;          // entry values g * s + k are 32-bit
+    int rc;
+    timing_mark(ctx, 4, st, true);
+    ScreenProf prof;
+    prof.mark("start", st);
+    ScreenFront F;
+    if ((rc = screen_front(ctx, d_hashes, d_nhash, N, 0, 1, st, prof, &F))) return rc;
+    if (F.M < 2) {
+        // fewer than two sketch entries: no pair shares a hash; every pair
+        // gets the no-shared-hash fill, no LIST work
+        if ((rc = screen_fill_impl(ctx, d_nhash, N, row0, row1, seg0, npairs, d_common, d_denom, st))) return rc;
+        timing_mark(ctx, 4, st, false);
+        res->entries = F.M;
+        res->use = true;
+        return DREPHIP_OK;
+    }
+    res->entries = F.M;
+    res->runs = (uint64_t)F.n2 + F.nruns;
+    res->checks = F.E;
+    if (!force && !screen_worth(N, s, F.E)) { timing_mark(ctx, 4, st, false); return DREPHIP_OK; }
+
+    const uint32_t rows = row1 - row0;
+    const uint32_t ntiles = (rows + R - 1) / R;
+    const uint32_t NW = (N + 31) / 32;
+    const uint32_t rshift = tile_shift(R);
+    uint32_t *d_bm;
+    if ((rc = scratch(ctx, "sc_bitmap", (uint64_t)ntiles * NW * 4, (void **)&d_bm))) return rc;
+    // Light cells (k_screen_light): a heavy-cell bitmap and each cell's first
+    // marking run, (ntiles x N) words -- taken when that fits kLightBudget
+    // (N = 10^4 with R = 4: 100 MB), for the band kernel only: at configs[4]
+    // its LIST time 9.0 -> 4.0 ms for +0.9 ms of screen; at configs[2] (the q
+    // kernel, s = 1000) 0.39 -> 0.35 ms of LIST for +0.33 ms of screen
+    // (profiles/r05_screen_light_c2_ab.txt).  DREPHIP_SCREEN_LIGHT=0/1 forces it (A/B)
+    const char *le = getenv("DREPHIP_SCREEN_LIGHT");
+    const bool light = (le ? atoi(le) != 0 : band) && (uint64_t)ntiles * N * 4 <= kLightBudget;
+    uint32_t *d_bmH = nullptr, *d_crun = nullptr;
+    if (light) {
+        if ((rc = scratch(ctx, "sc_bitmap_heavy", (uint64_t)ntiles * NW * 4, (void **)&d_bmH))) return rc;
+        if ((rc = scratch(ctx, "sc_crun", (uint64_t)ntiles * N * 4, (void **)&d_crun))) return rc;
+    }
+    // the pair map of the runs of two (k_screen_mark2), twice their count; a
+    // map beyond kMaxPairMap slots (16 B each) is not built: the dense path runs
+    uint64_t pcap;
+    unsigned long long *pkey = nullptr, *d_nsimple;
+    uint32_t *pcnt = nullptr, *ppos = nullptr;
+    if ((rc = screen_pair_map(ctx, F.n2, st, &pcap, &pkey, &pcnt, &ppos))) return rc;
+    if (pcap > kMaxPairMap) { timing_mark(ctx, 4, st, false); return DREPHIP_OK; }
+    if ((rc = scratch(ctx, "sc_nsimple", 8, (void **)&d_nsimple))) return rc;
+    prof.mark("readback+alloc", st);
+    // every pair as no-shared-hash first: the simple pairs are written over it
+    // below, the LIST kernel over both
+    if ((rc = screen_fill_impl(ctx, d_nhash, N, row0, row1, seg0, npairs, d_common, d_denom, st))) return rc;
+    prof.mark("fill", st);
+    HIPC(hipMemsetAsync(d_bm, 0, (uint64_t)ntiles * NW * 4, st));
+    if (light) HIPC(hipMemsetAsync(d_bmH, 0, (uint64_t)ntiles * NW * 4, st));
+    HIPC(hipMemsetAsync(d_nsimple, 0, 8, st));
+    prof.mark("bitmap-clear", st);
+    if ((rc = screen_mark_runs(ctx, F, d_hashes, N, row0, row1, rshift, NW, d_bm, d_bmH, d_crun, st, prof))) return rc;
+    if (F.n2) {
+        const uint32_t g2 = std::max(1u, std::min(8192u, (F.n2 + kScWG - 1) / kScWG));
+        hipLaunchKernelGGL(k_screen_mark2, dim3(g2), dim3(kScWG), 0, st, F.v_out, d_hashes, s, F.pairs, F.n2, row0, row1,
+                           pkey, pcnt, ppos, (uint32_t)(pcap - 1));
+        const uint32_t gs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(2048, (pcap + kScWG - 1) / kScWG));
+        hipLaunchKernelGGL(k_screen_simple, dim3(gs), dim3(kScWG), 0, st, pkey, pcnt, ppos, (uint32_t)pcap, d_nhash, s, N, row0,
+                           rshift, NW, seg0, d_bm, d_bmH, d_common, d_nsimple);
+    }
+    prof.mark("mark", st);
+    if (light && F.nruns) {
+        const uint64_t nwords = (uint64_t)ntiles * NW;
+        const uint32_t gl = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(4096, (nwords + kScWG - 1) / kScWG));
+        hipLaunchKernelGGL(k_screen_light, dim3(gl), dim3(kScWG), 0, st, d_bm, d_bmH, d_crun, F.runs, F.v_out, d_nhash, s, N,
+                           row0, row1, R, NW, nwords, seg0, d_common, d_nsimple);
+        prof.mark("light", st);
+    }
+    // the LIST kernels take the heavy cells (every marked cell without the light screen)
+    rc = screen_lists(ctx, light ? d_bmH : d_bm, ntiles, NW, C, row0, R, d_nsimple, st, prof, res);
+    timing_mark(ctx, 4, st, false);
+    return rc;
+}
+
+// ------------------------------------------------------- the sharded screen
+// Part `part` of `nparts` hash ranges (one per rank of a sharded job): its
+// entries grouped, its runs of >= 3 marked into a bitmap of row tiles of R
+// rows counted from row 0 -- every row, not only this rank's -- and its runs of
+// two listed as records.  The caller exchanges every part's bitmap and records
+// (drephip_screen_part_copy), and each rank finishes its rows from all of
+// them (screen_marked_impl).  Results stay in the context's scratch until the
+// next screen call.
+int screen_part_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N, uint32_t R,
+                     uint32_t part, uint32_t nparts, hipStream_t st, uint64_t *checks, uint32_t *nrec) {
+    const uint32_t s = ctx->s;
+    *checks = 0;
+    *nrec = 0;
+    ctx->part = PartResult{};
+    if ((uint64_t)N * s >= (1ull << 32)) { set_error("the screen needs N x s < 2^32"); return DREPHIP_ERR_UNSUPPORTED; }
+    int rc;
+    timing_mark(ctx, 4, st, true);
+    ScreenProf prof;
+    prof.mark("start", st);
+    ScreenFront F;
+    if ((rc = screen_front(ctx, d_hashes, d_nhash, N, part, nparts, st, prof, &F))) return rc;
+    const uint32_t NW = (N + 31) / 32, ntg = (N + R - 1) / R, rshift = tile_shift(R);
+    uint32_t *d_gbm, *d_nrec;
+    uint4 *d_rec;
+    if ((rc = scratch(ctx, "sc_part_bitmap", (uint64_t)ntg * NW * 4, (void **)&d_gbm))) return rc;
+    if ((rc = scratch(ctx, "sc_part_nrec", 8, (void **)&d_nrec))) return rc;
+    if ((rc = scratch(ctx, "sc_part_rec", (uint64_t)std::max<uint32_t>(F.n2, 1) * 16, (void **)&d_rec))) return rc;
+    HIPC(hipMemsetAsync(d_gbm, 0, (uint64_t)ntg * NW * 4, st));
+    HIPC(hipMemsetAsync(d_nrec, 0, 4, st));
+    if (F.M >= 2) {
+        if ((rc = screen_mark_runs(ctx, F, d_hashes, N, 0, N, rshift, NW, d_gbm, nullptr, nullptr, st, prof))) return rc;
+        if (F.n2) {
+            const uint32_t g2 = std::max(1u, std::min(8192u, (F.n2 + kScWG - 1) / kScWG));
+            hipLaunchKernelGGL(k_screen_emit2, dim3(g2), dim3(kScWG), 0, st, F.v_out, d_hashes, s, F.pairs, F.n2, d_rec,
+                               d_nrec);
+        }
+        prof.mark("mark", st);
+    }
+    HIPC(hipGetLastError());
+    uint64_t *h_tot;
+    if ((rc = pinned_host(ctx, "sc_tot", 64, (void **)&h_tot))) return rc;
+    HIPC(hipMemcpyAsync(h_tot, d_nrec, 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    timing_mark(ctx, 4, st, false);
+    ctx->part.valid = true;
+    ctx->part.N = N;
+    ctx->part.R = R;
+    ctx->part.bitmap = d_gbm;
+    ctx->part.bitmap_words = (uint64_t)ntg * NW;
+    ctx->part.rec = d_rec;
+    ctx->part.nrec = ((const uint32_t *)h_tot)[0];
+    ctx->part.entries = F.M;
+    ctx->part.runs = (uint64_t)F.n2 + F.nruns;
+    *checks = F.E;
+    *nrec = ctx->part.nrec;
+    return DREPHIP_OK;
+}
+
+// Rows [row0, row1) from every part's marks: the bitmap remapped to this
+// rank's row tiles, the pair map from every part's records of these rows, the
+// pairs sharing exactly one hash written here (k_screen_simple), the lists.
+// No light cells (their single marking run may live in another part).
+int screen_marked_impl(drephip_ctx *ctx, const uint32_t *d_nhash, uint32_t N, uint32_t row0, uint32_t row1,
+                       uint32_t R, uint32_t C, uint64_t seg0, uint64_t npairs, uint16_t *d_common, uint16_t *d_denom,
+                       const uint32_t *d_gbm, uint32_t nparts, const uint4 *d_rec, uint64_t nrec, hipStream_t st,
+                       ScreenResult *res) {
+    *res = ScreenResult{};
+    const uint32_t s = ctx->s;
+    int rc;
+    timing_mark(ctx, 4, st, true);
+    ScreenProf prof;
+    prof.mark("start", st);
+    const uint32_t rows = row1 - row0, ntiles = (rows + R - 1) / R, NW = (N + 31) / 32, ntg = (N + R - 1) / R;
+    const uint32_t rshift = tile_shift(R);
+    uint32_t *d_bm;
+    unsigned long long *pkey = nullptr, *d_nsimple;
+    uint32_t *pcnt = nullptr, *ppos = nullptr;
+    uint64_t pcap;
+    if ((rc = scratch(ctx, "sc_bitmap", (uint64_t)ntiles * NW * 4, (void **)&d_bm))) return rc;
+    if ((rc = scratch(ctx, "sc_nsimple", 8, (void **)&d_nsimple))) return rc;
+    // the pair map holds this rank's records only (every part's records of its rows)
+    uint64_t nown = 0;
+    if (nrec) {
+        uint64_t *h_tot;
+        if ((rc = pinned_host(ctx, "sc_tot", 64, (void **)&h_tot))) return rc;
+        HIPC(hipMemsetAsync(d_nsimple, 0, 8, st));
+        const uint32_t gc = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1024, (nrec + kScWG - 1) / kScWG));
+        hipLaunchKernelGGL(k_rec_count, dim3(gc), dim3(kScWG), 0, st, d_rec, nrec, row0, row1, d_nsimple);
+        HIPC(hipMemcpyAsync(h_tot, d_nsimple, 8, hipMemcpyDeviceToHost, st));
+        HIPC(hipStreamSynchronize(st));
+        nown = h_tot[0];
+    }
+    if ((rc = screen_pair_map(ctx, nown, st, &pcap, &pkey, &pcnt, &ppos))) return rc;
+    if (pcap > kMaxPairMap) { timing_mark(ctx, 4, st, false); return DREPHIP_OK; }
+    if ((rc = screen_fill_impl(ctx, d_nhash, N, row0, row1, seg0, npairs, d_common, d_denom, st))) return rc;
+    HIPC(hipMemsetAsync(d_nsimple, 0, 8, st));
+    const uint64_t nwords = (uint64_t)ntiles * NW;
+    const uint32_t gr = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(16384, (nwords + kScWG - 1) / kScWG));
+    hipLaunchKernelGGL(k_screen_remap, dim3(gr), dim3(kScWG), 0, st, d_gbm, nparts, ntg, NW, row0, row1, rshift, ntiles,
+                       d_bm);
+    prof.mark("remap", st);
+    if (nown) {
+        const uint32_t g2 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, (nrec + kScWG - 1) / kScWG));
+        hipLaunchKernelGGL(k_screen_map2, dim3(g2), dim3(kScWG), 0, st, d_rec, nrec, row0, row1, pkey, pcnt, ppos,
+                           (uint32_t)(pcap - 1));
+        const uint32_t gs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(2048, (pcap + kScWG - 1) / kScWG));
+        hipLaunchKernelGGL(k_screen_simple, dim3(gs), dim3(kScWG), 0, st, pkey, pcnt, ppos, (uint32_t)pcap, d_nhash, s, N,
+                           row0, rshift, NW, seg0, d_bm, nullptr, d_common, d_nsimple);
+    }
+    prof.mark("pairs", st);
+    HIPC(hipGetLastError());
+    rc = screen_lists(ctx, d_bm, ntiles, NW, C, row0, R, d_nsimple, st, prof, res);
+    timing_mark(ctx, 4, st, false);
+    return rc;
 }
 
 int screen_fill_impl(drephip_ctx *ctx, const uint32_t *d_nhash, uint32_t N, uint32_t row0, uint32_t row1,

@@ -367,18 +367,57 @@ def cached_sketches(data_folder: str, names: Sequence[str], s: int, group_size: 
     return out
 
 
+def sharded_screen_enabled() -> bool:
+    """DREPHIP_SCREEN_SHARD=0 turns the sharded screen off: every rank then
+    groups all N x s entries itself (the round-5 form)."""
+    return os.environ.get("DREPHIP_SCREEN_SHARD", "1") != "0"
+
+
 def hip_allpairs(ctx, stream: int, device):
-    """Stage 3: drephip_allpairs_device over this rank's rows, on its GPU."""
+    """Stage 3: drephip_allpairs_device over this rank's rows, on its GPU.
+
+    With several ranks and the screen on, the screen is sharded by hash range
+    (include/drephip.h drephip_screen_part): rank p groups hash part p of W,
+    the parts' bitmaps and runs-of-two records are all-gathered
+    (parallel.exchange_screen_parts), and each rank screens its rows from all
+    of them (drephip_allpairs_device_marked) -- instead of every rank sorting
+    all N x s entries.  The pair checks summed over the parts decide the
+    screen exactly as the one-GPU call decides it."""
     import torch
+    import torch.distributed as dist
+    from .parallel import exchange_screen_parts
 
     def fn(H, NH, p: ShardPlan, out=None):
         # `out`: where the segment goes (a slice of the root's full vector)
         seg = out if out is not None and p.seg_len else torch.zeros(max(p.seg_len, 1), dtype=torch.int16, device=device)
         partial = bool((NH < ctx.s).any().item())
         segd = torch.zeros(max(p.seg_len, 1), dtype=torch.int16, device=device) if partial else None
-        if p.seg_len:
-            ctx.allpairs_device(H.data_ptr(), NH.data_ptr(), p.N, p.r0, p.r1, seg.data_ptr(),
-                                segd.data_ptr() if segd is not None else None, stream)
+        dptr = segd.data_ptr() if segd is not None else None
+        world = dist.get_world_size() if dist.is_initialized() else 1
+        if world > 1 and sharded_screen_enabled() and ctx.screen_worth(p.N, 0)[0]:
+            # every rank takes this branch (same N, mode and environment): the
+            # exchange is collective
+            checks, nrec = ctx.screen_part(H.data_ptr(), NH.data_ptr(), p.N, dist.get_rank(), world, stream)
+            _, words = ctx.screen_geometry(p.N)
+            bm = torch.empty(words, dtype=torch.int32, device=device)
+            rec = torch.empty((max(nrec, 1), 4), dtype=torch.int32, device=device)
+            ctx.screen_part_copy(bm.data_ptr(), rec.data_ptr(), stream)
+            starts = [a for a, _ in row_partition(p.N, world)]        # the plan's row ranges (plan())
+            bms, recs, total = exchange_screen_parts(bm, rec, nrec, checks, row_starts=starts)
+            if p.seg_len:
+                if ctx.screen_worth(p.N, total)[1]:
+                    ctx.allpairs_device_marked(H.data_ptr(), NH.data_ptr(), p.N, p.r0, p.r1, seg.data_ptr(), dptr,
+                                               bms.data_ptr(), world, recs.data_ptr() if len(recs) else None,
+                                               len(recs), stream)
+                else:                                 # a dense set: the dense plan, as the one-GPU call
+                    mode = ctx.allpairs_screen
+                    ctx.set_allpairs_screen(ctx.SCREEN_OFF)
+                    try:
+                        ctx.allpairs_device(H.data_ptr(), NH.data_ptr(), p.N, p.r0, p.r1, seg.data_ptr(), dptr, stream)
+                    finally:
+                        ctx.set_allpairs_screen(mode)
+        elif p.seg_len:
+            ctx.allpairs_device(H.data_ptr(), NH.data_ptr(), p.N, p.r0, p.r1, seg.data_ptr(), dptr, stream)
         return seg, segd
     return fn
 

@@ -130,6 +130,63 @@ def gather_sketches(local_h, local_n, group=None):
     return all_h, all_n
 
 
+def exchange_screen_parts(bitmap, records, nrec: int, checks: int, row_starts=None, group=None):
+    """The sharded screen's exchange (include/drephip.h drephip_screen_part).
+
+    bitmap: this rank's part bitmap (uint32 words as int32, equal size on every
+    rank); records: its runs-of-two records ([>= nrec, 4] int32, {a, b, pos,
+    0}); checks: its pair checks.  Returns (bitmaps [world, words] in part
+    order, the records this rank needs [n, 4], total pair checks).
+
+    The bitmaps are all-gathered (every rank needs every part's cells of its
+    rows; one part's bitmap is ceil(N/R) x ceil(N/32) words).  The records go
+    to their owners only: with row_starts (every rank's first row, ascending)
+    record {a, ...} goes to the rank whose rows hold a, by one all-to-all;
+    without, every rank gets every record (an all-gather).  RCCL over xGMI with
+    nccl; gloo in rehearsals (records staged through the host there)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = bitmap.device
+    rec = records[:nrec]
+    if row_starts is not None:
+        starts = torch.as_tensor(np.asarray(row_starts, np.int64), device=dev)
+        owner = torch.searchsorted(starts, rec[:, 0].to(torch.int64), right=True) - 1
+        order = torch.argsort(owner, stable=True)
+        rec = rec[order]
+        send = torch.bincount(owner, minlength=world).to(torch.int64)
+    else:
+        send = torch.full((world,), nrec, dtype=torch.int64, device=dev)
+    # (outputs shaped [world * input rows, ...]: gloo splits them along dim 0)
+    meta = torch.cat([send, torch.tensor([nrec, checks], dtype=torch.int64, device=dev)])
+    allm = torch.empty(world * (world + 2), dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(allm, meta, group=group)
+    allm = allm.view(world, world + 2).cpu()
+    total_checks = int(allm[:, world + 1].sum())
+    bms = torch.empty(world * bitmap.numel(), dtype=bitmap.dtype, device=dev)
+    dist.all_gather_into_tensor(bms, bitmap.reshape(-1), group=group)
+    bms = bms.view(world, bitmap.numel())
+    if row_starts is not None:
+        send_sizes = [int(x) for x in allm[rank, :world]]
+        recv_sizes = [int(x) for x in allm[:, rank]]
+        host = dist.get_backend(group) == "gloo" and rec.is_cuda
+        src = rec.contiguous().cpu() if host else rec.contiguous()
+        out = torch.empty((sum(recv_sizes), 4), dtype=torch.int32, device=src.device)
+        dist.all_to_all_single(out, src, output_split_sizes=recv_sizes, input_split_sizes=send_sizes, group=group)
+        return bms, out.to(dev).contiguous(), total_checks
+    counts = [int(c) for c in allm[:, world]]
+    cmax = max(max(counts), 1)
+    padded = torch.zeros((cmax, 4), dtype=torch.int32, device=dev)
+    if nrec:
+        padded[:nrec] = rec
+    recs = torch.empty((world * cmax, 4), dtype=torch.int32, device=dev)
+    dist.all_gather_into_tensor(recs, padded, group=group)
+    recs = recs.view(world, cmax, 4)
+    keep = torch.cat([recs[p, :counts[p]] for p in range(world)]) if sum(counts) else recs[0, :0]
+    return bms, keep.contiguous(), total_checks
+
+
 def assemble_condensed(N: int, segments: Sequence[np.ndarray], world: int) -> np.ndarray:
     """Concatenate per-rank condensed segments (rank order) into the full
     condensed vector, checking every segment has its expected size."""

@@ -354,3 +354,58 @@ def test_file_weights_multi_member_and_bgzf(tmp_path):
     single = tmp_path / "s.fa.gz"
     single.write_bytes(gzip.compress(seq))
     assert D.file_weights([str(single)])[0] == len(seq)
+
+
+def _xworker(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    words = 7
+    bm = torch.full((words,), 1000 + rank, dtype=torch.int32)
+    nrec = (rank * 2) % 3                     # 0, 2, 1 records: one part has none
+    rec = torch.arange(max(nrec, 1) * 4, dtype=torch.int32).view(-1, 4) + 100 * rank
+    bms, recs, checks = parallel.exchange_screen_parts(bm, rec, nrec, 10 ** rank)
+    np.save(os.path.join(out_dir, "x%d.npy" % rank), np.concatenate([bms.numpy().ravel(), recs.numpy().ravel(),
+                                                                      [checks]]))
+    # to the owners: row a of record {a, b, pos, 0} owned by the rank whose rows
+    # start at or below it (rank r's rows start at 10 r; rank 1's range empty)
+    starts = [10 * r for r in range(world)]
+    if world > 2:
+        starts[2] = starts[1]
+    rng = np.random.default_rng(rank)
+    n = 5 + 3 * rank
+    a = rng.integers(0, 10 * world, n)
+    rec = torch.from_numpy(np.stack([a, a + 1, np.full(n, rank), np.arange(n)], 1).astype(np.int32))
+    bms, recs, checks = parallel.exchange_screen_parts(bm, rec, n, 1, row_starts=starts)
+    np.save(os.path.join(out_dir, "y%d.npy" % rank), recs.numpy())
+    np.save(os.path.join(out_dir, "ya%d.npy" % rank), rec.numpy())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_exchange_screen_parts(tmp_path, world):
+    """The sharded screen's exchange (parallel.exchange_screen_parts): every
+    part's bitmap in part order, the records of every part concatenated in part
+    order (parts with none included), the pair checks summed."""
+    import torch.multiprocessing as mp
+    port = _free_port()
+    mp.start_processes(_xworker, args=(world, port, str(tmp_path)), nprocs=world, join=True, start_method="spawn")
+    want_bm = np.concatenate([np.full(7, 1000 + r, np.int64) for r in range(world)])
+    want_rec = np.concatenate([(np.arange(((r * 2) % 3) * 4) + 100 * r) for r in range(world)]).astype(np.int64)
+    want = np.concatenate([want_bm, want_rec, [sum(10 ** r for r in range(world))]])
+    for r in range(world):
+        got = np.load(os.path.join(tmp_path, "x%d.npy" % r))
+        assert np.array_equal(got, want), (r, got, want)
+    # owner mode: every record lands on exactly the rank owning its row, in
+    # source-part order
+    sent = np.concatenate([np.load(os.path.join(tmp_path, "ya%d.npy" % r)) for r in range(world)])
+    starts = [10 * r for r in range(world)]
+    if world > 2:
+        starts[2] = starts[1]
+    owner = np.searchsorted(starts, sent[:, 0], side="right") - 1
+    for r in range(world):
+        got = np.load(os.path.join(tmp_path, "y%d.npy" % r))
+        mine = sent[owner == r]
+        assert np.array_equal(got, mine[np.lexsort((mine[:, 3], mine[:, 2]))]), r

@@ -260,3 +260,117 @@ def test_screen_mode_argument_checked():
         h = np.sort(np.random.default_rng(1).integers(1, 1 << 62, size=(3, 1000), dtype=np.uint64), axis=1)
         ctx.allpairs(h, np.full(3, 1000, np.uint32))
         assert not ctx.screen_stats()["used"]            # auto: N < 4096
+
+
+def sharded_screen(ctx, dH, dNH, N, W, ranges, want_denom=True):
+    """The sharded screen on one GPU, as a W-rank job runs it: every part
+    grouped (drephip_screen_part) and copied out, the parts' bitmaps and
+    records concatenated (the all-gather), each row range screened from all of
+    them (drephip_allpairs_device_marked).  Returns the segments, the summed
+    pair checks and the records per part."""
+    import torch
+    st = torch.cuda.current_stream().cuda_stream
+    R, words = ctx.screen_geometry(N)
+    bms, recs, checks, nrecs = [], [], 0, []
+    for p in range(W):
+        c, n = ctx.screen_part(dH.data_ptr(), dNH.data_ptr(), N, p, W, st)
+        bm = torch.empty(words, dtype=torch.int32, device="cuda")
+        rec = torch.empty((max(n, 1), 4), dtype=torch.int32, device="cuda")
+        ctx.screen_part_copy(bm.data_ptr(), rec.data_ptr(), st)
+        bms.append(bm)
+        recs.append(rec[:n])
+        checks += c
+        nrecs.append(n)
+    bms = torch.stack(bms).contiguous()
+    recs = torch.cat(recs).contiguous()
+
+    def start(i):
+        return i * N - i * (i + 1) // 2
+    out = []
+    for r0, r1 in ranges:
+        n = start(r1) - start(r0)
+        co = torch.zeros(max(n, 1), dtype=torch.int16, device="cuda")
+        do = torch.zeros(max(n, 1), dtype=torch.int16, device="cuda") if want_denom else None
+        ctx.allpairs_device_marked(dH.data_ptr(), dNH.data_ptr(), N, r0, r1, co.data_ptr(),
+                                   do.data_ptr() if do is not None else None, bms.data_ptr(), W,
+                                   recs.data_ptr() if len(recs) else None, len(recs), st)
+        assert ctx.screen_stats()["used"]
+        torch.cuda.synchronize()
+        out.append((co[:n].cpu().numpy().view(np.uint16), do[:n].cpu().numpy().view(np.uint16) if do is not None else None))
+    return out, checks, nrecs
+
+
+@pytest.mark.parametrize("s,N", [(64, 300), (1000, 200), (4096, 80)])
+@pytest.mark.parametrize("W", [1, 2, 3, 8])
+def test_sharded_screen_matches_oracle(s, N, W):
+    """The sharded screen (one hash part per rank, marks exchanged): every
+    rank's rows -- the job's row partition, and ranges that start off a row
+    tile boundary -- bit-exact against the oracle, on the planted sketches
+    (families, partial sketches, low-word twins, a hub in a third of the
+    genomes); the parts' pair checks add up to the one-call screen's."""
+    import torch
+    from drep_amd import parallel
+    H, NH = planted_sketches(N, s, seed=s + N + W)
+    oc, od = oracle.allpairs(H, NH, s, threads=8)
+    dH = torch.from_numpy(H.view(np.int64)).cuda()
+    dNH = torch.from_numpy(NH.view(np.int32)).cuda()
+
+    def start(i):
+        return i * N - i * (i + 1) // 2
+    with _lib.Context(0, 21, s, 42) as ctx:
+        ctx.set_allpairs_screen(ctx.SCREEN_ON)
+        ranges = [(a, min(b, N - 1)) for a, b in parallel.row_partition(N, W) if a < N - 1]
+        ranges += [(1, 6), (7, N // 2 + 3), (N - 9, N - 1)]
+        segs, checks, nrecs = sharded_screen(ctx, dH, dNH, N, W, ranges)
+        for (r0, r1), (co, do) in zip(ranges, segs):
+            assert np.array_equal(co, oc[start(r0):start(r1)]), (r0, r1)
+            assert np.array_equal(do, od[start(r0):start(r1)]), (r0, r1)
+        ctx.allpairs(H, NH, want_denom=True)
+        assert ctx.screen_stats()["checks"] == checks
+        assert ctx.screen_worth(N, checks) == (True, True)           # mode ON
+    assert sum(nrecs) > 0 and (oc > 0).sum() > N
+
+
+def test_sharded_screen_single_shared_hash_pairs():
+    """Pairs sharing exactly one hash (runs of two) whose runs land in
+    different parts: a pair held by two runs of two in two parts must reach
+    the kernel, one held by a single run is written by the screen -- the
+    records of every part meet in the owner's pair map."""
+    import torch
+    s, N = 256, 400
+    rng = np.random.default_rng(33)
+    H = np.sort(rng.integers(1, 1 << 62, size=(N, s), dtype=np.uint64), axis=1)
+    NH = np.full(N, s, dtype=np.uint32)
+    for g in range(0, N, 11):
+        NH[g] = rng.integers(s // 3, s)
+        H[g, NH[g]:] = UMAX
+    for _ in range(700):
+        a, b = sorted(rng.choice(N, 2, replace=False))
+        for _k in range(1 if rng.random() < 0.7 else 2):
+            i, j = int(rng.integers(0, NH[a])), int(rng.integers(0, NH[b]))
+            v = H[a, i]
+            if v in H[b, :NH[b]]:
+                continue
+            H[b, :NH[b]] = np.sort(np.concatenate([np.delete(H[b, :NH[b]], j), [v]]))
+    oc, od = oracle.allpairs(H, NH, s, threads=8)
+    dH = torch.from_numpy(H.view(np.int64)).cuda()
+    dNH = torch.from_numpy(NH.view(np.int32)).cuda()
+    with _lib.Context(0, 21, s, 42) as ctx:
+        ctx.set_allpairs_screen(ctx.SCREEN_ON)
+        for W in (2, 5):
+            segs, _, nrecs = sharded_screen(ctx, dH, dNH, N, W, [(0, N - 1)])
+            assert np.array_equal(segs[0][0], oc) and np.array_equal(segs[0][1], od), W
+            assert min(nrecs) > 50
+            assert ctx.screen_stats()["simple"] > 300
+
+
+def test_sharded_screen_arguments_checked():
+    import torch
+    with _lib.Context(0, 21, 1000, 42) as ctx:
+        h = torch.zeros((4, 1000), dtype=torch.int64, device="cuda")
+        n = torch.zeros(4, dtype=torch.int32, device="cuda")
+        with pytest.raises(_lib.DrepHipError, match="part must be below nparts"):
+            ctx.screen_part(h.data_ptr(), n.data_ptr(), 4, 2, 2)
+        with pytest.raises(_lib.DrepHipError, match="no screen part to copy"):
+            ctx.screen_part_copy(h.data_ptr(), h.data_ptr())
+        assert ctx.screen_geometry(10) == (4, 3 * 1)
