@@ -429,6 +429,13 @@ def main():
     r0, r1 = row_partition(N, world)[rank]
     seg = segment_size(N, r0, r1)
     d_common = torch.zeros(max(seg, 1), dtype=torch.int16, device=dev)
+    # several ranks with the screen on (N >= 4096): the screen sharded by hash
+    # range, its marks exchanged (every rank calls it, synchronous)
+    from drep_amd.distributed import allpairs_rows_sharded, sharded_screen_applies
+    sharded = sharded_screen_applies(ctx, N)
+
+    def allpairs_sharded(hh, nn):
+        return allpairs_rows_sharded(ctx, hh, nn, N, r0, r1, d_common.data_ptr() if seg else None, None, stream, dev)
 
     stage = {"sketch": 0.0, "gather": 0.0, "dist": 0.0}
     kms = {0: [0.0, 0], 1: [0.0, 0], 2: [0.0, 0], 3: [0.0, 0], 4: [0.0, 0]}
@@ -461,10 +468,14 @@ def main():
             ev[1].record()
         else:
             hh, nn = loc_h, loc_n
-        if seg:
+        part_ms = 0.0
+        if sharded:
+            part_ms = allpairs_sharded(hh, nn)
+        elif seg:
             ctx.allpairs_device(hh.data_ptr(), nn.data_ptr(), N, r0, r1, d_common.data_ptr(), None, stream)
         if record and seg:
             read_kms((2, 3, 4))
+            kms[4][0] += part_ms               # the sharded screen's part (its own library call)
         if nloc and ctx.sketch_wait():
             # a genome needed another threshold round: the sketches were redone.
             # One rank alone cannot redo the gather (the other ranks would hang
@@ -509,7 +520,9 @@ def main():
                 gev.append((e0, e1))
             else:
                 hh, nn = loc_h, loc_n
-            if seg:
+            if sharded:
+                allpairs_sharded(hh, nn)
+            elif seg:
                 ctx.allpairs_device_async(hh.data_ptr(), nn.data_ptr(), N, r0, r1, d_common.data_ptr(), None,
                                           stream)
         if nsteps:
@@ -748,8 +761,11 @@ def main():
             },
             "dist_kernel": {
                 "kernel": "k_allpairs_q (s <= 2048) / k_allpairs_band",
-                "screen": dict(screen, note="shared-hash screen (screen.hip): the kernel runs only on the (row "
-                               "tile, column) cells whose genomes share a hash; auto from 4096 genomes"),
+                "screen": dict(screen, sharded_by_hash_range=sharded,
+                               note="shared-hash screen (screen.hip): the kernel runs only on the (row "
+                                    "tile, column) cells whose genomes share a hash; auto from 4096 genomes; "
+                                    "with several ranks sharded by hash range (each rank groups one part, "
+                                    "the marks exchanged; screen_ms = its part + its rows' finish)"),
                 "bound": "VALU + LDS (random slot reads); integer set intersection, no MFMA",
                 "ms_per_launch": kms[2][0] / max(kms[2][1], 1),
                 "pairs_per_launch": segment_size(N, r0, r1),

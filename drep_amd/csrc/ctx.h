@@ -101,7 +101,7 @@ struct PartResult {
     uint64_t bitmap_words = 0;
     const uint4 *rec = nullptr;         // {a, b, (i << 16) | j, 0}
     uint32_t nrec = 0;
-    uint64_t entries = 0, runs = 0;
+    uint64_t entries = 0, runs = 0, checks = 0;
 };
 // Marks handed to the next all-pairs call (drephip_allpairs_device_marked):
 // every part's bitmap and records; the call screens its rows from them.

@@ -1198,6 +1198,7 @@ int screen_part_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t 
     ctx->part.nrec = ((const uint32_t *)h_tot)[0];
     ctx->part.entries = F.M;
     ctx->part.runs = (uint64_t)F.n2 + F.nruns;
+    ctx->part.checks = F.E;
     *checks = F.E;
     *nrec = ctx->part.nrec;
     return DREPHIP_OK;
@@ -1258,6 +1259,12 @@ int screen_marked_impl(drephip_ctx *ctx, const uint32_t *d_nhash, uint32_t N, ui
     HIPC(hipGetLastError());
     rc = screen_lists(ctx, d_bm, ntiles, NW, C, row0, R, d_nsimple, st, prof, res);
     timing_mark(ctx, 4, st, false);
+    if (ctx->part.valid && ctx->part.N == N) {
+        // this rank's own part (the entries it grouped), for the stats
+        res->entries = ctx->part.entries;
+        res->runs = ctx->part.runs;
+        res->checks = ctx->part.checks;
+    }
     return rc;
 }
 

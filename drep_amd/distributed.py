@@ -373,19 +373,61 @@ def sharded_screen_enabled() -> bool:
     return os.environ.get("DREPHIP_SCREEN_SHARD", "1") != "0"
 
 
-def hip_allpairs(ctx, stream: int, device):
-    """Stage 3: drephip_allpairs_device over this rank's rows, on its GPU.
+def sharded_screen_applies(ctx, N: int) -> bool:
+    """Whether this rank's all-pairs call over N genomes takes the sharded
+    screen: several ranks, DREPHIP_SCREEN_SHARD not 0, and a screen this
+    context would run for N (mode, N >= 4096 in auto, N x s < 2^32).  The
+    same on every rank (same N, mode and environment), as it must be: the
+    exchange is collective."""
+    import torch.distributed as dist
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    return world > 1 and sharded_screen_enabled() and ctx.screen_worth(N, 0)[0]
 
-    With several ranks and the screen on, the screen is sharded by hash range
-    (include/drephip.h drephip_screen_part): rank p groups hash part p of W,
-    the parts' bitmaps and runs-of-two records are all-gathered
-    (parallel.exchange_screen_parts), and each rank screens its rows from all
-    of them (drephip_allpairs_device_marked) -- instead of every rank sorting
-    all N x s entries.  The pair checks summed over the parts decide the
-    screen exactly as the one-GPU call decides it."""
+
+def allpairs_rows_sharded(ctx, H, NH, N: int, r0: int, r1: int, d_seg: Optional[int], d_denom: Optional[int],
+                          stream: int, device) -> float:
+    """Rows [r0, r1) with the screen sharded by hash range (every rank calls it:
+    collective).  Rank p groups hash part p of W (drephip_screen_part); the
+    parts' bitmaps are all-gathered and their runs-of-two records routed to the
+    ranks owning their rows (parallel.exchange_screen_parts); each rank then
+    screens its rows from all of them (drephip_allpairs_device_marked).  The
+    pair checks summed over the parts decide the screen as the one-GPU call
+    decides it; a dense set takes the dense plan.  d_seg None: a rank without
+    rows, which still groups its part and takes part in the exchange.
+    Returns the part's screen time (ms; 0 unless the context times kernel 4):
+    the marked call's own timings replace it in the context."""
     import torch
     import torch.distributed as dist
     from .parallel import exchange_screen_parts
+    world = dist.get_world_size()
+    checks, nrec = ctx.screen_part(H.data_ptr(), NH.data_ptr(), N, dist.get_rank(), world, stream)
+    part_ms = ctx.kernel_ms(4)[0]
+    _, words = ctx.screen_geometry(N)
+    bm = torch.empty(words, dtype=torch.int32, device=device)
+    rec = torch.empty((max(nrec, 1), 4), dtype=torch.int32, device=device)
+    ctx.screen_part_copy(bm.data_ptr(), rec.data_ptr(), stream)
+    starts = [a for a, _ in row_partition(N, world)]                 # every rank's rows (plan())
+    bms, recs, total = exchange_screen_parts(bm, rec, nrec, checks, row_starts=starts)
+    if d_seg is None:
+        return part_ms
+    if ctx.screen_worth(N, total)[1]:
+        ctx.allpairs_device_marked(H.data_ptr(), NH.data_ptr(), N, r0, r1, d_seg, d_denom, bms.data_ptr(), world,
+                                   recs.data_ptr() if len(recs) else None, len(recs), stream)
+    else:                                     # a dense set: the dense plan, as the one-GPU call
+        mode = ctx.allpairs_screen
+        ctx.set_allpairs_screen(ctx.SCREEN_OFF)
+        try:
+            ctx.allpairs_device(H.data_ptr(), NH.data_ptr(), N, r0, r1, d_seg, d_denom, stream)
+        finally:
+            ctx.set_allpairs_screen(mode)
+    return part_ms
+
+
+def hip_allpairs(ctx, stream: int, device):
+    """Stage 3: drephip_allpairs_device over this rank's rows, on its GPU --
+    with the screen sharded by hash range when it applies
+    (allpairs_rows_sharded) instead of every rank sorting all N x s entries."""
+    import torch
 
     def fn(H, NH, p: ShardPlan, out=None):
         # `out`: where the segment goes (a slice of the root's full vector)
@@ -393,29 +435,9 @@ def hip_allpairs(ctx, stream: int, device):
         partial = bool((NH < ctx.s).any().item())
         segd = torch.zeros(max(p.seg_len, 1), dtype=torch.int16, device=device) if partial else None
         dptr = segd.data_ptr() if segd is not None else None
-        world = dist.get_world_size() if dist.is_initialized() else 1
-        if world > 1 and sharded_screen_enabled() and ctx.screen_worth(p.N, 0)[0]:
-            # every rank takes this branch (same N, mode and environment): the
-            # exchange is collective
-            checks, nrec = ctx.screen_part(H.data_ptr(), NH.data_ptr(), p.N, dist.get_rank(), world, stream)
-            _, words = ctx.screen_geometry(p.N)
-            bm = torch.empty(words, dtype=torch.int32, device=device)
-            rec = torch.empty((max(nrec, 1), 4), dtype=torch.int32, device=device)
-            ctx.screen_part_copy(bm.data_ptr(), rec.data_ptr(), stream)
-            starts = [a for a, _ in row_partition(p.N, world)]        # the plan's row ranges (plan())
-            bms, recs, total = exchange_screen_parts(bm, rec, nrec, checks, row_starts=starts)
-            if p.seg_len:
-                if ctx.screen_worth(p.N, total)[1]:
-                    ctx.allpairs_device_marked(H.data_ptr(), NH.data_ptr(), p.N, p.r0, p.r1, seg.data_ptr(), dptr,
-                                               bms.data_ptr(), world, recs.data_ptr() if len(recs) else None,
-                                               len(recs), stream)
-                else:                                 # a dense set: the dense plan, as the one-GPU call
-                    mode = ctx.allpairs_screen
-                    ctx.set_allpairs_screen(ctx.SCREEN_OFF)
-                    try:
-                        ctx.allpairs_device(H.data_ptr(), NH.data_ptr(), p.N, p.r0, p.r1, seg.data_ptr(), dptr, stream)
-                    finally:
-                        ctx.set_allpairs_screen(mode)
+        if sharded_screen_applies(ctx, p.N):
+            allpairs_rows_sharded(ctx, H, NH, p.N, p.r0, p.r1, seg.data_ptr() if p.seg_len else None, dptr, stream,
+                                  device)
         elif p.seg_len:
             ctx.allpairs_device(H.data_ptr(), NH.data_ptr(), p.N, p.r0, p.r1, seg.data_ptr(), dptr, stream)
         return seg, segd

@@ -273,7 +273,9 @@ int drephip_set_allpairs_screen(drephip_ctx *ctx, int mode);
 /* The last all-pairs call's screen: whether it replaced the dense plan, the
  * sketch entries grouped, the runs of equal keys, the pair checks, the
  * marked (row tile, column) cells left to the kernels and the pairs sharing
- * exactly one hash that the screen wrote itself. */
+ * exactly one hash that the screen wrote itself.  After
+ * drephip_allpairs_device_marked: entries, runs and checks of the hash part
+ * this context grouped last. */
 int drephip_last_screen_stats(drephip_ctx *ctx, int *used, uint64_t *entries, uint64_t *runs, uint64_t *checks,
                               uint64_t *marked, uint64_t *simple);
 

@@ -20,11 +20,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 N, L = 240, 300_000
 
 
-def _run(world, out, port, n=N, sketch=1000, screen=None):
+def _run(world, out, port, n=N, sketch=1000, screen=None, shard=None):
     # the root's condensed vector starts poisoned: every pair must be written
     env = dict(os.environ, DREPHIP_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1", DREPHIP_SEGMENT_POISON="1")
     if screen is not None:          # the shared-hash screen forced on (1) / off (2) in every rank
         env["DREPHIP_AP_SCREEN"] = str(screen)
+    if shard is not None:           # the sharded screen (default on) / every rank grouping all entries
+        env["DREPHIP_SCREEN_SHARD"] = str(shard)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "drep_amd.distributed",
            "--genomes", str(n), "--genome-bp", str(L), "--family-size", "20", "--sketch", str(sketch),
@@ -96,18 +98,22 @@ def test_sharded_job_band_path_matches_single_rank(tmp_path):
 
 @pytest.mark.timeout(600)
 def test_sharded_job_screened_matches_unscreened(tmp_path):
-    """s = 1000 (whole-row kernel): 3 ranks with the shared-hash screen forced
-    on equal 1 rank with it off (stored counts, Z, Cdb), the root's vector
+    """s = 1000 (whole-row kernel): 3 and 8 ranks with the shared-hash screen
+    forced on -- sharded by hash range (each rank groups one part, the marks
+    exchanged), and at 3 ranks also unsharded (every rank groups every entry)
+    -- equal 1 rank with it off (stored counts, Z, Cdb), the root's vector
     starting poisoned."""
     off = _run(1, str(tmp_path / "off"), 29691, screen=2)
-    on = _run(3, str(tmp_path / "on"), 29701, screen=1)
-    assert off["n_gpus"] == 1 and on["n_gpus"] == 3
+    assert off["n_gpus"] == 1
     a = load_condensed(str(tmp_path / "off"), mmap=False)
-    b = load_condensed(str(tmp_path / "on"), mmap=False)
-    assert np.array_equal(a.common, b.common)
-    assert np.array_equal(load_primary_linkage(str(tmp_path / "off"))["linkage"],
-                          load_primary_linkage(str(tmp_path / "on"))["linkage"])
-    assert pd.read_csv(tmp_path / "off" / "primary_Cdb.csv").equals(pd.read_csv(tmp_path / "on" / "primary_Cdb.csv"))
+    for name, world, port, shard in (("on", 3, 29701, None), ("on8", 8, 29721, None), ("flat", 3, 29731, 0)):
+        on = _run(world, str(tmp_path / name), port, screen=1, shard=shard)
+        assert on["n_gpus"] == world
+        b = load_condensed(str(tmp_path / name), mmap=False)
+        assert np.array_equal(a.common, b.common), name
+        assert np.array_equal(load_primary_linkage(str(tmp_path / "off"))["linkage"],
+                              load_primary_linkage(str(tmp_path / name))["linkage"]), name
+        assert pd.read_csv(tmp_path / "off" / "primary_Cdb.csv").equals(pd.read_csv(tmp_path / name / "primary_Cdb.csv"))
 
 
 def _file_set(tmp_path, copies=6):
