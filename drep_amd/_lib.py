@@ -72,13 +72,13 @@ SIGNATURES = {
     "drephip_allpairs_device": (C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp]),
     "drephip_allpairs_device_async": (C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp]),
     "drephip_allpairs_wait": (C.c_int, [vp]),
-    "drephip_screen_geometry": (C.c_int, [vp, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
+    "drephip_screen_geometry": (C.c_int, [vp, C.POINTER(C.c_uint32)]),
     "drephip_screen_part": (C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64),
-                                      C.POINTER(C.c_uint32), vp]),
+                                      C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), vp]),
     "drephip_screen_part_copy": (C.c_int, [vp, vp, vp, vp]),
     "drephip_screen_worth": (C.c_int, [vp, C.c_uint32, C.c_uint64, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "drephip_allpairs_device_marked": (C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp,
-                                                 C.c_uint32, vp, C.c_uint64, vp]),
+                                                 C.c_uint64, vp, C.c_uint64, vp]),
     "drephip_allpairs_merge_device": (C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp]),
     "drephip_distance_lut": (C.c_int, [C.c_int, C.c_uint32, f64p]),
     "drephip_write_mash_table": (C.c_int, [C.c_char_p, C.POINTER(C.c_char_p), C.c_uint32, vp, vp, C.c_uint32,
@@ -597,22 +597,22 @@ class Context:
               "drephip_allpairs_device")
 
     # ---- the sharded screen (include/drephip.h: drephip_screen_part ...)
-    def screen_geometry(self, N: int) -> Tuple[int, int]:
-        """(rows per row tile, uint32 words of one part's bitmap)."""
-        r, w = C.c_uint32(), C.c_uint64()
-        check(lib().drephip_screen_geometry(self._h, N, C.byref(r), C.byref(w)), "drephip_screen_geometry")
-        return r.value, w.value
+    def screen_geometry(self) -> int:
+        """Rows per row tile of the sharded screen's marks (tile T = rows [T R, (T + 1) R))."""
+        r = C.c_uint32()
+        check(lib().drephip_screen_geometry(self._h, C.byref(r)), "drephip_screen_geometry")
+        return r.value
 
     def screen_part(self, d_hashes: int, d_nhash: int, N: int, part: int, nparts: int,
-                    stream: Optional[int] = None) -> Tuple[int, int]:
-        """Group hash part `part` of `nparts`: (its pair checks, its records)."""
-        c, n = C.c_uint64(), C.c_uint32()
-        check(lib().drephip_screen_part(self._h, d_hashes, d_nhash, N, part, nparts, C.byref(c), C.byref(n), stream),
-              "drephip_screen_part")
-        return c.value, n.value
+                    stream: Optional[int] = None) -> Tuple[int, int, int]:
+        """Group hash part `part` of `nparts`: (its pair checks, its cell words, its records)."""
+        c, nc, n = C.c_uint64(), C.c_uint32(), C.c_uint32()
+        check(lib().drephip_screen_part(self._h, d_hashes, d_nhash, N, part, nparts, C.byref(c), C.byref(nc),
+                                        C.byref(n), stream), "drephip_screen_part")
+        return c.value, nc.value, n.value
 
-    def screen_part_copy(self, d_bitmap: int, d_records: Optional[int], stream: Optional[int] = None) -> None:
-        check(lib().drephip_screen_part_copy(self._h, d_bitmap, d_records, stream), "drephip_screen_part_copy")
+    def screen_part_copy(self, d_cells: Optional[int], d_records: Optional[int], stream: Optional[int] = None) -> None:
+        check(lib().drephip_screen_part_copy(self._h, d_cells, d_records, stream), "drephip_screen_part_copy")
 
     def screen_worth(self, N: int, checks: int) -> Tuple[bool, bool]:
         """(the screen applies to N genomes at all, it would run with these checks)."""
@@ -621,10 +621,10 @@ class Context:
         return bool(a.value), bool(u.value)
 
     def allpairs_device_marked(self, d_hashes: int, d_nhash: int, N: int, row0: int, row1: int, d_common: int,
-                               d_denom: Optional[int], d_bitmaps: int, nparts: int, d_records: Optional[int],
+                               d_denom: Optional[int], d_cells: Optional[int], n_cells: int, d_records: Optional[int],
                                n_records: int, stream: Optional[int] = None) -> None:
         check(lib().drephip_allpairs_device_marked(self._h, d_hashes, d_nhash, N, row0, row1, d_common, d_denom,
-                                                   d_bitmaps, nparts, d_records, n_records, stream),
+                                                   d_cells, n_cells, d_records, n_records, stream),
               "drephip_allpairs_device_marked")
 
     def allpairs_device_async(self, d_hashes: int, d_nhash: int, N: int, row0: int, row1: int,

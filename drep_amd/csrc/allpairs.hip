@@ -1635,10 +1635,10 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
     const uint32_t min_n = mn ? (uint32_t)atoi(mn) : kScreenMinN;
     ScreenResult scr;
     if (ctx->ext.active) {
-        // the sharded screen: this call's rows from every part's marks
+        // the sharded screen: this call's rows from the parts' marks
         // (drephip_allpairs_device_marked); no light cells
         int rc = screen_marked_impl(ctx, d_nhash, N, row0, row1, R, path == DREPHIP_AP_BAND ? kBandCols : kListCols,
-                                    seg0, npairs, d_common, d_denom, ctx->ext.bitmaps, ctx->ext.nparts, ctx->ext.rec,
+                                    seg0, npairs, d_common, d_denom, ctx->ext.cells, ctx->ext.ncells, ctx->ext.rec,
                                     ctx->ext.nrec, st, &scr);
         if (rc) return rc;
         ctx->last_screen = scr;

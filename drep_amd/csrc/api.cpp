@@ -741,23 +741,21 @@ DREPHIP_EXPORT int drephip_allpairs_wait(drephip_ctx *ctx) {
 }
 
 // ------------------------------------------------------------ sharded screen
-DREPHIP_EXPORT int drephip_screen_geometry(drephip_ctx *ctx, uint32_t N, uint32_t *rows_per_tile,
-                                           uint64_t *bitmap_words) {
-    if (!ctx) { set_error("null context"); return DREPHIP_ERR_ARG; }
+DREPHIP_EXPORT int drephip_screen_geometry(drephip_ctx *ctx, uint32_t *rows_per_tile) {
+    if (!ctx || !rows_per_tile) { set_error("null argument"); return DREPHIP_ERR_ARG; }
     uint32_t R;
     int path;
     int rc = allpairs_geometry(ctx, &R, &path);
     if (rc) return rc;
-    if (rows_per_tile) *rows_per_tile = R;
-    if (bitmap_words) *bitmap_words = (uint64_t)((N + R - 1) / R) * ((N + 31) / 32);
+    *rows_per_tile = R;
     return DREPHIP_OK;
 }
 
 DREPHIP_EXPORT int drephip_screen_part(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash,
                                        uint32_t N, uint32_t part, uint32_t nparts, uint64_t *checks,
-                                       uint32_t *n_records, void *stream) {
+                                       uint32_t *n_cells, uint32_t *n_records, void *stream) {
     GUARD_CTX(ctx);
-    if (!d_hashes || !d_nhash || !checks || !n_records) { set_error("null argument"); return DREPHIP_ERR_ARG; }
+    if (!d_hashes || !d_nhash || !checks || !n_cells || !n_records) { set_error("null argument"); return DREPHIP_ERR_ARG; }
     if (nparts == 0 || part >= nparts) { set_error("part must be below nparts"); return DREPHIP_ERR_ARG; }
     if (N < 2) { set_error("the screen needs N >= 2"); return DREPHIP_ERR_ARG; }
     if (ctx->apend.active) {
@@ -769,19 +767,20 @@ DREPHIP_EXPORT int drephip_screen_part(drephip_ctx *ctx, const uint64_t *d_hashe
     int rc = allpairs_geometry(ctx, &R, &path);
     if (rc) return rc;
     timing_begin(ctx);
-    rc = screen_part_impl(ctx, d_hashes, d_nhash, N, R, part, nparts, pick_stream(ctx, stream), checks, n_records);
+    rc = screen_part_impl(ctx, d_hashes, d_nhash, N, R, part, nparts, pick_stream(ctx, stream), checks, n_cells,
+                          n_records);
     if (rc) return rc;
     timing_collect(ctx);
     return DREPHIP_OK;
 }
 
-DREPHIP_EXPORT int drephip_screen_part_copy(drephip_ctx *ctx, uint32_t *d_bitmap, uint32_t *d_records, void *stream) {
+DREPHIP_EXPORT int drephip_screen_part_copy(drephip_ctx *ctx, uint32_t *d_cells, uint32_t *d_records, void *stream) {
     GUARD_CTX(ctx);
     const PartResult &p = ctx->part;
     if (!p.valid) { set_error("no screen part to copy (drephip_screen_part first)"); return DREPHIP_ERR_ARG; }
-    if (!d_bitmap || (p.nrec && !d_records)) { set_error("null argument"); return DREPHIP_ERR_ARG; }
+    if ((p.ncells && !d_cells) || (p.nrec && !d_records)) { set_error("null argument"); return DREPHIP_ERR_ARG; }
     hipStream_t st = pick_stream(ctx, stream);
-    HIPC(hipMemcpyAsync(d_bitmap, p.bitmap, p.bitmap_words * 4, hipMemcpyDeviceToDevice, st));
+    if (p.ncells) HIPC(hipMemcpyAsync(d_cells, p.cells, (uint64_t)p.ncells * 16, hipMemcpyDeviceToDevice, st));
     if (p.nrec) HIPC(hipMemcpyAsync(d_records, p.rec, (uint64_t)p.nrec * 16, hipMemcpyDeviceToDevice, st));
     HIPC(hipStreamSynchronize(st));
     return DREPHIP_OK;
@@ -797,18 +796,17 @@ DREPHIP_EXPORT int drephip_screen_worth(drephip_ctx *ctx, uint32_t N, uint64_t c
 
 DREPHIP_EXPORT int drephip_allpairs_device_marked(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash,
                                                   uint32_t N, uint32_t row0, uint32_t row1, uint16_t *d_common,
-                                                  uint16_t *d_denom, const uint32_t *d_bitmaps, uint32_t nparts,
+                                                  uint16_t *d_denom, const uint32_t *d_cells, uint64_t n_cells,
                                                   const uint32_t *d_records, uint64_t n_records, void *stream) {
     GUARD_CTX(ctx);
-    if (!d_hashes || !d_nhash || !d_common || !d_bitmaps || (n_records && !d_records)) {
+    if (!d_hashes || !d_nhash || !d_common || (n_cells && !d_cells) || (n_records && !d_records)) {
         set_error("null argument");
         return DREPHIP_ERR_ARG;
     }
-    if (nparts == 0) { set_error("nparts must be positive"); return DREPHIP_ERR_ARG; }
     if ((uint64_t)N * ctx->s >= (1ull << 32)) { set_error("the screen needs N x s < 2^32"); return DREPHIP_ERR_UNSUPPORTED; }
     if (ctx->ap_path == DREPHIP_AP_MERGE) { set_error("marks need the table or band path"); return DREPHIP_ERR_ARG; }
     timing_begin(ctx);
-    ctx->ext = ExtMarks{true, d_bitmaps, nparts, (const uint4 *)d_records, n_records};
+    ctx->ext = ExtMarks{true, (const uint4 *)d_cells, n_cells, (const uint4 *)d_records, n_records};
     int rc = allpairs_device_impl(ctx, d_hashes, d_nhash, N, row0, row1, d_common, d_denom, pick_stream(ctx, stream),
                                   false);
     ctx->ext = ExtMarks{};

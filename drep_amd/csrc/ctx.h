@@ -91,24 +91,25 @@ struct ScreenResult {
     uint64_t simple = 0;          // pairs sharing exactly one hash, written by the screen itself
 };
 
-// The last hash part a sharded screen grouped (screen_part_impl): its bitmap
-// of (row tile from row 0, column) cells and its records of runs of two, in
-// the context's scratch until the next screen call.
+// The last hash part a sharded screen grouped (screen_part_impl): its marked
+// cells as the nonzero words of its (row tile from row 0, column) bitmap and
+// its records of runs of two, in the context's scratch until the next screen
+// call.
 struct PartResult {
     bool valid = false;
     uint32_t N = 0, R = 0;
-    const uint32_t *bitmap = nullptr;   // ceil(N / R) x ceil(N / 32) words
-    uint64_t bitmap_words = 0;
+    const uint4 *cells = nullptr;       // {row tile, word, bits, 0}
+    uint32_t ncells = 0;
     const uint4 *rec = nullptr;         // {a, b, (i << 16) | j, 0}
     uint32_t nrec = 0;
     uint64_t entries = 0, runs = 0, checks = 0;
 };
 // Marks handed to the next all-pairs call (drephip_allpairs_device_marked):
-// every part's bitmap and records; the call screens its rows from them.
+// the parts' cell words and records; the call screens its rows from them.
 struct ExtMarks {
     bool active = false;
-    const uint32_t *bitmaps = nullptr;  // nparts x ceil(N / R) x ceil(N / 32) words
-    uint32_t nparts = 0;
+    const uint4 *cells = nullptr;
+    uint64_t ncells = 0;
     const uint4 *rec = nullptr;
     uint64_t nrec = 0;
 };
@@ -238,10 +239,11 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
 // The sharded screen (screen.hip): one hash part's marks for every row
 // (ctx->part), and a rank's rows screened from every part's marks.
 int screen_part_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N, uint32_t R,
-                     uint32_t part, uint32_t nparts, hipStream_t st, uint64_t *checks, uint32_t *nrec);
+                     uint32_t part, uint32_t nparts, hipStream_t st, uint64_t *checks, uint32_t *ncells,
+                     uint32_t *nrec);
 int screen_marked_impl(drephip_ctx *ctx, const uint32_t *d_nhash, uint32_t N, uint32_t row0, uint32_t row1,
                        uint32_t R, uint32_t C, uint64_t seg0, uint64_t npairs, uint16_t *d_common, uint16_t *d_denom,
-                       const uint32_t *d_gbm, uint32_t nparts, const uint4 *d_rec, uint64_t nrec, hipStream_t st,
+                       const uint4 *d_cells, uint64_t ncells, const uint4 *d_rec, uint64_t nrec, hipStream_t st,
                        ScreenResult *res);
 // the dense-set rule on the whole triangle's pair checks E
 bool screen_worth(uint32_t N, uint32_t s, uint64_t E);

@@ -405,26 +405,58 @@ __global__ __launch_bounds__(kScWG) void k_screen_map2(const uint4 *__restrict__
     }
 }
 
-// The rank's bitmap from every part's: the parts mark (row tile, column) cells
-// with row tiles counted from row 0 (tile T = rows [T R, (T + 1) R)); this
-// rank's tiles start at row0.  Local tile t's word w is the OR, over the
-// parts, of the global tiles holding its rows -- a superset of its cells when
-// row0 is not a multiple of R (an extra cell costs kernel work, never
-// exactness: the kernels rewrite every pair of a marked cell).
-__global__ __launch_bounds__(kScWG) void k_screen_remap(const uint32_t *__restrict__ gbm, uint32_t nparts,
-                                                        uint32_t ntg, uint32_t NW, uint32_t row0, uint32_t row1,
-                                                        uint32_t rshift, uint32_t ntiles,
-                                                        uint32_t *__restrict__ bm) {
-    const uint64_t nwords = (uint64_t)ntiles * NW, gwords = (uint64_t)ntg * NW;
-    for (uint64_t wi = (uint64_t)blockIdx.x * kScWG + threadIdx.x; wi < nwords; wi += (uint64_t)gridDim.x * kScWG) {
-        const uint32_t t = (uint32_t)(wi / NW), w = (uint32_t)(wi % NW);
-        const uint32_t ra = row0 + (t << rshift);
-        const uint32_t rb = min(row1, ra + (1u << rshift)) - 1;
-        const uint32_t T0 = ra >> rshift, T1 = min(rb >> rshift, ntg - 1);
-        uint32_t v = 0;
-        for (uint32_t p = 0; p < nparts; p++)
-            for (uint32_t T = T0; T <= T1; T++) v |= gbm[p * gwords + (uint64_t)T * NW + w];
-        bm[wi] = v;
+// A part's marks leave as cell words: every nonzero word of its bitmap as
+// {row tile T (rows [T R, (T + 1) R) from row 0), word w (columns 32 w ..
+// 32 w + 31), bits, 0} -- ~1 record per marked cell word, against N^2 / (32 R)
+// words of the whole bitmap (312 MB per part at 10^5 genomes).  Counted per
+// chunk, scanned, written in order.
+__global__ __launch_bounds__(kScWG) void k_cells_count(const uint32_t *__restrict__ bm, uint64_t nwords, uint32_t chunk,
+                                                       uint32_t *__restrict__ bcount) {
+    __shared__ uint32_t red[kScWG / 64];
+    const uint64_t i0 = (uint64_t)blockIdx.x * chunk, i1 = min(i0 + chunk, nwords);
+    uint32_t c = 0;
+    for (uint64_t i = i0 + threadIdx.x; i < i1; i += kScWG) c += bm[i] != 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < kScWG / 64; w++) t += red[w];
+        bcount[blockIdx.x] = t;
+    }
+}
+__global__ __launch_bounds__(kScWG) void k_cells_write(const uint32_t *__restrict__ bm, uint64_t nwords, uint32_t chunk,
+                                                       const uint32_t *__restrict__ boff, uint32_t NW,
+                                                       uint4 *__restrict__ cells) {
+    __shared__ uint32_t wsum[kScWG / 64];
+    const uint64_t i0 = (uint64_t)blockIdx.x * chunk, i1 = min(i0 + chunk, nwords);
+    uint32_t o = boff[blockIdx.x];
+    for (uint64_t ib = i0; ib < i1; ib += kScWG) {                    // uniform trip count
+        const uint64_t i = ib + threadIdx.x;
+        const uint32_t v = i < i1 ? bm[i] : 0u;
+        uint32_t tot;
+        const uint32_t q = o + block_exclusive_count(v != 0, wsum, &tot);
+        if (v) cells[q] = make_uint4((uint32_t)(i / NW), (uint32_t)(i % NW), v, 0u);
+        o += tot;
+    }
+}
+// A rank's bitmap from every part's cell words: the cell's rows clipped to
+// [row0, row1) and OR-ed into the rank's tiles (rows from row0).  With tile-
+// aligned rank boundaries (parallel.row_partition) a part's tile is one of
+// the rank's; otherwise it covers two, each getting the whole word -- a
+// superset (an extra cell costs kernel work, never exactness: the kernels
+// rewrite every pair of a marked cell).
+__global__ __launch_bounds__(kScWG) void k_cells_scatter(const uint4 *__restrict__ cells, uint64_t ncells, uint32_t row0,
+                                                         uint32_t row1, uint32_t rshift, uint32_t NW,
+                                                         uint32_t *__restrict__ bm) {
+    for (uint64_t q = (uint64_t)blockIdx.x * kScWG + threadIdx.x; q < ncells; q += (uint64_t)gridDim.x * kScWG) {
+        const uint4 c = cells[q];
+        const uint64_t ra = max((uint64_t)c.x << rshift, (uint64_t)row0);
+        const uint64_t rb = min(((uint64_t)c.x + 1) << rshift, (uint64_t)row1);
+        if (ra >= rb) continue;                                        // not this rank's rows
+        const uint32_t ta = (uint32_t)((ra - row0) >> rshift), tb = (uint32_t)((rb - 1 - row0) >> rshift);
+        for (uint32_t t = ta; t <= tb; t++) atomicOr(bm + (uint64_t)t * NW + c.y, c.z);
     }
 }
 
@@ -1148,15 +1180,18 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
 // ------------------------------------------------------- the sharded screen
 // Part `part` of `nparts` hash ranges (one per rank of a sharded job): its
 // entries grouped, its runs of >= 3 marked into a bitmap of row tiles of R
-// rows counted from row 0 -- every row, not only this rank's -- and its runs of
-// two listed as records.  The caller exchanges every part's bitmap and records
-// (drephip_screen_part_copy), and each rank finishes its rows from all of
-// them (screen_marked_impl).  Results stay in the context's scratch until the
-// next screen call.
+// rows counted from row 0 -- every row, not only this rank's -- sent out as
+// its nonzero words (cell records), and its runs of two listed as records.
+// The caller routes every part's cells and records to the ranks owning their
+// rows (drephip_screen_part_copy), and each rank finishes its rows from them
+// (screen_marked_impl).  Results stay in the context's scratch until the next
+// screen call.
 int screen_part_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N, uint32_t R,
-                     uint32_t part, uint32_t nparts, hipStream_t st, uint64_t *checks, uint32_t *nrec) {
+                     uint32_t part, uint32_t nparts, hipStream_t st, uint64_t *checks, uint32_t *ncells_out,
+                     uint32_t *nrec) {
     const uint32_t s = ctx->s;
     *checks = 0;
+    *ncells_out = 0;
     *nrec = 0;
     ctx->part = PartResult{};
     if ((uint64_t)N * s >= (1ull << 32)) { set_error("the screen needs N x s < 2^32"); return DREPHIP_ERR_UNSUPPORTED; }
@@ -1169,10 +1204,11 @@ int screen_part_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t 
     const uint32_t NW = (N + 31) / 32, ntg = (N + R - 1) / R, rshift = tile_shift(R);
     uint32_t *d_gbm, *d_nrec;
     uint4 *d_rec;
-    if ((rc = scratch(ctx, "sc_part_bitmap", (uint64_t)ntg * NW * 4, (void **)&d_gbm))) return rc;
+    const uint64_t gwords = (uint64_t)ntg * NW;
+    if ((rc = scratch(ctx, "sc_part_bitmap", gwords * 4, (void **)&d_gbm))) return rc;
     if ((rc = scratch(ctx, "sc_part_nrec", 8, (void **)&d_nrec))) return rc;
     if ((rc = scratch(ctx, "sc_part_rec", (uint64_t)std::max<uint32_t>(F.n2, 1) * 16, (void **)&d_rec))) return rc;
-    HIPC(hipMemsetAsync(d_gbm, 0, (uint64_t)ntg * NW * 4, st));
+    HIPC(hipMemsetAsync(d_gbm, 0, gwords * 4, st));
     HIPC(hipMemsetAsync(d_nrec, 0, 4, st));
     if (F.M >= 2) {
         if ((rc = screen_mark_runs(ctx, F, d_hashes, N, 0, N, rshift, NW, d_gbm, nullptr, nullptr, st, prof))) return rc;
@@ -1183,34 +1219,51 @@ int screen_part_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t 
         }
         prof.mark("mark", st);
     }
-    HIPC(hipGetLastError());
+    // the marks as cell words (nonzero words of the bitmap)
+    const uint32_t cchunk = (uint32_t)std::max<uint64_t>(8192, (gwords + 8191) / 8192);
+    const uint32_t ncb = (uint32_t)((gwords + cchunk - 1) / cchunk);
+    uint32_t *ccnt, *coff;
+    if ((rc = scratch(ctx, "sc_cells_cnt", (ncb + 1) * 4ull, (void **)&ccnt))) return rc;
+    if ((rc = scratch(ctx, "sc_cells_off", (ncb + 1) * 4ull, (void **)&coff))) return rc;
+    HIPC(hipMemsetAsync(ccnt + ncb, 0, 4, st));
+    hipLaunchKernelGGL(k_cells_count, dim3(ncb), dim3(kScWG), 0, st, d_gbm, gwords, cchunk, ccnt);
+    if ((rc = hip_scan(ctx, "sc_scan_tmp6", ccnt, coff, ncb + 1, st))) return rc;
     uint64_t *h_tot;
     if ((rc = pinned_host(ctx, "sc_tot", 64, (void **)&h_tot))) return rc;
     HIPC(hipMemcpyAsync(h_tot, d_nrec, 4, hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync((uint32_t *)h_tot + 1, coff + ncb, 4, hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));
+    const uint32_t ncells = ((const uint32_t *)h_tot)[1];
+    uint4 *d_cells;
+    if ((rc = scratch(ctx, "sc_part_cells", (uint64_t)std::max<uint32_t>(ncells, 1) * 16, (void **)&d_cells))) return rc;
+    hipLaunchKernelGGL(k_cells_write, dim3(ncb), dim3(kScWG), 0, st, d_gbm, gwords, cchunk, coff, NW, d_cells);
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(st));
+    prof.mark("cells", st);
     timing_mark(ctx, 4, st, false);
     ctx->part.valid = true;
     ctx->part.N = N;
     ctx->part.R = R;
-    ctx->part.bitmap = d_gbm;
-    ctx->part.bitmap_words = (uint64_t)ntg * NW;
+    ctx->part.cells = d_cells;
+    ctx->part.ncells = ncells;
     ctx->part.rec = d_rec;
     ctx->part.nrec = ((const uint32_t *)h_tot)[0];
     ctx->part.entries = F.M;
     ctx->part.runs = (uint64_t)F.n2 + F.nruns;
     ctx->part.checks = F.E;
     *checks = F.E;
+    *ncells_out = ncells;
     *nrec = ctx->part.nrec;
     return DREPHIP_OK;
 }
 
-// Rows [row0, row1) from every part's marks: the bitmap remapped to this
+// Rows [row0, row1) from every part's marks: the cell words OR-ed into this
 // rank's row tiles, the pair map from every part's records of these rows, the
 // pairs sharing exactly one hash written here (k_screen_simple), the lists.
 // No light cells (their single marking run may live in another part).
 int screen_marked_impl(drephip_ctx *ctx, const uint32_t *d_nhash, uint32_t N, uint32_t row0, uint32_t row1,
                        uint32_t R, uint32_t C, uint64_t seg0, uint64_t npairs, uint16_t *d_common, uint16_t *d_denom,
-                       const uint32_t *d_gbm, uint32_t nparts, const uint4 *d_rec, uint64_t nrec, hipStream_t st,
+                       const uint4 *d_cells, uint64_t ncells, const uint4 *d_rec, uint64_t nrec, hipStream_t st,
                        ScreenResult *res) {
     *res = ScreenResult{};
     const uint32_t s = ctx->s;
@@ -1218,7 +1271,7 @@ int screen_marked_impl(drephip_ctx *ctx, const uint32_t *d_nhash, uint32_t N, ui
     timing_mark(ctx, 4, st, true);
     ScreenProf prof;
     prof.mark("start", st);
-    const uint32_t rows = row1 - row0, ntiles = (rows + R - 1) / R, NW = (N + 31) / 32, ntg = (N + R - 1) / R;
+    const uint32_t rows = row1 - row0, ntiles = (rows + R - 1) / R, NW = (N + 31) / 32;
     const uint32_t rshift = tile_shift(R);
     uint32_t *d_bm;
     unsigned long long *pkey = nullptr, *d_nsimple;
@@ -1242,11 +1295,12 @@ int screen_marked_impl(drephip_ctx *ctx, const uint32_t *d_nhash, uint32_t N, ui
     if (pcap > kMaxPairMap) { timing_mark(ctx, 4, st, false); return DREPHIP_OK; }
     if ((rc = screen_fill_impl(ctx, d_nhash, N, row0, row1, seg0, npairs, d_common, d_denom, st))) return rc;
     HIPC(hipMemsetAsync(d_nsimple, 0, 8, st));
-    const uint64_t nwords = (uint64_t)ntiles * NW;
-    const uint32_t gr = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(16384, (nwords + kScWG - 1) / kScWG));
-    hipLaunchKernelGGL(k_screen_remap, dim3(gr), dim3(kScWG), 0, st, d_gbm, nparts, ntg, NW, row0, row1, rshift, ntiles,
-                       d_bm);
-    prof.mark("remap", st);
+    HIPC(hipMemsetAsync(d_bm, 0, (uint64_t)ntiles * NW * 4, st));
+    if (ncells) {
+        const uint32_t gc = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(4096, (ncells + kScWG - 1) / kScWG));
+        hipLaunchKernelGGL(k_cells_scatter, dim3(gc), dim3(kScWG), 0, st, d_cells, ncells, row0, row1, rshift, NW, d_bm);
+    }
+    prof.mark("cells", st);
     if (nown) {
         const uint32_t g2 = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, (nrec + kScWG - 1) / kScWG));
         hipLaunchKernelGGL(k_screen_map2, dim3(g2), dim3(kScWG), 0, st, d_rec, nrec, row0, row1, pkey, pcnt, ppos,

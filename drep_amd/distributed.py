@@ -388,9 +388,9 @@ def allpairs_rows_sharded(ctx, H, NH, N: int, r0: int, r1: int, d_seg: Optional[
                           stream: int, device) -> float:
     """Rows [r0, r1) with the screen sharded by hash range (every rank calls it:
     collective).  Rank p groups hash part p of W (drephip_screen_part); the
-    parts' bitmaps are all-gathered and their runs-of-two records routed to the
-    ranks owning their rows (parallel.exchange_screen_parts); each rank then
-    screens its rows from all of them (drephip_allpairs_device_marked).  The
+    parts' marked cell words and runs-of-two records go to the ranks owning
+    their rows (parallel.exchange_screen_parts, one all-to-all); each rank then
+    screens its rows from what it received (drephip_allpairs_device_marked).  The
     pair checks summed over the parts decide the screen as the one-GPU call
     decides it; a dense set takes the dense plan.  d_seg None: a rank without
     rows, which still groups its part and takes part in the exchange.
@@ -400,18 +400,18 @@ def allpairs_rows_sharded(ctx, H, NH, N: int, r0: int, r1: int, d_seg: Optional[
     import torch.distributed as dist
     from .parallel import exchange_screen_parts
     world = dist.get_world_size()
-    checks, nrec = ctx.screen_part(H.data_ptr(), NH.data_ptr(), N, dist.get_rank(), world, stream)
+    checks, ncells, nrec = ctx.screen_part(H.data_ptr(), NH.data_ptr(), N, dist.get_rank(), world, stream)
     part_ms = ctx.kernel_ms(4)[0]
-    _, words = ctx.screen_geometry(N)
-    bm = torch.empty(words, dtype=torch.int32, device=device)
+    cells = torch.empty((max(ncells, 1), 4), dtype=torch.int32, device=device)
     rec = torch.empty((max(nrec, 1), 4), dtype=torch.int32, device=device)
-    ctx.screen_part_copy(bm.data_ptr(), rec.data_ptr(), stream)
+    ctx.screen_part_copy(cells.data_ptr(), rec.data_ptr(), stream)
     starts = [a for a, _ in row_partition(N, world)]                 # every rank's rows (plan())
-    bms, recs, total = exchange_screen_parts(bm, rec, nrec, checks, row_starts=starts)
+    cells, recs, total = exchange_screen_parts(cells, ncells, rec, nrec, checks, starts, ctx.screen_geometry())
     if d_seg is None:
         return part_ms
     if ctx.screen_worth(N, total)[1]:
-        ctx.allpairs_device_marked(H.data_ptr(), NH.data_ptr(), N, r0, r1, d_seg, d_denom, bms.data_ptr(), world,
+        ctx.allpairs_device_marked(H.data_ptr(), NH.data_ptr(), N, r0, r1, d_seg, d_denom,
+                                   cells.data_ptr() if len(cells) else None, len(cells),
                                    recs.data_ptr() if len(recs) else None, len(recs), stream)
     else:                                     # a dense set: the dense plan, as the one-GPU call
         mode = ctx.allpairs_screen

@@ -84,9 +84,16 @@ def cond_start(i: int, N: int) -> int:
     return i * N - i * (i + 1) // 2
 
 
+ROW_ALIGN = 8      # rank boundaries on multiples of 8 rows: the all-pairs row tiles (1, 2, 4 or 8 rows)
+
+
 def row_partition(N: int, world: int) -> List[Tuple[int, int]]:
     """Contiguous row ranges [r0, r1) of the upper triangle with near-equal
-    pair counts (row i has N-1-i pairs)."""
+    pair counts (row i has N-1-i pairs).  Interior boundaries fall on
+    multiples of ROW_ALIGN rows (the nearest one), so every rank's row tiles
+    are the sharded screen's tiles counted from row 0 (drephip_screen_part):
+    its marks map onto a rank's tiles exactly (a boundary inside a tile would
+    give the rank the union of two tiles' cells)."""
     pairs = np.arange(N - 1, -1, -1, dtype=np.float64)
     cum = np.concatenate([[0.0], np.cumsum(pairs)])
     total = cum[-1]
@@ -96,6 +103,9 @@ def row_partition(N: int, world: int) -> List[Tuple[int, int]]:
         i = int(np.searchsorted(cum, t))
         if i > 0 and abs(cum[i - 1] - t) <= abs(cum[min(i, N)] - t):
             i -= 1                                   # nearest row boundary
+        lo = i - i % ROW_ALIGN
+        hi = min(lo + ROW_ALIGN, N)
+        i = lo if abs(cum[lo] - t) <= abs(cum[hi] - t) else hi
         bounds.append(i)
     bounds.append(N)
     for r in range(1, len(bounds)):
@@ -130,61 +140,56 @@ def gather_sketches(local_h, local_n, group=None):
     return all_h, all_n
 
 
-def exchange_screen_parts(bitmap, records, nrec: int, checks: int, row_starts=None, group=None):
+def exchange_screen_parts(cells, ncells: int, records, nrec: int, checks: int, row_starts: Sequence[int],
+                          rows_per_tile: int, group=None):
     """The sharded screen's exchange (include/drephip.h drephip_screen_part).
 
-    bitmap: this rank's part bitmap (uint32 words as int32, equal size on every
-    rank); records: its runs-of-two records ([>= nrec, 4] int32, {a, b, pos,
-    0}); checks: its pair checks.  Returns (bitmaps [world, words] in part
-    order, the records this rank needs [n, 4], total pair checks).
-
-    The bitmaps are all-gathered (every rank needs every part's cells of its
-    rows; one part's bitmap is ceil(N/R) x ceil(N/32) words).  The records go
-    to their owners only: with row_starts (every rank's first row, ascending)
-    record {a, ...} goes to the rank whose rows hold a, by one all-to-all;
-    without, every rank gets every record (an all-gather).  RCCL over xGMI with
-    nccl; gloo in rehearsals (records staged through the host there)."""
+    This rank's part: `ncells` cell words {T, w, bits, 0} (row tile T = rows
+    [T R, (T + 1) R)) and `nrec` runs-of-two records {a, b, pos, 0}, as [n, 4]
+    int32 tensors (rows past n ignored), and its pair checks.  Each cell goes
+    to the rank whose rows hold row T R, each record to the rank whose rows
+    hold row a (row_starts: every rank's first row, ascending), by one
+    all-to-all; the counts ride an all-gather first (with the checks, whose sum
+    decides the screen).  Returns (the cells and the records this rank
+    received, in source-part order; the total pair checks).  RCCL over xGMI
+    with nccl; gloo in rehearsals (staged through the host there)."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    dev = bitmap.device
-    rec = records[:nrec]
-    if row_starts is not None:
-        starts = torch.as_tensor(np.asarray(row_starts, np.int64), device=dev)
-        owner = torch.searchsorted(starts, rec[:, 0].to(torch.int64), right=True) - 1
+    dev = cells.device
+    starts = torch.as_tensor(np.asarray(row_starts, np.int64), device=dev)
+
+    def by_owner(t, n, row_of):
+        t = t[:n]
+        owner = torch.searchsorted(starts, row_of(t), right=True) - 1
         order = torch.argsort(owner, stable=True)
-        rec = rec[order]
-        send = torch.bincount(owner, minlength=world).to(torch.int64)
-    else:
-        send = torch.full((world,), nrec, dtype=torch.int64, device=dev)
+        return t[order], torch.bincount(owner, minlength=world).to(torch.int64)
+    c, csend = by_owner(cells, ncells, lambda t: t[:, 0].to(torch.int64) * rows_per_tile)
+    r, rsend = by_owner(records, nrec, lambda t: t[:, 0].to(torch.int64))
     # (outputs shaped [world * input rows, ...]: gloo splits them along dim 0)
-    meta = torch.cat([send, torch.tensor([nrec, checks], dtype=torch.int64, device=dev)])
-    allm = torch.empty(world * (world + 2), dtype=torch.int64, device=dev)
+    meta = torch.cat([csend, rsend, torch.tensor([checks], dtype=torch.int64, device=dev)])
+    allm = torch.empty(world * (2 * world + 1), dtype=torch.int64, device=dev)
     dist.all_gather_into_tensor(allm, meta, group=group)
-    allm = allm.view(world, world + 2).cpu()
-    total_checks = int(allm[:, world + 1].sum())
-    bms = torch.empty(world * bitmap.numel(), dtype=bitmap.dtype, device=dev)
-    dist.all_gather_into_tensor(bms, bitmap.reshape(-1), group=group)
-    bms = bms.view(world, bitmap.numel())
-    if row_starts is not None:
-        send_sizes = [int(x) for x in allm[rank, :world]]
-        recv_sizes = [int(x) for x in allm[:, rank]]
-        host = dist.get_backend(group) == "gloo" and rec.is_cuda
-        src = rec.contiguous().cpu() if host else rec.contiguous()
-        out = torch.empty((sum(recv_sizes), 4), dtype=torch.int32, device=src.device)
-        dist.all_to_all_single(out, src, output_split_sizes=recv_sizes, input_split_sizes=send_sizes, group=group)
-        return bms, out.to(dev).contiguous(), total_checks
-    counts = [int(c) for c in allm[:, world]]
-    cmax = max(max(counts), 1)
-    padded = torch.zeros((cmax, 4), dtype=torch.int32, device=dev)
-    if nrec:
-        padded[:nrec] = rec
-    recs = torch.empty((world * cmax, 4), dtype=torch.int32, device=dev)
-    dist.all_gather_into_tensor(recs, padded, group=group)
-    recs = recs.view(world, cmax, 4)
-    keep = torch.cat([recs[p, :counts[p]] for p in range(world)]) if sum(counts) else recs[0, :0]
-    return bms, keep.contiguous(), total_checks
+    allm = allm.view(world, 2 * world + 1).cpu()
+    total_checks = int(allm[:, 2 * world].sum())
+    # one buffer: for each destination its cells, then its records
+    cs, rs = [int(x) for x in allm[rank, :world]], [int(x) for x in allm[rank, world:2 * world]]
+    co, ro = np.concatenate([[0], np.cumsum(cs)]), np.concatenate([[0], np.cumsum(rs)])
+    send = torch.cat([torch.cat([c[co[d]:co[d + 1]], r[ro[d]:ro[d + 1]]]) for d in range(world)]) if world else c
+    cin, rin = [int(x) for x in allm[:, rank]], [int(x) for x in allm[:, world + rank]]
+    host = dist.get_backend(group) == "gloo" and send.is_cuda
+    src = send.contiguous().cpu() if host else send.contiguous()
+    out = torch.empty((sum(cin) + sum(rin), 4), dtype=torch.int32, device=src.device)
+    dist.all_to_all_single(out, src, output_split_sizes=[a + b for a, b in zip(cin, rin)],
+                           input_split_sizes=[a + b for a, b in zip(cs, rs)], group=group)
+    out = out.to(dev)
+    got_c, got_r, o = [], [], 0
+    for p in range(world):
+        got_c.append(out[o:o + cin[p]])
+        got_r.append(out[o + cin[p]:o + cin[p] + rin[p]])
+        o += cin[p] + rin[p]
+    return torch.cat(got_c).contiguous(), torch.cat(got_r).contiguous(), total_checks
 
 
 def assemble_condensed(N: int, segments: Sequence[np.ndarray], world: int) -> np.ndarray:

@@ -283,34 +283,40 @@ int drephip_last_screen_stats(drephip_ctx *ctx, int *used, uint64_t *entries, ui
  * of every rank grouping all N x s entries, rank p groups hash part p of W
  * (entries whose low word lies in [p 2^32 / W, (p + 1) 2^32 / W): a run of
  * equal keys lies in one part), marks the (row tile, column) cells of EVERY
- * row from its runs of >= 3 and lists its runs of two as records; the ranks
- * exchange bitmaps and records (an all-gather: RCCL or gloo, the caller's),
- * and each rank screens its own rows from all of them.  Same result as
- * drephip_allpairs_device with the screen on (no light cells).  Replaces the
- * per-rank grouping inside the sharded form of drep/d_cluster.py:569-573.
+ * row from its runs of >= 3 and lists its runs of two; the ranks route the
+ * marks to the ranks owning their rows (an all-to-all: RCCL or gloo, the
+ * caller's), and each rank screens its own rows from what it received.  Same
+ * result as drephip_allpairs_device with the screen on (no light cells).
+ * Replaces the per-rank grouping inside the sharded form of
+ * drep/d_cluster.py:569-573.
  *
  * drephip_screen_geometry: rows per row tile R (the all-pairs kernels' for
- * this s) and the words of one part's bitmap, ceil(N / R) x ceil(N / 32).
+ * this s).  Row tiles count from row 0: tile T holds rows [T R, (T + 1) R).
  * drephip_screen_part: part `part` of `nparts`; *checks = the part's pair
  * checks (their sum over the parts decides the screen: drephip_screen_worth
  * sets *applies when this context screens N genomes at all -- mode, N, N x s --
  * and *use when it would screen them with those checks, as
- * drephip_allpairs_device decides),
+ * drephip_allpairs_device decides), *n_cells = its marked cell words,
  * *n_records = its runs-of-two records.  Blocking.  Results stay in the
- * context until drephip_screen_part_copy copies them out: the bitmap
- * (bitmap_words uint32) and the records (n_records x 4 uint32:
- * {a, b, (i << 16) | j, 0}, a < b genomes sharing one hash at positions i, j).
+ * context until drephip_screen_part_copy copies them out, each as 4 uint32:
+ *   cell   {T, w, bits, 0}: columns 32 w + b (bit b set) of row tile T marked
+ *   record {a, b, (i << 16) | j, 0}: genomes a < b hold one hash at positions
+ *          i, j (a run of two);
+ * route a cell to the rank owning rows T R.., a record to the rank owning row a.
  * drephip_allpairs_device_marked: drephip_allpairs_device over rows
- * [row0, row1) screened from every part's bitmap (nparts consecutive bitmaps)
- * and every part's records (concatenated). */
-int drephip_screen_geometry(drephip_ctx *ctx, uint32_t N, uint32_t *rows_per_tile, uint64_t *bitmap_words);
+ * [row0, row1) screened from the cells and records given (every part's for
+ * these rows; others are ignored).  Rank boundaries on multiples of R keep the
+ * marks exact; otherwise a tile straddling a boundary gives both ranks its
+ * cells (more kernel work, the same result). */
+int drephip_screen_geometry(drephip_ctx *ctx, uint32_t *rows_per_tile);
 int drephip_screen_part(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N,
-                        uint32_t part, uint32_t nparts, uint64_t *checks, uint32_t *n_records, void *stream);
-int drephip_screen_part_copy(drephip_ctx *ctx, uint32_t *d_bitmap, uint32_t *d_records, void *stream);
+                        uint32_t part, uint32_t nparts, uint64_t *checks, uint32_t *n_cells, uint32_t *n_records,
+                        void *stream);
+int drephip_screen_part_copy(drephip_ctx *ctx, uint32_t *d_cells, uint32_t *d_records, void *stream);
 int drephip_screen_worth(drephip_ctx *ctx, uint32_t N, uint64_t checks, int *applies /* nullable */, int *use);
 int drephip_allpairs_device_marked(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nhash, uint32_t N,
                                    uint32_t row0, uint32_t row1, uint16_t *d_common, uint16_t *d_denom,
-                                   const uint32_t *d_bitmaps, uint32_t nparts, const uint32_t *d_records,
+                                   const uint32_t *d_cells, uint64_t n_cells, const uint32_t *d_records,
                                    uint64_t n_records, void *stream);
 
 /* ---------------------------------------------------------- primary clustering

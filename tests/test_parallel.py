@@ -21,8 +21,10 @@ def test_row_partition_balanced_and_covering():
             assert all(a[1] == b[0] for a, b in zip(parts[:-1], parts[1:]))
             sizes = [parallel.segment_size(N, a, b) for a, b in parts]
             assert sum(sizes) == N * (N - 1) // 2
+            assert all(a % parallel.ROW_ALIGN == 0 for a, _ in parts[1:] if a < N)   # tile-aligned
             if N >= 1000:
-                assert max(sizes) - min(sizes) <= N          # within one row
+                # within one row of balance, up to the alignment (ROW_ALIGN rows)
+                assert max(sizes) - min(sizes) <= 2 * parallel.ROW_ALIGN * N
 
 
 def test_genome_shards_cover():
@@ -362,50 +364,50 @@ def _xworker(rank, world, port, out_dir):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    words = 7
-    bm = torch.full((words,), 1000 + rank, dtype=torch.int32)
-    nrec = (rank * 2) % 3                     # 0, 2, 1 records: one part has none
-    rec = torch.arange(max(nrec, 1) * 4, dtype=torch.int32).view(-1, 4) + 100 * rank
-    bms, recs, checks = parallel.exchange_screen_parts(bm, rec, nrec, 10 ** rank)
-    np.save(os.path.join(out_dir, "x%d.npy" % rank), np.concatenate([bms.numpy().ravel(), recs.numpy().ravel(),
-                                                                      [checks]]))
-    # to the owners: row a of record {a, b, pos, 0} owned by the rank whose rows
-    # start at or below it (rank r's rows start at 10 r; rank 1's range empty)
+    starts, R = _xstarts(world), 4
+    rng = np.random.default_rng(rank)
+    nc, nr = 6 + 2 * rank, (rank * 2) % 3                  # one part sends no records
+    T = rng.integers(0, 10 * world // R + 1, nc)
+    cells = np.stack([T, rng.integers(0, 9, nc), np.full(nc, rank), np.arange(nc)], 1).astype(np.int32)
+    a = rng.integers(0, 10 * world, nr)
+    recs = np.stack([a, a + 1, np.full(nr, rank), np.arange(nr)], 1).astype(np.int32)
+    # buffers longer than the counts (rows past them are ignored)
+    cpad = torch.from_numpy(np.concatenate([cells, np.full((2, 4), -7, np.int32)]))
+    rpad = torch.from_numpy(np.concatenate([recs, np.full((1, 4), -7, np.int32)]))
+    got_c, got_r, checks = parallel.exchange_screen_parts(cpad, nc, rpad, nr, 10 ** rank, starts, R)
+    np.save(os.path.join(out_dir, "c%d.npy" % rank), got_c.numpy())
+    np.save(os.path.join(out_dir, "r%d.npy" % rank), got_r.numpy())
+    np.save(os.path.join(out_dir, "sc%d.npy" % rank), cells)
+    np.save(os.path.join(out_dir, "sr%d.npy" % rank), recs)
+    np.save(os.path.join(out_dir, "k%d.npy" % rank), np.array([checks]))
+    dist.destroy_process_group()
+
+
+def _xstarts(world):
     starts = [10 * r for r in range(world)]
     if world > 2:
-        starts[2] = starts[1]
-    rng = np.random.default_rng(rank)
-    n = 5 + 3 * rank
-    a = rng.integers(0, 10 * world, n)
-    rec = torch.from_numpy(np.stack([a, a + 1, np.full(n, rank), np.arange(n)], 1).astype(np.int32))
-    bms, recs, checks = parallel.exchange_screen_parts(bm, rec, n, 1, row_starts=starts)
-    np.save(os.path.join(out_dir, "y%d.npy" % rank), recs.numpy())
-    np.save(os.path.join(out_dir, "ya%d.npy" % rank), rec.numpy())
-    dist.destroy_process_group()
+        starts[2] = starts[1]                              # rank 1's rows empty
+    return starts
 
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_gloo_exchange_screen_parts(tmp_path, world):
     """The sharded screen's exchange (parallel.exchange_screen_parts): every
-    part's bitmap in part order, the records of every part concatenated in part
-    order (parts with none included), the pair checks summed."""
+    cell word lands on the rank owning its row tile's first row, every record
+    on the rank owning its row a, in source-part order, with an empty part and
+    a rank without rows; the pair checks summed."""
     import torch.multiprocessing as mp
     port = _free_port()
     mp.start_processes(_xworker, args=(world, port, str(tmp_path)), nprocs=world, join=True, start_method="spawn")
-    want_bm = np.concatenate([np.full(7, 1000 + r, np.int64) for r in range(world)])
-    want_rec = np.concatenate([(np.arange(((r * 2) % 3) * 4) + 100 * r) for r in range(world)]).astype(np.int64)
-    want = np.concatenate([want_bm, want_rec, [sum(10 ** r for r in range(world))]])
+    starts = _xstarts(world)
+    sc = np.concatenate([np.load(os.path.join(tmp_path, "sc%d.npy" % r)) for r in range(world)])
+    sr = np.concatenate([np.load(os.path.join(tmp_path, "sr%d.npy" % r)) for r in range(world)])
+    oc = np.searchsorted(starts, sc[:, 0] * 4, side="right") - 1
+    orr = np.searchsorted(starts, sr[:, 0], side="right") - 1
     for r in range(world):
-        got = np.load(os.path.join(tmp_path, "x%d.npy" % r))
-        assert np.array_equal(got, want), (r, got, want)
-    # owner mode: every record lands on exactly the rank owning its row, in
-    # source-part order
-    sent = np.concatenate([np.load(os.path.join(tmp_path, "ya%d.npy" % r)) for r in range(world)])
-    starts = [10 * r for r in range(world)]
-    if world > 2:
-        starts[2] = starts[1]
-    owner = np.searchsorted(starts, sent[:, 0], side="right") - 1
-    for r in range(world):
-        got = np.load(os.path.join(tmp_path, "y%d.npy" % r))
-        mine = sent[owner == r]
-        assert np.array_equal(got, mine[np.lexsort((mine[:, 3], mine[:, 2]))]), r
+        gc = np.load(os.path.join(tmp_path, "c%d.npy" % r))
+        gr = np.load(os.path.join(tmp_path, "r%d.npy" % r))
+        wc, wr = sc[oc == r], sr[orr == r]
+        assert np.array_equal(gc, wc[np.lexsort((wc[:, 3], wc[:, 2]))]), r
+        assert np.array_equal(gr.reshape(-1, 4), wr[np.lexsort((wr[:, 3], wr[:, 2]))]), r
+        assert int(np.load(os.path.join(tmp_path, "k%d.npy" % r))[0]) == sum(10 ** q for q in range(world))

@@ -264,24 +264,23 @@ def test_screen_mode_argument_checked():
 
 def sharded_screen(ctx, dH, dNH, N, W, ranges, want_denom=True):
     """The sharded screen on one GPU, as a W-rank job runs it: every part
-    grouped (drephip_screen_part) and copied out, the parts' bitmaps and
-    records concatenated (the all-gather), each row range screened from all of
-    them (drephip_allpairs_device_marked).  Returns the segments, the summed
-    pair checks and the records per part."""
+    grouped (drephip_screen_part) and copied out, the parts' cell words and
+    records concatenated (each rank receives its own; the call ignores other
+    rows'), each row range screened from them (drephip_allpairs_device_marked).
+    Returns the segments, the summed pair checks and the records per part."""
     import torch
     st = torch.cuda.current_stream().cuda_stream
-    R, words = ctx.screen_geometry(N)
-    bms, recs, checks, nrecs = [], [], 0, []
+    cells, recs, checks, nrecs = [], [], 0, []
     for p in range(W):
-        c, n = ctx.screen_part(dH.data_ptr(), dNH.data_ptr(), N, p, W, st)
-        bm = torch.empty(words, dtype=torch.int32, device="cuda")
+        c, nc, n = ctx.screen_part(dH.data_ptr(), dNH.data_ptr(), N, p, W, st)
+        cl = torch.empty((max(nc, 1), 4), dtype=torch.int32, device="cuda")
         rec = torch.empty((max(n, 1), 4), dtype=torch.int32, device="cuda")
-        ctx.screen_part_copy(bm.data_ptr(), rec.data_ptr(), st)
-        bms.append(bm)
+        ctx.screen_part_copy(cl.data_ptr(), rec.data_ptr(), st)
+        cells.append(cl[:nc])
         recs.append(rec[:n])
         checks += c
         nrecs.append(n)
-    bms = torch.stack(bms).contiguous()
+    cells = torch.cat(cells).contiguous()
     recs = torch.cat(recs).contiguous()
 
     def start(i):
@@ -292,7 +291,8 @@ def sharded_screen(ctx, dH, dNH, N, W, ranges, want_denom=True):
         co = torch.zeros(max(n, 1), dtype=torch.int16, device="cuda")
         do = torch.zeros(max(n, 1), dtype=torch.int16, device="cuda") if want_denom else None
         ctx.allpairs_device_marked(dH.data_ptr(), dNH.data_ptr(), N, r0, r1, co.data_ptr(),
-                                   do.data_ptr() if do is not None else None, bms.data_ptr(), W,
+                                   do.data_ptr() if do is not None else None,
+                                   cells.data_ptr() if len(cells) else None, len(cells),
                                    recs.data_ptr() if len(recs) else None, len(recs), st)
         assert ctx.screen_stats()["used"]
         torch.cuda.synchronize()
@@ -303,9 +303,10 @@ def sharded_screen(ctx, dH, dNH, N, W, ranges, want_denom=True):
 @pytest.mark.parametrize("s,N", [(64, 300), (1000, 200), (4096, 80)])
 @pytest.mark.parametrize("W", [1, 2, 3, 8])
 def test_sharded_screen_matches_oracle(s, N, W):
-    """The sharded screen (one hash part per rank, marks exchanged): every
-    rank's rows -- the job's row partition, and ranges that start off a row
-    tile boundary -- bit-exact against the oracle, on the planted sketches
+    """The sharded screen (one hash part per rank, marks routed to row
+    owners): every rank's rows -- the job's row partition (tile-aligned), and
+    ranges that start off a row tile boundary (a part's tile then covers two
+    of the range's) -- bit-exact against the oracle, on the planted sketches
     (families, partial sketches, low-word twins, a hub in a third of the
     genomes); the parts' pair checks add up to the one-call screen's."""
     import torch
@@ -373,4 +374,4 @@ def test_sharded_screen_arguments_checked():
             ctx.screen_part(h.data_ptr(), n.data_ptr(), 4, 2, 2)
         with pytest.raises(_lib.DrepHipError, match="no screen part to copy"):
             ctx.screen_part_copy(h.data_ptr(), h.data_ptr())
-        assert ctx.screen_geometry(10) == (4, 3 * 1)
+        assert ctx.screen_geometry() == 4
