@@ -115,10 +115,14 @@ def dist_roofline(N, s, fam, screened, pairs_per_launch, launch_ms):
            "this_run_ms": launch_ms}
     if dv.get("valu_wave_insts_per_pair") and launch_ms and not screened:
         ach = dv["valu_wave_insts_per_pair"] * pairs_per_launch / (launch_ms * 1e-3)
-        out.update({"bound": "valu+lds", "achieved": ach, "peak": VALU_PEAK_WAVE_INST,
+        out.update({"bound": "valu+salu+lds (co-bound, DESIGN.md 10)", "achieved": ach, "peak": VALU_PEAK_WAVE_INST,
                     "unit": "wave64 VALU instructions/s", "frac": ach / VALU_PEAK_WAVE_INST,
                     "valu_wave_insts_per_pair": dv["valu_wave_insts_per_pair"],
                     "salu_over_valu": dv.get("salu_over_valu")})
+        salu = (d.get("counters_per_call") or {}).get("SQ_INSTS_SALU")
+        if salu and dv.get("kernel_cycles"):
+            # one scalar unit per CU issues at most one instruction per cycle
+            out["salu_per_cu_cycle"] = salu / (256.0 * dv["kernel_cycles"])
     for k in ("lds_busy_frac", "lds_bank_conflict_frac", "valu_issue_frac_2cyc", "wait_inst_any_frac",
               "wait_any_frac", "l2_hit_rate", "hbm_bytes_x2", "hbm_GBps_x2", "hbm_frac_of_8TBps_x2",
               "algorithmic_bytes", "hbm_over_algorithmic_x2", "effective_clock_ghz", "pairs_per_s"):
