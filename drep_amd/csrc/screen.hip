@@ -514,6 +514,13 @@ __global__ __launch_bounds__(kScWG) void k_screen_simple(const unsigned long lon
 // The x entries are in ascending genome order, so lanes of one row tile are
 // adjacent: only the first ok lane of each tile marks (one LDS atomic per
 // tile and y, none on a shared word).
+// (The per-entry hash read of the same-hash test is ~1.3 of the marking's
+// ~3.5 ms at configs[4] -- ablation build DREPHIP_SC_ABL=2, round 6 -- but it
+// pays: keys agreeing only in their low word are not rare among 10^8 entries,
+// and such a run spans two families' genomes, so marking it whole left 4.8x
+// the cells to the kernels (770k vs 159k at configs[4], band LIST kernel 9.2
+// vs 4.0 ms; measured with the light screen verifying each pair's hashes
+// instead).)
 #ifndef DREPHIP_SC_ABL
 #define DREPHIP_SC_ABL 0    // timing ablations (never the product): 1 no marking by same-hash runs, 2 no same-hash check
 #endif
@@ -973,11 +980,15 @@ static int screen_mark_runs(drephip_ctx *ctx, const ScreenFront &F, const uint64
     uint32_t *rfirst_s, *ridx_s;
     if ((rc = scratch(ctx, "sc_rfirst_s", (M / 2 + 1) * 4ull, (void **)&rfirst_s))) return rc;
     if ((rc = scratch(ctx, "sc_ridx_s", (M / 2 + 1) * 4ull, (void **)&ridx_s))) return rc;
+    // first genomes are < N: only their low bits are sorted (2 passes instead
+    // of 4 below 2^16 genomes)
+    int gbits = 1;
+    while (gbits < 32 && (1ull << gbits) < N) gbits++;
     size_t tb = 0;
-    HIPC(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, F.rfirst, rfirst_s, F.ridx, ridx_s, F.nruns, 0, 32, st));
+    HIPC(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, F.rfirst, rfirst_s, F.ridx, ridx_s, F.nruns, 0, gbits, st));
     void *tmp;
     if ((rc = scratch(ctx, "sc_sort_tmp2", std::max<size_t>(tb, 16), &tmp))) return rc;
-    HIPC(hipcub::DeviceRadixSort::SortPairs(tmp, tb, F.rfirst, rfirst_s, F.ridx, ridx_s, F.nruns, 0, 32, st));
+    HIPC(hipcub::DeviceRadixSort::SortPairs(tmp, tb, F.rfirst, rfirst_s, F.ridx, ridx_s, F.nruns, 0, gbits, st));
     prof.mark("run-sort", st);
     const dim3 grid((F.nruns + kMarkChunk - 1) / kMarkChunk);
     if (d_bmH)
