@@ -52,17 +52,26 @@ namespace drephip {
 constexpr int kScWG = 256;
 constexpr uint32_t kItemBlock = 32;          // row tiles per XCD block of the LIST items
 
+// Entry values: g s + k in the low vbits bits (vbits = the bits N s needs),
+// and in the bits above them, when there are any, the low bits of the hash's
+// high word -- a fingerprint: two entries of one run (equal low words) whose
+// fingerprints differ hold different hashes, with no read of the hashes
+// (k_screen_mark).  Every reader masks the index with vmask.
+__device__ __forceinline__ uint32_t entry_val(uint32_t idx, uint64_t h, uint32_t vbits) {
+    return vbits >= 32 ? idx : idx | ((uint32_t)(h >> 32) << vbits);
+}
 // every entry (g, k < nhash[g]) at eoff[g] + k; one workgroup per genome
 __global__ __launch_bounds__(kScWG) void k_screen_keys(const uint64_t *__restrict__ H, const uint32_t *__restrict__ nh,
-                                                       const uint64_t *__restrict__ eoff, uint32_t s,
+                                                       const uint64_t *__restrict__ eoff, uint32_t s, uint32_t vbits,
                                                        uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
     const uint32_t g = blockIdx.x;
     const uint32_t n = nh[g];
     const uint64_t o = eoff[g];
     const uint64_t *A = H + (uint64_t)g * s;
     for (uint32_t k = threadIdx.x; k < n; k += kScWG) {
-        keys[o + k] = (uint32_t)A[k];
-        vals[o + k] = g * s + k;
+        const uint64_t h = A[k];
+        keys[o + k] = (uint32_t)h;
+        vals[o + k] = entry_val(g * s + k, h, vbits);
     }
 }
 
@@ -124,7 +133,7 @@ __global__ __launch_bounds__(kScWG) void k_part_count(const uint64_t *__restrict
 // wave scan and the waves' totals
 __global__ __launch_bounds__(kScWG) void k_part_keys(const uint64_t *__restrict__ H, const uint32_t *__restrict__ nh,
                                                      const uint64_t *__restrict__ eoff, uint32_t s, uint32_t part,
-                                                     uint32_t nparts, uint32_t *__restrict__ keys,
+                                                     uint32_t nparts, uint32_t vbits, uint32_t *__restrict__ keys,
                                                      uint32_t *__restrict__ vals) {
     __shared__ uint32_t wsum[2][kScWG / 64];
     const uint32_t g = blockIdx.x, n = nh[g], lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -133,10 +142,12 @@ __global__ __launch_bounds__(kScWG) void k_part_keys(const uint64_t *__restrict_
     int buf = 0;
     for (uint32_t k0 = 0; k0 < n; k0 += kScWG * kPartPer) {            // uniform trip count
         const uint32_t k = k0 + threadIdx.x;
-        uint32_t key[kPartPer], c = 0, inmask = 0;
+        uint32_t key[kPartPer], hw[kPartPer], c = 0, inmask = 0;
 #pragma unroll
         for (uint32_t e = 0; e < kPartPer; e++) {
-            key[e] = k + e * kScWG < n ? (uint32_t)A[k + e * kScWG] : 0u;
+            const uint64_t h = k + e * kScWG < n ? A[k + e * kScWG] : 0ull;
+            key[e] = (uint32_t)h;
+            hw[e] = (uint32_t)(h >> 32);
             const bool in = k + e * kScWG < n && key_part(key[e], nparts) == part;
             inmask |= (uint32_t)in << e;
             c += in;
@@ -160,7 +171,7 @@ __global__ __launch_bounds__(kScWG) void k_part_keys(const uint64_t *__restrict_
         for (uint32_t e = 0; e < kPartPer; e++) {
             if ((inmask >> e) & 1u) {
                 keys[o + base] = key[e];
-                vals[o + base] = g * s + k + e * kScWG;
+                vals[o + base] = entry_val(g * s + k + e * kScWG, (uint64_t)hw[e] << 32, vbits);
                 base++;
             }
         }
@@ -280,7 +291,7 @@ __global__ __launch_bounds__(kScWG) void k_run_count(const uint32_t *__restrict_
 __global__ __launch_bounds__(kScWG) void k_run_write(const uint32_t *__restrict__ rstart,
                                                      const uint32_t *__restrict__ rend, uint32_t nr, uint32_t per,
                                                      const uint32_t *__restrict__ off2, const uint32_t *__restrict__ off3,
-                                                     const uint32_t *__restrict__ vals, uint32_t s,
+                                                     const uint32_t *__restrict__ vals, uint32_t s, uint32_t vmask,
                                                      uint32_t *__restrict__ pairs, uint2 *__restrict__ runs,
                                                      uint32_t *__restrict__ rfirst, uint32_t *__restrict__ ridx) {
     __shared__ uint32_t wsum[kScWG / 64];
@@ -296,7 +307,7 @@ __global__ __launch_bounds__(kScWG) void k_run_write(const uint32_t *__restrict_
         if (m == 2) pairs[q2] = st;
         if (m >= 3) {
             runs[q3] = make_uint2(st, m);
-            rfirst[q3] = vals[st] / s;
+            rfirst[q3] = (vals[st] & vmask) / s;
             ridx[q3] = q3;
         }
         b2 += t2;
@@ -317,13 +328,13 @@ __device__ __forceinline__ uint32_t pair_slot(uint64_t key, uint32_t mask) {
     return (uint32_t)(h >> 32) & mask;
 }
 __global__ __launch_bounds__(kScWG) void k_screen_mark2(const uint32_t *__restrict__ vals, const uint64_t *__restrict__ H,
-                                                        uint32_t s, const uint32_t *__restrict__ pairs, uint32_t n2,
+                                                        uint32_t s, uint32_t vmask, const uint32_t *__restrict__ pairs, uint32_t n2,
                                                         uint32_t row0, uint32_t row1,
                                                         unsigned long long *__restrict__ pkey, uint32_t *__restrict__ pcnt,
                                                         uint32_t *__restrict__ ppos, uint32_t pmask) {
     for (uint32_t q = blockIdx.x * kScWG + threadIdx.x; q < n2; q += gridDim.x * kScWG) {
         const uint32_t st = pairs[q];
-        const uint32_t ix = vals[st], iy = vals[st + 1];
+        const uint32_t ix = vals[st] & vmask, iy = vals[st + 1] & vmask;
         const uint32_t gx = ix / s, gy = iy / s;          // gx <= gy (a run is in genome order)
         if (gx == gy || gx < row0 || gx >= row1 || H[ix] != H[iy]) continue;
         const unsigned long long key = ((unsigned long long)gx << 32) | gy;
@@ -345,7 +356,7 @@ __global__ __launch_bounds__(kScWG) void k_screen_mark2(const uint32_t *__restri
 // row a builds the pair map from every part's records (k_screen_map2).  One
 // device counter, bumped once per wave.
 __global__ __launch_bounds__(kScWG) void k_screen_emit2(const uint32_t *__restrict__ vals, const uint64_t *__restrict__ H,
-                                                        uint32_t s, const uint32_t *__restrict__ pairs, uint32_t n2,
+                                                        uint32_t s, uint32_t vmask, const uint32_t *__restrict__ pairs, uint32_t n2,
                                                         uint4 *__restrict__ rec, uint32_t *__restrict__ nrec) {
     const uint32_t lane = threadIdx.x & 63;
     for (uint32_t q0 = blockIdx.x * kScWG; q0 < n2; q0 += gridDim.x * kScWG) {   // wave-uniform trip count
@@ -354,8 +365,8 @@ __global__ __launch_bounds__(kScWG) void k_screen_emit2(const uint32_t *__restri
         uint32_t ix = 0, iy = 0, gx = 0, gy = 0;
         if (q < n2) {
             const uint32_t st = pairs[q];
-            ix = vals[st];
-            iy = vals[st + 1];
+            ix = vals[st] & vmask;
+            iy = vals[st + 1] & vmask;
             gx = ix / s;
             gy = iy / s;
             ok = gx != gy && H[ix] == H[iy];
@@ -514,17 +525,16 @@ __global__ __launch_bounds__(kScWG) void k_screen_simple(const unsigned long lon
 // The x entries are in ascending genome order, so lanes of one row tile are
 // adjacent: only the first ok lane of each tile marks (one LDS atomic per
 // tile and y, none on a shared word).
-// (The per-entry hash read of the same-hash test is ~1.3 of the marking's
-// ~3.5 ms at configs[4] -- ablation build DREPHIP_SC_ABL=2, round 6 -- but it
-// pays: keys agreeing only in their low word are not rare among 10^8 entries,
-// and such a run spans two families' genomes, so marking it whole left 4.8x
-// the cells to the kernels (770k vs 159k at configs[4], band LIST kernel 9.2
-// vs 4.0 ms; measured with the light screen verifying each pair's hashes
-// instead).)
+// (Marking a collision run whole, without any same-hash test and with the
+// light screen checking each pair's hashes, left 4.8x the cells to the
+// kernels at configs[4] -- 770k vs 159k, band LIST kernel 9.2 vs 4.0 ms: such
+// runs are not rare among 10^8 entries and span two families' genomes.  The
+// fingerprint test below keeps them apart without the hash reads.)
 #ifndef DREPHIP_SC_ABL
 #define DREPHIP_SC_ABL 0    // timing ablations (never the product): 1 no marking by same-hash runs, 2 no same-hash check
 #endif
 constexpr uint32_t kMarkWG = 1024;
+constexpr uint32_t kFpBits = 4;      // fingerprint bits from which the same-hash test reads no hashes
 constexpr uint32_t kMarkChunk = 256;
 constexpr uint32_t kMarkTiles = 128;
 constexpr uint32_t kMarkCols = 2048;
@@ -532,7 +542,7 @@ constexpr uint32_t kMarkWords = kMarkCols / 32;
 constexpr uint32_t kMarkStride = kMarkWords + 1;
 template <bool LIGHT>
 __global__ __launch_bounds__(kMarkWG) void k_screen_mark(const uint32_t *__restrict__ vals, const uint64_t *__restrict__ H,
-                                                       uint32_t s, const uint2 *__restrict__ runs,
+                                                       uint32_t s, uint32_t vbits, const uint2 *__restrict__ runs,
                                                        const uint32_t *__restrict__ order,
                                                        const uint32_t *__restrict__ rfirst_sorted, uint32_t nruns,
                                                        uint32_t row0, uint32_t row1, uint32_t rshift, uint32_t NW,
@@ -581,14 +591,31 @@ __global__ __launch_bounds__(kMarkWG) void k_screen_mark(const uint32_t *__restr
         const uint2 run = runs[run_id];
         const uint32_t start = run.x, m = run.y;
         // a run whose entries all hold one 64-bit hash (a hash shared by m
-        // genomes; only a low-word collision breaks this) takes the fast path
+        // genomes; only a low-word collision breaks this) takes the fast path.
+        // With >= kFpBits fingerprint bits in the entry values the test reads
+        // only the values: different fingerprints, different hashes (the slow
+        // path); equal ones are taken as one hash -- a collision run whose
+        // fingerprints agree (1 in 2^fbits) then marks a superset, which the
+        // kernels and the light screen's hash check (k_screen_light) resolve.
+        // Without them, every entry's hash is read (~1.3 of the marking's 3.5 ms
+        // at configs[4] when it was the only test)
         bool same = true;
+        const uint32_t vmask = vbits >= 32 ? 0xFFFFFFFFu : (1u << vbits) - 1;
 #if DREPHIP_SC_ABL != 2
-        const uint64_t v0 = H[vals[start]];
-        for (uint32_t b = 0; b < m && same; b += 64) {
-            const uint32_t x = b + lane;
-            const uint64_t v = x < m ? H[vals[start + x]] : v0;
-            same = __ballot(v != v0) == 0;
+        if (32 - vbits >= kFpBits) {
+            const uint32_t f0 = vals[start] >> vbits;
+            for (uint32_t b = 0; b < m && same; b += 64) {
+                const uint32_t x = b + lane;
+                const uint32_t f = x < m ? vals[start + x] >> vbits : f0;
+                same = __ballot(f != f0) == 0;
+            }
+        } else {
+            const uint64_t v0 = H[vals[start] & vmask];
+            for (uint32_t b = 0; b < m && same; b += 64) {
+                const uint32_t x = b + lane;
+                const uint64_t v = x < m ? H[vals[start + x] & vmask] : v0;
+                same = __ballot(v != v0) == 0;
+            }
         }
 #endif
 #if DREPHIP_SC_ABL == 1
@@ -597,9 +624,8 @@ __global__ __launch_bounds__(kMarkWG) void k_screen_mark(const uint32_t *__restr
         uint32_t tcarry = 0xFFFFFFFFu;                       // the previous x block's last row tile
         for (uint32_t xb = 0; xb + 1 < m; xb += 64) {
             const uint32_t x = xb + lane;
-            const uint32_t ix = vals[start + (x < m ? x : m - 1)];
+            const uint32_t ix = vals[start + (x < m ? x : m - 1)] & vmask;
             const uint32_t gx = ix / s;
-            const uint64_t vx = H[ix];
             const bool x_ok = x < m && gx >= row0 && gx < row1;
             const uint32_t tx = x_ok ? (gx - row0) >> rshift : 0xFFFFFFFFu;
             // first lane of its row tile among the x entries (lanes are in
@@ -615,7 +641,7 @@ __global__ __launch_bounds__(kMarkWG) void k_screen_mark(const uint32_t *__restr
             for (uint32_t yb = xb; yb < m; yb += 64) {
                 const uint32_t yl = yb + lane;
                 const bool y_ok = yl < m;
-                const uint32_t iyl = vals[start + (y_ok ? yl : m - 1)];
+                const uint32_t iyl = vals[start + (y_ok ? yl : m - 1)] & vmask;
                 const uint32_t gyl = iyl / s;
                 if (same) {
                     // every x before y pairs with y: for each row tile T among the
@@ -644,6 +670,7 @@ __global__ __launch_bounds__(kMarkWG) void k_screen_mark(const uint32_t *__restr
                     }
                     continue;
                 }
+                const uint64_t vx = H[ix];
                 const uint64_t vyl = H[iyl];
                 const uint32_t ny = min(64u, m - yb);
                 for (uint32_t yi = 0; yi < ny; yi++) {
@@ -692,8 +719,9 @@ __global__ __launch_bounds__(kMarkWG) void k_screen_mark(const uint32_t *__restr
 // sketch goes heavy.  One thread per bitmap word.
 __global__ __launch_bounds__(kScWG) void k_screen_light(const uint32_t *__restrict__ bm, uint32_t *__restrict__ bmH,
                                                         const uint32_t *__restrict__ crun, const uint2 *__restrict__ runs,
-                                                        const uint32_t *__restrict__ vals, const uint32_t *__restrict__ nh,
-                                                        uint32_t s, uint32_t N, uint32_t row0, uint32_t row1, uint32_t R,
+                                                        const uint32_t *__restrict__ vals, const uint64_t *__restrict__ H,
+                                                        const uint32_t *__restrict__ nh, uint32_t s, uint32_t vmask,
+                                                        uint32_t N, uint32_t row0, uint32_t row1, uint32_t R,
                                                         uint32_t NW, uint64_t nwords, uint64_t seg0,
                                                         uint16_t *__restrict__ common,
                                                         unsigned long long *__restrict__ nlight) {
@@ -709,14 +737,20 @@ __global__ __launch_bounds__(kScWG) void k_screen_light(const uint32_t *__restri
             L &= L - 1;
             const uint32_t c = w * 32 + b;
             const uint2 run = runs[crun[(uint64_t)t * N + c]];
-            // position of genome g's entry in the run (entries in genome order), or -1
-            auto find = [&](uint32_t g) -> int32_t {
+            // position of genome g's entry in the run (entries in genome order),
+            // or -1; dup: g holds a second entry of the run (two hashes of g
+            // agreeing in their low word)
+            auto find = [&](uint32_t g, bool &dup) -> int32_t {
                 uint32_t lo = 0, hi = run.y;
                 while (lo < hi) {
                     const uint32_t mid = (lo + hi) >> 1;
-                    if (vals[run.x + mid] / s < g) lo = mid + 1; else hi = mid;
+                    if ((vals[run.x + mid] & vmask) / s < g) lo = mid + 1; else hi = mid;
                 }
-                if (lo < run.y && vals[run.x + lo] / s == g) return (int32_t)(vals[run.x + lo] - g * s);
+                dup = false;
+                if (lo < run.y && (vals[run.x + lo] & vmask) / s == g) {
+                    dup = lo + 1 < run.y && (vals[run.x + lo + 1] & vmask) / s == g;
+                    return (int32_t)((vals[run.x + lo] & vmask) - g * s);
+                }
                 return -1;
             };
             bool part = nh[c] != s;
@@ -725,17 +759,27 @@ __global__ __launch_bounds__(kScWG) void k_screen_light(const uint32_t *__restri
                 if (r >= row1 || r >= c) break;
                 part |= nh[r] != s;
             }
-            const int32_t pc = find(c);
-            if (part || pc < 0) { heavy |= 1u << b; continue; }
+            bool dup;
+            const int32_t pc = find(c, dup);
+            if (part || pc < 0 || dup) { heavy |= 1u << b; continue; }
+            // the run may mix hashes that agree in their low word (marked as one
+            // by the fingerprint test, k_screen_mark): a row holding another hash
+            // of the run than c shares none with c -- a second shared hash would
+            // be a second run marking the cell -- unless it holds two of them
+            const uint64_t hc = H[(uint64_t)c * s + pc];
+            uint32_t wrote = 0;
             for (uint32_t j = 0; j < R; j++) {
                 const uint32_t r = r0 + j;
                 if (r >= row1 || r >= c) break;
-                const int32_t pr = find(r);
+                const int32_t pr = find(r, dup);
                 if (pr < 0) continue;                                  // r shares no hash with c
+                if (dup) { heavy |= 1u << b; break; }                  // the kernel decides
+                if (H[(uint64_t)r * s + pr] != hc) continue;           // another hash of the run: none shared
                 const uint64_t o = (uint64_t)r * N - (uint64_t)r * (r + 1) / 2 + (c - r - 1) - seg0;
                 common[o] = (uint16_t)((uint32_t)(pr + pc) < s ? 1 : 0);
-                mine++;
+                wrote++;
             }
+            if (!((heavy >> b) & 1u)) mine += wrote;
         }
         if (heavy) atomicOr(bmH + wi, heavy);
     }
@@ -863,6 +907,7 @@ static int hip_scan(drephip_ctx *ctx, const char *name, const I *in, T *out, uin
 // ---------------------------------------------------------------- host phases
 // front: the entries (all, or one hash part's) grouped by key, and their runs
 struct ScreenFront {
+    uint32_t vbits = 32, vmask = 0xFFFFFFFFu;   // entry index bits (the rest: hash fingerprint, entry_val)
     uint32_t M = 0;                 // entries grouped
     uint32_t nr = 0;                // distinct keys
     uint32_t n2 = 0, nruns = 0;     // runs of two; of three or more
@@ -879,6 +924,9 @@ static int screen_front(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32
     int rc;
     uint64_t *d_eoff, *h_tot;
     uint32_t *d_pcnt = nullptr;
+    F->vbits = 1;
+    while (F->vbits < 32 && (1ull << F->vbits) < (uint64_t)N * s) F->vbits++;
+    F->vmask = F->vbits >= 32 ? 0xFFFFFFFFu : (1u << F->vbits) - 1;
     if ((rc = scratch(ctx, "sc_eoff", (N + 1) * 8ull, (void **)&d_eoff))) return rc;
     if ((rc = pinned_host(ctx, "sc_tot", 64, (void **)&h_tot))) return rc;
     if (nparts > 1) {
@@ -904,9 +952,10 @@ static int screen_front(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32
     if ((rc = scratch(ctx, "sc_runs", (M / 2 + 1) * 8ull, (void **)&F->runs))) return rc;
     prof.mark("offsets+alloc", st);
     if (nparts > 1)
-        hipLaunchKernelGGL(k_part_keys, dim3(N), dim3(kScWG), 0, st, d_hashes, d_nhash, d_eoff, s, part, nparts, k_in, v_in);
+        hipLaunchKernelGGL(k_part_keys, dim3(N), dim3(kScWG), 0, st, d_hashes, d_nhash, d_eoff, s, part, nparts, F->vbits,
+                           k_in, v_in);
     else
-        hipLaunchKernelGGL(k_screen_keys, dim3(N), dim3(kScWG), 0, st, d_hashes, d_nhash, d_eoff, s, k_in, v_in);
+        hipLaunchKernelGGL(k_screen_keys, dim3(N), dim3(kScWG), 0, st, d_hashes, d_nhash, d_eoff, s, F->vbits, k_in, v_in);
     prof.mark("keys", st);
     {
         size_t tb = 0;
@@ -952,7 +1001,7 @@ static int screen_front(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32
     if ((rc = hip_scan(ctx, "sc_scan_tmp4", bcnt2, boff2, kRunBlocks + 1, st))) return rc;
     if ((rc = hip_scan(ctx, "sc_scan_tmp5", bcnt3, boff3, kRunBlocks + 1, st))) return rc;
     hipLaunchKernelGGL(k_run_write, dim3(kRunBlocks), dim3(kScWG), 0, st, rstart, rend, nr, per, boff2, boff3, v_out, s,
-                       F->pairs, F->runs, F->rfirst, F->ridx);
+                       F->vmask, F->pairs, F->runs, F->rfirst, F->ridx);
     HIPC(hipGetLastError());
     unsigned long long *h_chk;
     if ((rc = pinned_host(ctx, "sc_chk", kRunBlocks * 8ull, (void **)&h_chk))) return rc;
@@ -992,10 +1041,10 @@ static int screen_mark_runs(drephip_ctx *ctx, const ScreenFront &F, const uint64
     prof.mark("run-sort", st);
     const dim3 grid((F.nruns + kMarkChunk - 1) / kMarkChunk);
     if (d_bmH)
-        hipLaunchKernelGGL(k_screen_mark<true>, grid, dim3(kMarkWG), 0, st, F.v_out, d_hashes, s, F.runs, ridx_s,
+        hipLaunchKernelGGL(k_screen_mark<true>, grid, dim3(kMarkWG), 0, st, F.v_out, d_hashes, s, F.vbits, F.runs, ridx_s,
                            rfirst_s, F.nruns, row0, row1, rshift, NW, d_bm, d_bmH, d_crun, N);
     else
-        hipLaunchKernelGGL(k_screen_mark<false>, grid, dim3(kMarkWG), 0, st, F.v_out, d_hashes, s, F.runs, ridx_s,
+        hipLaunchKernelGGL(k_screen_mark<false>, grid, dim3(kMarkWG), 0, st, F.v_out, d_hashes, s, F.vbits, F.runs, ridx_s,
                            rfirst_s, F.nruns, row0, row1, rshift, NW, d_bm, nullptr, nullptr, N);
     HIPC(hipGetLastError());
     return DREPHIP_OK;
@@ -1168,7 +1217,7 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
     if ((rc = screen_mark_runs(ctx, F, d_hashes, N, row0, row1, rshift, NW, d_bm, d_bmH, d_crun, st, prof))) return rc;
     if (F.n2) {
         const uint32_t g2 = std::max(1u, std::min(8192u, (F.n2 + kScWG - 1) / kScWG));
-        hipLaunchKernelGGL(k_screen_mark2, dim3(g2), dim3(kScWG), 0, st, F.v_out, d_hashes, s, F.pairs, F.n2, row0, row1,
+        hipLaunchKernelGGL(k_screen_mark2, dim3(g2), dim3(kScWG), 0, st, F.v_out, d_hashes, s, F.vmask, F.pairs, F.n2, row0, row1,
                            pkey, pcnt, ppos, (uint32_t)(pcap - 1));
         const uint32_t gs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(2048, (pcap + kScWG - 1) / kScWG));
         hipLaunchKernelGGL(k_screen_simple, dim3(gs), dim3(kScWG), 0, st, pkey, pcnt, ppos, (uint32_t)pcap, d_nhash, s, N, row0,
@@ -1178,8 +1227,8 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
     if (light && F.nruns) {
         const uint64_t nwords = (uint64_t)ntiles * NW;
         const uint32_t gl = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(4096, (nwords + kScWG - 1) / kScWG));
-        hipLaunchKernelGGL(k_screen_light, dim3(gl), dim3(kScWG), 0, st, d_bm, d_bmH, d_crun, F.runs, F.v_out, d_nhash, s, N,
-                           row0, row1, R, NW, nwords, seg0, d_common, d_nsimple);
+        hipLaunchKernelGGL(k_screen_light, dim3(gl), dim3(kScWG), 0, st, d_bm, d_bmH, d_crun, F.runs, F.v_out, d_hashes,
+                           d_nhash, s, F.vmask, N, row0, row1, R, NW, nwords, seg0, d_common, d_nsimple);
         prof.mark("light", st);
     }
     // the LIST kernels take the heavy cells (every marked cell without the light screen)
@@ -1225,8 +1274,8 @@ int screen_part_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t 
         if ((rc = screen_mark_runs(ctx, F, d_hashes, N, 0, N, rshift, NW, d_gbm, nullptr, nullptr, st, prof))) return rc;
         if (F.n2) {
             const uint32_t g2 = std::max(1u, std::min(8192u, (F.n2 + kScWG - 1) / kScWG));
-            hipLaunchKernelGGL(k_screen_emit2, dim3(g2), dim3(kScWG), 0, st, F.v_out, d_hashes, s, F.pairs, F.n2, d_rec,
-                               d_nrec);
+            hipLaunchKernelGGL(k_screen_emit2, dim3(g2), dim3(kScWG), 0, st, F.v_out, d_hashes, s, F.vmask, F.pairs, F.n2,
+                               d_rec, d_nrec);
         }
         prof.mark("mark", st);
     }
