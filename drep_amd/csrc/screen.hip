@@ -96,86 +96,94 @@ __device__ __forceinline__ void block_count_add(uint32_t mine, unsigned long lon
 }
 
 // Hash parts (the sharded screen, screen_part_impl): part p of P holds the
-// entries whose key (low word) lies in [p 2^32 / P, (p + 1) 2^32 / P), so a run
-// of equal keys lies in one part.  Keys are uniform (Murmur3 low words).
-__device__ __forceinline__ uint32_t key_part(uint32_t key, uint32_t nparts) {
-    return (uint32_t)(((uint64_t)key * nparts) >> 32);
-}
-// entries of genome g in the part (one workgroup per genome)
-constexpr uint32_t kPartPer = 4;
-__global__ __launch_bounds__(kScWG) void k_part_count(const uint64_t *__restrict__ H, const uint32_t *__restrict__ nh,
-                                                      uint32_t s, uint32_t part, uint32_t nparts,
-                                                      uint32_t *__restrict__ cnt) {
-    __shared__ uint32_t red[kScWG / 64];
-    const uint32_t g = blockIdx.x, n = nh[g];
-    const uint64_t *A = H + (uint64_t)g * s;
-    uint32_t c = 0;
-    for (uint32_t k = threadIdx.x; k < n; k += kScWG * kPartPer) {
-#pragma unroll
-        for (uint32_t e = 0; e < kPartPer; e++)
-            c += k + e * kScWG < n && key_part((uint32_t)A[k + e * kScWG], nparts) == part;
+// hashes in the value range [bnd[p - 1], bnd[p]) (bnd[-1] = 0, bnd[P - 1] =
+// infinity).  Equal hashes share a part, and as a sketch is ascending, a
+// genome's entries of one part are one contiguous range of its row, found by
+// two binary searches: a part's entries are read from 1/P of the matrix.
+// (The first sharded screen cut the parts by low word, which left every run
+// of equal keys whole but read all N s entries twice per part: 0.36 of its
+// 1.48 ms at configs[4], W = 8.)  A run of equal low words in one part holds
+// only that part's hashes, so low-word collisions across parts fall apart --
+// fewer pairwise checks, the same marks.
+//
+// A bottom-s sketch holds the s smallest hashes of its genome, ~uniform on
+// [0, T_g] with T_g set by the genome's k-mer count, so fixed cuts of the
+// 64-bit range would put every entry in part 0.  bnd[p - 1] is the median
+// over (up to 1024 evenly spaced) genomes of the genome's own p/P quantile
+// A_g[n_g p / P]: every rank computes the same cuts from the same gathered
+// sketches, and a part holds ~1/P of a typical genome's entries.  (Medians of
+// nondecreasing sequences are nondecreasing: the cuts are ordered.)
+constexpr uint32_t kBndSample = 1024;
+__global__ __launch_bounds__(kBndSample) void k_part_bounds(const uint64_t *__restrict__ H,
+                                                            const uint32_t *__restrict__ nh, uint32_t N, uint32_t s,
+                                                            uint32_t nparts, uint64_t *__restrict__ bnd) {
+    __shared__ uint64_t v[kBndSample];
+    const uint32_t p = blockIdx.x + 1, t = threadIdx.x;
+    const uint32_t ns = N < kBndSample ? N : kBndSample;
+    uint64_t x = ~0ull;                                                // no sample: sorts last
+    if (t < ns) {
+        const uint32_t g = (uint32_t)((uint64_t)t * N / ns), n = nh[g];
+        if (n) x = H[(uint64_t)g * s + (uint64_t)n * p / nparts];
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t t = 0;
-        for (int w = 0; w < kScWG / 64; w++) t += red[w];
-        cnt[g] = t;
-    }
-}
-// the part's entries in genome order: the sorted runs list their genomes in
-// ascending order, as k_screen_keys' full set does.  (Within a genome the
-// order is free: a genome's entries are distinct hashes, so two of them never
-// share a run's hash.)  A step covers kScWG x kPartPer entries, loads
-// coalesced (entry k0 + e kScWG + thread); each thread's count is placed by a
-// wave scan and the waves' totals
-__global__ __launch_bounds__(kScWG) void k_part_keys(const uint64_t *__restrict__ H, const uint32_t *__restrict__ nh,
-                                                     const uint64_t *__restrict__ eoff, uint32_t s, uint32_t part,
-                                                     uint32_t nparts, uint32_t vbits, uint32_t *__restrict__ keys,
-                                                     uint32_t *__restrict__ vals) {
-    __shared__ uint32_t wsum[2][kScWG / 64];
-    const uint32_t g = blockIdx.x, n = nh[g], lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t *A = H + (uint64_t)g * s;
-    uint64_t o = eoff[g];
-    int buf = 0;
-    for (uint32_t k0 = 0; k0 < n; k0 += kScWG * kPartPer) {            // uniform trip count
-        const uint32_t k = k0 + threadIdx.x;
-        uint32_t key[kPartPer], hw[kPartPer], c = 0, inmask = 0;
-#pragma unroll
-        for (uint32_t e = 0; e < kPartPer; e++) {
-            const uint64_t h = k + e * kScWG < n ? A[k + e * kScWG] : 0ull;
-            key[e] = (uint32_t)h;
-            hw[e] = (uint32_t)(h >> 32);
-            const bool in = k + e * kScWG < n && key_part(key[e], nparts) == part;
-            inmask |= (uint32_t)in << e;
-            c += in;
-        }
-        uint32_t inc = c;                                              // inclusive wave scan of the counts
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(inc, d, 64);
-            if (lane >= (uint32_t)d) inc += y;
-        }
-        if (lane == 63) wsum[buf][wave] = inc;
-        __syncthreads();
-        uint32_t base = inc - c, tot = 0;
-#pragma unroll
-        for (uint32_t w = 0; w < kScWG / 64; w++) {
-            if (w < wave) base += wsum[buf][w];
-            tot += wsum[buf][w];
-        }
-        buf ^= 1;                                                      // the next step writes the other copy
-#pragma unroll
-        for (uint32_t e = 0; e < kPartPer; e++) {
-            if ((inmask >> e) & 1u) {
-                keys[o + base] = key[e];
-                vals[o + base] = entry_val(g * s + k + e * kScWG, (uint64_t)hw[e] << 32, vbits);
-                base++;
+    const uint32_t valid = __syncthreads_count(x != ~0ull);
+    v[t] = x;
+    for (uint32_t k = 2; k <= kBndSample; k <<= 1)                     // bitonic sort, ascending
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            __syncthreads();
+            const uint32_t o = t ^ j;
+            if (o > t) {
+                const uint64_t a = v[t], b = v[o];
+                if ((a > b) == ((t & k) == 0)) {
+                    v[t] = b;
+                    v[o] = a;
+                }
             }
         }
-        o += tot;
+    __syncthreads();
+    if (t == 0) bnd[p - 1] = valid ? v[valid / 2] : ~0ull;
+}
+// first k in [0, n) with A[k] >= x (A ascending)
+__device__ __forceinline__ uint32_t lower_bound_u64(const uint64_t *__restrict__ A, uint32_t n, uint64_t x) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (A[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+// the part's range [beg[g], beg[g] + cnt[g]) of every genome's row
+__global__ __launch_bounds__(kScWG) void k_part_range(const uint64_t *__restrict__ H, const uint32_t *__restrict__ nh,
+                                                      const uint64_t *__restrict__ bnd, uint32_t N, uint32_t s,
+                                                      uint32_t part, uint32_t nparts, uint32_t *__restrict__ beg,
+                                                      uint32_t *__restrict__ cnt) {
+    const uint32_t g = blockIdx.x * kScWG + threadIdx.x;
+    if (g >= N) return;
+    const uint32_t n = nh[g];
+    const uint64_t *A = H + (uint64_t)g * s;
+    const uint32_t b = part == 0 ? 0 : lower_bound_u64(A, n, bnd[part - 1]);
+    const uint32_t e = part + 1 >= nparts ? n : b + lower_bound_u64(A + b, n - b, bnd[part]);
+    beg[g] = b;
+    cnt[g] = e - b;
+}
+// the part's entries in genome order (the sorted runs list their genomes in
+// ascending order, as k_screen_keys' full set does): one wave per genome
+// copies its range
+constexpr uint32_t kPartWaves = kScWG / 64;
+__global__ __launch_bounds__(kScWG) void k_part_keys(const uint64_t *__restrict__ H, const uint32_t *__restrict__ beg,
+                                                     const uint32_t *__restrict__ cnt, const uint64_t *__restrict__ eoff,
+                                                     uint32_t N, uint32_t s, uint32_t vbits, uint32_t *__restrict__ keys,
+                                                     uint32_t *__restrict__ vals) {
+    const uint32_t g = blockIdx.x * kPartWaves + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (g >= N) return;                                                // wave-uniform
+    const uint32_t b = beg[g], n = cnt[g];
+    const uint64_t o = eoff[g];
+    const uint64_t *A = H + (uint64_t)g * s + b;
+#pragma unroll 4
+    for (uint32_t k = lane; k < n; k += 64) {
+        const uint64_t h = A[k];
+        keys[o + k] = (uint32_t)h;
+        vals[o + k] = entry_val(g * s + b + k, h, vbits);
     }
 }
 
@@ -923,7 +931,7 @@ static int screen_front(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32
     const uint32_t s = ctx->s;
     int rc;
     uint64_t *d_eoff, *h_tot;
-    uint32_t *d_pcnt = nullptr;
+    uint32_t *d_pcnt = nullptr, *d_pbeg = nullptr;
     F->vbits = 1;
     while (F->vbits < 32 && (1ull << F->vbits) < (uint64_t)N * s) F->vbits++;
     F->vmask = F->vbits >= 32 ? 0xFFFFFFFFu : (1u << F->vbits) - 1;
@@ -932,7 +940,13 @@ static int screen_front(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32
     if (nparts > 1) {
         // the part's entries per genome, then their offsets
         if ((rc = scratch(ctx, "sc_part_cnt", (N + 1) * 4ull, (void **)&d_pcnt))) return rc;
-        hipLaunchKernelGGL(k_part_count, dim3(N), dim3(kScWG), 0, st, d_hashes, d_nhash, s, part, nparts, d_pcnt);
+        if ((rc = scratch(ctx, "sc_part_beg", (N + 1) * 4ull, (void **)&d_pbeg))) return rc;
+        uint64_t *d_bnd;
+        if ((rc = scratch(ctx, "sc_part_bnd", nparts * 8ull, (void **)&d_bnd))) return rc;
+        hipLaunchKernelGGL(k_part_bounds, dim3(nparts - 1), dim3(kBndSample), 0, st, d_hashes, d_nhash, N, s, nparts,
+                           d_bnd);
+        hipLaunchKernelGGL(k_part_range, dim3((N + kScWG - 1) / kScWG), dim3(kScWG), 0, st, d_hashes, d_nhash, d_bnd,
+                           N, s, part, nparts, d_pbeg, d_pcnt);
         if ((rc = hip_scan(ctx, "sc_scan_tmp0", (const uint32_t *)d_pcnt, d_eoff, N, st))) return rc;
         hipLaunchKernelGGL(k_screen_total, dim3(1), dim3(64), 0, st, d_pcnt, d_eoff, N);
     } else {
@@ -952,8 +966,8 @@ static int screen_front(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32
     if ((rc = scratch(ctx, "sc_runs", (M / 2 + 1) * 8ull, (void **)&F->runs))) return rc;
     prof.mark("offsets+alloc", st);
     if (nparts > 1)
-        hipLaunchKernelGGL(k_part_keys, dim3(N), dim3(kScWG), 0, st, d_hashes, d_nhash, d_eoff, s, part, nparts, F->vbits,
-                           k_in, v_in);
+        hipLaunchKernelGGL(k_part_keys, dim3((N + kPartWaves - 1) / kPartWaves), dim3(kScWG), 0, st, d_hashes, d_pbeg,
+                           d_pcnt, d_eoff, N, s, F->vbits, k_in, v_in);
     else
         hipLaunchKernelGGL(k_screen_keys, dim3(N), dim3(kScWG), 0, st, d_hashes, d_nhash, d_eoff, s, F->vbits, k_in, v_in);
     prof.mark("keys", st);

@@ -281,8 +281,10 @@ int drephip_last_screen_stats(drephip_ctx *ctx, int *used, uint64_t *entries, ui
 
 /* The sharded screen (a W-way sharded `mash dist`, one rank per GPU): instead
  * of every rank grouping all N x s entries, rank p groups hash part p of W
- * (entries whose low word lies in [p 2^32 / W, (p + 1) 2^32 / W): a run of
- * equal keys lies in one part), marks the (row tile, column) cells of EVERY
+ * (the p-th of W hash value ranges, cut at the medians over the genomes of
+ * each sketch's p/W quantiles, so every rank computes the same cuts: equal
+ * hashes lie in one part, and each sketch row -- ascending, as every all-pairs
+ * call requires -- holds a part's hashes in one range), marks the (row tile, column) cells of EVERY
  * row from its runs of >= 3 and lists its runs of two; the ranks route the
  * marks to the ranks owning their rows (an all-to-all: RCCL or gloo, the
  * caller's), and each rank screens its own rows from what it received.  Same

@@ -26,13 +26,13 @@ def planted_sketches(N, s, seed, fam=6, partial_every=7, lo_twins=40, hub=True):
     rng = np.random.default_rng(seed)
     H = np.full((N, s), UMAX, dtype=np.uint64)
     NH = np.zeros(N, dtype=np.uint32)
-    hubv = np.uint64(rng.integers(1, 1 << 40))
+    hubv = np.uint64(rng.integers(1, UMAX, dtype=np.uint64))
     pools = {}
     for g in range(N):
         f = g // fam
         if f not in pools:
-            pools[f] = rng.integers(1, 1 << 62, size=3 * s, dtype=np.uint64)
-        own = rng.integers(1, 1 << 62, size=s, dtype=np.uint64)
+            pools[f] = rng.integers(1, UMAX, size=3 * s, dtype=np.uint64)     # the whole 64-bit range
+        own = rng.integers(1, UMAX, size=s, dtype=np.uint64)
         take = rng.random(3 * s) < 0.3
         vals = np.unique(np.concatenate([pools[f][take], own] + ([np.array([hubv])] if hub and g % 3 == 0 else [])))
         n = s if g % partial_every else int(rng.integers(1, s))
@@ -44,7 +44,7 @@ def planted_sketches(N, s, seed, fam=6, partial_every=7, lo_twins=40, hub=True):
         if a == b or NH[a] == 0 or NH[b] == 0:
             continue
         v = H[a, rng.integers(0, NH[a])]
-        twin = (v & np.uint64(0xFFFFFFFF)) | (np.uint64(rng.integers(1, 1 << 30)) << np.uint64(32))
+        twin = (v & np.uint64(0xFFFFFFFF)) | (np.uint64(rng.integers(1, 1 << 32)) << np.uint64(32))
         if twin in H[b, :NH[b]] or twin in H[a, :NH[a]]:
             continue
         row = np.sort(np.concatenate([H[b, :NH[b]], [twin]]))[:s]
@@ -308,7 +308,7 @@ def test_sharded_screen_matches_oracle(s, N, W):
     ranges that start off a row tile boundary (a part's tile then covers two
     of the range's) -- bit-exact against the oracle, on the planted sketches
     (families, partial sketches, low-word twins, a hub in a third of the
-    genomes); the parts' pair checks add up to the one-call screen's."""
+    genomes); the parts' pair checks are at most the one-call screen's."""
     import torch
     from drep_amd import parallel
     H, NH = planted_sketches(N, s, seed=s + N + W)
@@ -327,7 +327,9 @@ def test_sharded_screen_matches_oracle(s, N, W):
             assert np.array_equal(co, oc[start(r0):start(r1)]), (r0, r1)
             assert np.array_equal(do, od[start(r0):start(r1)]), (r0, r1)
         ctx.allpairs(H, NH, want_denom=True)
-        assert ctx.screen_stats()["checks"] == checks
+        # a run of keys equal in their low word only may span parts (its
+        # hashes' high words differ): the parts check no more pairs than one call
+        assert 0 < checks <= ctx.screen_stats()["checks"]
         assert ctx.screen_worth(N, checks) == (True, True)           # mode ON
     assert sum(nrecs) > 0 and (oc > 0).sum() > N
 
@@ -340,7 +342,7 @@ def test_sharded_screen_single_shared_hash_pairs():
     import torch
     s, N = 256, 400
     rng = np.random.default_rng(33)
-    H = np.sort(rng.integers(1, 1 << 62, size=(N, s), dtype=np.uint64), axis=1)
+    H = np.sort(rng.integers(1, UMAX, size=(N, s), dtype=np.uint64), axis=1)
     NH = np.full(N, s, dtype=np.uint32)
     for g in range(0, N, 11):
         NH[g] = rng.integers(s // 3, s)
