@@ -367,6 +367,46 @@ def test_sharded_screen_single_shared_hash_pairs():
             assert ctx.screen_stats()["simple"] > 300
 
 
+@pytest.mark.parametrize("s,N,W", [(16, 1500, 8), (16, 1500, 3), (3, 600, 8)])
+def test_sharded_screen_value_cuts(s, N, W):
+    """The parts are value ranges cut at medians of per-sketch quantiles
+    (k_part_bounds): more genomes than the 1024 sampled ones, empty and
+    partial sketches among them, sketches of genomes of different sizes (a
+    small genome's bottom-s reaches higher values), and s = 3 with 8 parts
+    (equal cuts: empty parts).  Every hash shared anywhere in the value range
+    must be grouped by exactly one part: bit-exact against the oracle."""
+    import torch
+    rng = np.random.default_rng(s * N + W)
+    pool = rng.integers(1, UMAX, size=20 * s, dtype=np.uint64)
+    H = np.full((N, s), UMAX, dtype=np.uint64)
+    NH = np.zeros(N, dtype=np.uint32)
+    for g in range(N):
+        if g % 7 == 3:
+            continue                                          # empty sketch
+        scale = np.uint64(1 << int(rng.integers(0, 6)))       # "genome size": values up to UMAX / scale
+        own = rng.integers(1, UMAX, size=s, dtype=np.uint64) // scale
+        vals = np.unique(np.concatenate([rng.choice(pool, s // 2 + 1) // scale, own]))
+        n = s if g % 5 else int(rng.integers(1, s + 1))
+        H[g, :min(n, len(vals))] = vals[:n]
+        NH[g] = min(n, len(vals))
+    oc, od = oracle.allpairs(H, NH, s, threads=8)
+    dH = torch.from_numpy(H.view(np.int64)).cuda()
+    dNH = torch.from_numpy(NH.view(np.int32)).cuda()
+    from drep_amd import parallel
+
+    def start(i):
+        return i * N - i * (i + 1) // 2
+    with _lib.Context(0, 21, s, 42) as ctx:
+        ctx.set_allpairs_screen(ctx.SCREEN_ON)
+        ranges = [(a, min(b, N - 1)) for a, b in parallel.row_partition(N, W) if a < N - 1]
+        segs, checks, _ = sharded_screen(ctx, dH, dNH, N, W, ranges)
+        for (r0, r1), (co, do) in zip(ranges, segs):
+            assert np.array_equal(co, oc[start(r0):start(r1)]), (r0, r1)
+            assert np.array_equal(do, od[start(r0):start(r1)]), (r0, r1)
+        assert checks > 0
+    assert (oc > 0).sum() > N // 2
+
+
 def test_sharded_screen_arguments_checked():
     import torch
     with _lib.Context(0, 21, 1000, 42) as ctx:
