@@ -34,6 +34,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 namespace drephip {
@@ -367,7 +368,12 @@ __device__ __forceinline__ void probe_rows(const Slots<R> &sl, uint64_t b, uint3
 //   cnt += popc(rank & m);  mrun += popc(m)
 // nb[r] = -(s + mrun) is kept instead of mrun, so the rank operand is one
 // three-input add with a scalar (v_add3) and mbcnt needs no scalar base.
-template <int R>
+//
+// EXACT = false (a chunk the dense verdict's chunk mask leaves clear,
+// screen.hip k_cmask_*): no other 64-bit hash of the matrix shares a low word
+// with this chunk's elements, so a slot holding b's low word holds b itself --
+// the high-word reads and compares are skipped, m = ballot(f < nA).
+template <int R, bool EXACT = true>
 __device__ __forceinline__ void probe_rows_v(const Slots<R> &sl, uint64_t b, uint32_t jl, const uint32_t *V,
                                              uint32_t hm, uint32_t s, const uint32_t (&nA)[R], int32_t (&nb)[R],
                                              uint32_t (&cnt)[R]) {
@@ -396,13 +402,16 @@ __device__ __forceinline__ void probe_rows_v(const Slots<R> &sl, uint64_t b, uin
 #pragma unroll
     for (int r = 0; r < R; r++) {
         f[r] = min(xs1[r], xs2[r]);
-        vh[r] = V[min(f[r], s - 1) * R + r];                          // row-interleaved high words
+        if constexpr (EXACT) vh[r] = V[min(f[r], s - 1) * R + r];    // row-interleaved high words
+    }
+    if constexpr (EXACT) {
+#pragma unroll
+        for (int r = 0; r < R; r++) asm volatile("" : "+v"(vh[r]));  // all R reads issued before the first use
     }
 #pragma unroll
-    for (int r = 0; r < R; r++) asm volatile("" : "+v"(vh[r]));     // all R reads issued before the first use
-#pragma unroll
     for (int r = 0; r < R; r++) {
-        const uint64_t m = __builtin_amdgcn_ballot_w64(vh[r] == bhi) & __builtin_amdgcn_ballot_w64(f[r] < nA[r]);
+        const uint64_t m = EXACT ? __builtin_amdgcn_ballot_w64(vh[r] == bhi) & __builtin_amdgcn_ballot_w64(f[r] < nA[r])
+                                 : __builtin_amdgcn_ballot_w64(f[r] < nA[r]);
         const int32_t pre = (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         const int32_t key = (int32_t)(f[r] + jl) + nb[r];
@@ -458,7 +467,8 @@ __device__ __forceinline__ uint64_t ld_chunk_at(__amdgpu_buffer_rsrc_t rs, uint3
 // LIST (the screened path, screen.hip): the item's columns are clist[0..cend)
 // -- ascending, each sharing a hash with a row of the tile -- and c_first /
 // c_step walk that list instead of the column range.
-template <int R, int NCH, bool FAST, int KB, bool MASKED, bool LIST = false, bool HITQ = false, bool HITV = false>
+template <int R, int NCH, bool FAST, int KB, bool MASKED, bool LIST = false, bool HITQ = false, bool HITV = false,
+          bool COLL = false>
 __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, const uint32_t *__restrict__ nhash,
                                            const uint32_t *T, const uint32_t *V, uint32_t H, uint32_t hm, uint32_t s,
                                            uint32_t N, uint32_t i0, uint32_t nrows, uint32_t cend, uint32_t c_first,
@@ -467,7 +477,8 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
                                            const uint32_t (&o2)[R], const uint64_t (&alast)[R],
                                            const uint64_t (&thr1)[R], const uint64_t (&thr2)[R], uint32_t okmask,
                                            bool any_partial_row, uint16_t *__restrict__ common,
-                                           uint16_t *__restrict__ denom, uint64_t seg0) {
+                                           uint16_t *__restrict__ denom, uint64_t seg0,
+                                           const uint32_t *__restrict__ cmask = nullptr) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t lane_off = lane * 8u;
     const uint32_t nch = (s + 63) / 64;
@@ -480,6 +491,15 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
     uint32_t kc = rfl(c_first);                                      // wave-uniform: scalar column loop
     auto column_of = [&](uint32_t k) -> uint32_t { return LIST ? rfl(clist[k]) : k; };
     uint32_t c = kc < cend ? column_of(kc) : 0;
+    // COLL: the next column's chunk mask, by a vector (buffer) load issued with
+    // its first chunks -- a scalar load in flight across the chunk loop would
+    // hold every LDS wait there at lgkmcnt(0)
+    uint32_t cmn = ~0u;
+    const __amdgpu_buffer_rsrc_t rcm =
+        __builtin_amdgcn_make_buffer_rsrc((void *)cmask, (short)0, COLL ? (int)(N * 4u) : 0, kBufferRsrcWord3);
+    auto next_cmask = [&](uint32_t cn) {
+        if constexpr (COLL) cmn = __builtin_amdgcn_raw_buffer_load_b32(rcm, 0u, cn * 4u, 0);
+    };
     auto first_chunks = [&](__amdgpu_buffer_rsrc_t rn) {
         if constexpr (MASKED) {
 #pragma unroll
@@ -492,7 +512,10 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
         }
     };
     static_assert(kRing == 4, "first_chunks / refill offsets");
-    if (kc < cend) first_chunks(column_rsrc(hashes + (uint64_t)c * s, s));
+    if (kc < cend) {
+        next_cmask(c);
+        first_chunks(column_rsrc(hashes + (uint64_t)c * s, s));
+    }
     // per item, not per column: the active rows and their largest hash once
     // every row of the tile is left of the column (c >= i0 + R: all columns
     // but the diagonal tile's), and row 0's output offset (row r + 1's is row
@@ -510,9 +533,14 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
         const __amdgpu_buffer_rsrc_t rc = column_rsrc(hashes + (uint64_t)c * s, s);
 #pragma unroll
         for (int k = 0; k < kRing; k++) rg[k] = nx[k];
+        const uint32_t cmc = cmn;                                      // this column's chunk mask (COLL)
         const uint32_t kn = kc + c_step;
         cnext = kn < cend ? column_of(kn) : 0;
-        if (kn < cend) first_chunks(column_rsrc(hashes + (uint64_t)cnext * s, s));
+        if (kn < cend) {
+            next_cmask(cnext);
+            first_chunks(column_rsrc(hashes + (uint64_t)cnext * s, s));
+        }
+        const uint32_t cm = COLL ? rfl(cmc) : ~0u;                    // bit k: chunk k needs the high-word check
         uint32_t cnt[R], mrun[R], actmask = act_full;
         int32_t nb[R];                                                // HITV: -(s + matches so far), probe_rows_v
         // elements past every active row's largest hash cannot match: the
@@ -595,17 +623,21 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
                 if (((actmask >> r) & 1u) && !(pr[r] < nA[r] && hb > rfl(vr[r]))) all_past = false;
             return all_past;
         };
-        for (uint32_t kb = 0; kb < nch; kb += kRing) {
+        // one group of kRing chunks; false: the column's scan ends here.
+        // EXACT: every hit confirmed by its high word (COLL: only the groups
+        // from the first chunk the column's mask flags on; the groups before it
+        // run the unchecked probe, with no per-chunk branch)
+        auto group = [&](uint32_t kb, auto exact_tag) -> bool {
             {
                 const uint64_t b = rg[0];
                 // smallest element of the group (lane 0; readfirstlane returns
                 // int: through uint32_t so the low word is not sign-extended)
                 const uint64_t b0 = ((uint64_t)rfl((uint32_t)(b >> 32)) << 32) | rfl((uint32_t)b);
-                if (b0 == kEmpty || b0 > amax) break;
+                if (b0 == kEmpty || b0 > amax) return false;
 #if DREPHIP_AP_MID
-                if (!HITQ && kb > kb1 && past(b, thr2)) break;             // wave-uniform
+                if (!HITQ && kb > kb1 && past(b, thr2)) return false;      // wave-uniform
 #else
-                if (kb >= kb1 && past(b, kb == kb1 ? thr1 : thr2)) break;    // wave-uniform
+                if (kb >= kb1 && past(b, kb == kb1 ? thr1 : thr2)) return false;    // wave-uniform
 #endif
             }
             const uint32_t gofs = rfl(kb) * 512u;                        // the group's byte offset (SGPR)
@@ -626,7 +658,7 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
                 // waits for the refill load issued in the same chunk
                 if constexpr (HITV) {
                     static_assert(FAST && !MASKED, "probe_rows_v: the FAST unmasked path");
-                    probe_rows_v<R>(sb[u], b, k * 64 + lane, V, hm, s, nA, nb, cnt);
+                    probe_rows_v<R, decltype(exact_tag)::value>(sb[u], b, k * 64 + lane, V, hm, s, nA, nb, cnt);
                 } else if (!MASKED || k < nch) {                          // wave-uniform
                     probe_rows<R, FAST, !FAST, true>(sb[u], b, k * 64 + lane, V, s, hm, o1, o2, actmask, lm, zero, nA, s,
                                                mrun, cnt);
@@ -653,16 +685,25 @@ __device__ __forceinline__ void ap_columns(const uint64_t *__restrict__ hashes, 
                     // matches of every chunk before it
                     // (tested twice per group, chunks 0 and 2: 2 % slower on the dense
                     // 10^4 set, equal elsewhere -- profiles/r06_allpairs_hit_ab.txt)
-                    if (u == 0 && kb >= kb1 && kb + 1 < nch && past_v(rg[1], 64 * (kb + 1))) goto column_done;
+                    if (u == 0 && kb >= kb1 && kb + 1 < nch && past_v(rg[1], 64 * (kb + 1))) return false;
                 } else {
-                    if (u == 0 && kb == kb1 && kb1 + 1 < nch && past(rg[1], thr1)) goto column_done;
+                    if (u == 0 && kb == kb1 && kb1 + 1 < nch && past(rg[1], thr1)) return false;
                 }
 #endif
             }
+            return true;
+        };
+        {
+            uint32_t kb = 0;
+            if constexpr (COLL) {
+                const uint32_t kf = cm ? ((uint32_t)__builtin_ctz(cm) & ~(uint32_t)(kRing - 1)) : 32u;
+                for (; kb < kf && kb < nch; kb += kRing)
+                    if (!group(kb, std::false_type{})) goto column_done;
+            }
+            for (; kb < nch; kb += kRing)
+                if (!group(kb, std::true_type{})) goto column_done;
         }
-#if DREPHIP_AP_MID
     column_done:
-#endif
         if (lane == 0) {
             // the column's count is read only here: a scalar load left in flight
             // across the chunk loop would force every LDS wait there to lgkmcnt(0)
@@ -702,7 +743,7 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
     const uint32_t *__restrict__ blk, uint32_t stride, const uint8_t *__restrict__ fam, uint32_t s, uint32_t N,
     uint32_t row0, uint32_t row1, uint32_t B, const uint4 *__restrict__ items,
     uint16_t *__restrict__ common, uint16_t *__restrict__ denom, uint64_t seg0, const uint32_t *__restrict__ clist,
-    int hitq) {
+    int hitq, const uint32_t *__restrict__ cmask) {
     constexpr int WG = kApWG;
     extern __shared__ __align__(16) uint32_t lds[];    // 16-B aligned: slot words are read with ds_read_b128
     const uint32_t H = 1u << B, hm = H - 1, TS = 2 * H;
@@ -781,7 +822,13 @@ __global__ __launch_bounds__(kApWG, MINW) void k_allpairs_q(
     // The kernel declares no static LDS (.group_segment_fixed_size 0, checked
     // by tests/test_host.py), so `lds` is LDS address 0 (read_slots).
     constexpr int KB = NCH == 16 ? 11 : 0;
-    if (fast && !zero_key && hitq)
+    if (fast && !zero_key && hitq && !LIST && cmask)
+        // the dense path after the screen's verdict: chunk masks (probe_rows_v)
+        ap_columns<R, NCH, true, KB, false, LIST, true, true, !LIST>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend,
+                                                                    cfirst + wave, WG / 64, ilist, nA, o1, o2, alast, thr1,
+                                                                    thr2, ~failmask, any_partial_row, common, denom, seg0,
+                                                                    cmask);
+    else if (fast && !zero_key && hitq)
         ap_columns<R, NCH, true, KB, false, LIST, true, true>(hashes, nhash, T, V, H, hm, s, N, i0, nrows, cend,
                                                         cfirst + wave, WG / 64, ilist, nA, o1, o2, alast, thr1, thr2,
                                                         ~failmask, any_partial_row, common, denom, seg0);
@@ -1535,7 +1582,7 @@ template <int R, int NCH, int MINW, bool LIST>
 static int launch_q(drephip_ctx *ctx, uint32_t nitems, size_t lds, hipStream_t st, const uint64_t *h,
                     const uint32_t *nh, const uint32_t *blk, uint32_t stride, const uint8_t *fam, uint32_t N, uint32_t row0,
                     uint32_t row1, uint32_t B, const uint4 *items, uint16_t *cm, uint16_t *dn,
-                    uint64_t seg0, const uint32_t *clist) {
+                    uint64_t seg0, const uint32_t *clist, const uint32_t *cmask) {
     HIPC(hipFuncSetAttribute((const void *)k_allpairs_q<R, NCH, MINW, LIST>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)lds));
     // the branch-free hit probe and the union-rank end for rows with matches
@@ -1547,7 +1594,8 @@ static int launch_q(drephip_ctx *ctx, uint32_t nitems, size_t lds, hipStream_t s
     for (uint32_t i0 = 0; i0 < nitems; i0 += (uint32_t)max_blocks(kApWG))
         hipLaunchKernelGGL((k_allpairs_q<R, NCH, MINW, LIST>),
                            dim3(std::min<uint32_t>(nitems - i0, (uint32_t)max_blocks(kApWG))), dim3(kApWG), lds, st, h,
-                           nh, blk, stride, fam, ctx->s, N, row0, row1, B, items + i0, cm, dn, seg0, clist, hitq);
+                           nh, blk, stride, fam, ctx->s, N, row0, row1, B, items + i0, cm, dn, seg0, clist, hitq,
+                           LIST ? nullptr : cmask);
     timing_mark(ctx, 2, st, false);
     HIPC(hipGetLastError());
     return DREPHIP_OK;
@@ -1715,7 +1763,7 @@ int allpairs_device_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint3
     // two workgroups per CU when the LDS allows
     const bool two = lds <= 80 * 1024;
 #define DREPHIP_Q1(RR, NC, MW, LS) launch_q<RR, NC, MW, LS>(ctx, ni, lds, st, d_hashes, d_nhash, d_blk, stride, d_fam, N, row0, row1, B, \
-                                                          d_items, d_common, d_denom, seg0, scr.clist)
+                                                          d_items, d_common, d_denom, seg0, scr.clist, scr.use ? nullptr : scr.cmask)
 #define DREPHIP_Q(RR, NC) (two ? (lst ? DREPHIP_Q1(RR, NC, 8, true) : DREPHIP_Q1(RR, NC, 8, false)) \
                                : (lst ? DREPHIP_Q1(RR, NC, 4, true) : DREPHIP_Q1(RR, NC, 4, false)))
     if (nch <= 8) {

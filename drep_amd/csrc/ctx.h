@@ -89,6 +89,9 @@ struct ScreenResult {
     uint64_t checks = 0;          // pair checks of the marking (sum of m(m-1)/2)
     uint64_t marked = 0;          // marked (row tile, column) cells
     uint64_t simple = 0;          // pairs sharing exactly one hash, written by the screen itself
+    // use == false after a dense verdict: per genome, the 64-element chunks
+    // whose hits need the high-word check (k_cmask_*; device, or null)
+    const uint32_t *cmask = nullptr;
 };
 
 // The last hash part a sharded screen grouped (screen_part_impl): its marked

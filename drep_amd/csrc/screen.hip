@@ -328,6 +328,61 @@ __global__ __launch_bounds__(kScWG) void k_run_write(const uint32_t *__restrict_
 // such runs hold the pair; the hash's positions i in a and j in b) instead of
 // the bitmap: a pair that shares exactly one hash has count (i + j < s) --
 // the hash's rank in A u B is i + j -- and needs no kernel (k_screen_simple).
+// Chunk masks for the dense all-pairs kernel (the screen's verdict "dense"):
+// bit k of cmask[g] is set when 64-element chunk k of sketch g holds a
+// position the whole-row kernel must confirm by the hash's high word -- a
+// position at or past nhash[g] (padding, or past s: those lanes read 0), or an
+// entry whose low word (the sort key) another, different 64-bit hash of the
+// matrix shares.  A probe hit on a clear chunk then needs no high-word read:
+// the row key it found has the column element's low word, and no other hash
+// has that low word (k_allpairs_q, probe_rows_v).  Exact: a run of equal keys
+// is clean only when every entry's 64-bit hash equals the first's.
+//
+// Positions past nhash read UINT64_MAX (padding) or 0 (past s, through the
+// buffer bounds): harmless unless some entry of the matrix has the low word
+// 0xFFFFFFFF or 0 -- the sorted keys' last and first -- and only then are
+// their chunks flagged.
+__global__ __launch_bounds__(kScWG) void k_cmask_init(const uint32_t *__restrict__ nh, uint32_t N,
+                                                      const uint32_t *__restrict__ keys, uint32_t M,
+                                                      uint32_t *__restrict__ cmask) {
+    const uint32_t g = blockIdx.x * kScWG + threadIdx.x;
+    if (g >= N) return;
+    const bool edge = keys[0] == 0u || keys[M - 1] == 0xFFFFFFFFu;
+    const uint32_t first = nh[g] / 64;                             // the first chunk holding a position >= nhash
+    cmask[g] = (!edge || first >= 32) ? 0u : ~0u << first;
+}
+// runs of two: one lane each
+__global__ __launch_bounds__(kScWG) void k_cmask_pairs(const uint32_t *__restrict__ vals, const uint64_t *__restrict__ H,
+                                                       uint32_t s, uint32_t vmask, const uint32_t *__restrict__ pairs,
+                                                       uint32_t n2, uint32_t *__restrict__ cmask) {
+    for (uint32_t i = blockIdx.x * kScWG + threadIdx.x; i < n2; i += gridDim.x * kScWG) {
+        const uint32_t st = pairs[i];
+        const uint32_t a = vals[st] & vmask, b = vals[st + 1] & vmask;    // g s + k
+        if (H[a] != H[b]) {
+            atomicOr(&cmask[a / s], 1u << ((a % s) / 64));
+            atomicOr(&cmask[b / s], 1u << ((b % s) / 64));
+        }
+    }
+}
+// runs of three or more: one wave each (grid-stride over the runs)
+__global__ __launch_bounds__(kScWG) void k_cmask_runs(const uint32_t *__restrict__ vals, const uint64_t *__restrict__ H,
+                                                      uint32_t s, uint32_t vmask, const uint2 *__restrict__ runs,
+                                                      uint32_t nruns, uint32_t *__restrict__ cmask) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nw = gridDim.x * (kScWG / 64);
+    for (uint32_t r = blockIdx.x * (kScWG / 64) + (threadIdx.x >> 6); r < nruns; r += nw) {     // wave-uniform
+        const uint2 run = runs[r];
+        const uint64_t h0 = H[vals[run.x] & vmask];
+        bool mixed = false;
+        for (uint32_t e = lane; e < run.y; e += 64) mixed |= H[vals[run.x + e] & vmask] != h0;
+        if (__ballot(mixed) == 0) continue;
+        for (uint32_t e = lane; e < run.y; e += 64) {
+            const uint32_t v = vals[run.x + e] & vmask;
+            atomicOr(&cmask[v / s], 1u << ((v % s) / 64));
+        }
+    }
+}
+
 constexpr uint64_t kPairEmpty = ~0ull;
 constexpr uint64_t kMaxPairMap = 1ull << 30;   // pair-map slots (16 B each); above it the screen gives way
 constexpr uint64_t kLightBudget = 1ull << 30;  // bytes of the light screen's per-cell run ids (sc_crun)
@@ -920,6 +975,7 @@ struct ScreenFront {
     uint32_t nr = 0;                // distinct keys
     uint32_t n2 = 0, nruns = 0;     // runs of two; of three or more
     uint64_t E = 0;                 // pair checks of the runs: sum of m (m - 1) / 2
+    uint32_t *k_out = nullptr;      // the sorted keys
     uint32_t *v_out = nullptr;      // entry values g s + k in key order
     uint2 *runs = nullptr;          // {start, length} of the runs of >= 3
     uint32_t *rfirst = nullptr, *ridx = nullptr;      // their first genome, index (unsorted)
@@ -1029,6 +1085,7 @@ static int screen_front(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32
     uint64_t E = 0;
     for (uint32_t b = 0; b < kRunBlocks; b++) E += h_chk[b];
     F->E = E;
+    F->k_out = k_out;
     F->v_out = v_out;
     return DREPHIP_OK;
 }
@@ -1190,7 +1247,30 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
     res->entries = F.M;
     res->runs = (uint64_t)F.n2 + F.nruns;
     res->checks = F.E;
-    if (!force && !screen_worth(N, s, F.E)) { timing_mark(ctx, 4, st, false); return DREPHIP_OK; }
+    if (!force && !screen_worth(N, s, F.E)) {
+        // the dense path runs: its chunk masks from the runs just grouped
+        // (k_cmask_*; whole-row tables only, s <= 2048: <= 32 chunks).
+        // DREPHIP_AP_CMASK=0 leaves every chunk to the high-word check (A/B)
+        const char *ce = getenv("DREPHIP_AP_CMASK");
+        if (s <= 2048 && (!ce || atoi(ce) != 0)) {
+            uint32_t *d_cm;
+            if ((rc = scratch(ctx, "sc_cmask", N * 4ull, (void **)&d_cm))) return rc;
+            hipLaunchKernelGGL(k_cmask_init, dim3((N + kScWG - 1) / kScWG), dim3(kScWG), 0, st, d_nhash, N, F.k_out, F.M,
+                               d_cm);
+            if (F.n2)
+                hipLaunchKernelGGL(k_cmask_pairs, dim3(std::min(4096u, (F.n2 + kScWG - 1) / kScWG)), dim3(kScWG), 0, st,
+                                   F.v_out, d_hashes, s, F.vmask, F.pairs, F.n2, d_cm);
+            if (F.nruns)
+                hipLaunchKernelGGL(k_cmask_runs, dim3(std::min(4096u, (F.nruns + 3) / 4)), dim3(kScWG), 0, st, F.v_out,
+                                   d_hashes, s, F.vmask, F.runs, F.nruns, d_cm);
+            HIPC(hipGetLastError());
+            // timing A/B only: 2 = every chunk checked, 3 = none (wrong counts)
+            if (ce && atoi(ce) >= 2) HIPC(hipMemsetAsync(d_cm, atoi(ce) == 2 ? 0xFF : 0, N * 4ull, st));
+            res->cmask = d_cm;
+        }
+        timing_mark(ctx, 4, st, false);
+        return DREPHIP_OK;
+    }
 
     const uint32_t rows = row1 - row0;
     const uint32_t ntiles = (rows + R - 1) / R;

@@ -407,6 +407,52 @@ def test_sharded_screen_value_cuts(s, N, W):
     assert (oc > 0).sum() > N // 2
 
 
+@pytest.mark.parametrize("s,N,edge", [(600, 300, False), (1000, 240, False), (1000, 240, True), (2048, 120, True),
+                                      (64, 500, False), (64, 500, True)])
+def test_dense_verdict_chunk_masks(s, N, edge):
+    """After the screen's dense verdict the whole-row kernel skips the
+    high-word check on chunks whose low words no other hash of the set shares
+    (k_cmask_*, probe_rows_v<EXACT = false>).  One-species sets (the verdict
+    must be dense) with low-word twins -- hashes that share a low word and are
+    each held by many genomes, sometimes both by one -- partial sketches, and s
+    not a multiple of 64 (chunks past s read zeros), and (edge) hashes whose
+    low word is 0 or 0xFFFFFFFF, which the zeros past s and the padding of
+    partial sketches could match by low word: bit-exact against the oracle and
+    against the all-checked path (DREPHIP_AP_CMASK=0)."""
+    import os
+    rng = np.random.default_rng(s + N)
+    pool = rng.integers(1, UMAX, size=2 * s, dtype=np.uint64)
+    twins = (pool[:s // 8] & np.uint64(0xFFFFFFFF)) | (rng.integers(1, 1 << 32, size=s // 8, dtype=np.uint64)
+                                                       << np.uint64(32))
+    pool = np.concatenate([pool, twins])
+    if edge:
+        pool[:4] = (pool[:4] >> np.uint64(32)) << np.uint64(32)                       # low word 0
+        pool[4:8] = pool[4:8] | np.uint64(0xFFFFFFFF)                                  # low word 0xFFFFFFFF
+    H = np.full((N, s), UMAX, dtype=np.uint64)
+    NH = np.zeros(N, dtype=np.uint32)
+    for g in range(N):
+        vals = np.unique(np.concatenate([rng.choice(pool, size=int(1.2 * s), replace=False),
+                                         rng.integers(1, UMAX, size=s // 4, dtype=np.uint64)]))
+        n = s if g % 7 else int(rng.integers(1, s))
+        NH[g] = min(n, len(vals))
+        H[g, :NH[g]] = vals[:NH[g]]
+    oc, od = oracle.allpairs(H, NH, s, threads=8)
+    os.environ["DREPHIP_SCREEN_MIN_N"] = "2"
+    try:
+        with _lib.Context(0, 21, s, 42) as ctx:
+            c, d = ctx.allpairs(H, NH, want_denom=True)
+            st = ctx.screen_stats()
+            os.environ["DREPHIP_AP_CMASK"] = "0"
+            c0, d0 = ctx.allpairs(H, NH, want_denom=True)
+    finally:
+        os.environ.pop("DREPHIP_SCREEN_MIN_N")
+        os.environ.pop("DREPHIP_AP_CMASK", None)
+    assert not st["used"] and st["entries"] == int(NH.sum())          # the screen ran and gave way
+    assert np.array_equal(c, oc) and np.array_equal(d, od)
+    assert np.array_equal(c0, c) and np.array_equal(d0, d)
+    assert (oc > 0).mean() > 0.9
+
+
 def test_sharded_screen_arguments_checked():
     import torch
     with _lib.Context(0, 21, 1000, 42) as ctx:
