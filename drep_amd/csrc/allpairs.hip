@@ -401,7 +401,11 @@ __device__ __forceinline__ void probe_rows_v(const Slots<R> &sl, uint64_t b, uin
     uint32_t f[R], vh[R];
 #pragma unroll
     for (int r = 0; r < R; r++) {
-        f[r] = min(xs1[r], xs2[r]);
+        // !EXACT: clamped to hm (v_min3, no extra instruction), so a lane
+        // without a hit has f + j - (s + mrun) >= hm - s >= s - 1 >= 63 >= its
+        // lower-lane count (mrun <= j; the masks are built for s >= 64 only):
+        // the rank test below needs no AND with the match mask
+        f[r] = EXACT ? min(xs1[r], xs2[r]) : min(min(xs1[r], xs2[r]), hm);
         if constexpr (EXACT) vh[r] = V[min(f[r], s - 1) * R + r];    // row-interleaved high words
     }
     if constexpr (EXACT) {
@@ -415,7 +419,8 @@ __device__ __forceinline__ void probe_rows_v(const Slots<R> &sl, uint64_t b, uin
         const int32_t pre = (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         const int32_t key = (int32_t)(f[r] + jl) + nb[r];
-        cnt[r] += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(key < pre) & m);
+        const uint64_t rank = __builtin_amdgcn_ballot_w64(key < pre);
+        cnt[r] += (uint32_t)__popcll(EXACT ? rank & m : rank);
         nb[r] -= (int32_t)__popcll(m);
     }
 }

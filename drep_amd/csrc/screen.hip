@@ -1249,10 +1249,11 @@ int screen_impl(drephip_ctx *ctx, const uint64_t *d_hashes, const uint32_t *d_nh
     res->checks = F.E;
     if (!force && !screen_worth(N, s, F.E)) {
         // the dense path runs: its chunk masks from the runs just grouped
-        // (k_cmask_*; whole-row tables only, s <= 2048: <= 32 chunks).
+        // (k_cmask_*; whole-row tables only, s <= 2048: <= 32 chunks; and
+        // s >= 64, which the unchecked probe's rank test relies on).
         // DREPHIP_AP_CMASK=0 leaves every chunk to the high-word check (A/B)
         const char *ce = getenv("DREPHIP_AP_CMASK");
-        if (s <= 2048 && (!ce || atoi(ce) != 0)) {
+        if (s >= 64 && s <= 2048 && (!ce || atoi(ce) != 0)) {
             uint32_t *d_cm;
             if ((rc = scratch(ctx, "sc_cmask", N * 4ull, (void **)&d_cm))) return rc;
             hipLaunchKernelGGL(k_cmask_init, dim3((N + kScWG - 1) / kScWG), dim3(kScWG), 0, st, d_nhash, N, F.k_out, F.M,

@@ -20,6 +20,7 @@
 #   rank_screen  tools/rank_screen.py (RS_ARGS)
 #   scale        tools/gpu_scale.sh "$SCALE_SPECS"
 #   price        tools/valu_microbench.hip (instruction prices) + the sketch hash kernel at configs[1] (tools/sketch_ablate.py)
+#   dense_ab     bench at 10^4 genomes of one species once per value of DREPHIP_AP_CMASK in CMASK_VALUES (default "1 0 3 1 0 3")
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-.}
 export TMPDIR=/tmp
@@ -98,6 +99,10 @@ for step in ${STEPS:-tests smoke bench}; do
         echo "rep $r: $(cat $O/sketch_ms_$r.json)"
       done
       rm -f $O/valu_microbench ;;
+    dense_ab)
+      for v in ${CMASK_VALUES:-1 0 3 1 0 3}; do
+        DREPHIP_AP_CMASK=$v bench_line dense_cmask_$v --genomes 10000 --family-size 10000 --steps 3 --warmup 1 --cpu-baseline 0 --check 0
+      done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
