@@ -43,7 +43,14 @@ namespace drephip {
 #define DREPHIP_AP_MID 1          // first union-rank test one chunk into its group (ap_columns); 0: at the group start
 #endif
 constexpr int kApWG = 1024;                     // 16 waves per workgroup
-constexpr uint32_t kApCols = 128;               // columns per work item (fewer when the grid would not fill the chip)
+// columns per work item (fewer when the grid would not fill the chip): 512
+// amortises the row image's prologue over 4x the columns of round 5's 128 --
+// dense 10^4 set 14.9 -> 14.0 ms, configs[2] unscreened 7.1 -> 6.5 ms, 1024
+// slower again (profiles/r06_ap_cols_ab.txt); -DDREPHIP_AP_COLS=... for A/Bs
+#ifndef DREPHIP_AP_COLS
+#define DREPHIP_AP_COLS 512
+#endif
+constexpr uint32_t kApCols = DREPHIP_AP_COLS;
 constexpr uint32_t kApMinCols = 16;             // one column per wave
 constexpr uint32_t kApSlots = 2 * 256;          // workgroup slots of the chip (two per CU)
 constexpr uint32_t kMaxFam = 6;                 // cuckoo field families tried per table
